@@ -1,0 +1,323 @@
+"""Seeded synthetic movement traces for the AOI + sync path.
+
+Workload generator shared by tests/ and bench.py.  It is not oracle code: it
+only produces inputs.  Every random number comes from a counter-based
+SplitMix64 (value = mix64(key + (i+1)*golden)), so any (seed, stream, index)
+can be regenerated independently and the traces are identical on every host.
+
+Positions of the perf configs live on a dyadic grid of step 1/128 with
+|x| < 2**17, so x +- d is exact in float32 and the reference window test is
+symmetric.  Config #1 and the adversarial traces are
+deliberately non-dyadic float32 to exercise the rounded-bounds / seq rule.
+
+Sources of the workload shapes (reference paths):
+  #1 examples/test_game/Avatar.go:124-131 (integer positions in [-400,400)),
+     examples/test_client/ClientBot.go:214-223 (p=0.5 per 100 ms, dx~U(-.01,.01),
+     dz~U(-.01,0), yaw~U(0,3.14)), examples/test_game/MySpace.go:28 (EnableAOI(100)).
+  #2-#5 BASELINE.json configs, parameters from SURVEY.md 8(d).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import numpy as np
+
+GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+
+# gw_op layout of include/gpuaoi.h (24 bytes, little-endian)
+OP_DTYPE = np.dtype([("kind", "u1"), ("sync_flags", "u1"), ("reserved", "<u2"),
+                     ("slot", "<u4"), ("x", "<f4"), ("y", "<f4"), ("z", "<f4"),
+                     ("yaw", "<f4")])
+assert OP_DTYPE.itemsize == 24
+
+OP_ENTER, OP_MOVED, OP_LEAVE, OP_SYNC = 1, 2, 3, 4
+SIF_OWN, SIF_NEIGHBOR = 1, 2
+Q = 128.0  # dyadic quantum denominator
+
+
+def mix64(z: np.ndarray) -> np.ndarray:
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+    return z ^ (z >> np.uint64(31))
+
+
+def stream_key(seed: int, *stream: int) -> np.uint64:
+    k = mix64(np.uint64(seed & 0xFFFFFFFFFFFFFFFF))
+    for s in stream:
+        with np.errstate(over="ignore"):
+            k = mix64(k ^ mix64(np.uint64(s & 0xFFFFFFFFFFFFFFFF) + GOLDEN))
+    return np.uint64(k)
+
+
+def rand_u64(key, n: int, offset: int = 0) -> np.ndarray:
+    idx = np.arange(offset + 1, offset + n + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return mix64(np.uint64(key) + idx * GOLDEN)
+
+
+def rand_unit(key, n: int) -> np.ndarray:
+    """Uniform float64 in [0, 1)."""
+    return (rand_u64(key, n) >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
+def rand_f32(key, n: int) -> np.ndarray:
+    """Uniform float32 in [0, 1) with 24 random bits (like Go rand.Float32)."""
+    return ((rand_u64(key, n) >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0))
+
+
+def rand_int(key, n: int, lo: int, hi: int) -> np.ndarray:
+    """Uniform integers in [lo, hi)."""
+    span = hi - lo
+    return (lo + (rand_unit(key, n) * span).astype(np.int64)).clip(lo, hi - 1)
+
+
+def make_ops(n: int) -> np.ndarray:
+    return np.zeros(n, dtype=OP_DTYPE)
+
+
+@dataclasses.dataclass
+class SpaceTrace:
+    """One space: initial population + per-tick ops (local slots)."""
+    n: int                     # entities (== capacity unless extra headroom)
+    capacity: int
+    d: float
+    bounds: tuple              # (minx, minz, maxx, maxz)
+    init_slots: np.ndarray     # u32, bulk-enter order
+    init_x: np.ndarray
+    init_y: np.ndarray
+    init_z: np.ndarray
+    init_yaw: np.ndarray
+    ticks: list                # list of OP_DTYPE arrays
+    gates: np.ndarray | None = None  # u16 per slot (0 = no client)
+
+
+def _reflect_q(k: np.ndarray, lo_q: int, hi_q: int) -> np.ndarray:
+    """Reflect integer 1/128 units into [lo_q, hi_q)."""
+    k = np.where(k < lo_q, 2 * lo_q - k, k)
+    k = np.where(k >= hi_q, 2 * (hi_q - 1) - k, k)
+    return np.clip(k, lo_q, hi_q - 1)
+
+
+def _choose_movers(key, n: int, m: int) -> np.ndarray:
+    """m distinct slots, in random order (the op order of the tick)."""
+    r = rand_u64(key, n)
+    if m >= n:
+        return np.argsort(r, kind="stable").astype(np.uint32)
+    part = np.argpartition(r, m - 1)[:m]
+    return part[np.argsort(r[part], kind="stable")].astype(np.uint32)
+
+
+def dyadic_walk_trace(seed: int, n: int, side: float, d: float, ticks: int,
+                      move_frac: float = 0.10, step_q: int = 512,
+                      hot_frac: float = 0.0, n_hot: int = 64, sigma: float = 200.0,
+                      hot_step_q: int = 2048, gate_count: int = 1,
+                      client_frac: float = 1.0, capacity: int | None = None) -> SpaceTrace:
+    """Configs #2/#3/#4/#5: uniform (+ optional Gaussian hotspots) on the 1/128 grid."""
+    assert side / 2 * Q < 2 ** 24, "dyadic exactness needs |x| < 2**17"
+    half_q = int(side / 2 * Q)
+    lo_q, hi_q = -half_q, half_q
+    n_hot_ent = int(round(n * hot_frac))
+    n_bg = n - n_hot_ent
+    kx = rand_int(stream_key(seed, 1), n, lo_q, hi_q)
+    kz = rand_int(stream_key(seed, 2), n, lo_q, hi_q)
+    if n_hot_ent:
+        cx = rand_unit(stream_key(seed, 3), n_hot) * side - side / 2
+        cz = rand_unit(stream_key(seed, 4), n_hot) * side - side / 2
+        which = rand_int(stream_key(seed, 5), n_hot_ent, 0, n_hot)
+        u1 = 1.0 - rand_unit(stream_key(seed, 6), n_hot_ent)   # (0,1]
+        u2 = rand_unit(stream_key(seed, 7), n_hot_ent)
+        u3 = 1.0 - rand_unit(stream_key(seed, 8), n_hot_ent)
+        u4 = rand_unit(stream_key(seed, 9), n_hot_ent)
+        gx = np.sqrt(-2.0 * np.log(u1)) * np.cos(2 * math.pi * u2)
+        gz = np.sqrt(-2.0 * np.log(u3)) * np.cos(2 * math.pi * u4)
+        hx = np.round((cx[which] + sigma * gx) * Q).astype(np.int64)
+        hz = np.round((cz[which] + sigma * gz) * Q).astype(np.int64)
+        kx[n_bg:] = np.clip(hx, lo_q, hi_q - 1)
+        kz[n_bg:] = np.clip(hz, lo_q, hi_q - 1)
+    is_hot = np.zeros(n, dtype=bool)
+    is_hot[n_bg:] = True
+    yaw = (rand_f32(stream_key(seed, 10), n) * np.float32(2 * math.pi)).astype(np.float32)
+    cap = capacity or n
+    slots = np.arange(n, dtype=np.uint32)
+    init_x = (kx / Q).astype(np.float32)
+    init_z = (kz / Q).astype(np.float32)
+    tr = SpaceTrace(n=n, capacity=cap, d=float(d),
+                    bounds=(-side / 2, -side / 2, side / 2, side / 2),
+                    init_slots=slots, init_x=init_x, init_y=np.zeros(n, np.float32),
+                    init_z=init_z, init_yaw=yaw, ticks=[])
+    gates = np.zeros(cap, dtype=np.uint16)
+    has_client = rand_unit(stream_key(seed, 11), n) < client_frac
+    gsel = rand_int(stream_key(seed, 12), n, 1, gate_count + 1).astype(np.uint16)
+    gates[:n] = np.where(has_client, gsel, 0)
+    tr.gates = gates
+    m = int(round(n * move_frac))
+    for t in range(ticks):
+        movers = _choose_movers(stream_key(seed, 100, t), n, m)
+        sq = np.where(is_hot[movers], hot_step_q, step_q)
+        dx = (rand_unit(stream_key(seed, 101, t), m) * (2 * sq + 1)).astype(np.int64) - sq
+        dz = (rand_unit(stream_key(seed, 102, t), m) * (2 * sq + 1)).astype(np.int64) - sq
+        kx[movers] = _reflect_q(kx[movers] + dx, lo_q, hi_q)
+        kz[movers] = _reflect_q(kz[movers] + dz, lo_q, hi_q)
+        yaw[movers] = rand_f32(stream_key(seed, 103, t), m) * np.float32(2 * math.pi)
+        from_client = rand_unit(stream_key(seed, 104, t), m) < 0.5
+        ops = make_ops(m)
+        ops["kind"] = OP_MOVED
+        # setPositionYaw: neighbours always, own client unless the move came
+        # from the client (Entity.go:1199-1204)
+        ops["sync_flags"] = np.where(from_client, SIF_NEIGHBOR, SIF_NEIGHBOR | SIF_OWN)
+        ops["slot"] = movers
+        ops["x"] = (kx[movers] / Q).astype(np.float32)
+        ops["z"] = (kz[movers] / Q).astype(np.float32)
+        ops["yaw"] = yaw[movers]
+        tr.ticks.append(ops)
+    return tr
+
+
+def config2(ticks: int = 100, seed: int = 2, n: int = 100_000) -> SpaceTrace:
+    """#2: 100k uniform, L=10240, 10% movers, step +-4."""
+    return dyadic_walk_trace(seed, n, 10240.0, 100.0, ticks, 0.10, 512)
+
+
+def config3(ticks: int = 20, seed: int = 3, n: int = 1_000_000, side: float = 32768.0) -> SpaceTrace:
+    """#3: 1M clustered hotspots: 70% uniform, 30% in 64 Gaussians (sigma 200);
+    hotspot movers step +-16, others +-4; 10% movers."""
+    return dyadic_walk_trace(seed, n, side, 100.0, ticks, 0.10, 512,
+                             hot_frac=0.30, n_hot=64, sigma=200.0, hot_step_q=2048)
+
+
+def config4_space(space: int, ticks: int = 20, seed: int = 4, n: int = 1000) -> SpaceTrace:
+    """#4: one of the 10k independent spaces (1k entities, L=1024, d=100)."""
+    return dyadic_walk_trace(seed * 1_000_003 + space, n, 1024.0, 100.0, ticks, 0.10, 512)
+
+
+def config1(ticks: int = 1000, seed: int = 1, n: int = 1000, big_steps: bool = False) -> SpaceTrace:
+    """#1: examples/test_game single space, float32 random walk (non-dyadic).
+
+    Positions start on integers in [-400,400) (Avatar.go:124-131).  Each tick
+    every bot moves with p=0.5: X += -0.01 + 0.02*r, Z += -0.01 + 0.01*r,
+    yaw = r*3.14, all float32 (ClientBot.go:214-223).  Variant #1b
+    (big_steps) scales the step to +-4 to produce events."""
+    k = stream_key(seed, 1)
+    x = rand_int(k, n, -400, 400).astype(np.float32)
+    z = rand_int(stream_key(seed, 2), n, -400, 400).astype(np.float32)
+    yaw = np.zeros(n, np.float32)
+    tr = SpaceTrace(n=n, capacity=n, d=100.0, bounds=(-1000.0, -1000.0, 1000.0, 1000.0),
+                    init_slots=np.arange(n, dtype=np.uint32), init_x=x.copy(),
+                    init_y=np.zeros(n, np.float32), init_z=z.copy(), init_yaw=yaw.copy(), ticks=[])
+    tr.gates = np.ones(n, dtype=np.uint16)
+    mr = np.float32(4.0 if big_steps else 0.01)
+    for t in range(ticks):
+        mv = rand_unit(stream_key(seed, 100, t), n) < 0.5
+        order = np.argsort(rand_u64(stream_key(seed, 105, t), n), kind="stable")
+        movers = order[mv[order]].astype(np.uint32)
+        m = len(movers)
+        r1 = rand_f32(stream_key(seed, 101, t), m)
+        r2 = rand_f32(stream_key(seed, 102, t), m)
+        r3 = rand_f32(stream_key(seed, 103, t), m)
+        x[movers] = x[movers] + (-mr + (mr * np.float32(2)) * r1)
+        z[movers] = z[movers] + (-mr + mr * r2)
+        yaw[movers] = r3 * np.float32(3.14)
+        ops = make_ops(m)
+        ops["kind"] = OP_MOVED
+        ops["sync_flags"] = SIF_NEIGHBOR          # syncPositionYawFromClient: fromClient
+        ops["slot"] = movers
+        ops["x"] = x[movers]
+        ops["z"] = z[movers]
+        ops["yaw"] = yaw[movers]
+        tr.ticks.append(ops)
+    return tr
+
+
+def adversarial_trace(seed: int, n: int = 400, ticks: int = 30, d: float = 100.0,
+                      churn: bool = True) -> SpaceTrace:
+    """Non-dyadic float32 positions placed on the rounding edge of each other's
+    windows (other.x == fl(c.x +- d) +- 1 ulp), so the rounded-bounds test is
+    asymmetric and the seq rule decides.  With churn, ticks also contain
+    Leave / re-Enter / Sync ops and repeated ops on one slot."""
+    d32 = np.float32(d)
+    base_x = (rand_unit(stream_key(seed, 1), n) * 600 - 300).astype(np.float32)
+    base_z = (rand_unit(stream_key(seed, 2), n) * 600 - 300).astype(np.float32)
+    # pull half of the entities onto the window edge of a random partner
+    partner = rand_int(stream_key(seed, 3), n, 0, n)
+    sel = rand_unit(stream_key(seed, 4), n) < 0.5
+    sgn = np.where(rand_unit(stream_key(seed, 5), n) < 0.5, -1, 1)
+    ulps = rand_int(stream_key(seed, 6), n, -1, 2)
+    for i in np.nonzero(sel)[0]:
+        p = partner[i]
+        edge = np.float32(base_x[p] + d32) if sgn[i] > 0 else np.float32(base_x[p] - d32)
+        for _ in range(abs(int(ulps[i]))):
+            edge = np.nextafter(edge, np.float32(np.inf if ulps[i] > 0 else -np.inf), dtype=np.float32)
+        base_x[i] = edge
+        base_z[i] = base_z[p] + np.float32(rand_unit(stream_key(seed, 7, int(i)), 1)[0] * 50)
+    x, z = base_x.copy(), base_z.copy()
+    yaw = np.zeros(n, np.float32)
+    present = np.ones(n, dtype=bool)
+    tr = SpaceTrace(n=n, capacity=n, d=float(d), bounds=(-500.0, -500.0, 500.0, 500.0),
+                    init_slots=np.arange(n, dtype=np.uint32), init_x=x.copy(),
+                    init_y=np.zeros(n, np.float32), init_z=z.copy(), init_yaw=yaw.copy(), ticks=[])
+    tr.gates = np.where(np.arange(n) % 5 == 4, 0, 1 + np.arange(n) % 3).astype(np.uint16)
+    for t in range(ticks):
+        k = stream_key(seed, 200, t)
+        cnt = int(n * 0.3)
+        picks = rand_int(k, cnt, 0, n)          # repeats allowed: several ops per slot
+        kinds_r = rand_unit(stream_key(seed, 201, t), cnt)
+        tgt = rand_int(stream_key(seed, 202, t), cnt, 0, n)
+        edge_sgn = rand_unit(stream_key(seed, 203, t), cnt) < 0.5
+        rows = []
+        for j in range(cnt):
+            a = int(picks[j])
+            if not present[a]:
+                if churn and kinds_r[j] < 0.7:
+                    b = int(tgt[j])
+                    nx = np.float32(x[b] + d32) if edge_sgn[j] else np.float32(x[b] - d32)
+                    x[a], z[a] = nx, np.float32(z[b] + np.float32(kinds_r[j] * 30))
+                    present[a] = True
+                    rows.append((OP_ENTER, 3, a, x[a], z[a], yaw[a]))
+                continue
+            if churn and kinds_r[j] < 0.05:
+                present[a] = False
+                rows.append((OP_LEAVE, 0, a, x[a], z[a], yaw[a]))
+            elif churn and kinds_r[j] < 0.10:
+                yaw[a] = np.float32(kinds_r[j] * 31)
+                rows.append((OP_SYNC, 3, a, x[a], z[a], yaw[a]))
+            else:
+                b = int(tgt[j])
+                nx = np.float32(x[b] + d32) if edge_sgn[j] else np.float32(x[b] - d32)
+                if kinds_r[j] < 0.55:
+                    nx = np.nextafter(nx, np.float32(np.inf), dtype=np.float32)
+                x[a] = nx
+                z[a] = np.float32(z[b] + np.float32((kinds_r[j] - 0.5) * 120))
+                rows.append((OP_MOVED, 2 if kinds_r[j] < 0.5 else 3, a, x[a], z[a], yaw[a]))
+        ops = make_ops(len(rows))
+        if rows:
+            arr = np.array(rows, dtype=object)
+            ops["kind"] = arr[:, 0].astype(np.uint8)
+            ops["sync_flags"] = arr[:, 1].astype(np.uint8)
+            ops["slot"] = arr[:, 2].astype(np.uint32)
+            ops["x"] = arr[:, 3].astype(np.float32)
+            ops["z"] = arr[:, 4].astype(np.float32)
+            ops["yaw"] = arr[:, 5].astype(np.float32)
+        tr.ticks.append(ops)
+    return tr
+
+
+def with_global_slots(ops: np.ndarray, base: int) -> np.ndarray:
+    out = ops.copy()
+    out["slot"] = ops["slot"] + np.uint32(base)
+    return out
+
+
+def enter_ops(slots, x, y, z, yaw, flags: int = SIF_OWN | SIF_NEIGHBOR) -> np.ndarray:
+    """Enter ops for an initial population (Space.enter sets Own|Neighbor,
+    Space.go:196)."""
+    ops = make_ops(len(slots))
+    ops["kind"] = OP_ENTER
+    ops["sync_flags"] = flags
+    ops["slot"] = slots
+    ops["x"], ops["y"], ops["z"], ops["yaw"] = x, y, z, yaw
+    return ops

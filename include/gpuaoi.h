@@ -1,0 +1,201 @@
+/*
+ * gpuaoi.h — C ABI of the MI355X-native GoWorld AOI + entity-sync hot path.
+ *
+ * This is the drop-in boundary.  A Go shim package (engine/gpuaoi, source in
+ * INTEGRATION.md) binds it through cgo; the Python test/bench layer binds it
+ * through ctypes.  Plain C types only: no torch, no C++ types, no callbacks.
+ *
+ * What each entry point replaces in the reference (paths relative to the
+ * LiHeng/goworld tree; go-aoi v0.2.0 is the external module named in go.mod:25):
+ *
+ *   gw_space_create  <- Space.EnableAOI -> aoi.NewXZListAOIManager(d)
+ *                       (engine/entity/Space.go:91-106; manager stored in
+ *                        Space.aoiMgr, Space.go:33)
+ *   gw_submit        <- aoiMgr.Enter / aoiMgr.Moved / aoiMgr.Leave
+ *                       (Space.go:201-203, 211-213, 233-235, 250) plus the
+ *                       syncInfoFlag updates of Space.go:196,
+ *                       Entity.go:1189-1205 (setPositionYaw) and
+ *                       Entity.go:1284-1290 (SetYaw)
+ *   gw_tick          <- the OnEnterAOI/OnLeaveAOI callbacks go-aoi fires inside
+ *                       each call (Entity.go:227-246), batched per tick and
+ *                       returned as canonical net event streams
+ *   gw_neighbors     <- Entity.InterestedIn / InterestedBy (Entity.go:53-54;
+ *                       both sets are equal because go-aoi fires both
+ *                       directions of every enter/leave)
+ *   gw_sync_collect  <- entity.CollectEntitySyncInfos (Entity.go:1221-1267),
+ *                       called from GameService.serveRoutine (GameService.go:186)
+ *   gw_set_clients   <- GameClient attach/detach (Entity.client, GameClient.go:14-27)
+ *
+ * Conventions
+ *   - Every function returns 0 on success and a negative GW_E* code on error;
+ *     gw_last_error() gives the message.  Nothing throws or longjmps across the
+ *     ABI.  The Go shim turns errors into gwlog.Panicf, as the reference panics
+ *     on misuse (Space.go:92-102, 184-186, 220-222).
+ *   - Slots are GLOBAL per context: a space owns slots
+ *     [slot_base, slot_base + capacity) returned by gw_space_create.  Events
+ *     and sync records carry global slots.  Canonical order over global slots
+ *     equals (space, local slot) order because slot ranges are allocated in
+ *     space-id order.
+ *   - One host thread per context; not re-entrant (the reference calls AOI only
+ *     from the single game goroutine, GameService.go:89-189).
+ *   - Output pointers in gw_tick_out / gw_sync_out are owned by the library and
+ *     stay valid until the next gw_tick / gw_sync_collect on the same context.
+ *   - Coordinates must be finite.  Only X and Z take part in AOI (Space.go:202,
+ *     250); Y and yaw only travel in sync records.
+ */
+#ifndef GPUAOI_H
+#define GPUAOI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ------------------------------------------------------- */
+#define GW_OK          0
+#define GW_EINVAL     -1   /* bad argument / misuse (reference would panic)   */
+#define GW_ESTATE     -2   /* op sequence invalid for the entity's state       */
+#define GW_ENOMEM     -3   /* device or host allocation failed                 */
+#define GW_EDEVICE    -4   /* HIP runtime / kernel error                       */
+#define GW_ERANGE     -5   /* slot or space id out of range                    */
+
+/* ---- ops ---------------------------------------------------------------- */
+#define GW_OP_ENTER   1    /* aoiMgr.Enter(&e.aoi, x, z)      (Space.go:202)   */
+#define GW_OP_MOVED   2    /* aoiMgr.Moved(&e.aoi, x, z)      (Space.go:250)   */
+#define GW_OP_LEAVE   3    /* aoiMgr.Leave(&e.aoi)            (Space.go:234)   */
+#define GW_OP_SYNC    4    /* SetYaw: sync state only, no AOI adjust
+                              (Entity.go:1284-1290)                            */
+
+/* syncInfoFlag bits (Entity.go:91-96) */
+#define GW_SIF_OWN_CLIENT        1u
+#define GW_SIF_NEIGHBOR_CLIENTS  2u
+
+/* One AOI/sync operation, 24 bytes.  Submission order == reference call order
+ * (the seq number of the batched-parity contract is the index of the op in
+ * the tick's concatenated submission stream).  x,y,z,yaw are the entity's
+ * Position and yaw after the op (for LEAVE they are ignored).  sync_flags is
+ * ORed into the entity's syncInfoFlag; a LEAVE clears it. */
+typedef struct gw_op {
+    uint8_t  kind;        /* GW_OP_*                                        */
+    uint8_t  sync_flags;  /* GW_SIF_* bits set by this call                  */
+    uint16_t reserved;    /* must be 0                                       */
+    uint32_t slot;        /* global slot                                     */
+    float    x, y, z, yaw;
+} gw_op;
+
+/* A directed AOI event: watcher.OnEnterAOI(target) / OnLeaveAOI(target). */
+typedef struct gw_event {
+    uint32_t watcher;
+    uint32_t target;
+} gw_event;
+
+/* A compact sync record.  The wire form (Entity.go:1231-1253) is
+ * clientid(watcher)[16] eid(entity)[16] f32 x,y,z,yaw, grouped per gate;
+ * watcher == entity for the own-client record. */
+typedef struct gw_sync_record {
+    uint32_t watcher;     /* slot whose client receives the record            */
+    uint32_t entity;      /* slot whose position/yaw is synced                */
+    float    x, y, z, yaw;
+} gw_sync_record;
+
+/* gw_tick flags */
+#define GW_TICK_COPY_TO_HOST   1u  /* also copy events into pinned host buffers */
+#define GW_TICK_NO_EVENTS      2u  /* update neighbour state only (restore/bulk
+                                      path, Space.go:209-214)                   */
+
+typedef struct gw_tick_out {
+    /* canonical order: sorted by (watcher, target); each directed pair at most
+       once per tick (net diff, see DESIGN.md "batched parity contract") */
+    const gw_event* enter;        /* host pointer (NULL unless COPY_TO_HOST)   */
+    const gw_event* leave;
+    const gw_event* enter_dev;    /* device pointers, always valid             */
+    const gw_event* leave_dev;
+    uint64_t n_enter, n_leave;
+    uint64_t ops;                 /* ops consumed                              */
+    uint64_t movers;              /* distinct slots with an AOI op (M)         */
+    uint64_t pairs_tested;        /* candidate pairs evaluated                 */
+    uint64_t nbr_old, nbr_new;    /* A_old / A_new: list entries of movers     */
+    uint64_t bytes_alg;           /* SURVEY 8(d) algorithmic bytes of the AOI part */
+    double   device_us;           /* device time of the tick (HIP events)      */
+} gw_tick_out;
+
+/* gw_sync_collect flags */
+#define GW_SYNC_COPY_TO_HOST   1u
+
+typedef struct gw_sync_out {
+    /* canonical order: sorted by (gate(watcher), entity, watcher) */
+    const gw_sync_record* rec;      /* host pointer (NULL unless COPY_TO_HOST) */
+    const gw_sync_record* rec_dev;  /* device pointer, always valid            */
+    uint64_t n_rec;
+    const uint64_t* gate_off;       /* host: n_gates+1 offsets into rec, by gate id */
+    uint32_t n_gates;               /* max gate id + 1                          */
+    uint64_t flagged;               /* entities whose syncInfoFlag was set      */
+    uint64_t bytes_alg;
+    double   device_us;
+} gw_sync_out;
+
+typedef struct gw_ctx gw_ctx;
+
+/* Context on one HIP device (one process per GPU). */
+int  gw_init(int device_id, gw_ctx** out);
+void gw_shutdown(gw_ctx* ctx);
+const char* gw_last_error(const gw_ctx* ctx);
+
+/* Space.EnableAOI(d): d > 0.  bounds = {minx, minz, maxx, maxz} sizes the
+ * uniform grid (NULL = Space.GetSpaceRange default, Space.go:52-54); entities
+ * outside the bounds are still exact (clamped cells), only slower. */
+int  gw_space_create(gw_ctx* ctx, float aoi_dist, uint32_t capacity,
+                     const float* bounds, uint32_t* space_id, uint32_t* slot_base);
+int  gw_space_destroy(gw_ctx* ctx, uint32_t space_id);   /* space must be empty */
+
+/* Buffer ops (host memory, validated against the entity state; copied). */
+int  gw_submit(gw_ctx* ctx, const gw_op* ops, uint32_t n);
+/* Buffer ops already resident in device memory (not validated; the caller
+ * guarantees a valid sequence).  The pointer must stay valid until gw_tick. */
+int  gw_submit_device(gw_ctx* ctx, const gw_op* dev_ops, uint32_t n);
+
+/* Attach / detach clients: gate 0 = no client (GameClient nil). */
+int  gw_set_clients(gw_ctx* ctx, const uint32_t* slots, const uint16_t* gates, uint32_t n);
+
+/* Flush all buffered ops of all spaces: AOI update + canonical net events. */
+int  gw_tick(gw_ctx* ctx, uint32_t flags, gw_tick_out* out);
+
+/* CollectEntitySyncInfos for all spaces of the context; clears the flags. */
+int  gw_sync_collect(gw_ctx* ctx, uint32_t flags, gw_sync_out* out);
+
+/* InterestedIn(slot) == InterestedBy(slot), ascending slots. *n receives the
+ * full count even when it exceeds cap. */
+int  gw_neighbors(gw_ctx* ctx, uint32_t slot, uint32_t* buf, uint32_t cap, uint32_t* n);
+
+/* Per-stage device timings of the last tick / collect (HIP events on the
+ * library's stream), for bench.py's roofline.  names[i] are static strings. */
+#define GW_MAX_STAGES 32
+typedef struct gw_stage_times {
+    uint32_t n;
+    const char* name[GW_MAX_STAGES];
+    double   us[GW_MAX_STAGES];
+    uint64_t bytes_alg[GW_MAX_STAGES];   /* algorithmic bytes of the stage      */
+} gw_stage_times;
+int  gw_set_profiling(gw_ctx* ctx, int enable);
+int  gw_get_stage_times(gw_ctx* ctx, gw_stage_times* out);
+
+/* Total neighbour-list entries held (sum over slots of |InterestedIn|). */
+int  gw_total_neighbors(gw_ctx* ctx, uint64_t* out);
+
+/* Device pointer helpers for device-resident benchmarking. */
+int  gw_device_alloc(gw_ctx* ctx, size_t bytes, void** dev_ptr);
+int  gw_device_free(gw_ctx* ctx, void* dev_ptr);
+int  gw_memcpy_h2d(gw_ctx* ctx, void* dst_dev, const void* src_host, size_t bytes);
+int  gw_memcpy_d2h(gw_ctx* ctx, void* dst_host, const void* src_dev, size_t bytes);
+int  gw_synchronize(gw_ctx* ctx);
+
+/* ABI version (bumped on layout changes). */
+#define GW_ABI_VERSION 1
+int  gw_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPUAOI_H */

@@ -1,0 +1,31 @@
+# Build of the MI355X-native AOI library (gfx950 only) and the CPU oracle.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+# strict float32: the window bounds fl(c-d), fl(c+d) must round like Go's float32
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
+LIBDIR   := goworld_amd/lib
+SRC      := goworld_amd/csrc/kernels.hip goworld_amd/csrc/capi.cpp
+HDR      := goworld_amd/csrc/prim.hpp goworld_amd/csrc/gw_internal.hpp include/gpuaoi.h
+OBJ      := $(LIBDIR)/kernels.o $(LIBDIR)/capi.o
+
+all: $(LIBDIR)/libgpuaoi.so oracle
+
+$(LIBDIR)/kernels.o: goworld_amd/csrc/kernels.hip $(HDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIBDIR)/capi.o: goworld_amd/csrc/capi.cpp $(HDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIBDIR)/libgpuaoi.so: $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ)
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -rf $(LIBDIR)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean

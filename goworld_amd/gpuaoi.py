@@ -1,0 +1,279 @@
+"""ctypes binding of the C ABI in include/gpuaoi.h (libgpuaoi.so).
+
+This is the Python-side host of the drop-in boundary, used by tests/ and
+bench.py.  It mirrors the reference's calls one to one:
+
+  GpuAOI.create_space(d, ...)   <- Space.EnableAOI(d)          (engine/entity/Space.go:91-106)
+  GpuAOI.submit(ops)            <- aoiMgr.Enter/Moved/Leave    (Space.go:201-203, 233-235, 250)
+  GpuAOI.tick()                 <- OnEnterAOI/OnLeaveAOI fan-out (Entity.go:227-246), batched
+  GpuAOI.sync_collect()         <- CollectEntitySyncInfos       (Entity.go:1221-1267)
+  GpuAOI.neighbors(slot)        <- Entity.InterestedIn / InterestedBy (Entity.go:53-54)
+
+There is no CPU fallback: if the HIP library is missing or a call fails, an
+exception is raised (errors map to the reference's gwlog.Panicf on misuse).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+import os
+
+import numpy as np
+
+from .traces import OP_DTYPE
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgpuaoi.so")
+
+EVENT_DTYPE = np.dtype([("watcher", "<u4"), ("target", "<u4")])
+REC_DTYPE = np.dtype([("watcher", "<u4"), ("entity", "<u4"), ("x", "<f4"), ("y", "<f4"),
+                      ("z", "<f4"), ("yaw", "<f4")])
+
+TICK_COPY_TO_HOST, TICK_NO_EVENTS = 1, 2
+SYNC_COPY_TO_HOST = 1
+MAX_STAGES = 32
+
+_u64, _u32, _f64 = C.c_uint64, C.c_uint32, C.c_double
+
+
+class TickOut(C.Structure):
+    _fields_ = [("enter", C.c_void_p), ("leave", C.c_void_p), ("enter_dev", C.c_void_p),
+                ("leave_dev", C.c_void_p), ("n_enter", _u64), ("n_leave", _u64), ("ops", _u64),
+                ("movers", _u64), ("pairs_tested", _u64), ("nbr_old", _u64), ("nbr_new", _u64),
+                ("bytes_alg", _u64), ("device_us", _f64)]
+
+
+class SyncOut(C.Structure):
+    _fields_ = [("rec", C.c_void_p), ("rec_dev", C.c_void_p), ("n_rec", _u64),
+                ("gate_off", C.POINTER(_u64)), ("n_gates", _u32), ("flagged", _u64),
+                ("bytes_alg", _u64), ("device_us", _f64)]
+
+
+class StageTimes(C.Structure):
+    _fields_ = [("n", _u32), ("name", C.c_char_p * MAX_STAGES), ("us", _f64 * MAX_STAGES),
+                ("bytes_alg", _u64 * MAX_STAGES)]
+
+
+class GwError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"gpuaoi error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load libgpuaoi.so; raises if it was not built (no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `make` (HIP/gfx950); "
+                               "there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        vp = C.c_void_p
+        L.gw_abi_version.restype = C.c_int
+        L.gw_init.argtypes = [C.c_int, C.POINTER(vp)]
+        L.gw_shutdown.argtypes = [vp]
+        L.gw_shutdown.restype = None
+        L.gw_last_error.argtypes = [vp]
+        L.gw_last_error.restype = C.c_char_p
+        L.gw_space_create.argtypes = [vp, C.c_float, _u32, vp, C.POINTER(_u32), C.POINTER(_u32)]
+        L.gw_space_destroy.argtypes = [vp, _u32]
+        L.gw_submit.argtypes = [vp, vp, _u32]
+        L.gw_submit_device.argtypes = [vp, vp, _u32]
+        L.gw_set_clients.argtypes = [vp, vp, vp, _u32]
+        L.gw_tick.argtypes = [vp, _u32, C.POINTER(TickOut)]
+        L.gw_sync_collect.argtypes = [vp, _u32, C.POINTER(SyncOut)]
+        L.gw_neighbors.argtypes = [vp, _u32, vp, _u32, C.POINTER(_u32)]
+        L.gw_set_profiling.argtypes = [vp, C.c_int]
+        L.gw_get_stage_times.argtypes = [vp, C.POINTER(StageTimes)]
+        L.gw_total_neighbors.argtypes = [vp, C.POINTER(_u64)]
+        L.gw_device_alloc.argtypes = [vp, C.c_size_t, C.POINTER(vp)]
+        L.gw_device_free.argtypes = [vp, vp]
+        L.gw_memcpy_h2d.argtypes = [vp, vp, vp, C.c_size_t]
+        L.gw_memcpy_d2h.argtypes = [vp, vp, vp, C.c_size_t]
+        L.gw_synchronize.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_space_create",
+            "gw_space_destroy", "gw_submit", "gw_submit_device", "gw_set_clients", "gw_tick",
+            "gw_sync_collect", "gw_neighbors", "gw_set_profiling", "gw_get_stage_times",
+            "gw_total_neighbors", "gw_device_alloc", "gw_device_free", "gw_memcpy_h2d",
+            "gw_memcpy_d2h", "gw_synchronize"]
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+@dataclasses.dataclass
+class TickResult:
+    enter: np.ndarray | None
+    leave: np.ndarray | None
+    n_enter: int
+    n_leave: int
+    ops: int
+    movers: int
+    pairs_tested: int
+    nbr_old: int
+    nbr_new: int
+    bytes_alg: int
+    device_us: float
+    enter_dev: int = 0
+    leave_dev: int = 0
+
+
+@dataclasses.dataclass
+class SyncResult:
+    records: np.ndarray | None
+    n_rec: int
+    gate_off: np.ndarray
+    flagged: int
+    bytes_alg: int
+    device_us: float
+    rec_dev: int = 0
+
+
+class GpuAOI:
+    """One gw_ctx on one HIP device (one process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        self._h = C.c_void_p()
+        rc = lib().gw_init(device, C.byref(self._h))
+        if rc:
+            raise GwError(rc, "gw_init failed (no HIP device?)")
+        self.spaces: list[tuple[int, int, int]] = []   # (id, base, capacity)
+
+    def _chk(self, rc: int):
+        if rc:
+            raise GwError(rc, lib().gw_last_error(self._h).decode())
+
+    def close(self):
+        if self._h:
+            lib().gw_shutdown(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # Space.EnableAOI(d)
+    def create_space(self, d: float, capacity: int, bounds=None) -> tuple[int, int]:
+        sid, base = _u32(), _u32()
+        b = None
+        if bounds is not None:
+            barr = (C.c_float * 4)(*[float(v) for v in bounds])
+            b = C.cast(barr, C.c_void_p)
+        self._chk(lib().gw_space_create(self._h, float(d), int(capacity), b, C.byref(sid), C.byref(base)))
+        self.spaces.append((sid.value, base.value, capacity))
+        return sid.value, base.value
+
+    def destroy_space(self, sid: int):
+        self._chk(lib().gw_space_destroy(self._h, sid))
+
+    def submit(self, ops: np.ndarray):
+        ops = np.ascontiguousarray(ops, dtype=OP_DTYPE)
+        self._chk(lib().gw_submit(self._h, _p(ops), len(ops)))
+
+    def submit_device(self, dev_ptr: int, n: int):
+        self._chk(lib().gw_submit_device(self._h, C.c_void_p(dev_ptr), n))
+
+    def set_clients(self, slots, gates):
+        s = np.ascontiguousarray(slots, dtype=np.uint32)
+        g = np.ascontiguousarray(gates, dtype=np.uint16)
+        self._chk(lib().gw_set_clients(self._h, _p(s), _p(g), len(s)))
+
+    def tick(self, copy: bool = True, no_events: bool = False) -> TickResult:
+        o = TickOut()
+        fl = (TICK_COPY_TO_HOST if copy else 0) | (TICK_NO_EVENTS if no_events else 0)
+        self._chk(lib().gw_tick(self._h, fl, C.byref(o)))
+        e = l = None
+        if copy and not no_events:
+            e = np.zeros(o.n_enter, EVENT_DTYPE)
+            l = np.zeros(o.n_leave, EVENT_DTYPE)
+            if o.n_enter:
+                C.memmove(_p(e), o.enter, o.n_enter * 8)
+            if o.n_leave:
+                C.memmove(_p(l), o.leave, o.n_leave * 8)
+        return TickResult(e, l, o.n_enter, o.n_leave, o.ops, o.movers, o.pairs_tested, o.nbr_old,
+                          o.nbr_new, o.bytes_alg, o.device_us, o.enter_dev or 0, o.leave_dev or 0)
+
+    def sync_collect(self, copy: bool = True) -> SyncResult:
+        o = SyncOut()
+        self._chk(lib().gw_sync_collect(self._h, SYNC_COPY_TO_HOST if copy else 0, C.byref(o)))
+        r = None
+        if copy:
+            r = np.zeros(o.n_rec, REC_DTYPE)
+            if o.n_rec:
+                C.memmove(_p(r), o.rec, o.n_rec * 24)
+        goff = np.array([o.gate_off[i] for i in range(o.n_gates + 1)], dtype=np.uint64)
+        return SyncResult(r, o.n_rec, goff, o.flagged, o.bytes_alg, o.device_us, o.rec_dev or 0)
+
+    def neighbors(self, slot: int) -> np.ndarray:
+        n = _u32()
+        self._chk(lib().gw_neighbors(self._h, slot, None, 0, C.byref(n)))
+        buf = np.zeros(n.value, np.uint32)
+        if n.value:
+            self._chk(lib().gw_neighbors(self._h, slot, _p(buf), n.value, C.byref(n)))
+        return buf
+
+    def total_neighbors(self) -> int:
+        v = _u64()
+        self._chk(lib().gw_total_neighbors(self._h, C.byref(v)))
+        return v.value
+
+    def set_profiling(self, on: bool):
+        self._chk(lib().gw_set_profiling(self._h, 1 if on else 0))
+
+    def stage_times(self) -> list[tuple[str, float, int]]:
+        t = StageTimes()
+        self._chk(lib().gw_get_stage_times(self._h, C.byref(t)))
+        return [(t.name[i].decode(), t.us[i], t.bytes_alg[i]) for i in range(t.n)]
+
+    # device memory helpers (bench: inputs resident in HBM)
+    def dev_alloc(self, nbytes: int) -> int:
+        p = C.c_void_p()
+        self._chk(lib().gw_device_alloc(self._h, nbytes, C.byref(p)))
+        return p.value
+
+    def dev_free(self, ptr: int):
+        self._chk(lib().gw_device_free(self._h, C.c_void_p(ptr)))
+
+    def h2d(self, dev_ptr: int, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        self._chk(lib().gw_memcpy_h2d(self._h, C.c_void_p(dev_ptr), _p(arr), arr.nbytes))
+
+    def d2h(self, arr: np.ndarray, dev_ptr: int):
+        self._chk(lib().gw_memcpy_d2h(self._h, _p(arr), C.c_void_p(dev_ptr), arr.nbytes))
+
+    def synchronize(self):
+        self._chk(lib().gw_synchronize(self._h))
+
+
+def load_space(g: GpuAOI, tr, bounds=None, chunk: int = 1 << 21) -> tuple[int, int]:
+    """Create a space for a SpaceTrace and bulk-load its initial population.
+
+    The bulk load is Enter ops in trace order, flushed in chunks with
+    TICK_NO_EVENTS (the restore path, Space.go:209-214); ticks compose, so
+    chunking equals one sequential Enter stream."""
+    from .traces import enter_ops, with_global_slots
+    sid, base = g.create_space(tr.d, tr.capacity, bounds if bounds is not None else tr.bounds)
+    ops = with_global_slots(enter_ops(tr.init_slots, tr.init_x, tr.init_y, tr.init_z, tr.init_yaw), base)
+    for i in range(0, len(ops), chunk):
+        g.submit(ops[i:i + chunk])
+        g.tick(copy=False, no_events=True)
+    if tr.gates is not None:
+        nz = np.nonzero(tr.gates)[0]
+        g.set_clients(nz.astype(np.uint32) + base, tr.gates[nz])
+    return sid, base

@@ -1,0 +1,266 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on the
+same seeded traces — bit-exact events, sync records and neighbour lists.
+
+The oracle engines are equal to each other on every trace (test_oracle.py), so
+the GPU is checked against ORC_SEQRULE for speed and against ORC_XZLIST (the
+go-aoi restatement) on the small and adversarial traces.  Parity at the go-aoi
+boundary itself is unpinned (see oracle/orc.h).
+"""
+import numpy as np
+import pytest
+
+from goworld_amd import gpuaoi, traces as T
+from oracle import pyorc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx_factory():
+    made = []
+
+    def make():
+        g = gpuaoi.GpuAOI(0)
+        made.append(g)
+        return g
+    yield make
+    for g in made:
+        g.close()
+
+
+def _sorted_records(recs, gates_of):
+    if len(recs) == 0:
+        return recs
+    g = gates_of[recs["watcher"]]
+    order = np.lexsort((recs["watcher"], recs["entity"], g))
+    return recs[order]
+
+
+class Harness:
+    """One GPU context with several spaces, each mirrored by an oracle space."""
+
+    def __init__(self, g, trs, mode=pyorc.SEQRULE):
+        self.g, self.trs = g, trs
+        self.orcs, self.bases = [], []
+        cap_total = 0
+        for tr in trs:
+            sid, base = gpuaoi.load_space(g, tr)
+            o = pyorc.OracleSpace(tr.capacity, tr.d, mode)
+            pyorc.load_trace(o, tr)
+            self.orcs.append(o)
+            self.bases.append(base)
+            cap_total = base + tr.capacity
+        self.gates = np.zeros(cap_total, np.uint16)
+        for tr, b in zip(trs, self.bases):
+            if tr.gates is not None:
+                self.gates[b:b + tr.capacity] = tr.gates
+
+    def check_collect(self):
+        r = self.g.sync_collect()
+        exp = []
+        for o, b in zip(self.orcs, self.bases):
+            e = o.collect()
+            e["watcher"] += b
+            e["entity"] += b
+            exp.append(e)
+        exp = _sorted_records(np.concatenate(exp) if exp else np.zeros(0, pyorc.REC_DTYPE), self.gates)
+        assert r.n_rec == len(exp)
+        assert r.records.tobytes() == exp.tobytes(), "sync records differ"
+        # gate offsets partition the canonical stream
+        goff = r.gate_off
+        assert goff[0] == 0 and goff[-1] == r.n_rec
+        for gid in range(len(goff) - 1):
+            seg = r.records[goff[gid]:goff[gid + 1]]
+            assert np.all(self.gates[seg["watcher"]] == gid)
+        return r
+
+    def step(self, t):
+        ops = [T.with_global_slots(tr.ticks[t], b) for tr, b in zip(self.trs, self.bases)]
+        self.g.submit(np.concatenate(ops))
+        res = self.g.tick()
+        ee, ll = [], []
+        for tr, o, b in zip(self.trs, self.orcs, self.bases):
+            assert o.tick(tr.ticks[t]) == 0
+            e, l = o.events()
+            e = e.copy(); l = l.copy()
+            for a in (e, l):
+                a["watcher"] += b
+                a["target"] += b
+            ee.append(e); ll.append(l)
+        ee, ll = np.concatenate(ee), np.concatenate(ll)
+        assert res.n_enter == len(ee) and res.n_leave == len(ll), (res.n_enter, len(ee), res.n_leave, len(ll))
+        assert res.enter.tobytes() == ee.tobytes(), "enter events differ"
+        assert res.leave.tobytes() == ll.tobytes(), "leave events differ"
+        return res
+
+    def check_lists(self, sample=None):
+        for tr, o, b in zip(self.trs, self.orcs, self.bases):
+            slots = range(tr.capacity) if sample is None else sample
+            for s in slots:
+                got = self.g.neighbors(b + s)
+                exp = o.neighbors(s).astype(np.uint32) + b
+                assert np.array_equal(got, exp), f"neighbour list of slot {s} differs"
+
+
+def test_tiny_hand_made(ctx_factory):
+    g = ctx_factory()
+    sid, base = g.create_space(100.0, 8)
+    o = pyorc.OracleSpace(8, 100.0, pyorc.XZLIST)
+    ops = T.make_ops(4)
+    ops["kind"] = 1
+    ops["sync_flags"] = 3
+    ops["slot"] = [0, 1, 2, 3]
+    ops["x"] = [0, 50, 100, 400]
+    ops["z"] = [0, 0, 100, 0]
+    g.set_clients(np.arange(4, dtype=np.uint32) + base, np.ones(4, np.uint16))
+    for s in range(4):
+        o.set_client(s, 1)
+    g.submit(T.with_global_slots(ops, base))
+    r = g.tick()
+    assert o.tick(ops) == 0
+    e, l = o.events()
+    assert r.enter.tobytes() == e.tobytes() and r.n_leave == 0 == len(l)
+    assert list(g.neighbors(base + 0)) == [base + 1, base + 2]
+    rec = g.sync_collect().records
+    assert rec.tobytes() == o.collect().tobytes()
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_adversarial_rounding_and_churn_vs_xzlist(ctx_factory, seed):
+    tr = T.adversarial_trace(seed, n=300, ticks=12)
+    h = Harness(ctx_factory(), [tr], mode=pyorc.XZLIST)
+    h.check_collect()
+    for t in range(len(tr.ticks)):
+        h.step(t)
+        h.check_collect()
+    h.check_lists()
+
+
+def test_config1_float_walk_vs_xzlist(ctx_factory):
+    tr = T.config1(ticks=30, n=1000, big_steps=True)
+    h = Harness(ctx_factory(), [tr], mode=pyorc.XZLIST)
+    h.check_collect()
+    for t in range(len(tr.ticks)):
+        h.step(t)
+        h.check_collect()
+    h.check_lists()
+
+
+def test_config2_uniform_100k(ctx_factory):
+    tr = T.config2(ticks=3)
+    h = Harness(ctx_factory(), [tr])
+    h.check_collect()
+    for t in range(len(tr.ticks)):
+        h.step(t)
+        h.check_collect()
+    h.check_lists(sample=range(0, tr.capacity, 97))
+
+
+def test_hotspot_clustered_200k(ctx_factory):
+    tr = T.config3(ticks=2, n=200_000, side=14654.0)   # 1M-config density, smaller world
+    h = Harness(ctx_factory(), [tr])
+    h.check_collect()
+    for t in range(len(tr.ticks)):
+        r = h.step(t)
+        assert r.n_enter > 0
+        h.check_collect()
+    h.check_lists(sample=range(0, tr.capacity, 211))
+
+
+def test_many_spaces_one_launch(ctx_factory):
+    trs = [T.config4_space(s, ticks=3, n=300) for s in range(40)]
+    for i, tr in enumerate(trs):
+        tr.gates = np.where(tr.gates > 0, 1 + (i % 3), 0).astype(np.uint16)   # 3 gates
+    h = Harness(ctx_factory(), trs)
+    h.check_collect()
+    for t in range(3):
+        h.step(t)
+        h.check_collect()
+    h.check_lists()
+
+
+def test_everyone_at_one_point(ctx_factory):
+    """Maximum skew: every entity in one cell, K = N-1 (hotspot stress)."""
+    n = 3000
+    tr = T.SpaceTrace(n=n, capacity=n, d=100.0, bounds=(-1000, -1000, 1000, 1000),
+                      init_slots=np.arange(n, dtype=np.uint32), init_x=np.full(n, 5.0, np.float32),
+                      init_y=np.zeros(n, np.float32), init_z=np.full(n, -5.0, np.float32),
+                      init_yaw=np.zeros(n, np.float32), ticks=[], gates=np.ones(n, np.uint16))
+    ops = T.make_ops(n // 2)
+    ops["kind"] = T.OP_MOVED
+    ops["sync_flags"] = 2
+    ops["slot"] = np.arange(0, n, 2)
+    ops["x"] = np.where(np.arange(n // 2) % 3 == 0, 500.0, 5.0)
+    ops["z"] = -5.0
+    tr.ticks = [ops]
+    h = Harness(ctx_factory(), [tr])
+    h.check_collect()
+    h.step(0)
+    h.check_collect()
+    h.check_lists(sample=range(0, n, 37))
+
+
+def test_outside_bounds_and_large_coordinates(ctx_factory):
+    """Entities outside the grid bounds land in clamped edge cells: still exact."""
+    tr = T.adversarial_trace(21, n=200, ticks=6)
+    for a in (tr.init_x, tr.init_z):
+        a *= np.float32(40.0)          # +-12000, far outside the +-500 bounds
+    for ops in tr.ticks:
+        ops["x"] *= np.float32(40.0)
+        ops["z"] *= np.float32(40.0)
+    h = Harness(ctx_factory(), [tr], mode=pyorc.XZLIST)
+    for t in range(len(tr.ticks)):
+        h.step(t)
+        h.check_collect()
+    h.check_lists()
+
+
+def test_empty_and_sync_only_ticks(ctx_factory):
+    g = ctx_factory()
+    tr = T.dyadic_walk_trace(9, 500, 1024.0, 100.0, 1)
+    h = Harness(g, [tr])
+    h.check_collect()
+    r = g.tick()                       # nothing submitted
+    assert r.n_enter == r.n_leave == 0
+    ops = T.make_ops(5)
+    ops["kind"] = T.OP_SYNC
+    ops["sync_flags"] = 3
+    ops["slot"] = np.arange(5)
+    ops["yaw"] = 1.25
+    ops["x"] = tr.init_x[:5]
+    ops["z"] = tr.init_z[:5]
+    tr.ticks = [ops]
+    r = h.step(0)
+    assert r.n_enter == r.n_leave == 0
+    h.check_collect()
+
+
+def test_invalid_ops_raise(ctx_factory):
+    g = ctx_factory()
+    sid, base = g.create_space(100.0, 4)
+    bad = T.make_ops(1)
+    bad["kind"] = T.OP_MOVED
+    bad["slot"] = base
+    with pytest.raises(gpuaoi.GwError):
+        g.submit(bad)                  # Moved before Enter (reference: nil implData panic)
+    bad["kind"] = T.OP_ENTER
+    bad["slot"] = base + 99
+    with pytest.raises(gpuaoi.GwError):
+        g.submit(bad)
+    with pytest.raises(gpuaoi.GwError):
+        g.create_space(0.0, 4)         # EnableAOI(0) panics (Space.go:92-94)
+
+
+def test_repeat_runs_are_deterministic(ctx_factory):
+    tr = T.adversarial_trace(31, n=300, ticks=5)
+    outs = []
+    for _ in range(2):
+        g = ctx_factory()
+        gpuaoi.load_space(g, tr)
+        seq = []
+        for ops in tr.ticks:
+            g.submit(ops)
+            r = g.tick()
+            seq.append((r.enter.tobytes(), r.leave.tobytes(), g.sync_collect().records.tobytes()))
+        outs.append(seq)
+    assert outs[0] == outs[1]

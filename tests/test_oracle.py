@@ -1,0 +1,229 @@
+"""CPU tests of the oracle (test infrastructure) against the reference's
+known-answer facts and against itself.
+
+Parity at the go-aoi boundary is UNPINNED (go-aoi v0.2.0 and Go are absent;
+the reference has no AOI/sync tests or fixtures).  What the
+reference source does pin is checked here:
+  (i)   Y is ignored by AOI                    engine/entity/Space.go:202,250
+  (ii)  callbacks are symmetric: InterestedIn == InterestedBy
+                                               engine/entity/Entity.go:227-246
+  (iii) Leave removes every relation + destroy messages to clients
+                                               Space.go:233-237, GameClient.go:55-59
+  (iv)  sync record wire layout (48 B LE, u16 1502 + u16 gate header)
+                                               Entity.go:1210-1254, proto.go:107-109
+  (v)   own-client record only for non-client moves / Enter / SetYaw
+                                               Entity.go:1199-1204, Space.go:196, Entity.go:1286
+  (vi)  an entity at distance 0 is a neighbour examples/test_game/Avatar.go:264-276
+Plus: the XZList restatement equals an independent brute-force restatement and
+the batched seq-rule reducer (the GPU's contract) on every trace, including
+rounding-adversarial and churn traces.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+from goworld_amd import traces as T
+from oracle import pyorc
+
+MODES = [pyorc.XZLIST, pyorc.BRUTE, pyorc.SEQRULE]
+
+
+def run_mode(tr, mode, ticks=None):
+    sp = pyorc.OracleSpace(tr.capacity, tr.d, mode)
+    pyorc.load_trace(sp, tr)
+    outs = [sp.collect().tobytes()]
+    for ops in tr.ticks[:ticks]:
+        assert sp.tick(ops) == 0
+        e, l = sp.events()
+        outs.append((e.tobytes(), l.tobytes(), sp.collect().tobytes()))
+    return outs, sp
+
+
+def one(d=100.0, cap=8, mode=pyorc.XZLIST):
+    return pyorc.OracleSpace(cap, d, mode)
+
+
+def op(kind, slot, x=0.0, z=0.0, y=0.0, yaw=0.0, flags=3):
+    o = T.make_ops(1)
+    o["kind"], o["slot"], o["x"], o["y"], o["z"], o["yaw"], o["sync_flags"] = kind, slot, x, y, z, yaw, flags
+    return o
+
+
+@pytest.mark.parametrize("name,make", [
+    ("adversarial", lambda: T.adversarial_trace(11, n=300, ticks=12)),
+    ("adversarial_nochurn", lambda: T.adversarial_trace(12, n=250, ticks=10, churn=False)),
+    ("config1b", lambda: T.config1(ticks=30, n=300, big_steps=True)),
+    ("config1", lambda: T.config1(ticks=20, n=300)),
+    ("dyadic", lambda: T.dyadic_walk_trace(5, 1500, 1024.0, 100.0, 4)),
+    ("hotspot", lambda: T.dyadic_walk_trace(6, 1500, 4096.0, 100.0, 4, hot_frac=0.5, n_hot=3, sigma=60.0,
+                                            hot_step_q=2048)),
+])
+def test_three_engines_agree(name, make):
+    tr = make()
+    ref, sp0 = run_mode(tr, pyorc.XZLIST)
+    for mode in (pyorc.BRUTE, pyorc.SEQRULE):
+        got, sp = run_mode(tr, mode)
+        assert got == ref, f"mode {mode} diverges from XZList on {name}"
+        for s in range(tr.capacity):
+            assert np.array_equal(sp.neighbors(s), sp0.neighbors(s))
+
+
+def test_adversarial_trace_really_is_asymmetric():
+    tr = T.adversarial_trace(11, n=300, ticks=1)
+    x, z, d = tr.init_x, tr.init_z, np.float32(tr.d)
+    asym = 0
+    for a in range(tr.n):
+        for b in range(tr.n):
+            if a != b:
+                ab = pyorc.in_window(x[a], z[a], d, x[b], z[b])
+                ba = pyorc.in_window(x[b], z[b], d, x[a], z[a])
+                asym += ab != ba
+    assert asym > 0
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_bulk_enter_equals_sequential_enter(mode):
+    tr = T.adversarial_trace(3, n=200, ticks=1, churn=False)
+    a = pyorc.OracleSpace(tr.capacity, tr.d, mode)
+    a.bulk_enter(tr.init_slots, tr.init_x, tr.init_y, tr.init_z, tr.init_yaw)
+    b = pyorc.OracleSpace(tr.capacity, tr.d, mode)
+    ops = T.enter_ops(tr.init_slots, tr.init_x, tr.init_y, tr.init_z, tr.init_yaw)
+    assert b.tick(ops) == 0
+    for s in range(tr.capacity):
+        assert np.array_equal(a.neighbors(s), b.neighbors(s))
+    # continuing both with the same ticks stays identical
+    tr2 = T.adversarial_trace(3, n=200, ticks=5, churn=True)
+    for ops in tr2.ticks:
+        assert a.tick(ops) == 0 and b.tick(ops) == 0
+        ea, la = a.events()
+        eb, lb = b.events()
+        assert np.array_equal(ea, eb) and np.array_equal(la, lb)
+
+
+def test_y_is_ignored():                                     # (i)
+    sp = one()
+    sp.tick(np.concatenate([op(1, 0, 0, 0, y=0), op(1, 1, 50, 50, y=1e6)]))
+    assert list(sp.neighbors(0)) == [1]
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_symmetric_interest_sets(mode):                      # (ii)
+    tr = T.adversarial_trace(5, n=200, ticks=6)
+    _, sp = run_mode(tr, mode)
+    for s in range(tr.capacity):
+        assert np.array_equal(sp.neighbors(s), sp.interested_by(s))
+        for t in sp.neighbors(s):
+            assert s in sp.neighbors(int(t))
+
+
+def test_leave_removes_everything_and_sends_destroys():      # (iii)
+    sp = one()
+    sp.set_client(0, 1); sp.set_client(2, 1)
+    sp.tick(np.concatenate([op(1, 0, 0, 0), op(1, 1, 10, 10), op(1, 2, -10, 5), op(1, 3, 500, 500)]))
+    assert sorted(sp.neighbors(1)) == [0, 2]
+    assert sp.tick(op(3, 1)) == 0
+    e, l = sp.events()
+    assert len(e) == 0
+    assert sorted(map(tuple, l.tolist())) == [(0, 1), (1, 0), (1, 2), (2, 1)]
+    assert len(sp.neighbors(1)) == 0 and 1 not in sp.neighbors(0) and 1 not in sp.neighbors(2)
+    _, _, creates, destroys = sp.raw_counts()
+    assert destroys == 2            # only watchers 0 and 2 have clients (GameClient.go:55-59)
+
+
+def test_sync_wire_layout():                                 # (iv)
+    sp = one()
+    sp.set_client(0, 7); sp.set_client(1, 7)
+    sp.tick(np.concatenate([op(1, 0, 1.5, 2.5, y=3.0, yaw=0.25), op(1, 1, 3.0, 4.0, y=-1, yaw=1.0)]))
+    recs = sp.collect()
+    wire = sp.wire()
+    assert wire[:4] == struct.pack("<HH", 1502, 7)
+    assert len(wire) == 4 + 48 * len(recs)
+    for i, r in enumerate(recs):
+        rec = wire[4 + 48 * i: 4 + 48 * (i + 1)]
+        assert rec[:16] == pyorc.fixed_uuid(int(r["watcher"]) | 0x80000000)
+        assert rec[16:32] == pyorc.fixed_uuid(int(r["entity"]))
+        assert struct.unpack("<4f", rec[32:]) == (r["x"], r["y"], r["z"], r["yaw"])
+    # GenFixedUUID: base64 (A-Z a-z 0-9 _ .) of 12 left-padded bytes (uuid.go:48-59)
+    assert pyorc.fixed_uuid(0) == b"A" * 16
+    assert pyorc.fixed_uuid(1) == b"AAAAAAAAAAAAAAAB"
+
+
+def test_own_client_record_rules():                          # (v)
+    sp = one()
+    for s in range(3):
+        sp.set_client(s, 1)
+    sp.tick(np.concatenate([op(1, 0, 0, 0), op(1, 1, 1, 1), op(1, 2, 2, 2)]))
+    sp.collect()
+    sp.tick(op(2, 0, 5, 5, flags=2))      # syncPositionYawFromClient: fromClient=true -> neighbours only
+    r = sp.collect()
+    assert sorted(zip(r["watcher"], r["entity"])) == [(1, 0), (2, 0)]
+    sp.tick(op(2, 0, 6, 6, flags=3))      # SetPosition: own + neighbours
+    r = sp.collect()
+    assert sorted(zip(r["watcher"], r["entity"])) == [(0, 0), (1, 0), (2, 0)]
+    sp.tick(op(4, 1, 1, 1, yaw=2.0, flags=3))   # SetYaw (no AOI adjust)
+    r = sp.collect()
+    assert sorted(zip(r["watcher"], r["entity"])) == [(0, 1), (1, 1), (2, 1)]
+    assert all(r["yaw"] == np.float32(2.0))
+    assert len(sp.collect()) == 0         # flags cleared by the collect
+
+
+def test_distance_zero_and_inclusive_boundary():             # (vi)
+    sp = one()
+    d = np.float32(100.0)
+    x0 = np.float32(0.1)
+    edge = np.float32(x0 + d)
+    beyond = np.nextafter(edge, np.float32(np.inf), dtype=np.float32)
+    sp.tick(np.concatenate([op(1, 0, x0, 0), op(1, 1, x0, 0), op(1, 2, edge, 0), op(1, 3, beyond, 0)]))
+    nb = list(sp.neighbors(0))
+    assert 1 in nb and 2 in nb                  # distance 0 and exactly fl(x+d): inclusive
+    # slot 3 entered last, so its own window decides the pair (seq rule)
+    assert (3 in nb) == pyorc.in_window(beyond, 0, d, x0, 0)
+    assert not pyorc.in_window(x0, 0, d, beyond, 0)
+
+
+def test_rounding_asymmetry_decided_by_last_mover():
+    """fl(a+d) rounds up while fl(b-d) rounds down: inWin_a(b) != inWin_b(a).
+    The pair's relation is decided by whichever moved last."""
+    d = np.float32(100.0)
+    found = None
+    for a in np.linspace(0.1, 3.0, 4000, dtype=np.float32):
+        b = np.float32(a + d)                 # on a's upper edge
+        for cand in (b, np.nextafter(b, np.float32(np.inf), dtype=np.float32),
+                     np.nextafter(b, np.float32(-np.inf), dtype=np.float32)):
+            ab = pyorc.in_window(a, 0, d, cand, 0)
+            ba = pyorc.in_window(cand, 0, d, a, 0)
+            if ab != ba:
+                found = (a, cand, ab, ba)
+                break
+        if found:
+            break
+    assert found, "no asymmetric pair found"
+    a, b, ab, ba = found
+    for mode in MODES:
+        sp = one(mode=mode)
+        sp.tick(np.concatenate([op(1, 0, a, 0), op(1, 1, b, 0)]))       # 1 entered last -> inWin_1(0)
+        assert (1 in sp.neighbors(0)) == ba
+        sp.tick(op(2, 0, a, 0))                                           # 0 "moves" in place -> inWin_0(1)
+        assert (1 in sp.neighbors(0)) == ab
+        sp.tick(np.concatenate([op(2, 0, a, 0), op(2, 1, b, 0)]))       # both, 1 last
+        assert (1 in sp.neighbors(0)) == ba
+
+
+def test_invalid_sequences_rejected():
+    sp = one()
+    assert sp.tick(op(2, 0)) != 0            # Moved before Enter
+    sp = one()
+    assert sp.tick(np.concatenate([op(1, 0), op(1, 0)])) != 0   # double Enter
+    sp = one()
+    assert sp.tick(np.concatenate([op(1, 0), op(3, 0), op(1, 0, 5, 5)])) == 0   # leave + re-enter
+
+
+def test_net_events_cancel_transients():
+    sp = one(mode=pyorc.XZLIST)
+    sp.tick(np.concatenate([op(1, 0, 0, 0), op(1, 1, 500, 500)]))
+    # 1 walks into 0's window and back out within one tick: raw enter+leave, net nothing
+    assert sp.tick(np.concatenate([op(2, 1, 10, 10), op(2, 1, 500, 500)])) == 0
+    e, l = sp.events()
+    raw_e, raw_l, _, _ = sp.raw_counts()
+    assert len(e) == 0 and len(l) == 0 and raw_e == 2 and raw_l == 2

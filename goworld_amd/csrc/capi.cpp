@@ -1,15 +1,17 @@
 // capi.cpp — C ABI of include/gpuaoi.h on one HIP device.
 //
 // Host orchestration of the per-tick pipeline (kernels in kernels.hip):
-//   ops -> last-op dedupe -> movers -> grid (cell keys, LDS radix sort,
-//   cell_start scan) -> per-mover event bound [one host sync: size scratch,
-//   pool] -> diff -> event radix sort -> enter/leave split + watcher segments
-//   -> neighbour-list merge into the bump-allocated pool -> reset.
+//   ops -> grid (counting sort by cell) -> movers in cell order + leavers ->
+//   per-mover bounds and tiers [the one mid-tick host sync: size the event
+//   regions, reserve pool space] -> diff (tiers S/B/C) -> per-watcher offsets
+//   -> mirror scatter + own copy -> segment sorts -> op-less watchers' merges
+//   -> reset.
 // No torch, no CPU fallback: every compute step is a HIP kernel.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -63,22 +65,25 @@ struct gw_ctx {
     float4* pos = nullptr;
     uint32_t* flags = nullptr;
     uint16_t* gate = nullptr;
-    uint32_t* lst_off = nullptr;
-    uint32_t* lst_cnt = nullptr;
+    LstMeta* lst = nullptr;
+    uint8_t* is_mover = nullptr;
+    unsigned long long* cnt64 = nullptr;     // [slot_cap + 1], zero between ticks
     int32_t *last_pos = nullptr, *last_aoi = nullptr, *last_leave = nullptr;
     SpaceP* sp_dev = nullptr;
     uint32_t sp_cap = 0;
     uint32_t* pool = nullptr;
     uint64_t pool_cap = 0;
-    uint64_t h_pool_top = 0, h_total_entries = 0;
+    uint64_t h_pool_top = 0, h_total_entries = 0, h_live_caps = 0;
 
     DevStats* stats = nullptr;     // device
     DevStats* hstats = nullptr;    // pinned host
 
-    // scratch
-    DevBuf ops_buf, is_last, pre64, movers, keys0, vals0, keys1, vals1, cell_cnt, cell_start, se;
-    DevBuf ev0, ev1, packed, enter_d, leave_d, seg_start;
+    // tick scratch
+    DevBuf ops_buf, keys, cell_cnt, cell_start, cursor, se, pflag, pre, fpre;
+    DevBuf movers, bpk, tpk, reg_pk, tier_pre, list_s, list_b, list_c, c_temp_off, c_temp, own, mir, mir_cnt;
+    DevBuf off64, enter_d, leave_d, affected, bigseg, bigseg_off, bigseg_temp;
     DevBuf scan_tmp64, scan_tmp32, rs_hist, rs_scan_tmp;
+    // sync scratch
     DevBuf flag_mark, flag_pre, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1;
     uint32_t* scal32 = nullptr;    // small device scalars
 
@@ -94,9 +99,6 @@ struct gw_ctx {
     // outputs
     DevBuf h_enter, h_leave, h_rec;   // pinned host
     std::vector<uint64_t> gate_off;
-    gw_event* out_enter_dev = nullptr;
-    gw_event* out_leave_dev = nullptr;
-    gw_sync_record* out_rec_dev = nullptr;
 
     // profiling
     bool prof = false;
@@ -118,15 +120,16 @@ int set_err(gw_ctx* c, int code, const char* fmt, ...) {
     return code;
 }
 
-#define HIPCHK(expr)                                                                         \
-    do {                                                                                     \
-        hipError_t _e = (expr);                                                              \
-        if (_e != hipSuccess)                                                                \
+#define HIPCHK(expr)                                                                             \
+    do {                                                                                         \
+        hipError_t _e = (expr);                                                                  \
+        if (_e != hipSuccess)                                                                    \
             return set_err(c, GW_EDEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
-                           __FILE__, __LINE__);                                              \
+                           __FILE__, __LINE__);                                                  \
     } while (0)
 
-// (re)allocate scratch without preserving contents
+// (re)allocate scratch without preserving contents; callers only grow buffers
+// at points where the stream is idle (after a host sync)
 int ensure(gw_ctx* c, DevBuf& b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return 0;
@@ -199,12 +202,17 @@ void prof_begin(gw_ctx* c, const char* name) {
     s.bytes = 0;
     (void)hipEventRecord(s.a, c->st);
 }
-void prof_end(gw_ctx* c, uint64_t bytes) {
-    if (!c->prof) return;
+size_t prof_end(gw_ctx* c, uint64_t bytes) {
+    if (!c->prof) return 0;
     Stage& s = c->stages[c->nstage];
     s.bytes = bytes;
     (void)hipEventRecord(s.b, c->st);
+    size_t idx = c->nstage;
     if (c->nstage + 1 < GW_MAX_STAGES) c->nstage++;
+    return idx;
+}
+void prof_set_bytes(gw_ctx* c, size_t idx, uint64_t bytes) {
+    if (c->prof && idx < c->stages.size()) c->stages[idx].bytes = bytes;
 }
 void prof_collect(gw_ctx* c) {
     gw_stage_times& t = c->last_times;
@@ -250,8 +258,9 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->pos, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->flags, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->gate, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->lst_off, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->lst_cnt, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->lst, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->is_mover, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->cnt64, oc ? oc + 1 : 0, (size_t)nc + 1))) return rc;
     if ((rc = grow_preserve(c, c->last_pos, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_aoi, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_leave, oc, nc))) return rc;
@@ -260,11 +269,13 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     HIPCHK(hipMemsetAsync(c->pos + oc, 0, n * sizeof(float4), c->st));
     HIPCHK(hipMemsetAsync(c->flags + oc, 0, n * 4, c->st));
     HIPCHK(hipMemsetAsync(c->gate + oc, 0, n * 2, c->st));
-    HIPCHK(hipMemsetAsync(c->lst_off + oc, 0, n * 4, c->st));
-    HIPCHK(hipMemsetAsync(c->lst_cnt + oc, 0, n * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->lst + oc, 0, n * sizeof(LstMeta), c->st));
+    HIPCHK(hipMemsetAsync(c->is_mover + oc, 0, n, c->st));
+    HIPCHK(hipMemsetAsync(c->cnt64 + oc, 0, (n + 1) * 8, c->st));
     launch_fill_i32(c->last_pos + oc, -1, n, c->st);
     launch_fill_i32(c->last_aoi + oc, -1, n, c->st);
     launch_fill_i32(c->last_leave + oc, -1, n, c->st);
+    HIPCHK(hipStreamSynchronize(c->st));
     c->slot_cap = nc;
     c->present_h.resize(nc, 0);
     c->space_of_h.resize(nc, -1);
@@ -297,31 +308,39 @@ int upload_spaces(gw_ctx* c) {
 }
 
 int read_stats(gw_ctx* c) {
-    HIPCHK(hipMemcpyAsync(c->hstats, c->stats, sizeof(DevStats), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(c->hstats, c->stats, offsetof(DevStats, shard), hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
 }
 
-// make room in the pool for `extra` more entries past the current top
-int pool_reserve(gw_ctx* c, uint64_t extra) {
-    if (c->h_pool_top + extra <= c->pool_cap) return 0;
-    uint64_t live = c->h_total_entries;
-    uint64_t need = live + extra;
-    uint64_t ncap = std::max<uint64_t>(c->pool_cap, 2 * need + (1u << 20));
+// Guarantee `reserve` free entries past the pool top; when the pool cannot
+// hold them, compact every slot's current list (capacities kept) into a new
+// pool sized for the live capacities plus twice the reserve.
+int pool_reserve(gw_ctx* c, uint64_t reserve) {
+    if (c->pool && c->h_pool_top + reserve <= c->pool_cap) return 0;
+    int rc;
+    uint64_t live = 0;
+    if (c->pool && c->total_slots) {
+        // (sized by total_slots: gw_tick already holds buffers at least this big)
+        if ((rc = ensure(c, c->pflag, (size_t)c->total_slots * 4))) return rc;
+        if ((rc = ensure(c, c->pre, (size_t)c->total_slots * 8))) return rc;
+        if ((rc = ensure_scan64(c, (uint64_t)c->total_slots + 1))) return rc;
+        launch_cap2(c->lst, c->total_slots, P<uint32_t>(c->pflag), c->st);
+        scan_u32_u64(P<uint32_t>(c->pflag), P<uint64_t>(c->pre), c->total_slots, nullptr, P<uint64_t>(c->scan_tmp64),
+                     (uint64_t*)&c->stats->scratch, c->st);
+        HIPCHK(hipMemcpyAsync(&live, &c->stats->scratch, 8, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+    }
+    uint64_t ncap = 2 * (live + reserve) + (1u << 20);
+    if (ncap >= (1ull << 32)) ncap = (1ull << 32) - 1;
+    if (live + reserve > ncap) return set_err(c, GW_ENOMEM, "neighbour pool exceeds 2^32 entries");
     uint32_t* np = nullptr;
     if (hipMalloc(&np, ncap * 4) != hipSuccess) {
         (void)hipGetLastError();
         return set_err(c, GW_ENOMEM, "pool hipMalloc(%llu entries) failed", (unsigned long long)ncap);
     }
     if (c->pool && c->total_slots) {
-        // compaction: new offsets = exclusive scan of list sizes
-        int rc;
-        if ((rc = ensure(c, c->pre64, (size_t)c->slot_cap * 8))) return rc;
-        if ((rc = ensure_scan64(c, c->slot_cap))) return rc;
-        scan_u32_u64(c->lst_cnt, P<uint64_t>(c->pre64), c->total_slots, nullptr, P<uint64_t>(c->scan_tmp64),
-                     (uint64_t*)&c->stats->scan_total, c->st);
-        launch_pool_compact(c->lst_off, c->lst_cnt, P<uint64_t>(c->pre64), c->total_slots, c->pool, np,
-                            c->lst_off, c->st);
+        launch_pool_compact(c->lst, P<uint64_t>(c->pre), c->total_slots, c->pool, np, c->lst, c->st);
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(c->st));
     }
@@ -329,11 +348,12 @@ int pool_reserve(gw_ctx* c, uint64_t extra) {
     c->pool = np;
     c->pool_cap = ncap;
     c->h_pool_top = live;
+    c->h_live_caps = live;
     return 0;
 }
 
 int validate_ops(gw_ctx* c, const gw_op* ops, uint32_t n) {
-    // all-or-nothing: replay against a copy of the touched presence bits
+    // all-or-nothing: replay against the host presence mirror, undo on error
     std::vector<std::pair<uint32_t, uint8_t>> undo;
     int rc = 0;
     for (uint32_t i = 0; i < n && !rc; ++i) {
@@ -370,6 +390,11 @@ int validate_ops(gw_ctx* c, const gw_op* ops, uint32_t n) {
     return rc;
 }
 
+void reset_stats_host(gw_ctx* c) {
+    memset(c->hstats, 0, sizeof(DevStats));
+    c->hstats->pool_top = c->h_pool_top;
+}
+
 }  // namespace
 
 // =========================================================================
@@ -397,7 +422,7 @@ int gw_init(int device_id, gw_ctx** out) {
         (void)hipEventCreate(&c->ev_t1);
     } while (0);
     if (rc) {
-        fprintf(stderr, "gw_init: %s\n", c->err.c_str());
+        (void)hipGetLastError();
         gw_shutdown(c);
         return rc;
     }
@@ -409,15 +434,17 @@ void gw_shutdown(gw_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    DevBuf* bufs[] = {&c->ops_buf, &c->is_last, &c->pre64, &c->movers, &c->keys0, &c->vals0, &c->keys1,
-                      &c->vals1, &c->cell_cnt, &c->cell_start, &c->se, &c->ev0, &c->ev1, &c->packed,
-                      &c->enter_d, &c->leave_d, &c->seg_start, &c->scan_tmp64, &c->scan_tmp32, &c->rs_hist,
-                      &c->rs_scan_tmp, &c->flag_mark, &c->flag_pre, &c->flagged, &c->rec_cnt, &c->rec_off,
-                      &c->rec0, &c->rec1, &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1};
+    DevBuf* bufs[] = {&c->ops_buf, &c->keys, &c->cell_cnt, &c->cell_start, &c->cursor, &c->se, &c->pflag, &c->pre,
+                      &c->fpre, &c->movers, &c->bpk, &c->tpk, &c->reg_pk, &c->tier_pre, &c->list_s, &c->list_b,
+                      &c->list_c, &c->c_temp_off, &c->c_temp, &c->own, &c->mir, &c->mir_cnt, &c->off64,
+                      &c->enter_d, &c->leave_d, &c->affected, &c->bigseg, &c->bigseg_off, &c->bigseg_temp,
+                      &c->scan_tmp64, &c->scan_tmp32, &c->rs_hist, &c->rs_scan_tmp, &c->flag_mark, &c->flag_pre,
+                      &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1, &c->gate_hist, &c->gk0, &c->gv0,
+                      &c->gk1, &c->gv1};
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
-    void* ps[] = {c->aoi, c->pos, c->flags, c->gate, c->lst_off, c->lst_cnt, c->last_pos, c->last_aoi,
+    void* ps[] = {c->aoi, c->pos, c->flags, c->gate, c->lst, c->is_mover, c->cnt64, c->last_pos, c->last_aoi,
                   c->last_leave, c->sp_dev, c->pool, c->stats, c->scal32};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
@@ -502,7 +529,7 @@ int gw_submit(gw_ctx* c, const gw_op* ops, uint32_t n) {
 int gw_submit_device(gw_ctx* c, const gw_op* dev_ops, uint32_t n) {
     if (!c || (!dev_ops && n)) return GW_EINVAL;
     if (!n) return 0;
-    c->validate = false;   // device-resident ops are trusted; host mirror no longer exact
+    c->validate = false;   // device-resident ops are trusted; the host mirror is no longer exact
     c->segs.push_back(OpSeg{false, dev_ops, n, 0});
     return 0;
 }
@@ -541,10 +568,9 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     if (M == 0 || C == 0) {
         c->segs.clear();
         c->pend_host.clear();
-        out->enter_dev = out->leave_dev = nullptr;
         return 0;
     }
-    // ---- gather the tick's op stream (submission order) -----------------
+    // ---- the tick's op stream, in submission order -----------------------
     const gw_op* ops = nullptr;
     if (c->segs.size() == 1 && !c->segs[0].host) {
         ops = c->segs[0].dev;
@@ -562,148 +588,132 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         }
         ops = P<gw_op>(c->ops_buf);
     }
-    // ---- per-tick stats ---------------------------------------------------
-    memset(c->hstats, 0, sizeof(DevStats));
-    c->hstats->total_entries = c->h_total_entries;
-    c->hstats->pool_top = c->h_pool_top;
+    const uint32_t NC = c->total_cells;
+    const uint64_t CM = std::max<uint64_t>(C, M);
+    // ---- buffers whose size is known before the tick ----------------------
+    if ((rc = ensure(c, c->keys, (size_t)C * 4)) || (rc = ensure(c, c->cell_cnt, ((size_t)NC + 1) * 4)) ||
+        (rc = ensure(c, c->cell_start, ((size_t)NC + 2) * 4)) || (rc = ensure(c, c->cursor, ((size_t)NC + 1) * 4)) ||
+        (rc = ensure(c, c->se, (size_t)C * sizeof(SortEnt))) || (rc = ensure(c, c->pflag, CM * 4)) ||
+        (rc = ensure(c, c->pre, CM * 8)) || (rc = ensure(c, c->fpre, (size_t)C * 8)) ||
+        (rc = ensure(c, c->movers, (size_t)M * 4)) || (rc = ensure(c, c->bpk, (size_t)M * 8)) ||
+        (rc = ensure(c, c->tpk, (size_t)M * 8)) || (rc = ensure(c, c->reg_pk, (size_t)M * 8)) ||
+        (rc = ensure(c, c->tier_pre, (size_t)M * 8)) || (rc = ensure(c, c->list_s, (size_t)M * 4)) ||
+        (rc = ensure(c, c->list_b, (size_t)M * 4)) || (rc = ensure(c, c->list_c, (size_t)M * 4)) ||
+        (rc = ensure(c, c->c_temp_off, (size_t)M * 8)) || (rc = ensure(c, c->mir_cnt, (size_t)M * 4)) ||
+        (rc = ensure(c, c->off64, ((size_t)C + 2) * 8)) || (rc = ensure(c, c->affected, (size_t)C * 4)) ||
+        (rc = ensure(c, c->bigseg, (size_t)C * 4)) || (rc = ensure(c, c->bigseg_off, (size_t)C * 8)) ||
+        (rc = ensure_scan64(c, CM + 1)) || (rc = ensure_scan32(c, (uint64_t)NC + 1)))
+        return rc;
+    if (!c->pool && (rc = pool_reserve(c, 1u << 20))) return rc;
+    reset_stats_host(c);
     HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
     DevStats* st = c->stats;
 
-    // ---- ops -> per-slot state, movers -------------------------------------
-    if ((rc = ensure(c, c->is_last, (size_t)M * 4))) return rc;
-    if ((rc = ensure(c, c->pre64, (size_t)std::max<uint64_t>(M, C) * 8))) return rc;
-    if ((rc = ensure(c, c->movers, (size_t)M * 4))) return rc;
-    if ((rc = ensure_scan64(c, std::max<uint64_t>(M, C)))) return rc;
+    TickBufs b{};
+    b.ops = ops; b.m = M; b.cap = C; b.ncells = NC;
+    b.last_pos = c->last_pos; b.last_aoi = c->last_aoi; b.last_leave = c->last_leave;
+    b.flags = c->flags; b.pos = c->pos; b.aoi = c->aoi; b.is_mover = c->is_mover; b.lst = c->lst; b.sp = c->sp_dev;
+    b.pool = c->pool; b.pool_cap = c->pool_cap; b.st = st;
+    b.keys = P<uint32_t>(c->keys); b.cell_cnt = P<uint32_t>(c->cell_cnt); b.cell_start = P<uint32_t>(c->cell_start);
+    b.cursor = P<uint32_t>(c->cursor); b.se = P<SortEnt>(c->se); b.pflag = P<uint32_t>(c->pflag);
+    b.pre = P<uint64_t>(c->pre); b.fpre = P<uint64_t>(c->fpre);
+    b.movers = P<uint32_t>(c->movers); b.bpk = P<uint64_t>(c->bpk); b.tpk = P<uint64_t>(c->tpk);
+    b.reg_pk = P<uint64_t>(c->reg_pk); b.tier_pre = P<uint64_t>(c->tier_pre); b.list_s = P<uint32_t>(c->list_s);
+    b.list_b = P<uint32_t>(c->list_b); b.list_c = P<uint32_t>(c->list_c); b.c_temp_off = P<uint64_t>(c->c_temp_off);
+    b.mir_cnt = P<uint32_t>(c->mir_cnt); b.cnt64 = c->cnt64; b.off64 = P<uint64_t>(c->off64);
+    b.affected = P<uint32_t>(c->affected); b.bigseg = P<uint32_t>(c->bigseg); b.bigseg_off = P<uint64_t>(c->bigseg_off);
+    b.write_events = (flags & GW_TICK_NO_EVENTS) ? 0 : 1;
+
+    uint64_t* stmp = P<uint64_t>(c->scan_tmp64);
     prof_begin(c, "ops");
-    launch_ops(ops, M, C, c->last_pos, c->last_aoi, c->last_leave, c->flags, c->pos, c->aoi, P<uint32_t>(c->is_last),
-               st, c->st);
-    scan_u32_u64(P<uint32_t>(c->is_last), P<uint64_t>(c->pre64), M, nullptr, P<uint64_t>(c->scan_tmp64),
-                 (uint64_t*)&st->movers, c->st);
-    launch_compact_movers(ops, M, P<uint32_t>(c->is_last), P<uint64_t>(c->pre64), P<uint32_t>(c->movers), c->st);
-    prof_end(c, (uint64_t)M * 24 + (uint64_t)M * 4 * 4);
-
-    // ---- grid rebuild ----------------------------------------------------------
-    const uint32_t NC = c->total_cells;
-    if ((rc = ensure(c, c->keys0, (size_t)C * 4))) return rc;
-    if ((rc = ensure(c, c->vals0, (size_t)C * 4))) return rc;
-    if ((rc = ensure(c, c->keys1, (size_t)C * 4))) return rc;
-    if ((rc = ensure(c, c->vals1, (size_t)C * 4))) return rc;
-    if ((rc = ensure(c, c->cell_cnt, ((size_t)NC + 1) * 4))) return rc;
-    if ((rc = ensure(c, c->cell_start, ((size_t)NC + 2) * 4))) return rc;
-    if ((rc = ensure(c, c->se, (size_t)C * sizeof(SortEnt)))) return rc;
-    if ((rc = ensure_scan32(c, (uint64_t)NC + 1))) return rc;
-    RadixTmp rt;
-    uint64_t ev_bound_prev = std::max<uint64_t>(C, 1);
-    if ((rc = radix_tmp(c, ev_bound_prev, rt))) return rc;
+    tick_ops(b, c->st);
+    prof_end(c, (uint64_t)M * 24);
     prof_begin(c, "grid");
-    HIPCHK(hipMemsetAsync(c->cell_cnt.p, 0, ((size_t)NC + 1) * 4, c->st));
-    launch_cell_keys(c->aoi, c->sp_dev, C, NC, P<uint32_t>(c->keys0), P<uint32_t>(c->vals0), P<uint32_t>(c->cell_cnt),
-                     c->st);
-    scan_u32_u32(P<uint32_t>(c->cell_cnt), P<uint32_t>(c->cell_start), (uint64_t)NC + 1, nullptr,
-                 P<uint32_t>(c->scan_tmp32), nullptr, c->st);
-    int cell_bits = ceil_log2((uint64_t)NC + 1);
-    int where = sort_u32_u32(P<uint32_t>(c->keys0), P<uint32_t>(c->vals0), P<uint32_t>(c->keys1),
-                             P<uint32_t>(c->vals1), C, nullptr, 0, cell_bits, rt, c->st);
-    uint32_t* sorted_vals = where ? P<uint32_t>(c->vals1) : P<uint32_t>(c->vals0);
-    launch_gather_sorted(sorted_vals, c->aoi, P<uint32_t>(c->cell_start) + NC, C, P<SortEnt>(c->se), st, c->st);
-    prof_end(c, (uint64_t)C * (16 + 8 + 8 * ((cell_bits + 7) / 8) * 3 + 16));
-
-    // ---- event bound: the one mid-tick host sync -----------------------
-    prof_begin(c, "bounds");
-    launch_bounds(P<uint32_t>(c->movers), (const uint64_t*)&st->movers, M, c->aoi, c->sp_dev,
-                  P<uint32_t>(c->cell_start), c->lst_cnt, st, c->st);
-    prof_end(c, (uint64_t)M * 40);
+    tick_grid(b, stmp, P<uint32_t>(c->scan_tmp32), c->st);
+    size_t s_grid = prof_end(c, 0);
+    prof_begin(c, "movers");
+    tick_movers(b, stmp, c->st);
+    tick_bounds(b, stmp, c->st);
+    size_t s_movers = prof_end(c, 0);
     HIPCHK(hipGetLastError());
+    // ---- the one mid-tick host sync ---------------------------------------
     if ((rc = read_stats(c))) return rc;
-    if (c->hstats->bad_ops) return set_err(c, GW_EINVAL, "%llu ops with bad slot/kind", c->hstats->bad_ops);
-    const uint64_t nmov = c->hstats->movers;
-    const uint64_t bound = c->hstats->bound_total;
-    const uint64_t a_old = c->hstats->a_old;
-    if (bound >= (1ull << 32)) return set_err(c, GW_ERANGE, "event bound %llu too large for one tick", (unsigned long long)bound);
-    const int sb = ceil_log2((uint64_t)C);
-    if (2 * sb + 1 > 63) return set_err(c, GW_ERANGE, "slot bits");
-    const uint64_t EB = std::max<uint64_t>(bound, 1);
-    if ((rc = ensure(c, c->ev0, EB * 8))) return rc;
-    if ((rc = ensure(c, c->ev1, EB * 8))) return rc;
-    if ((rc = ensure(c, c->packed, EB * 8))) return rc;
-    if ((rc = ensure(c, c->enter_d, EB * sizeof(gw_event)))) return rc;
-    if ((rc = ensure(c, c->leave_d, EB * sizeof(gw_event)))) return rc;
-    if ((rc = ensure(c, c->seg_start, (EB + 2) * 4))) return rc;
-    if ((rc = ensure_scan64(c, std::max<uint64_t>(EB, std::max<uint64_t>(M, C))))) return rc;
-    if ((rc = radix_tmp(c, std::max<uint64_t>(EB, C), rt))) return rc;
-    if ((rc = pool_reserve(c, c->h_total_entries + bound))) return rc;
-    if (c->hstats->pool_top != c->h_pool_top) {   // compaction moved the top
+    DevStats hs0 = *c->hstats;
+    if (hs0.bad_ops) return set_err(c, GW_EINVAL, "%llu ops with bad slot/kind", hs0.bad_ops);
+    const uint64_t n_mov = hs0.movers_present + hs0.leavers;
+    const uint64_t sum_cand = hs0.bound_pk & 0xffffffffull, sum_old = hs0.bound_pk >> 32;
+    const uint64_t n_s = hs0.tier_pk & 0xffffffffull, n_b = hs0.tier_pk >> 32, n_c = hs0.n_tier_c;
+    const uint64_t region = std::max<uint64_t>(sum_cand + sum_old, 1);
+    if (sum_cand >= (1ull << 32) - 1 || sum_old >= (1ull << 32) - 1)
+        return set_err(c, GW_ERANGE, "tick too large: %llu candidates", (unsigned long long)sum_cand);
+    if ((rc = ensure(c, c->own, region * 4)) || (rc = ensure(c, c->mir, region * 8)) ||
+        (rc = ensure(c, c->enter_d, std::max<uint64_t>(2 * sum_cand, 1) * sizeof(gw_event))) ||
+        (rc = ensure(c, c->leave_d, std::max<uint64_t>(2 * sum_old, 1) * sizeof(gw_event))) ||
+        (rc = ensure(c, c->c_temp, std::max<uint64_t>(hs0.tier_c_temp, 4) * 4)) ||
+        (rc = ensure(c, c->bigseg_temp, std::max<uint64_t>(4 * (sum_cand + sum_old) + 64, 64) * 4)))
+        return rc;
+    // reallocations can only come from lists that outgrow their capacity:
+    // movers (<= cand entries each) and op-less watchers (<= old + enters)
+    const uint64_t reserve = 5 * (3 * sum_cand + c->h_total_entries) + 32 * ((uint64_t)C + n_mov) + (1u << 16);
+    uint64_t top_before = c->h_pool_top;
+    if ((rc = pool_reserve(c, reserve))) return rc;
+    if (c->h_pool_top != top_before) {   // compaction moved the lists
         c->hstats->pool_top = c->h_pool_top;
         HIPCHK(hipMemcpyAsync(&st->pool_top, &c->hstats->pool_top, 8, hipMemcpyHostToDevice, c->st));
     }
+    b.pool = c->pool; b.pool_cap = c->pool_cap;
+    b.own = P<uint32_t>(c->own); b.mir = P<uint64_t>(c->mir);
+    b.enter = P<gw_event>(c->enter_d); b.leave = P<gw_event>(c->leave_d);
+    b.enter_cap = std::max<uint64_t>(2 * sum_cand, 1); b.leave_cap = std::max<uint64_t>(2 * sum_old, 1);
+    b.c_temp = P<uint32_t>(c->c_temp); b.c_temp_cap = std::max<uint64_t>(hs0.tier_c_temp, 4);
+    b.bigseg_temp = P<uint32_t>(c->bigseg_temp); b.bigseg_temp_cap = c->bigseg_temp.cap / 4;
 
     // ---- diff ------------------------------------------------------------------
     prof_begin(c, "diff");
-    if (nmov)
-        launch_diff(P<uint32_t>(c->movers), (const uint64_t*)&st->movers, (uint32_t)nmov, c->aoi, c->sp_dev,
-                    P<uint32_t>(c->cell_start), P<SortEnt>(c->se), c->lst_off, c->lst_cnt, c->pool,
-                    P<uint64_t>(c->ev0), EB, sb, st, c->st);
-    prof_end(c, 0);   // bytes filled after the final read-back
-    size_t diff_stage = c->nstage ? c->nstage - 1 : 0;
-
-    // ---- canonical events ------------------------------------------------
-    const uint64_t* n_ev = (const uint64_t*)&st->ev_count;
-    prof_begin(c, "ev_sort");
-    int ew = sort_u64(P<uint64_t>(c->ev0), P<uint64_t>(c->ev1), EB, n_ev, 1, 1 + 2 * sb, rt, c->st);
-    prof_end(c, 0);
-    size_t sort_stage = c->nstage ? c->nstage - 1 : 0;
-    uint64_t* evs = ew ? P<uint64_t>(c->ev1) : P<uint64_t>(c->ev0);
-    prof_begin(c, "ev_split");
-    launch_ev_flags(evs, n_ev, EB, sb, P<uint64_t>(c->packed), c->st);
-    scan_u64_u64(P<uint64_t>(c->packed), P<uint64_t>(c->packed), EB, n_ev, P<uint64_t>(c->scan_tmp64),
-                 (uint64_t*)&st->ev_scan_total, c->st);
-    launch_ev_split(evs, n_ev, EB, sb, P<uint64_t>(c->packed), P<gw_event>(c->enter_d), P<gw_event>(c->leave_d),
-                    P<uint32_t>(c->seg_start), (flags & GW_TICK_NO_EVENTS) ? 0 : 1, c->st);
-    prof_end(c, 0);
-    size_t split_stage = c->nstage ? c->nstage - 1 : 0;
-
-    // ---- neighbour lists ------------------------------------------------------
-    prof_begin(c, "lists");
-    launch_list_update(evs, P<uint64_t>(c->packed), P<uint32_t>(c->seg_start), &st->ev_scan_total, EB, sb, c->aoi,
-                       c->lst_off, c->lst_cnt, c->pool, c->pool, c->pool_cap, st, c->st);
-    launch_tick_reset(ops, M, C, c->last_pos, c->last_aoi, c->last_leave, c->aoi, c->st);
-    prof_end(c, 0);
-    size_t list_stage = c->nstage ? c->nstage - 1 : 0;
+    tick_diff(b, n_s, n_b, n_c, c->st);
+    size_t s_diff = prof_end(c, 0);
+    prof_begin(c, "events");
+    tick_events(b, n_mov, stmp, c->st);
+    const uint64_t aff_max = std::min<uint64_t>(C, sum_cand + sum_old);
+    tick_nonmovers(b, aff_max, aff_max, n_mov, c->st);
+    size_t s_events = prof_end(c, 0);
+    prof_begin(c, "reset");
+    tick_reset(b, n_mov, c->st);
+    stats_reduce(st, c->st);
+    prof_end(c, (uint64_t)M * 40);
     HIPCHK(hipEventRecord(c->ev_t1, c->st));
     HIPCHK(hipGetLastError());
     if ((rc = read_stats(c))) return rc;
     DevStats& hs = *c->hstats;
     c->segs.clear();
     c->pend_host.clear();
-    if (hs.ev_overflow) return set_err(c, GW_EDEVICE, "internal: event scratch overflow");
-    if (hs.pool_overflow) return set_err(c, GW_EDEVICE, "internal: pool overflow");
-    c->h_total_entries = hs.total_entries;
+    if (hs.pool_overflow) return set_err(c, GW_EDEVICE, "internal: neighbour pool overflow");
+    if (hs.tmp_overflow) return set_err(c, GW_EDEVICE, "internal: segment scratch overflow");
+    const uint64_t n_enter = hs.ev_pk & 0xffffffffull, n_leave = hs.ev_pk >> 32;
     c->h_pool_top = hs.pool_top;
-    const uint64_t n_enter = (uint32_t)hs.ev_scan_total;
-    const uint64_t n_evt = hs.ev_count;
-    const uint64_t n_leave = n_evt - n_enter;
-    const uint64_t nseg = hs.ev_scan_total >> 32;
+    c->h_total_entries = c->h_total_entries + n_enter - n_leave;   // every list changes by its enters - leaves
     float ms = 0;
     (void)hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1);
     out->device_us = ms * 1000.0;
     out->ops = M;
-    out->movers = nmov;
+    out->movers = n_mov;
     out->pairs_tested = hs.pairs_tested;
-    out->nbr_old = a_old;
+    out->nbr_old = hs.a_old;
     out->nbr_new = hs.a_new;
     out->enter_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->enter_d);
     out->leave_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->leave_d);
     out->n_enter = n_enter;
     out->n_leave = n_leave;
-    // SURVEY 8(d) algorithmic bytes of the AOI part (sync records are counted by gw_sync_collect)
-    out->bytes_alg = 20ull * nmov + 8ull * hs.n_present + 4ull * (a_old + hs.a_new) + 8ull * n_evt;
-    // per-stage algorithmic bytes
+    // SURVEY 8(d) algorithmic bytes of the AOI part (records are counted by gw_sync_collect)
+    const uint64_t n_evt = n_enter + n_leave;
+    out->bytes_alg = 20ull * n_mov + 8ull * hs.n_present + 4ull * (hs.a_old + hs.a_new) + 8ull * n_evt;
     if (c->prof) {
-        c->stages[diff_stage].bytes = 16ull * hs.pairs_tested + 4ull * a_old * 2 + 16ull * a_old + 8ull * n_evt + 4ull * nmov;
-        int passes = (2 * sb + 7) / 8;
-        c->stages[sort_stage].bytes = (uint64_t)passes * n_evt * 8 * 3;
-        c->stages[split_stage].bytes = n_evt * (8 + 8 + 8 + 8 + 8 + 4);
-        c->stages[list_stage].bytes = 4ull * (a_old + hs.a_new) + n_evt * 8 + nseg * 16;
+        prof_set_bytes(c, s_grid, 16ull * C + 16ull * hs.n_present + 8ull * NC);
+        prof_set_bytes(c, s_movers, 8ull * hs.n_present + 40ull * n_mov);
+        // diff: candidates (16 B) + old lists read twice (4 B) + neighbour state gathered (16 B per old
+        // entry) + new lists (4 B) + own and mirror events (12 B per directed event)
+        prof_set_bytes(c, s_diff, 16ull * hs.pairs_tested + 24ull * hs.a_old + 4ull * hs.a_new + 12ull * n_evt);
+        prof_set_bytes(c, s_events, 16ull * (C + 1) + 24ull * n_evt);
         prof_collect(c);
     }
     if ((flags & GW_TICK_COPY_TO_HOST) && !(flags & GW_TICK_NO_EVENTS)) {
@@ -726,25 +736,23 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     const uint32_t C = c->total_slots;
     int rc;
     HIPCHK(hipEventRecord(c->ev_t0, c->st));
-    c->gate_off.assign((size_t)c->max_gate + 2, 0);
-    if (C == 0) {
+    const uint32_t G = (uint32_t)c->max_gate + 1;
+    c->gate_off.assign((size_t)G + 1, 0);
+    if (C == 0 || !c->pool) {
         out->gate_off = c->gate_off.data();
-        out->n_gates = (uint32_t)c->max_gate + 1;
+        out->n_gates = G;
         return 0;
     }
-    memset(c->hstats, 0, sizeof(DevStats));
-    c->hstats->total_entries = c->h_total_entries;
-    c->hstats->pool_top = c->h_pool_top;
-    HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
+    reset_stats_host(c);
+    HIPCHK(hipMemcpyAsync(c->stats, c->hstats, offsetof(DevStats, shard), hipMemcpyHostToDevice, c->st));
     DevStats* st = c->stats;
     const uint64_t rec_bound = (uint64_t)C + c->h_total_entries;
-    if ((rc = ensure(c, c->flag_mark, (size_t)C * 4))) return rc;
-    if ((rc = ensure(c, c->flag_pre, (size_t)C * 8))) return rc;
-    if ((rc = ensure(c, c->flagged, (size_t)C * 4))) return rc;
-    if ((rc = ensure(c, c->rec_cnt, (size_t)C * 4))) return rc;
-    if ((rc = ensure(c, c->rec_off, (size_t)C * 8))) return rc;
-    if ((rc = ensure(c, c->rec0, (size_t)std::max<uint64_t>(rec_bound, 1) * sizeof(gw_sync_record)))) return rc;
-    if ((rc = ensure_scan64(c, C))) return rc;
+    if ((rc = ensure(c, c->flag_mark, (size_t)C * 4)) || (rc = ensure(c, c->flag_pre, (size_t)C * 8)) ||
+        (rc = ensure(c, c->flagged, (size_t)C * 4)) || (rc = ensure(c, c->rec_cnt, (size_t)C * 4)) ||
+        (rc = ensure(c, c->rec_off, (size_t)C * 8)) ||
+        (rc = ensure(c, c->rec0, (size_t)std::max<uint64_t>(rec_bound, 1) * sizeof(gw_sync_record))) ||
+        (rc = ensure_scan64(c, C)))
+        return rc;
     prof_begin(c, "sync_flagged");
     launch_flag_mark(c->flags, C, P<uint32_t>(c->flag_mark), c->st);
     scan_u32_u64(P<uint32_t>(c->flag_mark), P<uint64_t>(c->flag_pre), C, nullptr, P<uint64_t>(c->scan_tmp64),
@@ -753,18 +761,16 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     prof_end(c, (uint64_t)C * 4 * 4);
     const uint64_t* nf = (const uint64_t*)&st->flagged;
     prof_begin(c, "sync_count");
-    launch_sync_count(P<uint32_t>(c->flagged), nf, C, c->flags, c->aoi, c->gate, c->lst_off, c->lst_cnt, c->pool,
+    launch_sync_count(P<uint32_t>(c->flagged), nf, C, c->flags, c->aoi, c->gate, c->lst, c->pool,
                       P<uint32_t>(c->rec_cnt), c->st);
     scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), C, nf, P<uint64_t>(c->scan_tmp64),
                  (uint64_t*)&st->rec_total, c->st);
-    prof_end(c, 0);
-    size_t count_stage = c->nstage ? c->nstage - 1 : 0;
+    size_t s_count = prof_end(c, 0);
     prof_begin(c, "sync_write");
-    launch_sync_write(P<uint32_t>(c->flagged), nf, C, c->flags, c->aoi, c->gate, c->lst_off, c->lst_cnt, c->pool,
-                      c->pos, P<uint64_t>(c->rec_off), P<gw_sync_record>(c->rec0),
-                      c->rec0.cap / sizeof(gw_sync_record), c->st);
-    prof_end(c, 0);
-    size_t write_stage = c->nstage ? c->nstage - 1 : 0;
+    launch_sync_write(P<uint32_t>(c->flagged), nf, C, c->flags, c->aoi, c->gate, c->lst, c->pool, c->pos,
+                      P<uint64_t>(c->rec_off), P<gw_sync_record>(c->rec0), c->rec0.cap / sizeof(gw_sync_record),
+                      c->st);
+    size_t s_write = prof_end(c, 0);
     HIPCHK(hipGetLastError());
     if ((rc = read_stats(c))) return rc;
     const uint64_t R = c->hstats->rec_total;
@@ -772,7 +778,6 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     if (R > rec_bound) return set_err(c, GW_EDEVICE, "internal: record bound exceeded");
     gw_sync_record* recs = P<gw_sync_record>(c->rec0);
     // ---- per-gate grouping (stable, keeps (entity, watcher) order) -------
-    const uint32_t G = (uint32_t)c->max_gate + 1;
     if (R && G > 2) {
         prof_begin(c, "sync_gates");
         if ((rc = ensure(c, c->gate_hist, (size_t)65536 * 4))) return rc;
@@ -802,7 +807,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         }
         prof_end(c, R * (24 * 2 + 8 * 4));
     } else {
-        // at most one gate id (1) in use: every record belongs to it
+        // at most one gate id in use: every record belongs to the last gate
         for (uint32_t g = 0; g <= G; ++g) c->gate_off[g] = (g == G) ? R : 0;
     }
     HIPCHK(hipEventRecord(c->ev_t1, c->st));
@@ -815,11 +820,10 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     out->rec_dev = recs;
     out->gate_off = c->gate_off.data();
     out->n_gates = G;
-    // algorithmic bytes: flags scan + list reads of flagged entities + records written
     out->bytes_alg = 24ull * R;
     if (c->prof) {
-        c->stages[count_stage].bytes = 4ull * R + NF * 8;
-        c->stages[write_stage].bytes = 4ull * R + 24ull * R + NF * 24;
+        prof_set_bytes(c, s_count, 4ull * R + NF * 24);
+        prof_set_bytes(c, s_write, 4ull * R + 24ull * R + NF * 24);
         prof_collect(c);
     }
     if (flags & GW_SYNC_COPY_TO_HOST) {
@@ -835,14 +839,13 @@ int gw_neighbors(gw_ctx* c, uint32_t slot, uint32_t* buf, uint32_t cap, uint32_t
     if (!c || !n) return GW_EINVAL;
     (void)hipSetDevice(c->dev);
     if (slot >= c->total_slots) return set_err(c, GW_ERANGE, "slot %u out of range", slot);
-    uint32_t off = 0, cnt = 0;
-    HIPCHK(hipMemcpyAsync(&off, c->lst_off + slot, 4, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipMemcpyAsync(&cnt, c->lst_cnt + slot, 4, hipMemcpyDeviceToHost, c->st));
+    LstMeta L{};
+    HIPCHK(hipMemcpyAsync(&L, c->lst + slot, sizeof L, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
-    *n = cnt;
-    uint32_t k = std::min(cnt, cap);
+    *n = L.cnt;
+    uint32_t k = std::min(L.cnt, cap);
     if (buf && k) {
-        HIPCHK(hipMemcpyAsync(buf, c->pool + off, (size_t)k * 4, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipMemcpyAsync(buf, c->pool + L.cur, (size_t)k * 4, hipMemcpyDeviceToHost, c->st));
         HIPCHK(hipStreamSynchronize(c->st));
     }
     return 0;

@@ -1,9 +1,9 @@
 // gw_internal.hpp — device data layout shared by kernels.hip and capi.cpp.
 //
 // Per context (one HIP device) the state of all spaces lives in one set of
-// slot-indexed SoA arrays in HBM ("shard"); a space owns a contiguous slot
-// range and a contiguous range of uniform-grid cells, so one launch ticks
-// every space of the device at once (BASELINE config #4: 10k spaces).
+// slot-indexed SoA arrays in HBM; a space owns a contiguous slot range and a
+// contiguous range of uniform-grid cells, so one launch ticks every space of
+// the device at once (BASELINE config #4: 10k spaces).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -28,9 +28,17 @@ struct alignas(16) SortEnt {
     int32_t seq;
 };
 
-// Per-space parameters (32 B).  Cells are squares of side cs = 1/inv_cs >= d
-// (DESIGN.md): a window spans at most 3x3 cells.  Any cell function that is
-// monotone in x and z keeps the search exact, whatever the float rounding.
+// Neighbour list of one slot (InterestedIn == InterestedBy), 16 B.  The list
+// lives in a pool region of 2*cap entries split in two halves: the current
+// list is at `cur`, the next tick's list is written to `alt` and the halves
+// swap, so no list is ever rewritten in place.  Lists are ascending slots.
+struct alignas(16) LstMeta {
+    uint32_t cur, alt, cnt, cap;
+};
+
+// Per-space parameters (32 B).  Cells are squares of side cs = 1/inv_cs >= d:
+// a window spans at most 3x3 cells.  The cell function is monotone in x and z,
+// which keeps the candidate search exact whatever the float rounding.
 struct alignas(16) SpaceP {
     float d;
     float x0, z0, inv_cs;
@@ -39,24 +47,31 @@ struct alignas(16) SpaceP {
     uint32_t alive;
 };
 
+constexpr int STAT_SHARDS = 256;
+constexpr int SH_PAIRS = 0, SH_AOLD = 1, SH_ANEW = 2, SH_REALLOC = 3;
+
 // Device-side counters of one tick / collect (read back once per call).
 struct DevStats {
-    unsigned long long bound_total;   // sum over movers of 2*(candidates + |old list|)
-    unsigned long long a_old;         // sum over movers of |old list|
-    unsigned long long a_new;         // sum over movers of |new list|
-    unsigned long long pairs_tested;
-    unsigned long long ev_count;      // events emitted into the scratch buffer
-    unsigned long long ev_overflow;
-    unsigned long long total_entries; // sum over slots of |list|
+    unsigned long long n_present;     // entities in the grid
+    unsigned long long movers_present;
+    unsigned long long leavers;
+    unsigned long long bound_pk;      // sum of (cand | old<<32) over movers
+    unsigned long long tier_pk;       // count of (tierS | tierB<<32)
+    unsigned long long n_tier_c;
+    unsigned long long tier_c_temp;   // u32 words of tier-C scratch
+    unsigned long long ev_pk;         // sum of (enters | leaves<<32) over watchers
+    unsigned long long n_affected;    // non-mover watchers with events
+    unsigned long long n_bigseg;      // watchers whose event segments need the block sort
+    unsigned long long bigseg_temp;   // u32 words of big-segment scratch
     unsigned long long pool_top;      // bump pointer of the neighbour pool (entries)
     unsigned long long pool_overflow;
-    unsigned long long movers;        // distinct AOI-op slots
-    unsigned long long n_present;     // entities in the grid
-    unsigned long long scan_total;    // generic scan total
-    unsigned long long ev_scan_total; // packed (segments<<32 | enters)
+    unsigned long long tmp_overflow;
+    unsigned long long bad_ops;
+    unsigned long long pairs_tested, a_old, a_new, reallocs;   // reduced from shards
     unsigned long long flagged;       // sync: flagged entities
     unsigned long long rec_total;     // sync: records
-    unsigned long long bad_ops;       // ops with slot out of range
+    unsigned long long scratch;       // generic scan total sink
+    unsigned long long shard[STAT_SHARDS][4];
 };
 
 // ---- primitives (instantiated in kernels.hip) ------------------------------
@@ -75,40 +90,75 @@ void scan_u64_u64(const uint64_t* in, uint64_t* out, uint64_t n_max, const uint6
                   uint64_t* total, hipStream_t s);
 int sort_u32_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
                  int lo_bit, int hi_bit, const RadixTmp& tmp, hipStream_t s);
-int sort_u64(uint64_t* k0, uint64_t* k1, uint64_t n_max, const uint64_t* n_dev, int lo_bit, int hi_bit,
-             const RadixTmp& tmp, hipStream_t s);
 
-// ---- kernel launchers (kernels.hip) ---------------------------------------
-void launch_ops(const gw_op* ops, uint32_t m, uint32_t cap, int32_t* last_pos, int32_t* last_aoi,
-                int32_t* last_leave, uint32_t* flags, float4* pos, AoiEnt* aoi, uint32_t* is_last,
-                DevStats* st, hipStream_t s);
-void launch_compact_movers(const gw_op* ops, uint32_t m, const uint32_t* is_last, const uint64_t* pre,
-                           uint32_t* movers, hipStream_t s);
-void launch_cell_keys(const AoiEnt* aoi, const SpaceP* sp, uint32_t cap, uint32_t ncells,
-                      uint32_t* keys, uint32_t* vals, uint32_t* cell_cnt, hipStream_t s);
-void launch_gather_sorted(const uint32_t* vals, const AoiEnt* aoi, const uint32_t* n_present_dev,
-                          uint32_t cap, SortEnt* se, DevStats* st, hipStream_t s);
-void launch_bounds(const uint32_t* movers, const uint64_t* n_movers_dev, uint32_t m_max,
-                   const AoiEnt* aoi, const SpaceP* sp, const uint32_t* cell_start,
-                   const uint32_t* lst_cnt, DevStats* st, hipStream_t s);
-void launch_diff(const uint32_t* movers, const uint64_t* n_movers_dev, uint32_t m_max,
-                 const AoiEnt* aoi, const SpaceP* sp, const uint32_t* cell_start, const SortEnt* se,
-                 const uint32_t* lst_off, const uint32_t* lst_cnt, const uint32_t* pool,
-                 uint64_t* ev, uint64_t ev_cap, int sb, DevStats* st, hipStream_t s);
-void launch_ev_flags(const uint64_t* ev, const uint64_t* n_ev_dev, uint64_t n_max, int sb,
-                     uint64_t* packed, hipStream_t s);
-void launch_ev_split(const uint64_t* ev, const uint64_t* n_ev_dev, uint64_t n_max, int sb,
-                     const uint64_t* packed_excl, gw_event* enter, gw_event* leave, uint32_t* seg_start,
-                     int write_events, hipStream_t s);
-void launch_list_update(const uint64_t* ev, const uint64_t* packed_excl, const uint32_t* seg_start,
-                        const unsigned long long* ev_scan_total, uint64_t seg_max, int sb,
-                        const AoiEnt* aoi, uint32_t* lst_off, uint32_t* lst_cnt, const uint32_t* pool_old,
-                        uint32_t* pool_new, uint64_t pool_cap, DevStats* st, hipStream_t s);
-void launch_tick_reset(const gw_op* ops, uint32_t m, uint32_t cap, int32_t* last_pos, int32_t* last_aoi,
-                       int32_t* last_leave, AoiEnt* aoi, hipStream_t s);
-void launch_pool_compact(const uint32_t* lst_off, const uint32_t* lst_cnt, const uint64_t* new_off,
-                         uint32_t cap, const uint32_t* pool_old, uint32_t* pool_new, uint32_t* lst_off_out,
-                         hipStream_t s);
+// ---- tick buffers handed to the launchers ----------------------------------
+struct TickBufs {
+    const gw_op* ops;
+    uint32_t m;               // ops in the stream
+    uint32_t cap;             // total slots
+    uint32_t ncells;
+    int32_t *last_pos, *last_aoi, *last_leave;
+    uint32_t* flags;
+    float4* pos;
+    AoiEnt* aoi;
+    uint8_t* is_mover;
+    LstMeta* lst;
+    const SpaceP* sp;
+    uint32_t* pool;
+    uint64_t pool_cap;
+    DevStats* st;
+    // grid
+    uint32_t* keys;           // [cap]
+    uint32_t* cell_cnt;       // [ncells+1]
+    uint32_t* cell_start;     // [ncells+1]
+    uint32_t* cursor;         // [ncells]
+    SortEnt* se;              // [cap]
+    uint32_t* pflag;          // [max(cap, m)]
+    uint64_t* pre;            // [max(cap, m)]
+    uint64_t* fpre;           // [cap] prefix of affected-watcher flags
+    // movers
+    uint32_t* movers;         // [m] slots, cell order then leavers
+    uint64_t* bpk;            // [m] cand | old<<32
+    uint64_t* tpk;            // [m] tierS | tierB<<32
+    uint64_t* reg_pk;         // [m] exclusive scan of bpk
+    uint64_t* tier_pre;       // [m] exclusive scan of tpk
+    uint32_t* list_s;         // [m] mover indices of tier S
+    uint32_t* list_b;         // [m] tier B
+    uint32_t* list_c;         // [m] tier C
+    uint64_t* c_temp_off;     // [m] tier C scratch offset (u32 words)
+    uint32_t* c_temp;         // tier C scratch
+    uint64_t c_temp_cap;
+    uint32_t* own;            // own events (targets): [sum cand+old]
+    uint64_t* mir;            // mirror events: [sum cand+old]
+    uint32_t* mir_cnt;        // [m]
+    // canonical events
+    unsigned long long* cnt64;  // [cap] enters | leaves<<32 per watcher (zero between ticks)
+    uint64_t* off64;          // [cap+1]
+    gw_event* enter;
+    gw_event* leave;
+    uint64_t enter_cap, leave_cap;
+    uint32_t* affected;       // [cap]
+    uint32_t* bigseg;         // [cap]
+    uint64_t* bigseg_off;     // [cap]
+    uint32_t* bigseg_temp;
+    uint64_t bigseg_temp_cap;
+    int write_events;
+};
+
+// ---- launchers (kernels.hip) ------------------------------------------------
+void tick_ops(const TickBufs& b, hipStream_t s);
+void tick_grid(const TickBufs& b, uint64_t* scan_tmp64, uint32_t* scan_tmp32, hipStream_t s);
+void tick_movers(const TickBufs& b, uint64_t* scan_tmp64, hipStream_t s);
+void tick_bounds(const TickBufs& b, uint64_t* scan_tmp64, hipStream_t s);
+void tick_diff(const TickBufs& b, uint64_t n_s, uint64_t n_b, uint64_t n_c, hipStream_t s);
+void tick_events(const TickBufs& b, uint64_t n_movers, uint64_t* scan_tmp64, hipStream_t s);
+void tick_nonmovers(const TickBufs& b, uint64_t n_affected, uint64_t n_big, uint64_t n_movers, hipStream_t s);
+void tick_reset(const TickBufs& b, uint64_t n_movers, hipStream_t s);
+void stats_reduce(DevStats* st, hipStream_t s);
+
+void launch_pool_compact(const LstMeta* lst_in, const uint64_t* new_off, uint32_t cap, const uint32_t* pool_old,
+                         uint32_t* pool_new, LstMeta* lst_out, hipStream_t s);
+void launch_cap2(const LstMeta* lst, uint32_t cap, uint32_t* out, hipStream_t s);
 void launch_set_clients(const uint32_t* slots, const uint16_t* gates, uint32_t n, uint32_t cap,
                         uint16_t* gate, hipStream_t s);
 // sync collect
@@ -116,12 +166,12 @@ void launch_flag_mark(const uint32_t* flags, uint32_t cap, uint32_t* mark, hipSt
 void launch_flag_compact(const uint32_t* mark, const uint64_t* pre, uint32_t cap, uint32_t* flagged,
                          hipStream_t s);
 void launch_sync_count(const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max, const uint32_t* flags,
-                       const AoiEnt* aoi, const uint16_t* gate, const uint32_t* lst_off,
-                       const uint32_t* lst_cnt, const uint32_t* pool, uint32_t* cnt, hipStream_t s);
+                       const AoiEnt* aoi, const uint16_t* gate, const LstMeta* lst, const uint32_t* pool,
+                       uint32_t* cnt, hipStream_t s);
 void launch_sync_write(const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max, uint32_t* flags,
-                       const AoiEnt* aoi, const uint16_t* gate, const uint32_t* lst_off,
-                       const uint32_t* lst_cnt, const uint32_t* pool, const float4* pos,
-                       const uint64_t* rec_off, gw_sync_record* rec, uint64_t rec_cap, hipStream_t s);
+                       const AoiEnt* aoi, const uint16_t* gate, const LstMeta* lst, const uint32_t* pool,
+                       const float4* pos, const uint64_t* rec_off, gw_sync_record* rec, uint64_t rec_cap,
+                       hipStream_t s);
 void launch_gate_hist(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,
                       uint32_t* hist /*65536*/, hipStream_t s);
 void launch_gate_keys(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,

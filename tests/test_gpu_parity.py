@@ -179,9 +179,10 @@ def test_many_spaces_one_launch(ctx_factory):
     h.check_lists()
 
 
-def test_everyone_at_one_point(ctx_factory):
-    """Maximum skew: every entity in one cell, K = N-1 (hotspot stress)."""
-    n = 3000
+@pytest.mark.parametrize("n", [3000, 9000])
+def test_everyone_at_one_point(ctx_factory, n):
+    """Maximum skew: every entity in one cell, K = N-1 (hotspot stress; n=9000
+    exceeds the LDS tiers and exercises the global-scratch paths)."""
     tr = T.SpaceTrace(n=n, capacity=n, d=100.0, bounds=(-1000, -1000, 1000, 1000),
                       init_slots=np.arange(n, dtype=np.uint32), init_x=np.full(n, 5.0, np.float32),
                       init_y=np.zeros(n, np.float32), init_z=np.full(n, -5.0, np.float32),

@@ -36,8 +36,8 @@ HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--entities", type=int, default=1_000_000)
     ap.add_argument("--side", type=float, default=32768.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

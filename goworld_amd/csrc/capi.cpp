@@ -68,6 +68,8 @@ struct gw_ctx {
     LstMeta* lst = nullptr;
     uint8_t* is_mover = nullptr;
     unsigned long long* cnt64 = nullptr;     // [slot_cap + 1], zero between ticks
+    uint32_t* log_cnt = nullptr;             // [slot_cap] pending delta-log entries
+    uint32_t* logs = nullptr;                // [slot_cap * LOGCAP]
     int32_t *last_pos = nullptr, *last_aoi = nullptr, *last_leave = nullptr;
     SpaceP* sp_dev = nullptr;
     uint32_t sp_cap = 0;
@@ -264,7 +266,10 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->last_pos, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_aoi, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_leave, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->log_cnt, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->logs, (size_t)oc * LOGCAP, (size_t)nc * LOGCAP))) return rc;
     size_t n = nc - oc;
+    HIPCHK(hipMemsetAsync(c->log_cnt + oc, 0, n * 4, c->st));
     HIPCHK(hipMemsetAsync(c->aoi + oc, 0, n * sizeof(AoiEnt), c->st));
     HIPCHK(hipMemsetAsync(c->pos + oc, 0, n * sizeof(float4), c->st));
     HIPCHK(hipMemsetAsync(c->flags + oc, 0, n * 4, c->st));
@@ -331,9 +336,8 @@ int pool_reserve(gw_ctx* c, uint64_t reserve) {
         HIPCHK(hipMemcpyAsync(&live, &c->stats->scratch, 8, hipMemcpyDeviceToHost, c->st));
         HIPCHK(hipStreamSynchronize(c->st));
     }
-    uint64_t ncap = 2 * (live + reserve) + (1u << 20);
-    if (ncap >= (1ull << 32)) ncap = (1ull << 32) - 1;
-    if (live + reserve > ncap) return set_err(c, GW_ENOMEM, "neighbour pool exceeds 2^32 entries");
+    uint64_t ncap = (2 * (live + reserve) + (1u << 20) + 15) & ~15ull;
+    if (ncap >= (1ull << 36)) return set_err(c, GW_ENOMEM, "neighbour pool exceeds 2^36 entries");
     uint32_t* np = nullptr;
     if (hipMalloc(&np, ncap * 4) != hipSuccess) {
         (void)hipGetLastError();
@@ -445,7 +449,7 @@ void gw_shutdown(gw_ctx* c) {
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
     void* ps[] = {c->aoi, c->pos, c->flags, c->gate, c->lst, c->is_mover, c->cnt64, c->last_pos, c->last_aoi,
-                  c->last_leave, c->sp_dev, c->pool, c->stats, c->scal32};
+                  c->last_leave, c->log_cnt, c->logs, c->sp_dev, c->pool, c->stats, c->scal32};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     for (auto& s : c->stages) { (void)hipEventDestroy(s.a); (void)hipEventDestroy(s.b); }
@@ -613,6 +617,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.ops = ops; b.m = M; b.cap = C; b.ncells = NC;
     b.last_pos = c->last_pos; b.last_aoi = c->last_aoi; b.last_leave = c->last_leave;
     b.flags = c->flags; b.pos = c->pos; b.aoi = c->aoi; b.is_mover = c->is_mover; b.lst = c->lst; b.sp = c->sp_dev;
+    b.log_cnt = c->log_cnt; b.logs = c->logs;
     b.pool = c->pool; b.pool_cap = c->pool_cap; b.st = st;
     b.keys = P<uint32_t>(c->keys); b.cell_cnt = P<uint32_t>(c->cell_cnt); b.cell_start = P<uint32_t>(c->cell_start);
     b.cursor = P<uint32_t>(c->cursor); b.se = P<SortEnt>(c->se); b.pflag = P<uint32_t>(c->pflag);
@@ -652,9 +657,13 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         (rc = ensure(c, c->c_temp, std::max<uint64_t>(hs0.tier_c_temp, 4) * 4)) ||
         (rc = ensure(c, c->bigseg_temp, std::max<uint64_t>(4 * (sum_cand + sum_old) + 64, 64) * 4)))
         return rc;
-    // reallocations can only come from lists that outgrow their capacity:
-    // movers (<= cand entries each) and op-less watchers (<= old + enters)
-    const uint64_t reserve = 5 * (3 * sum_cand + c->h_total_entries) + 32 * ((uint64_t)C + n_mov) + (1u << 16);
+    // worst-case reallocation of one tick (every list that outgrows its
+    // capacity moves to a region of 2 * 2.5 * size): movers' materialization
+    // (<= old + log), movers' new lists (<= cand), op-less watchers' bursts
+    // (<= old + enters) and log materializations (<= old + LOGCAP each)
+    const uint64_t n_aff_bound = std::min<uint64_t>(C, sum_cand + sum_old);
+    const uint64_t reserve = 5 * (3 * sum_cand + sum_old + 2 * c->h_total_entries) +
+                             (5 * LOGCAP + 64) * n_aff_bound + 64 * ((uint64_t)C + n_mov) + (1u << 16);
     uint64_t top_before = c->h_pool_top;
     if ((rc = pool_reserve(c, reserve))) return rc;
     if (c->h_pool_top != top_before) {   // compaction moved the lists
@@ -668,7 +677,10 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.c_temp = P<uint32_t>(c->c_temp); b.c_temp_cap = std::max<uint64_t>(hs0.tier_c_temp, 4);
     b.bigseg_temp = P<uint32_t>(c->bigseg_temp); b.bigseg_temp_cap = c->bigseg_temp.cap / 4;
 
-    // ---- diff ------------------------------------------------------------------
+    // ---- movers' delta logs, then the diff -----------------------------------
+    prof_begin(c, "materialize");
+    tick_materialize_movers(b, n_mov, c->st);
+    prof_end(c, 0);
     prof_begin(c, "diff");
     tick_diff(b, n_s, n_b, n_c, c->st);
     size_t s_diff = prof_end(c, 0);
@@ -743,8 +755,10 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         out->n_gates = G;
         return 0;
     }
+    // flagged entities with pending logs are materialized before reading lists
+    if ((rc = pool_reserve(c, 5 * c->h_total_entries + (5 * LOGCAP + 64) * (uint64_t)C + (1u << 16)))) return rc;
     reset_stats_host(c);
-    HIPCHK(hipMemcpyAsync(c->stats, c->hstats, offsetof(DevStats, shard), hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
     DevStats* st = c->stats;
     const uint64_t rec_bound = (uint64_t)C + c->h_total_entries;
     if ((rc = ensure(c, c->flag_mark, (size_t)C * 4)) || (rc = ensure(c, c->flag_pre, (size_t)C * 8)) ||
@@ -760,6 +774,10 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     launch_flag_compact(P<uint32_t>(c->flag_mark), P<uint64_t>(c->flag_pre), C, P<uint32_t>(c->flagged), c->st);
     prof_end(c, (uint64_t)C * 4 * 4);
     const uint64_t* nf = (const uint64_t*)&st->flagged;
+    prof_begin(c, "sync_materialize");
+    launch_materialize_slots(c->lst, c->pool, c->pool_cap, st, c->log_cnt, c->logs, P<uint32_t>(c->flagged), nf, C,
+                             c->st);
+    prof_end(c, 0);
     prof_begin(c, "sync_count");
     launch_sync_count(P<uint32_t>(c->flagged), nf, C, c->flags, c->aoi, c->gate, c->lst, c->pool,
                       P<uint32_t>(c->rec_cnt), c->st);
@@ -776,6 +794,8 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     const uint64_t R = c->hstats->rec_total;
     const uint64_t NF = c->hstats->flagged;
     if (R > rec_bound) return set_err(c, GW_EDEVICE, "internal: record bound exceeded");
+    if (c->hstats->pool_overflow) return set_err(c, GW_ENOMEM, "internal: neighbour pool overflow");
+    c->h_pool_top = c->hstats->pool_top;
     gw_sync_record* recs = P<gw_sync_record>(c->rec0);
     // ---- per-gate grouping (stable, keeps (entity, watcher) order) -------
     if (R && G > 2) {
@@ -840,14 +860,40 @@ int gw_neighbors(gw_ctx* c, uint32_t slot, uint32_t* buf, uint32_t cap, uint32_t
     (void)hipSetDevice(c->dev);
     if (slot >= c->total_slots) return set_err(c, GW_ERANGE, "slot %u out of range", slot);
     LstMeta L{};
+    uint32_t lc = 0;
     HIPCHK(hipMemcpyAsync(&L, c->lst + slot, sizeof L, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(&lc, c->log_cnt + slot, 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
-    *n = L.cnt;
-    uint32_t k = std::min(L.cnt, cap);
-    if (buf && k) {
-        HIPCHK(hipMemcpyAsync(buf, c->pool + L.cur, (size_t)k * 4, hipMemcpyDeviceToHost, c->st));
-        HIPCHK(hipStreamSynchronize(c->st));
+    std::vector<uint32_t> base(L.cnt), lg(lc);
+    if (L.cnt)
+        HIPCHK(hipMemcpyAsync(base.data(), c->pool + ((uint64_t)L.cur << 4), (size_t)L.cnt * 4,
+                              hipMemcpyDeviceToHost, c->st));
+    if (lc) HIPCHK(hipMemcpyAsync(lg.data(), c->logs + (uint64_t)slot * LOGCAP, (size_t)lc * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (lc) {   // net effect of the delta log: majority kind per target
+        std::sort(lg.begin(), lg.end());
+        std::vector<uint32_t> add, rem;
+        for (size_t i = 0; i < lg.size();) {
+            size_t j = i;
+            int ne = 0, nl = 0;
+            while (j < lg.size() && (lg[j] >> 1) == (lg[i] >> 1)) { if (lg[j] & 1) ++nl; else ++ne; ++j; }
+            if (ne > nl) add.push_back(lg[i] >> 1);
+            if (nl > ne) rem.push_back(lg[i] >> 1);
+            i = j;
+        }
+        std::vector<uint32_t> out;
+        out.reserve(base.size() + add.size());
+        size_t ia = 0;
+        for (uint32_t v : base) {
+            while (ia < add.size() && add[ia] < v) out.push_back(add[ia++]);
+            if (!std::binary_search(rem.begin(), rem.end(), v)) out.push_back(v);
+        }
+        while (ia < add.size()) out.push_back(add[ia++]);
+        base.swap(out);
     }
+    *n = (uint32_t)base.size();
+    uint32_t k = std::min<uint32_t>((uint32_t)base.size(), cap);
+    if (buf && k) memcpy(buf, base.data(), (size_t)k * 4);
     return 0;
 }
 

@@ -48,7 +48,14 @@ struct alignas(16) SpaceP {
 };
 
 constexpr int STAT_SHARDS = 256;
-constexpr int SH_PAIRS = 0, SH_AOLD = 1, SH_ANEW = 2, SH_REALLOC = 3;
+constexpr int SH_FIELDS = 8;
+constexpr int SH_PAIRS = 0, SH_AOLD = 1, SH_ANEW = 2, SH_REALLOC = 3, SH_MAT = 4, SH_LOGAPP = 5, SH_MERGE = 6;
+
+// Delta log of one slot: up to LOGCAP pending events (target<<1 | leave) of an
+// op-less watcher, applied to its sorted list lazily (when it moves, is
+// collected, is queried or the log fills).  Lists are the base list plus the
+// log's net effect.
+constexpr uint32_t LOGCAP = 128;
 
 // Device-side counters of one tick / collect (read back once per call).
 struct DevStats {
@@ -68,10 +75,11 @@ struct DevStats {
     unsigned long long tmp_overflow;
     unsigned long long bad_ops;
     unsigned long long pairs_tested, a_old, a_new, reallocs;   // reduced from shards
+    unsigned long long materialized, log_appends, seg_merges;
     unsigned long long flagged;       // sync: flagged entities
     unsigned long long rec_total;     // sync: records
     unsigned long long scratch;       // generic scan total sink
-    unsigned long long shard[STAT_SHARDS][4];
+    unsigned long long shard[STAT_SHARDS][SH_FIELDS];
 };
 
 // ---- primitives (instantiated in kernels.hip) ------------------------------
@@ -103,6 +111,8 @@ struct TickBufs {
     AoiEnt* aoi;
     uint8_t* is_mover;
     LstMeta* lst;
+    uint32_t* log_cnt;        // [cap] pending log entries per slot
+    uint32_t* logs;           // [cap * LOGCAP]
     const SpaceP* sp;
     uint32_t* pool;
     uint64_t pool_cap;
@@ -154,6 +164,10 @@ void tick_diff(const TickBufs& b, uint64_t n_s, uint64_t n_b, uint64_t n_c, hipS
 void tick_events(const TickBufs& b, uint64_t n_movers, uint64_t* scan_tmp64, hipStream_t s);
 void tick_nonmovers(const TickBufs& b, uint64_t n_affected, uint64_t n_big, uint64_t n_movers, hipStream_t s);
 void tick_reset(const TickBufs& b, uint64_t n_movers, hipStream_t s);
+void tick_materialize_movers(const TickBufs& b, uint64_t n_movers, hipStream_t s);
+void launch_materialize_slots(LstMeta* lst, uint32_t* pool, uint64_t pool_cap, DevStats* st, uint32_t* log_cnt,
+                              uint32_t* logs, const uint32_t* slots, const uint64_t* n_dev, uint64_t n_max,
+                              hipStream_t s);
 void stats_reduce(DevStats* st, hipStream_t s);
 
 void launch_pool_compact(const LstMeta* lst_in, const uint64_t* new_off, uint32_t cap, const uint32_t* pool_old,

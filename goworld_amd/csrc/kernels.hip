@@ -92,6 +92,16 @@ __device__ __forceinline__ uint32_t next_pow2(uint32_t v) {
     if (v <= 1) return 1;
     return 1u << (32 - __clz(v - 1));
 }
+// list offsets are in units of 16 entries (64 B): lists start on cache lines and
+// a u32 offset addresses 2^36 entries
+__device__ __forceinline__ uint32_t* lptr(uint32_t* pool, uint32_t off) { return pool + ((uint64_t)off << 4); }
+__device__ __forceinline__ const uint32_t* lptr(const uint32_t* pool, uint32_t off) {
+    return pool + ((uint64_t)off << 4);
+}
+__device__ __forceinline__ uint32_t round16(uint64_t v) {
+    v = (v + 15) & ~15ull;
+    return (uint32_t)(v > 0x7ffffff0ull ? 0x7ffffff0ull : v);
+}
 __device__ __forceinline__ uint64_t lo32(uint64_t v) { return v & 0xffffffffull; }
 __device__ __forceinline__ uint64_t hi32(uint64_t v) { return v >> 32; }
 
@@ -338,7 +348,7 @@ __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
     if (m >= nm) return;
     uint32_t A = b.movers[m];
     AoiEnt a = b.aoi[A];
-    uint32_t ko = b.lst[A].cnt;
+    uint32_t ko = b.lst[A].cnt + b.log_cnt[A];     // >= the list size after its log is applied
     uint64_t c = 0;
     if (a.meta & PRESENT_BIT) {
         SpaceP P = b.sp[a.meta & SPACE_MASK];
@@ -384,6 +394,144 @@ void tick_bounds(const TickBufs& b, uint64_t* scan_tmp64, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
+// delta logs: apply a slot's pending events to its sorted list (one wave)
+struct ListCtx {
+    LstMeta* lst;
+    uint32_t* pool;
+    uint64_t pool_cap;
+    DevStats* st;
+    uint32_t* log_cnt;
+    uint32_t* logs;
+};
+__device__ __forceinline__ ListCtx list_ctx(const TickBufs& b) {
+    ListCtx c;
+    c.lst = b.lst; c.pool = b.pool; c.pool_cap = b.pool_cap; c.st = b.st; c.log_cnt = b.log_cnt; c.logs = b.logs;
+    return c;
+}
+
+// destination of a list rewrite: the alternate half, or a new region of
+// 2*ncap entries when the list outgrew its capacity (one lane allocates)
+__device__ __forceinline__ bool list_dest(const ListCtx& c, const LstMeta& L, uint32_t nn, uint32_t key,
+                                          uint32_t& dst_off, uint32_t& alt_off, uint32_t& ncap) {
+    dst_off = L.alt; alt_off = L.cur; ncap = L.cap;
+    if (nn <= L.cap) return true;
+    ncap = round16((uint64_t)nn * 5 / 2 + 16);
+    unsigned long long base = 0;
+    if (lane_id() == 0) base = atomicAdd(&c.st->pool_top, 2ull * ncap);
+    base = __shfl(base, 0, 64);
+    if (base + 2ull * ncap > c.pool_cap) {
+        if (lane_id() == 0) atomicAdd(&c.st->pool_overflow, 1ull);
+        return false;
+    }
+    dst_off = (uint32_t)(base >> 4);
+    alt_off = (uint32_t)((base + ncap) >> 4);
+    if (lane_id() == 0) shard_add(c.st, key, SH_REALLOC, 1);
+    return true;
+}
+
+// lbuf: 3*LOGCAP words of this wave's LDS
+__device__ void wave_materialize(const ListCtx& c, uint32_t s, uint32_t* lbuf) {
+    const int ln = lane_id();
+    const uint32_t lc = c.log_cnt[s];
+    if (lc == 0) return;
+    const uint64_t lt = lanemask_lt();
+    const uint32_t* lg = c.logs + (uint64_t)s * LOGCAP;
+    const uint32_t P2 = next_pow2(lc);
+    Grp<64> G;
+    G.sl = nullptr;
+    G.sync();
+    for (uint32_t i = ln; i < P2; i += 64) lbuf[i] = i < lc ? lg[i] : 0xffffffffu;
+    G.sync();
+    group_bitonic<64>(lbuf, P2, G);
+    // net effect per target: events of one pair alternate, so the majority
+    // kind of its run decides (more enters -> add, more leaves -> remove)
+    uint32_t* ADD = lbuf + LOGCAP;
+    uint32_t* REM = lbuf + 2 * LOGCAP;
+    uint32_t nadd = 0, nrem = 0;
+    for (uint32_t base = 0; base < lc; base += 64) {
+        const uint32_t i = base + ln;
+        bool isadd = false, isrem = false;
+        uint32_t t = 0;
+        if (i < lc) {
+            const uint32_t v = lbuf[i];
+            t = v >> 1;
+            if (i == 0 || (lbuf[i - 1] >> 1) != t) {
+                int ne = 0, nl = 0;
+                for (uint32_t j = i; j < lc && (lbuf[j] >> 1) == t; ++j) {
+                    if (lbuf[j] & 1) ++nl; else ++ne;
+                }
+                isadd = ne > nl;
+                isrem = nl > ne;
+            }
+        }
+        const uint64_t b1 = wave_ballot(isadd), b2 = wave_ballot(isrem);
+        if (isadd) ADD[nadd + popc64(b1 & lt)] = t;
+        if (isrem) REM[nrem + popc64(b2 & lt)] = t;
+        nadd += popc64(b1);
+        nrem += popc64(b2);
+    }
+    G.sync();
+    const LstMeta L = c.lst[s];
+    const uint32_t ko = L.cnt;
+    const uint32_t* __restrict__ old = lptr(c.pool, L.cur);
+    const uint32_t nn = ko + nadd - nrem;
+    uint32_t dst_off, alt_off, ncap;
+    if (!list_dest(c, L, nn, s, dst_off, alt_off, ncap)) return;
+    uint32_t* dst = lptr(c.pool, dst_off);
+    for (uint32_t j = ln; j < ko; j += 64) {
+        const uint32_t o = old[j];
+        const uint32_t ir = lower_bound_u32(REM, nrem, o);
+        if (ir < nrem && REM[ir] == o) continue;
+        const uint32_t at = j - ir + lower_bound_u32(ADD, nadd, o);
+        if (at < nn) dst[at] = o;
+    }
+    for (uint32_t q = ln; q < nadd; q += 64) {
+        const uint32_t a = ADD[q];
+        const uint32_t at = q + lower_bound_u32(old, ko, a) - lower_bound_u32(REM, nrem, a);
+        if (at < nn) dst[at] = a;
+    }
+    if (ln == 0) {
+        LstMeta n2;
+        n2.cur = dst_off; n2.alt = alt_off; n2.cnt = nn; n2.cap = ncap;
+        c.lst[s] = n2;
+        c.log_cnt[s] = 0;
+        shard_add(c.st, s, SH_MAT, 1);
+    }
+    G.sync();
+}
+
+__global__ void __launch_bounds__(NT) k_materialize_movers(TickBufs b) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * 3 * LOGCAP];
+    const uint64_t nm = n_movers_dev(b.st);
+    const ListCtx c = list_ctx(b);
+    uint32_t* lbuf = lds + (threadIdx.x >> 6) * 3 * LOGCAP;
+    const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
+    for (uint64_t m = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); m < nm; m += stride)
+        wave_materialize(c, b.movers[m], lbuf);
+}
+void tick_materialize_movers(const TickBufs& b, uint64_t n_movers, hipStream_t s) {
+    if (n_movers) hipLaunchKernelGGL(k_materialize_movers, dim3(gstride(n_movers, NWAVE)), dim3(NT), 0, s, b);
+}
+
+__global__ void __launch_bounds__(NT) k_materialize_slots(ListCtx c, const uint32_t* __restrict__ slots,
+                                                          const uint64_t* n_dev, uint64_t n_max) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * 3 * LOGCAP];
+    const uint64_t n = load_n(n_max, n_dev);
+    uint32_t* lbuf = lds + (threadIdx.x >> 6) * 3 * LOGCAP;
+    const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
+    for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < n; k += stride)
+        wave_materialize(c, slots[k], lbuf);
+}
+void launch_materialize_slots(LstMeta* lst, uint32_t* pool, uint64_t pool_cap, DevStats* st, uint32_t* log_cnt,
+                              uint32_t* logs, const uint32_t* slots, const uint64_t* n_dev, uint64_t n_max,
+                              hipStream_t s) {
+    if (!n_max) return;
+    ListCtx c;
+    c.lst = lst; c.pool = pool; c.pool_cap = pool_cap; c.st = st; c.log_cnt = log_cnt; c.logs = logs;
+    hipLaunchKernelGGL(k_materialize_slots, dim3(gstride(n_max, NWAVE)), dim3(NT), 0, s, c, slots, n_dev, n_max);
+}
+
+// ---------------------------------------------------------------------------
 // diff of one mover A by a group of TPM threads.
 //   (i)   candidates b in A's widened window with related(A,b) and b not in
 //         old(A) -> enters (buffer E), mirror enter (b,A) if b has no op
@@ -414,11 +562,11 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b, const uint32_t* __rest
     const int seqA = a.seq;
     const LstMeta L = b.lst[A];
     const uint32_t ko = L.cnt;
-    const uint32_t* __restrict__ old = b.pool + L.cur;
+    const uint32_t* __restrict__ old = lptr(b.pool, L.cur);
     const uint64_t rp = b.reg_pk[m];
     const uint64_t reg = lo32(rp) + hi32(rp);
     uint32_t* own_l = b.own + reg;            // own leaves  [0, ko)
-    uint32_t* own_e = b.own + reg + ko;       // own enters  [0, cand)
+    uint32_t* own_e = b.own + reg + (uint32_t)hi32(b.bpk[m]);   // own enters [0, cand) after the leave bound
     uint64_t* mir = b.mir + reg;              // mirror events [0, cand + ko)
     uint64_t* KM;
     uint32_t *E, *KP;
@@ -525,8 +673,7 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b, const uint32_t* __rest
     uint32_t dst_off = L.alt, alt_off = L.cur, ncap = L.cap;
     bool ok = true;
     if (nn > L.cap) {                                        // outgrew: new region of 2*ncap
-        uint64_t c2 = (uint64_t)nn * 5 / 2 + 16;
-        ncap = (uint32_t)(c2 > 0x7fffffffull ? 0x7fffffffull : c2);
+        ncap = round16((uint64_t)nn * 5 / 2 + 16);
         unsigned long long base = 0;
         if (t == 0) base = atomicAdd(&b.st->pool_top, 2ull * ncap);
         base = G.bcast0(base);
@@ -534,12 +681,12 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b, const uint32_t* __rest
             ok = false;
             if (t == 0) atomicAdd(&b.st->pool_overflow, 1ull);
         }
-        dst_off = (uint32_t)base;
-        alt_off = (uint32_t)(base + ncap);
+        dst_off = (uint32_t)(base >> 4);
+        alt_off = (uint32_t)((base + ncap) >> 4);
         if (t == 0) shard_add(b.st, m, SH_REALLOC, 1);
     }
     if (ok) {
-        uint32_t* dst = b.pool + dst_off;
+        uint32_t* dst = lptr(b.pool, dst_off);
         for (uint32_t base = 0; base < ko; base += TPM) {
             const uint32_t j = base + t;
             if (j < ko) {
@@ -736,39 +883,44 @@ __global__ void __launch_bounds__(NT) k_seg_sort_big(TickBufs b) {
     }
 }
 
-// merge the sorted event segments into an op-less watcher's list
-__global__ void __launch_bounds__(NT) k_nonmover_merge(TickBufs b, const uint32_t* __restrict__ list, int big) {
-    const uint64_t nlist = big ? hi32(b.st->n_affected) : lo32(b.st->n_affected);
+// op-less watchers: append the tick's (sorted) events to the delta log; a
+// watcher whose log would overflow is materialized first, and a burst larger
+// than the whole log is merged straight into its list
+__global__ void __launch_bounds__(NT) k_nonmover_update(TickBufs b) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * 3 * LOGCAP];
+    const uint64_t n_small = lo32(b.st->n_affected), n_big = hi32(b.st->n_affected);
+    const uint64_t nlist = n_small + n_big;
     const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
     const int ln = lane_id();
+    const ListCtx c = list_ctx(b);
+    uint32_t* lbuf = lds + (threadIdx.x >> 6) * 3 * LOGCAP;
     for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < nlist; k += stride) {
-        const uint32_t w = list[k];
-        const LstMeta L = b.lst[w];
-        const uint32_t ko = L.cnt;
-        const uint32_t* __restrict__ old = b.pool + L.cur;
+        const uint32_t w = k < n_small ? b.affected[k] : b.bigseg[k - n_small];
         const uint64_t o0 = b.off64[w], o1 = b.off64[w + 1];
         const gw_event* E = b.enter + lo32(o0);
         const gw_event* Lv = b.leave + hi32(o0);
         const uint32_t ne = (uint32_t)(lo32(o1) - lo32(o0)), nlv = (uint32_t)(hi32(o1) - hi32(o0));
-        const uint32_t nn = ko - nlv + ne;
-        uint32_t dst_off = L.alt, alt_off = L.cur, ncap = L.cap;
-        bool ok = true;
-        if (nn > L.cap) {
-            uint64_t c2 = (uint64_t)nn * 5 / 2 + 16;
-            ncap = (uint32_t)(c2 > 0x7fffffffull ? 0x7fffffffull : c2);
-            unsigned long long base = 0;
-            if (ln == 0) base = atomicAdd(&b.st->pool_top, 2ull * ncap);
-            base = __shfl(base, 0, 64);
-            if (base + 2ull * ncap > b.pool_cap) {
-                ok = false;
-                if (ln == 0) atomicAdd(&b.st->pool_overflow, 1ull);
+        const uint32_t n = ne + nlv;
+        if (b.log_cnt[w] + n > LOGCAP) wave_materialize(c, w, lbuf);
+        if (n <= LOGCAP) {
+            const uint32_t lc = b.log_cnt[w];
+            uint32_t* lg = b.logs + (uint64_t)w * LOGCAP + lc;
+            for (uint32_t q = ln; q < ne; q += 64) lg[q] = E[q].target << 1;
+            for (uint32_t q = ln; q < nlv; q += 64) lg[ne + q] = (Lv[q].target << 1) | 1u;
+            if (ln == 0) {
+                b.log_cnt[w] = lc + n;
+                shard_add(b.st, w, SH_LOGAPP, 1);
             }
-            dst_off = (uint32_t)base;
-            alt_off = (uint32_t)(base + ncap);
-            if (ln == 0) shard_add(b.st, (uint32_t)k, SH_REALLOC, 1);
+            continue;
         }
-        if (!ok) continue;
-        uint32_t* dst = b.pool + dst_off;
+        // burst: log is empty now, merge the sorted segments into the list
+        const LstMeta L = b.lst[w];
+        const uint32_t ko = L.cnt;
+        const uint32_t* __restrict__ old = lptr(b.pool, L.cur);
+        const uint32_t nn = ko - nlv + ne;
+        uint32_t dst_off, alt_off, ncap;
+        if (!list_dest(c, L, nn, w, dst_off, alt_off, ncap)) continue;
+        uint32_t* dst = lptr(b.pool, dst_off);
         for (uint32_t j = ln; j < ko; j += 64) {
             const uint32_t o = old[j];
             const uint32_t il = lower_bound_ev(Lv, nlv, o);
@@ -785,6 +937,7 @@ __global__ void __launch_bounds__(NT) k_nonmover_merge(TickBufs b, const uint32_
             LstMeta n2;
             n2.cur = dst_off; n2.alt = alt_off; n2.cnt = nn; n2.cap = ncap;
             b.lst[w] = n2;
+            shard_add(b.st, w, SH_MERGE, 1);
         }
     }
 }
@@ -797,9 +950,7 @@ void tick_nonmovers(const TickBufs& b, uint64_t n_affected_max, uint64_t n_big_m
         hipLaunchKernelGGL(k_seg_sort_small, dim3(gstride(n_affected_max, NWAVE)), dim3(NT), 0, s, b);
         hipLaunchKernelGGL(k_seg_sort_big, dim3(gstride(n_big_max, 1) > 1024 ? 1024 : gstride(n_big_max, 1)),
                            dim3(NT), 0, s, b);
-        hipLaunchKernelGGL(k_nonmover_merge, dim3(gstride(n_affected_max, NWAVE)), dim3(NT), 0, s, b, b.affected,
-                           0);
-        hipLaunchKernelGGL(k_nonmover_merge, dim3(gstride(n_big_max, NWAVE)), dim3(NT), 0, s, b, b.bigseg, 1);
+        hipLaunchKernelGGL(k_nonmover_update, dim3(gstride(n_affected_max, NWAVE)), dim3(NT), 0, s, b);
     }
 }
 
@@ -822,8 +973,8 @@ void tick_reset(const TickBufs& b, uint64_t n_movers, hipStream_t s) {
 
 __global__ void __launch_bounds__(NT) k_stats_reduce(DevStats* st) {
     __shared__ unsigned long long l[NWAVE];
-    unsigned long long tot[4];
-    for (int f = 0; f < 4; ++f) {
+    unsigned long long tot[SH_FIELDS];
+    for (int f = 0; f < SH_FIELDS; ++f) {
         unsigned long long v = st->shard[threadIdx.x][f], tt;
         block_excl_scan<unsigned long long>(v, l, tt);
         tot[f] = tt;
@@ -833,6 +984,9 @@ __global__ void __launch_bounds__(NT) k_stats_reduce(DevStats* st) {
         st->a_old = tot[SH_AOLD];
         st->a_new = tot[SH_ANEW];
         st->reallocs = tot[SH_REALLOC];
+        st->materialized = tot[SH_MAT];
+        st->log_appends = tot[SH_LOGAPP];
+        st->seg_merges = tot[SH_MERGE];
     }
 }
 void stats_reduce(DevStats* st, hipStream_t s) {
@@ -848,13 +1002,13 @@ __global__ void __launch_bounds__(NT) k_pool_compact(const LstMeta* __restrict__
     uint64_t s = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
     if (s >= cap) return;
     LstMeta L = lst_in[s];
-    const uint32_t* src = pool_old + L.cur;
+    const uint32_t* src = lptr(pool_old, L.cur);
     uint32_t* dst = pool_new + new_off[s];
     for (uint32_t j = lane_id(); j < L.cnt; j += 64) dst[j] = src[j];
     if (lane_id() == 0) {
         LstMeta n;
-        n.cur = (uint32_t)new_off[s];
-        n.alt = (uint32_t)(new_off[s] + L.cap);
+        n.cur = (uint32_t)(new_off[s] >> 4);
+        n.alt = (uint32_t)((new_off[s] + L.cap) >> 4);
         n.cnt = L.cnt;
         n.cap = L.cap;
         lst_out[s] = n;
@@ -918,7 +1072,7 @@ __global__ void __launch_bounds__(NT) k_sync_count(const uint32_t* __restrict__ 
     if (aoi[e].meta & PRESENT_BIT) {
         if (f & GW_SIF_NEIGHBOR_CLIENTS) {
             LstMeta L = lst[e];
-            const uint32_t* Ls = pool + L.cur;
+            const uint32_t* Ls = lptr(pool, L.cur);
             for (uint32_t j = lane_id(); j < L.cnt; j += 64) r += gate[Ls[j]] != 0;
             r = wave_sum(r);
         }
@@ -957,7 +1111,7 @@ __global__ void __launch_bounds__(NT) k_sync_write(const uint32_t* __restrict__ 
         uint32_t run = 0, below = 0;
         if (f & GW_SIF_NEIGHBOR_CLIENTS) {
             LstMeta L = lst[e];
-            const uint32_t* Ls = pool + L.cur;
+            const uint32_t* Ls = lptr(pool, L.cur);
             for (uint32_t j0 = 0; j0 < L.cnt; j0 += 64) {
                 uint32_t j = j0 + ln;
                 uint32_t w = 0;

@@ -265,3 +265,41 @@ def test_repeat_runs_are_deterministic(ctx_factory):
             seq.append((r.enter.tobytes(), r.leave.tobytes(), g.sync_collect().records.tobytes()))
         outs.append(seq)
     assert outs[0] == outs[1]
+
+
+def test_long_dense_run_fills_delta_logs(ctx_factory):
+    """Dense world, many ticks: op-less watchers accumulate delta logs until
+    they overflow (materialize + append), movers materialize theirs, SetYaw
+    ops on op-less entities force collect-time materialization, and neighbour
+    queries see base + pending log."""
+    n, ticks = 1500, 40
+    tr = T.dyadic_walk_trace(77, n, 640.0, 100.0, ticks, move_frac=0.12, step_q=4096)
+    for t, ops in enumerate(tr.ticks):          # add SetYaw ops on entities that do not move
+        moving = set(ops["slot"].tolist())
+        extra = [s for s in range(t, n, 97) if s not in moving][:5]
+        if extra:
+            yo = T.make_ops(len(extra))
+            yo["kind"] = T.OP_SYNC
+            yo["sync_flags"] = 3
+            yo["slot"] = extra
+            yo["yaw"] = np.float32(t)
+            # SetYaw carries the entity's current position (Entity.go:1284-1290)
+            yo["x"], yo["z"] = 0, 0
+            tr.ticks[t] = np.concatenate([ops, yo])
+    # positions carried by the SYNC ops must be the entities' real positions
+    x, z = tr.init_x.copy(), tr.init_z.copy()
+    for ops in tr.ticks:
+        mv = ops["kind"] == T.OP_MOVED
+        x[ops["slot"][mv]] = ops["x"][mv]
+        z[ops["slot"][mv]] = ops["z"][mv]
+        sy = ops["kind"] == T.OP_SYNC
+        ops["x"][sy] = x[ops["slot"][sy]]
+        ops["z"][sy] = z[ops["slot"][sy]]
+    h = Harness(ctx_factory(), [tr])
+    h.check_collect()
+    for t in range(ticks):
+        h.step(t)
+        h.check_collect()
+        if t % 13 == 12:
+            h.check_lists(sample=range(0, n, 7))
+    h.check_lists()

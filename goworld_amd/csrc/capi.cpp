@@ -86,7 +86,7 @@ struct gw_ctx {
     DevBuf off64, enter_d, leave_d, affected, bigseg, bigseg_off, bigseg_temp;
     DevBuf scan_tmp64, scan_tmp32, rs_hist, rs_scan_tmp;
     // sync scratch
-    DevBuf flag_mark, flag_pre, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1;
+    DevBuf flag_mark, flag_pre, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, rec_act, act_off;
     uint32_t* scal32 = nullptr;    // small device scalars
 
     // host mirror for validation of host-submitted ops
@@ -444,7 +444,7 @@ void gw_shutdown(gw_ctx* c) {
                       &c->enter_d, &c->leave_d, &c->affected, &c->bigseg, &c->bigseg_off, &c->bigseg_temp,
                       &c->scan_tmp64, &c->scan_tmp32, &c->rs_hist, &c->rs_scan_tmp, &c->flag_mark, &c->flag_pre,
                       &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1, &c->gate_hist, &c->gk0, &c->gv0,
-                      &c->gk1, &c->gv1};
+                      &c->gk1, &c->gv1, &c->rec_act, &c->act_off};
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
@@ -763,7 +763,8 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     const uint64_t rec_bound = (uint64_t)C + c->h_total_entries;
     if ((rc = ensure(c, c->flag_mark, (size_t)C * 4)) || (rc = ensure(c, c->flag_pre, (size_t)C * 8)) ||
         (rc = ensure(c, c->flagged, (size_t)C * 4)) || (rc = ensure(c, c->rec_cnt, (size_t)C * 4)) ||
-        (rc = ensure(c, c->rec_off, (size_t)C * 8)) ||
+        (rc = ensure(c, c->rec_off, (size_t)C * 8)) || (rc = ensure(c, c->rec_act, (size_t)C * 4)) ||
+        (rc = ensure(c, c->act_off, (size_t)C * 8)) ||
         (rc = ensure(c, c->rec0, (size_t)std::max<uint64_t>(rec_bound, 1) * sizeof(gw_sync_record))) ||
         (rc = ensure_scan64(c, C)))
         return rc;
@@ -787,16 +788,29 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     prof_begin(c, "sync_write");
     launch_sync_write(P<uint32_t>(c->flagged), nf, C, c->flags, c->aoi, c->gate, c->lst, c->pool, c->pos,
                       P<uint64_t>(c->rec_off), P<gw_sync_record>(c->rec0), c->rec0.cap / sizeof(gw_sync_record),
-                      c->st);
+                      P<uint32_t>(c->rec_act), st, c->st);
     size_t s_write = prof_end(c, 0);
     HIPCHK(hipGetLastError());
     if ((rc = read_stats(c))) return rc;
-    const uint64_t R = c->hstats->rec_total;
+    uint64_t R = c->hstats->rec_total;         // the bound; exact unless gaps were flagged
     const uint64_t NF = c->hstats->flagged;
     if (R > rec_bound) return set_err(c, GW_EDEVICE, "internal: record bound exceeded");
     if (c->hstats->pool_overflow) return set_err(c, GW_ENOMEM, "internal: neighbour pool overflow");
     c->h_pool_top = c->hstats->pool_top;
     gw_sync_record* recs = P<gw_sync_record>(c->rec0);
+    if (c->hstats->scratch & 1) {            // some neighbours have no client: compact
+        prof_begin(c, "sync_compact");
+        if ((rc = ensure(c, c->rec1, std::max<uint64_t>(R, 1) * sizeof(gw_sync_record)))) return rc;
+        scan_u32_u64(P<uint32_t>(c->rec_act), P<uint64_t>(c->act_off), C, nf, P<uint64_t>(c->scan_tmp64),
+                     (uint64_t*)&st->rec_total, c->st);
+        launch_sync_compact(nf, C, P<uint64_t>(c->rec_off), P<uint32_t>(c->rec_act), P<uint64_t>(c->act_off), recs,
+                            P<gw_sync_record>(c->rec1), c->st);
+        prof_end(c, 48 * R);
+        if ((rc = read_stats(c))) return rc;
+        R = c->hstats->rec_total;
+        std::swap(c->rec0, c->rec1);
+        recs = P<gw_sync_record>(c->rec0);
+    }
     // ---- per-gate grouping (stable, keeps (entity, watcher) order) -------
     if (R && G > 2) {
         prof_begin(c, "sync_gates");
@@ -842,7 +856,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     out->n_gates = G;
     out->bytes_alg = 24ull * R;
     if (c->prof) {
-        prof_set_bytes(c, s_count, 4ull * R + NF * 24);
+        prof_set_bytes(c, s_count, NF * 32);
         prof_set_bytes(c, s_write, 4ull * R + 24ull * R + NF * 24);
         prof_collect(c);
     }

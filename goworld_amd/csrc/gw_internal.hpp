@@ -185,7 +185,9 @@ void launch_sync_count(const uint32_t* flagged, const uint64_t* nf_dev, uint32_t
 void launch_sync_write(const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max, uint32_t* flags,
                        const AoiEnt* aoi, const uint16_t* gate, const LstMeta* lst, const uint32_t* pool,
                        const float4* pos, const uint64_t* rec_off, gw_sync_record* rec, uint64_t rec_cap,
-                       hipStream_t s);
+                       uint32_t* act, DevStats* st, hipStream_t s);
+void launch_sync_compact(const uint64_t* nf_dev, uint32_t nf_max, const uint64_t* rec_off, const uint32_t* act,
+                         const uint64_t* act_off, const gw_sync_record* in, gw_sync_record* out, hipStream_t s);
 void launch_gate_hist(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,
                       uint32_t* hist /*65536*/, hipStream_t s);
 void launch_gate_keys(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,

@@ -34,7 +34,7 @@ static inline uint32_t gstride(uint64_t n, uint32_t per) {   // grid of a grid-s
 }
 
 constexpr uint32_t TS_ECAP = 512, TS_OCAP = 512;       // tier S: one wave per mover
-constexpr uint32_t TB_ECAP = 8192, TB_OCAP = 4096;     // tier B: one workgroup per mover
+constexpr uint32_t TB_ECAP = 4096, TB_OCAP = 4096;     // tier B: one workgroup per mover
 constexpr uint32_t SEG_SMALL = 512;                    // op-less watcher segments sorted by one wave
 
 __device__ __forceinline__ int cellc(float v, float o, float inv, int lim) {
@@ -540,9 +540,9 @@ void launch_materialize_slots(LstMeta* lst, uint32_t* pool, uint64_t pool_cap, D
 //   merge new = kept old U E into the alternate half (or a new region)
 // Buffers E/KM/KP are LDS for tiers S/B and global scratch for tier C.
 template <int TPM, uint32_t ECAP, uint32_t OCAP, bool GLOB>
-__global__ void __launch_bounds__(NT) k_mover(TickBufs b, const uint32_t* __restrict__ list, int which) {
+__global__ void __launch_bounds__(NT, (TPM == 64 ? 6 : 4)) k_mover(TickBufs b, const uint32_t* __restrict__ list, int which) {
     constexpr uint32_t KW = GLOB ? 1 : (OCAP + 63) / 64;          // u64 words of kept mask
-    constexpr uint32_t GWORDS = GLOB ? 4 : ((2 * KW + ECAP + KW + 1 + 3) & ~3u);
+    constexpr uint32_t GWORDS = GLOB ? 4 : ((2 * KW + ECAP + OCAP + KW + 1 + 3) & ~3u);
     constexpr int GPB = NT / TPM;                                  // groups per block
     __shared__ __attribute__((aligned(16))) uint32_t lds[GPB * GWORDS + 16];
     const int gi = TPM == 64 ? (int)(threadIdx.x >> 6) : 0;
@@ -562,7 +562,7 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b, const uint32_t* __rest
     const int seqA = a.seq;
     const LstMeta L = b.lst[A];
     const uint32_t ko = L.cnt;
-    const uint32_t* __restrict__ old = lptr(b.pool, L.cur);
+    const uint32_t* __restrict__ old_g = lptr(b.pool, L.cur);
     const uint64_t rp = b.reg_pk[m];
     const uint64_t reg = lo32(rp) + hi32(rp);
     uint32_t* own_l = b.own + reg;            // own leaves  [0, ko)
@@ -570,6 +570,7 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b, const uint32_t* __rest
     uint64_t* mir = b.mir + reg;              // mirror events [0, cand + ko)
     uint64_t* KM;
     uint32_t *E, *KP;
+    const uint32_t* old;
     if constexpr (GLOB) {
         uint32_t cand = (uint32_t)lo32(b.bpk[m]);
         uint32_t* base = b.c_temp + b.c_temp_off[m];
@@ -577,11 +578,18 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b, const uint32_t* __rest
         KM = (uint64_t*)base;
         E = base + 2 * nw;
         KP = E + next_pow2(cand ? cand : 1);
+        old = old_g;
     } else {
+        // the old list is staged in LDS: membership tests and merge ranks are
+        // binary searches over it
         uint32_t* gb = lds + gi * GWORDS;
         KM = (uint64_t*)gb;
         E = gb + 2 * KW;
-        KP = E + ECAP;
+        uint32_t* OL = E + ECAP;
+        KP = OL + OCAP;
+        for (uint32_t j = t; j < ko; j += TPM) OL[j] = old_g[j];
+        G.sync();
+        old = OL;
     }
     uint32_t n_e = 0, n_mir = 0;
     uint64_t tested = 0;
@@ -1056,35 +1064,32 @@ void launch_flag_compact(const uint32_t* mark, const uint64_t* pre, uint32_t cap
     hipLaunchKernelGGL(k_flag_compact, dim3(nblk1(cap, NT)), dim3(NT), 0, s, mark, pre, cap, flagged);
 }
 
-// records per flagged entity e: own (bit0 and e has a client) + one per
-// neighbour n in e.InterestedBy with a client (bit1)
+// record bound per flagged entity e: own (bit0 and e has a client) + |list|
+// (bit1).  Exact when every neighbour has a client (the usual case); the write
+// kernel flags gaps and a compaction pass closes them.
 __global__ void __launch_bounds__(NT) k_sync_count(const uint32_t* __restrict__ flagged, const uint64_t* nf_dev,
                                                    uint32_t nf_max, const uint32_t* __restrict__ flags,
                                                    const AoiEnt* __restrict__ aoi, const uint16_t* __restrict__ gate,
                                                    const LstMeta* __restrict__ lst,
                                                    const uint32_t* __restrict__ pool, uint32_t* cnt) {
+    (void)pool;
     uint64_t nf = load_n(nf_max, nf_dev);
-    uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
+    uint64_t k = (uint64_t)blockIdx.x * NT + threadIdx.x;
     if (k >= nf) return;
     uint32_t e = flagged[k];
     uint32_t f = flags[e];
     uint32_t r = 0;
     if (aoi[e].meta & PRESENT_BIT) {
-        if (f & GW_SIF_NEIGHBOR_CLIENTS) {
-            LstMeta L = lst[e];
-            const uint32_t* Ls = lptr(pool, L.cur);
-            for (uint32_t j = lane_id(); j < L.cnt; j += 64) r += gate[Ls[j]] != 0;
-            r = wave_sum(r);
-        }
+        if (f & GW_SIF_NEIGHBOR_CLIENTS) r += lst[e].cnt;
         if ((f & GW_SIF_OWN_CLIENT) && gate[e]) r += 1;
     }
-    if (lane_id() == 0) cnt[k] = r;
+    cnt[k] = r;
 }
 void launch_sync_count(const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max, const uint32_t* flags,
                        const AoiEnt* aoi, const uint16_t* gate, const LstMeta* lst, const uint32_t* pool,
                        uint32_t* cnt, hipStream_t s) {
     if (!nf_max) return;
-    hipLaunchKernelGGL(k_sync_count, dim3(nblk(nf_max, NWAVE)), dim3(NT), 0, s, flagged, nf_dev, nf_max, flags, aoi,
+    hipLaunchKernelGGL(k_sync_count, dim3(nblk(nf_max, NT)), dim3(NT), 0, s, flagged, nf_dev, nf_max, flags, aoi,
                        gate, lst, pool, cnt);
 }
 
@@ -1096,7 +1101,7 @@ __global__ void __launch_bounds__(NT) k_sync_write(const uint32_t* __restrict__ 
                                                    const LstMeta* __restrict__ lst,
                                                    const uint32_t* __restrict__ pool, const float4* __restrict__ pos,
                                                    const uint64_t* __restrict__ rec_off, gw_sync_record* rec,
-                                                   uint64_t rec_cap) {
+                                                   uint64_t rec_cap, uint32_t* act, DevStats* st) {
     const int ln = lane_id();
     uint64_t nf = load_n(nf_max, nf_dev);
     uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
@@ -1134,16 +1139,48 @@ __global__ void __launch_bounds__(NT) k_sync_write(const uint32_t* __restrict__ 
             r.watcher = e; r.entity = e; r.x = p.x; r.y = p.y; r.z = p.z; r.yaw = p.w;
             if (base + below < rec_cap) rec[base + below] = r;
         }
+        const uint32_t n_act = run + (own ? 1u : 0u);
+        if (ln == 0) {
+            act[k] = n_act;
+            if (f & GW_SIF_NEIGHBOR_CLIENTS) {
+                const uint32_t bound = lst[e].cnt + (own ? 1u : 0u);
+                if (n_act != bound) atomicOr((unsigned int*)&st->scratch, 1u);   // gaps: compact
+            }
+        }
+    } else if (ln == 0) {
+        act[k] = 0;
     }
     if (ln == 0) flags[e] = 0;
+}
+
+// close the gaps left by neighbours without clients: copy each entity's
+// records from its bound offset to its exact offset (into a second buffer)
+__global__ void __launch_bounds__(NT) k_sync_compact(const uint64_t* nf_dev, uint32_t nf_max,
+                                                     const uint64_t* __restrict__ rec_off,
+                                                     const uint32_t* __restrict__ act,
+                                                     const uint64_t* __restrict__ act_off,
+                                                     const gw_sync_record* __restrict__ in, gw_sync_record* out) {
+    uint64_t nf = load_n(nf_max, nf_dev);
+    uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
+    if (k >= nf) return;
+    const uint32_t n = act[k];
+    const gw_sync_record* src = in + rec_off[k];
+    gw_sync_record* dst = out + act_off[k];
+    for (uint32_t j = lane_id(); j < n; j += 64) dst[j] = src[j];
+}
+void launch_sync_compact(const uint64_t* nf_dev, uint32_t nf_max, const uint64_t* rec_off, const uint32_t* act,
+                         const uint64_t* act_off, const gw_sync_record* in, gw_sync_record* out, hipStream_t s) {
+    if (!nf_max) return;
+    hipLaunchKernelGGL(k_sync_compact, dim3(nblk(nf_max, NWAVE)), dim3(NT), 0, s, nf_dev, nf_max, rec_off, act,
+                       act_off, in, out);
 }
 void launch_sync_write(const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max, uint32_t* flags,
                        const AoiEnt* aoi, const uint16_t* gate, const LstMeta* lst, const uint32_t* pool,
                        const float4* pos, const uint64_t* rec_off, gw_sync_record* rec, uint64_t rec_cap,
-                       hipStream_t s) {
+                       uint32_t* act, DevStats* st, hipStream_t s) {
     if (!nf_max) return;
     hipLaunchKernelGGL(k_sync_write, dim3(nblk(nf_max, NWAVE)), dim3(NT), 0, s, flagged, nf_dev, nf_max, flags, aoi,
-                       gate, lst, pool, pos, rec_off, rec, rec_cap);
+                       gate, lst, pool, pos, rec_off, rec, rec_cap, act, st);
 }
 
 // per-gate record histogram: LDS buckets for gates < 256, global atomics above

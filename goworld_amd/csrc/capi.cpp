@@ -14,6 +14,7 @@
 #include <cstddef>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -53,6 +54,8 @@ struct Stage {
 
 struct gw_ctx {
     int dev = 0;
+    int ab = 1;           // GW_AB: kernel-variant switches for A/B timing (bit0 materialize movers
+                          // in a separate pass, bit1 separate small-segment sort); same results
     hipStream_t st = nullptr;
     std::string err;
 
@@ -413,6 +416,7 @@ int gw_init(int device_id, gw_ctx** out) {
     *out = nullptr;
     gw_ctx* c = new gw_ctx();
     c->dev = device_id;
+    if (const char* e = getenv("GW_AB")) c->ab = atoi(e);
     int rc = 0;
     do {
         if (hipSetDevice(device_id) != hipSuccess) { rc = set_err(c, GW_EDEVICE, "hipSetDevice(%d) failed", device_id); break; }
@@ -679,7 +683,8 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
 
     // ---- movers' delta logs, then the diff -----------------------------------
     prof_begin(c, "materialize");
-    tick_materialize_movers(b, n_mov, c->st);
+    if (c->ab & 1) tick_materialize_movers(b, hs0.movers_present, true, c->st);
+    else tick_materialize_movers(b, n_c, false, c->st);
     prof_end(c, 0);
     prof_begin(c, "diff");
     tick_diff(b, n_s, n_b, n_c, c->st);
@@ -687,7 +692,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     prof_begin(c, "events");
     tick_events(b, n_mov, stmp, c->st);
     const uint64_t aff_max = std::min<uint64_t>(C, sum_cand + sum_old);
-    tick_nonmovers(b, aff_max, aff_max, n_mov, c->st);
+    tick_nonmovers(b, aff_max, aff_max, n_mov, c->st, !(c->ab & 2));
     size_t s_events = prof_end(c, 0);
     prof_begin(c, "reset");
     tick_reset(b, n_mov, c->st);

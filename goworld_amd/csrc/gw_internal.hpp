@@ -162,9 +162,10 @@ void tick_movers(const TickBufs& b, uint64_t* scan_tmp64, hipStream_t s);
 void tick_bounds(const TickBufs& b, uint64_t* scan_tmp64, hipStream_t s);
 void tick_diff(const TickBufs& b, uint64_t n_s, uint64_t n_b, uint64_t n_c, hipStream_t s);
 void tick_events(const TickBufs& b, uint64_t n_movers, uint64_t* scan_tmp64, hipStream_t s);
-void tick_nonmovers(const TickBufs& b, uint64_t n_affected, uint64_t n_big, uint64_t n_movers, hipStream_t s);
+void tick_nonmovers(const TickBufs& b, uint64_t n_affected, uint64_t n_big, uint64_t n_movers, hipStream_t s,
+                    bool fuse_sort);
 void tick_reset(const TickBufs& b, uint64_t n_movers, hipStream_t s);
-void tick_materialize_movers(const TickBufs& b, uint64_t n_movers, hipStream_t s);
+void tick_materialize_movers(const TickBufs& b, uint64_t n, bool all, hipStream_t s);
 void launch_materialize_slots(LstMeta* lst, uint32_t* pool, uint64_t pool_cap, DevStats* st, uint32_t* log_cnt,
                               uint32_t* logs, const uint32_t* slots, const uint64_t* n_dev, uint64_t n_max,
                               hipStream_t s);

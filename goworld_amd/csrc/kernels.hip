@@ -500,17 +500,19 @@ __device__ void wave_materialize(const ListCtx& c, uint32_t s, uint32_t* lbuf) {
     G.sync();
 }
 
-__global__ void __launch_bounds__(NT) k_materialize_movers(TickBufs b) {
+// movers of tier C (global-scratch diff) materialise their logs first; tiers
+// S and B apply them while staging the old list in LDS
+__global__ void __launch_bounds__(NT) k_materialize_movers(TickBufs b, int all) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * 3 * LOGCAP];
-    const uint64_t nm = n_movers_dev(b.st);
+    const uint64_t nc = all ? b.st->movers_present : b.st->n_tier_c;
     const ListCtx c = list_ctx(b);
     uint32_t* lbuf = lds + (threadIdx.x >> 6) * 3 * LOGCAP;
     const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
-    for (uint64_t m = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); m < nm; m += stride)
-        wave_materialize(c, b.movers[m], lbuf);
+    for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < nc; k += stride)
+        wave_materialize(c, b.movers[all ? k : b.list_c[k]], lbuf);
 }
-void tick_materialize_movers(const TickBufs& b, uint64_t n_movers, hipStream_t s) {
-    if (n_movers) hipLaunchKernelGGL(k_materialize_movers, dim3(gstride(n_movers, NWAVE)), dim3(NT), 0, s, b);
+void tick_materialize_movers(const TickBufs& b, uint64_t n, bool all, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_materialize_movers, dim3(gstride(n, NWAVE)), dim3(NT), 0, s, b, (int)all);
 }
 
 __global__ void __launch_bounds__(NT) k_materialize_slots(ListCtx c, const uint32_t* __restrict__ slots,
@@ -542,6 +544,7 @@ void launch_materialize_slots(LstMeta* lst, uint32_t* pool, uint64_t pool_cap, D
 template <int TPM, uint32_t ECAP, uint32_t OCAP, bool GLOB>
 __global__ void __launch_bounds__(NT, (TPM == 64 ? 6 : 4)) k_mover(TickBufs b, const uint32_t* __restrict__ list, int which) {
     constexpr uint32_t KW = GLOB ? 1 : (OCAP + 63) / 64;          // u64 words of kept mask
+    static_assert(GLOB || ECAP >= 3 * LOGCAP, "the log is staged in E");
     constexpr uint32_t GWORDS = GLOB ? 4 : ((2 * KW + ECAP + OCAP + KW + 1 + 3) & ~3u);
     constexpr int GPB = NT / TPM;                                  // groups per block
     __shared__ __attribute__((aligned(16))) uint32_t lds[GPB * GWORDS + 16];
@@ -561,7 +564,7 @@ __global__ void __launch_bounds__(NT, (TPM == 64 ? 6 : 4)) k_mover(TickBufs b, c
     const float lox = a.x - d, hix = a.x + d, loz = a.z - d, hiz = a.z + d;   // fl(x-d), fl(x+d)
     const int seqA = a.seq;
     const LstMeta L = b.lst[A];
-    const uint32_t ko = L.cnt;
+    uint32_t ko = L.cnt;
     const uint32_t* __restrict__ old_g = lptr(b.pool, L.cur);
     const uint64_t rp = b.reg_pk[m];
     const uint64_t reg = lo32(rp) + hi32(rp);
@@ -587,7 +590,63 @@ __global__ void __launch_bounds__(NT, (TPM == 64 ? 6 : 4)) k_mover(TickBufs b, c
         E = gb + 2 * KW;
         uint32_t* OL = E + ECAP;
         KP = OL + OCAP;
-        for (uint32_t j = t; j < ko; j += TPM) OL[j] = old_g[j];
+        uint32_t* LG = E;                                        // 3*LOGCAP: log, adds, removes (E is free until (i))
+        const uint32_t lc = b.log_cnt[A];
+        if (lc == 0) {
+            for (uint32_t j = t; j < ko; j += TPM) OL[j] = old_g[j];
+        } else {
+            // the mover's pending delta log is applied here (base list + net
+            // adds - net removes -> OL); the materialised list is never written
+            const uint32_t* lg = b.logs + (uint64_t)A * LOGCAP;
+            const uint32_t LP2 = next_pow2(lc);
+            for (uint32_t i = t; i < LP2; i += TPM) LG[i] = i < lc ? lg[i] : 0xffffffffu;
+            G.sync();
+            group_bitonic<TPM>(LG, LP2, G);
+            uint32_t* ADD = LG + LOGCAP;
+            uint32_t* REM = LG + 2 * LOGCAP;
+            uint32_t nadd = 0, nrem = 0;
+            for (uint32_t base = 0; base < lc; base += TPM) {
+                const uint32_t i = base + t;
+                bool isadd = false, isrem = false;
+                uint32_t tg = 0;
+                if (i < lc) {
+                    tg = LG[i] >> 1;
+                    if (i == 0 || (LG[i - 1] >> 1) != tg) {
+                        int ne = 0, nl = 0;
+                        for (uint32_t j = i; j < lc && (LG[j] >> 1) == tg; ++j) {
+                            if (LG[j] & 1) ++nl; else ++ne;
+                        }
+                        isadd = ne > nl;
+                        isrem = nl > ne;
+                    }
+                }
+                uint32_t pa, pr, ta, tr;
+                G.excl2(isadd, isrem, pa, pr, ta, tr);
+                if (isadd) ADD[nadd + pa] = tg;
+                if (isrem) REM[nrem + pr] = tg;
+                nadd += ta;
+                nrem += tr;
+            }
+            G.sync();
+            const uint32_t kb0 = ko;
+            ko = kb0 + nadd - nrem;
+            for (uint32_t j = t; j < kb0; j += TPM) {
+                const uint32_t o = old_g[j];
+                const uint32_t ir = lower_bound_u32(REM, nrem, o);
+                if (ir < nrem && REM[ir] == o) continue;
+                const uint32_t at = j - ir + lower_bound_u32(ADD, nadd, o);
+                if (at < ko) OL[at] = o;
+            }
+            for (uint32_t q = t; q < nadd; q += TPM) {
+                const uint32_t av = ADD[q];
+                const uint32_t at = q + lower_bound_u32(old_g, kb0, av) - lower_bound_u32(REM, nrem, av);
+                if (at < ko) OL[at] = av;
+            }
+            if (t == 0) {
+                b.log_cnt[A] = 0;
+                shard_add(b.st, A, SH_MAT, 1);
+            }
+        }
         G.sync();
         old = OL;
     }
@@ -894,20 +953,26 @@ __global__ void __launch_bounds__(NT) k_seg_sort_big(TickBufs b) {
 // op-less watchers: append the tick's (sorted) events to the delta log; a
 // watcher whose log would overflow is materialized first, and a burst larger
 // than the whole log is merged straight into its list
-__global__ void __launch_bounds__(NT) k_nonmover_update(TickBufs b) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * 3 * LOGCAP];
+__global__ void __launch_bounds__(NT, 6) k_nonmover_update(TickBufs b, int sort_small) {
+    constexpr uint32_t WW = SEG_SMALL > 3 * LOGCAP ? SEG_SMALL : 3 * LOGCAP;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * WW];
     const uint64_t n_small = lo32(b.st->n_affected), n_big = hi32(b.st->n_affected);
     const uint64_t nlist = n_small + n_big;
     const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
     const int ln = lane_id();
     const ListCtx c = list_ctx(b);
-    uint32_t* lbuf = lds + (threadIdx.x >> 6) * 3 * LOGCAP;
+    uint32_t* lbuf = lds + (threadIdx.x >> 6) * WW;           // segment sort, then materialize
+    uint32_t* sbuf = lbuf;
     for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < nlist; k += stride) {
         const uint32_t w = k < n_small ? b.affected[k] : b.bigseg[k - n_small];
         const uint64_t o0 = b.off64[w], o1 = b.off64[w + 1];
-        const gw_event* E = b.enter + lo32(o0);
-        const gw_event* Lv = b.leave + hi32(o0);
+        gw_event* E = b.enter + lo32(o0);
+        gw_event* Lv = b.leave + hi32(o0);
         const uint32_t ne = (uint32_t)(lo32(o1) - lo32(o0)), nlv = (uint32_t)(hi32(o1) - hi32(o0));
+        if (sort_small && k < n_small) {     // big segments were sorted by k_seg_sort_big
+            wave_sort_segment(E, ne, sbuf);
+            wave_sort_segment(Lv, nlv, sbuf);
+        }
         const uint32_t n = ne + nlv;
         if (b.log_cnt[w] + n > LOGCAP) wave_materialize(c, w, lbuf);
         if (n <= LOGCAP) {
@@ -951,14 +1016,16 @@ __global__ void __launch_bounds__(NT) k_nonmover_update(TickBufs b) {
 }
 
 void tick_nonmovers(const TickBufs& b, uint64_t n_affected_max, uint64_t n_big_max, uint64_t n_movers,
-                    hipStream_t s) {
+                    hipStream_t s, bool fuse_sort) {
     if (n_movers)
         hipLaunchKernelGGL(k_events_scatter, dim3(nblk(n_movers, NWAVE)), dim3(NT), 0, s, b);
     if (n_affected_max) {
-        hipLaunchKernelGGL(k_seg_sort_small, dim3(gstride(n_affected_max, NWAVE)), dim3(NT), 0, s, b);
         hipLaunchKernelGGL(k_seg_sort_big, dim3(gstride(n_big_max, 1) > 1024 ? 1024 : gstride(n_big_max, 1)),
                            dim3(NT), 0, s, b);
-        hipLaunchKernelGGL(k_nonmover_update, dim3(gstride(n_affected_max, NWAVE)), dim3(NT), 0, s, b);
+        if (!fuse_sort)
+            hipLaunchKernelGGL(k_seg_sort_small, dim3(gstride(n_affected_max, NWAVE)), dim3(NT), 0, s, b);
+        hipLaunchKernelGGL(k_nonmover_update, dim3(gstride(n_affected_max, NWAVE)), dim3(NT), 0, s, b,
+                           (int)fuse_sort);
     }
 }
 

@@ -4,17 +4,17 @@ ARCH     ?= gfx950
 # strict float32: the window bounds fl(c-d), fl(c+d) must round like Go's float32
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
 LIBDIR   := goworld_amd/lib
-SRC      := goworld_amd/csrc/kernels.hip goworld_amd/csrc/capi.cpp
-HDR      := goworld_amd/csrc/prim.hpp goworld_amd/csrc/gw_internal.hpp include/gpuaoi.h
-OBJ      := $(LIBDIR)/kernels.o $(LIBDIR)/capi.o
+CSRC     := goworld_amd/csrc
+HDR      := $(CSRC)/prim.hpp $(CSRC)/gw_internal.hpp $(CSRC)/dev_common.hpp include/gpuaoi.h
+OBJ      := $(LIBDIR)/aoi.o $(LIBDIR)/sync.o $(LIBDIR)/capi.o
 
 all: $(LIBDIR)/libgpuaoi.so oracle
 
-$(LIBDIR)/kernels.o: goworld_amd/csrc/kernels.hip $(HDR)
+$(LIBDIR)/%.o: $(CSRC)/%.hip $(HDR)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIBDIR)/capi.o: goworld_amd/csrc/capi.cpp $(HDR)
+$(LIBDIR)/capi.o: $(CSRC)/capi.cpp $(HDR)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 

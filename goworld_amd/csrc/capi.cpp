@@ -1,12 +1,14 @@
 // capi.cpp — C ABI of include/gpuaoi.h on one HIP device.
 //
-// Host orchestration of the per-tick pipeline (kernels in kernels.hip):
-//   ops -> grid (counting sort by cell) -> movers in cell order + leavers ->
-//   per-mover bounds and tiers [the one mid-tick host sync: size the event
-//   regions, reserve pool space] -> diff (tiers S/B/C) -> per-watcher offsets
-//   -> mirror scatter + own copy -> segment sorts -> op-less watchers' merges
-//   -> reset.
-// No torch, no CPU fallback: every compute step is a HIP kernel.
+// Host orchestration of the per-tick pipeline (kernels in aoi.hip, sync.hip):
+//   ops -> grid (stable radix sort by cell) -> movers in grid order + leavers
+//   -> mover grid + per-mover candidate bounds [the one mid-tick host sync:
+//   size the own-event regions and the event arrays] -> diff (one wave per
+//   mover) -> op-less count pass -> per-watcher scan -> own copy + op-less
+//   write pass -> big-segment sorts -> reset.
+// No neighbour lists are kept (gw_internal.hpp): collect and queries evaluate
+// relations from the current grid.  No torch, no CPU fallback: every compute
+// step is a HIP kernel.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -54,42 +56,39 @@ struct Stage {
 
 struct gw_ctx {
     int dev = 0;
-    int ab = 1;           // GW_AB: kernel-variant switches for A/B timing (bit0 materialize movers
-                          // in a separate pass, bit1 separate small-segment sort); same results
     hipStream_t st = nullptr;
     std::string err;
 
     std::vector<SpaceHost> spaces;
     uint32_t total_slots = 0, slot_cap = 0, total_cells = 0;
     uint16_t max_gate = 0;
+    unsigned long long stamp_base = 1;   // global op counter (stamp 0 = never)
+    bool grid_dirty = true;              // gn/gn_start must be rebuilt before queries
+    uint64_t h_present = 0;
 
     // persistent device state (slot-indexed)
     AoiEnt* aoi = nullptr;
+    PrevEnt* prev = nullptr;
+    unsigned long long* stamp = nullptr;
     float4* pos = nullptr;
     uint32_t* flags = nullptr;
     uint16_t* gate = nullptr;
-    LstMeta* lst = nullptr;
-    uint8_t* is_mover = nullptr;
     unsigned long long* cnt64 = nullptr;     // [slot_cap + 1], zero between ticks
-    uint32_t* log_cnt = nullptr;             // [slot_cap] pending delta-log entries
-    uint32_t* logs = nullptr;                // [slot_cap * LOGCAP]
     int32_t *last_pos = nullptr, *last_aoi = nullptr, *last_leave = nullptr;
+    GEnt* gn = nullptr;
+    uint32_t* gidx = nullptr;
     SpaceP* sp_dev = nullptr;
     uint32_t sp_cap = 0;
-    uint32_t* pool = nullptr;
-    uint64_t pool_cap = 0;
-    uint64_t h_pool_top = 0, h_total_entries = 0, h_live_caps = 0;
 
     DevStats* stats = nullptr;     // device
     DevStats* hstats = nullptr;    // pinned host
 
-    // tick scratch
-    DevBuf ops_buf, keys, cell_cnt, cell_start, cursor, se, pflag, pre, fpre;
-    DevBuf movers, bpk, tpk, reg_pk, tier_pre, list_s, list_b, list_c, c_temp_off, c_temp, own, mir, mir_cnt;
-    DevBuf off64, enter_d, leave_d, affected, bigseg, bigseg_off, bigseg_temp;
-    DevBuf scan_tmp64, scan_tmp32, rs_hist, rs_scan_tmp;
-    // sync scratch
-    DevBuf flag_mark, flag_pre, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, rec_act, act_off;
+    // grid + tick scratch
+    DevBuf gn_start, ops_buf, k0, v0, k1, v1, pflag, pre, movers, gm_cnt, gm_start, gm, cand, reg, own, big;
+    DevBuf mir, mir_rank, mir_cnt;
+    DevBuf off64, enter_d, leave_d, scan_tmp64, scan_tmp32, rs_hist, rs_scan_tmp;
+    // sync / query scratch
+    DevBuf flag_mark, flag_pre, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
     uint32_t* scal32 = nullptr;    // small device scalars
 
     // host mirror for validation of host-submitted ops
@@ -140,7 +139,10 @@ int ensure(gw_ctx* c, DevBuf& b, size_t bytes) {
     if (b.cap >= bytes) return 0;
     size_t nb = std::max(bytes, b.cap + b.cap / 2);
     nb = (nb + 255) & ~(size_t)255;
-    if (b.p) HIPCHK(hipFree(b.p));
+    if (b.p) {
+        HIPCHK(hipStreamSynchronize(c->st));
+        HIPCHK(hipFree(b.p));
+    }
     b.p = nullptr;
     b.cap = 0;
     if (hipMalloc(&b.p, nb) != hipSuccess) {
@@ -260,25 +262,24 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     uint32_t oc = c->slot_cap;
     int rc;
     if ((rc = grow_preserve(c, c->aoi, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->prev, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->stamp, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->pos, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->flags, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->gate, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->lst, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->is_mover, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->cnt64, oc ? oc + 1 : 0, (size_t)nc + 1))) return rc;
     if ((rc = grow_preserve(c, c->last_pos, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_aoi, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_leave, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->log_cnt, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->logs, (size_t)oc * LOGCAP, (size_t)nc * LOGCAP))) return rc;
+    if ((rc = grow_preserve(c, c->gn, 0, nc))) return rc;        // rebuilt (grid_dirty)
+    if ((rc = grow_preserve(c, c->gidx, 0, nc))) return rc;
     size_t n = nc - oc;
-    HIPCHK(hipMemsetAsync(c->log_cnt + oc, 0, n * 4, c->st));
     HIPCHK(hipMemsetAsync(c->aoi + oc, 0, n * sizeof(AoiEnt), c->st));
+    HIPCHK(hipMemsetAsync(c->prev + oc, 0, n * sizeof(PrevEnt), c->st));
+    HIPCHK(hipMemsetAsync(c->stamp + oc, 0, n * 8, c->st));
     HIPCHK(hipMemsetAsync(c->pos + oc, 0, n * sizeof(float4), c->st));
     HIPCHK(hipMemsetAsync(c->flags + oc, 0, n * 4, c->st));
     HIPCHK(hipMemsetAsync(c->gate + oc, 0, n * 2, c->st));
-    HIPCHK(hipMemsetAsync(c->lst + oc, 0, n * sizeof(LstMeta), c->st));
-    HIPCHK(hipMemsetAsync(c->is_mover + oc, 0, n, c->st));
     HIPCHK(hipMemsetAsync(c->cnt64 + oc, 0, (n + 1) * 8, c->st));
     launch_fill_i32(c->last_pos + oc, -1, n, c->st);
     launch_fill_i32(c->last_aoi + oc, -1, n, c->st);
@@ -287,6 +288,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     c->slot_cap = nc;
     c->present_h.resize(nc, 0);
     c->space_of_h.resize(nc, -1);
+    c->grid_dirty = true;
     return 0;
 }
 
@@ -321,41 +323,51 @@ int read_stats(gw_ctx* c) {
     return 0;
 }
 
-// Guarantee `reserve` free entries past the pool top; when the pool cannot
-// hold them, compact every slot's current list (capacities kept) into a new
-// pool sized for the live capacities plus twice the reserve.
-int pool_reserve(gw_ctx* c, uint64_t reserve) {
-    if (c->pool && c->h_pool_top + reserve <= c->pool_cap) return 0;
+void reset_stats_host(gw_ctx* c) { memset(c->hstats, 0, sizeof(DevStats)); }
+
+World world(gw_ctx* c) {
+    World w;
+    w.cap = c->total_slots;
+    w.ncells = c->total_cells;
+    w.sp = c->sp_dev;
+    w.aoi = c->aoi; w.prev = c->prev; w.stamp = c->stamp; w.pos = c->pos; w.flags = c->flags; w.gate = c->gate;
+    w.gn = c->gn; w.gn_start = P<uint32_t>(c->gn_start); w.gidx = c->gidx;
+    return w;
+}
+
+int ensure_grid_bufs(gw_ctx* c, uint64_t CM) {
+    const uint32_t C = c->total_slots, NC = c->total_cells;
     int rc;
-    uint64_t live = 0;
-    if (c->pool && c->total_slots) {
-        // (sized by total_slots: gw_tick already holds buffers at least this big)
-        if ((rc = ensure(c, c->pflag, (size_t)c->total_slots * 4))) return rc;
-        if ((rc = ensure(c, c->pre, (size_t)c->total_slots * 8))) return rc;
-        if ((rc = ensure_scan64(c, (uint64_t)c->total_slots + 1))) return rc;
-        launch_cap2(c->lst, c->total_slots, P<uint32_t>(c->pflag), c->st);
-        scan_u32_u64(P<uint32_t>(c->pflag), P<uint64_t>(c->pre), c->total_slots, nullptr, P<uint64_t>(c->scan_tmp64),
-                     (uint64_t*)&c->stats->scratch, c->st);
-        HIPCHK(hipMemcpyAsync(&live, &c->stats->scratch, 8, hipMemcpyDeviceToHost, c->st));
-        HIPCHK(hipStreamSynchronize(c->st));
-    }
-    uint64_t ncap = (2 * (live + reserve) + (1u << 20) + 15) & ~15ull;
-    if (ncap >= (1ull << 36)) return set_err(c, GW_ENOMEM, "neighbour pool exceeds 2^36 entries");
-    uint32_t* np = nullptr;
-    if (hipMalloc(&np, ncap * 4) != hipSuccess) {
-        (void)hipGetLastError();
-        return set_err(c, GW_ENOMEM, "pool hipMalloc(%llu entries) failed", (unsigned long long)ncap);
-    }
-    if (c->pool && c->total_slots) {
-        launch_pool_compact(c->lst, P<uint64_t>(c->pre), c->total_slots, c->pool, np, c->lst, c->st);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipStreamSynchronize(c->st));
-    }
-    if (c->pool) HIPCHK(hipFree(c->pool));
-    c->pool = np;
-    c->pool_cap = ncap;
-    c->h_pool_top = live;
-    c->h_live_caps = live;
+    if ((rc = ensure(c, c->gn_start, ((size_t)NC + 2) * 4)) || (rc = ensure(c, c->k0, (size_t)C * 4)) ||
+        (rc = ensure(c, c->v0, (size_t)C * 4)) || (rc = ensure(c, c->k1, (size_t)C * 4)) ||
+        (rc = ensure(c, c->v1, (size_t)C * 4)) || (rc = ensure(c, c->pflag, CM * 4)) ||
+        (rc = ensure(c, c->pre, CM * 8)) || (rc = ensure_scan64(c, CM + 1)) ||
+        (rc = ensure_scan32(c, (uint64_t)NC + 1)))
+        return rc;
+    return 0;
+}
+
+// rebuild the current grid without a tick (new spaces/cells, queries)
+int rebuild_grid(gw_ctx* c) {
+    if (!c->grid_dirty) return 0;
+    const uint32_t C = c->total_slots;
+    int rc;
+    if ((rc = ensure_grid_bufs(c, C))) return rc;
+    RadixTmp rt;
+    if ((rc = radix_tmp(c, C, rt))) return rc;
+    reset_stats_host(c);
+    HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
+    TickBufs b{};
+    b.w = world(c);
+    b.st = c->stats;
+    b.k0 = P<uint32_t>(c->k0); b.v0 = P<uint32_t>(c->v0); b.k1 = P<uint32_t>(c->k1); b.v1 = P<uint32_t>(c->v1);
+    b.pflag = nullptr;
+    if (C) tick_grid(b, rt, ceil_log2((uint64_t)c->total_cells + 1), P<uint32_t>(c->scan_tmp32), c->st);
+    else HIPCHK(hipMemsetAsync(c->gn_start.p, 0, ((size_t)c->total_cells + 1) * 4, c->st));
+    HIPCHK(hipGetLastError());
+    if ((rc = read_stats(c))) return rc;
+    c->h_present = c->hstats->n_present;
+    c->grid_dirty = false;
     return 0;
 }
 
@@ -397,11 +409,6 @@ int validate_ops(gw_ctx* c, const gw_op* ops, uint32_t n) {
     return rc;
 }
 
-void reset_stats_host(gw_ctx* c) {
-    memset(c->hstats, 0, sizeof(DevStats));
-    c->hstats->pool_top = c->h_pool_top;
-}
-
 }  // namespace
 
 // =========================================================================
@@ -416,7 +423,6 @@ int gw_init(int device_id, gw_ctx** out) {
     *out = nullptr;
     gw_ctx* c = new gw_ctx();
     c->dev = device_id;
-    if (const char* e = getenv("GW_AB")) c->ab = atoi(e);
     int rc = 0;
     do {
         if (hipSetDevice(device_id) != hipSuccess) { rc = set_err(c, GW_EDEVICE, "hipSetDevice(%d) failed", device_id); break; }
@@ -442,18 +448,17 @@ void gw_shutdown(gw_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    DevBuf* bufs[] = {&c->ops_buf, &c->keys, &c->cell_cnt, &c->cell_start, &c->cursor, &c->se, &c->pflag, &c->pre,
-                      &c->fpre, &c->movers, &c->bpk, &c->tpk, &c->reg_pk, &c->tier_pre, &c->list_s, &c->list_b,
-                      &c->list_c, &c->c_temp_off, &c->c_temp, &c->own, &c->mir, &c->mir_cnt, &c->off64,
-                      &c->enter_d, &c->leave_d, &c->affected, &c->bigseg, &c->bigseg_off, &c->bigseg_temp,
-                      &c->scan_tmp64, &c->scan_tmp32, &c->rs_hist, &c->rs_scan_tmp, &c->flag_mark, &c->flag_pre,
-                      &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1, &c->gate_hist, &c->gk0, &c->gv0,
-                      &c->gk1, &c->gv1, &c->rec_act, &c->act_off};
+    DevBuf* bufs[] = {&c->gn_start, &c->ops_buf, &c->k0, &c->v0, &c->k1, &c->v1, &c->pflag, &c->pre, &c->movers,
+                      &c->gm_cnt, &c->gm_start, &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->off64, &c->mir,
+                      &c->mir_rank, &c->mir_cnt,
+                      &c->enter_d, &c->leave_d, &c->scan_tmp64, &c->scan_tmp32, &c->rs_hist, &c->rs_scan_tmp,
+                      &c->flag_mark, &c->flag_pre, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
+                      &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf};
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
-    void* ps[] = {c->aoi, c->pos, c->flags, c->gate, c->lst, c->is_mover, c->cnt64, c->last_pos, c->last_aoi,
-                  c->last_leave, c->log_cnt, c->logs, c->sp_dev, c->pool, c->stats, c->scal32};
+    void* ps[] = {c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->last_pos, c->last_aoi,
+                  c->last_leave, c->gn, c->gidx, c->sp_dev, c->stats, c->scal32};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     for (auto& s : c->stages) { (void)hipEventDestroy(s.a); (void)hipEventDestroy(s.b); }
@@ -501,6 +506,7 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
     c->spaces.push_back(s);
     c->total_slots += capacity;
     c->total_cells += (uint32_t)ncells;
+    c->grid_dirty = true;
     for (uint32_t i = 0; i < capacity; ++i) c->space_of_h[s.base + i] = (int32_t)sid;
     if ((rc = upload_spaces(c))) return rc;
     if (space_id) *space_id = sid;
@@ -555,7 +561,7 @@ int gw_set_clients(gw_ctx* c, const uint32_t* slots, const uint16_t* gates, uint
     if ((rc = ensure(c, c->gv0, (size_t)n * 2))) return rc;
     HIPCHK(hipMemcpyAsync(c->gk0.p, slots, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemcpyAsync(c->gv0.p, gates, (size_t)n * 2, hipMemcpyHostToDevice, c->st));
-    launch_set_clients(P<uint32_t>(c->gk0), (const uint16_t*)c->gv0.p, n, c->total_slots, c->gate, c->st);
+    launch_set_clients(world(c), P<uint32_t>(c->gk0), (const uint16_t*)c->gv0.p, n, c->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
@@ -599,100 +605,62 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     const uint32_t NC = c->total_cells;
     const uint64_t CM = std::max<uint64_t>(C, M);
     // ---- buffers whose size is known before the tick ----------------------
-    if ((rc = ensure(c, c->keys, (size_t)C * 4)) || (rc = ensure(c, c->cell_cnt, ((size_t)NC + 1) * 4)) ||
-        (rc = ensure(c, c->cell_start, ((size_t)NC + 2) * 4)) || (rc = ensure(c, c->cursor, ((size_t)NC + 1) * 4)) ||
-        (rc = ensure(c, c->se, (size_t)C * sizeof(SortEnt))) || (rc = ensure(c, c->pflag, CM * 4)) ||
-        (rc = ensure(c, c->pre, CM * 8)) || (rc = ensure(c, c->fpre, (size_t)C * 8)) ||
-        (rc = ensure(c, c->movers, (size_t)M * 4)) || (rc = ensure(c, c->bpk, (size_t)M * 8)) ||
-        (rc = ensure(c, c->tpk, (size_t)M * 8)) || (rc = ensure(c, c->reg_pk, (size_t)M * 8)) ||
-        (rc = ensure(c, c->tier_pre, (size_t)M * 8)) || (rc = ensure(c, c->list_s, (size_t)M * 4)) ||
-        (rc = ensure(c, c->list_b, (size_t)M * 4)) || (rc = ensure(c, c->list_c, (size_t)M * 4)) ||
-        (rc = ensure(c, c->c_temp_off, (size_t)M * 8)) || (rc = ensure(c, c->mir_cnt, (size_t)M * 4)) ||
-        (rc = ensure(c, c->off64, ((size_t)C + 2) * 8)) || (rc = ensure(c, c->affected, (size_t)C * 4)) ||
-        (rc = ensure(c, c->bigseg, (size_t)C * 4)) || (rc = ensure(c, c->bigseg_off, (size_t)C * 8)) ||
-        (rc = ensure_scan64(c, CM + 1)) || (rc = ensure_scan32(c, (uint64_t)NC + 1)))
+    RadixTmp rt;
+    if ((rc = ensure_grid_bufs(c, CM)) || (rc = radix_tmp(c, C, rt)) ||
+        (rc = ensure(c, c->movers, (size_t)M * 4)) || (rc = ensure(c, c->gm_cnt, ((size_t)NC + 1) * 4)) ||
+        (rc = ensure(c, c->gm_start, ((size_t)NC + 1) * 4)) || (rc = ensure(c, c->gm, (size_t)2 * M * sizeof(MEnt))) ||
+        (rc = ensure(c, c->cand, (size_t)M * 8)) || (rc = ensure(c, c->reg, (size_t)M * 8)) ||
+        (rc = ensure(c, c->big, ((size_t)M + C) * 4)) || (rc = ensure(c, c->off64, ((size_t)C + 2) * 8)) ||
+        (rc = ensure(c, c->mir_cnt, (size_t)M * 4)))
         return rc;
-    if (!c->pool && (rc = pool_reserve(c, 1u << 20))) return rc;
     reset_stats_host(c);
     HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
     DevStats* st = c->stats;
 
     TickBufs b{};
-    b.ops = ops; b.m = M; b.cap = C; b.ncells = NC;
+    b.w = world(c);
+    b.ops = ops; b.m = M; b.stamp_base = c->stamp_base;
     b.last_pos = c->last_pos; b.last_aoi = c->last_aoi; b.last_leave = c->last_leave;
-    b.flags = c->flags; b.pos = c->pos; b.aoi = c->aoi; b.is_mover = c->is_mover; b.lst = c->lst; b.sp = c->sp_dev;
-    b.log_cnt = c->log_cnt; b.logs = c->logs;
-    b.pool = c->pool; b.pool_cap = c->pool_cap; b.st = st;
-    b.keys = P<uint32_t>(c->keys); b.cell_cnt = P<uint32_t>(c->cell_cnt); b.cell_start = P<uint32_t>(c->cell_start);
-    b.cursor = P<uint32_t>(c->cursor); b.se = P<SortEnt>(c->se); b.pflag = P<uint32_t>(c->pflag);
-    b.pre = P<uint64_t>(c->pre); b.fpre = P<uint64_t>(c->fpre);
-    b.movers = P<uint32_t>(c->movers); b.bpk = P<uint64_t>(c->bpk); b.tpk = P<uint64_t>(c->tpk);
-    b.reg_pk = P<uint64_t>(c->reg_pk); b.tier_pre = P<uint64_t>(c->tier_pre); b.list_s = P<uint32_t>(c->list_s);
-    b.list_b = P<uint32_t>(c->list_b); b.list_c = P<uint32_t>(c->list_c); b.c_temp_off = P<uint64_t>(c->c_temp_off);
-    b.mir_cnt = P<uint32_t>(c->mir_cnt); b.cnt64 = c->cnt64; b.off64 = P<uint64_t>(c->off64);
-    b.affected = P<uint32_t>(c->affected); b.bigseg = P<uint32_t>(c->bigseg); b.bigseg_off = P<uint64_t>(c->bigseg_off);
-    b.write_events = (flags & GW_TICK_NO_EVENTS) ? 0 : 1;
+    b.st = st;
+    b.k0 = P<uint32_t>(c->k0); b.v0 = P<uint32_t>(c->v0); b.k1 = P<uint32_t>(c->k1); b.v1 = P<uint32_t>(c->v1);
+    b.pflag = P<uint32_t>(c->pflag); b.pre = P<uint64_t>(c->pre);
+    b.movers = P<uint32_t>(c->movers); b.gm_cnt = P<uint32_t>(c->gm_cnt); b.gm_start = P<uint32_t>(c->gm_start);
+    b.gm = P<MEnt>(c->gm); b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg); b.big = P<uint32_t>(c->big);
+    b.cnt64 = c->cnt64; b.off64 = P<uint64_t>(c->off64);
 
     uint64_t* stmp = P<uint64_t>(c->scan_tmp64);
     prof_begin(c, "ops");
     tick_ops(b, c->st);
     prof_end(c, (uint64_t)M * 24);
     prof_begin(c, "grid");
-    tick_grid(b, stmp, P<uint32_t>(c->scan_tmp32), c->st);
+    tick_grid(b, rt, ceil_log2((uint64_t)NC + 1), P<uint32_t>(c->scan_tmp32), c->st);
     size_t s_grid = prof_end(c, 0);
     prof_begin(c, "movers");
-    tick_movers(b, stmp, c->st);
-    tick_bounds(b, stmp, c->st);
+    tick_movers(b, stmp, P<uint32_t>(c->scan_tmp32), c->st);
     size_t s_movers = prof_end(c, 0);
     HIPCHK(hipGetLastError());
     // ---- the one mid-tick host sync ---------------------------------------
     if ((rc = read_stats(c))) return rc;
     DevStats hs0 = *c->hstats;
     if (hs0.bad_ops) return set_err(c, GW_EINVAL, "%llu ops with bad slot/kind", hs0.bad_ops);
-    const uint64_t n_mov = hs0.movers_present + hs0.leavers;
-    const uint64_t sum_cand = hs0.bound_pk & 0xffffffffull, sum_old = hs0.bound_pk >> 32;
-    const uint64_t n_s = hs0.tier_pk & 0xffffffffull, n_b = hs0.tier_pk >> 32, n_c = hs0.n_tier_c;
-    const uint64_t region = std::max<uint64_t>(sum_cand + sum_old, 1);
-    if (sum_cand >= (1ull << 32) - 1 || sum_old >= (1ull << 32) - 1)
-        return set_err(c, GW_ERANGE, "tick too large: %llu candidates", (unsigned long long)sum_cand);
-    if ((rc = ensure(c, c->own, region * 4)) || (rc = ensure(c, c->mir, region * 8)) ||
-        (rc = ensure(c, c->enter_d, std::max<uint64_t>(2 * sum_cand, 1) * sizeof(gw_event))) ||
-        (rc = ensure(c, c->leave_d, std::max<uint64_t>(2 * sum_old, 1) * sizeof(gw_event))) ||
-        (rc = ensure(c, c->c_temp, std::max<uint64_t>(hs0.tier_c_temp, 4) * 4)) ||
-        (rc = ensure(c, c->bigseg_temp, std::max<uint64_t>(4 * (sum_cand + sum_old) + 64, 64) * 4)))
+    const uint64_t n_mov = hs0.n_movers;
+    const uint64_t ctot = std::max<uint64_t>(hs0.cand_total, 1);
+    // own events <= candidates; each op-less event mirrors an own event of a
+    // mover (the relation is symmetric), so each stream holds <= 2 * ctot
+    if ((rc = ensure(c, c->own, ctot * 4)) || (rc = ensure(c, c->mir, ctot * 8)) ||
+        (rc = ensure(c, c->mir_rank, ctot * 4)) || (rc = ensure(c, c->enter_d, 2 * ctot * sizeof(gw_event))) ||
+        (rc = ensure(c, c->leave_d, 2 * ctot * sizeof(gw_event))))
         return rc;
-    // worst-case reallocation of one tick (every list that outgrows its
-    // capacity moves to a region of 2 * 2.5 * size): movers' materialization
-    // (<= old + log), movers' new lists (<= cand), op-less watchers' bursts
-    // (<= old + enters) and log materializations (<= old + LOGCAP each)
-    const uint64_t n_aff_bound = std::min<uint64_t>(C, sum_cand + sum_old);
-    const uint64_t reserve = 5 * (3 * sum_cand + sum_old + 2 * c->h_total_entries) +
-                             (5 * LOGCAP + 64) * n_aff_bound + 64 * ((uint64_t)C + n_mov) + (1u << 16);
-    uint64_t top_before = c->h_pool_top;
-    if ((rc = pool_reserve(c, reserve))) return rc;
-    if (c->h_pool_top != top_before) {   // compaction moved the lists
-        c->hstats->pool_top = c->h_pool_top;
-        HIPCHK(hipMemcpyAsync(&st->pool_top, &c->hstats->pool_top, 8, hipMemcpyHostToDevice, c->st));
-    }
-    b.pool = c->pool; b.pool_cap = c->pool_cap;
-    b.own = P<uint32_t>(c->own); b.mir = P<uint64_t>(c->mir);
+    b.own = P<uint32_t>(c->own);
+    b.mir = P<uint64_t>(c->mir); b.mir_rank = P<uint32_t>(c->mir_rank); b.mir_cnt = P<uint32_t>(c->mir_cnt);
     b.enter = P<gw_event>(c->enter_d); b.leave = P<gw_event>(c->leave_d);
-    b.enter_cap = std::max<uint64_t>(2 * sum_cand, 1); b.leave_cap = std::max<uint64_t>(2 * sum_old, 1);
-    b.c_temp = P<uint32_t>(c->c_temp); b.c_temp_cap = std::max<uint64_t>(hs0.tier_c_temp, 4);
-    b.bigseg_temp = P<uint32_t>(c->bigseg_temp); b.bigseg_temp_cap = c->bigseg_temp.cap / 4;
+    b.enter_cap = 2 * ctot; b.leave_cap = 2 * ctot;
 
-    // ---- movers' delta logs, then the diff -----------------------------------
-    prof_begin(c, "materialize");
-    if (c->ab & 1) tick_materialize_movers(b, hs0.movers_present, true, c->st);
-    else tick_materialize_movers(b, n_c, false, c->st);
-    prof_end(c, 0);
     prof_begin(c, "diff");
-    tick_diff(b, n_s, n_b, n_c, c->st);
+    tick_diff(b, n_mov, c->st);
     size_t s_diff = prof_end(c, 0);
     prof_begin(c, "events");
     tick_events(b, n_mov, stmp, c->st);
-    const uint64_t aff_max = std::min<uint64_t>(C, sum_cand + sum_old);
-    tick_nonmovers(b, aff_max, aff_max, n_mov, c->st, !(c->ab & 2));
     size_t s_events = prof_end(c, 0);
     prof_begin(c, "reset");
     tick_reset(b, n_mov, c->st);
@@ -704,11 +672,10 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     DevStats& hs = *c->hstats;
     c->segs.clear();
     c->pend_host.clear();
-    if (hs.pool_overflow) return set_err(c, GW_EDEVICE, "internal: neighbour pool overflow");
-    if (hs.tmp_overflow) return set_err(c, GW_EDEVICE, "internal: segment scratch overflow");
+    c->stamp_base += M;
+    c->grid_dirty = false;
+    c->h_present = hs.n_present;
     const uint64_t n_enter = hs.ev_pk & 0xffffffffull, n_leave = hs.ev_pk >> 32;
-    c->h_pool_top = hs.pool_top;
-    c->h_total_entries = c->h_total_entries + n_enter - n_leave;   // every list changes by its enters - leaves
     float ms = 0;
     (void)hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1);
     out->device_us = ms * 1000.0;
@@ -725,12 +692,13 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     const uint64_t n_evt = n_enter + n_leave;
     out->bytes_alg = 20ull * n_mov + 8ull * hs.n_present + 4ull * (hs.a_old + hs.a_new) + 8ull * n_evt;
     if (c->prof) {
-        prof_set_bytes(c, s_grid, 16ull * C + 16ull * hs.n_present + 8ull * NC);
-        prof_set_bytes(c, s_movers, 8ull * hs.n_present + 40ull * n_mov);
-        // diff: candidates (16 B) + old lists read twice (4 B) + neighbour state gathered (16 B per old
-        // entry) + new lists (4 B) + own and mirror events (12 B per directed event)
-        prof_set_bytes(c, s_diff, 16ull * hs.pairs_tested + 24ull * hs.a_old + 4ull * hs.a_new + 12ull * n_evt);
-        prof_set_bytes(c, s_events, 16ull * (C + 1) + 24ull * n_evt);
+        // grid: keys + 3 radix passes (8 B in, 8 B out) + entries (16 B) + slot index
+        prof_set_bytes(c, s_grid, 20ull * C + 16ull * 3 * C + 20ull * hs.n_present + 4ull * NC);
+        prof_set_bytes(c, s_movers, 8ull * hs.n_present + 80ull * n_mov + 8ull * NC);
+        // diff: candidates (16 B grid / 32 B mover grid; counted at 16 B) + own events (4 B)
+        prof_set_bytes(c, s_diff, 16ull * hs.pairs_tested + 4ull * n_evt);
+        // events: per-watcher counts and offsets (24 B per slot) + events (8 B) + own copies (4 B)
+        prof_set_bytes(c, s_events, 24ull * (C + 1) + 12ull * n_evt);
         prof_collect(c);
     }
     if ((flags & GW_TICK_COPY_TO_HOST) && !(flags & GW_TICK_NO_EVENTS)) {
@@ -755,24 +723,20 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     HIPCHK(hipEventRecord(c->ev_t0, c->st));
     const uint32_t G = (uint32_t)c->max_gate + 1;
     c->gate_off.assign((size_t)G + 1, 0);
-    if (C == 0 || !c->pool) {
+    if (C == 0) {
         out->gate_off = c->gate_off.data();
         out->n_gates = G;
         return 0;
     }
-    // flagged entities with pending logs are materialized before reading lists
-    if ((rc = pool_reserve(c, 5 * c->h_total_entries + (5 * LOGCAP + 64) * (uint64_t)C + (1u << 16)))) return rc;
+    if ((rc = rebuild_grid(c))) return rc;
     reset_stats_host(c);
     HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
     DevStats* st = c->stats;
-    const uint64_t rec_bound = (uint64_t)C + c->h_total_entries;
     if ((rc = ensure(c, c->flag_mark, (size_t)C * 4)) || (rc = ensure(c, c->flag_pre, (size_t)C * 8)) ||
         (rc = ensure(c, c->flagged, (size_t)C * 4)) || (rc = ensure(c, c->rec_cnt, (size_t)C * 4)) ||
-        (rc = ensure(c, c->rec_off, (size_t)C * 8)) || (rc = ensure(c, c->rec_act, (size_t)C * 4)) ||
-        (rc = ensure(c, c->act_off, (size_t)C * 8)) ||
-        (rc = ensure(c, c->rec0, (size_t)std::max<uint64_t>(rec_bound, 1) * sizeof(gw_sync_record))) ||
-        (rc = ensure_scan64(c, C)))
+        (rc = ensure(c, c->rec_off, (size_t)C * 8)) || (rc = ensure_scan64(c, C)))
         return rc;
+    const World w = world(c);
     prof_begin(c, "sync_flagged");
     launch_flag_mark(c->flags, C, P<uint32_t>(c->flag_mark), c->st);
     scan_u32_u64(P<uint32_t>(c->flag_mark), P<uint64_t>(c->flag_pre), C, nullptr, P<uint64_t>(c->scan_tmp64),
@@ -780,43 +744,23 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     launch_flag_compact(P<uint32_t>(c->flag_mark), P<uint64_t>(c->flag_pre), C, P<uint32_t>(c->flagged), c->st);
     prof_end(c, (uint64_t)C * 4 * 4);
     const uint64_t* nf = (const uint64_t*)&st->flagged;
-    prof_begin(c, "sync_materialize");
-    launch_materialize_slots(c->lst, c->pool, c->pool_cap, st, c->log_cnt, c->logs, P<uint32_t>(c->flagged), nf, C,
-                             c->st);
-    prof_end(c, 0);
     prof_begin(c, "sync_count");
-    launch_sync_count(P<uint32_t>(c->flagged), nf, C, c->flags, c->aoi, c->gate, c->lst, c->pool,
-                      P<uint32_t>(c->rec_cnt), c->st);
+    launch_sync_count(w, P<uint32_t>(c->flagged), nf, C, P<uint32_t>(c->rec_cnt), st, c->st);
     scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), C, nf, P<uint64_t>(c->scan_tmp64),
                  (uint64_t*)&st->rec_total, c->st);
     size_t s_count = prof_end(c, 0);
-    prof_begin(c, "sync_write");
-    launch_sync_write(P<uint32_t>(c->flagged), nf, C, c->flags, c->aoi, c->gate, c->lst, c->pool, c->pos,
-                      P<uint64_t>(c->rec_off), P<gw_sync_record>(c->rec0), c->rec0.cap / sizeof(gw_sync_record),
-                      P<uint32_t>(c->rec_act), st, c->st);
-    size_t s_write = prof_end(c, 0);
     HIPCHK(hipGetLastError());
     if ((rc = read_stats(c))) return rc;
-    uint64_t R = c->hstats->rec_total;         // the bound; exact unless gaps were flagged
+    const uint64_t R = c->hstats->rec_total;
     const uint64_t NF = c->hstats->flagged;
-    if (R > rec_bound) return set_err(c, GW_EDEVICE, "internal: record bound exceeded");
-    if (c->hstats->pool_overflow) return set_err(c, GW_ENOMEM, "internal: neighbour pool overflow");
-    c->h_pool_top = c->hstats->pool_top;
+    if ((rc = ensure(c, c->rec0, std::max<uint64_t>(R, 1) * sizeof(gw_sync_record)))) return rc;
+    prof_begin(c, "sync_write");
+    launch_sync_write(w, P<uint32_t>(c->flagged), nf, C, P<uint64_t>(c->rec_off), P<gw_sync_record>(c->rec0),
+                      std::max<uint64_t>(R, 1), c->st);
+    size_t s_write = prof_end(c, 0);
+    HIPCHK(hipGetLastError());
     gw_sync_record* recs = P<gw_sync_record>(c->rec0);
-    if (c->hstats->scratch & 1) {            // some neighbours have no client: compact
-        prof_begin(c, "sync_compact");
-        if ((rc = ensure(c, c->rec1, std::max<uint64_t>(R, 1) * sizeof(gw_sync_record)))) return rc;
-        scan_u32_u64(P<uint32_t>(c->rec_act), P<uint64_t>(c->act_off), C, nf, P<uint64_t>(c->scan_tmp64),
-                     (uint64_t*)&st->rec_total, c->st);
-        launch_sync_compact(nf, C, P<uint64_t>(c->rec_off), P<uint32_t>(c->rec_act), P<uint64_t>(c->act_off), recs,
-                            P<gw_sync_record>(c->rec1), c->st);
-        prof_end(c, 48 * R);
-        if ((rc = read_stats(c))) return rc;
-        R = c->hstats->rec_total;
-        std::swap(c->rec0, c->rec1);
-        recs = P<gw_sync_record>(c->rec0);
-    }
-    // ---- per-gate grouping (stable, keeps (entity, watcher) order) -------
+    // ---- per-gate grouping (stable, keeps the entity order) -------------
     if (R && G > 2) {
         prof_begin(c, "sync_gates");
         if ((rc = ensure(c, c->gate_hist, (size_t)65536 * 4))) return rc;
@@ -862,7 +806,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     out->bytes_alg = 24ull * R;
     if (c->prof) {
         prof_set_bytes(c, s_count, NF * 32);
-        prof_set_bytes(c, s_write, 4ull * R + 24ull * R + NF * 24);
+        prof_set_bytes(c, s_write, 24ull * R + NF * 32);
         prof_collect(c);
     }
     if (flags & GW_SYNC_COPY_TO_HOST) {
@@ -878,47 +822,40 @@ int gw_neighbors(gw_ctx* c, uint32_t slot, uint32_t* buf, uint32_t cap, uint32_t
     if (!c || !n) return GW_EINVAL;
     (void)hipSetDevice(c->dev);
     if (slot >= c->total_slots) return set_err(c, GW_ERANGE, "slot %u out of range", slot);
-    LstMeta L{};
-    uint32_t lc = 0;
-    HIPCHK(hipMemcpyAsync(&L, c->lst + slot, sizeof L, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipMemcpyAsync(&lc, c->log_cnt + slot, 4, hipMemcpyDeviceToHost, c->st));
+    int rc;
+    if ((rc = rebuild_grid(c))) return rc;
+    const uint32_t qcap = c->total_slots;
+    if ((rc = ensure(c, c->qbuf, ((size_t)qcap + 1) * 4))) return rc;
+    uint32_t* q = P<uint32_t>(c->qbuf);
+    launch_neighbors(world(c), slot, q + 1, q, qcap, c->st);
+    HIPCHK(hipGetLastError());
+    uint32_t cnt = 0;
+    HIPCHK(hipMemcpyAsync(&cnt, q, 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
-    std::vector<uint32_t> base(L.cnt), lg(lc);
-    if (L.cnt)
-        HIPCHK(hipMemcpyAsync(base.data(), c->pool + ((uint64_t)L.cur << 4), (size_t)L.cnt * 4,
-                              hipMemcpyDeviceToHost, c->st));
-    if (lc) HIPCHK(hipMemcpyAsync(lg.data(), c->logs + (uint64_t)slot * LOGCAP, (size_t)lc * 4, hipMemcpyDeviceToHost, c->st));
+    std::vector<uint32_t> v(std::min(cnt, qcap));
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(v.data(), q + 1, v.size() * 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
-    if (lc) {   // net effect of the delta log: majority kind per target
-        std::sort(lg.begin(), lg.end());
-        std::vector<uint32_t> add, rem;
-        for (size_t i = 0; i < lg.size();) {
-            size_t j = i;
-            int ne = 0, nl = 0;
-            while (j < lg.size() && (lg[j] >> 1) == (lg[i] >> 1)) { if (lg[j] & 1) ++nl; else ++ne; ++j; }
-            if (ne > nl) add.push_back(lg[i] >> 1);
-            if (nl > ne) rem.push_back(lg[i] >> 1);
-            i = j;
-        }
-        std::vector<uint32_t> out;
-        out.reserve(base.size() + add.size());
-        size_t ia = 0;
-        for (uint32_t v : base) {
-            while (ia < add.size() && add[ia] < v) out.push_back(add[ia++]);
-            if (!std::binary_search(rem.begin(), rem.end(), v)) out.push_back(v);
-        }
-        while (ia < add.size()) out.push_back(add[ia++]);
-        base.swap(out);
-    }
-    *n = (uint32_t)base.size();
-    uint32_t k = std::min<uint32_t>((uint32_t)base.size(), cap);
-    if (buf && k) memcpy(buf, base.data(), (size_t)k * 4);
+    std::sort(v.begin(), v.end());
+    *n = cnt;
+    uint32_t k = std::min<uint32_t>((uint32_t)v.size(), cap);
+    if (buf && k) memcpy(buf, v.data(), (size_t)k * 4);
     return 0;
 }
 
 int gw_total_neighbors(gw_ctx* c, uint64_t* out) {
     if (!c || !out) return GW_EINVAL;
-    *out = c->h_total_entries;
+    (void)hipSetDevice(c->dev);
+    *out = 0;
+    if (!c->total_slots) return 0;
+    int rc;
+    if ((rc = rebuild_grid(c))) return rc;
+    HIPCHK(hipMemsetAsync(c->scal32, 0, 8, c->st));
+    launch_count_all(world(c), c->h_present, (unsigned long long*)c->scal32, c->st);
+    HIPCHK(hipGetLastError());
+    unsigned long long t = 0;
+    HIPCHK(hipMemcpyAsync(&t, c->scal32, 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    *out = t;
     return 0;
 }
 

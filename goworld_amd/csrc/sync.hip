@@ -1,0 +1,283 @@
+// sync.hip — gfx950 kernels of CollectEntitySyncInfos (Entity.go:1221-1267),
+// neighbour queries (InterestedIn / InterestedBy), client updates and the
+// primitive instantiations used by the host code.
+//
+// A flagged entity e's records are: its own client's (syncInfoFlag bit0 and e
+// has a client), then one per neighbour w with a client (bit1), neighbours in
+// grid order ((cell, slot): deterministic).  The neighbours are evaluated from
+// the current grid with the stamp-resolved relation (dev_common.hpp), so no
+// list is kept.  Count pass, scan, write pass; records land at their final
+// offsets, grouped by gate afterwards with a stable radix sort.
+#include "dev_common.hpp"
+
+namespace gw {
+
+// ---------------------------------------------------------------------------
+// neighbours of a present entity e from the current grid: calls f(k, w, gate)
+// per lane for every related w != e (k = lane's candidate index)
+template <typename F>
+__device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) {
+    const AoiEnt a = w.aoi[e];
+    if (!(a.meta & PRESENT_BIT)) return;
+    const SpaceP P = w.sp[a.meta & SPACE_MASK];
+    const float d = P.d;
+    const Win we = win_of(a.x, a.z, d);
+    const Rect r = search_rect(P, a.x, a.z);
+    const int ln = lane_id();
+    unsigned long long se = 0;
+    bool have_se = false;
+    for (int cz = r.z0; cz <= r.z1; ++cz) {
+        const uint32_t row = P.cell_base + (uint32_t)cz * (uint32_t)P.W;
+        const uint32_t g0 = w.gn_start[row + r.x0], g1 = w.gn_start[row + r.x1 + 1];
+        // four candidate loads in flight per lane before any is used
+        for (uint32_t base = g0; base < g1; base += 256) {
+            GEnt gg[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = base + 64u * u + ln;
+                if (k < g1) gg[u] = w.gn[k];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (base + 64u * u >= g1) break;             // wave-uniform
+                const uint32_t k = base + 64u * u + ln;
+                bool rel = false;
+                const GEnt g = gg[u];
+                if (k < g1 && g.slot != e) {
+                    const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
+                    rel = ia;
+                    if (ia != ib) {
+                        if (!have_se) { se = w.stamp[e]; have_se = true; }
+                        rel = resolve(ia, ib, se, w.stamp[g.slot]);
+                    }
+                }
+                f(rel, g.slot, g.meta & GATE_MASK);
+            }
+        }
+    }
+}
+
+// record count per flagged entity (one wave each)
+__global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __restrict__ flagged,
+                                                   const uint64_t* nf_dev, uint32_t nf_max, uint32_t* cnt,
+                                                   DevStats* st) {
+    const uint64_t nf = load_n(nf_max, nf_dev);
+    const uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
+    if (k >= nf) return;
+    const uint32_t e = flagged[k];
+    const uint32_t f = w.flags[e];
+    uint32_t r = 0;
+    if (w.aoi[e].meta & PRESENT_BIT) {
+        if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) r = 1;
+        if (f & GW_SIF_NEIGHBOR_CLIENTS) {
+            uint32_t n = 0;
+            wave_neighbors(w, e, [&](bool rel, uint32_t, uint32_t g) {
+                n += (uint32_t)popc64(wave_ballot(rel && g != 0));
+            });
+            r += n;
+        }
+    }
+    if (lane_id() == 0) cnt[k] = r;
+    (void)st;
+}
+void launch_sync_count(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
+                       uint32_t* cnt, DevStats* st, hipStream_t s) {
+    if (!nf_max) return;
+    hipLaunchKernelGGL(k_sync_count, dim3(nblk(nf_max, NWAVE)), dim3(NT), 0, s, w, flagged, nf_dev, nf_max, cnt,
+                       st);
+}
+
+// writes e's records at rec_off[k] and clears e's flags
+__global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __restrict__ flagged,
+                                                   const uint64_t* nf_dev, uint32_t nf_max,
+                                                   const uint64_t* __restrict__ rec_off, gw_sync_record* rec,
+                                                   uint64_t rec_cap) {
+    const uint64_t nf = load_n(nf_max, nf_dev);
+    const uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
+    if (k >= nf) return;
+    const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint32_t e = flagged[k];
+    const uint32_t f = w.flags[e];
+    if (w.aoi[e].meta & PRESENT_BIT) {
+        const float4 p = w.pos[e];
+        uint64_t at = rec_off[k];
+        if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
+            if (ln == 0 && at < rec_cap) {
+                gw_sync_record r;
+                r.watcher = e; r.entity = e; r.x = p.x; r.y = p.y; r.z = p.z; r.yaw = p.w;
+                rec[at] = r;
+            }
+            ++at;
+        }
+        if (f & GW_SIF_NEIGHBOR_CLIENTS) {
+            wave_neighbors(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
+                const bool take = rel && g != 0;
+                const uint64_t bt = wave_ballot(take);
+                if (take) {
+                    const uint64_t i = at + (uint64_t)popc64(bt & lt);
+                    gw_sync_record r;
+                    r.watcher = ws; r.entity = e; r.x = p.x; r.y = p.y; r.z = p.z; r.yaw = p.w;
+                    if (i < rec_cap) rec[i] = r;
+                }
+                at += (uint64_t)popc64(bt);
+            });
+        }
+    }
+    if (ln == 0) w.flags[e] = 0;
+}
+void launch_sync_write(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
+                       const uint64_t* rec_off, gw_sync_record* rec, uint64_t rec_cap, hipStream_t s) {
+    if (!nf_max) return;
+    hipLaunchKernelGGL(k_sync_write, dim3(nblk(nf_max, NWAVE)), dim3(NT), 0, s, w, flagged, nf_dev, nf_max, rec_off,
+                       rec, rec_cap);
+}
+
+__global__ void __launch_bounds__(NT) k_flag_mark(const uint32_t* __restrict__ flags, uint32_t cap, uint32_t* mark) {
+    uint32_t s = blockIdx.x * NT + threadIdx.x;
+    if (s < cap) mark[s] = flags[s] != 0;
+}
+void launch_flag_mark(const uint32_t* flags, uint32_t cap, uint32_t* mark, hipStream_t s) {
+    hipLaunchKernelGGL(k_flag_mark, dim3(nblk1(cap, NT)), dim3(NT), 0, s, flags, cap, mark);
+}
+__global__ void __launch_bounds__(NT) k_flag_compact(const uint32_t* __restrict__ mark, const uint64_t* __restrict__ pre,
+                                                     uint32_t cap, uint32_t* flagged) {
+    uint32_t s = blockIdx.x * NT + threadIdx.x;
+    if (s < cap && mark[s]) flagged[pre[s]] = s;
+}
+void launch_flag_compact(const uint32_t* mark, const uint64_t* pre, uint32_t cap, uint32_t* flagged, hipStream_t s) {
+    hipLaunchKernelGGL(k_flag_compact, dim3(nblk1(cap, NT)), dim3(NT), 0, s, mark, pre, cap, flagged);
+}
+
+// per-gate record histogram: LDS buckets for gates < 256, global atomics above
+__global__ void __launch_bounds__(NT) k_gate_hist(const gw_sync_record* __restrict__ rec, const uint64_t* n_dev,
+                                                  uint64_t n_max, const uint16_t* __restrict__ gate, uint32_t* hist) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    uint64_t n = load_n(n_max, n_dev);
+    for (uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x; r < n; r += (uint64_t)gridDim.x * NT) {
+        uint32_t g = gate[rec[r].watcher];
+        if (g < 256) atomicAdd(&h[g], 1u); else atomicAdd(&hist[g], 1u);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+void launch_gate_hist(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,
+                      uint32_t* hist, hipStream_t s) {
+    uint32_t nb = nblk1(n_max, NT * 16);
+    if (nb > 2048) nb = 2048;
+    hipLaunchKernelGGL(k_gate_hist, dim3(nb), dim3(NT), 0, s, rec, n_dev, n_max, gate, hist);
+}
+__global__ void __launch_bounds__(NT) k_gate_keys(const gw_sync_record* __restrict__ rec, const uint64_t* n_dev,
+                                                  uint64_t n_max, const uint16_t* __restrict__ gate, uint32_t* keys,
+                                                  uint32_t* vals) {
+    uint64_t n = load_n(n_max, n_dev);
+    uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (r >= n) return;
+    keys[r] = gate[rec[r].watcher];
+    vals[r] = (uint32_t)r;
+}
+void launch_gate_keys(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,
+                      uint32_t* keys, uint32_t* vals, hipStream_t s) {
+    if (!n_max) return;
+    hipLaunchKernelGGL(k_gate_keys, dim3(nblk(n_max, NT)), dim3(NT), 0, s, rec, n_dev, n_max, gate, keys, vals);
+}
+__global__ void __launch_bounds__(NT) k_gather_records(const gw_sync_record* __restrict__ in,
+                                                       const uint32_t* __restrict__ idx, const uint64_t* n_dev,
+                                                       uint64_t n_max, gw_sync_record* out) {
+    uint64_t n = load_n(n_max, n_dev);
+    uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (r < n) out[r] = in[idx[r]];
+}
+void launch_gather_records(const gw_sync_record* in, const uint32_t* idx, const uint64_t* n_dev, uint64_t n_max,
+                           gw_sync_record* out, hipStream_t s) {
+    if (!n_max) return;
+    hipLaunchKernelGGL(k_gather_records, dim3(nblk(n_max, NT)), dim3(NT), 0, s, in, idx, n_dev, n_max, out);
+}
+
+// ---------------------------------------------------------------------------
+// client attach / detach (GameClient.go:14-27): the gate copy in the grid entry
+// is patched too, so a collect after set_clients sees the new gates
+__global__ void __launch_bounds__(NT) k_set_clients(World w, const uint32_t* slots, const uint16_t* gates,
+                                                    uint32_t n) {
+    uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i >= n || slots[i] >= w.cap) return;
+    const uint32_t s = slots[i];
+    w.gate[s] = gates[i];
+    if (w.aoi[s].meta & PRESENT_BIT) {
+        GEnt* g = w.gn + w.gidx[s];
+        if (g->slot == s) g->meta = (g->meta & ~GATE_MASK) | gates[i];
+    }
+}
+void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_set_clients, dim3(nblk(n, NT)), dim3(NT), 0, s, w, slots, gates, n);
+}
+
+// InterestedIn(slot) (== InterestedBy): related slots, unordered
+__global__ void __launch_bounds__(64) k_neighbors(World w, uint32_t slot, uint32_t* out, uint32_t* n_out,
+                                                  uint32_t cap) {
+    const uint64_t lt = lanemask_lt();
+    uint32_t n = 0;
+    wave_neighbors(w, slot, [&](bool rel, uint32_t ws, uint32_t) {
+        const uint64_t bt = wave_ballot(rel);
+        const uint32_t i = n + (uint32_t)popc64(bt & lt);
+        if (rel && i < cap) out[i] = ws;
+        n += (uint32_t)popc64(bt);
+    });
+    if (lane_id() == 0) *n_out = n;
+}
+void launch_neighbors(const World& w, uint32_t slot, uint32_t* out, uint32_t* n_out, uint32_t cap, hipStream_t s) {
+    hipLaunchKernelGGL(k_neighbors, dim3(1), dim3(64), 0, s, w, slot, out, n_out, cap);
+}
+
+// sum of |InterestedIn| over all present entities (one wave per entity)
+__global__ void __launch_bounds__(NT) k_count_all(World w, uint64_t np, unsigned long long* total) {
+    const uint64_t i = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
+    if (i >= np) return;
+    uint32_t n = 0;
+    wave_neighbors(w, w.gn[i].slot, [&](bool rel, uint32_t, uint32_t) { n += (uint32_t)popc64(wave_ballot(rel)); });
+    if (lane_id() == 0 && n) atomicAdd(total, (unsigned long long)n);
+}
+void launch_count_all(const World& w, uint64_t n_present, unsigned long long* total, hipStream_t s) {
+    if (n_present) hipLaunchKernelGGL(k_count_all, dim3(nblk(n_present, NWAVE)), dim3(NT), 0, s, w, n_present, total);
+}
+
+__global__ void k_fill_u32(uint32_t* p, uint32_t v, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+__global__ void k_fill_i32(int32_t* p, int32_t v, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+void launch_fill_u32(uint32_t* p, uint32_t v, uint64_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_fill_u32, dim3(nblk(n, NT)), dim3(NT), 0, s, p, v, n);
+}
+void launch_fill_i32(int32_t* p, int32_t v, uint64_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_fill_i32, dim3(nblk(n, NT)), dim3(NT), 0, s, p, v, n);
+}
+
+// ---------------------------------------------------------------------------
+// primitive instantiations for the host code
+uint64_t radix_tile() { return RS_TILE; }
+uint64_t scan_tile() { return SCAN_TILE; }
+void scan_u32_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint64_t* n_dev, uint32_t* tmp,
+                  uint32_t* total, hipStream_t s) {
+    scan_exclusive<uint32_t, uint32_t>(in, out, n_max, n_dev, tmp, total, s);
+}
+void scan_u32_u64(const uint32_t* in, uint64_t* out, uint64_t n_max, const uint64_t* n_dev, uint64_t* tmp,
+                  uint64_t* total, hipStream_t s) {
+    scan_exclusive<uint32_t, uint64_t>(in, out, n_max, n_dev, tmp, total, s);
+}
+void scan_u64_u64(const uint64_t* in, uint64_t* out, uint64_t n_max, const uint64_t* n_dev, uint64_t* tmp,
+                  uint64_t* total, hipStream_t s) {
+    scan_exclusive<uint64_t, uint64_t>(in, out, n_max, n_dev, tmp, total, s);
+}
+int sort_u32_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
+                 int lo_bit, int hi_bit, const RadixTmp& tmp, hipStream_t s) {
+    return radix_sort<uint32_t>(k0, v0, k1, v1, n_max, n_dev, lo_bit, hi_bit, tmp, s);
+}
+
+}  // namespace gw

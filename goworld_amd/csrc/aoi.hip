@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(NT) k_gm_scatter(TickBufs b) {
     const bool pn = (a.meta & PRESENT_BIT) != 0;
     e.x = pn ? a.x : qnan(); e.z = pn ? a.z : qnan();
     e.ox = p.ox; e.oz = p.oz;
-    e.slot = A; e.pad0 = 0; e.pad1 = 0;
+    e.slot = A; e.gate = b.w.gate[A]; e.pad1 = 0;
     if (co != 0xffffffffu) {
         e.tags = TAG_OLD | (cn == co ? TAG_NEW : 0u);
         b.gm[atomicAdd(&b.gm_cnt[co], 1u)] = e;
@@ -208,13 +208,9 @@ __global__ void __launch_bounds__(NT) k_gm_scatter(TickBufs b) {
 // The cells a mover scans: the rectangles of its old and new windows, merged
 // into their bounding box when they touch (visiting extra cells is harmless:
 // every candidate is evaluated exactly, each cell once).
-struct MoverRects {
-    Rect r[2];
-    int n;
-};
-__device__ __forceinline__ MoverRects mover_rects(const SpaceP& P, bool po, float ox, float oz, bool pn, float x,
-                                                  float z) {
-    MoverRects m;
+__device__ __forceinline__ Rects mover_rects(const SpaceP& P, bool po, float ox, float oz, bool pn, float x,
+                                             float z) {
+    Rects m;
     m.n = 0;
     Rect ro = po ? search_rect(P, ox, oz) : empty_rect();
     Rect rn = pn ? search_rect(P, x, z) : empty_rect();
@@ -246,7 +242,7 @@ __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
     const AoiEnt a = b.w.aoi[A];
     const PrevEnt p = b.w.prev[A];
     const SpaceP P = b.w.sp[a.meta & SPACE_MASK];
-    const MoverRects R = mover_rects(P, p.ox == p.ox, p.ox, p.oz, (a.meta & PRESENT_BIT) != 0, a.x, a.z);
+    const Rects R = mover_rects(P, p.ox == p.ox, p.ox, p.oz, (a.meta & PRESENT_BIT) != 0, a.x, a.z);
     uint64_t c = 0;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -291,9 +287,20 @@ void tick_movers(const TickBufs& b, uint64_t* scan_tmp64, uint32_t* scan_tmp32, 
 // r_old != r_new is an own event (A,B).  Non-movers come from gn (old = new
 // position), movers from the mover grid, where B's entry at its old cell
 // stands for the pair when r_old holds and its entry at the new cell when only
-// r_new does, so each pair is taken once.  Events (B<<1 | leave) go to A's
-// region and are sorted there: registers up to 64, LDS up to SORT_LDS, else a
-// block sort later.
+// r_new does, so each pair is taken once.  The row ranges of both grids are
+// walked flattened (Flat), DIFF_U chunks of 64 candidates with their loads in
+// flight together.  Events (B<<1 | leave) go to A's region and are sorted
+// there: registers up to 64, LDS up to SORT_LDS, else a block sort later.
+// The count of new neighbours with a client is kept for the next collect.
+constexpr int DIFF_U = 2;
+
+struct Cand {
+    float x, z, ox, oz;
+    uint32_t slot;
+    uint32_t info;       // tags | gate << 8 | CAND_NONMOVER
+};
+constexpr uint32_t CAND_NONMOVER = 1u << 31;
+
 __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * SORT_LDS];
     const uint64_t nm = b.st->n_movers;
@@ -311,98 +318,82 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
     const float nx = pn ? a.x : qnan(), nz = pn ? a.z : qnan();
     const unsigned long long sA = w.stamp[A], soA = p.ostamp;
     const Win wo = win_of(p.ox, p.oz, d), wn = win_of(nx, nz, d);
-    const MoverRects R = mover_rects(P, po, p.ox, p.oz, pn, nx, nz);
+    const Rects R = mover_rects(P, po, p.ox, p.oz, pn, nx, nz);
     uint32_t* out = b.own + b.reg[m];
     uint64_t* mir = b.mir + b.reg[m];
     uint32_t* mrk = b.mir_rank + b.reg[m];
     const uint64_t cap = b.cand[m];
     uint32_t n = 0, nl = 0, nm_ = 0;
-    uint32_t c_old = 0, c_new = 0, c_band = 0;
-    uint64_t tested = 0;
-    for (int q = 0; q < 2; ++q) {
-        if (q >= R.n) break;
-        const Rect rr = q == 0 ? R.r[0] : R.r[1];
-        for (int cz = rr.z0; cz <= rr.z1; ++cz) {
-            const uint32_t row = P.cell_base + (uint32_t)cz * (uint32_t)P.W;
-            // non-movers of the current grid
-            const uint32_t g0 = w.gn_start[row + rr.x0], g1 = w.gn_start[row + rr.x1 + 1];
-            tested += g1 - g0;
-            for (uint32_t base = g0; base < g1; base += 256) {
-                GEnt gg[4];
+    uint32_t c_old = 0, c_new = 0, c_band = 0, c_cli = 0;
+    Flat f = flat_build<2>(P, R, w.gn_start, b.gm_start);
+    const uint32_t tested = f.total;
+    for (uint32_t base = 0; base < f.total; base += 64u * DIFF_U) {
+        uint32_t idx[DIFF_U], kd[DIFF_U];
+        flat_map<DIFF_U, 2>(f, base, idx, kd);
+        Cand cc[DIFF_U];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const uint32_t k = base + 64u * u + ln;
-                    if (k < g1) gg[u] = w.gn[k];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (base + 64u * u >= g1) break;         // wave-uniform
-                    const uint32_t k = base + 64u * u + ln;
-                    bool ev = false, lv = false;
-                    uint32_t key = 0;
-                    const GEnt e = gg[u];
-                    if (k < g1 && !(e.meta & MOVER_BIT)) {
-                        const bool iao = wo.has(e.x, e.z), ibo = in_win(e.x, e.z, d, p.ox, p.oz);
-                        const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, nx, nz);
-                        bool ro = iao, rn = ian;
-                        if (iao != ibo || ian != ibn) {
-                            const unsigned long long sb = w.stamp[e.slot];
-                            if (iao != ibo) { ro = resolve(iao, ibo, soA, sb); ++c_band; }
-                            if (ian != ibn) { rn = resolve(ian, ibn, sA, sb); ++c_band; }
-                        }
-                        c_old += ro; c_new += rn;
-                        ev = ro != rn;
-                        lv = ro;
-                        key = (e.slot << 1) | (lv ? 1u : 0u);
-                    }
-                    // B has no op: (B,A) is B's event too; its rank in B's segment
-                    uint32_t rank = 0;
-                    if (ev) {
-                        const unsigned long long o = atomicAdd(&b.cnt64[e.slot], lv ? (1ull << 32) : 1ull);
-                        rank = lv ? (uint32_t)hi32(o) : (uint32_t)lo32(o);
-                    }
-                    const uint64_t be = wave_ballot(ev), bl = wave_ballot(ev && lv);
-                    const uint32_t pre = (uint32_t)popc64(be & lt);
-                    if (ev && n + pre < cap) out[n + pre] = key;
-                    if (ev && nm_ + pre < cap) {
-                        mir[nm_ + pre] = ((uint64_t)e.slot << 32) | (A << 1) | (lv ? 1u : 0u);
-                        mrk[nm_ + pre] = rank;
-                    }
-                    n += (uint32_t)popc64(be);
-                    nl += (uint32_t)popc64(bl);
-                    nm_ += (uint32_t)popc64(be);
+        for (int u = 0; u < DIFF_U; ++u) {
+            cc[u].info = 0;
+            cc[u].slot = A;                                    // invalid unless loaded below
+            if (idx[u] != ~0u) {
+                if (kd[u] == 0) {
+                    const GEnt e = w.gn[idx[u]];
+                    cc[u].x = cc[u].ox = e.x;
+                    cc[u].z = cc[u].oz = e.z;
+                    cc[u].slot = (e.meta & MOVER_BIT) ? A : e.slot;   // movers come from gm
+                    cc[u].info = TAG_OLD | TAG_NEW | ((e.meta & GATE_MASK) << 8) | CAND_NONMOVER;
+                } else {
+                    const MEnt e = b.gm[idx[u]];
+                    cc[u].x = e.x; cc[u].z = e.z; cc[u].ox = e.ox; cc[u].oz = e.oz;
+                    cc[u].slot = e.slot;
+                    cc[u].info = e.tags | (e.gate << 8);
                 }
             }
-            // movers of the mover grid
-            const uint32_t m0 = b.gm_start[row + rr.x0], m1 = b.gm_start[row + rr.x1 + 1];
-            tested += m1 - m0;
-            for (uint32_t base = m0; base < m1; base += 64) {
-                const uint32_t k = base + ln;
-                bool ev = false, lv = false;
-                uint32_t key = 0;
-                if (k < m1) {
-                    const MEnt e = b.gm[k];
-                    if (e.slot != A) {
-                        const bool iao = wo.has(e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, p.ox, p.oz);
-                        const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, nx, nz);
-                        bool ro = iao, rn = ian;
-                        if (iao != ibo) { ro = resolve(iao, ibo, soA, w.prev[e.slot].ostamp); ++c_band; }
-                        if (ian != ibn) { rn = resolve(ian, ibn, sA, w.stamp[e.slot]); ++c_band; }
-                        const bool take = ((e.tags & TAG_OLD) && ro) || ((e.tags & TAG_NEW) && rn && !ro);
-                        if (take) {
-                            c_old += ro; c_new += rn;
-                            ev = ro != rn;
-                            lv = ro;
-                            key = (e.slot << 1) | (lv ? 1u : 0u);
-                        }
-                    }
+        }
+#pragma unroll
+        for (int u = 0; u < DIFF_U; ++u) {
+            if (base + 64u * u >= f.total) break;              // wave-uniform
+            const Cand& e = cc[u];
+            bool ev = false, lv = false, nmv = false;
+            uint32_t key = 0;
+            if (e.slot != A) {
+                nmv = (e.info & CAND_NONMOVER) != 0;
+                const bool iao = wo.has(e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, p.ox, p.oz);
+                const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, nx, nz);
+                bool ro = iao, rn = ian;
+                if (iao != ibo || ian != ibn) {
+                    const unsigned long long sb = w.stamp[e.slot];
+                    const unsigned long long sbo = nmv ? sb : w.prev[e.slot].ostamp;
+                    if (iao != ibo) { ro = resolve(iao, ibo, soA, sbo); ++c_band; }
+                    if (ian != ibn) { rn = resolve(ian, ibn, sA, sb); ++c_band; }
                 }
-                const uint64_t be = wave_ballot(ev), bl = wave_ballot(ev && lv);
-                const uint32_t at = n + (uint32_t)popc64(be & lt);
-                if (ev && at < cap) out[at] = key;
-                n += (uint32_t)popc64(be);
-                nl += (uint32_t)popc64(bl);
+                const bool take = ((e.info & TAG_OLD) && ro) || ((e.info & TAG_NEW) && rn && !ro);
+                if (take) {
+                    c_old += ro; c_new += rn;
+                    c_cli += rn && (e.info & (GATE_MASK << 8)) != 0;
+                    ev = ro != rn;
+                    lv = ro;
+                    key = (e.slot << 1) | (lv ? 1u : 0u);
+                }
             }
+            const bool mev = ev && nmv;
+            // B has no op: (B,A) is B's event too; its rank in B's segment
+            uint32_t rank = 0;
+            if (mev) {
+                const unsigned long long o = atomicAdd(&b.cnt64[e.slot], lv ? (1ull << 32) : 1ull);
+                rank = lv ? (uint32_t)hi32(o) : (uint32_t)lo32(o);
+            }
+            const uint64_t be = wave_ballot(ev), bl = wave_ballot(ev && lv), bm = wave_ballot(mev);
+            const uint32_t at = n + (uint32_t)popc64(be & lt);
+            if (ev && at < cap) out[at] = key;
+            const uint32_t atm = nm_ + (uint32_t)popc64(bm & lt);
+            if (mev && atm < cap) {
+                mir[atm] = ((uint64_t)e.slot << 32) | (A << 1) | (lv ? 1u : 0u);
+                mrk[atm] = rank;
+            }
+            n += (uint32_t)popc64(be);
+            nl += (uint32_t)popc64(bl);
+            nm_ += (uint32_t)popc64(bm);
         }
     }
     // sort the own events by (target, kind)
@@ -423,13 +414,13 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
             b.big[atomicAdd(&b.st->n_big, 1ull)] = (uint32_t)m;
         }
     }
+    const uint32_t so = wave_sum<uint32_t>(c_old), sn = wave_sum<uint32_t>(c_new), sb = wave_sum<uint32_t>(c_band);
+    const uint32_t scl = wave_sum<uint32_t>(c_cli);
     if (ln == 0) {
         if (n) b.cnt64[A] = (unsigned long long)(n - nl) | ((unsigned long long)nl << 32);
         b.mir_cnt[m] = nm_;
+        if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | scl;
         shard_add(b.st, A, SH_PAIRS, tested);
-    }
-    const uint32_t so = wave_sum<uint32_t>(c_old), sn = wave_sum<uint32_t>(c_new), sb = wave_sum<uint32_t>(c_band);
-    if (ln == 0) {
         shard_add(b.st, A, SH_AOLD, so);
         shard_add(b.st, A, SH_ANEW, sn);
         shard_add(b.st, A, SH_BAND, sb);

@@ -63,6 +63,8 @@ struct gw_ctx {
     uint32_t total_slots = 0, slot_cap = 0, total_cells = 0;
     uint16_t max_gate = 0;
     unsigned long long stamp_base = 1;   // global op counter (stamp 0 = never)
+    uint32_t epoch = 1;                  // bumped by every tick and client change (World.nbc)
+    int cells_per_d = 2;                 // grid cells per AOI distance (GW_CELLS_PER_D)
     bool grid_dirty = true;              // gn/gn_start must be rebuilt before queries
     uint64_t h_present = 0;
 
@@ -74,6 +76,7 @@ struct gw_ctx {
     uint32_t* flags = nullptr;
     uint16_t* gate = nullptr;
     unsigned long long* cnt64 = nullptr;     // [slot_cap + 1], zero between ticks
+    unsigned long long* nbc = nullptr;       // [slot_cap] epoch<<32 | neighbours with a client
     int32_t *last_pos = nullptr, *last_aoi = nullptr, *last_leave = nullptr;
     GEnt* gn = nullptr;
     uint32_t* gidx = nullptr;
@@ -268,6 +271,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->flags, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->gate, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->cnt64, oc ? oc + 1 : 0, (size_t)nc + 1))) return rc;
+    if ((rc = grow_preserve(c, c->nbc, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_pos, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_aoi, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_leave, oc, nc))) return rc;
@@ -281,6 +285,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     HIPCHK(hipMemsetAsync(c->flags + oc, 0, n * 4, c->st));
     HIPCHK(hipMemsetAsync(c->gate + oc, 0, n * 2, c->st));
     HIPCHK(hipMemsetAsync(c->cnt64 + oc, 0, (n + 1) * 8, c->st));
+    HIPCHK(hipMemsetAsync(c->nbc + oc, 0, n * 8, c->st));
     launch_fill_i32(c->last_pos + oc, -1, n, c->st);
     launch_fill_i32(c->last_aoi + oc, -1, n, c->st);
     launch_fill_i32(c->last_leave + oc, -1, n, c->st);
@@ -332,6 +337,8 @@ World world(gw_ctx* c) {
     w.sp = c->sp_dev;
     w.aoi = c->aoi; w.prev = c->prev; w.stamp = c->stamp; w.pos = c->pos; w.flags = c->flags; w.gate = c->gate;
     w.gn = c->gn; w.gn_start = P<uint32_t>(c->gn_start); w.gidx = c->gidx;
+    w.nbc = c->nbc;
+    w.epoch = c->epoch;
     return w;
 }
 
@@ -434,6 +441,7 @@ int gw_init(int device_id, gw_ctx** out) {
         (void)hipMemset(c->stats, 0, sizeof(DevStats));
         (void)hipEventCreate(&c->ev_t0);
         (void)hipEventCreate(&c->ev_t1);
+        if (const char* e = getenv("GW_CELLS_PER_D")) c->cells_per_d = std::min(4, std::max(1, atoi(e)));
     } while (0);
     if (rc) {
         (void)hipGetLastError();
@@ -457,7 +465,7 @@ void gw_shutdown(gw_ctx* c) {
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
-    void* ps[] = {c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->last_pos, c->last_aoi,
+    void* ps[] = {c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->nbc, c->last_pos, c->last_aoi,
                   c->last_leave, c->gn, c->gidx, c->sp_dev, c->stats, c->scal32};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
@@ -481,9 +489,16 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
     if (!(b[2] > b[0]) || !(b[3] > b[1]) || !std::isfinite(b[0]) || !std::isfinite(b[1]) || !std::isfinite(b[2]) ||
         !std::isfinite(b[3]))
         return set_err(c, GW_EINVAL, "bad bounds");
-    // square cells of side >= d; at most 8192 cells per axis
+    // square cells of side >= d / cells_per_d; at most 8192 cells per axis; a
+    // search window (2d plus the rounding margin of dev_common.hpp
+    // search_rect) spans at most 11 rows, so a mover's two windows fit the
+    // 32 row ranges of one wave (Flat)
     double ex = (double)b[2] - b[0], ez = (double)b[3] - b[1];
-    double cs = std::max((double)aoi_dist, std::max(ex, ez) / 8192.0);
+    double maxabs = std::max(std::max(std::fabs((double)b[0]), std::fabs((double)b[2])),
+                             std::max(std::fabs((double)b[1]), std::fabs((double)b[3])));
+    double span = 2.0 * aoi_dist + 4e-6 * (maxabs + aoi_dist) + 1e-3;
+    double cs = std::max((double)aoi_dist / c->cells_per_d, std::max(ex, ez) / 8192.0);
+    cs = std::max(cs, span / 9.0);
     SpaceHost s{};
     s.d = aoi_dist;
     s.cap = capacity;
@@ -561,6 +576,7 @@ int gw_set_clients(gw_ctx* c, const uint32_t* slots, const uint16_t* gates, uint
     if ((rc = ensure(c, c->gv0, (size_t)n * 2))) return rc;
     HIPCHK(hipMemcpyAsync(c->gk0.p, slots, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemcpyAsync(c->gv0.p, gates, (size_t)n * 2, hipMemcpyHostToDevice, c->st));
+    ++c->epoch;   // neighbour-with-client counts cached by the last tick are stale
     launch_set_clients(world(c), P<uint32_t>(c->gk0), (const uint16_t*)c->gv0.p, n, c->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->st));
@@ -579,6 +595,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     const uint32_t C = c->total_slots;
     int rc;
     HIPCHK(hipEventRecord(c->ev_t0, c->st));
+    ++c->epoch;
     if (M == 0 || C == 0) {
         c->segs.clear();
         c->pend_host.clear();

@@ -51,6 +51,80 @@ __device__ __forceinline__ Rect search_rect(const SpaceP& P, float x, float z) {
 }
 __device__ __forceinline__ Rect empty_rect() { Rect r; r.x0 = 1; r.x1 = 0; r.z0 = 1; r.z1 = 0; return r; }
 
+// The cells a watcher scans: one or two rectangles (a mover's old and new
+// windows, merged into their bounding box when they touch).
+struct Rects {
+    Rect r[2];
+    int n;
+};
+
+// ---------------------------------------------------------------------------
+// Flattened candidate ranges of one wave.  A grid row of a rectangle is one
+// contiguous index range per grid (cells of a row are consecutive), so the
+// candidates of a watcher are <= 2 rects x 10 rows x NK grids ranges.  Lane j
+// holds range j (row j/NK, grid j%NK); the wave walks the concatenation in
+// 64-lane chunks, so a sparse window (a few entities per row) fills one chunk
+// instead of one mostly idle chunk per row.
+struct Flat {
+    uint32_t start, len, pre;   // per lane: range j = [start, start+len), exclusive prefix
+    uint64_t live;              // uniform: non-empty ranges not consumed yet
+    uint32_t total;             // uniform: candidates over all ranges
+};
+
+template <int NK>
+__device__ __forceinline__ Flat flat_build(const SpaceP& P, const Rects& R, const uint32_t* __restrict__ s0,
+                                           const uint32_t* __restrict__ s1) {
+    const int ln = lane_id();
+    const int row = NK == 2 ? (ln >> 1) : ln;
+    const int kind = NK == 2 ? (ln & 1) : 0;
+    const int nr0 = R.n > 0 ? R.r[0].z1 - R.r[0].z0 + 1 : 0;
+    const int nr1 = R.n > 1 ? R.r[1].z1 - R.r[1].z0 + 1 : 0;
+    uint32_t s = 0, l = 0;
+    if (row < nr0 + nr1) {
+        const bool first = row < nr0;
+        const int x0 = first ? R.r[0].x0 : R.r[1].x0;
+        const int x1 = first ? R.r[0].x1 : R.r[1].x1;
+        const int cz = first ? R.r[0].z0 + row : R.r[1].z0 + (row - nr0);
+        const uint32_t base = P.cell_base + (uint32_t)cz * (uint32_t)P.W;
+        const uint32_t* st = kind ? s1 : s0;
+        s = st[base + x0];
+        l = st[base + x1 + 1] - s;
+    }
+    Flat f;
+    const uint32_t inc = wave_incl_scan<uint32_t>(l);
+    f.start = s;
+    f.len = l;
+    f.pre = inc - l;
+    f.total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    f.live = wave_ballot(l != 0);
+    return f;
+}
+
+// Maps the lane's candidates k = B + 64u + lane (u < U) to (grid, index);
+// idx = ~0 past the end.  Ranges wholly before B + 64U are dropped from live.
+template <int U, int NK>
+__device__ __forceinline__ void flat_map(Flat& f, uint32_t B, uint32_t (&idx)[U], uint32_t (&kind)[U]) {
+    const int ln = lane_id();
+    const uint32_t end = B + 64u * U;
+#pragma unroll
+    for (int u = 0; u < U; ++u) { idx[u] = ~0u; kind[u] = 0; }
+    uint64_t m = f.live;
+    while (m) {
+        const int j = __builtin_ctzll(m);
+        const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)f.pre, j);
+        if (sp >= end) break;
+        const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)f.len, j);
+        const uint32_t ss = (uint32_t)__builtin_amdgcn_readlane((int)f.start, j);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t r = B + 64u * u + (uint32_t)ln - sp;
+            if (r < sl) { idx[u] = ss + r; kind[u] = NK == 2 ? (uint32_t)(j & 1) : 0u; }
+        }
+        if (sp + sl <= end) f.live &= ~(1ull << j);
+        m &= m - 1;
+    }
+}
+
 // A's rounded window, computed once per watcher
 struct Win {
     float lox, hix, loz, hiz;

@@ -48,7 +48,7 @@ constexpr uint32_t GATE_MASK = 0xffffu;
 // tags when the two cells agree.  Both positions travel with every entry.
 struct alignas(16) MEnt {
     float x, z, ox, oz;
-    uint32_t slot, tags, pad0, pad1;
+    uint32_t slot, tags, gate, pad1;
 };
 constexpr uint32_t TAG_OLD = 1u, TAG_NEW = 2u;
 
@@ -116,6 +116,11 @@ struct World {
     GEnt* gn;                  // [cap] current grid, n_present entries
     uint32_t* gn_start;        // [ncells+1]
     uint32_t* gidx;            // [cap] index of the slot in gn
+    // |{w related to e : w has a client}| as of the end of tick `epoch`
+    // (epoch<<32 | count), written for every present mover by the diff; a
+    // collect right after that tick takes it instead of walking e's window
+    unsigned long long* nbc;
+    uint32_t epoch;            // current epoch (bumped by every tick and client change)
 };
 
 // ---- tick buffers handed to the launchers ----------------------------------

@@ -13,8 +13,10 @@
 namespace gw {
 
 // ---------------------------------------------------------------------------
-// neighbours of a present entity e from the current grid: calls f(k, w, gate)
-// per lane for every related w != e (k = lane's candidate index)
+// neighbours of a present entity e from the current grid: calls
+// f(rel, w, gate) per lane for every candidate (rel: w != e is related to e).
+// The window's row ranges are walked flattened, NB_U chunks of 64 in flight.
+constexpr int NB_U = 4;
 template <typename F>
 __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) {
     const AoiEnt a = w.aoi[e];
@@ -22,37 +24,35 @@ __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) 
     const SpaceP P = w.sp[a.meta & SPACE_MASK];
     const float d = P.d;
     const Win we = win_of(a.x, a.z, d);
-    const Rect r = search_rect(P, a.x, a.z);
-    const int ln = lane_id();
+    Rects R;
+    R.n = 1;
+    R.r[0] = search_rect(P, a.x, a.z);
+    Flat fl = flat_build<1>(P, R, w.gn_start, nullptr);
     unsigned long long se = 0;
     bool have_se = false;
-    for (int cz = r.z0; cz <= r.z1; ++cz) {
-        const uint32_t row = P.cell_base + (uint32_t)cz * (uint32_t)P.W;
-        const uint32_t g0 = w.gn_start[row + r.x0], g1 = w.gn_start[row + r.x1 + 1];
-        // four candidate loads in flight per lane before any is used
-        for (uint32_t base = g0; base < g1; base += 256) {
-            GEnt gg[4];
+    for (uint32_t base = 0; base < fl.total; base += 64u * NB_U) {
+        uint32_t idx[NB_U], kd[NB_U];
+        flat_map<NB_U, 1>(fl, base, idx, kd);
+        GEnt gg[NB_U];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t k = base + 64u * u + ln;
-                if (k < g1) gg[u] = w.gn[k];
-            }
+        for (int u = 0; u < NB_U; ++u) {
+            gg[u].slot = e;
+            if (idx[u] != ~0u) gg[u] = w.gn[idx[u]];
+        }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (base + 64u * u >= g1) break;             // wave-uniform
-                const uint32_t k = base + 64u * u + ln;
-                bool rel = false;
-                const GEnt g = gg[u];
-                if (k < g1 && g.slot != e) {
-                    const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
-                    rel = ia;
-                    if (ia != ib) {
-                        if (!have_se) { se = w.stamp[e]; have_se = true; }
-                        rel = resolve(ia, ib, se, w.stamp[g.slot]);
-                    }
+        for (int u = 0; u < NB_U; ++u) {
+            if (base + 64u * u >= fl.total) break;            // wave-uniform
+            bool rel = false;
+            const GEnt g = gg[u];
+            if (g.slot != e) {
+                const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
+                rel = ia;
+                if (ia != ib) {
+                    if (!have_se) { se = w.stamp[e]; have_se = true; }
+                    rel = resolve(ia, ib, se, w.stamp[g.slot]);
                 }
-                f(rel, g.slot, g.meta & GATE_MASK);
             }
+            f(rel, g.slot, g.meta & GATE_MASK);
         }
     }
 }
@@ -70,11 +70,16 @@ __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __re
     if (w.aoi[e].meta & PRESENT_BIT) {
         if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) r = 1;
         if (f & GW_SIF_NEIGHBOR_CLIENTS) {
-            uint32_t n = 0;
-            wave_neighbors(w, e, [&](bool rel, uint32_t, uint32_t g) {
-                n += (uint32_t)popc64(wave_ballot(rel && g != 0));
-            });
-            r += n;
+            const unsigned long long c = w.nbc[e];
+            if ((uint32_t)(c >> 32) == w.epoch) {
+                r += (uint32_t)c;                            // counted by this tick's diff
+            } else {
+                uint32_t n = 0;
+                wave_neighbors(w, e, [&](bool rel, uint32_t, uint32_t g) {
+                    n += (uint32_t)popc64(wave_ballot(rel && g != 0));
+                });
+                r += n;
+            }
         }
     }
     if (lane_id() == 0) cnt[k] = r;

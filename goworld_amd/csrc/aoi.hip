@@ -130,8 +130,7 @@ __global__ void __launch_bounds__(NT) k_grid_starts(World w, const uint32_t* __r
     if (c == w.ncells && st) st->n_present = lo;
 }
 
-int tick_grid(const TickBufs& b, const RadixTmp& rt, int key_bits, uint32_t* scan_tmp32, hipStream_t s) {
-    (void)scan_tmp32;
+int tick_grid(const TickBufs& b, RadixTmp& rt, int key_bits, hipStream_t s) {
     const uint32_t C = b.w.cap;
     hipLaunchKernelGGL(k_grid_keys, dim3(nblk1(C, NT)), dim3(NT), 0, s, b);
     int r = radix_sort<uint32_t>(b.k0, b.v0, b.k1, b.v1, C, nullptr, 0, key_bits, rt, s);
@@ -257,14 +256,14 @@ __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
     b.cand[m] = c;
 }
 
-void tick_movers(const TickBufs& b, uint64_t* scan_tmp64, uint32_t* scan_tmp32, hipStream_t s) {
+void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint32_t C = b.w.cap, NC = b.w.ncells;
-    scan_exclusive<uint32_t, uint64_t>(b.pflag, b.pre, C, (const uint64_t*)&b.st->n_present, scan_tmp64,
+    scan_exclusive<uint32_t, uint64_t>(b.pflag, b.pre, C, (const uint64_t*)&b.st->n_present, sc,
                                        (uint64_t*)&b.st->movers_present, s);
     hipLaunchKernelGGL(k_compact_grid_movers, dim3(nblk1(C, NT)), dim3(NT), 0, s, b);
     if (b.m) {
         hipLaunchKernelGGL(k_leaver_flags, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
-        scan_exclusive<uint32_t, uint64_t>(b.pflag, b.pre, b.m, nullptr, scan_tmp64, (uint64_t*)&b.st->leavers, s);
+        scan_exclusive<uint32_t, uint64_t>(b.pflag, b.pre, b.m, nullptr, sc, (uint64_t*)&b.st->leavers, s);
         hipLaunchKernelGGL(k_compact_leavers, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
     } else {
         hipLaunchKernelGGL(k_set_nmov, dim3(1), dim3(1), 0, s, b.st);
@@ -272,12 +271,12 @@ void tick_movers(const TickBufs& b, uint64_t* scan_tmp64, uint32_t* scan_tmp32, 
     const uint64_t* nm = (const uint64_t*)&b.st->n_movers;
     (void)hipMemsetAsync(b.gm_cnt, 0, ((size_t)NC + 1) * 4, s);
     if (b.m) hipLaunchKernelGGL(k_gm_count, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
-    scan_exclusive<uint32_t, uint32_t>(b.gm_cnt, b.gm_start, (uint64_t)NC + 1, nullptr, scan_tmp32, nullptr, s);
+    scan_exclusive<uint32_t, uint32_t>(b.gm_cnt, b.gm_start, (uint64_t)NC + 1, nullptr, sc, (uint32_t*)nullptr, s);
     (void)hipMemcpyAsync(b.gm_cnt, b.gm_start, ((size_t)NC + 1) * 4, hipMemcpyDeviceToDevice, s);
     if (b.m) {
         hipLaunchKernelGGL(k_gm_scatter, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
         hipLaunchKernelGGL(k_bounds, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
-        scan_exclusive<uint64_t, uint64_t>(b.cand, b.reg, b.m, nm, scan_tmp64, (uint64_t*)&b.st->cand_total, s);
+        scan_exclusive<uint64_t, uint64_t>(b.cand, b.reg, b.m, nm, sc, (uint64_t*)&b.st->cand_total, s);
     }
 }
 
@@ -518,9 +517,9 @@ __global__ void __launch_bounds__(NT) k_seg_fix(TickBufs b) {
 
 __global__ void k_n_big_mark(DevStats* st) { st->scratch = st->n_big; }
 
-void tick_events(const TickBufs& b, uint64_t n_movers, uint64_t* scan_tmp64, hipStream_t s) {
+void tick_events(const TickBufs& b, uint64_t n_movers, ScanCtx& sc, hipStream_t s) {
     const uint32_t C = b.w.cap;
-    scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.cnt64, b.off64, (uint64_t)C + 1, nullptr, scan_tmp64,
+    scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.cnt64, b.off64, (uint64_t)C + 1, nullptr, sc,
                                        (uint64_t*)&b.st->ev_pk, s);
     if (n_movers) hipLaunchKernelGGL(k_own_copy, dim3(nblk(n_movers, NWAVE)), dim3(NT), 0, s, b);
     // big-own entries sit in b.big[0, n_big); op-less ones are appended after

@@ -89,7 +89,8 @@ struct gw_ctx {
     // grid + tick scratch
     DevBuf gn_start, ops_buf, k0, v0, k1, v1, pflag, pre, movers, gm_cnt, gm_start, gm, cand, reg, own, big;
     DevBuf mir, mir_rank, mir_cnt;
-    DevBuf off64, enter_d, leave_d, scan_tmp64, scan_tmp32, rs_hist, rs_scan_tmp;
+    DevBuf off64, enter_d, leave_d, scan_status, rs_hist;
+    ScanCtx sc{};                  // single-pass scan state (prim.hpp)
     // sync / query scratch
     DevBuf flag_mark, flag_pre, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
     uint32_t* scal32 = nullptr;    // small device scalars
@@ -238,24 +239,30 @@ void prof_collect(gw_ctx* c) {
     }
 }
 
+// status words for scans of up to n elements (zeroed when reallocated: zero
+// never matches a tag)
+int ensure_scan(gw_ctx* c, uint64_t n) {
+    const uint64_t tiles = (n + scan_tile() - 1) / scan_tile() + 2;
+    const uint64_t bytes = tiles * scan_words() * 8;
+    if (c->scan_status.cap >= bytes) return 0;
+    int rc;
+    if ((rc = ensure(c, c->scan_status, bytes))) return rc;
+    HIPCHK(hipMemsetAsync(c->scan_status.p, 0, c->scan_status.cap, c->st));
+    c->sc.status = P<unsigned long long>(c->scan_status);
+    c->sc.max_tiles = c->scan_status.cap / (scan_words() * 8);
+    return 0;
+}
+
 int radix_tmp(gw_ctx* c, uint64_t n_max, RadixTmp& rt) {
     uint64_t nb = (n_max + radix_tile() - 1) / radix_tile();
     if (!nb) nb = 1;
     uint64_t hn = 256 * nb;
     int rc;
     if ((rc = ensure(c, c->rs_hist, hn * 4))) return rc;
-    if ((rc = ensure(c, c->rs_scan_tmp, ((hn + scan_tile() - 1) / scan_tile() + 2) * 4))) return rc;
+    if ((rc = ensure_scan(c, hn))) return rc;
     rt.hist = P<uint32_t>(c->rs_hist);
-    rt.scan_tmp = P<uint32_t>(c->rs_scan_tmp);
-    rt.scan_total = c->scal32;
+    rt.sc = &c->sc;
     return 0;
-}
-
-int ensure_scan64(gw_ctx* c, uint64_t n) {
-    return ensure(c, c->scan_tmp64, ((n + scan_tile() - 1) / scan_tile() + 2) * 8);
-}
-int ensure_scan32(gw_ctx* c, uint64_t n) {
-    return ensure(c, c->scan_tmp32, ((n + scan_tile() - 1) / scan_tile() + 2) * 4);
 }
 
 // grow slot-indexed state to hold new_total slots, initialising the new range
@@ -348,8 +355,7 @@ int ensure_grid_bufs(gw_ctx* c, uint64_t CM) {
     if ((rc = ensure(c, c->gn_start, ((size_t)NC + 2) * 4)) || (rc = ensure(c, c->k0, (size_t)C * 4)) ||
         (rc = ensure(c, c->v0, (size_t)C * 4)) || (rc = ensure(c, c->k1, (size_t)C * 4)) ||
         (rc = ensure(c, c->v1, (size_t)C * 4)) || (rc = ensure(c, c->pflag, CM * 4)) ||
-        (rc = ensure(c, c->pre, CM * 8)) || (rc = ensure_scan64(c, CM + 1)) ||
-        (rc = ensure_scan32(c, (uint64_t)NC + 1)))
+        (rc = ensure(c, c->pre, CM * 8)) || (rc = ensure_scan(c, std::max<uint64_t>(CM, NC) + 1)))
         return rc;
     return 0;
 }
@@ -369,7 +375,7 @@ int rebuild_grid(gw_ctx* c) {
     b.st = c->stats;
     b.k0 = P<uint32_t>(c->k0); b.v0 = P<uint32_t>(c->v0); b.k1 = P<uint32_t>(c->k1); b.v1 = P<uint32_t>(c->v1);
     b.pflag = nullptr;
-    if (C) tick_grid(b, rt, ceil_log2((uint64_t)c->total_cells + 1), P<uint32_t>(c->scan_tmp32), c->st);
+    if (C) tick_grid(b, rt, ceil_log2((uint64_t)c->total_cells + 1), c->st);
     else HIPCHK(hipMemsetAsync(c->gn_start.p, 0, ((size_t)c->total_cells + 1) * 4, c->st));
     HIPCHK(hipGetLastError());
     if ((rc = read_stats(c))) return rc;
@@ -437,6 +443,8 @@ int gw_init(int device_id, gw_ctx** out) {
         if (hipMalloc(&c->stats, sizeof(DevStats)) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "stats"); break; }
         if (hipHostMalloc((void**)&c->hstats, sizeof(DevStats), hipHostMallocDefault) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "hstats"); break; }
         if (hipMalloc(&c->scal32, 64) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "scal"); break; }
+        if (hipMalloc(&c->sc.ticket, 8) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "ticket"); break; }
+        (void)hipMemset(c->sc.ticket, 0, 8);
         memset(c->hstats, 0, sizeof(DevStats));
         (void)hipMemset(c->stats, 0, sizeof(DevStats));
         (void)hipEventCreate(&c->ev_t0);
@@ -459,13 +467,13 @@ void gw_shutdown(gw_ctx* c) {
     DevBuf* bufs[] = {&c->gn_start, &c->ops_buf, &c->k0, &c->v0, &c->k1, &c->v1, &c->pflag, &c->pre, &c->movers,
                       &c->gm_cnt, &c->gm_start, &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->off64, &c->mir,
                       &c->mir_rank, &c->mir_cnt,
-                      &c->enter_d, &c->leave_d, &c->scan_tmp64, &c->scan_tmp32, &c->rs_hist, &c->rs_scan_tmp,
+                      &c->enter_d, &c->leave_d, &c->scan_status, &c->rs_hist,
                       &c->flag_mark, &c->flag_pre, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
                       &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf};
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
-    void* ps[] = {c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->nbc, c->last_pos, c->last_aoi,
+    void* ps[] = {c->sc.ticket, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->nbc, c->last_pos, c->last_aoi,
                   c->last_leave, c->gn, c->gidx, c->sp_dev, c->stats, c->scal32};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
@@ -645,15 +653,14 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.gm = P<MEnt>(c->gm); b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg); b.big = P<uint32_t>(c->big);
     b.cnt64 = c->cnt64; b.off64 = P<uint64_t>(c->off64);
 
-    uint64_t* stmp = P<uint64_t>(c->scan_tmp64);
     prof_begin(c, "ops");
     tick_ops(b, c->st);
     prof_end(c, (uint64_t)M * 24);
     prof_begin(c, "grid");
-    tick_grid(b, rt, ceil_log2((uint64_t)NC + 1), P<uint32_t>(c->scan_tmp32), c->st);
+    tick_grid(b, rt, ceil_log2((uint64_t)NC + 1), c->st);
     size_t s_grid = prof_end(c, 0);
     prof_begin(c, "movers");
-    tick_movers(b, stmp, P<uint32_t>(c->scan_tmp32), c->st);
+    tick_movers(b, c->sc, c->st);
     size_t s_movers = prof_end(c, 0);
     HIPCHK(hipGetLastError());
     // ---- the one mid-tick host sync ---------------------------------------
@@ -677,7 +684,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     tick_diff(b, n_mov, c->st);
     size_t s_diff = prof_end(c, 0);
     prof_begin(c, "events");
-    tick_events(b, n_mov, stmp, c->st);
+    tick_events(b, n_mov, c->sc, c->st);
     size_t s_events = prof_end(c, 0);
     prof_begin(c, "reset");
     tick_reset(b, n_mov, c->st);
@@ -751,19 +758,19 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     DevStats* st = c->stats;
     if ((rc = ensure(c, c->flag_mark, (size_t)C * 4)) || (rc = ensure(c, c->flag_pre, (size_t)C * 8)) ||
         (rc = ensure(c, c->flagged, (size_t)C * 4)) || (rc = ensure(c, c->rec_cnt, (size_t)C * 4)) ||
-        (rc = ensure(c, c->rec_off, (size_t)C * 8)) || (rc = ensure_scan64(c, C)))
+        (rc = ensure(c, c->rec_off, (size_t)C * 8)) || (rc = ensure_scan(c, C)))
         return rc;
     const World w = world(c);
     prof_begin(c, "sync_flagged");
     launch_flag_mark(c->flags, C, P<uint32_t>(c->flag_mark), c->st);
-    scan_u32_u64(P<uint32_t>(c->flag_mark), P<uint64_t>(c->flag_pre), C, nullptr, P<uint64_t>(c->scan_tmp64),
+    scan_u32_u64(P<uint32_t>(c->flag_mark), P<uint64_t>(c->flag_pre), C, nullptr, c->sc,
                  (uint64_t*)&st->flagged, c->st);
     launch_flag_compact(P<uint32_t>(c->flag_mark), P<uint64_t>(c->flag_pre), C, P<uint32_t>(c->flagged), c->st);
     prof_end(c, (uint64_t)C * 4 * 4);
     const uint64_t* nf = (const uint64_t*)&st->flagged;
     prof_begin(c, "sync_count");
     launch_sync_count(w, P<uint32_t>(c->flagged), nf, C, P<uint32_t>(c->rec_cnt), st, c->st);
-    scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), C, nf, P<uint64_t>(c->scan_tmp64),
+    scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), C, nf, c->sc,
                  (uint64_t*)&st->rec_total, c->st);
     size_t s_count = prof_end(c, 0);
     HIPCHK(hipGetLastError());

@@ -85,22 +85,31 @@ struct DevStats {
     unsigned long long shard[STAT_SHARDS][SH_FIELDS];
 };
 
-// ---- primitives (instantiated in kernels.hip) ------------------------------
+// ---- primitives (prim.hpp; host wrappers in sync.hip) -----------------------
+// State of the single-pass scans of one context (one stream): the tile status
+// words, the monotonic tile ticket, and the host-side ticket base and tag.
+struct ScanCtx {
+    unsigned long long* status;   // [max_tiles]
+    unsigned long long* ticket;   // one word, never reset
+    unsigned long long tbase;     // tickets handed out by earlier scans
+    uint32_t tag;                 // tag of the last scan (status words of other tags are stale)
+    uint64_t max_tiles;
+};
 struct RadixTmp {
     uint32_t* hist;      // 256 * radix_blocks(n_max)
-    uint32_t* scan_tmp;  // scan_tmp_elems(256 * radix_blocks(n_max))
-    uint32_t* scan_total;
+    ScanCtx* sc;
 };
 uint64_t radix_tile();            // keys per radix block
-uint64_t scan_tile();             // elements per scan block
-void scan_u32_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint64_t* n_dev, uint32_t* tmp,
+uint64_t scan_tile();             // elements per scan tile
+uint64_t scan_words();            // status words per scan tile
+void scan_u32_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
                   uint32_t* total, hipStream_t s);
-void scan_u32_u64(const uint32_t* in, uint64_t* out, uint64_t n_max, const uint64_t* n_dev, uint64_t* tmp,
+void scan_u32_u64(const uint32_t* in, uint64_t* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
                   uint64_t* total, hipStream_t s);
-void scan_u64_u64(const uint64_t* in, uint64_t* out, uint64_t n_max, const uint64_t* n_dev, uint64_t* tmp,
+void scan_u64_u64(const uint64_t* in, uint64_t* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
                   uint64_t* total, hipStream_t s);
 int sort_u32_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
-                 int lo_bit, int hi_bit, const RadixTmp& tmp, hipStream_t s);
+                 int lo_bit, int hi_bit, RadixTmp& tmp, hipStream_t s);
 
 // ---- persistent per-context state -----------------------------------------
 struct World {
@@ -157,10 +166,10 @@ struct TickBufs {
 
 // ---- launchers --------------------------------------------------------------
 void tick_ops(const TickBufs& b, hipStream_t s);
-int tick_grid(const TickBufs& b, const RadixTmp& rt, int key_bits, uint32_t* scan_tmp32, hipStream_t s);
-void tick_movers(const TickBufs& b, uint64_t* scan_tmp64, uint32_t* scan_tmp32, hipStream_t s);
+int tick_grid(const TickBufs& b, RadixTmp& rt, int key_bits, hipStream_t s);
+void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s);
 void tick_diff(const TickBufs& b, uint64_t n_movers, hipStream_t s);
-void tick_events(const TickBufs& b, uint64_t n_movers, uint64_t* scan_tmp64, hipStream_t s);
+void tick_events(const TickBufs& b, uint64_t n_movers, ScanCtx& sc, hipStream_t s);
 void tick_reset(const TickBufs& b, uint64_t n_movers, hipStream_t s);
 void stats_reduce(DevStats* st, hipStream_t s);
 

@@ -67,93 +67,129 @@ __device__ __forceinline__ uint64_t load_n(uint64_t n_max, const uint64_t* n_dev
 }
 
 // ---------------------------------------------------------------------------
-// Device exclusive scan: out[i] = sum(in[0..i)), *total = sum(in[0..n)).
-// Phase 1 reduces 4096-element tiles, phase 2 scans the tile sums in one
-// workgroup, phase 3 rescans each tile with its carry.
+// Device exclusive scan in ONE launch (decoupled look-back): out[i] =
+// sum(in[0..i)), *total = sum(in[0..n)).  Tiles of 4096 elements take a
+// ticket in dispatch order (a tile only waits on tiles that already run), post
+// their aggregate, and wave 0 looks back over up to 64 predecessors at a time
+// until it meets an inclusive prefix.  A tile publishes 4 status words: the
+// aggregate and the inclusive prefix, each split into 32-bit halves; every
+// word carries tag | flag | half in one 8-B agent-scope atomic (no separate
+// payload, so no fence), and a reader takes the inclusive pair if both halves
+// are posted, else the aggregate pair.  The per-call tag makes words of
+// earlier scans read as "not posted", so the status array is never cleared.
 constexpr int SCAN_IPT = 16;
 constexpr int SCAN_TILE = NT * SCAN_IPT;
+constexpr int SCAN_SHIFT = 34;                       // tag above flag bit 33 and the 32-bit half
+constexpr unsigned long long SCAN_POSTED = 1ull << 33;
+constexpr uint32_t SCAN_TAG_MAX = (1u << 22) - 1;
+constexpr int SCAN_WORDS = 4;                        // agg lo/hi, incl lo/hi
 
-template <typename TI, typename TO>
-__global__ void __launch_bounds__(NT) k_scan_reduce(const TI* __restrict__ in, uint64_t n_max,
-                                                    const uint64_t* n_dev, TO* __restrict__ partial) {
-    __shared__ TO lds[NWAVE];
-    uint64_t n = load_n(n_max, n_dev);
-    uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
-    TO s = 0;
-#pragma unroll
-    for (int j = 0; j < SCAN_IPT; ++j) {
-        uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
-        if (i < n) s += (TO)in[i];
-    }
-    TO tot;
-    block_excl_scan<TO>(s, lds, tot);
-    if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+__device__ __forceinline__ unsigned long long scan_ld(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
+__device__ __forceinline__ void scan_st(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <typename TO>
-__global__ void __launch_bounds__(NT) k_scan_partials(TO* __restrict__ partial, uint32_t nb, TO* total_out) {
-    __shared__ TO lds[NWAVE];
-    TO carry = 0;
-    for (uint32_t base = 0; base < nb; base += NT * 4) {
-        TO v[4];
-        TO s = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint32_t i = base + threadIdx.x * 4 + j;
-            v[j] = i < nb ? partial[i] : (TO)0;
-            s += v[j];
-        }
-        TO tot;
-        TO pre = block_excl_scan<TO>(s, lds, tot);
-        TO run = carry + pre;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint32_t i = base + threadIdx.x * 4 + j;
-            if (i < nb) partial[i] = run;
-            run += v[j];
-        }
-        carry += tot;
-    }
-    if (threadIdx.x == 0 && total_out) *total_out = carry;
+__device__ __forceinline__ void scan_post(unsigned long long* w, unsigned long long tg, TO v) {
+    const unsigned long long x = (unsigned long long)v;
+    scan_st(w, tg | SCAN_POSTED | (x & 0xffffffffull));
+    scan_st(w + 1, tg | SCAN_POSTED | (x >> 32));
 }
 
 template <typename TI, typename TO>
-__global__ void __launch_bounds__(NT) k_scan_down(const TI* __restrict__ in, TO* __restrict__ out,
-                                                  uint64_t n_max, const uint64_t* n_dev,
-                                                  const TO* __restrict__ partial) {
+__global__ void __launch_bounds__(NT) k_scan1(const TI* in, TO* out, uint64_t n_max, const uint64_t* n_dev,
+                                              unsigned long long* __restrict__ status,
+                                              unsigned long long* __restrict__ ticket, unsigned long long tbase,
+                                              uint32_t tag, TO* total) {
     __shared__ TO lds[NWAVE];
-    uint64_t n = load_n(n_max, n_dev);
-    uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_IPT;
+    __shared__ uint32_t s_tile;
+    __shared__ TO s_prefix;
+    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tbase);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t n = load_n(n_max, n_dev);
+    const uint64_t base = (uint64_t)tile * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_IPT;
     TO v[SCAN_IPT];
     TO s = 0;
 #pragma unroll
     for (int j = 0; j < SCAN_IPT; ++j) {
-        uint64_t i = base + j;
+        const uint64_t i = base + j;
         v[j] = i < n ? (TO)in[i] : (TO)0;
         s += v[j];
     }
     TO tot;
-    TO run = block_excl_scan<TO>(s, lds, tot) + partial[blockIdx.x];
-#pragma unroll
-    for (int j = 0; j < SCAN_IPT; ++j) {
-        uint64_t i = base + j;
-        if (i < n) out[i] = run;
-        run += v[j];
+    const TO pre = block_excl_scan<TO>(s, lds, tot);
+    const unsigned long long tg = (unsigned long long)tag << SCAN_SHIFT;
+    if (threadIdx.x < 64) {
+        TO excl = 0;
+        unsigned long long* my = status + (uint64_t)tile * SCAN_WORDS;
+        if (tile == 0) {
+            if (threadIdx.x == 0) scan_post<TO>(my + 2, tg, tot);
+        } else {
+            if (threadIdx.x == 0) scan_post<TO>(my, tg, tot);
+            const int ln = (int)threadIdx.x;
+            int64_t j = (int64_t)tile - 1;
+            while (true) {
+                const int64_t q = j - ln;
+                bool ready = true, incl = true;
+                unsigned long long lo = 0, hi = 0;
+                if (q >= 0) {
+                    const unsigned long long* w = status + (uint64_t)q * SCAN_WORDS;
+                    const unsigned long long il = scan_ld(w + 2), ih = scan_ld(w + 3);
+                    const bool ok = (il >> SCAN_SHIFT) == tag && (ih >> SCAN_SHIFT) == tag;
+                    if (ok) {
+                        lo = il; hi = ih;
+                    } else {
+                        incl = false;
+                        lo = scan_ld(w);
+                        hi = scan_ld(w + 1);
+                        ready = (lo >> SCAN_SHIFT) == tag && (hi >> SCAN_SHIFT) == tag;
+                    }
+                }
+                const uint64_t bi = wave_ballot(ready && incl);
+                const uint64_t nr = wave_ballot(!ready);
+                const int f = bi ? __builtin_ctzll(bi) : 64;
+                const uint64_t need = f >= 63 ? ~0ull : ((2ull << f) - 1);  // lanes 0..f
+                if (nr & need) continue;                                     // spin on the window
+                const unsigned long long x = (lo & 0xffffffffull) | ((hi & 0xffffffffull) << 32);
+                excl += wave_sum<TO>((ln <= f) ? (TO)x : (TO)0);
+                if (f < 64) break;
+                j -= 64;
+            }
+            if (threadIdx.x == 0) scan_post<TO>(my + 2, tg, excl + tot);
+        }
+        if (threadIdx.x == 0) s_prefix = excl;
     }
+    __syncthreads();
+    TO run = s_prefix + pre;
+    if (out) {
+#pragma unroll
+        for (int j = 0; j < SCAN_IPT; ++j) {
+            const uint64_t i = base + j;
+            if (i < n) out[i] = run;
+            run += v[j];
+        }
+    }
+    if (total && tile == gridDim.x - 1 && threadIdx.x == 0) *total = s_prefix + tot;
 }
 
-// host launcher: tmp must hold ceil(n_max/SCAN_TILE) elements of TO.
+// host launcher; sc.status must hold SCAN_WORDS * ceil(n_max / SCAN_TILE) words
 template <typename TI, typename TO>
-inline void scan_exclusive(const TI* in, TO* out, uint64_t n_max, const uint64_t* n_dev,
-                           TO* tmp, TO* total_dev, hipStream_t st) {
+inline void scan_exclusive(const TI* in, TO* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
+                           TO* total_dev, hipStream_t st) {
     uint32_t nb = (uint32_t)((n_max + SCAN_TILE - 1) / SCAN_TILE);
     if (nb == 0) nb = 1;
-    hipLaunchKernelGGL((k_scan_reduce<TI, TO>), dim3(nb), dim3(NT), 0, st, in, n_max, n_dev, tmp);
-    hipLaunchKernelGGL((k_scan_partials<TO>), dim3(1), dim3(NT), 0, st, tmp, nb, total_dev);
-    if (out)
-        hipLaunchKernelGGL((k_scan_down<TI, TO>), dim3(nb), dim3(NT), 0, st, in, out, n_max, n_dev, tmp);
+    if (sc.tag >= SCAN_TAG_MAX) {   // tags exhausted: clear the status words once
+        (void)hipMemsetAsync(sc.status, 0, sc.max_tiles * SCAN_WORDS * 8, st);
+        sc.tag = 0;
+    }
+    ++sc.tag;
+    hipLaunchKernelGGL((k_scan1<TI, TO>), dim3(nb), dim3(NT), 0, st, in, out, n_max, n_dev, sc.status, sc.ticket,
+                       sc.tbase, sc.tag, total_dev);
+    sc.tbase += nb;
 }
-inline uint64_t scan_tmp_elems(uint64_t n_max) { return (n_max + SCAN_TILE - 1) / SCAN_TILE + 1; }
+inline uint64_t scan_tiles(uint64_t n_max) { return (n_max + SCAN_TILE - 1) / SCAN_TILE + 1; }
 
 // ---------------------------------------------------------------------------
 // Stable LSD radix sort, 8-bit digits.  Per pass: block digit histograms
@@ -235,7 +271,7 @@ inline uint64_t radix_blocks(uint64_t n_max) { return (n_max + RS_TILE - 1) / RS
 // Returns 0 if the result is in (k0,v0), 1 if in (k1,v1).
 template <typename K>
 inline int radix_sort(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
-                      int lo_bit, int hi_bit, const RadixTmp& tmp, hipStream_t st) {
+                      int lo_bit, int hi_bit, RadixTmp& tmp, hipStream_t st) {
     uint32_t nb = (uint32_t)radix_blocks(n_max);
     if (nb == 0) return 0;
     int cur = 0;
@@ -243,8 +279,8 @@ inline int radix_sort(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n_max, 
         K* ki = cur ? k1 : k0; K* ko = cur ? k0 : k1;
         uint32_t* vi = cur ? v1 : v0; uint32_t* vo = cur ? v0 : v1;
         hipLaunchKernelGGL((k_rs_hist<K>), dim3(nb), dim3(NT), 0, st, ki, n_max, n_dev, shift, tmp.hist, nb);
-        scan_exclusive<uint32_t, uint32_t>(tmp.hist, tmp.hist, (uint64_t)RS_RADIX * nb, nullptr,
-                                           tmp.scan_tmp, tmp.scan_total, st);
+        scan_exclusive<uint32_t, uint32_t>(tmp.hist, tmp.hist, (uint64_t)RS_RADIX * nb, nullptr, *tmp.sc,
+                                           (uint32_t*)nullptr, st);
         if (v0)
             hipLaunchKernelGGL((k_rs_scatter<K, true>), dim3(nb), dim3(NT), 0, st, ki, vi, ko, vo, n_max,
                                n_dev, shift, tmp.hist, nb);

@@ -57,39 +57,45 @@ __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) 
     }
 }
 
+// Flagged entities are walked by a capped grid of waves (grid-stride): the
+// count lives on the device, so a grid sized for the worst case would
+// dispatch mostly empty waves.
+constexpr uint32_t SYNC_MAX_BLOCKS = 8192;
+
 // record count per flagged entity (one wave each)
 __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __restrict__ flagged,
                                                    const uint64_t* nf_dev, uint32_t nf_max, uint32_t* cnt,
                                                    DevStats* st) {
     const uint64_t nf = load_n(nf_max, nf_dev);
-    const uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
-    if (k >= nf) return;
-    const uint32_t e = flagged[k];
-    const uint32_t f = w.flags[e];
-    uint32_t r = 0;
-    if (w.aoi[e].meta & PRESENT_BIT) {
-        if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) r = 1;
-        if (f & GW_SIF_NEIGHBOR_CLIENTS) {
-            const unsigned long long c = w.nbc[e];
-            if ((uint32_t)(c >> 32) == w.epoch) {
-                r += (uint32_t)c;                            // counted by this tick's diff
-            } else {
-                uint32_t n = 0;
-                wave_neighbors(w, e, [&](bool rel, uint32_t, uint32_t g) {
-                    n += (uint32_t)popc64(wave_ballot(rel && g != 0));
-                });
-                r += n;
+    const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
+    for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < nf; k += stride) {
+        const uint32_t e = flagged[k];
+        const uint32_t f = w.flags[e];
+        uint32_t r = 0;
+        if (w.aoi[e].meta & PRESENT_BIT) {
+            if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) r = 1;
+            if (f & GW_SIF_NEIGHBOR_CLIENTS) {
+                const unsigned long long c = w.nbc[e];
+                if ((uint32_t)(c >> 32) == w.epoch) {
+                    r += (uint32_t)c;                        // counted by this tick's diff
+                } else {
+                    uint32_t n = 0;
+                    wave_neighbors(w, e, [&](bool rel, uint32_t, uint32_t g) {
+                        n += (uint32_t)popc64(wave_ballot(rel && g != 0));
+                    });
+                    r += n;
+                }
             }
         }
+        if (lane_id() == 0) cnt[k] = r;
     }
-    if (lane_id() == 0) cnt[k] = r;
     (void)st;
 }
 void launch_sync_count(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
                        uint32_t* cnt, DevStats* st, hipStream_t s) {
     if (!nf_max) return;
-    hipLaunchKernelGGL(k_sync_count, dim3(nblk(nf_max, NWAVE)), dim3(NT), 0, s, w, flagged, nf_dev, nf_max, cnt,
-                       st);
+    hipLaunchKernelGGL(k_sync_count, dim3(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS)), dim3(NT), 0, s, w,
+                       flagged, nf_dev, nf_max, cnt, st);
 }
 
 // writes e's records at rec_off[k] and clears e's flags
@@ -98,44 +104,45 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
                                                    const uint64_t* __restrict__ rec_off, gw_sync_record* rec,
                                                    uint64_t rec_cap) {
     const uint64_t nf = load_n(nf_max, nf_dev);
-    const uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
-    if (k >= nf) return;
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
-    const uint32_t e = flagged[k];
-    const uint32_t f = w.flags[e];
-    if (w.aoi[e].meta & PRESENT_BIT) {
-        const float4 p = w.pos[e];
-        uint64_t at = rec_off[k];
-        if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
-            if (ln == 0 && at < rec_cap) {
-                gw_sync_record r;
-                r.watcher = e; r.entity = e; r.x = p.x; r.y = p.y; r.z = p.z; r.yaw = p.w;
-                rec[at] = r;
-            }
-            ++at;
-        }
-        if (f & GW_SIF_NEIGHBOR_CLIENTS) {
-            wave_neighbors(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
-                const bool take = rel && g != 0;
-                const uint64_t bt = wave_ballot(take);
-                if (take) {
-                    const uint64_t i = at + (uint64_t)popc64(bt & lt);
+    const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
+    for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < nf; k += stride) {
+        const uint32_t e = flagged[k];
+        const uint32_t f = w.flags[e];
+        if (w.aoi[e].meta & PRESENT_BIT) {
+            const float4 p = w.pos[e];
+            uint64_t at = rec_off[k];
+            if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
+                if (ln == 0 && at < rec_cap) {
                     gw_sync_record r;
-                    r.watcher = ws; r.entity = e; r.x = p.x; r.y = p.y; r.z = p.z; r.yaw = p.w;
-                    if (i < rec_cap) rec[i] = r;
+                    r.watcher = e; r.entity = e; r.x = p.x; r.y = p.y; r.z = p.z; r.yaw = p.w;
+                    rec[at] = r;
                 }
-                at += (uint64_t)popc64(bt);
-            });
+                ++at;
+            }
+            if (f & GW_SIF_NEIGHBOR_CLIENTS) {
+                wave_neighbors(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
+                    const bool take = rel && g != 0;
+                    const uint64_t bt = wave_ballot(take);
+                    if (take) {
+                        const uint64_t i = at + (uint64_t)popc64(bt & lt);
+                        gw_sync_record r;
+                        r.watcher = ws; r.entity = e; r.x = p.x; r.y = p.y; r.z = p.z; r.yaw = p.w;
+                        if (i < rec_cap) rec[i] = r;
+                    }
+                    at += (uint64_t)popc64(bt);
+                });
+            }
         }
+        if (ln == 0) w.flags[e] = 0;
     }
-    if (ln == 0) w.flags[e] = 0;
 }
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
                        const uint64_t* rec_off, gw_sync_record* rec, uint64_t rec_cap, hipStream_t s) {
     if (!nf_max) return;
-    hipLaunchKernelGGL(k_sync_write, dim3(nblk(nf_max, NWAVE)), dim3(NT), 0, s, w, flagged, nf_dev, nf_max, rec_off,
-                       rec, rec_cap);
+    hipLaunchKernelGGL(k_sync_write, dim3(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS)), dim3(NT), 0, s, w,
+                       flagged, nf_dev, nf_max, rec_off, rec, rec_cap);
 }
 
 __global__ void __launch_bounds__(NT) k_flag_mark(const uint32_t* __restrict__ flags, uint32_t cap, uint32_t* mark) {
@@ -268,20 +275,21 @@ void launch_fill_i32(int32_t* p, int32_t v, uint64_t n, hipStream_t s) {
 // primitive instantiations for the host code
 uint64_t radix_tile() { return RS_TILE; }
 uint64_t scan_tile() { return SCAN_TILE; }
-void scan_u32_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint64_t* n_dev, uint32_t* tmp,
+uint64_t scan_words() { return SCAN_WORDS; }
+void scan_u32_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
                   uint32_t* total, hipStream_t s) {
-    scan_exclusive<uint32_t, uint32_t>(in, out, n_max, n_dev, tmp, total, s);
+    scan_exclusive<uint32_t, uint32_t>(in, out, n_max, n_dev, sc, total, s);
 }
-void scan_u32_u64(const uint32_t* in, uint64_t* out, uint64_t n_max, const uint64_t* n_dev, uint64_t* tmp,
+void scan_u32_u64(const uint32_t* in, uint64_t* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
                   uint64_t* total, hipStream_t s) {
-    scan_exclusive<uint32_t, uint64_t>(in, out, n_max, n_dev, tmp, total, s);
+    scan_exclusive<uint32_t, uint64_t>(in, out, n_max, n_dev, sc, total, s);
 }
-void scan_u64_u64(const uint64_t* in, uint64_t* out, uint64_t n_max, const uint64_t* n_dev, uint64_t* tmp,
+void scan_u64_u64(const uint64_t* in, uint64_t* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
                   uint64_t* total, hipStream_t s) {
-    scan_exclusive<uint64_t, uint64_t>(in, out, n_max, n_dev, tmp, total, s);
+    scan_exclusive<uint64_t, uint64_t>(in, out, n_max, n_dev, sc, total, s);
 }
 int sort_u32_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
-                 int lo_bit, int hi_bit, const RadixTmp& tmp, hipStream_t s) {
+                 int lo_bit, int hi_bit, RadixTmp& tmp, hipStream_t s) {
     return radix_sort<uint32_t>(k0, v0, k1, v1, n_max, n_dev, lo_bit, hi_bit, tmp, s);
 }
 

@@ -4,30 +4,48 @@
 // the global stamps of the members' last AOI ops (gw_internal.hpp, DESIGN.md
 // §2), so the tick keeps no neighbour lists.  For one tick:
 //   ops      last-op dedupe per slot; movers save their pre-tick position and
-//            stamp (PrevEnt) and take a new stamp
-//   grid     stable radix sort of (cell, slot) -> current grid gn[] in (cell,
-//            slot) order + cell starts; movers in grid order, then leavers
-//   gm       mover grid: each mover at its old and its new cell (counting sort)
-//   diff     one wave per mover scans non-movers of gn and the mover grid over
-//            the cells of its old and new windows, evaluates the old and the
-//            new relation of every candidate and emits own events, sorted
+//            stamp (PrevEnt), take a new stamp and join the mover list
+//   grid     incremental: movers that stay in their cell are patched in
+//            place; cells that lose or gain entities are re-sorted by slot (a
+//            wave per cell, LDS bitonic), every other cell is shifted by the
+//            scan of the new cell counts.  gn stays in (cell, slot) order.
+//   gm       mover grid: each mover at its old and its new cell (counting
+//            sort whose cursor counts back to zero)
+//   diff     one wave per mover (in mover-grid order, i.e. by cell: windows
+//            of neighbouring waves overlap in L2) walks the non-movers of gn
+//            and the mover grid over its old and new windows, evaluates the
+//            old and new relation of every candidate and emits own events,
+//            sorted
 //   mirror   the relation is symmetric, so an own event (A,B) of a mover with
 //            an op-less B is also B's event (B,A): the mover counts it into
 //            B's packed counter (the returned value is its rank in B's
 //            segment) and keeps (B, A, rank) for the scatter
 //   events   scan of the per-watcher counts -> canonical offsets; movers copy
-//            their sorted events and scatter the mirror ones; op-less segments
-//            are insertion-sorted by one thread each (block sort when long)
+//            their sorted events and scatter the mirror ones; the segments of
+//            touched op-less watchers are sorted by target
 // Outputs are placed by scans; the atomics are histogram/cursor updates, one
-// counter increment per mirror event (spread over watchers), per-shard
-// statistics and the rare big-segment lists.  No MFMA: compare and
-// gather work bound by L2/HBM latency and bandwidth.
+// counter increment per mirror event (spread over watchers), wave-aggregated
+// list appends and per-shard statistics.  No MFMA: compare and gather work
+// bound by L2/HBM latency and bandwidth.
 #include "dev_common.hpp"
 
 namespace gw {
 
 constexpr uint32_t SORT_LDS = 1024;     // own events sorted in a wave's LDS up to this many
-constexpr uint32_t INS_MAX = 16;        // op-less segments insertion-sorted up to this many
+constexpr uint32_t NO_CELL = 0xffffffffu;
+constexpr uint32_t GS_BLOCKS = 4096;    // cap of grid-stride launches
+
+// appends v for every lane with pred to list (64-bit counter), one atomic per
+// wave; every lane of the wave must call it
+__device__ __forceinline__ void wave_append(bool pred, uint32_t v, uint32_t* list, unsigned long long* cnt) {
+    const uint64_t bm = wave_ballot(pred);
+    if (!bm) return;
+    const int leader = __builtin_ctzll(bm);
+    unsigned long long base = 0;
+    if (lane_id() == leader) base = atomicAdd(cnt, (unsigned long long)popc64(bm));
+    base = __shfl(base, leader, 64);
+    if (pred) list[base + (uint64_t)popc64(bm & lanemask_lt())] = v;
+}
 
 // ---------------------------------------------------------------------------
 // ops: last-op dedupe per slot (seq = index in the tick's op stream)
@@ -54,68 +72,64 @@ __global__ void __launch_bounds__(NT) k_ops2(TickBufs b) {
 }
 
 __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
-    uint32_t i = blockIdx.x * NT + threadIdx.x;
-    if (i >= b.m) return;
-    gw_op op = b.ops[i];
-    if (op.slot >= b.w.cap || op.kind < GW_OP_ENTER || op.kind > GW_OP_SYNC) return;
-    const uint32_t s = op.slot;
-    // syncInfoFlag |= bits of every call after the last Leave (Space.go:196,
-    // Entity.go:1199-1204, 1286)
-    if ((int32_t)i > b.last_leave[s] && op.sync_flags) atomicOr(&b.w.flags[s], (uint32_t)op.sync_flags);
-    if (b.last_pos[s] == (int32_t)i) b.w.pos[s] = make_float4(op.x, op.y, op.z, op.yaw);
-    if (b.last_aoi[s] == (int32_t)i) {
-        AoiEnt a = b.w.aoi[s];
-        PrevEnt p;
-        const bool was = (a.meta & PRESENT_BIT) != 0;
-        p.ox = was ? a.x : qnan();
-        p.oz = was ? a.z : qnan();
-        p.ostamp = b.w.stamp[s];
-        b.w.prev[s] = p;
-        b.w.stamp[s] = b.stamp_base + i;
-        a.seq = (int32_t)i;
-        if (op.kind == GW_OP_LEAVE) a.meta &= ~PRESENT_BIT;
-        else { a.x = op.x; a.z = op.z; a.meta |= PRESENT_BIT; }
-        b.w.aoi[s] = a;
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i < b.m) {
+        const gw_op op = b.ops[i];
+        const uint32_t s = op.slot;
+        if (s < b.w.cap && op.kind >= GW_OP_ENTER && op.kind <= GW_OP_SYNC) {
+            // syncInfoFlag |= bits of every call after the last Leave (Space.go:196,
+            // Entity.go:1199-1204, 1286)
+            if ((int32_t)i > b.last_leave[s] && op.sync_flags) atomicOr(&b.w.flags[s], (uint32_t)op.sync_flags);
+            if (b.last_pos[s] == (int32_t)i) b.w.pos[s] = make_float4(op.x, op.y, op.z, op.yaw);
+            if (b.last_aoi[s] == (int32_t)i) {
+                AoiEnt a = b.w.aoi[s];
+                PrevEnt p;
+                const bool was = (a.meta & PRESENT_BIT) != 0;
+                p.ox = was ? a.x : qnan();
+                p.oz = was ? a.z : qnan();
+                p.ostamp = b.w.stamp[s];
+                b.w.prev[s] = p;
+                b.w.stamp[s] = b.stamp_base + i;
+                if (op.kind == GW_OP_LEAVE) a.meta &= ~PRESENT_BIT;
+                else { a.x = op.x; a.z = op.z; a.meta |= PRESENT_BIT; }
+                b.w.aoi[s] = a;
+            }
+        }
     }
 }
 
 void tick_ops(const TickBufs& b, hipStream_t s) {
-    if (!b.m) return;
     hipLaunchKernelGGL(k_ops1, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_ops2, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_ops3, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
 }
 
 // ---------------------------------------------------------------------------
-// current grid: stable LSD radix sort of (cell, slot) pairs (absent slots get
-// the sentinel key ncells and sort last), so gn[] is in (cell, slot) order and
-// every output that follows grid order is deterministic
-__global__ void __launch_bounds__(NT) k_grid_keys(TickBufs b) {
+// full rebuild: stable LSD radix sort of (cell, slot) pairs (absent slots get
+// the sentinel key ncells and sort last), so gn[] is in (cell, slot) order
+__global__ void __launch_bounds__(NT) k_grid_keys(World w, uint32_t* k0, uint32_t* v0) {
     uint32_t s = blockIdx.x * NT + threadIdx.x;
-    if (s >= b.w.cap) return;
-    const AoiEnt a = b.w.aoi[s];
-    uint32_t key = b.w.ncells;
-    if (a.meta & PRESENT_BIT) key = cell_of(b.w.sp[a.meta & SPACE_MASK], a.x, a.z);
-    b.k0[s] = key;
-    b.v0[s] = s;
+    if (s >= w.cap) return;
+    const AoiEnt a = w.aoi[s];
+    uint32_t key = w.ncells;
+    if (a.meta & PRESENT_BIT) key = cell_of(w.sp[a.meta & SPACE_MASK], a.x, a.z);
+    k0[s] = key;
+    v0[s] = s;
 }
 __global__ void __launch_bounds__(NT) k_grid_fill(World w, const uint32_t* __restrict__ keys,
-                                                  const uint32_t* __restrict__ slots, uint32_t* pflag) {
+                                                  const uint32_t* __restrict__ slots) {
     uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i >= w.cap) return;
     const uint32_t key = keys[i];
-    uint32_t mv = 0;
     if (key < w.ncells) {
         const uint32_t s = slots[i];
         const AoiEnt a = w.aoi[s];
         GEnt e;
         e.x = a.x; e.z = a.z; e.slot = s;
-        mv = a.seq >= 0;
-        e.meta = (uint32_t)w.gate[s] | (mv ? MOVER_BIT : 0u);
+        e.meta = key | (w.gate[s] ? CLIENT_BIT : 0u);
         w.gn[i] = e;
         w.gidx[s] = i;
     }
-    if (pflag) pflag[i] = mv;
 }
 // gn_start[c] = first index with key >= c (binary search over the sorted keys)
 __global__ void __launch_bounds__(NT) k_grid_starts(World w, const uint32_t* __restrict__ keys, DevStats* st) {
@@ -130,80 +144,241 @@ __global__ void __launch_bounds__(NT) k_grid_starts(World w, const uint32_t* __r
     if (c == w.ncells && st) st->n_present = lo;
 }
 
-int tick_grid(const TickBufs& b, RadixTmp& rt, int key_bits, hipStream_t s) {
-    const uint32_t C = b.w.cap;
-    hipLaunchKernelGGL(k_grid_keys, dim3(nblk1(C, NT)), dim3(NT), 0, s, b);
-    int r = radix_sort<uint32_t>(b.k0, b.v0, b.k1, b.v1, C, nullptr, 0, key_bits, rt, s);
-    const uint32_t* keys = r ? b.k1 : b.k0;
-    const uint32_t* slots = r ? b.v1 : b.v0;
-    hipLaunchKernelGGL(k_grid_fill, dim3(nblk1(C, NT)), dim3(NT), 0, s, b.w, keys, slots, b.pflag);
-    hipLaunchKernelGGL(k_grid_starts, dim3(nblk1((uint64_t)b.w.ncells + 1, NT)), dim3(NT), 0, s, b.w, keys, b.st);
-    return r;
+void grid_rebuild(const World& w, DevStats* st, uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1,
+                  RadixTmp& rt, int key_bits, hipStream_t s) {
+    const uint32_t C = w.cap;
+    hipLaunchKernelGGL(k_grid_keys, dim3(nblk1(C, NT)), dim3(NT), 0, s, w, k0, v0);
+    int r = radix_sort<uint32_t>(k0, v0, k1, v1, C, nullptr, 0, key_bits, rt, s);
+    const uint32_t* keys = r ? k1 : k0;
+    const uint32_t* slots = r ? v1 : v0;
+    hipLaunchKernelGGL(k_grid_fill, dim3(nblk1(C, NT)), dim3(NT), 0, s, w, keys, slots);
+    hipLaunchKernelGGL(k_grid_starts, dim3(nblk1((uint64_t)w.ncells + 1, NT)), dim3(NT), 0, s, w, keys, st);
 }
 
 // ---------------------------------------------------------------------------
-// movers: present movers in grid order (windows of neighbouring movers overlap
-// in L2), then the leavers
-__global__ void __launch_bounds__(NT) k_compact_grid_movers(TickBufs b) {
-    uint64_t p = (uint64_t)blockIdx.x * NT + threadIdx.x;
-    if (p >= b.st->n_present) return;
-    if (b.pflag[p]) b.movers[b.pre[p]] = b.w.gn[p].slot;
+// incremental grid.  co / cn: the mover's cell before / after the tick
+// (NO_CELL when absent).  co is the cell its pre-tick grid entry sits in.
+struct MoverCells {
+    uint32_t A, co, cn;
+    AoiEnt a;
+    PrevEnt p;
+};
+__device__ __forceinline__ MoverCells mover_cells(const World& w, uint32_t A) {
+    MoverCells m;
+    m.A = A;
+    m.a = w.aoi[A];
+    m.p = w.prev[A];
+    const SpaceP P = w.sp[m.a.meta & SPACE_MASK];
+    m.co = m.cn = NO_CELL;
+    if (m.p.ox == m.p.ox) m.co = cell_of(P, m.p.ox, m.p.oz);
+    if (m.a.meta & PRESENT_BIT) m.cn = cell_of(P, m.a.x, m.a.z);
+    return m;
 }
-__global__ void __launch_bounds__(NT) k_leaver_flags(TickBufs b) {
-    uint32_t i = blockIdx.x * NT + threadIdx.x;
-    if (i >= b.m) return;
-    gw_op op = b.ops[i];
-    bool f = op.kind == GW_OP_LEAVE && op.slot < b.w.cap && b.last_aoi[op.slot] == (int32_t)i;
-    b.pflag[i] = f;
-}
-__global__ void __launch_bounds__(NT) k_compact_leavers(TickBufs b) {
-    uint32_t i = blockIdx.x * NT + threadIdx.x;
-    if (i >= b.m) return;
-    if (b.pflag[i]) b.movers[b.st->movers_present + b.pre[i]] = b.ops[i].slot;
-    if (i == 0) b.st->n_movers = b.st->movers_present + b.st->leavers;
-}
-__global__ void k_set_nmov(DevStats* st) { st->n_movers = st->movers_present + st->leavers; }
 
-// mover grid: the cells of a mover's old and new positions
-__device__ __forceinline__ void mover_cells(const World& w, uint32_t A, uint32_t& co, uint32_t& cn) {
-    const AoiEnt a = w.aoi[A];
-    const PrevEnt p = w.prev[A];
-    const SpaceP P = w.sp[a.meta & SPACE_MASK];
-    co = cn = 0xffffffffu;
-    if (p.ox == p.ox) co = cell_of(P, p.ox, p.oz);
-    if (a.meta & PRESENT_BIT) cn = cell_of(P, a.x, a.z);
+// op i is slot s's mover entry when it is s's last AOI op (no list: a
+// single-address list counter serialises across the chip)
+__device__ __forceinline__ bool op_mover(const TickBufs& b, uint32_t i, uint32_t& s) {
+    const gw_op op = b.ops[i];
+    s = op.slot;
+    return s < b.w.cap && op.kind >= GW_OP_ENTER && op.kind <= GW_OP_LEAVE && b.last_aoi[s] == (int32_t)i;
 }
-__global__ void __launch_bounds__(NT) k_gm_count(TickBufs b) {
-    uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x;
-    if (m >= b.st->n_movers) return;
-    uint32_t co, cn;
-    mover_cells(b.w, b.movers[m], co, cn);
-    if (co != 0xffffffffu) atomicAdd(&b.gm_cnt[co], 1u);
-    if (cn != 0xffffffffu && cn != co) atomicAdd(&b.gm_cnt[cn], 1u);
-}
-__global__ void __launch_bounds__(NT) k_gm_scatter(TickBufs b) {
-    uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x;
-    if (m >= b.st->n_movers) return;
-    const uint32_t A = b.movers[m];
-    uint32_t co, cn;
-    mover_cells(b.w, A, co, cn);
-    const AoiEnt a = b.w.aoi[A];
-    const PrevEnt p = b.w.prev[A];
-    MEnt e;
-    const bool pn = (a.meta & PRESENT_BIT) != 0;
-    e.x = pn ? a.x : qnan(); e.z = pn ? a.z : qnan();
-    e.ox = p.ox; e.oz = p.oz;
-    e.slot = A; e.gate = b.w.gate[A]; e.pad1 = 0;
-    if (co != 0xffffffffu) {
-        e.tags = TAG_OLD | (cn == co ? TAG_NEW : 0u);
-        b.gm[atomicAdd(&b.gm_cnt[co], 1u)] = e;
-    }
-    if (cn != 0xffffffffu && cn != co) {
-        e.tags = TAG_NEW;
-        b.gm[atomicAdd(&b.gm_cnt[cn], 1u)] = e;
+
+// per mover: mover-grid histogram; a mover staying in its cell is patched in
+// place, the others count as a departure / an arrival of their cells
+__global__ void __launch_bounds__(NT) k_classify(TickBufs b) {
+    __shared__ uint32_t lds[NWAVE];
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    uint32_t A = 0;
+    const bool mv = i < b.m && op_mover(b, i, A);
+    uint32_t tot;
+    (void)block_excl_scan<uint32_t>(mv ? 1u : 0u, lds, tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(&b.st->n_movers, (unsigned long long)tot);
+    if (mv) {
+        const MoverCells mc = mover_cells(b.w, A);
+        if (mc.co != NO_CELL) atomicAdd(&b.gm_cnt[mc.co], 1u);
+        if (mc.cn != NO_CELL && mc.cn != mc.co) atomicAdd(&b.gm_cnt[mc.cn], 1u);
+        if (mc.co != NO_CELL && mc.co == mc.cn) {
+            GEnt e;
+            e.x = mc.a.x; e.z = mc.a.z; e.slot = mc.A;
+            e.meta = mc.cn | (b.w.gate[mc.A] ? CLIENT_BIT : 0u) | MOVER_BIT;
+            b.w.gn[b.w.gidx[mc.A]] = e;
+        } else {
+            if (mc.co != NO_CELL) {
+                atomicAdd(&b.dep[mc.co], 1u);
+                b.w.gn[b.w.gidx[mc.A]].slot = DEPARTED;
+            }
+            if (mc.cn != NO_CELL) atomicAdd(&b.arr[mc.cn], 1u);
+        }
     }
 }
 
+// per cell: entries after the tick; cells with departures or arrivals are
+// flagged dirty
+__global__ void __launch_bounds__(NT) k_cellcnt(TickBufs b) {
+    const uint32_t c = blockIdx.x * NT + threadIdx.x;
+    const uint32_t NC = b.w.ncells;
+    if (c < NC) {
+        const uint32_t old = b.w.gn_start[c + 1] - b.w.gn_start[c];
+        const uint32_t d = b.dep[c], r = b.arr[c];
+        b.cnt_new[c] = old - d + r;
+        if (d | r) b.dep[c] = d | CELL_DIRTY;
+    } else if (c == NC) {
+        b.cnt_new[c] = 0;
+    }
+}
+
+// per mover: its mover-grid entries (the cursor counts gm_cnt back to zero)
+// and, for an arrival, its grid entry behind the kept entries of the new cell
+__global__ void __launch_bounds__(NT) k_place(TickBufs b) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    uint32_t A = 0;
+    if (i < b.m && op_mover(b, i, A)) {
+        const MoverCells mc = mover_cells(b.w, A);
+        const bool cl = b.w.gate[mc.A] != 0;
+        const bool pn = mc.cn != NO_CELL;
+        MEnt e;
+        e.x = pn ? mc.a.x : qnan(); e.z = pn ? mc.a.z : qnan();
+        e.ox = mc.p.ox; e.oz = mc.p.oz;
+        e.slot = mc.A; e.client = cl ? 1u : 0u; e.space = mc.a.meta & SPACE_MASK;
+        if (mc.co != NO_CELL) {
+            e.tags = TAG_OLD | (mc.cn == mc.co ? TAG_NEW | TAG_PRIMARY : 0u) | (pn ? 0u : TAG_PRIMARY);
+            b.gm[b.gm_start[mc.co] + atomicSub(&b.gm_cnt[mc.co], 1u) - 1u] = e;
+        }
+        if (pn && mc.cn != mc.co) {
+            e.tags = TAG_NEW | TAG_PRIMARY;
+            b.gm[b.gm_start[mc.cn] + atomicSub(&b.gm_cnt[mc.cn], 1u) - 1u] = e;
+            const uint32_t kept = (b.w.gn_start[mc.cn + 1] - b.w.gn_start[mc.cn]) - (b.dep[mc.cn] & ~CELL_DIRTY);
+            const uint32_t at = b.start_nxt[mc.cn] + kept + atomicSub(&b.arr[mc.cn], 1u) - 1u;
+            GEnt g;
+            g.x = mc.a.x; g.z = mc.a.z; g.slot = mc.A;
+            g.meta = mc.cn | (cl ? CLIENT_BIT : 0u) | MOVER_BIT;
+            b.gn_nxt[at] = g;
+        }
+    }
+}
+
+// clean cells move as a block: new index = start_nxt + offset in the cell
+__global__ void __launch_bounds__(NT) k_grid_copy(TickBufs b) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i >= b.w.gn_start[b.w.ncells]) return;
+    const GEnt e = b.w.gn[i];
+    if (e.slot == DEPARTED) return;
+    const uint32_t c = e.meta & CELL_MASK;
+    if (b.dep[c] & CELL_DIRTY) return;
+    const uint32_t at = b.start_nxt[c] + (i - b.w.gn_start[c]);
+    b.gn_nxt[at] = e;
+    b.w.gidx[e.slot] = at;
+}
+
+// Dirty cells: the kept entries (already in slot order) merge with the
+// arrivals (few, in arrival order at the cell's tail) by rank: a kept entry
+// moves up by the arrivals with a smaller slot, an arrival lands after the
+// kept entries and arrivals with a smaller slot.  A wave scans the flags of
+// DIRTY_SPAN cells and merges its dirty ones; cells with more than 64
+// arrivals go to the block path.
+constexpr uint32_t DIRTY_SPAN = 16;
+__global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) {
+    const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint32_t c0 = (blockIdx.x * NWAVE + (threadIdx.x >> 6)) * DIRTY_SPAN;
+    if (c0 >= b.w.ncells) return;
+    const uint32_t cl = c0 + ln;
+    uint64_t dm = wave_ballot(ln < (int)DIRTY_SPAN && cl < b.w.ncells && (b.dep[cl] & CELL_DIRTY));
+    while (dm) {
+        const uint32_t c = c0 + (uint32_t)__builtin_ctzll(dm);
+        dm &= dm - 1;
+        const uint32_t so = b.w.gn_start[c], old = b.w.gn_start[c + 1] - so;
+        const uint32_t sn = b.start_nxt[c], nn = b.start_nxt[c + 1] - sn;
+        const uint32_t kept = old - (b.dep[c] & ~CELL_DIRTY);
+        const uint32_t narr = nn - kept;
+        if (narr > 64) {
+            if (ln == 0) b.bigcell[atomicAdd(&b.st->n_bigcell, 1ull)] = c;   // rare
+            continue;
+        }
+        // arrivals: one per lane, read before any write of the cell's new range
+        GEnt ar;
+        ar.slot = 0xffffffffu;
+        if (ln < (int)narr) ar = b.gn_nxt[sn + kept + ln];
+        uint32_t arank = 0;                       // arrivals with a smaller slot, then + kept below
+        for (uint32_t j = 0; j < narr; ++j) {
+            const uint32_t aj = (uint32_t)__builtin_amdgcn_readlane((int)ar.slot, (int)j);
+            arank += (ln < (int)narr && aj < ar.slot) ? 1u : 0u;
+        }
+        uint32_t k0 = 0;                          // kept entries before this chunk
+        for (uint32_t base = 0; base < old; base += 64) {
+            const uint32_t i = base + ln;
+            GEnt e;
+            e.slot = DEPARTED;
+            if (i < old) e = b.w.gn[so + i];
+            const bool keep = i < old && e.slot != DEPARTED;
+            const uint64_t bm = wave_ballot(keep);
+            uint32_t below = 0;                   // arrivals below this kept entry
+            for (uint32_t j = 0; j < narr; ++j) {
+                const uint32_t aj = (uint32_t)__builtin_amdgcn_readlane((int)ar.slot, (int)j);
+                below += aj < e.slot ? 1u : 0u;
+                const uint32_t kb = (uint32_t)popc64(wave_ballot(keep && e.slot < aj));
+                if (ln == (int)j) arank += kb;
+            }
+            if (keep) {
+                const uint32_t at = sn + k0 + (uint32_t)popc64(bm & lt) + below;
+                b.gn_nxt[at] = e;
+                b.w.gidx[e.slot] = at;
+            }
+            k0 += (uint32_t)popc64(bm);
+        }
+        if (ln < (int)narr) {
+            b.gn_nxt[sn + arank] = ar;
+            b.w.gidx[ar.slot] = sn + arank;
+        }
+        if (ln == 0) b.dep[c] = 0;
+    }
+}
+
+// dirty cells with more than 64 arrivals: block compaction + bitonic in place
+__global__ void __launch_bounds__(NT) k_grid_bigcell(TickBufs b) {
+    __shared__ uint32_t lds[NWAVE];
+    const uint64_t nb = b.st->n_bigcell;
+    for (uint64_t k = blockIdx.x; k < nb; k += gridDim.x) {
+        const uint32_t c = b.bigcell[k];
+        const uint32_t so = b.w.gn_start[c], old = b.w.gn_start[c + 1] - so;
+        const uint32_t sn = b.start_nxt[c], nn = b.start_nxt[c + 1] - sn;
+        uint32_t run = 0;
+        for (uint32_t base = 0; base < old; base += NT) {
+            const uint32_t i = base + threadIdx.x;
+            GEnt e;
+            e.slot = DEPARTED;
+            if (i < old) e = b.w.gn[so + i];
+            const uint32_t keep = (i < old && e.slot != DEPARTED) ? 1u : 0u;
+            uint32_t tot;
+            const uint32_t pre = block_excl_scan<uint32_t>(keep, lds, tot);
+            if (keep) b.gn_nxt[sn + run + pre] = e;
+            run += tot;
+        }
+        __syncthreads();
+        bitonic_inplace<NT>(b.gn_nxt + sn, nn, (int)threadIdx.x, [](const GEnt& e) { return e.slot; },
+                            [] { __syncthreads(); });
+        for (uint32_t j = threadIdx.x; j < nn; j += NT) b.w.gidx[b.gn_nxt[sn + j].slot] = sn + j;
+        if (threadIdx.x == 0) b.dep[c] = 0;
+        __syncthreads();
+    }
+}
+
+void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
+    const uint32_t NC = b.w.ncells;
+    hipLaunchKernelGGL(k_classify, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_cellcnt, dim3(nblk1((uint64_t)NC + 1, NT)), dim3(NT), 0, s, b);
+    // totals land in the low words of the (zeroed, little-endian) 64-bit counters
+    scan_exclusive<uint32_t, uint32_t>(b.cnt_new, b.start_nxt, (uint64_t)NC + 1, nullptr, sc,
+                                       (uint32_t*)&b.st->n_present, s);
+    scan_exclusive<uint32_t, uint32_t>(b.gm_cnt, b.gm_start, (uint64_t)NC + 1, nullptr, sc,
+                                       (uint32_t*)&b.st->n_gm, s);
+    hipLaunchKernelGGL(k_place, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_grid_copy, dim3(nblk1(b.w.cap, NT)), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_grid_dirty, dim3(nblk1((uint64_t)NC, DIRTY_SPAN * NWAVE)), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_grid_bigcell, dim3(64), dim3(NT), 0, s, b);
+}
+
+// ---------------------------------------------------------------------------
 // The cells a mover scans: the rectangles of its old and new windows, merged
 // into their bounding box when they touch (visiting extra cells is harmless:
 // every candidate is evaluated exactly, each cell once).
@@ -232,100 +407,88 @@ __device__ __forceinline__ Rects mover_rects(const SpaceP& P, bool po, float ox,
     return m;
 }
 
-// candidate bound of each mover (entries of gn and gm in its cells) -> the
-// size of its own-event region
+// candidate bound of each primary mover-grid entry (entries of gn and gm in
+// its cells) -> the size of its own-event region
 __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
-    uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x;
-    if (m >= b.st->n_movers) return;
-    const uint32_t A = b.movers[m];
-    const AoiEnt a = b.w.aoi[A];
-    const PrevEnt p = b.w.prev[A];
-    const SpaceP P = b.w.sp[a.meta & SPACE_MASK];
-    const Rects R = mover_rects(P, p.ox == p.ox, p.ox, p.oz, (a.meta & PRESENT_BIT) != 0, a.x, a.z);
+    const uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (m >= b.st->n_gm) return;
+    const MEnt e = b.gm[m];
     uint64_t c = 0;
+    if (e.tags & TAG_PRIMARY) {
+        const SpaceP P = b.w.sp[e.space];
+        const Rects R = mover_rects(P, e.ox == e.ox, e.ox, e.oz, e.x == e.x, e.x, e.z);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        if (q >= R.n) break;
-        const Rect rr = q == 0 ? R.r[0] : R.r[1];
-        for (int cz = rr.z0; cz <= rr.z1; ++cz) {
-            const uint32_t row = P.cell_base + (uint32_t)cz * (uint32_t)P.W;
-            c += b.w.gn_start[row + rr.x1 + 1] - b.w.gn_start[row + rr.x0];
-            c += b.gm_start[row + rr.x1 + 1] - b.gm_start[row + rr.x0];
+        for (int q = 0; q < 2; ++q) {
+            if (q >= R.n) break;
+            const Rect rr = q == 0 ? R.r[0] : R.r[1];
+            for (int cz = rr.z0; cz <= rr.z1; ++cz) {
+                const uint32_t row = P.cell_base + (uint32_t)cz * (uint32_t)P.W;
+                c += b.w.gn_start[row + rr.x1 + 1] - b.w.gn_start[row + rr.x0];
+                c += b.gm_start[row + rr.x1 + 1] - b.gm_start[row + rr.x0];
+            }
         }
     }
     b.cand[m] = c;
 }
 
 void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
-    const uint32_t C = b.w.cap, NC = b.w.ncells;
-    scan_exclusive<uint32_t, uint64_t>(b.pflag, b.pre, C, (const uint64_t*)&b.st->n_present, sc,
-                                       (uint64_t*)&b.st->movers_present, s);
-    hipLaunchKernelGGL(k_compact_grid_movers, dim3(nblk1(C, NT)), dim3(NT), 0, s, b);
-    if (b.m) {
-        hipLaunchKernelGGL(k_leaver_flags, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
-        scan_exclusive<uint32_t, uint64_t>(b.pflag, b.pre, b.m, nullptr, sc, (uint64_t*)&b.st->leavers, s);
-        hipLaunchKernelGGL(k_compact_leavers, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
-    } else {
-        hipLaunchKernelGGL(k_set_nmov, dim3(1), dim3(1), 0, s, b.st);
-    }
-    const uint64_t* nm = (const uint64_t*)&b.st->n_movers;
-    (void)hipMemsetAsync(b.gm_cnt, 0, ((size_t)NC + 1) * 4, s);
-    if (b.m) hipLaunchKernelGGL(k_gm_count, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
-    scan_exclusive<uint32_t, uint32_t>(b.gm_cnt, b.gm_start, (uint64_t)NC + 1, nullptr, sc, (uint32_t*)nullptr, s);
-    (void)hipMemcpyAsync(b.gm_cnt, b.gm_start, ((size_t)NC + 1) * 4, hipMemcpyDeviceToDevice, s);
-    if (b.m) {
-        hipLaunchKernelGGL(k_gm_scatter, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
-        hipLaunchKernelGGL(k_bounds, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
-        scan_exclusive<uint64_t, uint64_t>(b.cand, b.reg, b.m, nm, sc, (uint64_t*)&b.st->cand_total, s);
-    }
+    const uint64_t nmax = 2ull * b.m;
+    const uint64_t* ngm = (const uint64_t*)&b.st->n_gm;
+    hipLaunchKernelGGL(k_bounds, dim3(nblk1(nmax, NT)), dim3(NT), 0, s, b);
+    scan_exclusive<uint64_t, uint64_t>(b.cand, b.reg, nmax, ngm, sc, (uint64_t*)&b.st->cand_total, s);
 }
 
 // ---------------------------------------------------------------------------
-// diff: one wave per mover A.  For every candidate B in A's cells the old
-// relation (pre-tick positions and stamps) and the new one are evaluated;
-// r_old != r_new is an own event (A,B).  Non-movers come from gn (old = new
-// position), movers from the mover grid, where B's entry at its old cell
-// stands for the pair when r_old holds and its entry at the new cell when only
-// r_new does, so each pair is taken once.  The row ranges of both grids are
-// walked flattened (Flat), DIFF_U chunks of 64 candidates with their loads in
-// flight together.  Events (B<<1 | leave) go to A's region and are sorted
-// there: registers up to 64, LDS up to SORT_LDS, else a block sort later.
-// The count of new neighbours with a client is kept for the next collect.
+// diff: one wave per primary mover-grid entry (mover A).  For every candidate
+// B in A's cells the old relation (pre-tick positions and stamps) and the new
+// one are evaluated; r_old != r_new is an own event (A,B).  Non-movers come
+// from gn (old = new position), movers from the mover grid, where B's entry at
+// its old cell stands for the pair when r_old holds and its entry at the new
+// cell when only r_new does, so each pair is taken once.  The row ranges of
+// both grids are walked flattened (Flat), DIFF_U chunks of 64 candidates with
+// their loads in flight together.  Events (B<<1 | leave) go to A's region and
+// are sorted there: registers up to 64, LDS up to SORT_LDS, else a block sort
+// later.  The count of new neighbours with a client is kept for the collect.
 constexpr int DIFF_U = 2;
 
 struct Cand {
     float x, z, ox, oz;
     uint32_t slot;
-    uint32_t info;       // tags | gate << 8 | CAND_NONMOVER
+    uint32_t info;       // tags | CAND_CLIENT | CAND_NONMOVER
 };
 constexpr uint32_t CAND_NONMOVER = 1u << 31;
+constexpr uint32_t CAND_CLIENT = 1u << 30;
+constexpr uint32_t MIR_OWNER = 1u;   // in mir_rank: this event took the watcher's counter to zero
 
 __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * SORT_LDS];
-    const uint64_t nm = b.st->n_movers;
     const uint64_t m = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
-    if (m >= nm) return;
+    if (m >= b.st->n_gm) return;
+    const MEnt me = b.gm[m];
+    if (!(me.tags & TAG_PRIMARY)) return;
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
     const World& w = b.w;
-    const uint32_t A = b.movers[m];
-    const AoiEnt a = w.aoi[A];
-    const PrevEnt p = w.prev[A];
-    const SpaceP P = w.sp[a.meta & SPACE_MASK];
+    const uint64_t reg = b.reg[m], cap = b.cand[m];
+    if (reg + cap > b.own_cap) {                      // region past the buffers: the host redoes the diff
+        if (ln == 0) {
+            atomicOr(&b.st->overflow, 1ull);
+            b.mir_cnt[m] = 0;
+        }
+        return;
+    }
+    const uint32_t A = me.slot;
+    const SpaceP P = w.sp[me.space];
     const float d = P.d;
-    const bool pn = (a.meta & PRESENT_BIT) != 0, po = p.ox == p.ox;
-    const float nx = pn ? a.x : qnan(), nz = pn ? a.z : qnan();
-    const unsigned long long sA = w.stamp[A], soA = p.ostamp;
-    const Win wo = win_of(p.ox, p.oz, d), wn = win_of(nx, nz, d);
-    const Rects R = mover_rects(P, po, p.ox, p.oz, pn, nx, nz);
-    uint32_t* out = b.own + b.reg[m];
-    uint64_t* mir = b.mir + b.reg[m];
-    uint32_t* mrk = b.mir_rank + b.reg[m];
-    const uint64_t cap = b.cand[m];
+    const bool pn = me.x == me.x, po = me.ox == me.ox;
+    const unsigned long long sA = w.stamp[A], soA = w.prev[A].ostamp;
+    const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
+    const Rects R = mover_rects(P, po, me.ox, me.oz, pn, me.x, me.z);
+    uint32_t* out = b.own + reg;
+    uint64_t* mir = b.mir + reg;
     uint32_t n = 0, nl = 0, nm_ = 0;
     uint32_t c_old = 0, c_new = 0, c_band = 0, c_cli = 0;
     Flat f = flat_build<2>(P, R, w.gn_start, b.gm_start);
-    const uint32_t tested = f.total;
     for (uint32_t base = 0; base < f.total; base += 64u * DIFF_U) {
         uint32_t idx[DIFF_U], kd[DIFF_U];
         flat_map<DIFF_U, 2>(f, base, idx, kd);
@@ -340,12 +503,12 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
                     cc[u].x = cc[u].ox = e.x;
                     cc[u].z = cc[u].oz = e.z;
                     cc[u].slot = (e.meta & MOVER_BIT) ? A : e.slot;   // movers come from gm
-                    cc[u].info = TAG_OLD | TAG_NEW | ((e.meta & GATE_MASK) << 8) | CAND_NONMOVER;
+                    cc[u].info = TAG_OLD | TAG_NEW | (e.meta & CLIENT_BIT ? CAND_CLIENT : 0u) | CAND_NONMOVER;
                 } else {
                     const MEnt e = b.gm[idx[u]];
                     cc[u].x = e.x; cc[u].z = e.z; cc[u].ox = e.ox; cc[u].oz = e.oz;
                     cc[u].slot = e.slot;
-                    cc[u].info = e.tags | (e.gate << 8);
+                    cc[u].info = e.tags | (e.client ? CAND_CLIENT : 0u);
                 }
             }
         }
@@ -357,8 +520,8 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
             uint32_t key = 0;
             if (e.slot != A) {
                 nmv = (e.info & CAND_NONMOVER) != 0;
-                const bool iao = wo.has(e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, p.ox, p.oz);
-                const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, nx, nz);
+                const bool iao = wo.has(e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, me.ox, me.oz);
+                const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, me.x, me.z);
                 bool ro = iao, rn = ian;
                 if (iao != ibo || ian != ibn) {
                     const unsigned long long sb = w.stamp[e.slot];
@@ -369,27 +532,21 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
                 const bool take = ((e.info & TAG_OLD) && ro) || ((e.info & TAG_NEW) && rn && !ro);
                 if (take) {
                     c_old += ro; c_new += rn;
-                    c_cli += rn && (e.info & (GATE_MASK << 8)) != 0;
+                    c_cli += rn && (e.info & CAND_CLIENT) != 0;
                     ev = ro != rn;
                     lv = ro;
                     key = (e.slot << 1) | (lv ? 1u : 0u);
                 }
             }
             const bool mev = ev && nmv;
-            // B has no op: (B,A) is B's event too; its rank in B's segment
-            uint32_t rank = 0;
-            if (mev) {
-                const unsigned long long o = atomicAdd(&b.cnt64[e.slot], lv ? (1ull << 32) : 1ull);
-                rank = lv ? (uint32_t)hi32(o) : (uint32_t)lo32(o);
-            }
+            // B has no op: (B,A) is B's event too: count it (no return value,
+            // so the candidate loop never waits on the atomic)
+            if (mev) atomicAdd(&b.cnt64[e.slot], lv ? (1ull << 32) : 1ull);
             const uint64_t be = wave_ballot(ev), bl = wave_ballot(ev && lv), bm = wave_ballot(mev);
             const uint32_t at = n + (uint32_t)popc64(be & lt);
             if (ev && at < cap) out[at] = key;
             const uint32_t atm = nm_ + (uint32_t)popc64(bm & lt);
-            if (mev && atm < cap) {
-                mir[atm] = ((uint64_t)e.slot << 32) | (A << 1) | (lv ? 1u : 0u);
-                mrk[atm] = rank;
-            }
+            if (mev && atm < cap) mir[atm] = ((uint64_t)e.slot << 32) | (A << 1) | (lv ? 1u : 0u);
             n += (uint32_t)popc64(be);
             nl += (uint32_t)popc64(bl);
             nm_ += (uint32_t)popc64(bm);
@@ -419,10 +576,8 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
         if (n) b.cnt64[A] = (unsigned long long)(n - nl) | ((unsigned long long)nl << 32);
         b.mir_cnt[m] = nm_;
         if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | scl;
-        shard_add(b.st, A, SH_PAIRS, tested);
-        shard_add(b.st, A, SH_AOLD, so);
-        shard_add(b.st, A, SH_ANEW, sn);
-        shard_add(b.st, A, SH_BAND, sb);
+        shard_add(b.st, blockIdx.x, SH_AOLD, (unsigned long long)so | ((unsigned long long)sn << 32));
+        shard_add(b.st, blockIdx.x, SH_BAND, sb);
     }
 }
 
@@ -431,7 +586,7 @@ __global__ void __launch_bounds__(NT) k_big_own(TickBufs b) {
     const uint64_t nb = b.st->n_big;
     for (uint64_t k = blockIdx.x; k < nb; k += gridDim.x) {
         const uint32_t m = b.big[k];
-        const uint64_t c = b.cnt64[b.movers[m]];
+        const uint64_t c = b.cnt64[b.gm[m].slot];
         const uint32_t n = (uint32_t)(lo32(c) + hi32(c));
         bitonic_inplace<NT>(b.own + b.reg[m], n, (int)threadIdx.x, [](uint32_t v) { return v; },
                             [] { __syncthreads(); });
@@ -439,26 +594,20 @@ __global__ void __launch_bounds__(NT) k_big_own(TickBufs b) {
     }
 }
 
-void tick_diff(const TickBufs& b, uint64_t n_movers, hipStream_t s) {
-    if (!n_movers) return;
-    hipLaunchKernelGGL(k_mover, dim3(nblk(n_movers, NWAVE)), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_big_own, dim3(64), dim3(NT), 0, s, b);
-}
-
-// ---------------------------------------------------------------------------
-
 // movers copy their sorted own events into the canonical arrays and scatter
 // their mirror events to the op-less watchers' segments (offset + rank)
 __global__ void __launch_bounds__(NT) k_own_copy(TickBufs b) {
-    const uint64_t nmv = b.st->n_movers;
     const uint64_t m = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
-    if (m >= nmv) return;
+    if (m >= b.st->n_gm) return;
+    const MEnt me = b.gm[m];
+    if (!(me.tags & TAG_PRIMARY)) return;
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
-    const uint32_t A = b.movers[m];
+    const uint64_t reg = b.reg[m];
+    if (reg + b.cand[m] > b.own_cap) return;          // overflowed region (k_mover): nothing was written
+    const uint32_t A = me.slot;
     const uint64_t c = b.cnt64[A];
     const uint32_t n = (uint32_t)(lo32(c) + hi32(c));
-    const uint64_t reg = b.reg[m];
     if (n) {
         const uint64_t off = b.off64[A];
         const uint32_t* own = b.own + reg;
@@ -470,116 +619,163 @@ __global__ void __launch_bounds__(NT) k_own_copy(TickBufs b) {
             const bool lv = v && (key & 1u), en = v && !(key & 1u);
             const uint64_t be = wave_ballot(en), bl = wave_ballot(lv);
             gw_event ev; ev.watcher = A; ev.target = key >> 1;
-            if (en) { uint64_t at = lo32(off) + ie + popc64(be & lt); if (at < b.enter_cap) b.enter[at] = ev; }
-            if (lv) { uint64_t at = hi32(off) + il + popc64(bl & lt); if (at < b.leave_cap) b.leave[at] = ev; }
+            if (en) { uint64_t at = lo32(off) + ie + popc64(be & lt); if (at < b.ev_cap) b.enter[at] = ev; }
+            if (lv) { uint64_t at = hi32(off) + il + popc64(bl & lt); if (at < b.ev_cap) b.leave[at] = ev; }
             ie += (uint32_t)popc64(be);
             il += (uint32_t)popc64(bl);
         }
+        if (ln == 0) b.cnt64[A] = 0;
     }
+    // mirror events: the watcher's counter (its full count after the scan) is
+    // counted back down, the returned value is the event's rank in the
+    // segment and the event that reaches zero marks the segment's owner
     const uint32_t nmr = b.mir_cnt[m];
     for (uint32_t j = ln; j < nmr; j += 64) {
         const uint64_t v = b.mir[reg + j];
         const uint32_t W = (uint32_t)hi32(v), al = (uint32_t)lo32(v);
+        const unsigned long long inc = (al & 1u) ? (1ull << 32) : 1ull;
+        const unsigned long long o = atomicSub(&b.cnt64[W], inc);
         const uint64_t off = b.off64[W];
         gw_event ev; ev.watcher = W; ev.target = al >> 1;
-        if (al & 1u) { uint64_t at = hi32(off) + b.mir_rank[reg + j]; if (at < b.leave_cap) b.leave[at] = ev; }
-        else { uint64_t at = lo32(off) + b.mir_rank[reg + j]; if (at < b.enter_cap) b.enter[at] = ev; }
+        if (al & 1u) { uint64_t at = hi32(off) + hi32(o) - 1; if (at < b.ev_cap) b.leave[at] = ev; }
+        else { uint64_t at = lo32(off) + lo32(o) - 1; if (at < b.ev_cap) b.enter[at] = ev; }
+        b.mir_rank[reg + j] = o == inc ? MIR_OWNER : 0u;
     }
 }
 
-// op-less watchers: order their segments by target (the ranks came from
-// atomics): insertion sort by one thread up to INS_MAX entries, else the block
-// sort; every watcher's counter is cleared for the next tick
-__device__ __forceinline__ void ins_sort(gw_event* a, uint32_t n) {
-    for (uint32_t i = 1; i < n; ++i) {
-        const gw_event x = a[i];
-        uint32_t j = i;
-        while (j > 0 && a[j - 1].target > x.target) { a[j] = a[j - 1]; --j; }
-        a[j] = x;
+// Touched op-less watchers: their segments are ordered by target (the ranks
+// came from atomics).  The mirror event whose count-down reached zero owns
+// the watcher (MIR_OWNER).  A lane sorts an owned segment of up to REG_SORT
+// targets in its registers (bitonic network, indices fixed at compile time);
+// longer ones are loaded into the wave's lanes and sorted across them (up to
+// 64) or go to the block sort.  (The count-down left the counters at zero.)
+constexpr int REG_SORT = 16;
+template <int N>
+__device__ __forceinline__ void reg_sort(uint32_t (&v)[N]) {
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const bool up = (i & k) == 0;
+                    const uint32_t a = v[i], c = v[l];
+                    if ((a > c) == up) { v[i] = c; v[l] = a; }
+                }
+            }
+}
+__device__ __forceinline__ void lane_sort_segment(gw_event* seg, uint32_t n) {
+    uint32_t v[REG_SORT];
+#pragma unroll
+    for (int i = 0; i < REG_SORT; ++i) v[i] = i < (int)n ? seg[i].target : 0xffffffffu;
+    reg_sort<REG_SORT>(v);
+#pragma unroll
+    for (int i = 0; i < REG_SORT; ++i)
+        if (i < (int)n) seg[i].target = v[i];
+}
+__device__ __forceinline__ void wave_sort_segment(gw_event* seg, uint32_t n, uint32_t W) {
+    const int ln = lane_id();
+    uint32_t t = ln < (int)n ? seg[ln].target : 0xffffffffu;
+    t = wave_sort64(t);
+    if (ln < (int)n) {
+        gw_event e; e.watcher = W; e.target = t;
+        seg[ln] = e;
     }
 }
 __global__ void __launch_bounds__(NT) k_seg_fix(TickBufs b) {
-    const uint32_t s = blockIdx.x * NT + threadIdx.x;
-    if (s >= b.w.cap) return;
-    const uint64_t o0 = b.off64[s], o1 = b.off64[s + 1];
-    if (o0 == o1) return;
-    b.cnt64[s] = 0;
-    const uint32_t ne = (uint32_t)(lo32(o1) - lo32(o0)), nl = (uint32_t)(hi32(o1) - hi32(o0));
-    if (ne < 2 && nl < 2) return;
-    if (b.w.aoi[s].seq >= 0) return;                 // a mover: its own events are sorted
-    if (ne > INS_MAX || nl > INS_MAX) {
-        b.big[atomicAdd(&b.st->n_big, 1ull)] = s;
-        return;
+    const uint64_t m = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
+    if (m >= b.st->n_gm) return;
+    if (!(b.gm[m].tags & TAG_PRIMARY)) return;
+    const uint64_t reg = b.reg[m];
+    if (reg + b.cand[m] > b.own_cap) return;
+    const int ln = lane_id();
+    const uint32_t nmr = b.mir_cnt[m];
+    for (uint32_t base = 0; base < nmr; base += 64) {
+        const uint32_t j = base + ln;
+        const bool own = j < nmr && (b.mir_rank[reg + j] & MIR_OWNER);
+        uint32_t W = 0;
+        uint64_t o0 = 0, o1 = 0;
+        if (own) {
+            W = (uint32_t)hi32(b.mir[reg + j]);
+            o0 = b.off64[W];
+            o1 = b.off64[W + 1];
+        }
+        const uint32_t ne = (uint32_t)(lo32(o1) - lo32(o0)), nl = (uint32_t)(hi32(o1) - hi32(o0));
+        const bool big = own && (ne > 64 || nl > 64);
+        if (big) b.bigseg[atomicAdd(&b.st->n_bigseg, 1ull)] = W;           // rare
+        const bool small = own && !big && ne <= (uint32_t)REG_SORT && nl <= (uint32_t)REG_SORT;
+        if (small) {
+            if (ne > 1 && lo32(o0) + ne <= b.ev_cap) lane_sort_segment(b.enter + lo32(o0), ne);
+            if (nl > 1 && hi32(o0) + nl <= b.ev_cap) lane_sort_segment(b.leave + hi32(o0), nl);
+        }
+        uint64_t todo = wave_ballot(own && !big && !small);
+        while (todo) {
+            const int q = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t Wq = (uint32_t)__builtin_amdgcn_readlane((int)W, q);
+            const uint32_t eq = (uint32_t)__builtin_amdgcn_readlane((int)lo32(o0), q);
+            const uint32_t lq = (uint32_t)__builtin_amdgcn_readlane((int)hi32(o0), q);
+            const uint32_t neq = (uint32_t)__builtin_amdgcn_readlane((int)ne, q);
+            const uint32_t nlq = (uint32_t)__builtin_amdgcn_readlane((int)nl, q);
+            if (neq > 1 && (uint64_t)eq + neq <= b.ev_cap) wave_sort_segment(b.enter + eq, neq, Wq);
+            if (nlq > 1 && (uint64_t)lq + nlq <= b.ev_cap) wave_sort_segment(b.leave + lq, nlq, Wq);
+        }
     }
-    ins_sort(b.enter + lo32(o0), ne);
-    ins_sort(b.leave + hi32(o0), nl);
 }
 
-__global__ void k_n_big_mark(DevStats* st) { st->scratch = st->n_big; }
-
-void tick_events(const TickBufs& b, uint64_t n_movers, ScanCtx& sc, hipStream_t s) {
-    const uint32_t C = b.w.cap;
-    scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.cnt64, b.off64, (uint64_t)C + 1, nullptr, sc,
-                                       (uint64_t*)&b.st->ev_pk, s);
-    if (n_movers) hipLaunchKernelGGL(k_own_copy, dim3(nblk(n_movers, NWAVE)), dim3(NT), 0, s, b);
-    // big-own entries sit in b.big[0, n_big); op-less ones are appended after
-    hipLaunchKernelGGL(k_n_big_mark, dim3(1), dim3(1), 0, s, b.st);
-    hipLaunchKernelGGL(k_seg_fix, dim3(nblk1(C, NT)), dim3(NT), 0, s, b);
-}
-
-// block sort of op-less segments longer than INS_MAX (by target); they follow
-// the big-own entries in b.big, from the index kept in st->scratch
-__global__ void __launch_bounds__(NT) k_big_seg_dev(TickBufs b) {
-    const uint64_t first = b.st->scratch, nb = b.st->n_big;
-    for (uint64_t k = first + blockIdx.x; k < nb; k += gridDim.x) {
-        const uint32_t B = b.big[k];
+// block sort of op-less segments longer than 64 (by target)
+__global__ void __launch_bounds__(NT) k_big_seg(TickBufs b) {
+    const uint64_t nb = b.st->n_bigseg;
+    for (uint64_t k = blockIdx.x; k < nb; k += gridDim.x) {
+        const uint32_t B = b.bigseg[k];
         const uint64_t o0 = b.off64[B], o1 = b.off64[B + 1];
         auto key = [](const gw_event& e) { return e.target; };
         auto sy = [] { __syncthreads(); };
-        bitonic_inplace<NT>(b.enter + lo32(o0), (uint32_t)(lo32(o1) - lo32(o0)), (int)threadIdx.x, key, sy);
-        bitonic_inplace<NT>(b.leave + hi32(o0), (uint32_t)(hi32(o1) - hi32(o0)), (int)threadIdx.x, key, sy);
+        const uint32_t ne = (uint32_t)(lo32(o1) - lo32(o0)), nl = (uint32_t)(hi32(o1) - hi32(o0));
+        if (lo32(o0) + ne <= b.ev_cap) bitonic_inplace<NT>(b.enter + lo32(o0), ne, (int)threadIdx.x, key, sy);
+        if (hi32(o0) + nl <= b.ev_cap) bitonic_inplace<NT>(b.leave + hi32(o0), nl, (int)threadIdx.x, key, sy);
         __syncthreads();
     }
 }
-void tick_sort_big_segments(const TickBufs& b, hipStream_t s) {
-    hipLaunchKernelGGL(k_big_seg_dev, dim3(64), dim3(NT), 0, s, b);
+
+void tick_diff(const TickBufs& b, hipStream_t s) {
+    const uint64_t nmax = 2ull * b.m;
+    hipLaunchKernelGGL(k_mover, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_big_own, dim3(64), dim3(NT), 0, s, b);
+}
+void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
+    const uint64_t nmax = 2ull * b.m;
+    const uint32_t C = b.w.cap;
+    scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.cnt64, b.off64, (uint64_t)C + 1, nullptr, sc,
+                                       (uint64_t*)&b.st->ev_pk, s);
+    hipLaunchKernelGGL(k_own_copy, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_seg_fix, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_big_seg, dim3(64), dim3(NT), 0, s, b);
 }
 
 // ---------------------------------------------------------------------------
+// after the tick: per-op dedupe state of every op's slot back to -1 (thread
+// i: op i); MOVER bits cleared at the movers' new grid entries (thread i:
+// mover-grid entry i)
 __global__ void __launch_bounds__(NT) k_tick_reset(TickBufs b) {
-    uint32_t i = blockIdx.x * NT + threadIdx.x;
-    if (i >= b.m) return;
-    uint32_t s = b.ops[i].slot;
-    if (s >= b.w.cap) return;
-    b.last_pos[s] = -1;
-    b.last_aoi[s] = -1;
-    b.last_leave[s] = -1;
-    b.w.aoi[s].seq = -1;
-}
-void tick_reset(const TickBufs& b, uint64_t n_movers, hipStream_t s) {
-    (void)n_movers;
-    tick_sort_big_segments(b, s);
-    if (b.m) hipLaunchKernelGGL(k_tick_reset, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
-}
-
-__global__ void __launch_bounds__(NT) k_stats_reduce(DevStats* st) {
-    __shared__ unsigned long long l[NWAVE];
-    unsigned long long tot[SH_FIELDS];
-    for (int f = 0; f < SH_FIELDS; ++f) {
-        unsigned long long v = st->shard[threadIdx.x][f], tt;
-        block_excl_scan<unsigned long long>(v, l, tt);
-        tot[f] = tt;
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i < b.m) {
+        const uint32_t s = b.ops[i].slot;
+        if (s < b.w.cap) {
+            b.last_pos[s] = -1;
+            b.last_aoi[s] = -1;
+            b.last_leave[s] = -1;
+        }
     }
-    if (threadIdx.x == 0) {
-        st->pairs_tested = tot[SH_PAIRS];
-        st->a_old = tot[SH_AOLD];
-        st->a_new = tot[SH_ANEW];
-        st->band = tot[SH_BAND];
+    if (i < b.st->n_gm) {
+        const MEnt e = b.gm[i];
+        if (e.tags & TAG_NEW) b.w.gn[b.w.gidx[e.slot]].meta &= ~MOVER_BIT;
     }
 }
-void stats_reduce(DevStats* st, hipStream_t s) {
-    static_assert(STAT_SHARDS == NT, "one thread per shard");
-    hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(NT), 0, s, st);
+void tick_reset(const TickBufs& b, hipStream_t s) {
+    hipLaunchKernelGGL(k_tick_reset, dim3(nblk1(2ull * b.m, NT)), dim3(NT), 0, s, b);
 }
 
 }  // namespace gw

@@ -1,11 +1,11 @@
 // capi.cpp — C ABI of include/gpuaoi.h on one HIP device.
 //
 // Host orchestration of the per-tick pipeline (kernels in aoi.hip, sync.hip):
-//   ops -> grid (stable radix sort by cell) -> movers in grid order + leavers
-//   -> mover grid + per-mover candidate bounds [the one mid-tick host sync:
-//   size the own-event regions and the event arrays] -> diff (one wave per
-//   mover) -> op-less count pass -> per-watcher scan -> own copy + op-less
-//   write pass -> big-segment sorts -> reset.
+//   ops -> incremental grid (patch / shift / re-sort dirty cells) + mover grid
+//   -> per-mover candidate bounds + scan -> diff (one wave per mover) ->
+//   per-watcher scan -> own copy + mirror scatter -> segment sorts
+//   [the one host sync: counts; if the event regions overflowed their
+//   capacity, grow and rerun diff + events] -> reset (async).
 // No neighbour lists are kept (gw_internal.hpp): collect and queries evaluate
 // relations from the current grid.  No torch, no CPU fallback: every compute
 // step is a HIP kernel.
@@ -67,6 +67,8 @@ struct gw_ctx {
     int cells_per_d = 2;                 // grid cells per AOI distance (GW_CELLS_PER_D)
     bool grid_dirty = true;              // gn/gn_start must be rebuilt before queries
     uint64_t h_present = 0;
+    uint64_t own_cap = 0;                // capacity of the own-event regions (grows on overflow)
+    bool cells_zero = false;             // dep / arr / gm_cnt hold zeros
 
     // persistent device state (slot-indexed)
     AoiEnt* aoi = nullptr;
@@ -78,7 +80,12 @@ struct gw_ctx {
     unsigned long long* cnt64 = nullptr;     // [slot_cap + 1], zero between ticks
     unsigned long long* nbc = nullptr;       // [slot_cap] epoch<<32 | neighbours with a client
     int32_t *last_pos = nullptr, *last_aoi = nullptr, *last_leave = nullptr;
-    GEnt* gn = nullptr;
+    GEnt* gnb[2] = {nullptr, nullptr};   // grid ping-pong (gnb[gcur] is current)
+    uint32_t* gsb[2] = {nullptr, nullptr};  // cell starts ping-pong
+    int gcur = 0;
+    uint32_t cells_cap = 0;              // words in each per-cell array
+    uint32_t *dep = nullptr, *arr = nullptr, *gm_cnt = nullptr, *cnt_new = nullptr, *dirty = nullptr,
+             *bigcell = nullptr, *gm_start = nullptr;
     uint32_t* gidx = nullptr;
     SpaceP* sp_dev = nullptr;
     uint32_t sp_cap = 0;
@@ -87,7 +94,7 @@ struct gw_ctx {
     DevStats* hstats = nullptr;    // pinned host
 
     // grid + tick scratch
-    DevBuf gn_start, ops_buf, k0, v0, k1, v1, pflag, pre, movers, gm_cnt, gm_start, gm, cand, reg, own, big;
+    DevBuf ops_buf, k0, v0, k1, v1, gm, cand, reg, own, big, bigseg;
     DevBuf mir, mir_rank, mir_cnt;
     DevBuf off64, enter_d, leave_d, scan_status, rs_hist;
     ScanCtx sc{};                  // single-pass scan state (prim.hpp)
@@ -200,8 +207,10 @@ int ceil_log2(uint64_t v) {   // bits needed to represent values in [0, v)
 }
 
 // ---- profiling ------------------------------------------------------------
+// Stage events accumulate over calls until gw_get_stage_times reads them
+// (after the caller's own sync), so timing adds no host sync to a tick.
 void prof_begin(gw_ctx* c, const char* name) {
-    if (!c->prof) return;
+    if (!c->prof || c->nstage >= GW_MAX_STAGES) return;
     if (c->nstage >= c->stages.size()) {
         Stage s{};
         (void)hipEventCreate(&s.a);
@@ -214,13 +223,11 @@ void prof_begin(gw_ctx* c, const char* name) {
     (void)hipEventRecord(s.a, c->st);
 }
 size_t prof_end(gw_ctx* c, uint64_t bytes) {
-    if (!c->prof) return 0;
+    if (!c->prof || c->nstage >= GW_MAX_STAGES) return GW_MAX_STAGES;
     Stage& s = c->stages[c->nstage];
     s.bytes = bytes;
     (void)hipEventRecord(s.b, c->st);
-    size_t idx = c->nstage;
-    if (c->nstage + 1 < GW_MAX_STAGES) c->nstage++;
-    return idx;
+    return c->nstage++;
 }
 void prof_set_bytes(gw_ctx* c, size_t idx, uint64_t bytes) {
     if (c->prof && idx < c->stages.size()) c->stages[idx].bytes = bytes;
@@ -228,7 +235,7 @@ void prof_set_bytes(gw_ctx* c, size_t idx, uint64_t bytes) {
 void prof_collect(gw_ctx* c) {
     gw_stage_times& t = c->last_times;
     t.n = 0;
-    if (!c->prof) return;
+    if (c->nstage) (void)hipEventSynchronize(c->stages[c->nstage - 1].b);
     for (size_t i = 0; i < c->nstage && i < GW_MAX_STAGES; ++i) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, c->stages[i].a, c->stages[i].b);
@@ -237,6 +244,7 @@ void prof_collect(gw_ctx* c) {
         t.bytes_alg[t.n] = c->stages[i].bytes;
         t.n++;
     }
+    c->nstage = 0;
 }
 
 // status words for scans of up to n elements (zeroed when reallocated: zero
@@ -282,7 +290,8 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->last_pos, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_aoi, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_leave, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->gn, 0, nc))) return rc;        // rebuilt (grid_dirty)
+    if ((rc = grow_preserve(c, c->gnb[0], 0, nc))) return rc;    // rebuilt (grid_dirty)
+    if ((rc = grow_preserve(c, c->gnb[1], 0, nc))) return rc;
     if ((rc = grow_preserve(c, c->gidx, 0, nc))) return rc;
     size_t n = nc - oc;
     HIPCHK(hipMemsetAsync(c->aoi + oc, 0, n * sizeof(AoiEnt), c->st));
@@ -330,9 +339,15 @@ int upload_spaces(gw_ctx* c) {
 }
 
 int read_stats(gw_ctx* c) {
-    HIPCHK(hipMemcpyAsync(c->hstats, c->stats, offsetof(DevStats, shard), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(c->hstats, c->stats, sizeof(DevStats), hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
+}
+
+unsigned long long shard_sum(const DevStats& s, int f) {
+    unsigned long long t = 0;
+    for (int i = 0; i < STAT_SHARDS; ++i) t += s.shard[i][f];
+    return t;
 }
 
 void reset_stats_host(gw_ctx* c) { memset(c->hstats, 0, sizeof(DevStats)); }
@@ -343,40 +358,63 @@ World world(gw_ctx* c) {
     w.ncells = c->total_cells;
     w.sp = c->sp_dev;
     w.aoi = c->aoi; w.prev = c->prev; w.stamp = c->stamp; w.pos = c->pos; w.flags = c->flags; w.gate = c->gate;
-    w.gn = c->gn; w.gn_start = P<uint32_t>(c->gn_start); w.gidx = c->gidx;
+    w.gn = c->gnb[c->gcur]; w.gn_start = c->gsb[c->gcur]; w.gidx = c->gidx;
     w.nbc = c->nbc;
     w.epoch = c->epoch;
     return w;
 }
 
-int ensure_grid_bufs(gw_ctx* c, uint64_t CM) {
-    const uint32_t C = c->total_slots, NC = c->total_cells;
-    int rc;
-    if ((rc = ensure(c, c->gn_start, ((size_t)NC + 2) * 4)) || (rc = ensure(c, c->k0, (size_t)C * 4)) ||
-        (rc = ensure(c, c->v0, (size_t)C * 4)) || (rc = ensure(c, c->k1, (size_t)C * 4)) ||
-        (rc = ensure(c, c->v1, (size_t)C * 4)) || (rc = ensure(c, c->pflag, CM * 4)) ||
-        (rc = ensure(c, c->pre, CM * 8)) || (rc = ensure_scan(c, std::max<uint64_t>(CM, NC) + 1)))
-        return rc;
+// per-cell arrays for total_cells (+2); dep / arr / gm_cnt must hold zeros
+// between ticks (their counters return to zero inside a tick)
+int ensure_cells(gw_ctx* c) {
+    const uint32_t need = c->total_cells + 2;
+    if (c->cells_cap < need) {
+        const uint32_t nc = std::max(need, c->cells_cap + c->cells_cap / 2);
+        uint32_t** arrs[] = {&c->gsb[0], &c->gsb[1], &c->dep, &c->arr, &c->gm_cnt, &c->cnt_new, &c->dirty,
+                             &c->bigcell, &c->gm_start};
+        HIPCHK(hipStreamSynchronize(c->st));
+        for (uint32_t** a : arrs) {
+            if (*a) HIPCHK(hipFree(*a));
+            *a = nullptr;
+        }
+        for (uint32_t** a : arrs) {
+            if (hipMalloc(a, (size_t)nc * 4) != hipSuccess) {
+                (void)hipGetLastError();
+                c->cells_cap = 0;
+                return set_err(c, GW_ENOMEM, "hipMalloc(%zu) failed", (size_t)nc * 4);
+            }
+        }
+        c->cells_cap = nc;
+        c->cells_zero = false;
+        c->grid_dirty = true;
+    }
+    if (!c->cells_zero) {
+        HIPCHK(hipMemsetAsync(c->dep, 0, (size_t)c->cells_cap * 4, c->st));
+        HIPCHK(hipMemsetAsync(c->arr, 0, (size_t)c->cells_cap * 4, c->st));
+        HIPCHK(hipMemsetAsync(c->gm_cnt, 0, (size_t)c->cells_cap * 4, c->st));
+        c->cells_zero = true;
+    }
     return 0;
 }
 
-// rebuild the current grid without a tick (new spaces/cells, queries)
+// rebuild the current grid from the slot state (new spaces / cells)
 int rebuild_grid(gw_ctx* c) {
+    int rc;
+    if ((rc = ensure_cells(c))) return rc;
     if (!c->grid_dirty) return 0;
     const uint32_t C = c->total_slots;
-    int rc;
-    if ((rc = ensure_grid_bufs(c, C))) return rc;
+    if ((rc = ensure(c, c->k0, (size_t)C * 4)) || (rc = ensure(c, c->v0, (size_t)C * 4)) ||
+        (rc = ensure(c, c->k1, (size_t)C * 4)) || (rc = ensure(c, c->v1, (size_t)C * 4)))
+        return rc;
     RadixTmp rt;
     if ((rc = radix_tmp(c, C, rt))) return rc;
     reset_stats_host(c);
     HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
-    TickBufs b{};
-    b.w = world(c);
-    b.st = c->stats;
-    b.k0 = P<uint32_t>(c->k0); b.v0 = P<uint32_t>(c->v0); b.k1 = P<uint32_t>(c->k1); b.v1 = P<uint32_t>(c->v1);
-    b.pflag = nullptr;
-    if (C) tick_grid(b, rt, ceil_log2((uint64_t)c->total_cells + 1), c->st);
-    else HIPCHK(hipMemsetAsync(c->gn_start.p, 0, ((size_t)c->total_cells + 1) * 4, c->st));
+    if (C)
+        grid_rebuild(world(c), c->stats, P<uint32_t>(c->k0), P<uint32_t>(c->v0), P<uint32_t>(c->k1),
+                     P<uint32_t>(c->v1), rt, ceil_log2((uint64_t)c->total_cells + 1), c->st);
+    else
+        HIPCHK(hipMemsetAsync(c->gsb[c->gcur], 0, ((size_t)c->total_cells + 1) * 4, c->st));
     HIPCHK(hipGetLastError());
     if ((rc = read_stats(c))) return rc;
     c->h_present = c->hstats->n_present;
@@ -464,8 +502,8 @@ void gw_shutdown(gw_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    DevBuf* bufs[] = {&c->gn_start, &c->ops_buf, &c->k0, &c->v0, &c->k1, &c->v1, &c->pflag, &c->pre, &c->movers,
-                      &c->gm_cnt, &c->gm_start, &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->off64, &c->mir,
+    DevBuf* bufs[] = {&c->ops_buf, &c->k0, &c->v0, &c->k1, &c->v1, &c->bigseg,
+                      &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->off64, &c->mir,
                       &c->mir_rank, &c->mir_cnt,
                       &c->enter_d, &c->leave_d, &c->scan_status, &c->rs_hist,
                       &c->flag_mark, &c->flag_pre, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
@@ -474,7 +512,8 @@ void gw_shutdown(gw_ctx* c) {
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
     void* ps[] = {c->sc.ticket, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->nbc, c->last_pos, c->last_aoi,
-                  c->last_leave, c->gn, c->gidx, c->sp_dev, c->stats, c->scal32};
+                  c->last_leave, c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->scal32, c->gsb[0],
+                  c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->bigcell, c->gm_start};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     for (auto& s : c->stages) { (void)hipEventDestroy(s.a); (void)hipEventDestroy(s.b); }
@@ -595,10 +634,9 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     if (!c || !out) return GW_EINVAL;
     (void)hipSetDevice(c->dev);
     memset(out, 0, sizeof *out);
-    c->nstage = 0;
     uint64_t M64 = 0;
     for (auto& s : c->segs) M64 += s.n;
-    if (M64 >= (1ull << 31)) return set_err(c, GW_ERANGE, "too many ops in one tick");
+    if (M64 >= (1ull << 30)) return set_err(c, GW_ERANGE, "too many ops in one tick");
     const uint32_t M = (uint32_t)M64;
     const uint32_t C = c->total_slots;
     int rc;
@@ -609,6 +647,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         c->pend_host.clear();
         return 0;
     }
+    if ((rc = rebuild_grid(c))) return rc;           // the pre-tick grid (syncs only when dirty)
     // ---- the tick's op stream, in submission order -----------------------
     const gw_op* ops = nullptr;
     if (c->segs.size() == 1 && !c->segs[0].host) {
@@ -628,16 +667,26 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         ops = P<gw_op>(c->ops_buf);
     }
     const uint32_t NC = c->total_cells;
-    const uint64_t CM = std::max<uint64_t>(C, M);
-    // ---- buffers whose size is known before the tick ----------------------
-    RadixTmp rt;
-    if ((rc = ensure_grid_bufs(c, CM)) || (rc = radix_tmp(c, C, rt)) ||
-        (rc = ensure(c, c->movers, (size_t)M * 4)) || (rc = ensure(c, c->gm_cnt, ((size_t)NC + 1) * 4)) ||
-        (rc = ensure(c, c->gm_start, ((size_t)NC + 1) * 4)) || (rc = ensure(c, c->gm, (size_t)2 * M * sizeof(MEnt))) ||
-        (rc = ensure(c, c->cand, (size_t)M * 8)) || (rc = ensure(c, c->reg, (size_t)M * 8)) ||
-        (rc = ensure(c, c->big, ((size_t)M + C) * 4)) || (rc = ensure(c, c->off64, ((size_t)C + 2) * 8)) ||
-        (rc = ensure(c, c->mir_cnt, (size_t)M * 4)))
+    const uint64_t M2 = 2ull * M;
+    // ---- buffers (event regions sized from the last tick; grown on overflow)
+    c->own_cap = std::max<uint64_t>(c->own_cap, 64ull * M + 4096);
+    if ((rc = ensure(c, c->gm, M2 * sizeof(MEnt))) ||
+        (rc = ensure(c, c->cand, M2 * 8)) || (rc = ensure(c, c->reg, M2 * 8)) ||
+        (rc = ensure(c, c->mir_cnt, M2 * 4)) || (rc = ensure(c, c->big, M2 * 4)) ||
+        (rc = ensure(c, c->bigseg, (size_t)C * 4)) ||
+        (rc = ensure(c, c->off64, ((size_t)C + 2) * 8)) ||
+        (rc = ensure_scan(c, std::max<uint64_t>(std::max<uint64_t>(M2, (uint64_t)C + 1), (uint64_t)NC + 1))))
         return rc;
+    auto ensure_events = [&]() -> int {
+        int r;
+        if ((r = ensure(c, c->own, c->own_cap * 4)) || (r = ensure(c, c->mir, c->own_cap * 8)) ||
+            (r = ensure(c, c->mir_rank, c->own_cap * 4)) ||
+            (r = ensure(c, c->enter_d, 2 * c->own_cap * sizeof(gw_event))) ||
+            (r = ensure(c, c->leave_d, 2 * c->own_cap * sizeof(gw_event))))
+            return r;
+        return 0;
+    };
+    if ((rc = ensure_events())) return rc;
     reset_stats_host(c);
     HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
     DevStats* st = c->stats;
@@ -647,83 +696,105 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.ops = ops; b.m = M; b.stamp_base = c->stamp_base;
     b.last_pos = c->last_pos; b.last_aoi = c->last_aoi; b.last_leave = c->last_leave;
     b.st = st;
-    b.k0 = P<uint32_t>(c->k0); b.v0 = P<uint32_t>(c->v0); b.k1 = P<uint32_t>(c->k1); b.v1 = P<uint32_t>(c->v1);
-    b.pflag = P<uint32_t>(c->pflag); b.pre = P<uint64_t>(c->pre);
-    b.movers = P<uint32_t>(c->movers); b.gm_cnt = P<uint32_t>(c->gm_cnt); b.gm_start = P<uint32_t>(c->gm_start);
-    b.gm = P<MEnt>(c->gm); b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg); b.big = P<uint32_t>(c->big);
+    b.gn_nxt = c->gnb[c->gcur ^ 1]; b.start_nxt = c->gsb[c->gcur ^ 1];
+    b.dep = c->dep; b.arr = c->arr; b.cnt_new = c->cnt_new; b.bigcell = c->bigcell;
+    b.gm_cnt = c->gm_cnt; b.gm_start = c->gm_start; b.gm = P<MEnt>(c->gm);
+    b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg);
+    b.mir_cnt = P<uint32_t>(c->mir_cnt); b.big = P<uint32_t>(c->big);
+    b.bigseg = P<uint32_t>(c->bigseg);
     b.cnt64 = c->cnt64; b.off64 = P<uint64_t>(c->off64);
+    auto bind_events = [&]() {
+        b.own_cap = c->own_cap;
+        b.own = P<uint32_t>(c->own); b.mir = P<uint64_t>(c->mir); b.mir_rank = P<uint32_t>(c->mir_rank);
+        b.enter = P<gw_event>(c->enter_d); b.leave = P<gw_event>(c->leave_d);
+        b.ev_cap = 2 * c->own_cap;
+    };
+    bind_events();
 
     prof_begin(c, "ops");
     tick_ops(b, c->st);
     prof_end(c, (uint64_t)M * 24);
     prof_begin(c, "grid");
-    tick_grid(b, rt, ceil_log2((uint64_t)NC + 1), c->st);
+    c->cells_zero = false;                           // counters are in flight until the grid stage ends
+    tick_grid(b, c->sc, c->st);
+    c->cells_zero = true;
     size_t s_grid = prof_end(c, 0);
+    c->gcur ^= 1;                                    // the new grid is current from here on
+    b.w = world(c);
     prof_begin(c, "movers");
     tick_movers(b, c->sc, c->st);
     size_t s_movers = prof_end(c, 0);
-    HIPCHK(hipGetLastError());
-    // ---- the one mid-tick host sync ---------------------------------------
-    if ((rc = read_stats(c))) return rc;
-    DevStats hs0 = *c->hstats;
-    if (hs0.bad_ops) return set_err(c, GW_EINVAL, "%llu ops with bad slot/kind", hs0.bad_ops);
-    const uint64_t n_mov = hs0.n_movers;
-    const uint64_t ctot = std::max<uint64_t>(hs0.cand_total, 1);
-    // own events <= candidates; each op-less event mirrors an own event of a
-    // mover (the relation is symmetric), so each stream holds <= 2 * ctot
-    if ((rc = ensure(c, c->own, ctot * 4)) || (rc = ensure(c, c->mir, ctot * 8)) ||
-        (rc = ensure(c, c->mir_rank, ctot * 4)) || (rc = ensure(c, c->enter_d, 2 * ctot * sizeof(gw_event))) ||
-        (rc = ensure(c, c->leave_d, 2 * ctot * sizeof(gw_event))))
-        return rc;
-    b.own = P<uint32_t>(c->own);
-    b.mir = P<uint64_t>(c->mir); b.mir_rank = P<uint32_t>(c->mir_rank); b.mir_cnt = P<uint32_t>(c->mir_cnt);
-    b.enter = P<gw_event>(c->enter_d); b.leave = P<gw_event>(c->leave_d);
-    b.enter_cap = 2 * ctot; b.leave_cap = 2 * ctot;
-
     prof_begin(c, "diff");
-    tick_diff(b, n_mov, c->st);
+    tick_diff(b, c->st);
     size_t s_diff = prof_end(c, 0);
     prof_begin(c, "events");
-    tick_events(b, n_mov, c->sc, c->st);
+    tick_events(b, c->sc, c->st);
     size_t s_events = prof_end(c, 0);
+    HIPCHK(hipGetLastError());
+    // ---- the one host sync --------------------------------------------------
+    if ((rc = read_stats(c))) return rc;
+    if (c->hstats->overflow) {
+        // the own-event regions did not fit: grow to the exact bound, clear the
+        // per-watcher counters and rerun diff + events (their inputs are intact)
+        c->own_cap = c->hstats->cand_total + c->hstats->cand_total / 4 + 4096;
+        if ((rc = ensure_events())) return rc;
+        bind_events();
+        HIPCHK(hipMemsetAsync(c->cnt64, 0, ((size_t)C + 1) * 8, c->st));
+        DevStats* h = c->hstats;
+        h->overflow = 0; h->n_big = 0; h->n_bigseg = 0; h->ev_pk = 0;
+        memset(h->shard, 0, sizeof h->shard);
+        HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
+        if (s_diff < GW_MAX_STAGES) c->nstage = s_diff;
+        prof_begin(c, "diff");
+        tick_diff(b, c->st);
+        s_diff = prof_end(c, 0);
+        prof_begin(c, "events");
+        tick_events(b, c->sc, c->st);
+        s_events = prof_end(c, 0);
+        HIPCHK(hipGetLastError());
+        if ((rc = read_stats(c))) return rc;
+        if (c->hstats->overflow) return set_err(c, GW_ENOMEM, "event regions overflowed twice");
+    }
     prof_begin(c, "reset");
-    tick_reset(b, n_mov, c->st);
-    stats_reduce(st, c->st);
-    prof_end(c, (uint64_t)M * 40);
+    tick_reset(b, c->st);                            // asynchronous: the next call orders behind it
+    prof_end(c, (uint64_t)M * 24);
     HIPCHK(hipEventRecord(c->ev_t1, c->st));
     HIPCHK(hipGetLastError());
-    if ((rc = read_stats(c))) return rc;
     DevStats& hs = *c->hstats;
     c->segs.clear();
     c->pend_host.clear();
     c->stamp_base += M;
-    c->grid_dirty = false;
     c->h_present = hs.n_present;
+    if (hs.bad_ops) return set_err(c, GW_EINVAL, "%llu ops with bad slot/kind (ignored)", hs.bad_ops);
     const uint64_t n_enter = hs.ev_pk & 0xffffffffull, n_leave = hs.ev_pk >> 32;
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1);
-    out->device_us = ms * 1000.0;
+    const uint64_t n_mov = hs.n_movers;
+    // candidates tested == the candidate bounds; a_old | a_new << 32 per shard
+    const uint64_t pairs = hs.cand_total;
+    uint64_t a_old = 0, a_new = 0;
+    for (int i = 0; i < STAT_SHARDS; ++i) {
+        a_old += hs.shard[i][SH_AOLD] & 0xffffffffull;
+        a_new += hs.shard[i][SH_AOLD] >> 32;
+    }
     out->ops = M;
     out->movers = n_mov;
-    out->pairs_tested = hs.pairs_tested;
-    out->nbr_old = hs.a_old;
-    out->nbr_new = hs.a_new;
+    out->pairs_tested = pairs;
+    out->nbr_old = a_old;
+    out->nbr_new = a_new;
     out->enter_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->enter_d);
     out->leave_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->leave_d);
     out->n_enter = n_enter;
     out->n_leave = n_leave;
     // SURVEY 8(d) algorithmic bytes of the AOI part (records are counted by gw_sync_collect)
     const uint64_t n_evt = n_enter + n_leave;
-    out->bytes_alg = 20ull * n_mov + 8ull * hs.n_present + 4ull * (hs.a_old + hs.a_new) + 8ull * n_evt;
+    out->bytes_alg = 20ull * n_mov + 8ull * hs.n_present + 4ull * (a_old + a_new) + 8ull * n_evt;
     if (c->prof) {
-        // grid: keys + 3 radix passes (8 B in, 8 B out) + entries (16 B) + slot index
-        prof_set_bytes(c, s_grid, 20ull * C + 16ull * 3 * C + 20ull * hs.n_present + 4ull * NC);
-        prof_set_bytes(c, s_movers, 8ull * hs.n_present + 80ull * n_mov + 8ull * NC);
+        // grid: entries moved (16 B read + 16 B written + 4 B index) + per-cell counts (16 B)
+        prof_set_bytes(c, s_grid, 36ull * hs.n_present + 16ull * NC);
+        prof_set_bytes(c, s_movers, 40ull * hs.n_gm);
         // diff: candidates (16 B grid / 32 B mover grid; counted at 16 B) + own events (4 B)
-        prof_set_bytes(c, s_diff, 16ull * hs.pairs_tested + 4ull * n_evt);
-        // events: per-watcher counts and offsets (24 B per slot) + events (8 B) + own copies (4 B)
-        prof_set_bytes(c, s_events, 24ull * (C + 1) + 12ull * n_evt);
-        prof_collect(c);
+        prof_set_bytes(c, s_diff, 16ull * pairs + 4ull * n_evt);
+        // events: per-watcher counts and offsets (16 B per slot) + events (8 B) + own copies (4 B)
+        prof_set_bytes(c, s_events, 16ull * (C + 1) + 12ull * n_evt);
     }
     if ((flags & GW_TICK_COPY_TO_HOST) && !(flags & GW_TICK_NO_EVENTS)) {
         if ((rc = ensure_host(c, c->h_enter, std::max<uint64_t>(n_enter, 1) * sizeof(gw_event)))) return rc;
@@ -734,6 +805,12 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         out->enter = (const gw_event*)c->h_enter.p;
         out->leave = (const gw_event*)c->h_leave.p;
     }
+    float ms = 0;
+    if (flags & GW_TICK_COPY_TO_HOST) {                // synced above: the span is known
+        HIPCHK(hipEventSynchronize(c->ev_t1));
+        (void)hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1);
+    }
+    out->device_us = ms * 1000.0;
     return 0;
 }
 
@@ -741,7 +818,6 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     if (!c || !out) return GW_EINVAL;
     (void)hipSetDevice(c->dev);
     memset(out, 0, sizeof *out);
-    c->nstage = 0;
     const uint32_t C = c->total_slots;
     int rc;
     HIPCHK(hipEventRecord(c->ev_t0, c->st));
@@ -831,7 +907,6 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     if (c->prof) {
         prof_set_bytes(c, s_count, NF * 32);
         prof_set_bytes(c, s_write, 24ull * R + NF * 32);
-        prof_collect(c);
     }
     if (flags & GW_SYNC_COPY_TO_HOST) {
         if ((rc = ensure_host(c, c->h_rec, std::max<uint64_t>(R, 1) * sizeof(gw_sync_record)))) return rc;
@@ -891,6 +966,7 @@ int gw_set_profiling(gw_ctx* c, int enable) {
 
 int gw_get_stage_times(gw_ctx* c, gw_stage_times* out) {
     if (!c || !out) return GW_EINVAL;
+    prof_collect(c);                 // waits for the last recorded stage, then clears the record
     *out = c->last_times;
     return 0;
 }

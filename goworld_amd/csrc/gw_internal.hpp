@@ -21,40 +21,47 @@ namespace gw {
 // AOI state of one slot, 16 B (one dwordx4).  meta = space id | present<<31.
 struct alignas(16) AoiEnt {
     float x, z;        // aoi.x, aoi.y of go-aoi == Position.X, Position.Z
-    int32_t seq;       // index of the slot's last AOI op in the current tick, -1 otherwise
+    int32_t seq;       // unused (kept for the 16-B layout)
     uint32_t meta;
 };
 constexpr uint32_t PRESENT_BIT = 0x80000000u;
 constexpr uint32_t SPACE_MASK = 0x7fffffffu;
 
-// State of a mover before the tick, 16 B (valid while seq >= 0).  ox/oz are
-// NaN when the slot was absent, so every window test against them fails.
+// State of a mover before the tick, 16 B (written for this tick's movers).
+// ox/oz are NaN when the slot was absent, so every window test against them
+// fails.
 struct alignas(16) PrevEnt {
     float ox, oz;
     unsigned long long ostamp;
 };
 
-// Entity of the current grid (cell-sorted, slot order inside a cell), 16 B.
+// Entry of the grid (cell-sorted, slot order inside a cell), 16 B.
 struct alignas(16) GEnt {
     float x, z;
-    uint32_t slot;
-    uint32_t meta;     // gate (client gate id, 0 = none) | MOVER_BIT
+    uint32_t slot;     // DEPARTED: the entity left this cell during the tick being built
+    uint32_t meta;     // cell | CLIENT_BIT | MOVER_BIT
 };
-constexpr uint32_t MOVER_BIT = 0x80000000u;
-constexpr uint32_t GATE_MASK = 0xffffu;
+constexpr uint32_t MOVER_BIT = 0x80000000u;    // moved this tick (its pairs come from the mover grid)
+constexpr uint32_t CLIENT_BIT = 0x40000000u;   // has a client (GameClient != nil)
+constexpr uint32_t CELL_MASK = 0x3fffffffu;
+constexpr uint32_t DEPARTED = 0xffffffffu;
+constexpr uint32_t CELL_DIRTY = 0x80000000u;   // flag in dep[c]: the cell is re-sorted this tick
 
 // Entry of the mover grid, 32 B: a mover appears at the cell of its old
 // position (TAG_OLD) and at the cell of its new one (TAG_NEW), once with both
-// tags when the two cells agree.  Both positions travel with every entry.
+// tags when the two cells agree.  Both positions travel with every entry.  The
+// TAG_PRIMARY entry (the new one, or the old one of a leaver) is where the
+// mover's own diff runs, so movers are processed in cell order.
 struct alignas(16) MEnt {
-    float x, z, ox, oz;
-    uint32_t slot, tags, gate, pad1;
+    float x, z, ox, oz;          // NaN when absent after / before the tick
+    uint32_t slot, tags, client, space;
 };
-constexpr uint32_t TAG_OLD = 1u, TAG_NEW = 2u;
+constexpr uint32_t TAG_OLD = 1u, TAG_NEW = 2u, TAG_PRIMARY = 4u;
 
-// Per-space parameters (32 B).  Cells are squares of side cs = 1/inv_cs >= d:
-// a window spans at most 4x4 cells.  The cell function is monotone in x and z,
-// which keeps the candidate search exact whatever the float rounding.
+// Per-space parameters (32 B).  Cells are squares of side cs = 1/inv_cs >=
+// d / cells_per_d; a window spans at most 10 rows (capi.cpp).  The cell
+// function is monotone in x and z, which keeps the candidate search exact
+// whatever the float rounding.
 struct alignas(16) SpaceP {
     float d;
     float x0, z0, inv_cs;
@@ -65,31 +72,31 @@ struct alignas(16) SpaceP {
 
 constexpr int STAT_SHARDS = 256;
 constexpr int SH_FIELDS = 4;
-constexpr int SH_PAIRS = 0, SH_AOLD = 1, SH_ANEW = 2, SH_BAND = 3;
+constexpr int SH_AOLD = 1;    // a_old | a_new << 32 (per-shard sums stay below 2^32)
+constexpr int SH_BAND = 3;
 
 // Device-side counters of one tick / collect (read back once per call).
 struct DevStats {
     unsigned long long n_present;     // entities in the grid
-    unsigned long long movers_present;
-    unsigned long long leavers;
-    unsigned long long n_movers;      // movers_present + leavers
+    unsigned long long n_movers;      // distinct slots with an AOI op this tick
+    unsigned long long n_bigcell;     // dirty cells too large for one wave
     unsigned long long cand_total;    // sum of candidate bounds over movers
     unsigned long long n_gm;          // mover-grid entries
     unsigned long long ev_pk;         // sum of (enters | leaves<<32) over watchers
-    unsigned long long n_big;         // event segments left for the block sort
+    unsigned long long n_big;         // own-event segments left for the block sort
+    unsigned long long n_bigseg;      // op-less segments left for the block sort
+    unsigned long long overflow;      // event regions exceeded their capacity
     unsigned long long bad_ops;
-    unsigned long long pairs_tested, a_old, a_new, band;   // reduced from shards
     unsigned long long flagged;       // sync: flagged entities
     unsigned long long rec_total;     // sync: records
-    unsigned long long scratch;       // generic scan total sink
-    unsigned long long shard[STAT_SHARDS][SH_FIELDS];
+    unsigned long long shard[STAT_SHARDS][SH_FIELDS];   // summed on the host
 };
 
 // ---- primitives (prim.hpp; host wrappers in sync.hip) -----------------------
 // State of the single-pass scans of one context (one stream): the tile status
 // words, the monotonic tile ticket, and the host-side ticket base and tag.
 struct ScanCtx {
-    unsigned long long* status;   // [max_tiles]
+    unsigned long long* status;   // [max_tiles * scan_words()]
     unsigned long long* ticket;   // one word, never reset
     unsigned long long tbase;     // tickets handed out by earlier scans
     uint32_t tag;                 // tag of the last scan (status words of other tags are stale)
@@ -123,7 +130,7 @@ struct World {
     uint32_t* flags;           // syncInfoFlag
     uint16_t* gate;            // client gate, 0 = no client
     GEnt* gn;                  // [cap] current grid, n_present entries
-    uint32_t* gn_start;        // [ncells+1]
+    uint32_t* gn_start;        // [ncells+1] first entry of each cell
     uint32_t* gidx;            // [cap] index of the slot in gn
     // |{w related to e : w has a client}| as of the end of tick `epoch`
     // (epoch<<32 | count), written for every present mover by the diff; a
@@ -134,44 +141,53 @@ struct World {
 
 // ---- tick buffers handed to the launchers ----------------------------------
 struct TickBufs {
-    World w;
+    World w;                  // gn / gn_start: the grid before the tick (the new one from tick_movers on)
     const gw_op* ops;
     uint32_t m;               // ops in the stream
     unsigned long long stamp_base;
     int32_t *last_pos, *last_aoi, *last_leave;
     DevStats* st;
-    // grid build
-    uint32_t *k0, *v0, *k1, *v1;   // [cap] radix ping-pong (cell key, slot)
-    uint32_t* pflag;          // [max(cap, m)]
-    uint64_t* pre;            // [max(cap, m)]
-    // movers
-    uint32_t* movers;         // [m] slots, grid order then leavers
-    uint32_t* gm_cnt;         // [ncells+1] mover-grid histogram / cursor
+    // incremental grid: gn -> gn_nxt
+    GEnt* gn_nxt;             // [cap]
+    uint32_t* start_nxt;      // [ncells+1]
+    uint32_t* dep;            // [ncells] departures (| CELL_DIRTY), zero between ticks
+    uint32_t* arr;            // [ncells] arrivals, zero between ticks
+    uint32_t* cnt_new;        // [ncells+1] entries per cell after the tick
+    uint32_t* bigcell;        // [ncells] dirty cells for the block path
+    // mover grid (counting sort by cell; gm_cnt is zero between ticks)
+    uint32_t* gm_cnt;         // [ncells+1]
     uint32_t* gm_start;       // [ncells+1]
     MEnt* gm;                 // [2m]
-    uint64_t* cand;           // [m] candidate bound per mover
-    uint64_t* reg;            // [m] exclusive scan of cand
-    uint32_t* own;            // own events (target<<1 | leave), [cand_total]
+    // diff (indexed by mover-grid entry)
+    uint64_t* cand;           // [2m] candidate bound (0 unless TAG_PRIMARY)
+    uint64_t* reg;            // [2m] exclusive scan of cand
+    uint64_t own_cap;         // capacity of own / mir / mir_rank
+    uint32_t* own;            // own events (target<<1 | leave)
     uint64_t* mir;            // mirror events of op-less neighbours: watcher<<32 | mover<<1 | leave
-    uint32_t* mir_rank;       // rank of the mirror event in its watcher's segment
-    uint32_t* mir_cnt;        // [m] mirror events per mover
-    uint32_t* big;            // [m+cap] movers / watchers whose segment needs the block sort
+    uint32_t* mir_rank;       // MIR_OWNER flag of each mirror event (k_own_copy -> k_seg_fix)
+    uint32_t* mir_cnt;        // [2m] mirror events per entry
+    uint32_t* big;            // [2m] entries whose own events need the block sort
+    uint32_t* bigseg;         // [cap] op-less watchers whose segments need the block sort
     // canonical events
-    unsigned long long* cnt64;  // [cap+1] enters | leaves<<32 per watcher
+    unsigned long long* cnt64;  // [cap+1] enters | leaves<<32 per watcher, zero between ticks
     uint64_t* off64;          // [cap+1]
     gw_event* enter;
     gw_event* leave;
-    uint64_t enter_cap, leave_cap;
+    uint64_t ev_cap;          // capacity of enter and of leave
 };
 
 // ---- launchers --------------------------------------------------------------
+// full rebuild of the grid (spaces created, first use): stable radix sort of
+// (cell, slot) pairs into w.gn / w.gn_start; k0..v1 hold cap keys each
+void grid_rebuild(const World& w, DevStats* st, uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1,
+                  RadixTmp& rt, int key_bits, hipStream_t s);
+// one tick, in launch order (device-side counts only: no host sync inside)
 void tick_ops(const TickBufs& b, hipStream_t s);
-int tick_grid(const TickBufs& b, RadixTmp& rt, int key_bits, hipStream_t s);
-void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s);
-void tick_diff(const TickBufs& b, uint64_t n_movers, hipStream_t s);
-void tick_events(const TickBufs& b, uint64_t n_movers, ScanCtx& sc, hipStream_t s);
-void tick_reset(const TickBufs& b, uint64_t n_movers, hipStream_t s);
-void stats_reduce(DevStats* st, hipStream_t s);
+void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s);     // gn -> gn_nxt, start_nxt
+void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s);   // b.w: the new grid
+void tick_diff(const TickBufs& b, hipStream_t s);                  // own + mirror events per mover
+void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s);   // canonical event arrays
+void tick_reset(const TickBufs& b, hipStream_t s);                 // after the host read the counts
 
 void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n,
                         hipStream_t s);

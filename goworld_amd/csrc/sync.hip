@@ -14,7 +14,7 @@ namespace gw {
 
 // ---------------------------------------------------------------------------
 // neighbours of a present entity e from the current grid: calls
-// f(rel, w, gate) per lane for every candidate (rel: w != e is related to e).
+// f(rel, w, has_client) per lane for every candidate (rel: w != e is related to e).
 // The window's row ranges are walked flattened, NB_U chunks of 64 in flight.
 constexpr int NB_U = 4;
 template <typename F>
@@ -52,7 +52,7 @@ __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) 
                     rel = resolve(ia, ib, se, w.stamp[g.slot]);
                 }
             }
-            f(rel, g.slot, g.meta & GATE_MASK);
+            f(rel, g.slot, (g.meta & CLIENT_BIT) ? 1u : 0u);
         }
     }
 }
@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(NT) k_set_clients(World w, const uint32_t* slo
     w.gate[s] = gates[i];
     if (w.aoi[s].meta & PRESENT_BIT) {
         GEnt* g = w.gn + w.gidx[s];
-        if (g->slot == s) g->meta = (g->meta & ~GATE_MASK) | gates[i];
+        if (g->slot == s) g->meta = (g->meta & ~CLIENT_BIT) | (gates[i] ? CLIENT_BIT : 0u);
     }
 }
 void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n, hipStream_t s) {

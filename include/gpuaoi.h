@@ -118,7 +118,9 @@ typedef struct gw_tick_out {
     uint64_t pairs_tested;        /* candidate pairs evaluated                 */
     uint64_t nbr_old, nbr_new;    /* A_old / A_new: list entries of movers     */
     uint64_t bytes_alg;           /* SURVEY 8(d) algorithmic bytes of the AOI part */
-    double   device_us;           /* device time of the tick (HIP events)      */
+    double   device_us;           /* device time of the tick (HIP events); only
+                                     with GW_TICK_COPY_TO_HOST (0 otherwise: the
+                                     tick returns before its last kernels end) */
 } gw_tick_out;
 
 /* gw_sync_collect flags */
@@ -169,8 +171,11 @@ int  gw_sync_collect(gw_ctx* ctx, uint32_t flags, gw_sync_out* out);
  * full count even when it exceeds cap. */
 int  gw_neighbors(gw_ctx* ctx, uint32_t slot, uint32_t* buf, uint32_t cap, uint32_t* n);
 
-/* Per-stage device timings of the last tick / collect (HIP events on the
- * library's stream), for bench.py's roofline.  names[i] are static strings. */
+/* Per-stage device timings (HIP events on the library's stream), for
+ * bench.py's roofline.  Stages of successive gw_tick / gw_sync_collect calls
+ * accumulate (up to GW_MAX_STAGES) until gw_get_stage_times returns and
+ * clears them, so recording adds no host sync to a call.  names[i] are static
+ * strings. */
 #define GW_MAX_STAGES 32
 typedef struct gw_stage_times {
     uint32_t n;

@@ -446,10 +446,9 @@ void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
 // its old cell stands for the pair when r_old holds and its entry at the new
 // cell when only r_new does, so each pair is taken once.  The row ranges of
 // both grids are walked flattened (Flat), DIFF_U chunks of 64 candidates with
-// their loads in flight together.  Events (B<<1 | leave) go to A's region and
+// their loads in flight together (DIFF_U: GW_DIFF_U, default 2).  Events (B<<1 | leave) go to A's region and
 // are sorted there: registers up to 64, LDS up to SORT_LDS, else a block sort
 // later.  The count of new neighbours with a client is kept for the collect.
-constexpr int DIFF_U = 2;
 
 struct Cand {
     float x, z, ox, oz;
@@ -460,6 +459,7 @@ constexpr uint32_t CAND_NONMOVER = 1u << 31;
 constexpr uint32_t CAND_CLIENT = 1u << 30;
 constexpr uint32_t MIR_OWNER = 1u;   // in mir_rank: this event took the watcher's counter to zero
 
+template <int DIFF_U>
 __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * SORT_LDS];
     const uint64_t m = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
@@ -541,7 +541,9 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
             const bool mev = ev && nmv;
             // B has no op: (B,A) is B's event too: count it (no return value,
             // so the candidate loop never waits on the atomic)
+#ifndef GW_EXP_NO_MIR_ATOMIC
             if (mev) atomicAdd(&b.cnt64[e.slot], lv ? (1ull << 32) : 1ull);
+#endif
             const uint64_t be = wave_ballot(ev), bl = wave_ballot(ev && lv), bm = wave_ballot(mev);
             const uint32_t at = n + (uint32_t)popc64(be & lt);
             if (ev && at < cap) out[at] = key;
@@ -573,11 +575,13 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
     const uint32_t so = wave_sum<uint32_t>(c_old), sn = wave_sum<uint32_t>(c_new), sb = wave_sum<uint32_t>(c_band);
     const uint32_t scl = wave_sum<uint32_t>(c_cli);
     if (ln == 0) {
-        if (n) b.cnt64[A] = (unsigned long long)(n - nl) | ((unsigned long long)nl << 32);
+        b.cnt64[A] = (unsigned long long)(n - nl) | ((unsigned long long)nl << 32);
         b.mir_cnt[m] = nm_;
         if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | scl;
+#ifndef GW_EXP_NO_SHARD
         shard_add(b.st, blockIdx.x, SH_AOLD, (unsigned long long)so | ((unsigned long long)sn << 32));
         shard_add(b.st, blockIdx.x, SH_BAND, sb);
+#endif
     }
 }
 
@@ -595,7 +599,8 @@ __global__ void __launch_bounds__(NT) k_big_own(TickBufs b) {
 }
 
 // movers copy their sorted own events into the canonical arrays and scatter
-// their mirror events to the op-less watchers' segments (offset + rank)
+// their mirror events to the op-less watchers' segments.  Loads are issued in
+// independent batches ahead of the stores (vmcnt retires in issue order).
 __global__ void __launch_bounds__(NT) k_own_copy(TickBufs b) {
     const uint64_t m = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
     if (m >= b.st->n_gm) return;
@@ -603,19 +608,24 @@ __global__ void __launch_bounds__(NT) k_own_copy(TickBufs b) {
     if (!(me.tags & TAG_PRIMARY)) return;
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
-    const uint64_t reg = b.reg[m];
-    if (reg + b.cand[m] > b.own_cap) return;          // overflowed region (k_mover): nothing was written
     const uint32_t A = me.slot;
+    const uint64_t reg = b.reg[m], capm = b.cand[m];
+    const uint32_t nmr = b.mir_cnt[m];
     const uint64_t c = b.cnt64[A];
+    const uint64_t off = b.off64[A];
+    if (reg + capm > b.own_cap) return;               // overflowed region (k_mover): nothing was written
     const uint32_t n = (uint32_t)(lo32(c) + hi32(c));
+    // first chunks of both streams in flight together
+    const uint32_t* own = b.own + reg;
+    uint32_t key = (ln < (int)n) ? own[ln] : 0u;
+    uint64_t mv = (ln < (int)nmr) ? b.mir[reg + ln] : 0ull;
+    uint64_t moff = (ln < (int)nmr) ? b.off64[hi32(mv)] : 0ull;
     if (n) {
-        const uint64_t off = b.off64[A];
-        const uint32_t* own = b.own + reg;
         uint32_t ie = 0, il = 0;
         for (uint32_t base = 0; base < n; base += 64) {
             const uint32_t j = base + ln;
             const bool v = j < n;
-            const uint32_t key = v ? own[j] : 0;
+            if (base) key = v ? own[j] : 0u;
             const bool lv = v && (key & 1u), en = v && !(key & 1u);
             const uint64_t be = wave_ballot(en), bl = wave_ballot(lv);
             gw_event ev; ev.watcher = A; ev.target = key >> 1;
@@ -629,17 +639,21 @@ __global__ void __launch_bounds__(NT) k_own_copy(TickBufs b) {
     // mirror events: the watcher's counter (its full count after the scan) is
     // counted back down, the returned value is the event's rank in the
     // segment and the event that reaches zero marks the segment's owner
-    const uint32_t nmr = b.mir_cnt[m];
-    for (uint32_t j = ln; j < nmr; j += 64) {
-        const uint64_t v = b.mir[reg + j];
-        const uint32_t W = (uint32_t)hi32(v), al = (uint32_t)lo32(v);
-        const unsigned long long inc = (al & 1u) ? (1ull << 32) : 1ull;
-        const unsigned long long o = atomicSub(&b.cnt64[W], inc);
-        const uint64_t off = b.off64[W];
-        gw_event ev; ev.watcher = W; ev.target = al >> 1;
-        if (al & 1u) { uint64_t at = hi32(off) + hi32(o) - 1; if (at < b.ev_cap) b.leave[at] = ev; }
-        else { uint64_t at = lo32(off) + lo32(o) - 1; if (at < b.ev_cap) b.enter[at] = ev; }
-        b.mir_rank[reg + j] = o == inc ? MIR_OWNER : 0u;
+    for (uint32_t base = 0; base < nmr; base += 64) {
+        const uint32_t j = base + ln;
+        if (base && j < nmr) {
+            mv = b.mir[reg + j];
+            moff = b.off64[hi32(mv)];
+        }
+        if (j < nmr) {
+            const uint32_t W = (uint32_t)hi32(mv), al = (uint32_t)lo32(mv);
+            const unsigned long long inc = (al & 1u) ? (1ull << 32) : 1ull;
+            const unsigned long long o = atomicSub(&b.cnt64[W], inc);
+            gw_event ev; ev.watcher = W; ev.target = al >> 1;
+            if (al & 1u) { uint64_t at = hi32(moff) + hi32(o) - 1; if (at < b.ev_cap) b.leave[at] = ev; }
+            else { uint64_t at = lo32(moff) + lo32(o) - 1; if (at < b.ev_cap) b.enter[at] = ev; }
+            b.mir_rank[reg + j] = o == inc ? MIR_OWNER : 0u;
+        }
     }
 }
 
@@ -650,6 +664,9 @@ __global__ void __launch_bounds__(NT) k_own_copy(TickBufs b) {
 // longer ones are loaded into the wave's lanes and sorted across them (up to
 // 64) or go to the block sort.  (The count-down left the counters at zero.)
 constexpr int REG_SORT = 16;
+#ifndef GW_SEG_STATS
+#define GW_SEG_STATS 0
+#endif
 template <int N>
 __device__ __forceinline__ void reg_sort(uint32_t (&v)[N]) {
 #pragma unroll
@@ -711,6 +728,10 @@ __global__ void __launch_bounds__(NT) k_seg_fix(TickBufs b) {
             if (nl > 1 && hi32(o0) + nl <= b.ev_cap) lane_sort_segment(b.leave + hi32(o0), nl);
         }
         uint64_t todo = wave_ballot(own && !big && !small);
+        if (GW_SEG_STATS && ln == 0) {
+            shard_add(b.st, blockIdx.x, 0, (unsigned long long)popc64(wave_ballot(small)));
+            shard_add(b.st, blockIdx.x, 2, (unsigned long long)popc64(todo));
+        }
         while (todo) {
             const int q = __builtin_ctzll(todo);
             todo &= todo - 1;
@@ -742,7 +763,9 @@ __global__ void __launch_bounds__(NT) k_big_seg(TickBufs b) {
 
 void tick_diff(const TickBufs& b, hipStream_t s) {
     const uint64_t nmax = 2ull * b.m;
-    hipLaunchKernelGGL(k_mover, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
+    if (b.diff_u >= 4) hipLaunchKernelGGL(k_mover<4>, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
+    else if (b.diff_u == 1) hipLaunchKernelGGL(k_mover<1>, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
+    else hipLaunchKernelGGL(k_mover<2>, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_big_own, dim3(64), dim3(NT), 0, s, b);
 }
 void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {

@@ -65,6 +65,7 @@ struct gw_ctx {
     unsigned long long stamp_base = 1;   // global op counter (stamp 0 = never)
     uint32_t epoch = 1;                  // bumped by every tick and client change (World.nbc)
     int cells_per_d = 2;                 // grid cells per AOI distance (GW_CELLS_PER_D)
+    int diff_u = 2, nb_u = 4;            // chunks in flight in k_mover / sync walks (GW_DIFF_U, GW_NB_U)
     bool grid_dirty = true;              // gn/gn_start must be rebuilt before queries
     uint64_t h_present = 0;
     uint64_t own_cap = 0;                // capacity of the own-event regions (grows on overflow)
@@ -361,6 +362,7 @@ World world(gw_ctx* c) {
     w.gn = c->gnb[c->gcur]; w.gn_start = c->gsb[c->gcur]; w.gidx = c->gidx;
     w.nbc = c->nbc;
     w.epoch = c->epoch;
+    w.nb_u = c->nb_u;
     return w;
 }
 
@@ -488,6 +490,8 @@ int gw_init(int device_id, gw_ctx** out) {
         (void)hipEventCreate(&c->ev_t0);
         (void)hipEventCreate(&c->ev_t1);
         if (const char* e = getenv("GW_CELLS_PER_D")) c->cells_per_d = std::min(4, std::max(1, atoi(e)));
+        if (const char* e = getenv("GW_DIFF_U")) c->diff_u = atoi(e);
+        if (const char* e = getenv("GW_NB_U")) c->nb_u = atoi(e);
     } while (0);
     if (rc) {
         (void)hipGetLastError();
@@ -694,6 +698,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     TickBufs b{};
     b.w = world(c);
     b.ops = ops; b.m = M; b.stamp_base = c->stamp_base;
+    b.diff_u = c->diff_u;
     b.last_pos = c->last_pos; b.last_aoi = c->last_aoi; b.last_leave = c->last_leave;
     b.st = st;
     b.gn_nxt = c->gnb[c->gcur ^ 1]; b.start_nxt = c->gsb[c->gcur ^ 1];
@@ -774,6 +779,13 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     for (int i = 0; i < STAT_SHARDS; ++i) {
         a_old += hs.shard[i][SH_AOLD] & 0xffffffffull;
         a_new += hs.shard[i][SH_AOLD] >> 32;
+    }
+    if (getenv("GW_DEBUG_STATS")) {
+        unsigned long long f0 = 0, f2 = 0;
+        for (int i = 0; i < STAT_SHARDS; ++i) { f0 += hs.shard[i][0]; f2 += hs.shard[i][2]; }
+        fprintf(stderr, "gw_tick: movers %llu gm %llu cand %llu ev %llu+%llu big %llu bigseg %llu bigcell %llu "
+                "seg_lane %llu seg_wave %llu\n", hs.n_movers, hs.n_gm, hs.cand_total, hs.ev_pk & 0xffffffffull,
+                hs.ev_pk >> 32, hs.n_big, hs.n_bigseg, hs.n_bigcell, f0, f2);
     }
     out->ops = M;
     out->movers = n_mov;

@@ -137,6 +137,7 @@ struct World {
     // collect right after that tick takes it instead of walking e's window
     unsigned long long* nbc;
     uint32_t epoch;            // current epoch (bumped by every tick and client change)
+    int nb_u;                  // candidate chunks of 64 in flight in the sync walks
 };
 
 // ---- tick buffers handed to the launchers ----------------------------------
@@ -174,6 +175,7 @@ struct TickBufs {
     gw_event* enter;
     gw_event* leave;
     uint64_t ev_cap;          // capacity of enter and of leave
+    int diff_u;               // candidate chunks of 64 in flight per k_mover iteration
 };
 
 // ---- launchers --------------------------------------------------------------

@@ -16,8 +16,7 @@ namespace gw {
 // neighbours of a present entity e from the current grid: calls
 // f(rel, w, has_client) per lane for every candidate (rel: w != e is related to e).
 // The window's row ranges are walked flattened, NB_U chunks of 64 in flight.
-constexpr int NB_U = 4;
-template <typename F>
+template <int NB_U = 4, typename F>
 __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) {
     const AoiEnt a = w.aoi[e];
     if (!(a.meta & PRESENT_BIT)) return;
@@ -63,6 +62,7 @@ __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) 
 constexpr uint32_t SYNC_MAX_BLOCKS = 8192;
 
 // record count per flagged entity (one wave each)
+template <int U>
 __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __restrict__ flagged,
                                                    const uint64_t* nf_dev, uint32_t nf_max, uint32_t* cnt,
                                                    DevStats* st) {
@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __re
                     r += (uint32_t)c;                        // counted by this tick's diff
                 } else {
                     uint32_t n = 0;
-                    wave_neighbors(w, e, [&](bool rel, uint32_t, uint32_t g) {
+                    wave_neighbors<U>(w, e, [&](bool rel, uint32_t, uint32_t g) {
                         n += (uint32_t)popc64(wave_ballot(rel && g != 0));
                     });
                     r += n;
@@ -94,11 +94,14 @@ __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __re
 void launch_sync_count(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
                        uint32_t* cnt, DevStats* st, hipStream_t s) {
     if (!nf_max) return;
-    hipLaunchKernelGGL(k_sync_count, dim3(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS)), dim3(NT), 0, s, w,
-                       flagged, nf_dev, nf_max, cnt, st);
+    const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
+    if (w.nb_u >= 8) hipLaunchKernelGGL(k_sync_count<8>, g, dim3(NT), 0, s, w, flagged, nf_dev, nf_max, cnt, st);
+    else if (w.nb_u <= 2) hipLaunchKernelGGL(k_sync_count<2>, g, dim3(NT), 0, s, w, flagged, nf_dev, nf_max, cnt, st);
+    else hipLaunchKernelGGL(k_sync_count<4>, g, dim3(NT), 0, s, w, flagged, nf_dev, nf_max, cnt, st);
 }
 
 // writes e's records at rec_off[k] and clears e's flags
+template <int U>
 __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __restrict__ flagged,
                                                    const uint64_t* nf_dev, uint32_t nf_max,
                                                    const uint64_t* __restrict__ rec_off, gw_sync_record* rec,
@@ -122,7 +125,7 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
                 ++at;
             }
             if (f & GW_SIF_NEIGHBOR_CLIENTS) {
-                wave_neighbors(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
+                wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
                     const bool take = rel && g != 0;
                     const uint64_t bt = wave_ballot(take);
                     if (take) {
@@ -141,8 +144,13 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
                        const uint64_t* rec_off, gw_sync_record* rec, uint64_t rec_cap, hipStream_t s) {
     if (!nf_max) return;
-    hipLaunchKernelGGL(k_sync_write, dim3(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS)), dim3(NT), 0, s, w,
-                       flagged, nf_dev, nf_max, rec_off, rec, rec_cap);
+    const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
+    if (w.nb_u >= 8)
+        hipLaunchKernelGGL(k_sync_write<8>, g, dim3(NT), 0, s, w, flagged, nf_dev, nf_max, rec_off, rec, rec_cap);
+    else if (w.nb_u <= 2)
+        hipLaunchKernelGGL(k_sync_write<2>, g, dim3(NT), 0, s, w, flagged, nf_dev, nf_max, rec_off, rec, rec_cap);
+    else
+        hipLaunchKernelGGL(k_sync_write<4>, g, dim3(NT), 0, s, w, flagged, nf_dev, nf_max, rec_off, rec, rec_cap);
 }
 
 __global__ void __launch_bounds__(NT) k_flag_mark(const uint32_t* __restrict__ flags, uint32_t cap, uint32_t* mark) {

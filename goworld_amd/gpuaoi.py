@@ -23,7 +23,8 @@ import numpy as np
 from .traces import OP_DTYPE
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libgpuaoi.so")
+# GW_LIB_PATH selects another build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("GW_LIB_PATH") or os.path.join(_HERE, "lib", "libgpuaoi.so")
 
 EVENT_DTYPE = np.dtype([("watcher", "<u4"), ("target", "<u4")])
 REC_DTYPE = np.dtype([("watcher", "<u4"), ("entity", "<u4"), ("x", "<f4"), ("y", "<f4"),

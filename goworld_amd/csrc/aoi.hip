@@ -11,41 +11,29 @@
 //            scan of the new cell counts.  gn stays in (cell, slot) order.
 //   gm       mover grid: each mover at its old and its new cell (counting
 //            sort whose cursor counts back to zero)
-//   diff     one wave per mover (in mover-grid order, i.e. by cell: windows
-//            of neighbouring waves overlap in L2) walks the non-movers of gn
-//            and the mover grid over its old and new windows, evaluates the
-//            old and new relation of every candidate and emits own events,
-//            sorted
-//   mirror   the relation is symmetric, so an own event (A,B) of a mover with
-//            an op-less B is also B's event (B,A): the mover counts it into
-//            B's packed counter (the returned value is its rank in B's
-//            segment) and keeps (B, A, rank) for the scatter
+//   diff     one wave per mover (in mover-grid order, i.e. by cell) walks
+//            the non-movers of gn and the mover grid over its old and new
+//            windows, evaluates the old and new relation of every candidate
+//            and emits its own events, sorted (no atomics)
+//   opless   the events of op-less watchers (pairs with a mover) come from
+//            the watcher side: 64 consecutive grid entries per wave, the
+//            movers of their search rectangles staged once, sorted by slot
+//            and broadcast to every lane -- counted in one pass, written at
+//            the scanned offsets in a second (no atomics, no scatter, no
+//            per-watcher sort)
 //   events   scan of the per-watcher counts -> canonical offsets; movers copy
-//            their sorted events and scatter the mirror ones; the segments of
-//            touched op-less watchers are sorted by target
-// Outputs are placed by scans; the atomics are histogram/cursor updates, one
-// counter increment per mirror event (spread over watchers), wave-aggregated
-// list appends and per-shard statistics.  No MFMA: compare and gather work
-// bound by L2/HBM latency and bandwidth.
+//            their sorted own events, op-less watchers write theirs
+// Outputs are placed by scans; the atomics left are per-cell histogram /
+// cursor updates of the grid and per-shard statistics.  No MFMA: compare and
+// gather work bound by L2/HBM latency and bandwidth.
+#include <climits>
+
 #include "dev_common.hpp"
 
 namespace gw {
 
 constexpr uint32_t SORT_LDS = 1024;     // own events sorted in a wave's LDS up to this many
 constexpr uint32_t NO_CELL = 0xffffffffu;
-constexpr uint32_t GS_BLOCKS = 4096;    // cap of grid-stride launches
-
-// appends v for every lane with pred to list (64-bit counter), one atomic per
-// wave; every lane of the wave must call it
-__device__ __forceinline__ void wave_append(bool pred, uint32_t v, uint32_t* list, unsigned long long* cnt) {
-    const uint64_t bm = wave_ballot(pred);
-    if (!bm) return;
-    const int leader = __builtin_ctzll(bm);
-    unsigned long long base = 0;
-    if (lane_id() == leader) base = atomicAdd(cnt, (unsigned long long)popc64(bm));
-    base = __shfl(base, leader, 64);
-    if (pred) list[base + (uint64_t)popc64(bm & lanemask_lt())] = v;
-}
 
 // ---------------------------------------------------------------------------
 // ops: last-op dedupe per slot (seq = index in the tick's op stream)
@@ -439,17 +427,19 @@ void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// diff: one wave per primary mover-grid entry (mover A).  For every candidate
-// B in A's cells the old relation (pre-tick positions and stamps) and the new
-// one are evaluated; r_old != r_new is an own event (A,B).  Non-movers come
-// from gn (old = new position), movers from the mover grid, where B's entry at
-// its old cell stands for the pair when r_old holds and its entry at the new
-// cell when only r_new does, so each pair is taken once.  The row ranges of
-// both grids are walked flattened (Flat), DIFF_U chunks of 64 candidates with
-// their loads in flight together (DIFF_U: GW_DIFF_U, default 2).  Events (B<<1 | leave) go to A's region and
-// are sorted there: registers up to 64, LDS up to SORT_LDS, else a block sort
-// later.  The count of new neighbours with a client is kept for the collect.
-
+// diff: one wave per primary mover-grid entry (mover A): its own events.  For
+// every candidate B in A's cells the old relation (pre-tick positions and
+// stamps) and the new one are evaluated; r_old != r_new is an own event (A,B).
+// Non-movers come from gn (old = new position), movers from the mover grid,
+// where B's entry at its old cell stands for the pair when r_old holds and its
+// entry at the new cell when only r_new does, so each pair is taken once.  The
+// row ranges of both grids are walked flattened (Flat), DIFF_U chunks of 64
+// candidates with their loads in flight together.  Events (B<<1 | leave) go to
+// A's region and are sorted there: registers up to 64, LDS up to SORT_LDS,
+// else a block sort later.  The events of the op-less B of such pairs come
+// from k_opless (watcher side, the same float expressions evaluated from B),
+// so this pass has no atomics.  The count of new
+// neighbours with a client is kept for the collect.
 struct Cand {
     float x, z, ox, oz;
     uint32_t slot;
@@ -457,12 +447,13 @@ struct Cand {
 };
 constexpr uint32_t CAND_NONMOVER = 1u << 31;
 constexpr uint32_t CAND_CLIENT = 1u << 30;
-constexpr uint32_t MIR_OWNER = 1u;   // in mir_rank: this event took the watcher's counter to zero
 
-template <int DIFF_U>
-__global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * SORT_LDS];
-    const uint64_t m = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
+// WPB waves per block: a block keeps its LDS until its slowest wave ends, so
+// small blocks keep more waves resident when hotspot movers run long
+template <int DIFF_U, int WPB>
+__global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[WPB * SORT_LDS];
+    const uint64_t m = (uint64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
     if (m >= b.st->n_gm) return;
     const MEnt me = b.gm[m];
     if (!(me.tags & TAG_PRIMARY)) return;
@@ -470,23 +461,21 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
     const uint64_t lt = lanemask_lt();
     const World& w = b.w;
     const uint64_t reg = b.reg[m], cap = b.cand[m];
+    const uint32_t A = me.slot;
     if (reg + cap > b.own_cap) {                      // region past the buffers: the host redoes the diff
         if (ln == 0) {
             atomicOr(&b.st->overflow, 1ull);
-            b.mir_cnt[m] = 0;
+            b.cnt64[A] = 0;
         }
         return;
     }
-    const uint32_t A = me.slot;
     const SpaceP P = w.sp[me.space];
     const float d = P.d;
     const bool pn = me.x == me.x, po = me.ox == me.ox;
     const unsigned long long sA = w.stamp[A], soA = w.prev[A].ostamp;
-    const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
     const Rects R = mover_rects(P, po, me.ox, me.oz, pn, me.x, me.z);
     uint32_t* out = b.own + reg;
-    uint64_t* mir = b.mir + reg;
-    uint32_t n = 0, nl = 0, nm_ = 0;
+    uint32_t n = 0, nl = 0;
     uint32_t c_old = 0, c_new = 0, c_band = 0, c_cli = 0;
     Flat f = flat_build<2>(P, R, w.gn_start, b.gm_start);
     for (uint32_t base = 0; base < f.total; base += 64u * DIFF_U) {
@@ -516,12 +505,13 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
         for (int u = 0; u < DIFF_U; ++u) {
             if (base + 64u * u >= f.total) break;              // wave-uniform
             const Cand& e = cc[u];
-            bool ev = false, lv = false, nmv = false;
+            bool ev = false, lv = false;
             uint32_t key = 0;
             if (e.slot != A) {
-                nmv = (e.info & CAND_NONMOVER) != 0;
-                const bool iao = wo.has(e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, me.ox, me.oz);
-                const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, me.x, me.z);
+                const bool nmv = (e.info & CAND_NONMOVER) != 0;
+                // A's view: A's windows around B's old / new position
+                const bool iao = in_win(me.ox, me.oz, d, e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, me.ox, me.oz);
+                const bool ian = in_win(me.x, me.z, d, e.x, e.z), ibn = in_win(e.x, e.z, d, me.x, me.z);
                 bool ro = iao, rn = ian;
                 if (iao != ibo || ian != ibn) {
                     const unsigned long long sb = w.stamp[e.slot];
@@ -538,20 +528,11 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
                     key = (e.slot << 1) | (lv ? 1u : 0u);
                 }
             }
-            const bool mev = ev && nmv;
-            // B has no op: (B,A) is B's event too: count it (no return value,
-            // so the candidate loop never waits on the atomic)
-#ifndef GW_EXP_NO_MIR_ATOMIC
-            if (mev) atomicAdd(&b.cnt64[e.slot], lv ? (1ull << 32) : 1ull);
-#endif
-            const uint64_t be = wave_ballot(ev), bl = wave_ballot(ev && lv), bm = wave_ballot(mev);
+            const uint64_t be = wave_ballot(ev), bl = wave_ballot(ev && lv);
             const uint32_t at = n + (uint32_t)popc64(be & lt);
             if (ev && at < cap) out[at] = key;
-            const uint32_t atm = nm_ + (uint32_t)popc64(bm & lt);
-            if (mev && atm < cap) mir[atm] = ((uint64_t)e.slot << 32) | (A << 1) | (lv ? 1u : 0u);
             n += (uint32_t)popc64(be);
             nl += (uint32_t)popc64(bl);
-            nm_ += (uint32_t)popc64(bm);
         }
     }
     // sort the own events by (target, kind)
@@ -576,12 +557,9 @@ __global__ void __launch_bounds__(NT) k_mover(TickBufs b) {
     const uint32_t scl = wave_sum<uint32_t>(c_cli);
     if (ln == 0) {
         b.cnt64[A] = (unsigned long long)(n - nl) | ((unsigned long long)nl << 32);
-        b.mir_cnt[m] = nm_;
         if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | scl;
-#ifndef GW_EXP_NO_SHARD
         shard_add(b.st, blockIdx.x, SH_AOLD, (unsigned long long)so | ((unsigned long long)sn << 32));
         shard_add(b.st, blockIdx.x, SH_BAND, sb);
-#endif
     }
 }
 
@@ -598,9 +576,169 @@ __global__ void __launch_bounds__(NT) k_big_own(TickBufs b) {
     }
 }
 
-// movers copy their sorted own events into the canonical arrays and scatter
-// their mirror events to the op-less watchers' segments.  Loads are issued in
-// independent batches ahead of the stores (vmcnt retires in issue order).
+// ---------------------------------------------------------------------------
+// opless: the events of the op-less watchers, computed on the watcher side
+// (no atomics, no scatter).  A wave takes 64 consecutive grid entries and
+// groups its op-less watchers by grid row; for each group the movers (mover-
+// grid entries) of the union of the watchers' search rectangles are staged in
+// LDS sorted by slot, and every lane tests its watcher B against each of them
+// in turn, so B's events come out in target order.  PASS 0 counts (packed
+// enters | leaves << 32 into cnt64[B]), PASS 1 writes at the scanned offsets
+// and clears the counter.  A group with more than OPL_CAP movers is handled in
+// chunks; its watchers' segments are then re-sorted by the block sort.
+constexpr uint32_t OPL_CAP = 256;
+
+// ascending sort of one 64-bit key per lane across the wave (registers)
+__device__ __forceinline__ uint64_t wave_sort64_u64(uint64_t v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t o = __shfl_xor(v, j, 64);
+            const bool up = (l & k) == 0, lower = (l & j) == 0;
+            const uint64_t mn = v < o ? v : o, mx = v < o ? o : v;
+            v = (lower == up) ? mn : mx;
+        }
+    }
+    return v;
+}
+
+template <int PASS>
+__global__ void __launch_bounds__(64) k_opless(TickBufs b) {
+    __shared__ __attribute__((aligned(16))) MEnt L[OPL_CAP];
+    __shared__ uint64_t K[OPL_CAP];
+    const World& w = b.w;
+    const uint32_t np = w.gn_start[w.ncells];
+    const uint32_t i0 = blockIdx.x * 64u;
+    if (i0 >= np) return;
+    const int ln = lane_id();
+    // this lane's watcher
+    const uint32_t gi = i0 + ln;
+    GEnt e;
+    e.x = e.z = 0.0f;
+    e.slot = DEPARTED;
+    e.meta = MOVER_BIT;
+    if (gi < np) e = w.gn[gi];
+    const bool valid = gi < np && !(e.meta & MOVER_BIT);
+    uint32_t space = 0;
+    if (valid) space = w.aoi[e.slot].meta & SPACE_MASK;
+    const SpaceP P = w.sp[space];
+    const uint32_t cell = e.meta & CELL_MASK;
+    const uint32_t rowkey = valid ? cell - (cell - P.cell_base) % (uint32_t)P.W : 0xffffffffu;
+    const Rect r = search_rect(P, e.x, e.z);
+    unsigned long long sbv = 0;
+    bool have_sb = false;
+    uint32_t ne = 0, nl = 0;
+    uint64_t off = 0;
+    if (PASS == 1 && valid) off = b.off64[e.slot];
+    bool chunked = false;
+    uint64_t todo = wave_ballot(valid);
+    while (todo) {
+        // the group: lanes of the lowest remaining row
+        const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)rowkey, __builtin_ctzll(todo));
+        const bool mine = valid && rowkey == key;
+        const uint64_t gmask = wave_ballot(mine);
+        todo &= ~gmask;
+        // the group's space and union rectangle
+        const int lead = __builtin_ctzll(gmask);
+        const uint32_t gsp = (uint32_t)__builtin_amdgcn_readlane((int)space, lead);
+        const SpaceP G = w.sp[gsp];
+        const float d = G.d;
+        int x0 = mine ? r.x0 : INT_MAX, z0 = mine ? r.z0 : INT_MAX;
+        int x1 = mine ? r.x1 : INT_MIN, z1 = mine ? r.z1 : INT_MIN;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            x0 = min(x0, __shfl_xor(x0, o, 64)); z0 = min(z0, __shfl_xor(z0, o, 64));
+            x1 = max(x1, __shfl_xor(x1, o, 64)); z1 = max(z1, __shfl_xor(z1, o, 64));
+        }
+        Rects U;
+        U.n = 1;
+        U.r[0].x0 = x0; U.r[0].x1 = x1; U.r[0].z0 = z0; U.r[0].z1 = z1;
+        Flat f = flat_build<1>(G, U, b.gm_start, nullptr);
+        if (f.total > OPL_CAP) chunked = true;
+        for (uint32_t cb = 0; cb < f.total; cb += OPL_CAP) {
+            const uint32_t cn = min(OPL_CAP, f.total - cb);
+            // the chunk's movers in slot order: registers for one lane-chunk,
+            // else staged in LDS, sorted by (slot, index) and gathered back
+            MEnt mv;
+            mv.slot = 0xffffffffu;
+            uint32_t nlc = 0;                              // lane-chunks of sorted movers
+            if (cn <= 64) {
+                uint32_t idx[1], kd[1];
+                flat_map<1, 1>(f, cb, idx, kd);
+                MEnt me;
+                me.slot = 0xffffffffu;
+                if (ln < (int)cn) me = b.gm[idx[0]];
+                if (ln < (int)cn) L[ln] = me;
+                const uint64_t k = ln < (int)cn ? (((uint64_t)me.slot << 32) | (uint32_t)ln) : ~0ull;
+                const uint64_t sk = wave_sort64_u64(k);
+                wave_sync();
+                if (ln < (int)cn) mv = L[(uint32_t)sk];
+                nlc = 1;
+            } else {
+                for (uint32_t j = 0; j < cn; j += 64) {
+                    uint32_t idx[1], kd[1];
+                    flat_map<1, 1>(f, cb + j, idx, kd);
+                    if (j + ln < cn) {
+                        const MEnt me = b.gm[idx[0]];
+                        L[j + ln] = me;
+                        K[j + ln] = ((uint64_t)me.slot << 32) | (j + ln);
+                    }
+                }
+                wave_sync();
+                bitonic_inplace<64>(K, cn, ln, [](uint64_t v) { return v; }, [] { wave_sync(); });
+                nlc = (cn + 63) / 64;
+            }
+            for (uint32_t c = 0; c < nlc; ++c) {
+                if (nlc > 1) {                             // gather the next 64 sorted movers into lanes
+                    wave_sync();
+                    mv.slot = 0xffffffffu;
+                    if (c * 64 + ln < cn) mv = L[(uint32_t)K[c * 64 + ln]];
+                }
+                const uint32_t cnt = min(64u, cn - c * 64);
+                // each mover broadcast to every lane of the group, in slot order
+                for (uint32_t j = 0; j < cnt; ++j) {
+                    const float mx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mv.x), (int)j));
+                    const float mz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mv.z), (int)j));
+                    const float mox = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mv.ox), (int)j));
+                    const float moz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mv.oz), (int)j));
+                    const uint32_t ms = (uint32_t)__builtin_amdgcn_readlane((int)mv.slot, (int)j);
+                    const uint32_t mt = (uint32_t)__builtin_amdgcn_readlane((int)mv.tags, (int)j);
+                    if (!mine) continue;
+                    const bool iao = in_win(mox, moz, d, e.x, e.z), ibo = in_win(e.x, e.z, d, mox, moz);
+                    const bool ian = in_win(mx, mz, d, e.x, e.z), ibn = in_win(e.x, e.z, d, mx, mz);
+                    bool ro = iao, rn = ian;
+                    if (iao != ibo || ian != ibn) {
+                        if (!have_sb) { sbv = w.stamp[e.slot]; have_sb = true; }
+                        if (iao != ibo) ro = resolve(iao, ibo, w.prev[ms].ostamp, sbv);
+                        if (ian != ibn) rn = resolve(ian, ibn, w.stamp[ms], sbv);
+                    }
+                    const bool take = ((mt & TAG_OLD) && ro) || ((mt & TAG_NEW) && rn && !ro);
+                    if (take && ro != rn) {
+                        gw_event ev; ev.watcher = e.slot; ev.target = ms;
+                        if (ro) {
+                            if (PASS == 1) { uint64_t at = hi32(off) + nl; if (at < b.ev_cap) b.leave[at] = ev; }
+                            ++nl;
+                        } else {
+                            if (PASS == 1) { uint64_t at = lo32(off) + ne; if (at < b.ev_cap) b.enter[at] = ev; }
+                            ++ne;
+                        }
+                    }
+                }
+            }
+            wave_sync();
+        }
+    }
+    if (PASS == 0) {
+        if (valid && (ne | nl)) b.cnt64[e.slot] = (unsigned long long)ne | ((unsigned long long)nl << 32);
+    } else if (valid && (ne | nl)) {
+        b.cnt64[e.slot] = 0;
+        if (chunked && (ne > 1 || nl > 1)) b.bigseg[atomicAdd(&b.st->n_bigseg, 1ull)] = e.slot;   // rare
+    }
+}
+
+// movers copy their sorted own events into the canonical arrays
 __global__ void __launch_bounds__(NT) k_own_copy(TickBufs b) {
     const uint64_t m = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
     if (m >= b.st->n_gm) return;
@@ -610,143 +748,29 @@ __global__ void __launch_bounds__(NT) k_own_copy(TickBufs b) {
     const uint64_t lt = lanemask_lt();
     const uint32_t A = me.slot;
     const uint64_t reg = b.reg[m], capm = b.cand[m];
-    const uint32_t nmr = b.mir_cnt[m];
     const uint64_t c = b.cnt64[A];
     const uint64_t off = b.off64[A];
     if (reg + capm > b.own_cap) return;               // overflowed region (k_mover): nothing was written
     const uint32_t n = (uint32_t)(lo32(c) + hi32(c));
-    // first chunks of both streams in flight together
+    if (!n) return;
     const uint32_t* own = b.own + reg;
-    uint32_t key = (ln < (int)n) ? own[ln] : 0u;
-    uint64_t mv = (ln < (int)nmr) ? b.mir[reg + ln] : 0ull;
-    uint64_t moff = (ln < (int)nmr) ? b.off64[hi32(mv)] : 0ull;
-    if (n) {
-        uint32_t ie = 0, il = 0;
-        for (uint32_t base = 0; base < n; base += 64) {
-            const uint32_t j = base + ln;
-            const bool v = j < n;
-            if (base) key = v ? own[j] : 0u;
-            const bool lv = v && (key & 1u), en = v && !(key & 1u);
-            const uint64_t be = wave_ballot(en), bl = wave_ballot(lv);
-            gw_event ev; ev.watcher = A; ev.target = key >> 1;
-            if (en) { uint64_t at = lo32(off) + ie + popc64(be & lt); if (at < b.ev_cap) b.enter[at] = ev; }
-            if (lv) { uint64_t at = hi32(off) + il + popc64(bl & lt); if (at < b.ev_cap) b.leave[at] = ev; }
-            ie += (uint32_t)popc64(be);
-            il += (uint32_t)popc64(bl);
-        }
-        if (ln == 0) b.cnt64[A] = 0;
-    }
-    // mirror events: the watcher's counter (its full count after the scan) is
-    // counted back down, the returned value is the event's rank in the
-    // segment and the event that reaches zero marks the segment's owner
-    for (uint32_t base = 0; base < nmr; base += 64) {
+    uint32_t ie = 0, il = 0;
+    for (uint32_t base = 0; base < n; base += 64) {
         const uint32_t j = base + ln;
-        if (base && j < nmr) {
-            mv = b.mir[reg + j];
-            moff = b.off64[hi32(mv)];
-        }
-        if (j < nmr) {
-            const uint32_t W = (uint32_t)hi32(mv), al = (uint32_t)lo32(mv);
-            const unsigned long long inc = (al & 1u) ? (1ull << 32) : 1ull;
-            const unsigned long long o = atomicSub(&b.cnt64[W], inc);
-            gw_event ev; ev.watcher = W; ev.target = al >> 1;
-            if (al & 1u) { uint64_t at = hi32(moff) + hi32(o) - 1; if (at < b.ev_cap) b.leave[at] = ev; }
-            else { uint64_t at = lo32(moff) + lo32(o) - 1; if (at < b.ev_cap) b.enter[at] = ev; }
-            b.mir_rank[reg + j] = o == inc ? MIR_OWNER : 0u;
-        }
+        const bool v = j < n;
+        const uint32_t key = v ? own[j] : 0u;
+        const bool lv = v && (key & 1u), en = v && !(key & 1u);
+        const uint64_t be = wave_ballot(en), bl = wave_ballot(lv);
+        gw_event ev; ev.watcher = A; ev.target = key >> 1;
+        if (en) { uint64_t at = lo32(off) + ie + popc64(be & lt); if (at < b.ev_cap) b.enter[at] = ev; }
+        if (lv) { uint64_t at = hi32(off) + il + popc64(bl & lt); if (at < b.ev_cap) b.leave[at] = ev; }
+        ie += (uint32_t)popc64(be);
+        il += (uint32_t)popc64(bl);
     }
+    if (ln == 0) b.cnt64[A] = 0;
 }
 
-// Touched op-less watchers: their segments are ordered by target (the ranks
-// came from atomics).  The mirror event whose count-down reached zero owns
-// the watcher (MIR_OWNER).  A lane sorts an owned segment of up to REG_SORT
-// targets in its registers (bitonic network, indices fixed at compile time);
-// longer ones are loaded into the wave's lanes and sorted across them (up to
-// 64) or go to the block sort.  (The count-down left the counters at zero.)
-constexpr int REG_SORT = 16;
-#ifndef GW_SEG_STATS
-#define GW_SEG_STATS 0
-#endif
-template <int N>
-__device__ __forceinline__ void reg_sort(uint32_t (&v)[N]) {
-#pragma unroll
-    for (int k = 2; k <= N; k <<= 1)
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1)
-#pragma unroll
-            for (int i = 0; i < N; ++i) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const bool up = (i & k) == 0;
-                    const uint32_t a = v[i], c = v[l];
-                    if ((a > c) == up) { v[i] = c; v[l] = a; }
-                }
-            }
-}
-__device__ __forceinline__ void lane_sort_segment(gw_event* seg, uint32_t n) {
-    uint32_t v[REG_SORT];
-#pragma unroll
-    for (int i = 0; i < REG_SORT; ++i) v[i] = i < (int)n ? seg[i].target : 0xffffffffu;
-    reg_sort<REG_SORT>(v);
-#pragma unroll
-    for (int i = 0; i < REG_SORT; ++i)
-        if (i < (int)n) seg[i].target = v[i];
-}
-__device__ __forceinline__ void wave_sort_segment(gw_event* seg, uint32_t n, uint32_t W) {
-    const int ln = lane_id();
-    uint32_t t = ln < (int)n ? seg[ln].target : 0xffffffffu;
-    t = wave_sort64(t);
-    if (ln < (int)n) {
-        gw_event e; e.watcher = W; e.target = t;
-        seg[ln] = e;
-    }
-}
-__global__ void __launch_bounds__(NT) k_seg_fix(TickBufs b) {
-    const uint64_t m = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
-    if (m >= b.st->n_gm) return;
-    if (!(b.gm[m].tags & TAG_PRIMARY)) return;
-    const uint64_t reg = b.reg[m];
-    if (reg + b.cand[m] > b.own_cap) return;
-    const int ln = lane_id();
-    const uint32_t nmr = b.mir_cnt[m];
-    for (uint32_t base = 0; base < nmr; base += 64) {
-        const uint32_t j = base + ln;
-        const bool own = j < nmr && (b.mir_rank[reg + j] & MIR_OWNER);
-        uint32_t W = 0;
-        uint64_t o0 = 0, o1 = 0;
-        if (own) {
-            W = (uint32_t)hi32(b.mir[reg + j]);
-            o0 = b.off64[W];
-            o1 = b.off64[W + 1];
-        }
-        const uint32_t ne = (uint32_t)(lo32(o1) - lo32(o0)), nl = (uint32_t)(hi32(o1) - hi32(o0));
-        const bool big = own && (ne > 64 || nl > 64);
-        if (big) b.bigseg[atomicAdd(&b.st->n_bigseg, 1ull)] = W;           // rare
-        const bool small = own && !big && ne <= (uint32_t)REG_SORT && nl <= (uint32_t)REG_SORT;
-        if (small) {
-            if (ne > 1 && lo32(o0) + ne <= b.ev_cap) lane_sort_segment(b.enter + lo32(o0), ne);
-            if (nl > 1 && hi32(o0) + nl <= b.ev_cap) lane_sort_segment(b.leave + hi32(o0), nl);
-        }
-        uint64_t todo = wave_ballot(own && !big && !small);
-        if (GW_SEG_STATS && ln == 0) {
-            shard_add(b.st, blockIdx.x, 0, (unsigned long long)popc64(wave_ballot(small)));
-            shard_add(b.st, blockIdx.x, 2, (unsigned long long)popc64(todo));
-        }
-        while (todo) {
-            const int q = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const uint32_t Wq = (uint32_t)__builtin_amdgcn_readlane((int)W, q);
-            const uint32_t eq = (uint32_t)__builtin_amdgcn_readlane((int)lo32(o0), q);
-            const uint32_t lq = (uint32_t)__builtin_amdgcn_readlane((int)hi32(o0), q);
-            const uint32_t neq = (uint32_t)__builtin_amdgcn_readlane((int)ne, q);
-            const uint32_t nlq = (uint32_t)__builtin_amdgcn_readlane((int)nl, q);
-            if (neq > 1 && (uint64_t)eq + neq <= b.ev_cap) wave_sort_segment(b.enter + eq, neq, Wq);
-            if (nlq > 1 && (uint64_t)lq + nlq <= b.ev_cap) wave_sort_segment(b.leave + lq, nlq, Wq);
-        }
-    }
-}
-
-// block sort of op-less segments longer than 64 (by target)
+// block sort of op-less segments assembled from several mover chunks (by target)
 __global__ void __launch_bounds__(NT) k_big_seg(TickBufs b) {
     const uint64_t nb = b.st->n_bigseg;
     for (uint64_t k = blockIdx.x; k < nb; k += gridDim.x) {
@@ -763,10 +787,13 @@ __global__ void __launch_bounds__(NT) k_big_seg(TickBufs b) {
 
 void tick_diff(const TickBufs& b, hipStream_t s) {
     const uint64_t nmax = 2ull * b.m;
-    if (b.diff_u >= 4) hipLaunchKernelGGL(k_mover<4>, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
-    else if (b.diff_u == 1) hipLaunchKernelGGL(k_mover<1>, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
-    else hipLaunchKernelGGL(k_mover<2>, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
+    switch (b.diff_u) {                    // GW_MOVER_WPB: waves per k_mover block
+    case 2: hipLaunchKernelGGL((k_mover<2, 2>), dim3(nblk1(nmax, 2)), dim3(128), 0, s, b); break;
+    case 4: hipLaunchKernelGGL((k_mover<2, 4>), dim3(nblk1(nmax, 4)), dim3(256), 0, s, b); break;
+    default: hipLaunchKernelGGL((k_mover<2, 1>), dim3(nblk1(nmax, 1)), dim3(64), 0, s, b); break;
+    }
     hipLaunchKernelGGL(k_big_own, dim3(64), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_opless<0>, dim3(nblk1(b.w.cap, 64)), dim3(64), 0, s, b);
 }
 void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint64_t nmax = 2ull * b.m;
@@ -774,7 +801,7 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.cnt64, b.off64, (uint64_t)C + 1, nullptr, sc,
                                        (uint64_t*)&b.st->ev_pk, s);
     hipLaunchKernelGGL(k_own_copy, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_seg_fix, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_opless<1>, dim3(nblk1(C, 64)), dim3(64), 0, s, b);
     hipLaunchKernelGGL(k_big_seg, dim3(64), dim3(NT), 0, s, b);
 }
 

@@ -65,7 +65,7 @@ struct gw_ctx {
     unsigned long long stamp_base = 1;   // global op counter (stamp 0 = never)
     uint32_t epoch = 1;                  // bumped by every tick and client change (World.nbc)
     int cells_per_d = 2;                 // grid cells per AOI distance (GW_CELLS_PER_D)
-    int diff_u = 2, nb_u = 4;            // chunks in flight in k_mover / sync walks (GW_DIFF_U, GW_NB_U)
+    int diff_u = 1, nb_u = 4;            // k_mover waves per block (GW_MOVER_WPB), sync chunks in flight (GW_NB_U)
     bool grid_dirty = true;              // gn/gn_start must be rebuilt before queries
     uint64_t h_present = 0;
     uint64_t own_cap = 0;                // capacity of the own-event regions (grows on overflow)
@@ -490,7 +490,7 @@ int gw_init(int device_id, gw_ctx** out) {
         (void)hipEventCreate(&c->ev_t0);
         (void)hipEventCreate(&c->ev_t1);
         if (const char* e = getenv("GW_CELLS_PER_D")) c->cells_per_d = std::min(4, std::max(1, atoi(e)));
-        if (const char* e = getenv("GW_DIFF_U")) c->diff_u = atoi(e);
+        if (const char* e = getenv("GW_MOVER_WPB")) c->diff_u = atoi(e);
         if (const char* e = getenv("GW_NB_U")) c->nb_u = atoi(e);
     } while (0);
     if (rc) {

@@ -11,29 +11,41 @@
 //            scan of the new cell counts.  gn stays in (cell, slot) order.
 //   gm       mover grid: each mover at its old and its new cell (counting
 //            sort whose cursor counts back to zero)
-//   diff     one wave per mover (in mover-grid order, i.e. by cell) walks
-//            the non-movers of gn and the mover grid over its old and new
-//            windows, evaluates the old and new relation of every candidate
-//            and emits its own events, sorted (no atomics)
-//   opless   the events of op-less watchers (pairs with a mover) come from
-//            the watcher side: 64 consecutive grid entries per wave, the
-//            movers of their search rectangles staged once, sorted by slot
-//            and broadcast to every lane -- counted in one pass, written at
-//            the scanned offsets in a second (no atomics, no scatter, no
-//            per-watcher sort)
+//   diff     one wave per mover (in mover-grid order, i.e. by cell: windows
+//            of neighbouring waves overlap in L2) walks the non-movers of gn
+//            and the mover grid over its old and new windows, evaluates the
+//            old and new relation of every candidate and emits own events,
+//            sorted
+//   mirror   the relation is symmetric, so an own event (A,B) of a mover with
+//            an op-less B is also B's event (B,A): the mover counts it into
+//            B's packed counter (no return value) and keeps (B, A) for later
 //   events   scan of the per-watcher counts -> canonical offsets; movers copy
-//            their sorted own events, op-less watchers write theirs
-// Outputs are placed by scans; the atomics left are per-cell histogram /
-// cursor updates of the grid and per-shard statistics.  No MFMA: compare and
-// gather work bound by L2/HBM latency and bandwidth.
-#include <climits>
-
+//            their sorted own events; each mirror event counts its watcher's
+//            counter back down (the returned value is its rank in the
+//            segment, the last one lists the watcher for the sort); the
+//            listed segments are sorted by target in registers
+// Outputs are placed by scans; the atomics are histogram/cursor updates, one
+// counter increment per mirror event (spread over watchers), wave-aggregated
+// list appends and per-shard statistics.  No MFMA: compare and gather work
+// bound by L2/HBM latency and bandwidth.
 #include "dev_common.hpp"
 
 namespace gw {
 
 constexpr uint32_t SORT_LDS = 1024;     // own events sorted in a wave's LDS up to this many
 constexpr uint32_t NO_CELL = 0xffffffffu;
+
+// appends v for every lane with pred to list (64-bit counter), one atomic per
+// wave; every lane of the wave must call it
+__device__ __forceinline__ void wave_append(bool pred, uint32_t v, uint32_t* list, unsigned long long* cnt) {
+    const uint64_t bm = wave_ballot(pred);
+    if (!bm) return;
+    const int leader = __builtin_ctzll(bm);
+    unsigned long long base = 0;
+    if (lane_id() == leader) base = atomicAdd(cnt, (unsigned long long)popc64(bm));
+    base = __shfl(base, leader, 64);
+    if (pred) list[base + (uint64_t)popc64(bm & lanemask_lt())] = v;
+}
 
 // ---------------------------------------------------------------------------
 // ops: last-op dedupe per slot (seq = index in the tick's op stream)
@@ -427,19 +439,17 @@ void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// diff: one wave per primary mover-grid entry (mover A): its own events.  For
-// every candidate B in A's cells the old relation (pre-tick positions and
-// stamps) and the new one are evaluated; r_old != r_new is an own event (A,B).
-// Non-movers come from gn (old = new position), movers from the mover grid,
-// where B's entry at its old cell stands for the pair when r_old holds and its
-// entry at the new cell when only r_new does, so each pair is taken once.  The
-// row ranges of both grids are walked flattened (Flat), DIFF_U chunks of 64
-// candidates with their loads in flight together.  Events (B<<1 | leave) go to
-// A's region and are sorted there: registers up to 64, LDS up to SORT_LDS,
-// else a block sort later.  The events of the op-less B of such pairs come
-// from k_opless (watcher side, the same float expressions evaluated from B),
-// so this pass has no atomics.  The count of new
-// neighbours with a client is kept for the collect.
+// diff: one wave per primary mover-grid entry (mover A).  For every candidate
+// B in A's cells the old relation (pre-tick positions and stamps) and the new
+// one are evaluated; r_old != r_new is an own event (A,B).  Non-movers come
+// from gn (old = new position), movers from the mover grid, where B's entry at
+// its old cell stands for the pair when r_old holds and its entry at the new
+// cell when only r_new does, so each pair is taken once.  The row ranges of
+// both grids are walked flattened (Flat), DIFF_U chunks of 64 candidates with
+// their loads in flight together.  Events (B<<1 | leave) go to A's region and
+// are sorted there: registers up to 64, LDS up to SORT_LDS, else a block sort
+// later.  The count of new neighbours with a client is kept for the collect.
+
 struct Cand {
     float x, z, ox, oz;
     uint32_t slot;
@@ -461,21 +471,23 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     const uint64_t lt = lanemask_lt();
     const World& w = b.w;
     const uint64_t reg = b.reg[m], cap = b.cand[m];
-    const uint32_t A = me.slot;
     if (reg + cap > b.own_cap) {                      // region past the buffers: the host redoes the diff
         if (ln == 0) {
             atomicOr(&b.st->overflow, 1ull);
-            b.cnt64[A] = 0;
+            b.mir_cnt[m] = 0;
         }
         return;
     }
+    const uint32_t A = me.slot;
     const SpaceP P = w.sp[me.space];
     const float d = P.d;
     const bool pn = me.x == me.x, po = me.ox == me.ox;
     const unsigned long long sA = w.stamp[A], soA = w.prev[A].ostamp;
+    const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
     const Rects R = mover_rects(P, po, me.ox, me.oz, pn, me.x, me.z);
     uint32_t* out = b.own + reg;
-    uint32_t n = 0, nl = 0;
+    uint64_t* mir = b.mir + reg;
+    uint32_t n = 0, nl = 0, nm_ = 0;
     uint32_t c_old = 0, c_new = 0, c_band = 0, c_cli = 0;
     Flat f = flat_build<2>(P, R, w.gn_start, b.gm_start);
     for (uint32_t base = 0; base < f.total; base += 64u * DIFF_U) {
@@ -505,13 +517,12 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
         for (int u = 0; u < DIFF_U; ++u) {
             if (base + 64u * u >= f.total) break;              // wave-uniform
             const Cand& e = cc[u];
-            bool ev = false, lv = false;
+            bool ev = false, lv = false, nmv = false;
             uint32_t key = 0;
             if (e.slot != A) {
-                const bool nmv = (e.info & CAND_NONMOVER) != 0;
-                // A's view: A's windows around B's old / new position
-                const bool iao = in_win(me.ox, me.oz, d, e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, me.ox, me.oz);
-                const bool ian = in_win(me.x, me.z, d, e.x, e.z), ibn = in_win(e.x, e.z, d, me.x, me.z);
+                nmv = (e.info & CAND_NONMOVER) != 0;
+                const bool iao = wo.has(e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, me.ox, me.oz);
+                const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, me.x, me.z);
                 bool ro = iao, rn = ian;
                 if (iao != ibo || ian != ibn) {
                     const unsigned long long sb = w.stamp[e.slot];
@@ -528,11 +539,20 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
                     key = (e.slot << 1) | (lv ? 1u : 0u);
                 }
             }
-            const uint64_t be = wave_ballot(ev), bl = wave_ballot(ev && lv);
+            const bool mev = ev && nmv;
+            // B has no op: (B,A) is B's event too: count it (no return value,
+            // so the candidate loop never waits on the atomic)
+#ifndef GW_EXP_NO_MIR_ATOMIC
+            if (mev) atomicAdd(&b.cnt64[e.slot], lv ? (1ull << 32) : 1ull);
+#endif
+            const uint64_t be = wave_ballot(ev), bl = wave_ballot(ev && lv), bm = wave_ballot(mev);
             const uint32_t at = n + (uint32_t)popc64(be & lt);
             if (ev && at < cap) out[at] = key;
+            const uint32_t atm = nm_ + (uint32_t)popc64(bm & lt);
+            if (mev && atm < cap) mir[atm] = ((uint64_t)e.slot << 32) | (A << 1) | (lv ? 1u : 0u);
             n += (uint32_t)popc64(be);
             nl += (uint32_t)popc64(bl);
+            nm_ += (uint32_t)popc64(bm);
         }
     }
     // sort the own events by (target, kind)
@@ -557,9 +577,12 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     const uint32_t scl = wave_sum<uint32_t>(c_cli);
     if (ln == 0) {
         b.cnt64[A] = (unsigned long long)(n - nl) | ((unsigned long long)nl << 32);
+        b.mir_cnt[m] = nm_;
         if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | scl;
+#ifndef GW_EXP_NO_SHARD
         shard_add(b.st, blockIdx.x, SH_AOLD, (unsigned long long)so | ((unsigned long long)sn << 32));
         shard_add(b.st, blockIdx.x, SH_BAND, sb);
+#endif
     }
 }
 
@@ -576,169 +599,9 @@ __global__ void __launch_bounds__(NT) k_big_own(TickBufs b) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// opless: the events of the op-less watchers, computed on the watcher side
-// (no atomics, no scatter).  A wave takes 64 consecutive grid entries and
-// groups its op-less watchers by grid row; for each group the movers (mover-
-// grid entries) of the union of the watchers' search rectangles are staged in
-// LDS sorted by slot, and every lane tests its watcher B against each of them
-// in turn, so B's events come out in target order.  PASS 0 counts (packed
-// enters | leaves << 32 into cnt64[B]), PASS 1 writes at the scanned offsets
-// and clears the counter.  A group with more than OPL_CAP movers is handled in
-// chunks; its watchers' segments are then re-sorted by the block sort.
-constexpr uint32_t OPL_CAP = 256;
-
-// ascending sort of one 64-bit key per lane across the wave (registers)
-__device__ __forceinline__ uint64_t wave_sort64_u64(uint64_t v) {
-    const int l = lane_id();
-#pragma unroll
-    for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint64_t o = __shfl_xor(v, j, 64);
-            const bool up = (l & k) == 0, lower = (l & j) == 0;
-            const uint64_t mn = v < o ? v : o, mx = v < o ? o : v;
-            v = (lower == up) ? mn : mx;
-        }
-    }
-    return v;
-}
-
-template <int PASS>
-__global__ void __launch_bounds__(64) k_opless(TickBufs b) {
-    __shared__ __attribute__((aligned(16))) MEnt L[OPL_CAP];
-    __shared__ uint64_t K[OPL_CAP];
-    const World& w = b.w;
-    const uint32_t np = w.gn_start[w.ncells];
-    const uint32_t i0 = blockIdx.x * 64u;
-    if (i0 >= np) return;
-    const int ln = lane_id();
-    // this lane's watcher
-    const uint32_t gi = i0 + ln;
-    GEnt e;
-    e.x = e.z = 0.0f;
-    e.slot = DEPARTED;
-    e.meta = MOVER_BIT;
-    if (gi < np) e = w.gn[gi];
-    const bool valid = gi < np && !(e.meta & MOVER_BIT);
-    uint32_t space = 0;
-    if (valid) space = w.aoi[e.slot].meta & SPACE_MASK;
-    const SpaceP P = w.sp[space];
-    const uint32_t cell = e.meta & CELL_MASK;
-    const uint32_t rowkey = valid ? cell - (cell - P.cell_base) % (uint32_t)P.W : 0xffffffffu;
-    const Rect r = search_rect(P, e.x, e.z);
-    unsigned long long sbv = 0;
-    bool have_sb = false;
-    uint32_t ne = 0, nl = 0;
-    uint64_t off = 0;
-    if (PASS == 1 && valid) off = b.off64[e.slot];
-    bool chunked = false;
-    uint64_t todo = wave_ballot(valid);
-    while (todo) {
-        // the group: lanes of the lowest remaining row
-        const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)rowkey, __builtin_ctzll(todo));
-        const bool mine = valid && rowkey == key;
-        const uint64_t gmask = wave_ballot(mine);
-        todo &= ~gmask;
-        // the group's space and union rectangle
-        const int lead = __builtin_ctzll(gmask);
-        const uint32_t gsp = (uint32_t)__builtin_amdgcn_readlane((int)space, lead);
-        const SpaceP G = w.sp[gsp];
-        const float d = G.d;
-        int x0 = mine ? r.x0 : INT_MAX, z0 = mine ? r.z0 : INT_MAX;
-        int x1 = mine ? r.x1 : INT_MIN, z1 = mine ? r.z1 : INT_MIN;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            x0 = min(x0, __shfl_xor(x0, o, 64)); z0 = min(z0, __shfl_xor(z0, o, 64));
-            x1 = max(x1, __shfl_xor(x1, o, 64)); z1 = max(z1, __shfl_xor(z1, o, 64));
-        }
-        Rects U;
-        U.n = 1;
-        U.r[0].x0 = x0; U.r[0].x1 = x1; U.r[0].z0 = z0; U.r[0].z1 = z1;
-        Flat f = flat_build<1>(G, U, b.gm_start, nullptr);
-        if (f.total > OPL_CAP) chunked = true;
-        for (uint32_t cb = 0; cb < f.total; cb += OPL_CAP) {
-            const uint32_t cn = min(OPL_CAP, f.total - cb);
-            // the chunk's movers in slot order: registers for one lane-chunk,
-            // else staged in LDS, sorted by (slot, index) and gathered back
-            MEnt mv;
-            mv.slot = 0xffffffffu;
-            uint32_t nlc = 0;                              // lane-chunks of sorted movers
-            if (cn <= 64) {
-                uint32_t idx[1], kd[1];
-                flat_map<1, 1>(f, cb, idx, kd);
-                MEnt me;
-                me.slot = 0xffffffffu;
-                if (ln < (int)cn) me = b.gm[idx[0]];
-                if (ln < (int)cn) L[ln] = me;
-                const uint64_t k = ln < (int)cn ? (((uint64_t)me.slot << 32) | (uint32_t)ln) : ~0ull;
-                const uint64_t sk = wave_sort64_u64(k);
-                wave_sync();
-                if (ln < (int)cn) mv = L[(uint32_t)sk];
-                nlc = 1;
-            } else {
-                for (uint32_t j = 0; j < cn; j += 64) {
-                    uint32_t idx[1], kd[1];
-                    flat_map<1, 1>(f, cb + j, idx, kd);
-                    if (j + ln < cn) {
-                        const MEnt me = b.gm[idx[0]];
-                        L[j + ln] = me;
-                        K[j + ln] = ((uint64_t)me.slot << 32) | (j + ln);
-                    }
-                }
-                wave_sync();
-                bitonic_inplace<64>(K, cn, ln, [](uint64_t v) { return v; }, [] { wave_sync(); });
-                nlc = (cn + 63) / 64;
-            }
-            for (uint32_t c = 0; c < nlc; ++c) {
-                if (nlc > 1) {                             // gather the next 64 sorted movers into lanes
-                    wave_sync();
-                    mv.slot = 0xffffffffu;
-                    if (c * 64 + ln < cn) mv = L[(uint32_t)K[c * 64 + ln]];
-                }
-                const uint32_t cnt = min(64u, cn - c * 64);
-                // each mover broadcast to every lane of the group, in slot order
-                for (uint32_t j = 0; j < cnt; ++j) {
-                    const float mx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mv.x), (int)j));
-                    const float mz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mv.z), (int)j));
-                    const float mox = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mv.ox), (int)j));
-                    const float moz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mv.oz), (int)j));
-                    const uint32_t ms = (uint32_t)__builtin_amdgcn_readlane((int)mv.slot, (int)j);
-                    const uint32_t mt = (uint32_t)__builtin_amdgcn_readlane((int)mv.tags, (int)j);
-                    if (!mine) continue;
-                    const bool iao = in_win(mox, moz, d, e.x, e.z), ibo = in_win(e.x, e.z, d, mox, moz);
-                    const bool ian = in_win(mx, mz, d, e.x, e.z), ibn = in_win(e.x, e.z, d, mx, mz);
-                    bool ro = iao, rn = ian;
-                    if (iao != ibo || ian != ibn) {
-                        if (!have_sb) { sbv = w.stamp[e.slot]; have_sb = true; }
-                        if (iao != ibo) ro = resolve(iao, ibo, w.prev[ms].ostamp, sbv);
-                        if (ian != ibn) rn = resolve(ian, ibn, w.stamp[ms], sbv);
-                    }
-                    const bool take = ((mt & TAG_OLD) && ro) || ((mt & TAG_NEW) && rn && !ro);
-                    if (take && ro != rn) {
-                        gw_event ev; ev.watcher = e.slot; ev.target = ms;
-                        if (ro) {
-                            if (PASS == 1) { uint64_t at = hi32(off) + nl; if (at < b.ev_cap) b.leave[at] = ev; }
-                            ++nl;
-                        } else {
-                            if (PASS == 1) { uint64_t at = lo32(off) + ne; if (at < b.ev_cap) b.enter[at] = ev; }
-                            ++ne;
-                        }
-                    }
-                }
-            }
-            wave_sync();
-        }
-    }
-    if (PASS == 0) {
-        if (valid && (ne | nl)) b.cnt64[e.slot] = (unsigned long long)ne | ((unsigned long long)nl << 32);
-    } else if (valid && (ne | nl)) {
-        b.cnt64[e.slot] = 0;
-        if (chunked && (ne > 1 || nl > 1)) b.bigseg[atomicAdd(&b.st->n_bigseg, 1ull)] = e.slot;   // rare
-    }
-}
-
-// movers copy their sorted own events into the canonical arrays
+// movers copy their sorted own events into the canonical arrays and scatter
+// their mirror events to the op-less watchers' segments.  Loads are issued in
+// independent batches ahead of the stores (vmcnt retires in issue order).
 __global__ void __launch_bounds__(NT) k_own_copy(TickBufs b) {
     const uint64_t m = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
     if (m >= b.st->n_gm) return;
@@ -748,29 +611,104 @@ __global__ void __launch_bounds__(NT) k_own_copy(TickBufs b) {
     const uint64_t lt = lanemask_lt();
     const uint32_t A = me.slot;
     const uint64_t reg = b.reg[m], capm = b.cand[m];
+    const uint32_t nmr = b.mir_cnt[m];
     const uint64_t c = b.cnt64[A];
     const uint64_t off = b.off64[A];
     if (reg + capm > b.own_cap) return;               // overflowed region (k_mover): nothing was written
     const uint32_t n = (uint32_t)(lo32(c) + hi32(c));
-    if (!n) return;
+    // first chunks of both streams in flight together
     const uint32_t* own = b.own + reg;
-    uint32_t ie = 0, il = 0;
-    for (uint32_t base = 0; base < n; base += 64) {
-        const uint32_t j = base + ln;
-        const bool v = j < n;
-        const uint32_t key = v ? own[j] : 0u;
-        const bool lv = v && (key & 1u), en = v && !(key & 1u);
-        const uint64_t be = wave_ballot(en), bl = wave_ballot(lv);
-        gw_event ev; ev.watcher = A; ev.target = key >> 1;
-        if (en) { uint64_t at = lo32(off) + ie + popc64(be & lt); if (at < b.ev_cap) b.enter[at] = ev; }
-        if (lv) { uint64_t at = hi32(off) + il + popc64(bl & lt); if (at < b.ev_cap) b.leave[at] = ev; }
-        ie += (uint32_t)popc64(be);
-        il += (uint32_t)popc64(bl);
+    uint32_t key = (ln < (int)n) ? own[ln] : 0u;
+    uint64_t mv = (ln < (int)nmr) ? b.mir[reg + ln] : 0ull;
+    uint64_t moff = (ln < (int)nmr) ? b.off64[hi32(mv)] : 0ull;
+    if (n) {
+        uint32_t ie = 0, il = 0;
+        for (uint32_t base = 0; base < n; base += 64) {
+            const uint32_t j = base + ln;
+            const bool v = j < n;
+            if (base) key = v ? own[j] : 0u;
+            const bool lv = v && (key & 1u), en = v && !(key & 1u);
+            const uint64_t be = wave_ballot(en), bl = wave_ballot(lv);
+            gw_event ev; ev.watcher = A; ev.target = key >> 1;
+            if (en) { uint64_t at = lo32(off) + ie + popc64(be & lt); if (at < b.ev_cap) b.enter[at] = ev; }
+            if (lv) { uint64_t at = hi32(off) + il + popc64(bl & lt); if (at < b.ev_cap) b.leave[at] = ev; }
+            ie += (uint32_t)popc64(be);
+            il += (uint32_t)popc64(bl);
+        }
+        if (ln == 0) b.cnt64[A] = 0;
     }
-    if (ln == 0) b.cnt64[A] = 0;
+    // mirror events: the watcher's counter (its full count after the scan) is
+    // counted back down, the returned value is the event's rank in the
+    // segment and the event that reaches zero marks the segment's owner
+    for (uint32_t base = 0; base < nmr; base += 64) {
+        const uint32_t j = base + ln;
+        if (base && j < nmr) {
+            mv = b.mir[reg + j];
+            moff = b.off64[hi32(mv)];
+        }
+        if (j < nmr) {
+            const uint32_t W = (uint32_t)hi32(mv), al = (uint32_t)lo32(mv);
+            const unsigned long long inc = (al & 1u) ? (1ull << 32) : 1ull;
+            const unsigned long long o = atomicSub(&b.cnt64[W], inc);
+            gw_event ev; ev.watcher = W; ev.target = al >> 1;
+            if (al & 1u) { uint64_t at = hi32(moff) + hi32(o) - 1; if (at < b.ev_cap) b.leave[at] = ev; }
+            else { uint64_t at = lo32(moff) + lo32(o) - 1; if (at < b.ev_cap) b.enter[at] = ev; }
+            // the last event of the watcher marks it for the sort: one bit per
+        // slot, so no two owners contend on a counter
+        if (o == inc) atomicOr(&b.ownbits[W >> 5], 1u << (W & 31u));
+        }
+    }
 }
 
-// block sort of op-less segments assembled from several mover chunks (by target)
+// Touched op-less watchers: their segments are ordered by target (the ranks
+// came from atomics).  The mirror event whose count-down reached zero set the
+// watcher's bit in ownbits; a thread per bit sorts its watcher's segments of
+// up to REG_SORT targets in registers (bitonic network, indices fixed at
+// compile time) and hands longer ones to the block sort; the first lane of a
+// word clears it.
+constexpr int REG_SORT = 16;
+template <int N>
+__device__ __forceinline__ void reg_sort(uint32_t (&v)[N]) {
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const bool up = (i & k) == 0;
+                    const uint32_t a = v[i], c = v[l];
+                    if ((a > c) == up) { v[i] = c; v[l] = a; }
+                }
+            }
+}
+__device__ __forceinline__ void lane_sort_segment(gw_event* seg, uint32_t n) {
+    uint32_t v[REG_SORT];
+#pragma unroll
+    for (int i = 0; i < REG_SORT; ++i) v[i] = i < (int)n ? seg[i].target : 0xffffffffu;
+    reg_sort<REG_SORT>(v);
+#pragma unroll
+    for (int i = 0; i < REG_SORT; ++i)
+        if (i < (int)n) seg[i].target = v[i];
+}
+__global__ void __launch_bounds__(NT) k_seg_fix(TickBufs b) {
+    const uint32_t W = blockIdx.x * NT + threadIdx.x;     // one thread per slot bit
+    if (W >= b.w.cap) return;
+    const uint32_t bits = b.ownbits[W >> 5];
+    if ((W & 31u) == 0 && bits) b.ownbits[W >> 5] = 0;    // lanes of one word share a wave: all read first
+    if (!((bits >> (W & 31u)) & 1u)) return;
+    const uint64_t o0 = b.off64[W], o1 = b.off64[W + 1];
+    const uint32_t ne = (uint32_t)(lo32(o1) - lo32(o0)), nl = (uint32_t)(hi32(o1) - hi32(o0));
+    if (ne > (uint32_t)REG_SORT || nl > (uint32_t)REG_SORT) {
+        b.bigseg[atomicAdd(&b.st->n_bigseg, 1ull)] = W;                      // rare
+        return;
+    }
+    if (ne > 1 && lo32(o0) + ne <= b.ev_cap) lane_sort_segment(b.enter + lo32(o0), ne);
+    if (nl > 1 && hi32(o0) + nl <= b.ev_cap) lane_sort_segment(b.leave + hi32(o0), nl);
+}
+
+// block sort of op-less segments longer than REG_SORT (by target)
 __global__ void __launch_bounds__(NT) k_big_seg(TickBufs b) {
     const uint64_t nb = b.st->n_bigseg;
     for (uint64_t k = blockIdx.x; k < nb; k += gridDim.x) {
@@ -793,7 +731,6 @@ void tick_diff(const TickBufs& b, hipStream_t s) {
     default: hipLaunchKernelGGL((k_mover<2, 1>), dim3(nblk1(nmax, 1)), dim3(64), 0, s, b); break;
     }
     hipLaunchKernelGGL(k_big_own, dim3(64), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_opless<0>, dim3(nblk1(b.w.cap, 64)), dim3(64), 0, s, b);
 }
 void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint64_t nmax = 2ull * b.m;
@@ -801,7 +738,7 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.cnt64, b.off64, (uint64_t)C + 1, nullptr, sc,
                                        (uint64_t*)&b.st->ev_pk, s);
     hipLaunchKernelGGL(k_own_copy, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_opless<1>, dim3(nblk1(C, 64)), dim3(64), 0, s, b);
+    hipLaunchKernelGGL(k_seg_fix, dim3(nblk1(C, NT)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_big_seg, dim3(64), dim3(NT), 0, s, b);
 }
 

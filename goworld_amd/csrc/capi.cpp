@@ -80,6 +80,7 @@ struct gw_ctx {
     uint16_t* gate = nullptr;
     unsigned long long* cnt64 = nullptr;     // [slot_cap + 1], zero between ticks
     unsigned long long* nbc = nullptr;       // [slot_cap] epoch<<32 | neighbours with a client
+    uint32_t* ownbits = nullptr;             // [slot_cap/32 + 1] zero between ticks
     int32_t *last_pos = nullptr, *last_aoi = nullptr, *last_leave = nullptr;
     GEnt* gnb[2] = {nullptr, nullptr};   // grid ping-pong (gnb[gcur] is current)
     uint32_t* gsb[2] = {nullptr, nullptr};  // cell starts ping-pong
@@ -96,7 +97,7 @@ struct gw_ctx {
 
     // grid + tick scratch
     DevBuf ops_buf, k0, v0, k1, v1, gm, cand, reg, own, big, bigseg;
-    DevBuf mir, mir_rank, mir_cnt;
+    DevBuf mir, mir_cnt;
     DevBuf off64, enter_d, leave_d, scan_status, rs_hist;
     ScanCtx sc{};                  // single-pass scan state (prim.hpp)
     // sync / query scratch
@@ -288,6 +289,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->gate, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->cnt64, oc ? oc + 1 : 0, (size_t)nc + 1))) return rc;
     if ((rc = grow_preserve(c, c->nbc, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->ownbits, 0, (size_t)nc / 32 + 1))) return rc;
     if ((rc = grow_preserve(c, c->last_pos, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_aoi, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_leave, oc, nc))) return rc;
@@ -303,6 +305,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     HIPCHK(hipMemsetAsync(c->gate + oc, 0, n * 2, c->st));
     HIPCHK(hipMemsetAsync(c->cnt64 + oc, 0, (n + 1) * 8, c->st));
     HIPCHK(hipMemsetAsync(c->nbc + oc, 0, n * 8, c->st));
+    HIPCHK(hipMemsetAsync(c->ownbits, 0, ((size_t)nc / 32 + 1) * 4, c->st));
     launch_fill_i32(c->last_pos + oc, -1, n, c->st);
     launch_fill_i32(c->last_aoi + oc, -1, n, c->st);
     launch_fill_i32(c->last_leave + oc, -1, n, c->st);
@@ -508,14 +511,14 @@ void gw_shutdown(gw_ctx* c) {
     if (c->st) (void)hipStreamSynchronize(c->st);
     DevBuf* bufs[] = {&c->ops_buf, &c->k0, &c->v0, &c->k1, &c->v1, &c->bigseg,
                       &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->off64, &c->mir,
-                      &c->mir_rank, &c->mir_cnt,
+                      &c->mir_cnt,
                       &c->enter_d, &c->leave_d, &c->scan_status, &c->rs_hist,
                       &c->flag_mark, &c->flag_pre, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
                       &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf};
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
-    void* ps[] = {c->sc.ticket, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->nbc, c->last_pos, c->last_aoi,
+    void* ps[] = {c->sc.ticket, c->ownbits, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->nbc, c->last_pos, c->last_aoi,
                   c->last_leave, c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->scal32, c->gsb[0],
                   c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->bigcell, c->gm_start};
     for (void* p : ps) if (p) (void)hipFree(p);
@@ -684,7 +687,6 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     auto ensure_events = [&]() -> int {
         int r;
         if ((r = ensure(c, c->own, c->own_cap * 4)) || (r = ensure(c, c->mir, c->own_cap * 8)) ||
-            (r = ensure(c, c->mir_rank, c->own_cap * 4)) ||
             (r = ensure(c, c->enter_d, 2 * c->own_cap * sizeof(gw_event))) ||
             (r = ensure(c, c->leave_d, 2 * c->own_cap * sizeof(gw_event))))
             return r;
@@ -707,10 +709,11 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg);
     b.mir_cnt = P<uint32_t>(c->mir_cnt); b.big = P<uint32_t>(c->big);
     b.bigseg = P<uint32_t>(c->bigseg);
+    b.ownbits = c->ownbits;
     b.cnt64 = c->cnt64; b.off64 = P<uint64_t>(c->off64);
     auto bind_events = [&]() {
         b.own_cap = c->own_cap;
-        b.own = P<uint32_t>(c->own); b.mir = P<uint64_t>(c->mir); b.mir_rank = P<uint32_t>(c->mir_rank);
+        b.own = P<uint32_t>(c->own); b.mir = P<uint64_t>(c->mir);
         b.enter = P<gw_event>(c->enter_d); b.leave = P<gw_event>(c->leave_d);
         b.ev_cap = 2 * c->own_cap;
     };
@@ -745,6 +748,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         if ((rc = ensure_events())) return rc;
         bind_events();
         HIPCHK(hipMemsetAsync(c->cnt64, 0, ((size_t)C + 1) * 8, c->st));
+        HIPCHK(hipMemsetAsync(c->ownbits, 0, ((size_t)C / 32 + 1) * 4, c->st));
         DevStats* h = c->hstats;
         h->overflow = 0; h->n_big = 0; h->n_bigseg = 0; h->ev_pk = 0;
         memset(h->shard, 0, sizeof h->shard);

@@ -162,10 +162,10 @@ struct TickBufs {
     // diff (indexed by mover-grid entry)
     uint64_t* cand;           // [2m] candidate bound (0 unless TAG_PRIMARY)
     uint64_t* reg;            // [2m] exclusive scan of cand
-    uint64_t own_cap;         // capacity of own / mir / mir_rank
+    uint64_t own_cap;         // capacity of own / mir
     uint32_t* own;            // own events (target<<1 | leave)
     uint64_t* mir;            // mirror events of op-less neighbours: watcher<<32 | mover<<1 | leave
-    uint32_t* mir_rank;       // MIR_OWNER flag of each mirror event (k_own_copy -> k_seg_fix)
+    uint32_t* ownbits;        // [cap/32 + 1] touched op-less watchers to sort, zero between ticks
     uint32_t* mir_cnt;        // [2m] mirror events per entry
     uint32_t* big;            // [2m] entries whose own events need the block sort
     uint32_t* bigseg;         // [cap] op-less watchers whose segments need the block sort

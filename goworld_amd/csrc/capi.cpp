@@ -101,7 +101,8 @@ struct gw_ctx {
     DevBuf off64, enter_d, leave_d, scan_status, rs_hist;
     ScanCtx sc{};                  // single-pass scan state (prim.hpp)
     // sync / query scratch
-    DevBuf flag_mark, flag_pre, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
+    DevBuf fbits, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
+    uint64_t rec_cap = 0;                // records the rec0 buffer holds (grows on overflow)
     uint32_t* scal32 = nullptr;    // small device scalars
 
     // host mirror for validation of host-submitted ops
@@ -513,7 +514,7 @@ void gw_shutdown(gw_ctx* c) {
                       &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->off64, &c->mir,
                       &c->mir_cnt,
                       &c->enter_d, &c->leave_d, &c->scan_status, &c->rs_hist,
-                      &c->flag_mark, &c->flag_pre, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
+                      &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
                       &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf};
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec};
@@ -848,33 +849,44 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     reset_stats_host(c);
     HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
     DevStats* st = c->stats;
-    if ((rc = ensure(c, c->flag_mark, (size_t)C * 4)) || (rc = ensure(c, c->flag_pre, (size_t)C * 8)) ||
-        (rc = ensure(c, c->flagged, (size_t)C * 4)) || (rc = ensure(c, c->rec_cnt, (size_t)C * 4)) ||
-        (rc = ensure(c, c->rec_off, (size_t)C * 8)) || (rc = ensure_scan(c, C)))
+    if ((rc = ensure(c, c->fbits, (size_t)C * 4)) || (rc = ensure(c, c->flagged, (size_t)C * 4)) ||
+        (rc = ensure(c, c->rec_cnt, (size_t)C * 4)) || (rc = ensure(c, c->rec_off, (size_t)C * 8)) ||
+        (rc = ensure_scan(c, C)))
         return rc;
+    // records land in a buffer sized from the last collect; if it was too
+    // small, the write pass (which reads only the compacted list) reruns
+    c->rec_cap = std::max<uint64_t>(c->rec_cap, 4ull * C + 1024);
+    if ((rc = ensure(c, c->rec0, c->rec_cap * sizeof(gw_sync_record)))) return rc;
     const World w = world(c);
     prof_begin(c, "sync_flagged");
-    launch_flag_mark(c->flags, C, P<uint32_t>(c->flag_mark), c->st);
-    scan_u32_u64(P<uint32_t>(c->flag_mark), P<uint64_t>(c->flag_pre), C, nullptr, c->sc,
-                 (uint64_t*)&st->flagged, c->st);
-    launch_flag_compact(P<uint32_t>(c->flag_mark), P<uint64_t>(c->flag_pre), C, P<uint32_t>(c->flagged), c->st);
-    prof_end(c, (uint64_t)C * 4 * 4);
+    launch_flag_compact(c->flags, C, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), c->sc, (uint32_t*)&st->flagged,
+                        c->st);
+    prof_end(c, (uint64_t)C * 4 * 2);
     const uint64_t* nf = (const uint64_t*)&st->flagged;
     prof_begin(c, "sync_count");
-    launch_sync_count(w, P<uint32_t>(c->flagged), nf, C, P<uint32_t>(c->rec_cnt), st, c->st);
+    launch_sync_count(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint32_t>(c->rec_cnt), c->st);
     scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), C, nf, c->sc,
                  (uint64_t*)&st->rec_total, c->st);
     size_t s_count = prof_end(c, 0);
-    HIPCHK(hipGetLastError());
-    if ((rc = read_stats(c))) return rc;
-    const uint64_t R = c->hstats->rec_total;
-    const uint64_t NF = c->hstats->flagged;
-    if ((rc = ensure(c, c->rec0, std::max<uint64_t>(R, 1) * sizeof(gw_sync_record)))) return rc;
     prof_begin(c, "sync_write");
-    launch_sync_write(w, P<uint32_t>(c->flagged), nf, C, P<uint64_t>(c->rec_off), P<gw_sync_record>(c->rec0),
-                      std::max<uint64_t>(R, 1), c->st);
+    launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint64_t>(c->rec_off),
+                      P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
     size_t s_write = prof_end(c, 0);
     HIPCHK(hipGetLastError());
+    if ((rc = read_stats(c))) return rc;                 // the one host sync
+    const uint64_t R = c->hstats->rec_total;
+    const uint64_t NF = c->hstats->flagged;
+    if (c->hstats->overflow) {
+        c->rec_cap = R + R / 4 + 1024;
+        if ((rc = ensure(c, c->rec0, c->rec_cap * sizeof(gw_sync_record)))) return rc;
+        c->hstats->overflow = 0;
+        HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
+        launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint64_t>(c->rec_off),
+                          P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
+        HIPCHK(hipGetLastError());
+        if ((rc = read_stats(c))) return rc;
+        if (c->hstats->overflow) return set_err(c, GW_ENOMEM, "sync record buffer overflowed twice");
+    }
     gw_sync_record* recs = P<gw_sync_record>(c->rec0);
     // ---- per-gate grouping (stable, keeps the entity order) -------------
     if (R && G > 2) {

@@ -194,13 +194,13 @@ void tick_reset(const TickBufs& b, hipStream_t s);                 // after the 
 void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n,
                         hipStream_t s);
 // sync collect
-void launch_flag_mark(const uint32_t* flags, uint32_t cap, uint32_t* mark, hipStream_t s);
-void launch_flag_compact(const uint32_t* mark, const uint64_t* pre, uint32_t cap, uint32_t* flagged,
-                         hipStream_t s);
-void launch_sync_count(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
-                       uint32_t* cnt, DevStats* st, hipStream_t s);
-void launch_sync_write(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
-                       const uint64_t* rec_off, gw_sync_record* rec, uint64_t rec_cap, hipStream_t s);
+void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint32_t* fbits, ScanCtx& sc,
+                         uint32_t* total, hipStream_t s);
+void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
+                       uint32_t nf_max, uint32_t* cnt, hipStream_t s);
+void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
+                       uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
+                       uint64_t rec_cap, DevStats* st, hipStream_t s);
 void launch_gate_hist(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,
                       uint32_t* hist /*65536*/, hipStream_t s);
 void launch_gate_keys(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,

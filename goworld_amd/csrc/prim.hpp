@@ -97,6 +97,53 @@ __device__ __forceinline__ void scan_post(unsigned long long* w, unsigned long l
     scan_st(w + 1, tg | SCAN_POSTED | (x >> 32));
 }
 
+// Look-back of tile `tile` whose aggregate is tot, run by wave 0 (threads
+// 0..63) of the block; returns the exclusive prefix of the tile (to every lane
+// of wave 0) after posting the tile's inclusive prefix.
+template <typename TO>
+__device__ __forceinline__ TO scan_lookback(unsigned long long* __restrict__ status, uint32_t tile, uint32_t tag,
+                                            TO tot) {
+    const unsigned long long tg = (unsigned long long)tag << SCAN_SHIFT;
+    unsigned long long* my = status + (uint64_t)tile * SCAN_WORDS;
+    TO excl = 0;
+    if (tile == 0) {
+        if (threadIdx.x == 0) scan_post<TO>(my + 2, tg, tot);
+        return excl;
+    }
+    if (threadIdx.x == 0) scan_post<TO>(my, tg, tot);
+    const int ln = (int)threadIdx.x;
+    int64_t j = (int64_t)tile - 1;
+    while (true) {
+        const int64_t q = j - ln;
+        bool ready = true, incl = true;
+        unsigned long long lo = 0, hi = 0;
+        if (q >= 0) {
+            const unsigned long long* w = status + (uint64_t)q * SCAN_WORDS;
+            const unsigned long long il = scan_ld(w + 2), ih = scan_ld(w + 3);
+            const bool ok = (il >> SCAN_SHIFT) == tag && (ih >> SCAN_SHIFT) == tag;
+            if (ok) {
+                lo = il; hi = ih;
+            } else {
+                incl = false;
+                lo = scan_ld(w);
+                hi = scan_ld(w + 1);
+                ready = (lo >> SCAN_SHIFT) == tag && (hi >> SCAN_SHIFT) == tag;
+            }
+        }
+        const uint64_t bi = wave_ballot(ready && incl);
+        const uint64_t nr = wave_ballot(!ready);
+        const int f = bi ? __builtin_ctzll(bi) : 64;
+        const uint64_t need = f >= 63 ? ~0ull : ((2ull << f) - 1);  // lanes 0..f
+        if (nr & need) continue;                                     // spin on the window
+        const unsigned long long x = (lo & 0xffffffffull) | ((hi & 0xffffffffull) << 32);
+        excl += wave_sum<TO>((ln <= f) ? (TO)x : (TO)0);
+        if (f < 64) break;
+        j -= 64;
+    }
+    if (threadIdx.x == 0) scan_post<TO>(my + 2, tg, excl + tot);
+    return excl;
+}
+
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(NT) k_scan1(const TI* in, TO* out, uint64_t n_max, const uint64_t* n_dev,
                                               unsigned long long* __restrict__ status,
@@ -120,45 +167,8 @@ __global__ void __launch_bounds__(NT) k_scan1(const TI* in, TO* out, uint64_t n_
     }
     TO tot;
     const TO pre = block_excl_scan<TO>(s, lds, tot);
-    const unsigned long long tg = (unsigned long long)tag << SCAN_SHIFT;
     if (threadIdx.x < 64) {
-        TO excl = 0;
-        unsigned long long* my = status + (uint64_t)tile * SCAN_WORDS;
-        if (tile == 0) {
-            if (threadIdx.x == 0) scan_post<TO>(my + 2, tg, tot);
-        } else {
-            if (threadIdx.x == 0) scan_post<TO>(my, tg, tot);
-            const int ln = (int)threadIdx.x;
-            int64_t j = (int64_t)tile - 1;
-            while (true) {
-                const int64_t q = j - ln;
-                bool ready = true, incl = true;
-                unsigned long long lo = 0, hi = 0;
-                if (q >= 0) {
-                    const unsigned long long* w = status + (uint64_t)q * SCAN_WORDS;
-                    const unsigned long long il = scan_ld(w + 2), ih = scan_ld(w + 3);
-                    const bool ok = (il >> SCAN_SHIFT) == tag && (ih >> SCAN_SHIFT) == tag;
-                    if (ok) {
-                        lo = il; hi = ih;
-                    } else {
-                        incl = false;
-                        lo = scan_ld(w);
-                        hi = scan_ld(w + 1);
-                        ready = (lo >> SCAN_SHIFT) == tag && (hi >> SCAN_SHIFT) == tag;
-                    }
-                }
-                const uint64_t bi = wave_ballot(ready && incl);
-                const uint64_t nr = wave_ballot(!ready);
-                const int f = bi ? __builtin_ctzll(bi) : 64;
-                const uint64_t need = f >= 63 ? ~0ull : ((2ull << f) - 1);  // lanes 0..f
-                if (nr & need) continue;                                     // spin on the window
-                const unsigned long long x = (lo & 0xffffffffull) | ((hi & 0xffffffffull) << 32);
-                excl += wave_sum<TO>((ln <= f) ? (TO)x : (TO)0);
-                if (f < 64) break;
-                j -= 64;
-            }
-            if (threadIdx.x == 0) scan_post<TO>(my + 2, tg, excl + tot);
-        }
+        const TO excl = scan_lookback<TO>(status, tile, tag, tot);
         if (threadIdx.x == 0) s_prefix = excl;
     }
     __syncthreads();

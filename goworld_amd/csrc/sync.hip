@@ -56,117 +56,175 @@ __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) 
     }
 }
 
+// ---------------------------------------------------------------------------
+// flagged entities in slot order, by a one-launch stream compaction (decoupled
+// look-back, prim.hpp): flagged[k] = slot, fbits[k] = its syncInfoFlag.  The
+// flags are cleared here, so the write pass reads fbits and can be rerun
+// after the record buffer overflowed.
+__global__ void __launch_bounds__(NT) k_flag_compact1(uint32_t* __restrict__ flags, uint32_t cap,
+                                                      uint32_t* __restrict__ flagged, uint32_t* __restrict__ fbits,
+                                                      unsigned long long* __restrict__ status,
+                                                      unsigned long long* __restrict__ ticket,
+                                                      unsigned long long tbase, uint32_t tag, uint32_t* total) {
+    __shared__ uint32_t lds[NWAVE];
+    __shared__ uint32_t s_tile, s_prefix;
+    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tbase);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t base = (uint64_t)tile * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_IPT;
+    uint32_t f[SCAN_IPT];
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_IPT; ++j) {
+        f[j] = base + j < cap ? flags[base + j] : 0u;
+        c += f[j] != 0;
+    }
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan<uint32_t>(c, lds, tot);
+    if (threadIdx.x < 64) {
+        const uint32_t excl = scan_lookback<uint32_t>(status, tile, tag, tot);
+        if (threadIdx.x == 0) s_prefix = excl;
+    }
+    __syncthreads();
+    uint32_t at = s_prefix + pre;
+#pragma unroll
+    for (int j = 0; j < SCAN_IPT; ++j) {
+        if (f[j]) {
+            flagged[at] = (uint32_t)(base + j);
+            fbits[at] = f[j];
+            flags[base + j] = 0;
+            ++at;
+        }
+    }
+    if (tile == gridDim.x - 1 && threadIdx.x == 0) *total = s_prefix + tot;
+}
+void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint32_t* fbits, ScanCtx& sc,
+                         uint32_t* total, hipStream_t s) {
+    uint32_t nb = (uint32_t)((cap + SCAN_TILE - 1) / SCAN_TILE);
+    if (nb == 0) nb = 1;
+    if (sc.tag >= SCAN_TAG_MAX) {
+        (void)hipMemsetAsync(sc.status, 0, sc.max_tiles * SCAN_WORDS * 8, s);
+        sc.tag = 0;
+    }
+    ++sc.tag;
+    hipLaunchKernelGGL(k_flag_compact1, dim3(nb), dim3(NT), 0, s, flags, cap, flagged, fbits, sc.status, sc.ticket,
+                       sc.tbase, sc.tag, total);
+    sc.tbase += nb;
+}
+
 // Flagged entities are walked by a capped grid of waves (grid-stride): the
 // count lives on the device, so a grid sized for the worst case would
 // dispatch mostly empty waves.
 constexpr uint32_t SYNC_MAX_BLOCKS = 8192;
 
-// record count per flagged entity (one wave each)
+// record count per flagged entity: a lane per entity (the diff's cached count
+// of neighbours with a client when it is from this epoch); the entities that
+// need a window walk are then walked one at a time by the whole wave
 template <int U>
 __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __restrict__ flagged,
-                                                   const uint64_t* nf_dev, uint32_t nf_max, uint32_t* cnt,
-                                                   DevStats* st) {
+                                                   const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
+                                                   uint32_t nf_max, uint32_t* cnt) {
     const uint64_t nf = load_n(nf_max, nf_dev);
-    const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
-    for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < nf; k += stride) {
-        const uint32_t e = flagged[k];
-        const uint32_t f = w.flags[e];
-        uint32_t r = 0;
-        if (w.aoi[e].meta & PRESENT_BIT) {
-            if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) r = 1;
-            if (f & GW_SIF_NEIGHBOR_CLIENTS) {
-                const unsigned long long c = w.nbc[e];
-                if ((uint32_t)(c >> 32) == w.epoch) {
-                    r += (uint32_t)c;                        // counted by this tick's diff
-                } else {
-                    uint32_t n = 0;
-                    wave_neighbors<U>(w, e, [&](bool rel, uint32_t, uint32_t g) {
-                        n += (uint32_t)popc64(wave_ballot(rel && g != 0));
-                    });
-                    r += n;
+    const int ln = lane_id();
+    const uint64_t stride = (uint64_t)gridDim.x * NT;
+    for (uint64_t base = (uint64_t)blockIdx.x * NT + (threadIdx.x & ~63u); base < nf; base += stride) {
+        const uint64_t k = base + ln;
+        const bool valid = k < nf;
+        uint32_t e = 0, f = 0, r = 0;
+        bool walk = false;
+        if (valid) {
+            e = flagged[k];
+            f = fbits[k];
+            if (w.aoi[e].meta & PRESENT_BIT) {
+                if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) r = 1;
+                if (f & GW_SIF_NEIGHBOR_CLIENTS) {
+                    const unsigned long long c = w.nbc[e];
+                    if ((uint32_t)(c >> 32) == w.epoch) r += (uint32_t)c;   // counted by this tick's diff
+                    else walk = true;
                 }
             }
         }
-        if (lane_id() == 0) cnt[k] = r;
+        uint64_t todo = wave_ballot(walk);
+        while (todo) {
+            const int q = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t eq = (uint32_t)__builtin_amdgcn_readlane((int)e, q);
+            uint32_t n = 0;
+            wave_neighbors<U>(w, eq, [&](bool rel, uint32_t, uint32_t g) {
+                n += (uint32_t)popc64(wave_ballot(rel && g != 0));
+            });
+            if (ln == q) r += n;
+        }
+        if (valid) cnt[k] = r;
     }
-    (void)st;
 }
-void launch_sync_count(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
-                       uint32_t* cnt, DevStats* st, hipStream_t s) {
+void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
+                       uint32_t nf_max, uint32_t* cnt, hipStream_t s) {
     if (!nf_max) return;
-    const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
-    if (w.nb_u >= 8) hipLaunchKernelGGL(k_sync_count<8>, g, dim3(NT), 0, s, w, flagged, nf_dev, nf_max, cnt, st);
-    else if (w.nb_u <= 2) hipLaunchKernelGGL(k_sync_count<2>, g, dim3(NT), 0, s, w, flagged, nf_dev, nf_max, cnt, st);
-    else hipLaunchKernelGGL(k_sync_count<4>, g, dim3(NT), 0, s, w, flagged, nf_dev, nf_max, cnt, st);
+    const dim3 g(std::min(nblk(nf_max, NT), SYNC_MAX_BLOCKS));
+    if (w.nb_u >= 8) hipLaunchKernelGGL(k_sync_count<8>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, cnt);
+    else if (w.nb_u <= 2) hipLaunchKernelGGL(k_sync_count<2>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, cnt);
+    else hipLaunchKernelGGL(k_sync_count<4>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, cnt);
 }
 
-// writes e's records at rec_off[k] and clears e's flags
+// writes e's records at rec_off[k] (nothing if the buffer is too small: the
+// host grows it and reruns this pass)
 template <int U>
 __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __restrict__ flagged,
-                                                   const uint64_t* nf_dev, uint32_t nf_max,
-                                                   const uint64_t* __restrict__ rec_off, gw_sync_record* rec,
-                                                   uint64_t rec_cap) {
+                                                   const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
+                                                   uint32_t nf_max, const uint64_t* __restrict__ rec_off,
+                                                   const uint32_t* __restrict__ cnt, gw_sync_record* rec,
+                                                   uint64_t rec_cap, DevStats* st) {
     const uint64_t nf = load_n(nf_max, nf_dev);
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
     const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
     for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < nf; k += stride) {
         const uint32_t e = flagged[k];
-        const uint32_t f = w.flags[e];
-        if (w.aoi[e].meta & PRESENT_BIT) {
-            const float4 p = w.pos[e];
-            uint64_t at = rec_off[k];
-            if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
-                if (ln == 0 && at < rec_cap) {
-                    gw_sync_record r;
-                    r.watcher = e; r.entity = e; r.x = p.x; r.y = p.y; r.z = p.z; r.yaw = p.w;
-                    rec[at] = r;
-                }
-                ++at;
-            }
-            if (f & GW_SIF_NEIGHBOR_CLIENTS) {
-                wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
-                    const bool take = rel && g != 0;
-                    const uint64_t bt = wave_ballot(take);
-                    if (take) {
-                        const uint64_t i = at + (uint64_t)popc64(bt & lt);
-                        gw_sync_record r;
-                        r.watcher = ws; r.entity = e; r.x = p.x; r.y = p.y; r.z = p.z; r.yaw = p.w;
-                        if (i < rec_cap) rec[i] = r;
-                    }
-                    at += (uint64_t)popc64(bt);
-                });
-            }
+        const uint32_t f = fbits[k];
+        uint64_t at = rec_off[k];
+        if (at + cnt[k] > rec_cap) {
+            if (ln == 0) atomicOr(&st->overflow, 1ull);
+            continue;
         }
-        if (ln == 0) w.flags[e] = 0;
+        if (!(w.aoi[e].meta & PRESENT_BIT)) continue;
+        const float4 p = w.pos[e];
+        if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
+            if (ln == 0) {
+                gw_sync_record r;
+                r.watcher = e; r.entity = e; r.x = p.x; r.y = p.y; r.z = p.z; r.yaw = p.w;
+                rec[at] = r;
+            }
+            ++at;
+        }
+        if (f & GW_SIF_NEIGHBOR_CLIENTS) {
+            wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
+                const bool take = rel && g != 0;
+                const uint64_t bt = wave_ballot(take);
+                if (take) {
+                    gw_sync_record r;
+                    r.watcher = ws; r.entity = e; r.x = p.x; r.y = p.y; r.z = p.z; r.yaw = p.w;
+                    rec[at + (uint64_t)popc64(bt & lt)] = r;
+                }
+                at += (uint64_t)popc64(bt);
+            });
+        }
     }
 }
-void launch_sync_write(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
-                       const uint64_t* rec_off, gw_sync_record* rec, uint64_t rec_cap, hipStream_t s) {
+void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
+                       uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
+                       uint64_t rec_cap, DevStats* st, hipStream_t s) {
     if (!nf_max) return;
     const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
     if (w.nb_u >= 8)
-        hipLaunchKernelGGL(k_sync_write<8>, g, dim3(NT), 0, s, w, flagged, nf_dev, nf_max, rec_off, rec, rec_cap);
+        hipLaunchKernelGGL(k_sync_write<8>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
+                           rec_cap, st);
     else if (w.nb_u <= 2)
-        hipLaunchKernelGGL(k_sync_write<2>, g, dim3(NT), 0, s, w, flagged, nf_dev, nf_max, rec_off, rec, rec_cap);
+        hipLaunchKernelGGL(k_sync_write<2>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
+                           rec_cap, st);
     else
-        hipLaunchKernelGGL(k_sync_write<4>, g, dim3(NT), 0, s, w, flagged, nf_dev, nf_max, rec_off, rec, rec_cap);
-}
-
-__global__ void __launch_bounds__(NT) k_flag_mark(const uint32_t* __restrict__ flags, uint32_t cap, uint32_t* mark) {
-    uint32_t s = blockIdx.x * NT + threadIdx.x;
-    if (s < cap) mark[s] = flags[s] != 0;
-}
-void launch_flag_mark(const uint32_t* flags, uint32_t cap, uint32_t* mark, hipStream_t s) {
-    hipLaunchKernelGGL(k_flag_mark, dim3(nblk1(cap, NT)), dim3(NT), 0, s, flags, cap, mark);
-}
-__global__ void __launch_bounds__(NT) k_flag_compact(const uint32_t* __restrict__ mark, const uint64_t* __restrict__ pre,
-                                                     uint32_t cap, uint32_t* flagged) {
-    uint32_t s = blockIdx.x * NT + threadIdx.x;
-    if (s < cap && mark[s]) flagged[pre[s]] = s;
-}
-void launch_flag_compact(const uint32_t* mark, const uint64_t* pre, uint32_t cap, uint32_t* flagged, hipStream_t s) {
-    hipLaunchKernelGGL(k_flag_compact, dim3(nblk1(cap, NT)), dim3(NT), 0, s, mark, pre, cap, flagged);
+        hipLaunchKernelGGL(k_sync_write<4>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
+                           rec_cap, st);
 }
 
 // per-gate record histogram: LDS buckets for gates < 256, global atomics above

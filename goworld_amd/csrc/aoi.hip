@@ -730,11 +730,11 @@ void tick_diff(const TickBufs& b, hipStream_t s) {
     case 4: hipLaunchKernelGGL((k_mover<2, 4>), dim3(nblk1(nmax, 4)), dim3(256), 0, s, b); break;
     default: hipLaunchKernelGGL((k_mover<2, 1>), dim3(nblk1(nmax, 1)), dim3(64), 0, s, b); break;
     }
-    hipLaunchKernelGGL(k_big_own, dim3(64), dim3(NT), 0, s, b);
 }
 void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint64_t nmax = 2ull * b.m;
     const uint32_t C = b.w.cap;
+    hipLaunchKernelGGL(k_big_own, dim3(64), dim3(NT), 0, s, b);
     scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.cnt64, b.off64, (uint64_t)C + 1, nullptr, sc,
                                        (uint64_t*)&b.st->ev_pk, s);
     hipLaunchKernelGGL(k_own_copy, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);

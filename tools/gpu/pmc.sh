@@ -10,6 +10,7 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d gpurun_out/pmc_$tag/p$i -o run -- python3 bench.py --steps 3 --warmup 10 --no-cpu-baseline --profile-stages 0 > gpurun_out/pmc_$tag/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmc_$tag/p$i.log; exit 1; }
   f=$(find gpurun_out/pmc_$tag/p$i -name '*counter_collection.csv' | head -1)
-  python3 tools/pmc_summary.py "$f" > gpurun_out/pmc_$tag/p$i.txt && rm -f "$f" $(find gpurun_out/pmc_$tag/p$i -name '*kernel_trace.csv')
+  python3 tools/pmc_summary.py "$f" --json gpurun_out/pmc_$tag/pmc.json > gpurun_out/pmc_$tag/p$i.txt && rm -f "$f" $(find gpurun_out/pmc_$tag/p$i -name '*kernel_trace.csv')
   cat gpurun_out/pmc_$tag/p$i.txt
 done
+cp gpurun_out/pmc_$tag/pmc.json gpurun_out/pmc_${tag}.json

@@ -53,7 +53,8 @@ __global__ void __launch_bounds__(NT) k_ops1(TickBufs b) {
     uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i >= b.m) return;
     gw_op op = b.ops[i];
-    if (op.slot >= b.w.cap || op.kind < GW_OP_ENTER || op.kind > GW_OP_SYNC) {
+    if (op.kind == GW_OP_NOP) return;
+    if (op.slot >= b.w.cap || op.kind > GW_OP_SYNC) {
         atomicAdd(&b.st->bad_ops, 1ull);
         return;
     }
@@ -89,7 +90,7 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
                 p.oz = was ? a.z : qnan();
                 p.ostamp = b.w.stamp[s];
                 b.w.prev[s] = p;
-                b.w.stamp[s] = b.stamp_base + i;
+                b.w.stamp[s] = b.stamps ? b.stamps[i] : b.stamp_base + i;
                 if (op.kind == GW_OP_LEAVE) a.meta &= ~PRESENT_BIT;
                 else { a.x = op.x; a.z = op.z; a.meta |= PRESENT_BIT; }
                 b.w.aoi[s] = a;
@@ -482,6 +483,9 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     const SpaceP P = w.sp[me.space];
     const float d = P.d;
     const bool pn = me.x == me.x, po = me.ox == me.ox;
+    // decomposed world: A's own events only where A is owned (after the tick,
+    // before it for a leaver); an op-less B's events only where B is owned
+    const bool ownA = owned_x(P, pn ? me.x : me.ox);
     const unsigned long long sA = w.stamp[A], soA = w.prev[A].ostamp;
     const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
     const Rects R = mover_rects(P, po, me.ox, me.oz, pn, me.x, me.z);
@@ -539,7 +543,8 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
                     key = (e.slot << 1) | (lv ? 1u : 0u);
                 }
             }
-            const bool mev = ev && nmv;
+            const bool mev = ev && nmv && owned_x(P, e.x);
+            ev = ev && ownA;
             // B has no op: (B,A) is B's event too: count it (no return value,
             // so the candidate loop never waits on the atomic)
 #ifndef GW_EXP_NO_MIR_ATOMIC

@@ -42,6 +42,7 @@ struct SpaceHost {
 struct OpSeg {            // submission order of a tick: host or device segment
     bool host;
     const gw_op* dev;
+    const uint64_t* stamps;   // explicit global stamps (device) or nullptr
     uint32_t n;
     size_t host_off;
 };
@@ -57,6 +58,7 @@ struct Stage {
 struct gw_ctx {
     int dev = 0;
     hipStream_t st = nullptr;
+    hipStream_t own_st = nullptr;   // the context's own stream (st may be a caller's)
     std::string err;
 
     std::vector<SpaceHost> spaces;
@@ -96,7 +98,7 @@ struct gw_ctx {
     DevStats* hstats = nullptr;    // pinned host
 
     // grid + tick scratch
-    DevBuf ops_buf, k0, v0, k1, v1, gm, cand, reg, own, big, bigseg;
+    DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, cand, reg, own, big, bigseg;
     DevBuf mir, mir_cnt;
     DevBuf off64, enter_d, leave_d, scan_status, rs_hist;
     ScanCtx sc{};                  // single-pass scan state (prim.hpp)
@@ -483,7 +485,8 @@ int gw_init(int device_id, gw_ctx** out) {
     int rc = 0;
     do {
         if (hipSetDevice(device_id) != hipSuccess) { rc = set_err(c, GW_EDEVICE, "hipSetDevice(%d) failed", device_id); break; }
-        if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { rc = set_err(c, GW_EDEVICE, "stream"); break; }
+        if (hipStreamCreateWithFlags(&c->own_st, hipStreamNonBlocking) != hipSuccess) { rc = set_err(c, GW_EDEVICE, "stream"); break; }
+        c->st = c->own_st;
         if (hipMalloc(&c->stats, sizeof(DevStats)) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "stats"); break; }
         if (hipHostMalloc((void**)&c->hstats, sizeof(DevStats), hipHostMallocDefault) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "hstats"); break; }
         if (hipMalloc(&c->scal32, 64) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "scal"); break; }
@@ -510,7 +513,7 @@ void gw_shutdown(gw_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    DevBuf* bufs[] = {&c->ops_buf, &c->k0, &c->v0, &c->k1, &c->v1, &c->bigseg,
+    DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->k0, &c->v0, &c->k1, &c->v1, &c->bigseg,
                       &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->off64, &c->mir,
                       &c->mir_cnt,
                       &c->enter_d, &c->leave_d, &c->scan_status, &c->rs_hist,
@@ -527,7 +530,7 @@ void gw_shutdown(gw_ctx* c) {
     for (auto& s : c->stages) { (void)hipEventDestroy(s.a); (void)hipEventDestroy(s.b); }
     if (c->ev_t0) (void)hipEventDestroy(c->ev_t0);
     if (c->ev_t1) (void)hipEventDestroy(c->ev_t1);
-    if (c->st) (void)hipStreamDestroy(c->st);
+    if (c->own_st) (void)hipStreamDestroy(c->own_st);
     delete c;
 }
 
@@ -567,6 +570,8 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
     s.p.H = std::max(1, (int)std::ceil(ez / cs));
     s.p.cell_base = c->total_cells;
     s.p.alive = 1;
+    s.p.own_lo = -INFINITY;
+    s.p.own_hi = INFINITY;
     uint64_t ncells = (uint64_t)s.p.W * (uint64_t)s.p.H;
     if ((uint64_t)c->total_cells + ncells + 1 >= (1ull << 31)) return set_err(c, GW_ERANGE, "too many grid cells");
     int rc;
@@ -604,7 +609,7 @@ int gw_submit(gw_ctx* c, const gw_op* ops, uint32_t n) {
         int rc = validate_ops(c, ops, n);
         if (rc) return rc;
     }
-    OpSeg sg{true, nullptr, n, c->pend_host.size()};
+    OpSeg sg{true, nullptr, nullptr, n, c->pend_host.size()};
     c->pend_host.insert(c->pend_host.end(), ops, ops + n);
     c->segs.push_back(sg);
     return 0;
@@ -614,8 +619,25 @@ int gw_submit_device(gw_ctx* c, const gw_op* dev_ops, uint32_t n) {
     if (!c || (!dev_ops && n)) return GW_EINVAL;
     if (!n) return 0;
     c->validate = false;   // device-resident ops are trusted; the host mirror is no longer exact
-    c->segs.push_back(OpSeg{false, dev_ops, n, 0});
+    c->segs.push_back(OpSeg{false, dev_ops, nullptr, n, 0});
     return 0;
+}
+
+int gw_submit_device_stamped(gw_ctx* c, const gw_op* dev_ops, const uint64_t* dev_stamps, uint32_t n) {
+    if (!c || ((!dev_ops || !dev_stamps) && n)) return GW_EINVAL;
+    if (!n) return 0;
+    c->validate = false;
+    c->segs.push_back(OpSeg{false, dev_ops, dev_stamps, n, 0});
+    return 0;
+}
+
+int gw_space_set_ownership(gw_ctx* c, uint32_t sid, float x_lo, float x_hi) {
+    if (!c) return GW_EINVAL;
+    if (sid >= c->spaces.size() || !c->spaces[sid].alive) return set_err(c, GW_ERANGE, "no space %u", sid);
+    if (!(x_lo < x_hi)) return set_err(c, GW_EINVAL, "empty ownership range");
+    c->spaces[sid].p.own_lo = x_lo;
+    c->spaces[sid].p.own_hi = x_hi;
+    return upload_spaces(c);
 }
 
 int gw_set_clients(gw_ctx* c, const uint32_t* slots, const uint16_t* gates, uint32_t n) {
@@ -658,10 +680,23 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     if ((rc = rebuild_grid(c))) return rc;           // the pre-tick grid (syncs only when dirty)
     // ---- the tick's op stream, in submission order -----------------------
     const gw_op* ops = nullptr;
+    const unsigned long long* stamps = nullptr;
+    bool any_stamped = false, all_stamped = true;
+    for (auto& s : c->segs) {
+        any_stamped |= s.stamps != nullptr;
+        all_stamped &= s.stamps != nullptr;
+    }
+    if (any_stamped && !all_stamped) {
+        c->segs.clear();
+        c->pend_host.clear();
+        return set_err(c, GW_EINVAL, "a tick mixes stamped and unstamped ops");
+    }
     if (c->segs.size() == 1 && !c->segs[0].host) {
         ops = c->segs[0].dev;
+        stamps = (const unsigned long long*)c->segs[0].stamps;
     } else {
         if ((rc = ensure(c, c->ops_buf, (size_t)M * sizeof(gw_op)))) return rc;
+        if (any_stamped && (rc = ensure(c, c->stamp_buf, (size_t)M * 8))) return rc;
         size_t off = 0;
         for (auto& s : c->segs) {
             if (s.host)
@@ -670,9 +705,13 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
             else
                 HIPCHK(hipMemcpyAsync(P<gw_op>(c->ops_buf) + off, s.dev, (size_t)s.n * sizeof(gw_op),
                                       hipMemcpyDeviceToDevice, c->st));
+            if (s.stamps)
+                HIPCHK(hipMemcpyAsync(P<uint64_t>(c->stamp_buf) + off, s.stamps, (size_t)s.n * 8,
+                                      hipMemcpyDeviceToDevice, c->st));
             off += s.n;
         }
         ops = P<gw_op>(c->ops_buf);
+        if (any_stamped) stamps = P<unsigned long long>(c->stamp_buf);
     }
     const uint32_t NC = c->total_cells;
     const uint64_t M2 = 2ull * M;
@@ -701,6 +740,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     TickBufs b{};
     b.w = world(c);
     b.ops = ops; b.m = M; b.stamp_base = c->stamp_base;
+    b.stamps = stamps;
     b.diff_u = c->diff_u;
     b.last_pos = c->last_pos; b.last_aoi = c->last_aoi; b.last_leave = c->last_leave;
     b.st = st;
@@ -1028,6 +1068,14 @@ int gw_memcpy_d2h(gw_ctx* c, void* dst, const void* src, size_t bytes) {
 int gw_synchronize(gw_ctx* c) {
     if (!c) return GW_EINVAL;
     HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int gw_set_stream(gw_ctx* c, void* stream) {
+    if (!c) return GW_EINVAL;
+    (void)hipSetDevice(c->dev);
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->st = stream ? (hipStream_t)stream : c->own_st;
     return 0;
 }
 

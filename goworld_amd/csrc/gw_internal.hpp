@@ -68,7 +68,10 @@ struct alignas(16) SpaceP {
     int32_t W, H;
     uint32_t cell_base;
     uint32_t alive;
+    float own_lo, own_hi;      // ownership x-range (decomposed world), default (-inf, +inf)
+    float pad0, pad1;
 };
+__device__ __forceinline__ bool owned_x(const SpaceP& P, float x) { return x >= P.own_lo && x < P.own_hi; }
 
 constexpr int STAT_SHARDS = 256;
 constexpr int SH_FIELDS = 4;
@@ -144,6 +147,7 @@ struct World {
 struct TickBufs {
     World w;                  // gn / gn_start: the grid before the tick (the new one from tick_movers on)
     const gw_op* ops;
+    const unsigned long long* stamps;   // explicit global stamps (nullptr: stamp_base + index)
     uint32_t m;               // ops in the stream
     unsigned long long stamp_base;
     int32_t *last_pos, *last_aoi, *last_leave;

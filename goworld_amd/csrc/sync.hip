@@ -135,7 +135,8 @@ __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __re
         if (valid) {
             e = flagged[k];
             f = fbits[k];
-            if (w.aoi[e].meta & PRESENT_BIT) {
+            const AoiEnt a = w.aoi[e];
+            if ((a.meta & PRESENT_BIT) && owned_x(w.sp[a.meta & SPACE_MASK], a.x)) {
                 if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) r = 1;
                 if (f & GW_SIF_NEIGHBOR_CLIENTS) {
                     const unsigned long long c = w.nbc[e];
@@ -187,7 +188,8 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
             if (ln == 0) atomicOr(&st->overflow, 1ull);
             continue;
         }
-        if (!(w.aoi[e].meta & PRESENT_BIT)) continue;
+        const AoiEnt a = w.aoi[e];
+        if (!(a.meta & PRESENT_BIT) || !owned_x(w.sp[a.meta & SPACE_MASK], a.x)) continue;
         const float4 p = w.pos[e];
         if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
             if (ln == 0) {

@@ -1,0 +1,384 @@
+"""Decomposed world: one AOI space split into X-strips, one strip per process
+(SURVEY.md 8(e) regime 2, BASELINE config #5).
+
+The reference never splits a space across processes (one Space lives in one
+game process, engine/entity/SpaceManager.go:11-31); this is the scale-out of
+the same contract.  go-aoi's relation is a pure function of the two positions
+and of which member made the later AOI call, so a strip needs
+no neighbour lists from its neighbours, only the current state of the
+entities near its borders:
+
+* rank r OWNS the entities whose x lies in [lo_r, hi_r) and HOLDS, in one
+  local space, every entity whose x lies in its extended range
+  [lo_r - h, hi_r + h) (owned + ghosts), h = d + 2*max_step + margin;
+* the owner (at the start of the tick) applies an entity's ops and forwards
+  their NET effect to each neighbour whose extended range the entity is in
+  before or after the tick, as up to three rows per entity, in order:
+    LEAVE  (the entity left the space and came back inside the tick),
+    ENTER / MOVED / LEAVE  (the net AOI change relative to that range; the
+           payload and global stamp of the entity's last AOI op),
+    SYNC   (the payload of its last non-Leave op and every sync flag still
+           pending since the last collect);
+  which reproduces exactly the state the engine keeps per entity (Space.go:
+  196-250 via gw_op semantics: pos = last non-Leave op, AOI state and stamp =
+  last AOI op, flags = OR since the last Leave);
+* every op carries a global stamp (tick-major, then rank-major, then the op's
+  index), so all ranks order the ops of all ranks the same way;
+* after the tick a rank emits events only for watchers, and sync records only
+  for entities, that it owns (gw_space_set_ownership).  An entity that
+  crosses a border is a ghost of the new owner already, so its old relations
+  are known where its events are computed.
+
+Requirements (checked): a present entity moves at most max_step in x per tick;
+strips are wider than h + max_step, so an entity is only ever held by its
+owner and the owner's two neighbours.
+
+The op routing (masks, per-entity reductions, compaction into fixed-size
+NOP-padded buffers) is torch on the engine's device with no host sync; the
+halo exchange is torch.distributed point-to-point (RCCL over xGMI with the
+nccl backend, gloo for the CPU tests); all AOI work is the HIP engine's
+(gpuaoi.py), on torch's stream (gw_set_stream).  Local slots are the global
+entity ids (the local space's capacity is the world population).
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+import torch
+
+OP_NOP, OP_ENTER, OP_MOVED, OP_LEAVE, OP_SYNC = 0, 1, 2, 3, 4
+SIF_MASK = 3            # GW_SIF_OWN_CLIENT | GW_SIF_NEIGHBOR_CLIENTS (include/gpuaoi.h)
+OP_WORDS = 6            # gw_op as 6 int32 words: kind | flags<<8, slot, x, y, z, yaw
+ROW_WORDS = 8           # + the u64 stamp
+ROWS_PER_ENTITY = 3
+STAMP_STRIDE = 1 << 26  # stamp = 1 + (tick * ranks + rank) * STAMP_STRIDE + op index
+
+
+@dataclasses.dataclass
+class Strips:
+    """Geometry: strip r = [x0 + r*w, x0 + (r+1)*w); the outer strips extend
+    to infinity."""
+    x0: float
+    w: float
+    ranks: int
+    d: float
+    max_step: float
+
+    def __post_init__(self):
+        if self.ranks > 2 and not self.w > self.h + self.max_step:
+            raise ValueError(f"strip width {self.w} must exceed halo {self.h} + max_step {self.max_step}")
+
+    @property
+    def h(self) -> float:
+        # a relation needs |dx| <= d (+ float32 rounding of c +- d); an entity
+        # that crossed a border moved <= max_step, so its old neighbours lie
+        # within d + max_step of the strip; one more max_step for their moves
+        return float(self.d + 2 * self.max_step + 1.0 + 1e-5 * (abs(self.x0) + self.ranks * self.w))
+
+    def lo(self, r: int) -> float:
+        return -np.inf if r == 0 else self.x0 + r * self.w
+
+    def hi(self, r: int) -> float:
+        return np.inf if r == self.ranks - 1 else self.x0 + (r + 1) * self.w
+
+    def ext(self, r: int) -> tuple[float, float]:
+        return self.lo(r) - self.h, self.hi(r) + self.h
+
+    def owner(self, x) -> np.ndarray:
+        r = np.floor((np.asarray(x, np.float64) - self.x0) / self.w).astype(np.int64)
+        return np.clip(r, 0, self.ranks - 1)
+
+    def own_range_f32(self, r: int) -> tuple[float, float]:
+        """[lo, hi) as float32 bounds with the same membership for float32 x."""
+        def f(v, side):
+            if not np.isfinite(v):
+                return float(np.float32(-3.0e38 if side < 0 else 3.0e38))
+            v32 = np.float32(v)
+            # smallest float32 >= v (x >= lo  <=>  x >= that float32)
+            if float(v32) < v:
+                v32 = np.nextafter(v32, np.float32(np.inf), dtype=np.float32)
+            return float(v32)
+        return f(self.lo(r), -1), f(self.hi(r), 1)
+
+
+def stamps_for(tick: int, rank: int, ranks: int, n: int, device) -> torch.Tensor:
+    if n >= STAMP_STRIDE:
+        raise ValueError("too many ops in one tick for the stamp layout")
+    base = 1 + (tick * ranks + rank) * STAMP_STRIDE
+    return torch.arange(base, base + n, dtype=torch.int64, device=device)
+
+
+def ops_to_words(ops: np.ndarray) -> np.ndarray:
+    """gw_op structured array -> (n, 6) int32 words (same bytes)."""
+    return np.ascontiguousarray(ops).view(np.int32).reshape(-1, OP_WORDS)
+
+
+def words_to_ops(words: np.ndarray) -> np.ndarray:
+    from .traces import OP_DTYPE
+    return np.ascontiguousarray(words, dtype=np.int32).reshape(-1).view(OP_DTYPE)
+
+
+def _f32(words_col: torch.Tensor) -> torch.Tensor:
+    return words_col.contiguous().view(torch.float32)
+
+
+class Router:
+    """Routing state of one rank: position, presence and pending sync flags of
+    every entity the rank holds (owned or ghost), indexed by global id (+ one
+    dummy row, index n, that absorbs masked-out scatters)."""
+
+    def __init__(self, geom: Strips, rank: int, n_global: int, device, halo_cap: int):
+        self.g, self.r, self.n, self.dev, self.K = geom, rank, n_global, device, halo_cap
+        n1 = n_global + 1
+        self.x = torch.zeros(n1, dtype=torch.float32, device=device)
+        self.present = torch.zeros(n1, dtype=torch.bool, device=device)
+        self.pflags = torch.zeros(n1, dtype=torch.int32, device=device)
+        self.scratch = torch.full((n1,), -1, dtype=torch.int64, device=device)
+        self.overflow = torch.zeros((), dtype=torch.int64, device=device)
+        self.bad_moves = torch.zeros((), dtype=torch.int64, device=device)
+        self.ext_lo, self.ext_hi = geom.ext(rank)
+        self.lo, self.hi = geom.lo(rank), geom.hi(rank)
+
+    # -- per-entity reductions over one op list (scratch is left all -1) ----
+    def _last(self, slot, idx, mask):
+        t = self.scratch
+        key = torch.where(mask, idx, torch.full_like(idx, -1))
+        t.scatter_reduce_(0, slot, key, reduce="amax", include_self=True)
+        out = t[slot]
+        t[slot] = -1
+        return out
+
+    def _or_flags(self, slot, flags, mask):
+        out = torch.zeros_like(flags)
+        t = self.scratch
+        for b in range(2):
+            bit = torch.where(mask, (flags >> b) & 1, torch.zeros_like(flags)).to(torch.int64)
+            t.scatter_reduce_(0, slot, bit, reduce="amax", include_self=True)
+            out |= (t[slot].clamp(min=0).to(flags.dtype) << b)
+            t[slot] = -1
+        return out
+
+    def route(self, words: torch.Tensor, stamps: torch.Tensor):
+        """Owned ops of one tick -> (send to left, send to right): NOP-padded
+        int32 row buffers ((K+1) * 3, 8).  Updates the routing state.  No host
+        sync."""
+        g, r = self.g, self.r
+        m = words.shape[0]
+        dev = self.dev
+        kind = words[:, 0] & 0xFF
+        flags = (words[:, 0] >> 8) & SIF_MASK
+        valid = (kind >= OP_ENTER) & (kind <= OP_SYNC)
+        slot = torch.where(valid, words[:, 1].to(torch.int64), torch.full((m,), self.n, dtype=torch.int64, device=dev))
+        idx = torch.arange(m, dtype=torch.int64, device=dev)
+        aoi = valid & (kind != OP_SYNC)
+        lv = kind == OP_LEAVE
+        la = self._last(slot, idx, aoi)                       # last AOI op
+        ll = self._last(slot, idx, lv)                        # last Leave
+        lp = self._last(slot, idx, valid & ~lv)               # last payload op
+        lany = self._last(slot, idx, valid)                   # the entity's representative row
+        fo = self._or_flags(slot, flags, valid & (idx > ll))
+        rep = valid & (lany == idx)
+        has_aoi, had_leave = la >= 0, ll >= 0
+        la_c, lp_c = la.clamp(min=0), lp.clamp(min=0)
+        ka = kind[la_c]
+        xa = _f32(words[:, 2])[la_c]
+        old_x, old_p, old_f = self.x[slot], self.present[slot], self.pflags[slot]
+        new_p = torch.where(has_aoi, ka != OP_LEAVE, old_p)
+        new_x = torch.where(has_aoi & new_p, xa, old_x)
+        new_f = torch.where(new_p, torch.where(had_leave, torch.zeros_like(old_f), old_f) | fo,
+                            torch.zeros_like(old_f))
+        # the strip contract: an owned entity stays inside this rank's range + max_step
+        moved = rep & has_aoi & old_p & new_p
+        self.bad_moves += (moved & ((new_x - old_x).abs() > g.max_step)).sum()
+        sends = []
+        for nb in (r - 1, r + 1):
+            if nb < 0 or nb >= g.ranks:
+                sends.append(None)
+                continue
+            lo, hi = g.ext(nb)
+            was = old_p & (old_x >= lo) & (old_x < hi)
+            now = new_p & (new_x >= lo) & (new_x < hi)
+            nop = torch.zeros_like(kind)
+            k0 = torch.where(has_aoi & had_leave & was & now, torch.full_like(kind, OP_LEAVE), nop)
+            k1 = torch.where(now & (~was | had_leave), torch.full_like(kind, OP_ENTER),
+                             torch.where(was & now, torch.full_like(kind, OP_MOVED),
+                                         torch.where(was, torch.full_like(kind, OP_LEAVE), nop)))
+            k1 = torch.where(has_aoi, k1, nop)
+            k2 = torch.where(now & ((new_f != 0) | (lp > la)), torch.full_like(kind, OP_SYNC), nop)
+            sel = rep & ((k0 | k1 | k2) != 0)
+            sends.append(self._pack(words, stamps, slot, sel, k0, ll.clamp(min=0), k1, la_c,
+                                    k2, lp_c, new_f, lany))
+        # routing state of the rows this rank owns (dummy row n absorbs the rest)
+        s = torch.where(rep, slot, torch.full_like(slot, self.n))
+        self.x[s] = new_x
+        self.present[s] = new_p
+        self.pflags[s] = new_f
+        return sends[0], sends[1]
+
+    def _pack(self, words, stamps, slot, sel, k0, i0, k1, i1, k2, i2, f2, i_last):
+        """Entity rows (row 0, 1, 2 of each selected entity) compacted into a
+        buffer of K entities; unused rows are NOPs (all-zero)."""
+        K = self.K
+        m = words.shape[0]
+        pos = torch.cumsum(sel.to(torch.int64), 0) - 1
+        self.overflow = torch.maximum(self.overflow, sel.sum() - K)
+        dst = torch.where(sel & (pos < K), pos, torch.full_like(pos, K))
+        st32 = stamps.contiguous().view(torch.int32).view(-1, 2)
+        rows = torch.zeros((m, ROWS_PER_ENTITY, ROW_WORDS), dtype=torch.int32, device=self.dev)
+        s32 = slot.to(torch.int32)
+        # row 0: LEAVE before a re-Enter inside the tick
+        rows[:, 0, 0] = k0
+        rows[:, 0, 1] = s32
+        rows[:, 0, 6:] = st32[i0]
+        # row 1: the net AOI op, with the last AOI op's payload and stamp
+        rows[:, 1, 0] = k1
+        rows[:, 1, 1] = s32
+        rows[:, 1, 2:6] = words[i1, 2:6]
+        rows[:, 1, 6:] = st32[i1]
+        # row 2: SYNC with the latest payload and the pending flags
+        rows[:, 2, 0] = k2 | (f2 << 8)
+        rows[:, 2, 1] = s32
+        rows[:, 2, 2:6] = words[i2, 2:6]
+        rows[:, 2, 6:] = st32[i_last.clamp(min=0)]
+        rows = rows * (torch.stack([k0, k1, k2], 1) != 0).to(torch.int32).unsqueeze(2)
+        buf = torch.zeros((K + 1, ROWS_PER_ENTITY, ROW_WORDS), dtype=torch.int32, device=self.dev)
+        buf.index_copy_(0, dst, rows)   # duplicates only at the trash row K
+        buf[K].zero_()
+        return buf.view(-1, ROW_WORDS)
+
+    def receive(self, buf: torch.Tensor):
+        """Ghost rows from a neighbour -> (words, stamps) for the engine;
+        updates the routing state."""
+        K = self.K
+        rows = buf.view(K + 1, ROWS_PER_ENTITY, ROW_WORDS)[:K]
+        k1 = rows[:, 1, 0] & 0xFF
+        k2 = rows[:, 2, 0] & 0xFF
+        f2 = (rows[:, 2, 0] >> 8) & SIF_MASK
+        kany = (rows[:, 0, 0] | rows[:, 1, 0] | rows[:, 2, 0]) & 0xFF
+        slot = torch.maximum(torch.maximum(rows[:, 0, 1], rows[:, 1, 1]), rows[:, 2, 1]).to(torch.int64)
+        slot = torch.where(kany != 0, slot, torch.full_like(slot, self.n))
+        cur_x, cur_p = self.x[slot], self.present[slot]
+        p = torch.where(k1 != 0, k1 != OP_LEAVE, cur_p)
+        x = torch.where((k1 != 0) & p, _f32(rows[:, 1, 2]), cur_x)
+        f = torch.where(k2 != 0, f2, torch.zeros_like(f2))
+        self.x[slot] = x
+        self.present[slot] = p
+        self.pflags[slot] = f
+        flat = rows.reshape(-1, ROW_WORDS)
+        return flat[:, :OP_WORDS].contiguous(), flat[:, OP_WORDS:].contiguous().view(torch.int64).view(-1)
+
+    def collected(self):
+        """Sync flags are cleared everywhere by a collect (Entity.go:1221-1267)."""
+        self.pflags.zero_()
+
+
+def exchange(pg, rank: int, ranks: int, send_left, send_right, nrows: int, device, comm_device):
+    """Halo exchange with both neighbours (point-to-point, one round)."""
+    import torch.distributed as dist
+    shape = (nrows, ROW_WORDS)
+    mv = (lambda t: t) if comm_device == device else (lambda t: t.to(comm_device))
+    recv = {}
+    ops = []
+    for nb, send in ((rank - 1, send_left), (rank + 1, send_right)):
+        if 0 <= nb < ranks:
+            recv[nb] = torch.empty(shape, dtype=torch.int32, device=comm_device)
+            ops.append(dist.P2POp(dist.isend, mv(send).contiguous(), nb, group=pg))
+            ops.append(dist.P2POp(dist.irecv, recv[nb], nb, group=pg))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    back = (lambda t: t) if comm_device == device else (lambda t: t.to(device))
+    return [back(recv[nb]) for nb in (rank - 1, rank + 1) if nb in recv]
+
+
+class HipStrip:
+    """Engine adapter: a gpuaoi.GpuAOI context sharing one stream with torch
+    (made torch's current stream), so routing kernels, collectives and AOI
+    kernels are ordered without host syncs."""
+
+    def __init__(self, g):
+        self.g = g
+        self._keep = []
+        self.stream = torch.cuda.Stream()
+        torch.cuda.set_stream(self.stream)
+        g.set_stream(self.stream.cuda_stream)
+
+    def create_space(self, d, cap, bounds):
+        return self.g.create_space(d, cap, bounds)
+
+    def set_ownership(self, sid, lo, hi):
+        self.g.set_ownership(sid, lo, hi)
+
+    def set_clients(self, slots, gates):
+        self.g.set_clients(slots, gates)
+
+    def submit(self, words: torch.Tensor, stamps: torch.Tensor):
+        words, stamps = words.contiguous(), stamps.contiguous()
+        self._keep += [words, stamps]        # alive until the tick has consumed them
+        self.g.submit_device_stamped(words.data_ptr(), stamps.data_ptr(), words.shape[0])
+
+    def tick(self, copy=True):
+        res = self.g.tick(copy=copy)
+        self._keep = []
+        return res
+
+    def collect(self, copy=True):
+        return self.g.sync_collect(copy=copy)
+
+
+class StripRank:
+    """One rank of a decomposed world.  `engine` follows HipStrip's interface
+    (create_space / set_ownership / set_clients / submit / tick / collect)."""
+
+    def __init__(self, engine, geom: Strips, rank: int, n_global: int, bounds, device,
+                 pg=None, comm_device=None, halo_cap: int = 1 << 14):
+        self.e, self.g, self.r = engine, geom, rank
+        self.dev = device
+        self.pg = pg
+        self.cdev = comm_device if comm_device is not None else device
+        self.router = Router(geom, rank, n_global, device, halo_cap)
+        self.sid, base = engine.create_space(geom.d, n_global, bounds)
+        if base != 0:
+            raise ValueError("a strip rank holds one space per context (local slot = global id)")
+        engine.set_ownership(self.sid, *geom.own_range_f32(rank))
+        self.tick_no = 0
+
+    def submit(self, words: torch.Tensor):
+        """Queue this rank's owned ops of one tick (int32 (m, 6) gw_op words on
+        the device, in call order), route and exchange the halo rows."""
+        m = words.shape[0]
+        st = stamps_for(self.tick_no, self.r, self.g.ranks, m, self.dev)
+        sl, sr = self.router.route(words, st)
+        nrows = (self.router.K + 1) * ROWS_PER_ENTITY
+        if self.g.ranks > 1:
+            recvd = exchange(self.pg, self.r, self.g.ranks, sl, sr, nrows, self.dev, self.cdev)
+        else:
+            recvd = []
+        parts_w, parts_s = [words], [st]
+        for buf in recvd:
+            w, s = self.router.receive(buf)
+            parts_w.append(w)
+            parts_s.append(s)
+        self.e.submit(torch.cat(parts_w), torch.cat(parts_s))
+        self.tick_no += 1
+
+    def tick(self, copy=True):
+        return self.e.tick(copy=copy)
+
+    def step(self, words: torch.Tensor, copy=True):
+        self.submit(words)
+        return self.tick(copy=copy)
+
+    def collect(self, copy=True):
+        res = self.e.collect(copy=copy)
+        self.router.collected()
+        return res
+
+    def check(self):
+        """Host check of the contract counters (one sync; call outside timed loops)."""
+        ov, bad = int(self.router.overflow.item()), int(self.router.bad_moves.item())
+        if ov > 0:
+            raise RuntimeError(f"halo buffer overflow by {ov} entities (raise halo_cap)")
+        if bad:
+            raise RuntimeError(f"{bad} owned entities moved more than max_step in one tick")

@@ -95,6 +95,9 @@ def lib():
         L.gw_memcpy_h2d.argtypes = [vp, vp, vp, C.c_size_t]
         L.gw_memcpy_d2h.argtypes = [vp, vp, vp, C.c_size_t]
         L.gw_synchronize.argtypes = [vp]
+        L.gw_submit_device_stamped.argtypes = [vp, vp, vp, _u32]
+        L.gw_space_set_ownership.argtypes = [vp, _u32, C.c_float, C.c_float]
+        L.gw_set_stream.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -103,7 +106,8 @@ EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_spa
             "gw_space_destroy", "gw_submit", "gw_submit_device", "gw_set_clients", "gw_tick",
             "gw_sync_collect", "gw_neighbors", "gw_set_profiling", "gw_get_stage_times",
             "gw_total_neighbors", "gw_device_alloc", "gw_device_free", "gw_memcpy_h2d",
-            "gw_memcpy_d2h", "gw_synchronize"]
+            "gw_memcpy_d2h", "gw_synchronize", "gw_submit_device_stamped", "gw_space_set_ownership",
+            "gw_set_stream"]
 
 
 def _p(a: np.ndarray):
@@ -189,6 +193,18 @@ class GpuAOI:
 
     def submit_device(self, dev_ptr: int, n: int):
         self._chk(lib().gw_submit_device(self._h, C.c_void_p(dev_ptr), n))
+
+    def submit_device_stamped(self, dev_ops: int, dev_stamps: int, n: int):
+        """Device ops with explicit global stamps (decomposed world)."""
+        self._chk(lib().gw_submit_device_stamped(self._h, C.c_void_p(dev_ops), C.c_void_p(dev_stamps), n))
+
+    def set_ownership(self, sid: int, x_lo: float, x_hi: float):
+        """Emit events / records only for entities with x in [x_lo, x_hi) (Space strip)."""
+        self._chk(lib().gw_space_set_ownership(self._h, sid, x_lo, x_hi))
+
+    def set_stream(self, hip_stream: int | None):
+        """Run on a caller's stream (e.g. torch.cuda.current_stream().cuda_stream)."""
+        self._chk(lib().gw_set_stream(self._h, hip_stream or None))
 
     def set_clients(self, slots, gates):
         s = np.ascontiguousarray(slots, dtype=np.uint32)

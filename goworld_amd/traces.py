@@ -321,3 +321,134 @@ def enter_ops(slots, x, y, z, yaw, flags: int = SIF_OWN | SIF_NEIGHBOR) -> np.nd
     ops["slot"] = slots
     ops["x"], ops["y"], ops["z"], ops["yaw"] = x, y, z, yaw
     return ops
+
+
+@dataclasses.dataclass
+class StripTrace:
+    """A decomposed world (config #5 shape): global ops per tick, each tagged
+    with the rank that owns it (the strip of the entity's x at the start of
+    the tick, or of the Enter position).  Tick 0 enters the population."""
+    n: int
+    d: float
+    ranks: int
+    strip_w: float
+    max_step: float
+    bounds: tuple
+    gates: np.ndarray
+    ticks: list                # list of (ops OP_DTYPE, owner int64) per tick
+
+    def rank_ops(self, t: int, r: int) -> np.ndarray:
+        ops, own = self.ticks[t]
+        return ops[own == r]
+
+    def global_ops(self, t: int) -> np.ndarray:
+        """The reference call order: rank-major, each rank's ops in order
+        (the order of the global stamps)."""
+        ops, own = self.ticks[t]
+        return ops[np.argsort(own, kind="stable")]
+
+
+def strip_world_trace(seed: int, n: int, ranks: int, strip_w: float, height: float, d: float,
+                      ticks: int, max_step: float, move_frac: float = 0.5,
+                      churn: bool = True, edge_frac: float = 0.2) -> StripTrace:
+    """Random walk across strips (entities migrate between ranks) with churn:
+    Leave, re-Enter anywhere, Leave + re-Enter nearby inside one tick, two
+    moves of one entity in one tick, Sync ops.  Positions are dyadic except
+    an `edge_frac` share placed on strip borders and on the window edge of a
+    border entity (x = border +- d, +-1 ulp)."""
+    W = ranks * strip_w
+    step_q = int(max_step * Q) // 2          # half a step per move, <= 2 moves per tick
+    lo_q, hi_q = 0, int(W * Q)
+    zlo_q, zhi_q = 0, int(height * Q)
+    kx = rand_int(stream_key(seed, 1), n, lo_q, hi_q)
+    kz = rand_int(stream_key(seed, 2), n, zlo_q, zhi_q)
+    x = (kx / Q).astype(np.float32)
+    z = (kz / Q).astype(np.float32)
+    # edge cases: entities on the borders and on window edges across them
+    sel = np.nonzero(rand_unit(stream_key(seed, 3), n) < edge_frac)[0]
+    border = (rand_int(stream_key(seed, 4), len(sel), 1, max(2, ranks)) * strip_w).astype(np.float32)
+    kind = rand_int(stream_key(seed, 5), len(sel), 0, 5)
+    d32 = np.float32(d)
+    for j, i in enumerate(sel):
+        b = border[j]
+        v = [b, np.float32(b + d32), np.float32(b - d32),
+             np.nextafter(np.float32(b + d32), np.float32(np.inf), dtype=np.float32),
+             np.nextafter(b, np.float32(-np.inf), dtype=np.float32)][int(kind[j])]
+        x[i] = np.float32(min(max(v, 0.0), W - 1.0))
+    yaw = np.zeros(n, np.float32)
+    present = np.ones(n, dtype=bool)
+    gates = np.where(np.arange(n) % 5 == 4, 0, 1 + np.arange(n) % 3).astype(np.uint16)
+
+    def owner(xs):
+        return np.clip(np.floor(np.asarray(xs, np.float64) / strip_w).astype(np.int64), 0, ranks - 1)
+
+    def walk(xv, zv, key, cnt):
+        dx = rand_int(stream_key(seed, *key, 0), cnt, -step_q, step_q + 1)
+        dz = rand_int(stream_key(seed, *key, 1), cnt, -step_q, step_q + 1)
+        nx = np.clip(xv.astype(np.float64) + dx / Q, 0.0, W - 1.0).astype(np.float32)
+        nz = np.clip(zv.astype(np.float64) + dz / Q, 0.0, height - 1.0).astype(np.float32)
+        return nx, nz
+
+    tr = StripTrace(n=n, d=float(d), ranks=ranks, strip_w=float(strip_w), max_step=float(max_step),
+                    bounds=(0.0, 0.0, float(W), float(height)), gates=gates, ticks=[])
+    ops = make_ops(n)
+    ops["kind"] = OP_ENTER
+    ops["sync_flags"] = SIF_OWN | SIF_NEIGHBOR
+    ops["slot"] = np.arange(n, dtype=np.uint32)
+    ops["x"], ops["z"], ops["yaw"] = x, z, yaw
+    order = np.argsort(rand_u64(stream_key(seed, 6), n), kind="stable")
+    tr.ticks.append((ops[order], owner(x[order])))
+    for t in range(1, ticks):
+        u = rand_unit(stream_key(seed, 100, t), n)
+        v = rand_unit(stream_key(seed, 101, t), n)
+        own0 = owner(x)
+        rows1, rows2 = [], []                 # first / second op of an entity
+
+        def emit(rows, k, f, ids, xs, zs, ys):
+            o = make_ops(len(ids))
+            o["kind"], o["sync_flags"], o["slot"] = k, f, ids
+            o["x"], o["z"], o["yaw"] = xs, zs, ys
+            rows.append(o)
+        ids = np.arange(n)
+        pres = present.copy()
+        # plain moves (one or two per tick, half a step each)
+        mv = ids[pres & (u < move_frac)]
+        nx, nz = walk(x[mv], z[mv], (102, t), len(mv))
+        x[mv], z[mv] = nx, nz
+        emit(rows1, OP_MOVED, np.where(v[mv] < 0.5, SIF_NEIGHBOR, SIF_NEIGHBOR | SIF_OWN), mv, nx, nz, yaw[mv])
+        two = mv[v[mv] < 0.15]
+        nx, nz = walk(x[two], z[two], (103, t), len(two))
+        x[two], z[two] = nx, nz
+        emit(rows2, OP_MOVED, 0, two, nx, nz, yaw[two])
+        # sync-only ops (SetYaw)
+        sy = ids[pres & (u >= move_frac) & (u < move_frac + 0.1)]
+        yaw[sy] = (v[sy] * 6.25).astype(np.float32)
+        emit(rows1, OP_SYNC, np.where(v[sy] < 0.3, SIF_OWN, SIF_NEIGHBOR | SIF_OWN), sy, x[sy], z[sy], yaw[sy])
+        enter_owner = {}
+        if churn:
+            lv = ids[pres & (u >= 0.97) & (u < 0.985)]            # leave for a while
+            emit(rows1, OP_LEAVE, 0, lv, x[lv], z[lv], yaw[lv])
+            present[lv] = False
+            rl = ids[pres & (u >= 0.985)]                        # leave + re-enter nearby
+            emit(rows1, OP_LEAVE, 0, rl, x[rl], z[rl], yaw[rl])
+            nx, nz = walk(x[rl], z[rl], (104, t), len(rl))
+            x[rl], z[rl] = nx, nz
+            emit(rows2, OP_ENTER, SIF_OWN | SIF_NEIGHBOR, rl, nx, nz, yaw[rl])
+            back = ids[~pres & (u < 0.4)]                         # re-enter anywhere
+            bx = (rand_int(stream_key(seed, 105, t), len(back), lo_q, hi_q) / Q).astype(np.float32)
+            bz = (rand_int(stream_key(seed, 106, t), len(back), zlo_q, zhi_q) / Q).astype(np.float32)
+            x[back], z[back] = bx, bz
+            present[back] = True
+            emit(rows1, OP_ENTER, SIF_OWN | SIF_NEIGHBOR, back, bx, bz, yaw[back])
+            enter_owner = dict(zip(back.tolist(), owner(bx).tolist()))
+        r1 = np.concatenate(rows1)
+        r1 = r1[np.argsort(rand_u64(stream_key(seed, 107, t), len(r1)), kind="stable")]
+        r2 = np.concatenate(rows2)
+        r2 = r2[np.argsort(rand_u64(stream_key(seed, 108, t), len(r2)), kind="stable")]
+        allops = np.concatenate([r1, r2])
+        own = own0[allops["slot"]].copy()
+        for k, i in enumerate(allops["slot"].tolist()):
+            if i in enter_owner:
+                own[k] = enter_owner[i]
+        tr.ticks.append((allops, own))
+    return tr

@@ -62,6 +62,7 @@ extern "C" {
 #define GW_ERANGE     -5   /* slot or space id out of range                    */
 
 /* ---- ops ---------------------------------------------------------------- */
+#define GW_OP_NOP     0    /* ignored (padding of fixed-size device buffers)   */
 #define GW_OP_ENTER   1    /* aoiMgr.Enter(&e.aoi, x, z)      (Space.go:202)   */
 #define GW_OP_MOVED   2    /* aoiMgr.Moved(&e.aoi, x, z)      (Space.go:250)   */
 #define GW_OP_LEAVE   3    /* aoiMgr.Leave(&e.aoi)            (Space.go:234)   */
@@ -158,6 +159,21 @@ int  gw_submit(gw_ctx* ctx, const gw_op* ops, uint32_t n);
  * guarantees a valid sequence).  The pointer must stay valid until gw_tick. */
 int  gw_submit_device(gw_ctx* ctx, const gw_op* dev_ops, uint32_t n);
 
+/* Ops already in device memory with explicit global stamps (one u64 per op,
+ * also in device memory): the stamp replaces the op's position in the tick's
+ * stream when go-aoi's "which member moved last" is decided.
+ * Stamps must grow with the reference call order and exceed every stamp used
+ * before; a decomposed world (one space split over processes) uses them so
+ * that every process orders the ops of all processes the same way. */
+int  gw_submit_device_stamped(gw_ctx* ctx, const gw_op* dev_ops, const uint64_t* dev_stamps, uint32_t n);
+
+/* Ownership x-range of a space in a decomposed world: events are emitted only
+ * for watchers, and sync records only for entities, whose x (the position
+ * after the tick; before it for an entity that left) lies in [x_lo, x_hi).
+ * Entities outside it are ghosts mirrored from the neighbouring processes.
+ * Default: the whole line. */
+int  gw_space_set_ownership(gw_ctx* ctx, uint32_t space_id, float x_lo, float x_hi);
+
 /* Attach / detach clients: gate 0 = no client (GameClient nil). */
 int  gw_set_clients(gw_ctx* ctx, const uint32_t* slots, const uint16_t* gates, uint32_t n);
 
@@ -196,8 +212,14 @@ int  gw_memcpy_h2d(gw_ctx* ctx, void* dst_dev, const void* src_host, size_t byte
 int  gw_memcpy_d2h(gw_ctx* ctx, void* dst_host, const void* src_dev, size_t bytes);
 int  gw_synchronize(gw_ctx* ctx);
 
+/* Run the context's work on a caller's stream (a hipStream_t of the same
+ * device, e.g. torch's current stream, so that device-resident ops produced
+ * there and results consumed there need no host synchronisation); NULL
+ * restores the context's own stream.  Drains the previous stream first. */
+int  gw_set_stream(gw_ctx* ctx, void* hip_stream);
+
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 1
+#define GW_ABI_VERSION 2
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

@@ -1,0 +1,131 @@
+"""One rank of a decomposed-world parity run (launched by tests/test_dworld.py
+as a subprocess; gloo over 127.0.0.1).
+
+--engine oracle : the rank's local space is a CPU oracle space (test
+                  infrastructure: checks the routing / halo protocol alone);
+--engine hip    : the rank's local space is the HIP engine on cuda:0 (the
+                  product path; several ranks share the one GPU).
+
+Writes the rank's owned events per tick and records per collect to --out.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from goworld_amd import dworld, traces as T  # noqa: E402
+
+
+class OracleStrip:
+    """Mock engine (test only): an oracle space fed the rank's local op rows
+    in global-stamp order, with the engine's ownership filters."""
+
+    def __init__(self):
+        from oracle import pyorc
+        self.pyorc = pyorc
+        self.words, self.stamps = [], []
+
+    def create_space(self, d, cap, bounds):
+        self.o = self.pyorc.OracleSpace(cap, d, self.pyorc.SEQRULE)
+        self.x = np.zeros(cap, np.float32)
+        self.present = np.zeros(cap, bool)
+        return 0, 0
+
+    def set_ownership(self, sid, lo, hi):
+        self.lo, self.hi = np.float32(lo), np.float32(hi)
+
+    def set_clients(self, slots, gates):
+        for s, g in zip(np.asarray(slots).tolist(), np.asarray(gates).tolist()):
+            if g:
+                self.o.set_client(int(s), int(g))
+
+    def submit(self, words, stamps):
+        self.words.append(words.cpu().numpy())
+        self.stamps.append(stamps.cpu().numpy())
+
+    def _owned(self, xs):
+        return (xs >= self.lo) & (xs < self.hi)
+
+    def tick(self, copy=True):
+        w = np.concatenate(self.words)
+        s = np.concatenate(self.stamps)
+        self.words, self.stamps = [], []
+        keep = (w[:, 0] & 0xFF) != 0
+        w, s = w[keep], s[keep]
+        ops = dworld.words_to_ops(w[np.argsort(s, kind="stable")])
+        x0, p0 = self.x.copy(), self.present.copy()
+        for op in ops:
+            k, sl = int(op["kind"]), int(op["slot"])
+            if k in (T.OP_ENTER, T.OP_MOVED):
+                self.x[sl], self.present[sl] = op["x"], True
+            elif k == T.OP_LEAVE:
+                self.present[sl] = False
+        assert self.o.tick(ops) == 0
+        e, l = self.o.events()
+        xr = np.where(self.present, self.x, x0)
+        own = self._owned(xr)
+        return _Res(enter=e[own[e["watcher"]]].copy(), leave=l[own[l["watcher"]]].copy())
+
+    def collect(self, copy=True):
+        r = self.o.collect()
+        ent = r["entity"]
+        keep = self.present[ent] & self._owned(self.x[ent])
+        return _Res(records=r[keep].copy())
+
+
+class _Res:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rank", type=int, required=True)
+    ap.add_argument("--world", type=int, required=True)
+    ap.add_argument("--port", type=int, required=True)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--engine", choices=["oracle", "hip"], default="oracle")
+    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--n", type=int, default=800)
+    ap.add_argument("--strip-w", type=float, default=300.0)
+    ap.add_argument("--height", type=float, default=600.0)
+    ap.add_argument("--d", type=float, default=50.0)
+    ap.add_argument("--max-step", type=float, default=8.0)
+    ap.add_argument("--ticks", type=int, default=12)
+    ap.add_argument("--collect-every", type=int, default=3)
+    ap.add_argument("--halo-cap", type=int, default=512)
+    a = ap.parse_args()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{a.port}", rank=a.rank,
+                            world_size=a.world)
+    tr = T.strip_world_trace(a.seed, a.n, a.world, a.strip_w, a.height, a.d, a.ticks, a.max_step)
+    geom = dworld.Strips(0.0, tr.strip_w, a.world, tr.d, tr.max_step)
+    if a.engine == "oracle":
+        eng, dev = OracleStrip(), torch.device("cpu")
+    else:
+        from goworld_amd import gpuaoi
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        eng = dworld.HipStrip(gpuaoi.GpuAOI(0))
+    sr = dworld.StripRank(eng, geom, a.rank, a.n, tr.bounds, dev, comm_device=torch.device("cpu"),
+                          halo_cap=a.halo_cap)
+    eng.set_clients(np.arange(a.n, dtype=np.uint32), tr.gates)
+    out = {}
+    for t in range(len(tr.ticks)):
+        w = torch.from_numpy(dworld.ops_to_words(tr.rank_ops(t, a.rank)).copy()).to(dev)
+        res = sr.step(w)
+        out[f"enter_{t}"], out[f"leave_{t}"] = res.enter, res.leave
+        if (t + 1) % a.collect_every == 0 or t == len(tr.ticks) - 1:
+            out[f"rec_{t}"] = sr.collect().records
+    sr.check()
+    np.savez(a.out, **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,126 @@
+"""Decomposed world (SURVEY.md 8(e) regime 2): the union of what the strip
+ranks emit for the entities they own equals, tick by tick, what one global
+oracle space emits for the whole world — events and sync records — on a
+strip trace with migration across borders, churn, Leave + re-Enter inside a
+tick, repeated moves and Sync ops.
+
+CPU tests run the halo protocol over gloo with world_size 2 and 3 and an
+oracle space per rank; the GPU test runs the same ranks on the HIP engine
+(two processes on the one GPU, gloo between them)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from goworld_amd import dworld, traces as T
+from oracle import pyorc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+TRACE = dict(seed=7, n=800, strip_w=300.0, height=600.0, d=50.0, max_step=8.0, ticks=12)
+COLLECT_EVERY = 3
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_ranks(world, engine, tmp_path, timeout=240):
+    port = _free_port()
+    procs, outs = [], []
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for r in range(world):
+        out = str(tmp_path / f"rank{r}.npz")
+        outs.append(out)
+        cmd = [sys.executable, os.path.join(HERE, "dworld_worker.py"), "--rank", str(r), "--world", str(world),
+               "--port", str(port), "--out", out, "--engine", engine,
+               "--collect-every", str(COLLECT_EVERY)]
+        for k, v in TRACE.items():
+            cmd += [f"--{k.replace('_', '-')}", str(v)]
+        procs.append(subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    logs = []
+    try:
+        for p in procs:
+            o, _ = p.communicate(timeout=timeout)
+            logs.append(o.decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed:\n{logs[r][-3000:]}"
+    return [np.load(o) for o in outs]
+
+
+def _sort_ev(e):
+    return e[np.lexsort((e["target"], e["watcher"]))]
+
+
+def _sort_rec(r):
+    return r[np.lexsort((r["watcher"], r["entity"]))]
+
+
+def _check(world, results):
+    tr = T.strip_world_trace(TRACE["seed"], TRACE["n"], world, TRACE["strip_w"], TRACE["height"],
+                             TRACE["d"], TRACE["ticks"], TRACE["max_step"])
+    o = pyorc.OracleSpace(tr.n, tr.d, pyorc.SEQRULE)
+    o.set_clients(tr.gates)
+    n_ev = n_rec = 0
+    for t in range(len(tr.ticks)):
+        assert o.tick(tr.global_ops(t)) == 0
+        e, l = o.events()
+        for name, exp in (("enter", e), ("leave", l)):
+            got = np.concatenate([res[f"{name}_{t}"] for res in results])
+            assert len(got) == len(exp), (t, name, len(got), len(exp))
+            assert _sort_ev(got).tobytes() == _sort_ev(exp).tobytes(), f"tick {t}: {name} events differ"
+            n_ev += len(exp)
+        if f"rec_{t}" in results[0]:
+            exp = o.collect()
+            got = np.concatenate([res[f"rec_{t}"] for res in results])
+            assert len(got) == len(exp), (t, len(got), len(exp))
+            assert _sort_rec(got).tobytes() == _sort_rec(exp).tobytes(), f"tick {t}: records differ"
+            n_rec += len(exp)
+    assert n_ev > 1000 and n_rec > 1000       # the trace exercises the protocol
+
+
+def test_strip_geometry():
+    g = dworld.Strips(0.0, 300.0, 3, 50.0, 8.0)
+    assert g.h > g.d + 2 * g.max_step
+    assert g.ext(1) == (300.0 - g.h, 600.0 + g.h)
+    assert list(g.owner([-5.0, 0.0, 299.99, 300.0, 900.0])) == [0, 0, 0, 1, 2]
+    lo, hi = g.own_range_f32(1)
+    assert (lo, hi) == (300.0, 600.0)
+    assert g.own_range_f32(0)[0] < -1e38 and g.own_range_f32(2)[1] > 1e38
+    with pytest.raises(ValueError):
+        dworld.Strips(0.0, 60.0, 3, 50.0, 8.0)      # strips narrower than the halo
+
+
+def test_strip_trace_migrates():
+    tr = T.strip_world_trace(TRACE["seed"], TRACE["n"], 2, TRACE["strip_w"], TRACE["height"],
+                             TRACE["d"], TRACE["ticks"], TRACE["max_step"])
+    # owners are strips of the start-of-tick positions; entities cross borders
+    x = np.zeros(tr.n, np.float32)
+    crossings = 0
+    for t, (ops, own) in enumerate(tr.ticks):
+        for op, r in zip(ops, own):
+            if op["kind"] in (T.OP_ENTER, T.OP_MOVED):
+                if t and op["kind"] == T.OP_MOVED:
+                    crossings += int((x[op["slot"]] >= 300.0) != (op["x"] >= 300.0))
+                x[op["slot"]] = op["x"]
+    assert crossings > 5
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dworld_gloo_oracle_ranks(world, tmp_path):
+    _check(world, _run_ranks(world, "oracle", tmp_path))
+
+
+@pytest.mark.gpu
+def test_dworld_gpu_two_ranks(tmp_path):
+    _check(2, _run_ranks(2, "hip", tmp_path, timeout=100))

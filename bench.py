@@ -5,11 +5,21 @@ A step = one game tick of the hot path over one batch of synthetic input:
 gw_tick (apply the tick's 100k Moved ops, update every neighbour list, emit the
 canonical enter/leave streams) + gw_sync_collect (CollectEntitySyncInfos:
 per-watcher position/yaw records).  Workload at N=1 is BASELINE config #3,
-the 1M-entity clustered-hotspot single space the metric is quoted on.  With
---gpus N each rank owns an independent 1M-entity space on its own GPU (spaces
-never span processes in the reference, SpaceManager.go:11-31): weak scaling,
-no data-path collective.  Inputs (ops of every tick) are resident in HBM
-before the timed region; outputs stay in HBM (device-resident boundary).
+the 1M-entity clustered-hotspot single space the metric is quoted on.
+
+N>1, --mode world (default): one world space decomposed into N X-strips, one
+per GPU (BASELINE config #5, goworld_amd/dworld.py): each strip has config
+#3's statistics (1M entities per strip by default, --entities 2000000 gives
+config #5's 16M at N=8), and each tick every rank routes its ops, exchanges
+its halo rows with both neighbours over RCCL (xGMI) and ticks its strip.
+Weak scaling.  Bench strips reflect their walkers at the strip borders
+(migration is covered by the parity tests, tests/test_dworld.py); the halo
+traffic of the border bands is real.
+N>1, --mode spaces: an independent 1M-entity space per GPU (spaces never span
+processes in the reference, SpaceManager.go:11-31): no data-path collective.
+
+Inputs (ops of every tick) are resident in HBM before the timed region;
+outputs stay in HBM (device-resident boundary).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
 N>1:  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -43,34 +53,51 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--profile-stages", type=int, default=1, help="HIP-event stage timing in the timed region")
+    ap.add_argument("--mode", choices=["world", "spaces"], default="world", help="N>1 regime")
+    ap.add_argument("--comm", choices=["nccl", "gloo"], default="nccl",
+                    help="halo exchange backend (gloo: rehearsal of several ranks on one GPU)")
+    ap.add_argument("--halo-cap", type=int, default=16384, help="halo entities per neighbour per tick")
+    ap.add_argument("--device", type=int, default=None, help="force a device (rehearsals on one GPU)")
     return ap.parse_args()
 
 
-def dist_setup(n_gpus):
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    pg = None
-    if ws > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=ws)   # control plane only (barrier, max)
-        pg = dist
-    return rank, local, ws, pg
+class Ctl:
+    """Control plane (barrier, max/sum of scalars) on a gloo group; the data
+    path (halo rows) uses the default group (RCCL) in world mode."""
 
+    def __init__(self, a):
+        self.ws = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0")) if a.device is None else a.device
+        self.group = None
+        if self.ws > 1:
+            import torch
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if a.mode == "world" and a.comm == "nccl":
+                torch.cuda.set_device(self.local)
+                dist.init_process_group("nccl", rank=self.rank, world_size=self.ws,
+                                        device_id=torch.device("cuda", self.local))
+                self.group = dist.new_group(backend="gloo")
+                t = torch.ones(1, device=torch.device("cuda", self.local))
+                dist.all_reduce(t)            # bring up the RCCL communicator on all ranks
+                torch.cuda.synchronize()
+            else:
+                dist.init_process_group("gloo", rank=self.rank, world_size=self.ws)
+                self.group = dist.group.WORLD
+            self.dist = dist
 
-def barrier(pg):
-    if pg is not None:
-        pg.barrier()
+    def barrier(self):
+        if self.group is not None:
+            self.dist.barrier(group=self.group)
 
-
-def allreduce(pg, vals, op):
-    if pg is None:
-        return vals
-    import torch
-    t = torch.tensor(vals, dtype=torch.float64)
-    pg.all_reduce(t, op=op)
-    return t.tolist()
+    def reduce(self, vals, op):
+        if self.group is None:
+            return vals
+        import torch
+        t = torch.tensor(vals, dtype=torch.float64)
+        self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op), group=self.group)
+        return t.tolist()
 
 
 STAGE_KERNEL = {"diff": "k_mover<2, 1>"}
@@ -114,22 +141,93 @@ def cpu_baseline(tr, seconds):
             "per_op_us": spent / done * 1e6}
 
 
+class SpaceRun:
+    """N=1 (config #3) and --mode spaces: one independent space per GPU."""
+
+    def __init__(self, a, ctl, ticks):
+        self.tr = traces.config3(ticks=ticks, seed=3 + ctl.rank, n=a.entities, side=a.side)
+        self.g = g = gpuaoi.GpuAOI(ctl.local)
+        gpuaoi.load_space(g, self.tr, chunk=1 << 18)
+        g.sync_collect(copy=False)                      # clear the Enter flags (untimed)
+        # all ticks' ops resident in HBM before timing
+        self.m = len(self.tr.ticks[0])
+        ops_all = np.concatenate(self.tr.ticks)
+        self.dev_ops = g.dev_alloc(ops_all.nbytes)
+        g.h2d(self.dev_ops, ops_all)
+        self.nbytes_tick = self.m * traces.OP_DTYPE.itemsize
+        self.parallelism = f"independent spaces x{ctl.ws} (no comm)" if ctl.ws > 1 else "single GPU"
+
+    def step(self, t):
+        g = self.g
+        g.submit_device(self.dev_ops + t * self.nbytes_tick, self.m)
+        r = g.tick(copy=False)
+        s = g.sync_collect(copy=False)
+        return r.movers, r, s
+
+    def close(self):
+        self.g.dev_free(self.dev_ops)
+        self.g.close()
+
+
+class WorldRun:
+    """--mode world, N>1: one world of N strips (dworld.StripRank per rank)."""
+
+    def __init__(self, a, ctl, ticks):
+        import torch
+        from goworld_amd import dworld
+        self.torch = torch
+        dev = torch.device("cuda", ctl.local)
+        torch.cuda.set_device(dev)
+        ws, r, n, side = ctl.ws, ctl.rank, a.entities, a.side
+        x0 = -ws * side / 2
+        tr = traces.config3(ticks=ticks, seed=3 + r, n=n, side=side)
+        geom = dworld.Strips(x0, side, ws, tr.d, 16.0)          # config #3 steps: +-4, hotspots +-16
+        off = np.float32(x0 + (r + 0.5) * side)                 # strip r's centre (exact in f32)
+        lo, hi = geom.ext(r)
+        bounds = (max(lo, x0), -side / 2, min(hi, x0 + ws * side), side / 2)
+        self.g = gpuaoi.GpuAOI(ctl.local)
+        eng = dworld.HipStrip(self.g)
+        pg = None if a.comm == "nccl" else ctl.group
+        cdev = dev if a.comm == "nccl" else torch.device("cpu")
+        self.sr = sr = dworld.StripRank(eng, geom, r, n * ws, bounds, dev, pg=pg, comm_device=cdev,
+                                        halo_cap=a.halo_cap)
+        eng.set_clients(np.arange(n * ws, dtype=np.uint32), np.ones(n * ws, np.uint16))  # config #3: 1 gate, all clients
+
+        def words(ops):
+            o = ops.copy()
+            o["slot"] += np.uint32(r * n)
+            o["x"] += off
+            return torch.from_numpy(dworld.ops_to_words(o).copy()).to(dev)
+        enter = traces.enter_ops(tr.init_slots, tr.init_x, tr.init_y, tr.init_z, tr.init_yaw)
+        for i in range(0, n, 1 << 18):
+            sr.step(words(enter[i:i + (1 << 18)]), copy=False, no_events=True)
+        sr.collect(copy=False)
+        self.m = len(tr.ticks[0])
+        self.words = [words(t) for t in tr.ticks]              # resident in HBM
+        torch.cuda.synchronize()
+        self.parallelism = f"decomposed world, {ws} X-strips, halo rows over {a.comm.upper()}"
+        self.tr = tr
+
+    def step(self, t):
+        r = self.sr.step(self.words[t], copy=False)
+        s = self.sr.collect(copy=False)
+        return self.m, r, s
+
+    def close(self):
+        self.sr.check()
+        self.g.close()
+
+
 def main():
     a = parse()
-    rank, local, ws, pg = dist_setup(a.gpus)
+    ctl = Ctl(a)
+    ws, rank = ctl.ws, ctl.rank
     ticks = a.warmup + a.steps
-    tr = traces.config3(ticks=ticks, seed=3 + rank, n=a.entities, side=a.side)
-    g = gpuaoi.GpuAOI(local)
     t_load = time.perf_counter()
-    sid, base = gpuaoi.load_space(g, tr, chunk=1 << 18)
-    g.sync_collect(copy=False)                      # clear the Enter flags (untimed)
+    world = ws > 1 and a.mode == "world"
+    run = WorldRun(a, ctl, ticks) if world else SpaceRun(a, ctl, ticks)
     t_load = time.perf_counter() - t_load
-    # all ticks' ops resident in HBM before timing
-    m = len(tr.ticks[0])
-    ops_all = np.concatenate(tr.ticks)
-    dev_ops = g.dev_alloc(ops_all.nbytes)
-    g.h2d(dev_ops, ops_all)
-    nbytes_tick = m * traces.OP_DTYPE.itemsize
+    g = run.g
 
     stage_us, stage_bytes, stage_n = {}, {}, {}
 
@@ -139,43 +237,40 @@ def main():
             stage_bytes[name] = stage_bytes.get(name, 0) + b
             stage_n[name] = stage_n.get(name, 0) + 1
 
-    def step(t, prof):
-        g.submit_device(dev_ops + t * nbytes_tick, m)
-        r = g.tick(copy=False)
-        s = g.sync_collect(copy=False)
-        if prof:
-            acc_stages()          # tick + collect stages; the collect already synced the stream
-        return r, s
-
     for t in range(a.warmup):
-        step(t, False)
+        run.step(t)
     g.set_profiling(bool(a.profile_stages))
-    tot = dict(ops=0, events=0, records=0, bytes_alg=0, pairs=0, a_old=0, a_new=0)
-    barrier(pg)
+    tot = dict(ops=0, events=0, records=0, bytes_alg=0)
+    ctl.barrier()
     g.synchronize()
     t0 = time.perf_counter()
     for t in range(a.warmup, ticks):
-        r, s = step(t, bool(a.profile_stages))
-        tot["ops"] += r.movers
+        upd, r, s = run.step(t)
+        if a.profile_stages:
+            acc_stages()          # tick + collect stages; the collect already synced the stream
+        tot["ops"] += upd
         tot["events"] += r.n_enter + r.n_leave
         tot["records"] += s.n_rec
         tot["bytes_alg"] += r.bytes_alg + s.bytes_alg
-        tot["pairs"] += r.pairs_tested
-        tot["a_old"] += r.nbr_old
-        tot["a_new"] += r.nbr_new
     g.synchronize()
     t1 = time.perf_counter()
-    barrier(pg)
+    ctl.barrier()
     elapsed = t1 - t0
-    if pg is not None:
-        mx = allreduce(pg, [elapsed], pg.ReduceOp.MAX)[0]
-        sums = allreduce(pg, [tot["ops"], tot["events"], tot["records"]], pg.ReduceOp.SUM)
-    else:
-        mx = elapsed
-        sums = [tot["ops"], tot["events"], tot["records"]]
+    mx = ctl.reduce([elapsed], "MAX")[0]
+    sums = ctl.reduce([tot["ops"], tot["events"], tot["records"]], "SUM")
     if rank != 0:
+        run.close()
         return
     K = a.steps
+    if world:
+        workload = (f"config #5 shape: one world space of {ws} x {a.entities} entities decomposed into {ws} "
+                    f"X-strips of {a.side:g} x {a.side:g}, each with config #3 statistics (70% uniform + 30% in "
+                    f"64 Gaussian hotspots, 10% movers per tick), AOI distance 100; step = route + halo "
+                    f"exchange + gw_tick + gw_sync_collect on every rank")
+    else:
+        workload = ("config #3: single AOI space per GPU, 1M entities, 70% uniform + 30% in 64 "
+                    "Gaussian hotspots (sigma 200), 10% movers per tick (+-4 / hotspot +-16), "
+                    "AOI distance 100, world 32768^2; step = gw_tick + gw_sync_collect")
     line = {
         "metric": "entity AOI updates/sec + enter/leave events/sec, 1M-entity space, 1/2/4/8 GPU",
         "value": sums[0] / mx,
@@ -188,12 +283,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #3)",
-        "config": {"workload": "config #3: single AOI space per GPU, 1M entities, 70% uniform + 30% in 64 "
-                               "Gaussian hotspots (sigma 200), 10% movers per tick (+-4 / hotspot +-16), "
-                               "AOI distance 100, world 32768^2; step = gw_tick + gw_sync_collect",
-                   "entities_per_gpu": a.entities, "movers_per_tick": m, "aoi_dist": 100.0,
-                   "world_side": a.side, "gates": 1, "parallelism": f"independent spaces x{ws} (no comm)"},
+        "data": "synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #3" + (" per strip)" if world else ")"),
+        "config": {"workload": workload,
+                   "entities_per_gpu": a.entities, "world_entities": a.entities * (ws if world else 1),
+                   "movers_per_tick_per_gpu": run.m, "aoi_dist": 100.0,
+                   "world_side": a.side, "gates": 1, "parallelism": run.parallelism},
         "events_per_sec": sums[1] / mx,
         "records_per_sec": sums[2] / mx,
         "device_us_per_step": (sum(stage_us.values()) / K) if stage_us else None,
@@ -221,8 +315,7 @@ def main():
         cb = cpu_baseline(traces.config3(ticks=1, seed=3, n=a.entities, side=a.side), a.cpu_seconds)
         line["cpu_baseline"] = cb
     print(json.dumps(line), flush=True)
-    g.dev_free(dev_ops)
-    g.close()
+    run.close()
 
 
 if __name__ == "__main__":

@@ -45,6 +45,7 @@ struct OpSeg {            // submission order of a tick: host or device segment
     const uint64_t* stamps;   // explicit global stamps (device) or nullptr
     uint32_t n;
     size_t host_off;
+    const gw_halo_row* rows;  // halo rows (device): ops with inline stamps
 };
 
 struct Stage {
@@ -84,6 +85,8 @@ struct gw_ctx {
     unsigned long long* nbc = nullptr;       // [slot_cap] epoch<<32 | neighbours with a client
     uint32_t* ownbits = nullptr;             // [slot_cap/32 + 1] zero between ticks
     int32_t *last_pos = nullptr, *last_aoi = nullptr, *last_leave = nullptr;
+    uint32_t* rflag = nullptr;                // [slot_cap] halo routing scratch, zero between calls
+    HaloStats* halo = nullptr;                // halo routing counters (device)
     GEnt* gnb[2] = {nullptr, nullptr};   // grid ping-pong (gnb[gcur] is current)
     uint32_t* gsb[2] = {nullptr, nullptr};  // cell starts ping-pong
     int gcur = 0;
@@ -296,6 +299,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->last_pos, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_aoi, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_leave, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->rflag, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->gnb[0], 0, nc))) return rc;    // rebuilt (grid_dirty)
     if ((rc = grow_preserve(c, c->gnb[1], 0, nc))) return rc;
     if ((rc = grow_preserve(c, c->gidx, 0, nc))) return rc;
@@ -305,6 +309,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     HIPCHK(hipMemsetAsync(c->stamp + oc, 0, n * 8, c->st));
     HIPCHK(hipMemsetAsync(c->pos + oc, 0, n * sizeof(float4), c->st));
     HIPCHK(hipMemsetAsync(c->flags + oc, 0, n * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->rflag + oc, 0, n * 4, c->st));
     HIPCHK(hipMemsetAsync(c->gate + oc, 0, n * 2, c->st));
     HIPCHK(hipMemsetAsync(c->cnt64 + oc, 0, (n + 1) * 8, c->st));
     HIPCHK(hipMemsetAsync(c->nbc + oc, 0, n * 8, c->st));
@@ -490,6 +495,8 @@ int gw_init(int device_id, gw_ctx** out) {
         if (hipMalloc(&c->stats, sizeof(DevStats)) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "stats"); break; }
         if (hipHostMalloc((void**)&c->hstats, sizeof(DevStats), hipHostMallocDefault) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "hstats"); break; }
         if (hipMalloc(&c->scal32, 64) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "scal"); break; }
+        if (hipMalloc(&c->halo, sizeof(HaloStats)) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "halo"); break; }
+        (void)hipMemset(c->halo, 0, sizeof(HaloStats));
         if (hipMalloc(&c->sc.ticket, 8) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "ticket"); break; }
         (void)hipMemset(c->sc.ticket, 0, 8);
         memset(c->hstats, 0, sizeof(DevStats));
@@ -522,7 +529,7 @@ void gw_shutdown(gw_ctx* c) {
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
-    void* ps[] = {c->sc.ticket, c->ownbits, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->nbc, c->last_pos, c->last_aoi,
+    void* ps[] = {c->halo, c->rflag, c->sc.ticket, c->ownbits, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->nbc, c->last_pos, c->last_aoi,
                   c->last_leave, c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->scal32, c->gsb[0],
                   c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->bigcell, c->gm_start};
     for (void* p : ps) if (p) (void)hipFree(p);
@@ -609,7 +616,7 @@ int gw_submit(gw_ctx* c, const gw_op* ops, uint32_t n) {
         int rc = validate_ops(c, ops, n);
         if (rc) return rc;
     }
-    OpSeg sg{true, nullptr, nullptr, n, c->pend_host.size()};
+    OpSeg sg{true, nullptr, nullptr, n, c->pend_host.size(), nullptr};
     c->pend_host.insert(c->pend_host.end(), ops, ops + n);
     c->segs.push_back(sg);
     return 0;
@@ -619,7 +626,7 @@ int gw_submit_device(gw_ctx* c, const gw_op* dev_ops, uint32_t n) {
     if (!c || (!dev_ops && n)) return GW_EINVAL;
     if (!n) return 0;
     c->validate = false;   // device-resident ops are trusted; the host mirror is no longer exact
-    c->segs.push_back(OpSeg{false, dev_ops, nullptr, n, 0});
+    c->segs.push_back(OpSeg{false, dev_ops, nullptr, n, 0, nullptr});
     return 0;
 }
 
@@ -627,7 +634,50 @@ int gw_submit_device_stamped(gw_ctx* c, const gw_op* dev_ops, const uint64_t* de
     if (!c || ((!dev_ops || !dev_stamps) && n)) return GW_EINVAL;
     if (!n) return 0;
     c->validate = false;
-    c->segs.push_back(OpSeg{false, dev_ops, dev_stamps, n, 0});
+    c->segs.push_back(OpSeg{false, dev_ops, dev_stamps, n, 0, nullptr});
+    return 0;
+}
+
+int gw_submit_device_rows(gw_ctx* c, const gw_halo_row* dev_rows, uint32_t n) {
+    if (!c || (!dev_rows && n)) return GW_EINVAL;
+    if (!n) return 0;
+    c->validate = false;
+    c->segs.push_back(OpSeg{false, nullptr, nullptr, n, 0, dev_rows});
+    return 0;
+}
+
+int gw_route_halo(gw_ctx* c, const gw_op* dev_ops, const uint64_t* dev_stamps, uint32_t n, float max_step,
+                  const gw_halo_dst* dsts, uint32_t n_dst) {
+    if (!c || (n && (!dev_ops || !dev_stamps)) || (n_dst && !dsts)) return GW_EINVAL;
+    if (n_dst > 2) return set_err(c, GW_EINVAL, "at most 2 halo destinations");
+    if (!(max_step >= 0)) return set_err(c, GW_EINVAL, "max_step must be >= 0");
+    (void)hipSetDevice(c->dev);
+    HaloDsts D{};
+    D.n = n_dst;
+    for (uint32_t d = 0; d < n_dst; ++d) {
+        if (!dsts[d].rows && dsts[d].cap_entities) return GW_EINVAL;
+        D.d[d] = HaloDst{dsts[d].x_lo, dsts[d].x_hi, dsts[d].rows, dsts[d].cap_entities};
+        if (dsts[d].cap_entities)
+            HIPCHK(hipMemsetAsync(dsts[d].rows, 0, (size_t)dsts[d].cap_entities * 3 * sizeof(gw_halo_row), c->st));
+    }
+    HIPCHK(hipMemsetAsync(c->halo->cnt, 0, sizeof c->halo->cnt, c->st));
+    if (!n || !c->total_slots) return 0;
+    launch_route_halo(world(c), dev_ops, (const unsigned long long*)dev_stamps, n, max_step, D, c->last_pos,
+                      c->last_aoi, c->last_leave, c->rflag, c->halo, c->st);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int gw_halo_status(gw_ctx* c, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops) {
+    if (!c) return GW_EINVAL;
+    (void)hipSetDevice(c->dev);
+    HaloStats h{};
+    HIPCHK(hipMemcpyAsync(&h, c->halo, sizeof h, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemsetAsync(c->halo, 0, sizeof h, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (overflow) *overflow = h.overflow;
+    if (bad_moves) *bad_moves = h.bad_moves;
+    if (bad_ops) *bad_ops = h.bad_ops;
     return 0;
 }
 
@@ -683,15 +733,15 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     const unsigned long long* stamps = nullptr;
     bool any_stamped = false, all_stamped = true;
     for (auto& s : c->segs) {
-        any_stamped |= s.stamps != nullptr;
-        all_stamped &= s.stamps != nullptr;
+        any_stamped |= s.stamps != nullptr || s.rows != nullptr;
+        all_stamped &= s.stamps != nullptr || s.rows != nullptr;
     }
     if (any_stamped && !all_stamped) {
         c->segs.clear();
         c->pend_host.clear();
         return set_err(c, GW_EINVAL, "a tick mixes stamped and unstamped ops");
     }
-    if (c->segs.size() == 1 && !c->segs[0].host) {
+    if (c->segs.size() == 1 && !c->segs[0].host && !c->segs[0].rows) {
         ops = c->segs[0].dev;
         stamps = (const unsigned long long*)c->segs[0].stamps;
     } else {
@@ -699,7 +749,10 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         if (any_stamped && (rc = ensure(c, c->stamp_buf, (size_t)M * 8))) return rc;
         size_t off = 0;
         for (auto& s : c->segs) {
-            if (s.host)
+            if (s.rows)
+                launch_split_rows(s.rows, s.n, P<gw_op>(c->ops_buf) + off, P<unsigned long long>(c->stamp_buf) + off,
+                                  c->st);
+            else if (s.host)
                 HIPCHK(hipMemcpyAsync(P<gw_op>(c->ops_buf) + off, c->pend_host.data() + s.host_off,
                                       (size_t)s.n * sizeof(gw_op), hipMemcpyHostToDevice, c->st));
             else

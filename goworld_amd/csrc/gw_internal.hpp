@@ -214,6 +214,26 @@ void launch_gather_records(const gw_sync_record* in, const uint32_t* idx, const 
 // queries
 void launch_neighbors(const World& w, uint32_t slot, uint32_t* out, uint32_t* n_out, uint32_t cap, hipStream_t s);
 void launch_count_all(const World& w, uint64_t n_present, unsigned long long* total, hipStream_t s);
+// ---- decomposed world: owner-side halo routing (halo.hip) -----------------
+constexpr uint8_t SIF_ROUTED = GW_SIF_OWN_CLIENT | GW_SIF_NEIGHBOR_CLIENTS;   // flag bits rows carry
+struct HaloStats {
+    unsigned long long overflow, bad_moves, bad_ops;
+    uint32_t cnt[2];           // entities placed per destination (this call)
+};
+struct HaloDst {
+    float x_lo, x_hi;
+    gw_halo_row* rows;
+    uint32_t cap;
+};
+struct HaloDsts {
+    HaloDst d[2];
+    uint32_t n;
+};
+void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
+                       float max_step, const HaloDsts& D, int32_t* last_pos, int32_t* last_aoi,
+                       int32_t* last_leave, uint32_t* rflag, HaloStats* hs, hipStream_t s);
+void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,
+                       hipStream_t s);
 void launch_fill_u32(uint32_t* p, uint32_t v, uint64_t n, hipStream_t s);
 void launch_fill_i32(int32_t* p, int32_t v, uint64_t n, hipStream_t s);
 

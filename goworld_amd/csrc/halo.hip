@@ -1,0 +1,184 @@
+// halo.hip — owner-side routing of a decomposed world (gw_route_halo).
+//
+// A strip process forwards, for each entity its ops touched this tick, the
+// net effect those ops have on a neighbour's copy (goworld_amd/dworld.py
+// module doc).  The entity state before the tick IS the
+// routing state: AoiEnt (x, present), flags (sync flags pending since the
+// last collect).  Four light passes over the owned ops, O(ops), no host sync:
+//   r1  last AOI op / last payload op / last Leave per slot (atomicMax, as
+//       k_ops1 of the tick; the same per-slot arrays, left at -1 after r4)
+//   r2  OR of the sync flags of the ops after the last Leave (atomicOr)
+//   r3  the entity's last op writes up to 3 rows per destination, entities
+//       placed by one wave-aggregated atomic per wave and destination
+//   r4  reset of the per-slot scratch
+// Integer/byte work bound by latency of the per-slot gathers; no LDS or MFMA.
+#include "dev_common.hpp"
+
+namespace gw {
+
+namespace {
+
+constexpr uint32_t ROWS = 3;
+
+__device__ __forceinline__ bool op_valid(const gw_op& op, uint32_t cap) {
+    return op.kind >= GW_OP_ENTER && op.kind <= GW_OP_SYNC && op.slot < cap;
+}
+
+__global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
+                                                int32_t* last_pos, int32_t* last_aoi, int32_t* last_leave,
+                                                HaloStats* hs) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const gw_op op = ops[i];
+    if (op.kind == GW_OP_NOP) return;
+    if (!op_valid(op, cap)) {
+        atomicAdd(&hs->bad_ops, 1ull);
+        return;
+    }
+    if (op.kind != GW_OP_LEAVE) atomicMax(&last_pos[op.slot], (int32_t)i);
+    if (op.kind != GW_OP_SYNC) atomicMax(&last_aoi[op.slot], (int32_t)i);
+    if (op.kind == GW_OP_LEAVE) atomicMax(&last_leave[op.slot], (int32_t)i);
+}
+
+__global__ void __launch_bounds__(NT) k_route2(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
+                                                const int32_t* __restrict__ last_leave, uint32_t* rflag) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const gw_op op = ops[i];
+    if (!op_valid(op, cap) || !(op.sync_flags & SIF_ROUTED)) return;
+    if ((int32_t)i > last_leave[op.slot]) atomicOr(&rflag[op.slot], (uint32_t)(op.sync_flags & SIF_ROUTED));
+}
+
+__device__ __forceinline__ gw_op mk_op(uint8_t kind, uint8_t flags, uint32_t slot, const gw_op* payload) {
+    gw_op o;
+    o.kind = kind;
+    o.sync_flags = flags;
+    o.reserved = 0;
+    o.slot = slot;
+    if (payload) {
+        o.x = payload->x; o.y = payload->y; o.z = payload->z; o.yaw = payload->yaw;
+    } else {
+        o.x = o.y = o.z = o.yaw = 0.f;
+    }
+    return o;
+}
+
+__device__ __forceinline__ void put_row(gw_halo_row* r, const gw_op& o, unsigned long long stamp) {
+    r->op = o;
+    r->stamp = stamp;
+}
+
+__global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, const unsigned long long* __restrict__ stamps,
+                                                uint32_t n, World w, const int32_t* __restrict__ last_pos,
+                                                const int32_t* __restrict__ last_aoi,
+                                                const int32_t* __restrict__ last_leave,
+                                                const uint32_t* __restrict__ rflag, float max_step, HaloDsts D,
+                                                HaloStats* hs) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    // every lane reaches the wave-aggregated appends below
+    bool rep = false;
+    uint32_t s = 0;
+    int32_t la = -1, ll = -1, lp = -1;
+    if (i < n) {
+        const gw_op op = ops[i];
+        if (op_valid(op, w.cap)) {
+            s = op.slot;
+            la = last_aoi[s];
+            ll = last_leave[s];
+            lp = last_pos[s];
+            rep = (int32_t)i == max(lp, ll);          // the entity's last op
+        }
+    }
+    bool old_p = false, new_p = false;
+    float old_x = 0.f, new_x = 0.f;
+    uint32_t f = 0;
+    gw_op oa{}, op_pos{};
+    if (rep) {
+        const AoiEnt a = w.aoi[s];
+        old_p = (a.meta & PRESENT_BIT) != 0;
+        old_x = a.x;
+        new_p = old_p;
+        new_x = old_x;
+        if (la >= 0) {
+            oa = ops[la];
+            new_p = oa.kind != GW_OP_LEAVE;
+            if (new_p) new_x = oa.x;
+            if (old_p && new_p && fabsf(new_x - old_x) > max_step) atomicAdd(&hs->bad_moves, 1ull);
+        }
+        if (lp >= 0) op_pos = ops[lp];
+        f = (((ll >= 0) ? 0u : w.flags[s]) | rflag[s]) & SIF_ROUTED;   // syncInfoFlag since the last Leave
+    }
+    for (uint32_t d = 0; d < D.n; ++d) {
+        const HaloDst& dst = D.d[d];
+        const bool was = old_p && old_x >= dst.x_lo && old_x < dst.x_hi;
+        const bool now = new_p && new_x >= dst.x_lo && new_x < dst.x_hi;
+        uint8_t k0 = GW_OP_NOP, k1 = GW_OP_NOP, k2 = GW_OP_NOP;
+        if (rep) {
+            if (la >= 0) {
+                if (ll >= 0 && was && now) k0 = GW_OP_LEAVE;
+                if (now && (!was || ll >= 0)) k1 = GW_OP_ENTER;
+                else if (was && now) k1 = GW_OP_MOVED;
+                else if (was) k1 = GW_OP_LEAVE;
+            }
+            if (now && (f != 0 || lp > la)) k2 = GW_OP_SYNC;
+        }
+        const bool emit = rep && (k0 | k1 | k2);
+        const uint64_t bm = wave_ballot(emit);
+        if (!bm) continue;
+        const int leader = __builtin_ctzll(bm);
+        uint32_t base = 0;
+        if (lane_id() == leader) base = atomicAdd(&hs->cnt[d], (uint32_t)popc64(bm));
+        base = __shfl(base, leader, 64);
+        if (!emit) continue;
+        const uint32_t e = base + (uint32_t)popc64(bm & lanemask_lt());
+        if (e >= dst.cap) {
+            atomicAdd(&hs->overflow, 1ull);
+            continue;
+        }
+        gw_halo_row* r = dst.rows + (size_t)e * ROWS;
+        if (k0) put_row(r + 0, mk_op(k0, 0, s, nullptr), stamps[ll]);
+        if (k1) put_row(r + 1, mk_op(k1, 0, s, &oa), stamps[la]);
+        if (k2) put_row(r + 2, mk_op(k2, (uint8_t)f, s, &op_pos), stamps[i]);
+    }
+}
+
+__global__ void __launch_bounds__(NT) k_route4(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
+                                                int32_t* last_pos, int32_t* last_aoi, int32_t* last_leave,
+                                                uint32_t* rflag) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const gw_op op = ops[i];
+    if (!op_valid(op, cap)) return;
+    last_pos[op.slot] = -1;
+    last_aoi[op.slot] = -1;
+    last_leave[op.slot] = -1;
+    rflag[op.slot] = 0;
+}
+
+__global__ void __launch_bounds__(NT) k_split_rows(const gw_halo_row* __restrict__ rows, uint32_t n,
+                                                    gw_op* __restrict__ ops, unsigned long long* __restrict__ stamps) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    ops[i] = rows[i].op;
+    stamps[i] = rows[i].stamp;
+}
+
+}  // namespace
+
+void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
+                       float max_step, const HaloDsts& D, int32_t* last_pos, int32_t* last_aoi,
+                       int32_t* last_leave, uint32_t* rflag, HaloStats* hs, hipStream_t s) {
+    const uint32_t nb = nblk1(n, NT);
+    hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, last_pos, last_aoi, last_leave, hs);
+    hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, last_leave, rflag);
+    hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, last_pos, last_aoi, last_leave,
+                       rflag, max_step, D, hs);
+    hipLaunchKernelGGL(k_route4, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, last_pos, last_aoi, last_leave, rflag);
+}
+
+void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,
+                       hipStream_t s) {
+    hipLaunchKernelGGL(k_split_rows, dim3(nblk1(n, NT)), dim3(NT), 0, s, rows, n, ops, stamps);
+}
+
+}  // namespace gw

@@ -33,12 +33,16 @@ Requirements (checked): a present entity moves at most max_step in x per tick;
 strips are wider than h + max_step, so an entity is only ever held by its
 owner and the owner's two neighbours.
 
-The op routing (masks, per-entity reductions, compaction into fixed-size
-NOP-padded buffers) is torch on the engine's device with no host sync; the
-halo exchange is torch.distributed point-to-point (RCCL over xGMI with the
-nccl backend, gloo for the CPU tests); all AOI work is the HIP engine's
-(gpuaoi.py), on torch's stream (gw_set_stream).  Local slots are the global
-entity ids (the local space's capacity is the world population).
+On the GPU the routing is the engine's (gw_route_halo, halo.hip: the entity
+state before the tick is the routing state; four light passes over the owned
+ops, rows placed by wave-aggregated atomics into fixed-size NOP-padded
+buffers, no host sync).  `Router` below is the same protocol in torch, kept
+as its readable statement and for the CPU tests' mock engine; the two are
+checked row for row against each other on the GPU.  The halo exchange is
+torch.distributed point-to-point (RCCL over xGMI with the nccl backend, gloo
+for the CPU tests); all AOI work is the HIP engine's, on torch's stream
+(gw_set_stream).  Local slots are the global entity ids (the local space's
+capacity is the world population).
 """
 from __future__ import annotations
 
@@ -124,9 +128,11 @@ def _f32(words_col: torch.Tensor) -> torch.Tensor:
 
 
 class Router:
-    """Routing state of one rank: position, presence and pending sync flags of
-    every entity the rank holds (owned or ghost), indexed by global id (+ one
-    dummy row, index n, that absorbs masked-out scatters)."""
+    """Torch statement of the routing protocol (the GPU path runs HipRouter).
+
+    State of one rank: position, presence and pending sync flags of every
+    entity the rank holds (owned or ghost), indexed by global id (+ one dummy
+    row, index n, that absorbs masked-out scatters and invalid slots)."""
 
     def __init__(self, geom: Strips, rank: int, n_global: int, device, halo_cap: int):
         self.g, self.r, self.n, self.dev, self.K = geom, rank, n_global, device, halo_cap
@@ -161,15 +167,16 @@ class Router:
 
     def route(self, words: torch.Tensor, stamps: torch.Tensor):
         """Owned ops of one tick -> (send to left, send to right): NOP-padded
-        int32 row buffers ((K+1) * 3, 8).  Updates the routing state.  No host
-        sync."""
+        int32 row buffers (K * 3, 8) in gw_halo_row layout.  Updates the
+        routing state.  No host sync."""
         g, r = self.g, self.r
         m = words.shape[0]
         dev = self.dev
         kind = words[:, 0] & 0xFF
         flags = (words[:, 0] >> 8) & SIF_MASK
-        valid = (kind >= OP_ENTER) & (kind <= OP_SYNC)
-        slot = torch.where(valid, words[:, 1].to(torch.int64), torch.full((m,), self.n, dtype=torch.int64, device=dev))
+        raw = words[:, 1].to(torch.int64) & 0xFFFFFFFF
+        valid = (kind >= OP_ENTER) & (kind <= OP_SYNC) & (raw < self.n)
+        slot = torch.where(valid, raw, torch.full((m,), self.n, dtype=torch.int64, device=dev))
         idx = torch.arange(m, dtype=torch.int64, device=dev)
         aoi = valid & (kind != OP_SYNC)
         lv = kind == OP_LEAVE
@@ -186,8 +193,8 @@ class Router:
         old_x, old_p, old_f = self.x[slot], self.present[slot], self.pflags[slot]
         new_p = torch.where(has_aoi, ka != OP_LEAVE, old_p)
         new_x = torch.where(has_aoi & new_p, xa, old_x)
-        new_f = torch.where(new_p, torch.where(had_leave, torch.zeros_like(old_f), old_f) | fo,
-                            torch.zeros_like(old_f))
+        # the engine's syncInfoFlag rule: OR of the flags since the last Leave
+        new_f = torch.where(had_leave, torch.zeros_like(old_f), old_f) | fo
         # the strip contract: an owned entity stays inside this rank's range + max_step
         moved = rep & has_aoi & old_p & new_p
         self.bad_moves += (moved & ((new_x - old_x).abs() > g.max_step)).sum()
@@ -244,14 +251,12 @@ class Router:
         rows = rows * (torch.stack([k0, k1, k2], 1) != 0).to(torch.int32).unsqueeze(2)
         buf = torch.zeros((K + 1, ROWS_PER_ENTITY, ROW_WORDS), dtype=torch.int32, device=self.dev)
         buf.index_copy_(0, dst, rows)   # duplicates only at the trash row K
-        buf[K].zero_()
-        return buf.view(-1, ROW_WORDS)
+        return buf[:K].reshape(-1, ROW_WORDS)
 
     def receive(self, buf: torch.Tensor):
-        """Ghost rows from a neighbour -> (words, stamps) for the engine;
-        updates the routing state."""
+        """Ghost rows from a neighbour: updates the routing state."""
         K = self.K
-        rows = buf.view(K + 1, ROWS_PER_ENTITY, ROW_WORDS)[:K]
+        rows = buf.view(K, ROWS_PER_ENTITY, ROW_WORDS)
         k1 = rows[:, 1, 0] & 0xFF
         k2 = rows[:, 2, 0] & 0xFF
         f2 = (rows[:, 2, 0] >> 8) & SIF_MASK
@@ -265,12 +270,52 @@ class Router:
         self.x[slot] = x
         self.present[slot] = p
         self.pflags[slot] = f
-        flat = rows.reshape(-1, ROW_WORDS)
-        return flat[:, :OP_WORDS].contiguous(), flat[:, OP_WORDS:].contiguous().view(torch.int64).view(-1)
 
     def collected(self):
         """Sync flags are cleared everywhere by a collect (Entity.go:1221-1267)."""
         self.pflags.zero_()
+
+    def status(self):
+        ov, bad = int(self.overflow.item()), int(self.bad_moves.item())
+        self.overflow.zero_()
+        self.bad_moves.zero_()
+        return max(ov, 0), bad, 0
+
+
+def split_rows(buf: torch.Tensor):
+    """gw_halo_row buffer (rows, 8) int32 -> (op words (rows, 6), stamps (rows,))."""
+    return buf[:, :OP_WORDS].contiguous(), buf[:, OP_WORDS:].contiguous().view(torch.int64).view(-1)
+
+
+class HipRouter:
+    """The routing on the GPU: gw_route_halo of the rank's engine context
+    writes the rows of both neighbours into persistent torch buffers."""
+
+    def __init__(self, g, geom: Strips, rank: int, device, halo_cap: int):
+        self.g, self.geom, self.r, self.K = g, geom, rank, halo_cap
+        self.bufs, self.dsts = [], []
+        for nb in (rank - 1, rank + 1):
+            if 0 <= nb < geom.ranks:
+                b = torch.zeros((halo_cap * ROWS_PER_ENTITY, ROW_WORDS), dtype=torch.int32, device=device)
+                lo, hi = geom.ext(nb)
+                self.bufs.append(b)
+                self.dsts.append((float(np.float32(lo)), float(np.float32(hi)), b.data_ptr(), halo_cap))
+            else:
+                self.bufs.append(None)
+
+    def route(self, words: torch.Tensor, stamps: torch.Tensor):
+        self.g.route_halo(words.data_ptr(), stamps.data_ptr(), words.shape[0], float(self.geom.max_step),
+                          self.dsts)
+        return self.bufs[0], self.bufs[1]
+
+    def receive(self, buf):
+        pass                        # the engine's own state is the routing state
+
+    def collected(self):
+        pass
+
+    def status(self):
+        return self.g.halo_status()
 
 
 def exchange(pg, rank: int, ranks: int, send_left, send_right, nrows: int, device, comm_device):
@@ -295,7 +340,7 @@ def exchange(pg, rank: int, ranks: int, send_left, send_right, nrows: int, devic
 class HipStrip:
     """Engine adapter: a gpuaoi.GpuAOI context sharing one stream with torch
     (made torch's current stream), so routing kernels, collectives and AOI
-    kernels are ordered without host syncs."""
+    kernels are ordered without host syncs.  Routing: HipRouter."""
 
     def __init__(self, g):
         self.g = g
@@ -313,13 +358,21 @@ class HipStrip:
     def set_clients(self, slots, gates):
         self.g.set_clients(slots, gates)
 
+    def make_router(self, geom, rank, n_global, device, halo_cap):
+        return HipRouter(self.g, geom, rank, device, halo_cap)
+
     def submit(self, words: torch.Tensor, stamps: torch.Tensor):
         words, stamps = words.contiguous(), stamps.contiguous()
         self._keep += [words, stamps]        # alive until the tick has consumed them
         self.g.submit_device_stamped(words.data_ptr(), stamps.data_ptr(), words.shape[0])
 
-    def tick(self, copy=True):
-        res = self.g.tick(copy=copy)
+    def submit_rows(self, rows: torch.Tensor):
+        rows = rows.contiguous()
+        self._keep.append(rows)
+        self.g.submit_device_rows(rows.data_ptr(), rows.shape[0])
+
+    def tick(self, copy=True, no_events=False):
+        res = self.g.tick(copy=copy, no_events=no_events)
         self._keep = []
         return res
 
@@ -329,7 +382,8 @@ class HipStrip:
 
 class StripRank:
     """One rank of a decomposed world.  `engine` follows HipStrip's interface
-    (create_space / set_ownership / set_clients / submit / tick / collect)."""
+    (make_router / create_space / set_ownership / set_clients / submit /
+    submit_rows / tick / collect)."""
 
     def __init__(self, engine, geom: Strips, rank: int, n_global: int, bounds, device,
                  pg=None, comm_device=None, halo_cap: int = 1 << 14):
@@ -337,7 +391,7 @@ class StripRank:
         self.dev = device
         self.pg = pg
         self.cdev = comm_device if comm_device is not None else device
-        self.router = Router(geom, rank, n_global, device, halo_cap)
+        self.router = engine.make_router(geom, rank, n_global, device, halo_cap)
         self.sid, base = engine.create_space(geom.d, n_global, bounds)
         if base != 0:
             raise ValueError("a strip rank holds one space per context (local slot = global id)")
@@ -350,25 +404,23 @@ class StripRank:
         m = words.shape[0]
         st = stamps_for(self.tick_no, self.r, self.g.ranks, m, self.dev)
         sl, sr = self.router.route(words, st)
-        nrows = (self.router.K + 1) * ROWS_PER_ENTITY
+        nrows = self.router.K * ROWS_PER_ENTITY
         if self.g.ranks > 1:
             recvd = exchange(self.pg, self.r, self.g.ranks, sl, sr, nrows, self.dev, self.cdev)
         else:
             recvd = []
-        parts_w, parts_s = [words], [st]
+        self.e.submit(words, st)
         for buf in recvd:
-            w, s = self.router.receive(buf)
-            parts_w.append(w)
-            parts_s.append(s)
-        self.e.submit(torch.cat(parts_w), torch.cat(parts_s))
+            self.router.receive(buf)
+            self.e.submit_rows(buf)
         self.tick_no += 1
 
-    def tick(self, copy=True):
-        return self.e.tick(copy=copy)
+    def tick(self, copy=True, **kw):
+        return self.e.tick(copy=copy, **kw)
 
-    def step(self, words: torch.Tensor, copy=True):
+    def step(self, words: torch.Tensor, copy=True, **kw):
         self.submit(words)
-        return self.tick(copy=copy)
+        return self.tick(copy=copy, **kw)
 
     def collect(self, copy=True):
         res = self.e.collect(copy=copy)
@@ -377,8 +429,10 @@ class StripRank:
 
     def check(self):
         """Host check of the contract counters (one sync; call outside timed loops)."""
-        ov, bad = int(self.router.overflow.item()), int(self.router.bad_moves.item())
+        ov, bad, bad_ops = self.router.status()
         if ov > 0:
-            raise RuntimeError(f"halo buffer overflow by {ov} entities (raise halo_cap)")
+            raise RuntimeError(f"halo buffers overflowed by {ov} entities (raise halo_cap)")
         if bad:
             raise RuntimeError(f"{bad} owned entities moved more than max_step in one tick")
+        if bad_ops:
+            raise RuntimeError(f"{bad_ops} ops with an invalid slot or kind")

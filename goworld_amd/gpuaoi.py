@@ -55,6 +55,11 @@ class StageTimes(C.Structure):
                 ("bytes_alg", _u64 * MAX_STAGES)]
 
 
+class HaloDst(C.Structure):
+    _fields_ = [("x_lo", C.c_float), ("x_hi", C.c_float), ("rows", C.c_void_p), ("cap_entities", _u32),
+                ("reserved", _u32)]
+
+
 class GwError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"gpuaoi error {code}: {msg}")
@@ -98,6 +103,9 @@ def lib():
         L.gw_submit_device_stamped.argtypes = [vp, vp, vp, _u32]
         L.gw_space_set_ownership.argtypes = [vp, _u32, C.c_float, C.c_float]
         L.gw_set_stream.argtypes = [vp, vp]
+        L.gw_route_halo.argtypes = [vp, vp, vp, _u32, C.c_float, C.POINTER(HaloDst), _u32]
+        L.gw_submit_device_rows.argtypes = [vp, vp, _u32]
+        L.gw_halo_status.argtypes = [vp, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64)]
         _lib = L
     return _lib
 
@@ -107,7 +115,7 @@ EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_spa
             "gw_sync_collect", "gw_neighbors", "gw_set_profiling", "gw_get_stage_times",
             "gw_total_neighbors", "gw_device_alloc", "gw_device_free", "gw_memcpy_h2d",
             "gw_memcpy_d2h", "gw_synchronize", "gw_submit_device_stamped", "gw_space_set_ownership",
-            "gw_set_stream"]
+            "gw_set_stream", "gw_route_halo", "gw_submit_device_rows", "gw_halo_status"]
 
 
 def _p(a: np.ndarray):
@@ -205,6 +213,20 @@ class GpuAOI:
     def set_stream(self, hip_stream: int | None):
         """Run on a caller's stream (e.g. torch.cuda.current_stream().cuda_stream)."""
         self._chk(lib().gw_set_stream(self._h, hip_stream or None))
+
+    def route_halo(self, dev_ops: int, dev_stamps: int, n: int, max_step: float, dsts):
+        """dsts: list of (x_lo, x_hi, dev_rows_ptr, cap_entities) (decomposed world, owner side)."""
+        arr = (HaloDst * max(1, len(dsts)))(*[HaloDst(lo, hi, C.c_void_p(p), cap, 0) for lo, hi, p, cap in dsts])
+        self._chk(lib().gw_route_halo(self._h, C.c_void_p(dev_ops), C.c_void_p(dev_stamps), n, max_step, arr,
+                                      len(dsts)))
+
+    def submit_device_rows(self, dev_rows: int, n: int):
+        self._chk(lib().gw_submit_device_rows(self._h, C.c_void_p(dev_rows), n))
+
+    def halo_status(self) -> tuple[int, int, int]:
+        v = [_u64() for _ in range(3)]
+        self._chk(lib().gw_halo_status(self._h, *[C.byref(x) for x in v]))
+        return tuple(x.value for x in v)
 
     def set_clients(self, slots, gates):
         s = np.ascontiguousarray(slots, dtype=np.uint32)

@@ -174,6 +174,46 @@ int  gw_submit_device_stamped(gw_ctx* ctx, const gw_op* dev_ops, const uint64_t*
  * Default: the whole line. */
 int  gw_space_set_ownership(gw_ctx* ctx, uint32_t space_id, float x_lo, float x_hi);
 
+/* ---- decomposed world (one space split into X-strips over processes) ----
+ * A halo row (32 B) is an op with its global stamp.  A destination is a
+ * neighbour process: the x-range its local space holds (its strip widened by
+ * the halo) and a device buffer of cap_entities * 3 rows. */
+typedef struct gw_halo_row {
+    gw_op    op;
+    uint64_t stamp;
+} gw_halo_row;
+
+typedef struct gw_halo_dst {
+    float        x_lo, x_hi;     /* the neighbour holds entities with x in [x_lo, x_hi) */
+    gw_halo_row* rows;           /* device memory, cap_entities * 3 rows               */
+    uint32_t     cap_entities;
+    uint32_t     reserved;
+} gw_halo_dst;
+
+/* Owner side, BEFORE submitting the same ops: for this process's owned ops
+ * of the tick (device memory, with their global stamps) write, per
+ * destination, the rows that bring the neighbour's copy of every affected
+ * entity up to date, 3 per entity in this order (NOP rows where not needed):
+ *   LEAVE   the entity left the space and re-entered inside the tick;
+ *   ENTER / MOVED / LEAVE   the net AOI change relative to [x_lo, x_hi),
+ *           with the payload and stamp of the entity's last AOI op;
+ *   SYNC    the payload of its last non-Leave op and all sync flags pending
+ *           since the last collect.
+ * Unused rows are zero (GW_OP_NOP).  Reads the entity state before the
+ * tick; no host sync.  Entities beyond a buffer's capacity, moves longer
+ * than max_step in x and ops with an invalid slot or kind are counted
+ * (gw_halo_status). */
+int  gw_route_halo(gw_ctx* ctx, const gw_op* dev_ops, const uint64_t* dev_stamps, uint32_t n,
+                   float max_step, const gw_halo_dst* dsts, uint32_t n_dst);
+
+/* Receiver side: rows from a neighbour's gw_route_halo (device memory), part
+ * of this tick's op stream like gw_submit_device_stamped ops. */
+int  gw_submit_device_rows(gw_ctx* ctx, const gw_halo_row* dev_rows, uint32_t n);
+
+/* Counters accumulated by gw_route_halo since the last call (synchronises,
+ * then resets them). */
+int  gw_halo_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops);
+
 /* Attach / detach clients: gate 0 = no client (GameClient nil). */
 int  gw_set_clients(gw_ctx* ctx, const uint32_t* slots, const uint16_t* gates, uint32_t n);
 
@@ -219,7 +259,7 @@ int  gw_synchronize(gw_ctx* ctx);
 int  gw_set_stream(gw_ctx* ctx, void* hip_stream);
 
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 2
+#define GW_ABI_VERSION 3
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

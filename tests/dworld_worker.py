@@ -30,6 +30,12 @@ class OracleStrip:
         self.pyorc = pyorc
         self.words, self.stamps = [], []
 
+    def make_router(self, geom, rank, n_global, device, halo_cap):
+        return dworld.Router(geom, rank, n_global, device, halo_cap)
+
+    def submit_rows(self, rows):
+        self.submit(*dworld.split_rows(rows))
+
     def create_space(self, d, cap, bounds):
         self.o = self.pyorc.OracleSpace(cap, d, self.pyorc.SEQRULE)
         self.x = np.zeros(cap, np.float32)

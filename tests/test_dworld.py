@@ -124,3 +124,53 @@ def test_dworld_gloo_oracle_ranks(world, tmp_path):
 @pytest.mark.gpu
 def test_dworld_gpu_two_ranks(tmp_path):
     _check(2, _run_ranks(2, "hip", tmp_path, timeout=100))
+
+
+def _canon_rows(buf, K):
+    rows = buf.view(K, 3, 8).cpu().numpy()
+    used = rows[np.any(rows[:, :, 0] & 0xFF, axis=1)]
+    slot = used[:, :, 1].max(axis=1)
+    return used[np.argsort(slot, kind="stable")]
+
+
+@pytest.mark.gpu
+def test_hip_router_rows_match_torch_router():
+    """gw_route_halo (halo.hip) writes, per neighbour, the same entity rows
+    as the torch statement of the protocol (dworld.Router), tick by tick, for
+    the middle rank of a 3-strip world (order of entities aside)."""
+    import torch
+    from goworld_amd import gpuaoi
+    tr = T.strip_world_trace(TRACE["seed"], TRACE["n"], 3, TRACE["strip_w"], TRACE["height"],
+                             TRACE["d"], TRACE["ticks"], TRACE["max_step"])
+    geom = dworld.Strips(0.0, tr.strip_w, 3, tr.d, tr.max_step)
+    dev = torch.device("cuda:0")
+    K = 512
+    with gpuaoi.GpuAOI(0) as g:
+        eng = dworld.HipStrip(g)
+        eng.create_space(tr.d, tr.n, tr.bounds)
+        hip = eng.make_router(geom, 1, tr.n, dev, K)
+        ref = dworld.Router(geom, 1, tr.n, dev, K)
+        n_rows = 0
+        for t in range(len(tr.ticks)):
+            w = torch.from_numpy(dworld.ops_to_words(tr.rank_ops(t, 1)).copy()).to(dev)
+            st = dworld.stamps_for(t, 1, 3, w.shape[0], dev)
+            for side, (a, b) in enumerate(zip(hip.route(w, st), ref.route(w, st))):
+                ca, cb = _canon_rows(a, K), _canon_rows(b, K)
+                assert ca.shape == cb.shape, (t, side, ca.shape, cb.shape)
+                assert ca.tobytes() == cb.tobytes(), f"tick {t} side {side}: halo rows differ"
+                n_rows += len(ca)
+            eng.submit(w, st)
+            eng.tick(copy=False)
+            if t % 3 == 2:
+                eng.collect(copy=False)
+                ref.collected()
+        assert n_rows > 300
+        # no overflow; the same move-bound violations (entities that come back
+        # after ticks owned elsewhere, whose ghost rows this lone rank never got)
+        assert hip.status() == ref.status()
+        # invalid slots are counted, never followed
+        bad = w.clone()
+        bad[:, 1] = tr.n + 5
+        hip.route(bad, st)
+        assert hip.status()[2] == bad.shape[0]
+        torch.cuda.synchronize()

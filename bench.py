@@ -58,6 +58,8 @@ def parse():
                     help="halo exchange backend (gloo: rehearsal of several ranks on one GPU)")
     ap.add_argument("--halo-cap", type=int, default=16384, help="halo entities per neighbour per tick")
     ap.add_argument("--device", type=int, default=None, help="force a device (rehearsals on one GPU)")
+    ap.add_argument("--capacity", type=int, default=None,
+                    help="slot capacity of the space (N=1: cost of a strip's id range at N ranks)")
     return ap.parse_args()
 
 
@@ -146,6 +148,9 @@ class SpaceRun:
 
     def __init__(self, a, ctl, ticks):
         self.tr = traces.config3(ticks=ticks, seed=3 + ctl.rank, n=a.entities, side=a.side)
+        if a.capacity:
+            self.tr.capacity = max(a.capacity, a.entities)
+            self.tr.gates = np.concatenate([self.tr.gates, np.zeros(self.tr.capacity - a.entities, np.uint16)])
         self.g = g = gpuaoi.GpuAOI(ctl.local)
         gpuaoi.load_space(g, self.tr, chunk=1 << 18)
         g.sync_collect(copy=False)                      # clear the Enter flags (untimed)

@@ -60,6 +60,45 @@ __device__ __forceinline__ T block_excl_scan(T x, T* lds, T& total) {
     return pre + inc - x;
 }
 
+// Exclusive scan of one tile of IPT * NT values held STRIPED (thread t holds
+// elements j * NT + t, j < IPT: every load and store of the caller is
+// coalesced).  Each row j is scanned by wave scans; the IPT * NWAVE row/wave
+// partials (64 of them) are scanned once more by every wave, lane k holding
+// partial k = j * NWAVE + w.  v[j] becomes the exclusive prefix of its element
+// within the tile; total gets the tile sum.  lds: 64 elements.
+template <typename T, int IPT>
+__device__ __forceinline__ void tile_excl_scan_striped(T (&v)[IPT], T* lds, T& total) {
+    constexpr int P = IPT * NWAVE;            // row/wave partials
+    constexpr int Q = P / 64;                 // partials per lane
+    static_assert(P % 64 == 0, "whole partials per lane");
+    const int w = (int)(threadIdx.x >> 6), ln = lane_id();
+    T inc[IPT];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        inc[j] = wave_incl_scan(v[j]);
+        if (ln == 63) lds[j * NWAVE + w] = inc[j];
+    }
+    __syncthreads();
+    // lane k holds partials k*Q .. k*Q+Q-1 (row-major: j * NWAVE + w)
+    T q[Q], ls = 0;
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {
+        q[k] = ls;
+        ls += lds[ln * Q + k];
+    }
+    const T li = wave_incl_scan(ls);
+    total = __shfl(li, 63, 64);
+    const T le = li - ls;
+#pragma unroll
+    for (int k = 0; k < Q; ++k) q[k] += le;      // exclusive prefix of each partial
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const int idx = j * NWAVE + w;            // wave-uniform
+        v[j] = __shfl(q[idx % Q], idx / Q, 64) + inc[j] - v[j];
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ uint64_t load_n(uint64_t n_max, const uint64_t* n_dev) {
     if (!n_dev) return n_max;
     uint64_t n = *n_dev;
@@ -79,6 +118,7 @@ __device__ __forceinline__ uint64_t load_n(uint64_t n_max, const uint64_t* n_dev
 // earlier scans read as "not posted", so the status array is never cleared.
 constexpr int SCAN_IPT = 16;
 constexpr int SCAN_TILE = NT * SCAN_IPT;
+constexpr uint64_t SCAN_BIG = 1ull << 21;           // larger scans use 2 * SCAN_TILE tiles
 constexpr int SCAN_SHIFT = 34;                       // tag above flag bit 33 and the 32-bit half
 constexpr unsigned long long SCAN_POSTED = 1ull << 33;
 constexpr uint32_t SCAN_TAG_MAX = (1u << 22) - 1;
@@ -144,59 +184,67 @@ __device__ __forceinline__ TO scan_lookback(unsigned long long* __restrict__ sta
     return excl;
 }
 
-template <typename TI, typename TO>
+template <typename TI, typename TO, int IPT>
 __global__ void __launch_bounds__(NT) k_scan1(const TI* in, TO* out, uint64_t n_max, const uint64_t* n_dev,
                                               unsigned long long* __restrict__ status,
                                               unsigned long long* __restrict__ ticket, unsigned long long tbase,
                                               uint32_t tag, TO* total) {
-    __shared__ TO lds[NWAVE];
+    __shared__ TO lds[IPT * NWAVE];
     __shared__ uint32_t s_tile;
     __shared__ TO s_prefix;
     if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tbase);
     __syncthreads();
     const uint32_t tile = s_tile;
     const uint64_t n = load_n(n_max, n_dev);
-    const uint64_t base = (uint64_t)tile * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_IPT;
-    TO v[SCAN_IPT];
-    TO s = 0;
+    const uint64_t t0 = (uint64_t)tile * (IPT * NT);
+    // tiles past a device-side count do nothing (no later tile waits on them)
+    if (t0 >= n && tile > 0) return;
+    TO v[IPT];
 #pragma unroll
-    for (int j = 0; j < SCAN_IPT; ++j) {
-        const uint64_t i = base + j;
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
         v[j] = i < n ? (TO)in[i] : (TO)0;
-        s += v[j];
     }
     TO tot;
-    const TO pre = block_excl_scan<TO>(s, lds, tot);
+    tile_excl_scan_striped<TO, IPT>(v, lds, tot);
     if (threadIdx.x < 64) {
         const TO excl = scan_lookback<TO>(status, tile, tag, tot);
         if (threadIdx.x == 0) s_prefix = excl;
     }
     __syncthreads();
-    TO run = s_prefix + pre;
+    const TO pre = s_prefix;
     if (out) {
 #pragma unroll
-        for (int j = 0; j < SCAN_IPT; ++j) {
-            const uint64_t i = base + j;
-            if (i < n) out[i] = run;
-            run += v[j];
+        for (int j = 0; j < IPT; ++j) {
+            const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
+            if (i < n) out[i] = pre + v[j];
         }
     }
-    if (total && tile == gridDim.x - 1 && threadIdx.x == 0) *total = s_prefix + tot;
+    // the last tile holding data (tile 0 when n == 0) writes the total
+    const uint64_t last = n ? (n - 1) / (IPT * NT) : 0;
+    if (total && tile == last && threadIdx.x == 0) *total = pre + tot;
 }
 
 // host launcher; sc.status must hold SCAN_WORDS * ceil(n_max / SCAN_TILE) words
 template <typename TI, typename TO>
 inline void scan_exclusive(const TI* in, TO* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
                            TO* total_dev, hipStream_t st) {
-    uint32_t nb = (uint32_t)((n_max + SCAN_TILE - 1) / SCAN_TILE);
+    // big scans take 8192-element tiles: half the tickets and look-back windows
+    const bool big = n_max > SCAN_BIG;
+    const uint64_t tile = big ? 2 * SCAN_TILE : SCAN_TILE;
+    uint32_t nb = (uint32_t)((n_max + tile - 1) / tile);
     if (nb == 0) nb = 1;
     if (sc.tag >= SCAN_TAG_MAX) {   // tags exhausted: clear the status words once
         (void)hipMemsetAsync(sc.status, 0, sc.max_tiles * SCAN_WORDS * 8, st);
         sc.tag = 0;
     }
     ++sc.tag;
-    hipLaunchKernelGGL((k_scan1<TI, TO>), dim3(nb), dim3(NT), 0, st, in, out, n_max, n_dev, sc.status, sc.ticket,
-                       sc.tbase, sc.tag, total_dev);
+    if (big)
+        hipLaunchKernelGGL((k_scan1<TI, TO, 2 * SCAN_IPT>), dim3(nb), dim3(NT), 0, st, in, out, n_max, n_dev,
+                           sc.status, sc.ticket, sc.tbase, sc.tag, total_dev);
+    else
+        hipLaunchKernelGGL((k_scan1<TI, TO, SCAN_IPT>), dim3(nb), dim3(NT), 0, st, in, out, n_max, n_dev,
+                           sc.status, sc.ticket, sc.tbase, sc.tag, total_dev);
     sc.tbase += nb;
 }
 inline uint64_t scan_tiles(uint64_t n_max) { return (n_max + SCAN_TILE - 1) / SCAN_TILE + 1; }

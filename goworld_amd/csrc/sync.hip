@@ -61,54 +61,62 @@ __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) 
 // look-back, prim.hpp): flagged[k] = slot, fbits[k] = its syncInfoFlag.  The
 // flags are cleared here, so the write pass reads fbits and can be rerun
 // after the record buffer overflowed.
+template <int IPT>
 __global__ void __launch_bounds__(NT) k_flag_compact1(uint32_t* __restrict__ flags, uint32_t cap,
                                                       uint32_t* __restrict__ flagged, uint32_t* __restrict__ fbits,
                                                       unsigned long long* __restrict__ status,
                                                       unsigned long long* __restrict__ ticket,
                                                       unsigned long long tbase, uint32_t tag, uint32_t* total) {
-    __shared__ uint32_t lds[NWAVE];
+    __shared__ uint32_t lds[IPT * NWAVE];
     __shared__ uint32_t s_tile, s_prefix;
     if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tbase);
     __syncthreads();
     const uint32_t tile = s_tile;
-    const uint64_t base = (uint64_t)tile * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_IPT;
-    uint32_t f[SCAN_IPT];
-    uint32_t c = 0;
+    const uint64_t t0 = (uint64_t)tile * (IPT * NT);
+    uint32_t f[IPT], c[IPT];
 #pragma unroll
-    for (int j = 0; j < SCAN_IPT; ++j) {
-        f[j] = base + j < cap ? flags[base + j] : 0u;
-        c += f[j] != 0;
+    for (int j = 0; j < IPT; ++j) {       // striped: coalesced loads
+        const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
+        f[j] = i < cap ? flags[i] : 0u;
+        c[j] = f[j] != 0;
     }
     uint32_t tot;
-    const uint32_t pre = block_excl_scan<uint32_t>(c, lds, tot);
+    tile_excl_scan_striped<uint32_t, IPT>(c, lds, tot);
     if (threadIdx.x < 64) {
         const uint32_t excl = scan_lookback<uint32_t>(status, tile, tag, tot);
         if (threadIdx.x == 0) s_prefix = excl;
     }
     __syncthreads();
-    uint32_t at = s_prefix + pre;
+    const uint32_t pre = s_prefix;
 #pragma unroll
-    for (int j = 0; j < SCAN_IPT; ++j) {
+    for (int j = 0; j < IPT; ++j) {
         if (f[j]) {
-            flagged[at] = (uint32_t)(base + j);
-            fbits[at] = f[j];
-            flags[base + j] = 0;
-            ++at;
+            const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
+            flagged[pre + c[j]] = (uint32_t)i;
+            fbits[pre + c[j]] = f[j];
+            flags[i] = 0;
         }
     }
-    if (tile == gridDim.x - 1 && threadIdx.x == 0) *total = s_prefix + tot;
+    if (tile == gridDim.x - 1 && threadIdx.x == 0) *total = pre + tot;
 }
+
 void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint32_t* fbits, ScanCtx& sc,
                          uint32_t* total, hipStream_t s) {
-    uint32_t nb = (uint32_t)((cap + SCAN_TILE - 1) / SCAN_TILE);
+    const bool big = cap > SCAN_BIG;
+    const uint64_t tile = big ? 2 * SCAN_TILE : SCAN_TILE;
+    uint32_t nb = (uint32_t)((cap + tile - 1) / tile);
     if (nb == 0) nb = 1;
     if (sc.tag >= SCAN_TAG_MAX) {
         (void)hipMemsetAsync(sc.status, 0, sc.max_tiles * SCAN_WORDS * 8, s);
         sc.tag = 0;
     }
     ++sc.tag;
-    hipLaunchKernelGGL(k_flag_compact1, dim3(nb), dim3(NT), 0, s, flags, cap, flagged, fbits, sc.status, sc.ticket,
-                       sc.tbase, sc.tag, total);
+    if (big)
+        hipLaunchKernelGGL(k_flag_compact1<2 * SCAN_IPT>, dim3(nb), dim3(NT), 0, s, flags, cap, flagged, fbits,
+                           sc.status, sc.ticket, sc.tbase, sc.tag, total);
+    else
+        hipLaunchKernelGGL(k_flag_compact1<SCAN_IPT>, dim3(nb), dim3(NT), 0, s, flags, cap, flagged, fbits,
+                           sc.status, sc.ticket, sc.tbase, sc.tag, total);
     sc.tbase += nb;
 }
 

@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--profile-stages", type=int, default=1, help="HIP-event stage timing in the timed region")
     ap.add_argument("--mode", choices=["world", "spaces"], default="world", help="N>1 regime")
+    ap.add_argument("--config", type=int, choices=[3, 5], default=3,
+                    help="3: config #3 per GPU (weak); 5: the 16M uniform world of config #5 over N strips (strong)")
     ap.add_argument("--comm", choices=["nccl", "gloo"], default="nccl",
                     help="halo exchange backend (gloo: rehearsal of several ranks on one GPU)")
     ap.add_argument("--halo-cap", type=int, default=16384, help="halo entities per neighbour per tick")
@@ -161,6 +163,7 @@ class SpaceRun:
         g.h2d(self.dev_ops, ops_all)
         self.nbytes_tick = self.m * traces.OP_DTYPE.itemsize
         self.parallelism = f"independent spaces x{ctl.ws} (no comm)" if ctl.ws > 1 else "single GPU"
+        self.n_world = a.entities * (ctl.ws if ctl.ws > 1 else 1)
 
     def step(self, t):
         g = self.g
@@ -175,7 +178,7 @@ class SpaceRun:
 
 
 class WorldRun:
-    """--mode world, N>1: one world of N strips (dworld.StripRank per rank)."""
+    """--mode world, N>1 (or --config 5): one world of N strips (dworld.StripRank per rank)."""
 
     def __init__(self, a, ctl, ticks):
         import torch
@@ -183,13 +186,21 @@ class WorldRun:
         self.torch = torch
         dev = torch.device("cuda", ctl.local)
         torch.cuda.set_device(dev)
-        ws, r, n, side = ctl.ws, ctl.rank, a.entities, a.side
+        ws, r = ctl.ws, ctl.rank
+        if a.config == 5:
+            # config #5: 16M uniform, L = 131072, strips of L / N, step +-4
+            tr = traces.config5_strip(r, ws, ticks=ticks)
+            n, side, side_z, max_step = tr.n, 131072.0 / ws, 131072.0, 4.0
+        else:
+            n, side = a.entities, a.side
+            tr = traces.config3(ticks=ticks, seed=3 + r, n=n, side=side)
+            side_z, max_step = side, 16.0                       # config #3 steps: +-4, hotspots +-16
         x0 = -ws * side / 2
-        tr = traces.config3(ticks=ticks, seed=3 + r, n=n, side=side)
-        geom = dworld.Strips(x0, side, ws, tr.d, 16.0)          # config #3 steps: +-4, hotspots +-16
+        geom = dworld.Strips(x0, side, ws, tr.d, max_step)
         off = np.float32(x0 + (r + 0.5) * side)                 # strip r's centre (exact in f32)
         lo, hi = geom.ext(r)
-        bounds = (max(lo, x0), -side / 2, min(hi, x0 + ws * side), side / 2)
+        bounds = (max(lo, x0), -side_z / 2, min(hi, x0 + ws * side), side_z / 2)
+        self.n_world = n * ws
         self.g = gpuaoi.GpuAOI(ctl.local)
         eng = dworld.HipStrip(self.g)
         pg = None if a.comm == "nccl" else ctl.group
@@ -210,7 +221,8 @@ class WorldRun:
         self.m = len(tr.ticks[0])
         self.words = [words(t) for t in tr.ticks]              # resident in HBM
         torch.cuda.synchronize()
-        self.parallelism = f"decomposed world, {ws} X-strips, halo rows over {a.comm.upper()}"
+        self.parallelism = (f"decomposed world, {ws} X-strips, halo rows over {a.comm.upper()}" if ws > 1
+                            else "single GPU, one-strip world")
         self.tr = tr
 
     def step(self, t):
@@ -229,7 +241,7 @@ def main():
     ws, rank = ctl.ws, ctl.rank
     ticks = a.warmup + a.steps
     t_load = time.perf_counter()
-    world = ws > 1 and a.mode == "world"
+    world = (ws > 1 and a.mode == "world") or a.config == 5
     run = WorldRun(a, ctl, ticks) if world else SpaceRun(a, ctl, ticks)
     t_load = time.perf_counter() - t_load
     g = run.g
@@ -267,7 +279,11 @@ def main():
         run.close()
         return
     K = a.steps
-    if world:
+    if a.config == 5:
+        workload = (f"config #5: one 16M-entity uniform world space, L = 131072, AOI distance 100, 10% movers "
+                    f"per tick (step +-4), decomposed into {ws} X-strip(s) of {131072 // ws} x 131072 (walkers "
+                    f"reflect at strip borders); step = route + halo exchange + gw_tick + gw_sync_collect")
+    elif world:
         workload = (f"config #5 shape: one world space of {ws} x {a.entities} entities decomposed into {ws} "
                     f"X-strips of {a.side:g} x {a.side:g}, each with config #3 statistics (70% uniform + 30% in "
                     f"64 Gaussian hotspots, 10% movers per tick), AOI distance 100; step = route + halo "
@@ -285,14 +301,16 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": mx / K * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if a.config == 5 else "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #3" + (" per strip)" if world else ")"),
+        "data": ("synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #5)" if a.config == 5 else
+                 "synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #3" + (" per strip)" if world else ")")),
         "config": {"workload": workload,
-                   "entities_per_gpu": a.entities, "world_entities": a.entities * (ws if world else 1),
+                   "entities_per_gpu": run.n_world // ws, "world_entities": run.n_world,
                    "movers_per_tick_per_gpu": run.m, "aoi_dist": 100.0,
-                   "world_side": a.side, "gates": 1, "parallelism": run.parallelism},
+                   "world_side": 131072.0 if a.config == 5 else a.side, "gates": 1,
+                   "parallelism": run.parallelism},
         "events_per_sec": sums[1] / mx,
         "records_per_sec": sums[2] / mx,
         "device_us_per_step": (sum(stage_us.values()) / K) if stage_us else None,
@@ -316,7 +334,7 @@ def main():
             v["bytes_alg"] / max(v["avg_us"], 1e-9) / 1e3, 1)} for n, v in stages.items()}
     else:
         line["roofline"] = None
-    if not a.no_cpu_baseline and ws == 1:
+    if not a.no_cpu_baseline and ws == 1 and a.config == 3:
         cb = cpu_baseline(traces.config3(ticks=1, seed=3, n=a.entities, side=a.side), a.cpu_seconds)
         line["cpu_baseline"] = cb
     print(json.dumps(line), flush=True)

@@ -304,6 +304,8 @@ class HipRouter:
                 self.bufs.append(None)
 
     def route(self, words: torch.Tensor, stamps: torch.Tensor):
+        if not self.dsts:
+            return None, None            # a one-strip world has no neighbours
         self.g.route_halo(words.data_ptr(), stamps.data_ptr(), words.shape[0], float(self.geom.max_step),
                           self.dsts)
         return self.bufs[0], self.bufs[1]

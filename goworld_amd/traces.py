@@ -116,15 +116,19 @@ def dyadic_walk_trace(seed: int, n: int, side: float, d: float, ticks: int,
                       move_frac: float = 0.10, step_q: int = 512,
                       hot_frac: float = 0.0, n_hot: int = 64, sigma: float = 200.0,
                       hot_step_q: int = 2048, gate_count: int = 1,
-                      client_frac: float = 1.0, capacity: int | None = None) -> SpaceTrace:
-    """Configs #2/#3/#4/#5: uniform (+ optional Gaussian hotspots) on the 1/128 grid."""
-    assert side / 2 * Q < 2 ** 24, "dyadic exactness needs |x| < 2**17"
+                      client_frac: float = 1.0, capacity: int | None = None,
+                      side_z: float | None = None) -> SpaceTrace:
+    """Configs #2/#3/#4/#5: uniform (+ optional Gaussian hotspots) on the 1/128
+    grid, in [-side/2, side/2) x [-side_z/2, side_z/2) (side_z = side)."""
+    side_z = side if side_z is None else side_z
+    assert max(side, side_z) / 2 * Q <= 2 ** 24, "dyadic exactness needs |x| <= 2**17"
     half_q = int(side / 2 * Q)
     lo_q, hi_q = -half_q, half_q
+    zlo_q, zhi_q = -int(side_z / 2 * Q), int(side_z / 2 * Q)
     n_hot_ent = int(round(n * hot_frac))
     n_bg = n - n_hot_ent
     kx = rand_int(stream_key(seed, 1), n, lo_q, hi_q)
-    kz = rand_int(stream_key(seed, 2), n, lo_q, hi_q)
+    kz = rand_int(stream_key(seed, 2), n, zlo_q, zhi_q)
     if n_hot_ent:
         cx = rand_unit(stream_key(seed, 3), n_hot) * side - side / 2
         cz = rand_unit(stream_key(seed, 4), n_hot) * side - side / 2
@@ -138,7 +142,7 @@ def dyadic_walk_trace(seed: int, n: int, side: float, d: float, ticks: int,
         hx = np.round((cx[which] + sigma * gx) * Q).astype(np.int64)
         hz = np.round((cz[which] + sigma * gz) * Q).astype(np.int64)
         kx[n_bg:] = np.clip(hx, lo_q, hi_q - 1)
-        kz[n_bg:] = np.clip(hz, lo_q, hi_q - 1)
+        kz[n_bg:] = np.clip(hz, zlo_q, zhi_q - 1)
     is_hot = np.zeros(n, dtype=bool)
     is_hot[n_bg:] = True
     yaw = (rand_f32(stream_key(seed, 10), n) * np.float32(2 * math.pi)).astype(np.float32)
@@ -147,7 +151,7 @@ def dyadic_walk_trace(seed: int, n: int, side: float, d: float, ticks: int,
     init_x = (kx / Q).astype(np.float32)
     init_z = (kz / Q).astype(np.float32)
     tr = SpaceTrace(n=n, capacity=cap, d=float(d),
-                    bounds=(-side / 2, -side / 2, side / 2, side / 2),
+                    bounds=(-side / 2, -side_z / 2, side / 2, side_z / 2),
                     init_slots=slots, init_x=init_x, init_y=np.zeros(n, np.float32),
                     init_z=init_z, init_yaw=yaw, ticks=[])
     gates = np.zeros(cap, dtype=np.uint16)
@@ -162,7 +166,7 @@ def dyadic_walk_trace(seed: int, n: int, side: float, d: float, ticks: int,
         dx = (rand_unit(stream_key(seed, 101, t), m) * (2 * sq + 1)).astype(np.int64) - sq
         dz = (rand_unit(stream_key(seed, 102, t), m) * (2 * sq + 1)).astype(np.int64) - sq
         kx[movers] = _reflect_q(kx[movers] + dx, lo_q, hi_q)
-        kz[movers] = _reflect_q(kz[movers] + dz, lo_q, hi_q)
+        kz[movers] = _reflect_q(kz[movers] + dz, zlo_q, zhi_q)
         yaw[movers] = rand_f32(stream_key(seed, 103, t), m) * np.float32(2 * math.pi)
         from_client = rand_unit(stream_key(seed, 104, t), m) < 0.5
         ops = make_ops(m)
@@ -188,6 +192,16 @@ def config3(ticks: int = 20, seed: int = 3, n: int = 1_000_000, side: float = 32
     hotspot movers step +-16, others +-4; 10% movers."""
     return dyadic_walk_trace(seed, n, side, 100.0, ticks, 0.10, 512,
                              hot_frac=0.30, n_hot=64, sigma=200.0, hot_step_q=2048)
+
+
+def config5_strip(rank: int, ranks: int, ticks: int = 20, seed: int = 5,
+                  n_world: int = 16_000_000, side: float = 131072.0) -> SpaceTrace:
+    """#5: the 16M uniform world (L = 131072, d = 100, 10% movers, step +-4)
+    cut into `ranks` X-strips; strip `rank`'s population (n_world / ranks
+    entities, uniform in the strip, centred at x = 0: shift by the strip's
+    centre).  Walkers reflect at the strip borders."""
+    return dyadic_walk_trace(seed * 1000 + rank, n_world // ranks, side / ranks, 100.0, ticks, 0.10, 512,
+                             side_z=side)
 
 
 def config4_space(space: int, ticks: int = 20, seed: int = 4, n: int = 1000) -> SpaceTrace:

@@ -72,11 +72,11 @@ __device__ __forceinline__ void tile_excl_scan_striped(T (&v)[IPT], T* lds, T& t
     constexpr int Q = P / 64;                 // partials per lane
     static_assert(P % 64 == 0, "whole partials per lane");
     const int w = (int)(threadIdx.x >> 6), ln = lane_id();
-    T inc[IPT];
 #pragma unroll
-    for (int j = 0; j < IPT; ++j) {
-        inc[j] = wave_incl_scan(v[j]);
-        if (ln == 63) lds[j * NWAVE + w] = inc[j];
+    for (int j = 0; j < IPT; ++j) {             // v[j] becomes the in-wave exclusive prefix
+        const T inc = wave_incl_scan(v[j]);
+        if (ln == 63) lds[j * NWAVE + w] = inc;
+        v[j] = inc - v[j];
     }
     __syncthreads();
     // lane k holds partials k*Q .. k*Q+Q-1 (row-major: j * NWAVE + w)
@@ -94,7 +94,7 @@ __device__ __forceinline__ void tile_excl_scan_striped(T (&v)[IPT], T* lds, T& t
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
         const int idx = j * NWAVE + w;            // wave-uniform
-        v[j] = __shfl(q[idx % Q], idx / Q, 64) + inc[j] - v[j];
+        v[j] += __shfl(q[idx % Q], idx / Q, 64);
     }
     __syncthreads();
 }

@@ -52,7 +52,9 @@ def parse():
     ap.add_argument("--side", type=float, default=32768.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
-    ap.add_argument("--profile-stages", type=int, default=1, help="HIP-event stage timing in the timed region")
+    ap.add_argument("--profile-stages", type=int, default=1,
+                    help="1: HIP events around the dominant kernel's stage in the timed region (roofline) and "
+                         "a per-stage breakdown over extra untimed steps; 0: none")
     ap.add_argument("--mode", choices=["world", "spaces"], default="world", help="N>1 regime")
     ap.add_argument("--config", type=int, choices=[3, 5], default=3,
                     help="3: config #3 per GPU (weak); 5: the 16M uniform world of config #5 over N strips (strong)")
@@ -168,8 +170,9 @@ class SpaceRun:
     def step(self, t):
         g = self.g
         g.submit_device(self.dev_ops + t * self.nbytes_tick, self.m)
-        r = g.tick(copy=False)
+        g.tick(copy=False, defer=True)       # no host sync: the collect's sync settles it
         s = g.sync_collect(copy=False)
+        r = g.tick_result()
         return r.movers, r, s
 
     def close(self):
@@ -226,9 +229,9 @@ class WorldRun:
         self.tr = tr
 
     def step(self, t):
-        r = self.sr.step(self.words[t], copy=False)
+        self.sr.step(self.words[t], copy=False, defer=True)
         s = self.sr.collect(copy=False)
-        return self.m, r, s
+        return self.m, self.sr.e.tick_result(), s
 
     def close(self):
         self.sr.check()
@@ -239,7 +242,8 @@ def main():
     a = parse()
     ctl = Ctl(a)
     ws, rank = ctl.ws, ctl.rank
-    ticks = a.warmup + a.steps
+    extra = 5 if a.profile_stages else 0         # untimed steps for the per-stage breakdown
+    ticks = a.warmup + a.steps + extra
     t_load = time.perf_counter()
     world = (ws > 1 and a.mode == "world") or a.config == 5
     run = WorldRun(a, ctl, ticks) if world else SpaceRun(a, ctl, ticks)
@@ -249,22 +253,20 @@ def main():
     stage_us, stage_bytes, stage_n = {}, {}, {}
 
     def acc_stages():
-        for name, us, b in g.stage_times():
+        for name, us, b, calls in g.stage_times():
             stage_us[name] = stage_us.get(name, 0.0) + us
             stage_bytes[name] = stage_bytes.get(name, 0) + b
-            stage_n[name] = stage_n.get(name, 0) + 1
+            stage_n[name] = stage_n.get(name, 0) + calls
 
     for t in range(a.warmup):
         run.step(t)
-    g.set_profiling(bool(a.profile_stages))
+    g.set_profiling(2 if a.profile_stages else 0)    # the dominant kernel's stage only
     tot = dict(ops=0, events=0, records=0, bytes_alg=0)
     ctl.barrier()
     g.synchronize()
     t0 = time.perf_counter()
-    for t in range(a.warmup, ticks):
+    for t in range(a.warmup, a.warmup + a.steps):
         upd, r, s = run.step(t)
-        if a.profile_stages:
-            acc_stages()          # tick + collect stages; the collect already synced the stream
         tot["ops"] += upd
         tot["events"] += r.n_enter + r.n_leave
         tot["records"] += s.n_rec
@@ -273,6 +275,18 @@ def main():
     t1 = time.perf_counter()
     ctl.barrier()
     elapsed = t1 - t0
+    dom_us = dom_bytes = None
+    if a.profile_stages:
+        # HIP events recorded live around the dominant kernel in the timed region, read back here
+        for name, us, b, calls in g.stage_times():
+            if name == "diff":
+                dom_us, dom_bytes = us / calls, b / calls
+        # per-stage breakdown: every stage timed over a few more (untimed) steps
+        g.set_profiling(1)
+        for t in range(a.warmup + a.steps, ticks):
+            run.step(t)
+        acc_stages()
+        g.set_profiling(0)
     mx = ctl.reduce([elapsed], "MAX")[0]
     sums = ctl.reduce([tot["ops"], tot["events"], tot["records"]], "SUM")
     if rank != 0:
@@ -313,7 +327,7 @@ def main():
                    "parallelism": run.parallelism},
         "events_per_sec": sums[1] / mx,
         "records_per_sec": sums[2] / mx,
-        "device_us_per_step": (sum(stage_us.values()) / K) if stage_us else None,
+        "device_us_per_step": (sum(stage_us.values()) / extra) if stage_us else None,
         "bytes_alg_per_step": tot["bytes_alg"] / K,
         "tick_hbm_frac": (tot["bytes_alg"] / K) / (mx / K) / (HBM_PEAK_GBS * 1e9),
         "load_s": t_load,
@@ -324,12 +338,13 @@ def main():
         # the dominant kernel: k_mover, alone in stage "diff" (16 B per candidate tested + 4 B per
         # own event), timed by HIP events on the library's stream
         dom = "diff"
-        ach = stages[dom]["bytes_alg"] / (stages[dom]["avg_us"] * 1e-6) / 1e9
+        ach = dom_bytes / (dom_us * 1e-6) / 1e9
         traffic, src = pmc_traffic(STAGE_KERNEL[dom])
         line["roofline"] = {"bound": "hbm", "kernel": STAGE_KERNEL[dom], "achieved": ach, "peak": HBM_PEAK_GBS,
                             "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                             "traffic_unit": "bytes/launch", "traffic_source": src,
-                            "bytes_alg_per_launch": stages[dom]["bytes_alg"], "avg_us": stages[dom]["avg_us"]}
+                            "bytes_alg_per_launch": dom_bytes, "avg_us": dom_us,
+                            "timing": "HIP events around the kernel on its stream, every timed step"}
         line["stages"] = {n: {"avg_us": round(v["avg_us"], 2), "GBps_alg": round(
             v["bytes_alg"] / max(v["avg_us"], 1e-9) / 1e3, 1)} for n, v in stages.items()}
     else:

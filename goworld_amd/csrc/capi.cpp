@@ -97,8 +97,20 @@ struct gw_ctx {
     SpaceP* sp_dev = nullptr;
     uint32_t sp_cap = 0;
 
-    DevStats* stats = nullptr;     // device
+    DevStats* stats = nullptr;     // device (grid rebuild, tick)
     DevStats* hstats = nullptr;    // pinned host
+    DevStats* cstats = nullptr;    // device (collect: a deferred tick's stats stay intact)
+    DevStats* hcstats = nullptr;   // pinned host
+
+    // a tick launched but not read back yet (GW_TICK_DEFER): settled by the
+    // next call that needs its results (the collect's one sync covers it)
+    struct Pending {
+        bool on = false, copied = false;
+        uint32_t M = 0, C = 0, NC = 0, flags = 0;
+        size_t s_grid = 0, s_movers = 0, s_diff = 0, s_events = 0;
+        TickBufs b{};
+    } pt;
+    gw_tick_out last_out{};
 
     // grid + tick scratch
     DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, cand, reg, own, big, bigseg;
@@ -124,12 +136,15 @@ struct gw_ctx {
     std::vector<uint64_t> gate_off;
 
     // profiling
-    bool prof = false;
+    int prof = 0;                      // 0 off, 1 every stage, 2 the "diff" stage only
+    bool prof_cur = false;             // the stage being recorded is on
     std::vector<Stage> stages;
     size_t nstage = 0;
     hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
     gw_stage_times last_times{};
 };
+
+static int settle(gw_ctx* c);   // finish a deferred tick (GW_TICK_DEFER)
 
 namespace {
 
@@ -217,8 +232,14 @@ int ceil_log2(uint64_t v) {   // bits needed to represent values in [0, v)
 // ---- profiling ------------------------------------------------------------
 // Stage events accumulate over calls until gw_get_stage_times reads them
 // (after the caller's own sync), so timing adds no host sync to a tick.
+constexpr size_t PROF_MAX_RECORDS = 1 << 16;   // stage records kept between collections
+// prof: 0 off, 1 every stage, 2 only the dominant kernel's stage ("diff")
+static bool prof_on(const gw_ctx* c, const char* name) {
+    return c->prof == 1 || (c->prof == 2 && strcmp(name, "diff") == 0);
+}
 void prof_begin(gw_ctx* c, const char* name) {
-    if (!c->prof || c->nstage >= GW_MAX_STAGES) return;
+    c->prof_cur = prof_on(c, name);
+    if (!c->prof_cur || c->nstage >= PROF_MAX_RECORDS) return;
     if (c->nstage >= c->stages.size()) {
         Stage s{};
         (void)hipEventCreate(&s.a);
@@ -231,7 +252,7 @@ void prof_begin(gw_ctx* c, const char* name) {
     (void)hipEventRecord(s.a, c->st);
 }
 size_t prof_end(gw_ctx* c, uint64_t bytes) {
-    if (!c->prof || c->nstage >= GW_MAX_STAGES) return GW_MAX_STAGES;
+    if (!c->prof_cur || c->nstage >= PROF_MAX_RECORDS) return PROF_MAX_RECORDS;
     Stage& s = c->stages[c->nstage];
     s.bytes = bytes;
     (void)hipEventRecord(s.b, c->st);
@@ -240,17 +261,24 @@ size_t prof_end(gw_ctx* c, uint64_t bytes) {
 void prof_set_bytes(gw_ctx* c, size_t idx, uint64_t bytes) {
     if (c->prof && idx < c->stages.size()) c->stages[idx].bytes = bytes;
 }
+// every recorded stage since the last collection, summed per stage name
+// (one host sync and the event queries happen here, outside any timed loop)
 void prof_collect(gw_ctx* c) {
     gw_stage_times& t = c->last_times;
-    t.n = 0;
+    memset(&t, 0, sizeof t);
     if (c->nstage) (void)hipEventSynchronize(c->stages[c->nstage - 1].b);
-    for (size_t i = 0; i < c->nstage && i < GW_MAX_STAGES; ++i) {
+    for (size_t i = 0; i < c->nstage; ++i) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, c->stages[i].a, c->stages[i].b);
-        t.name[t.n] = c->stages[i].name;
-        t.us[t.n] = ms * 1000.0;
-        t.bytes_alg[t.n] = c->stages[i].bytes;
-        t.n++;
+        uint32_t k = 0;
+        while (k < t.n && strcmp(t.name[k], c->stages[i].name) != 0) ++k;
+        if (k == t.n) {
+            if (t.n == GW_MAX_STAGES) continue;
+            t.name[t.n++] = c->stages[i].name;
+        }
+        t.us[k] += ms * 1000.0;
+        t.bytes_alg[k] += c->stages[i].bytes;
+        t.calls[k] += 1;
     }
     c->nstage = 0;
 }
@@ -352,6 +380,12 @@ int upload_spaces(gw_ctx* c) {
 
 int read_stats(gw_ctx* c) {
     HIPCHK(hipMemcpyAsync(c->hstats, c->stats, sizeof(DevStats), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int read_cstats(gw_ctx* c) {
+    HIPCHK(hipMemcpyAsync(c->hcstats, c->cstats, sizeof(DevStats), hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
 }
@@ -494,6 +528,8 @@ int gw_init(int device_id, gw_ctx** out) {
         c->st = c->own_st;
         if (hipMalloc(&c->stats, sizeof(DevStats)) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "stats"); break; }
         if (hipHostMalloc((void**)&c->hstats, sizeof(DevStats), hipHostMallocDefault) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "hstats"); break; }
+        if (hipMalloc(&c->cstats, sizeof(DevStats)) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "cstats"); break; }
+        if (hipHostMalloc((void**)&c->hcstats, sizeof(DevStats), hipHostMallocDefault) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "hcstats"); break; }
         if (hipMalloc(&c->scal32, 64) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "scal"); break; }
         if (hipMalloc(&c->halo, sizeof(HaloStats)) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "halo"); break; }
         (void)hipMemset(c->halo, 0, sizeof(HaloStats));
@@ -518,6 +554,7 @@ int gw_init(int device_id, gw_ctx** out) {
 
 void gw_shutdown(gw_ctx* c) {
     if (!c) return;
+    (void)settle(c);
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
     DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->k0, &c->v0, &c->k1, &c->v1, &c->bigseg,
@@ -530,10 +567,11 @@ void gw_shutdown(gw_ctx* c) {
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
     void* ps[] = {c->halo, c->rflag, c->sc.ticket, c->ownbits, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->nbc, c->last_pos, c->last_aoi,
-                  c->last_leave, c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->scal32, c->gsb[0],
+                  c->last_leave, c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->cstats, c->scal32, c->gsb[0],
                   c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->bigcell, c->gm_start};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
+    if (c->hcstats) (void)hipHostFree(c->hcstats);
     for (auto& s : c->stages) { (void)hipEventDestroy(s.a); (void)hipEventDestroy(s.b); }
     if (c->ev_t0) (void)hipEventDestroy(c->ev_t0);
     if (c->ev_t1) (void)hipEventDestroy(c->ev_t1);
@@ -544,6 +582,7 @@ void gw_shutdown(gw_ctx* c) {
 int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* bounds, uint32_t* space_id,
                     uint32_t* slot_base) {
     if (!c) return GW_EINVAL;
+    if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
     if (!(aoi_dist > 0) || !std::isfinite(aoi_dist))
         return set_err(c, GW_EINVAL, "defaultAOIDistance <= 0");          // Space.go:92-94
@@ -598,6 +637,7 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
 
 int gw_space_destroy(gw_ctx* c, uint32_t sid) {
     if (!c) return GW_EINVAL;
+    if (int rs = settle(c)) return rs;
     if (sid >= c->spaces.size() || !c->spaces[sid].alive) return set_err(c, GW_ERANGE, "no space %u", sid);
     SpaceHost& s = c->spaces[sid];
     if (c->validate) {
@@ -650,6 +690,7 @@ int gw_route_halo(gw_ctx* c, const gw_op* dev_ops, const uint64_t* dev_stamps, u
                   const gw_halo_dst* dsts, uint32_t n_dst) {
     if (!c || (n && (!dev_ops || !dev_stamps)) || (n_dst && !dsts)) return GW_EINVAL;
     if (n_dst > 2) return set_err(c, GW_EINVAL, "at most 2 halo destinations");
+    if (int rs = settle(c)) return rs;
     if (!(max_step >= 0)) return set_err(c, GW_EINVAL, "max_step must be >= 0");
     (void)hipSetDevice(c->dev);
     HaloDsts D{};
@@ -670,6 +711,7 @@ int gw_route_halo(gw_ctx* c, const gw_op* dev_ops, const uint64_t* dev_stamps, u
 
 int gw_halo_status(gw_ctx* c, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops) {
     if (!c) return GW_EINVAL;
+    if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
     HaloStats h{};
     HIPCHK(hipMemcpyAsync(&h, c->halo, sizeof h, hipMemcpyDeviceToHost, c->st));
@@ -683,6 +725,7 @@ int gw_halo_status(gw_ctx* c, uint64_t* overflow, uint64_t* bad_moves, uint64_t*
 
 int gw_space_set_ownership(gw_ctx* c, uint32_t sid, float x_lo, float x_hi) {
     if (!c) return GW_EINVAL;
+    if (int rs = settle(c)) return rs;
     if (sid >= c->spaces.size() || !c->spaces[sid].alive) return set_err(c, GW_ERANGE, "no space %u", sid);
     if (!(x_lo < x_hi)) return set_err(c, GW_EINVAL, "empty ownership range");
     c->spaces[sid].p.own_lo = x_lo;
@@ -693,6 +736,7 @@ int gw_space_set_ownership(gw_ctx* c, uint32_t sid, float x_lo, float x_hi) {
 int gw_set_clients(gw_ctx* c, const uint32_t* slots, const uint16_t* gates, uint32_t n) {
     if (!c || (n && (!slots || !gates))) return GW_EINVAL;
     if (!n) return 0;
+    if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
     for (uint32_t i = 0; i < n; ++i) {
         if (slots[i] >= c->total_slots) return set_err(c, GW_ERANGE, "slot %u out of range", slots[i]);
@@ -710,10 +754,139 @@ int gw_set_clients(gw_ctx* c, const uint32_t* slots, const uint16_t* gates, uint
     return 0;
 }
 
+static int ensure_events(gw_ctx* c) {
+    int r;
+    if ((r = ensure(c, c->own, c->own_cap * 4)) || (r = ensure(c, c->mir, c->own_cap * 8)) ||
+        (r = ensure(c, c->enter_d, 2 * c->own_cap * sizeof(gw_event))) ||
+        (r = ensure(c, c->leave_d, 2 * c->own_cap * sizeof(gw_event))))
+        return r;
+    return 0;
+}
+
+static void bind_events(gw_ctx* c, TickBufs& b) {
+    b.own_cap = c->own_cap;
+    b.own = P<uint32_t>(c->own); b.mir = P<uint64_t>(c->mir);
+    b.enter = P<gw_event>(c->enter_d); b.leave = P<gw_event>(c->leave_d);
+    b.ev_cap = 2 * c->own_cap;
+}
+
+// Second half of a tick: read the statistics (one host sync, or none when a
+// collect has just synced the stream), redo diff + events if the own-event
+// regions overflowed, reset the per-op state, fill the outputs.
+static int finish_tick(gw_ctx* c, gw_tick_out* out) {
+    auto& p = c->pt;
+    if (!p.on) {
+        if (out) *out = c->last_out;
+        return 0;
+    }
+    p.on = false;
+    (void)hipSetDevice(c->dev);
+    TickBufs b = p.b;
+    const uint32_t M = p.M, C = p.C, NC = p.NC, flags = p.flags;
+    size_t s_grid = p.s_grid, s_movers = p.s_movers, s_diff = p.s_diff, s_events = p.s_events;
+    int rc;
+    if (p.copied) HIPCHK(hipStreamSynchronize(c->st));
+    else if ((rc = read_stats(c))) return rc;
+    if (c->hstats->overflow) {
+        // the own-event regions did not fit: grow to the exact bound, clear the
+        // per-watcher counters and rerun diff + events (their inputs are intact)
+        c->own_cap = c->hstats->cand_total + c->hstats->cand_total / 4 + 4096;
+        if ((rc = ensure_events(c))) return rc;
+        bind_events(c, b);
+        HIPCHK(hipMemsetAsync(c->cnt64, 0, ((size_t)C + 1) * 8, c->st));
+        HIPCHK(hipMemsetAsync(c->ownbits, 0, ((size_t)C / 32 + 1) * 4, c->st));
+        DevStats* h = c->hstats;
+        h->overflow = 0; h->n_big = 0; h->n_bigseg = 0; h->ev_pk = 0;
+        memset(h->shard, 0, sizeof h->shard);
+        HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
+        prof_begin(c, "diff");
+        tick_diff(b, c->st);
+        s_diff = prof_end(c, 0);
+        prof_begin(c, "events");
+        tick_events(b, c->sc, c->st);
+        s_events = prof_end(c, 0);
+        HIPCHK(hipGetLastError());
+        if ((rc = read_stats(c))) return rc;
+        if (c->hstats->overflow) return set_err(c, GW_ENOMEM, "event regions overflowed twice");
+    }
+    prof_begin(c, "reset");
+    tick_reset(b, c->st);                            // asynchronous: the next call orders behind it
+    prof_end(c, (uint64_t)M * 24);
+    HIPCHK(hipEventRecord(c->ev_t1, c->st));
+    HIPCHK(hipGetLastError());
+    DevStats& hs = *c->hstats;
+    c->h_present = hs.n_present;
+    gw_tick_out o{};
+    const uint64_t n_enter = hs.ev_pk & 0xffffffffull, n_leave = hs.ev_pk >> 32;
+    const uint64_t n_mov = hs.n_movers;
+    // candidates tested == the candidate bounds; a_old | a_new << 32 per shard
+    const uint64_t pairs = hs.cand_total;
+    uint64_t a_old = 0, a_new = 0;
+    for (int i = 0; i < STAT_SHARDS; ++i) {
+        a_old += hs.shard[i][SH_AOLD] & 0xffffffffull;
+        a_new += hs.shard[i][SH_AOLD] >> 32;
+    }
+    if (getenv("GW_DEBUG_STATS")) {
+        unsigned long long f0 = 0, f2 = 0;
+        for (int i = 0; i < STAT_SHARDS; ++i) { f0 += hs.shard[i][0]; f2 += hs.shard[i][2]; }
+        fprintf(stderr, "gw_tick: movers %llu gm %llu cand %llu ev %llu+%llu big %llu bigseg %llu bigcell %llu "
+                "seg_lane %llu seg_wave %llu\n", hs.n_movers, hs.n_gm, hs.cand_total, hs.ev_pk & 0xffffffffull,
+                hs.ev_pk >> 32, hs.n_big, hs.n_bigseg, hs.n_bigcell, f0, f2);
+    }
+    o.ops = M;
+    o.movers = n_mov;
+    o.pairs_tested = pairs;
+    o.nbr_old = a_old;
+    o.nbr_new = a_new;
+    o.enter_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->enter_d);
+    o.leave_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->leave_d);
+    o.n_enter = n_enter;
+    o.n_leave = n_leave;
+    // SURVEY 8(d) algorithmic bytes of the AOI part (records are counted by gw_sync_collect)
+    const uint64_t n_evt = n_enter + n_leave;
+    o.bytes_alg = 20ull * n_mov + 8ull * hs.n_present + 4ull * (a_old + a_new) + 8ull * n_evt;
+    if (c->prof) {
+        // grid: entries moved (16 B read + 16 B written + 4 B index) + per-cell counts (16 B)
+        prof_set_bytes(c, s_grid, 36ull * hs.n_present + 16ull * NC);
+        prof_set_bytes(c, s_movers, 40ull * hs.n_gm);
+        // diff: candidates (16 B grid / 32 B mover grid; counted at 16 B) + own events (4 B)
+        prof_set_bytes(c, s_diff, 16ull * pairs + 4ull * n_evt);
+        // events: per-watcher counts and offsets (16 B per slot) + events (8 B) + own copies (4 B)
+        prof_set_bytes(c, s_events, 16ull * (C + 1) + 12ull * n_evt);
+    }
+    if ((flags & GW_TICK_COPY_TO_HOST) && !(flags & GW_TICK_NO_EVENTS)) {
+        if ((rc = ensure_host(c, c->h_enter, std::max<uint64_t>(n_enter, 1) * sizeof(gw_event)))) return rc;
+        if ((rc = ensure_host(c, c->h_leave, std::max<uint64_t>(n_leave, 1) * sizeof(gw_event)))) return rc;
+        if (n_enter) HIPCHK(hipMemcpyAsync(c->h_enter.p, c->enter_d.p, n_enter * sizeof(gw_event), hipMemcpyDeviceToHost, c->st));
+        if (n_leave) HIPCHK(hipMemcpyAsync(c->h_leave.p, c->leave_d.p, n_leave * sizeof(gw_event), hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        o.enter = (const gw_event*)c->h_enter.p;
+        o.leave = (const gw_event*)c->h_leave.p;
+    }
+    float ms = 0;
+    if (flags & GW_TICK_COPY_TO_HOST) {                // synced above: the span is known
+        HIPCHK(hipEventSynchronize(c->ev_t1));
+        (void)hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1);
+    }
+    o.device_us = ms * 1000.0;
+    c->last_out = o;
+    if (out) *out = o;
+    if (hs.bad_ops) return set_err(c, GW_EINVAL, "%llu ops with bad slot/kind (ignored)", hs.bad_ops);
+    return 0;
+}
+
+static int settle(gw_ctx* c) { return finish_tick(c, nullptr); }
+
+
+
 int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     if (!c || !out) return GW_EINVAL;
     (void)hipSetDevice(c->dev);
     memset(out, 0, sizeof *out);
+    int rc0 = settle(c);                             // a deferred tick before this one
+    if (rc0) return rc0;
+    bool host_ops = false;                           // pageable host ops: no deferral
+    for (auto& sg : c->segs) host_ops |= sg.host;
     uint64_t M64 = 0;
     for (auto& s : c->segs) M64 += s.n;
     if (M64 >= (1ull << 30)) return set_err(c, GW_ERANGE, "too many ops in one tick");
@@ -777,15 +950,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         (rc = ensure(c, c->off64, ((size_t)C + 2) * 8)) ||
         (rc = ensure_scan(c, std::max<uint64_t>(std::max<uint64_t>(M2, (uint64_t)C + 1), (uint64_t)NC + 1))))
         return rc;
-    auto ensure_events = [&]() -> int {
-        int r;
-        if ((r = ensure(c, c->own, c->own_cap * 4)) || (r = ensure(c, c->mir, c->own_cap * 8)) ||
-            (r = ensure(c, c->enter_d, 2 * c->own_cap * sizeof(gw_event))) ||
-            (r = ensure(c, c->leave_d, 2 * c->own_cap * sizeof(gw_event))))
-            return r;
-        return 0;
-    };
-    if ((rc = ensure_events())) return rc;
+    if ((rc = ensure_events(c))) return rc;
     reset_stats_host(c);
     HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
     DevStats* st = c->stats;
@@ -805,13 +970,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.bigseg = P<uint32_t>(c->bigseg);
     b.ownbits = c->ownbits;
     b.cnt64 = c->cnt64; b.off64 = P<uint64_t>(c->off64);
-    auto bind_events = [&]() {
-        b.own_cap = c->own_cap;
-        b.own = P<uint32_t>(c->own); b.mir = P<uint64_t>(c->mir);
-        b.enter = P<gw_event>(c->enter_d); b.leave = P<gw_event>(c->leave_d);
-        b.ev_cap = 2 * c->own_cap;
-    };
-    bind_events();
+    bind_events(c, b);
 
     prof_begin(c, "ops");
     tick_ops(b, c->st);
@@ -833,95 +992,23 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     tick_events(b, c->sc, c->st);
     size_t s_events = prof_end(c, 0);
     HIPCHK(hipGetLastError());
-    // ---- the one host sync --------------------------------------------------
-    if ((rc = read_stats(c))) return rc;
-    if (c->hstats->overflow) {
-        // the own-event regions did not fit: grow to the exact bound, clear the
-        // per-watcher counters and rerun diff + events (their inputs are intact)
-        c->own_cap = c->hstats->cand_total + c->hstats->cand_total / 4 + 4096;
-        if ((rc = ensure_events())) return rc;
-        bind_events();
-        HIPCHK(hipMemsetAsync(c->cnt64, 0, ((size_t)C + 1) * 8, c->st));
-        HIPCHK(hipMemsetAsync(c->ownbits, 0, ((size_t)C / 32 + 1) * 4, c->st));
-        DevStats* h = c->hstats;
-        h->overflow = 0; h->n_big = 0; h->n_bigseg = 0; h->ev_pk = 0;
-        memset(h->shard, 0, sizeof h->shard);
-        HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
-        if (s_diff < GW_MAX_STAGES) c->nstage = s_diff;
-        prof_begin(c, "diff");
-        tick_diff(b, c->st);
-        s_diff = prof_end(c, 0);
-        prof_begin(c, "events");
-        tick_events(b, c->sc, c->st);
-        s_events = prof_end(c, 0);
-        HIPCHK(hipGetLastError());
-        if ((rc = read_stats(c))) return rc;
-        if (c->hstats->overflow) return set_err(c, GW_ENOMEM, "event regions overflowed twice");
-    }
-    prof_begin(c, "reset");
-    tick_reset(b, c->st);                            // asynchronous: the next call orders behind it
-    prof_end(c, (uint64_t)M * 24);
-    HIPCHK(hipEventRecord(c->ev_t1, c->st));
-    HIPCHK(hipGetLastError());
-    DevStats& hs = *c->hstats;
     c->segs.clear();
     c->pend_host.clear();
     c->stamp_base += M;
-    c->h_present = hs.n_present;
-    if (hs.bad_ops) return set_err(c, GW_EINVAL, "%llu ops with bad slot/kind (ignored)", hs.bad_ops);
-    const uint64_t n_enter = hs.ev_pk & 0xffffffffull, n_leave = hs.ev_pk >> 32;
-    const uint64_t n_mov = hs.n_movers;
-    // candidates tested == the candidate bounds; a_old | a_new << 32 per shard
-    const uint64_t pairs = hs.cand_total;
-    uint64_t a_old = 0, a_new = 0;
-    for (int i = 0; i < STAT_SHARDS; ++i) {
-        a_old += hs.shard[i][SH_AOLD] & 0xffffffffull;
-        a_new += hs.shard[i][SH_AOLD] >> 32;
+    auto& p = c->pt;
+    p.on = true;
+    p.copied = false;
+    p.M = M; p.C = C; p.NC = NC; p.flags = flags;
+    p.s_grid = s_grid; p.s_movers = s_movers; p.s_diff = s_diff; p.s_events = s_events;
+    p.b = b;
+    if ((flags & GW_TICK_DEFER) && !(flags & GW_TICK_COPY_TO_HOST) && !host_ops) {
+        // no host sync now: the next call that needs the results settles it
+        HIPCHK(hipMemcpyAsync(c->hstats, c->stats, sizeof(DevStats), hipMemcpyDeviceToHost, c->st));
+        p.copied = true;
+        out->ops = M;
+        return 0;
     }
-    if (getenv("GW_DEBUG_STATS")) {
-        unsigned long long f0 = 0, f2 = 0;
-        for (int i = 0; i < STAT_SHARDS; ++i) { f0 += hs.shard[i][0]; f2 += hs.shard[i][2]; }
-        fprintf(stderr, "gw_tick: movers %llu gm %llu cand %llu ev %llu+%llu big %llu bigseg %llu bigcell %llu "
-                "seg_lane %llu seg_wave %llu\n", hs.n_movers, hs.n_gm, hs.cand_total, hs.ev_pk & 0xffffffffull,
-                hs.ev_pk >> 32, hs.n_big, hs.n_bigseg, hs.n_bigcell, f0, f2);
-    }
-    out->ops = M;
-    out->movers = n_mov;
-    out->pairs_tested = pairs;
-    out->nbr_old = a_old;
-    out->nbr_new = a_new;
-    out->enter_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->enter_d);
-    out->leave_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->leave_d);
-    out->n_enter = n_enter;
-    out->n_leave = n_leave;
-    // SURVEY 8(d) algorithmic bytes of the AOI part (records are counted by gw_sync_collect)
-    const uint64_t n_evt = n_enter + n_leave;
-    out->bytes_alg = 20ull * n_mov + 8ull * hs.n_present + 4ull * (a_old + a_new) + 8ull * n_evt;
-    if (c->prof) {
-        // grid: entries moved (16 B read + 16 B written + 4 B index) + per-cell counts (16 B)
-        prof_set_bytes(c, s_grid, 36ull * hs.n_present + 16ull * NC);
-        prof_set_bytes(c, s_movers, 40ull * hs.n_gm);
-        // diff: candidates (16 B grid / 32 B mover grid; counted at 16 B) + own events (4 B)
-        prof_set_bytes(c, s_diff, 16ull * pairs + 4ull * n_evt);
-        // events: per-watcher counts and offsets (16 B per slot) + events (8 B) + own copies (4 B)
-        prof_set_bytes(c, s_events, 16ull * (C + 1) + 12ull * n_evt);
-    }
-    if ((flags & GW_TICK_COPY_TO_HOST) && !(flags & GW_TICK_NO_EVENTS)) {
-        if ((rc = ensure_host(c, c->h_enter, std::max<uint64_t>(n_enter, 1) * sizeof(gw_event)))) return rc;
-        if ((rc = ensure_host(c, c->h_leave, std::max<uint64_t>(n_leave, 1) * sizeof(gw_event)))) return rc;
-        if (n_enter) HIPCHK(hipMemcpyAsync(c->h_enter.p, c->enter_d.p, n_enter * sizeof(gw_event), hipMemcpyDeviceToHost, c->st));
-        if (n_leave) HIPCHK(hipMemcpyAsync(c->h_leave.p, c->leave_d.p, n_leave * sizeof(gw_event), hipMemcpyDeviceToHost, c->st));
-        HIPCHK(hipStreamSynchronize(c->st));
-        out->enter = (const gw_event*)c->h_enter.p;
-        out->leave = (const gw_event*)c->h_leave.p;
-    }
-    float ms = 0;
-    if (flags & GW_TICK_COPY_TO_HOST) {                // synced above: the span is known
-        HIPCHK(hipEventSynchronize(c->ev_t1));
-        (void)hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1);
-    }
-    out->device_us = ms * 1000.0;
-    return 0;
+    return finish_tick(c, out);
 }
 
 int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
@@ -938,10 +1025,11 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         out->n_gates = G;
         return 0;
     }
+    if (c->grid_dirty && (rc = settle(c))) return rc;
     if ((rc = rebuild_grid(c))) return rc;
-    reset_stats_host(c);
-    HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
-    DevStats* st = c->stats;
+    memset(c->hcstats, 0, sizeof(DevStats));
+    HIPCHK(hipMemcpyAsync(c->cstats, c->hcstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
+    DevStats* st = c->cstats;
     if ((rc = ensure(c, c->fbits, (size_t)C * 4)) || (rc = ensure(c, c->flagged, (size_t)C * 4)) ||
         (rc = ensure(c, c->rec_cnt, (size_t)C * 4)) || (rc = ensure(c, c->rec_off, (size_t)C * 8)) ||
         (rc = ensure_scan(c, C)))
@@ -966,19 +1054,20 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
                       P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
     size_t s_write = prof_end(c, 0);
     HIPCHK(hipGetLastError());
-    if ((rc = read_stats(c))) return rc;                 // the one host sync
-    const uint64_t R = c->hstats->rec_total;
-    const uint64_t NF = c->hstats->flagged;
-    if (c->hstats->overflow) {
+    if ((rc = read_cstats(c))) return rc;                // the one host sync
+    if ((rc = settle(c))) return rc;                     // a deferred tick: its stats came with it
+    const uint64_t R = c->hcstats->rec_total;
+    const uint64_t NF = c->hcstats->flagged;
+    if (c->hcstats->overflow) {
         c->rec_cap = R + R / 4 + 1024;
         if ((rc = ensure(c, c->rec0, c->rec_cap * sizeof(gw_sync_record)))) return rc;
-        c->hstats->overflow = 0;
-        HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
+        c->hcstats->overflow = 0;
+        HIPCHK(hipMemcpyAsync(c->cstats, c->hcstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
         launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint64_t>(c->rec_off),
                           P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
         HIPCHK(hipGetLastError());
-        if ((rc = read_stats(c))) return rc;
-        if (c->hstats->overflow) return set_err(c, GW_ENOMEM, "sync record buffer overflowed twice");
+        if ((rc = read_cstats(c))) return rc;
+        if (c->hcstats->overflow) return set_err(c, GW_ENOMEM, "sync record buffer overflowed twice");
     }
     gw_sync_record* recs = P<gw_sync_record>(c->rec0);
     // ---- per-gate grouping (stable, keeps the entity order) -------------
@@ -1040,6 +1129,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
 
 int gw_neighbors(gw_ctx* c, uint32_t slot, uint32_t* buf, uint32_t cap, uint32_t* n) {
     if (!c || !n) return GW_EINVAL;
+    if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
     if (slot >= c->total_slots) return set_err(c, GW_ERANGE, "slot %u out of range", slot);
     int rc;
@@ -1064,6 +1154,7 @@ int gw_neighbors(gw_ctx* c, uint32_t slot, uint32_t* buf, uint32_t cap, uint32_t
 
 int gw_total_neighbors(gw_ctx* c, uint64_t* out) {
     if (!c || !out) return GW_EINVAL;
+    if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
     *out = 0;
     if (!c->total_slots) return 0;
@@ -1081,7 +1172,7 @@ int gw_total_neighbors(gw_ctx* c, uint64_t* out) {
 
 int gw_set_profiling(gw_ctx* c, int enable) {
     if (!c) return GW_EINVAL;
-    c->prof = enable != 0;
+    c->prof = enable < 0 ? 0 : (enable > 2 ? 1 : enable);
     return 0;
 }
 
@@ -1118,14 +1209,22 @@ int gw_memcpy_d2h(gw_ctx* c, void* dst, const void* src, size_t bytes) {
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
 }
+int gw_tick_result(gw_ctx* c, gw_tick_out* out) {
+    if (!c || !out) return GW_EINVAL;
+    (void)hipSetDevice(c->dev);
+    return finish_tick(c, out);
+}
+
 int gw_synchronize(gw_ctx* c) {
     if (!c) return GW_EINVAL;
+    if (int rs = settle(c)) return rs;
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
 }
 
 int gw_set_stream(gw_ctx* c, void* stream) {
     if (!c) return GW_EINVAL;
+    if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
     HIPCHK(hipStreamSynchronize(c->st));
     c->st = stream ? (hipStream_t)stream : c->own_st;

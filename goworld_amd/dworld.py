@@ -373,13 +373,19 @@ class HipStrip:
         self._keep.append(rows)
         self.g.submit_device_rows(rows.data_ptr(), rows.shape[0])
 
-    def tick(self, copy=True, no_events=False):
-        res = self.g.tick(copy=copy, no_events=no_events)
-        self._keep = []
+    def tick(self, copy=True, no_events=False, defer=False):
+        res = self.g.tick(copy=copy, no_events=no_events, defer=defer)
+        if not defer or copy:
+            self._keep = []          # consumed (a deferred tick keeps them until its collect)
         return res
 
+    def tick_result(self):
+        return self.g.tick_result()
+
     def collect(self, copy=True):
-        return self.g.sync_collect(copy=copy)
+        res = self.g.sync_collect(copy=copy)     # settles a deferred tick
+        self._keep = []
+        return res
 
 
 class StripRank:

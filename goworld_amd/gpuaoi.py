@@ -30,7 +30,7 @@ EVENT_DTYPE = np.dtype([("watcher", "<u4"), ("target", "<u4")])
 REC_DTYPE = np.dtype([("watcher", "<u4"), ("entity", "<u4"), ("x", "<f4"), ("y", "<f4"),
                       ("z", "<f4"), ("yaw", "<f4")])
 
-TICK_COPY_TO_HOST, TICK_NO_EVENTS = 1, 2
+TICK_COPY_TO_HOST, TICK_NO_EVENTS, TICK_DEFER = 1, 2, 4
 SYNC_COPY_TO_HOST = 1
 MAX_STAGES = 32
 
@@ -52,7 +52,7 @@ class SyncOut(C.Structure):
 
 class StageTimes(C.Structure):
     _fields_ = [("n", _u32), ("name", C.c_char_p * MAX_STAGES), ("us", _f64 * MAX_STAGES),
-                ("bytes_alg", _u64 * MAX_STAGES)]
+                ("bytes_alg", _u64 * MAX_STAGES), ("calls", _u32 * MAX_STAGES)]
 
 
 class HaloDst(C.Structure):
@@ -90,6 +90,7 @@ def lib():
         L.gw_submit_device.argtypes = [vp, vp, _u32]
         L.gw_set_clients.argtypes = [vp, vp, vp, _u32]
         L.gw_tick.argtypes = [vp, _u32, C.POINTER(TickOut)]
+        L.gw_tick_result.argtypes = [vp, C.POINTER(TickOut)]
         L.gw_sync_collect.argtypes = [vp, _u32, C.POINTER(SyncOut)]
         L.gw_neighbors.argtypes = [vp, _u32, vp, _u32, C.POINTER(_u32)]
         L.gw_set_profiling.argtypes = [vp, C.c_int]
@@ -115,7 +116,7 @@ EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_spa
             "gw_sync_collect", "gw_neighbors", "gw_set_profiling", "gw_get_stage_times",
             "gw_total_neighbors", "gw_device_alloc", "gw_device_free", "gw_memcpy_h2d",
             "gw_memcpy_d2h", "gw_synchronize", "gw_submit_device_stamped", "gw_space_set_ownership",
-            "gw_set_stream", "gw_route_halo", "gw_submit_device_rows", "gw_halo_status"]
+            "gw_set_stream", "gw_route_halo", "gw_submit_device_rows", "gw_halo_status", "gw_tick_result"]
 
 
 def _p(a: np.ndarray):
@@ -233,10 +234,22 @@ class GpuAOI:
         g = np.ascontiguousarray(gates, dtype=np.uint16)
         self._chk(lib().gw_set_clients(self._h, _p(s), _p(g), len(s)))
 
-    def tick(self, copy: bool = True, no_events: bool = False) -> TickResult:
+    def tick(self, copy: bool = True, no_events: bool = False, defer: bool = False) -> TickResult:
+        """defer (device-resident ops, copy=False): launch without a host sync;
+        the result holds only `ops` until tick_result() (or the next collect)."""
         o = TickOut()
-        fl = (TICK_COPY_TO_HOST if copy else 0) | (TICK_NO_EVENTS if no_events else 0)
+        fl = (TICK_COPY_TO_HOST if copy else 0) | (TICK_NO_EVENTS if no_events else 0) | \
+            (TICK_DEFER if defer and not copy else 0)
         self._chk(lib().gw_tick(self._h, fl, C.byref(o)))
+        return self._tick_result(o, copy, no_events)
+
+    def tick_result(self) -> TickResult:
+        """Outputs of the last tick (settles a deferred tick)."""
+        o = TickOut()
+        self._chk(lib().gw_tick_result(self._h, C.byref(o)))
+        return self._tick_result(o, False, False)
+
+    def _tick_result(self, o, copy, no_events) -> TickResult:
         e = l = None
         if copy and not no_events:
             e = np.zeros(o.n_enter, EVENT_DTYPE)
@@ -272,13 +285,16 @@ class GpuAOI:
         self._chk(lib().gw_total_neighbors(self._h, C.byref(v)))
         return v.value
 
-    def set_profiling(self, on: bool):
-        self._chk(lib().gw_set_profiling(self._h, 1 if on else 0))
+    def set_profiling(self, mode):
+        """0 / False off, 1 / True every stage, 2 only the dominant kernel's stage ("diff")."""
+        self._chk(lib().gw_set_profiling(self._h, int(mode)))
 
-    def stage_times(self) -> list[tuple[str, float, int]]:
+    def stage_times(self) -> list[tuple[str, float, int, int]]:
+        """(stage, total us, total algorithmic bytes, calls) over every stage
+        recorded since the last call (one host sync, here)."""
         t = StageTimes()
         self._chk(lib().gw_get_stage_times(self._h, C.byref(t)))
-        return [(t.name[i].decode(), t.us[i], t.bytes_alg[i]) for i in range(t.n)]
+        return [(t.name[i].decode(), t.us[i], t.bytes_alg[i], t.calls[i]) for i in range(t.n)]
 
     # device memory helpers (bench: inputs resident in HBM)
     def dev_alloc(self, nbytes: int) -> int:

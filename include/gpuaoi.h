@@ -105,6 +105,12 @@ typedef struct gw_sync_record {
 #define GW_TICK_COPY_TO_HOST   1u  /* also copy events into pinned host buffers */
 #define GW_TICK_NO_EVENTS      2u  /* update neighbour state only (restore/bulk
                                       path, Space.go:209-214)                   */
+#define GW_TICK_DEFER          4u  /* device-resident ops only, no COPY_TO_HOST:
+                                     launch the tick and return without a host
+                                     sync; out holds only `ops`.  The next call
+                                     that needs the results settles it (the
+                                     collect's one sync covers it); the outputs
+                                     are then read with gw_tick_result */
 
 typedef struct gw_tick_out {
     /* canonical order: sorted by (watcher, target); each directed pair at most
@@ -220,6 +226,9 @@ int  gw_set_clients(gw_ctx* ctx, const uint32_t* slots, const uint16_t* gates, u
 /* Flush all buffered ops of all spaces: AOI update + canonical net events. */
 int  gw_tick(gw_ctx* ctx, uint32_t flags, gw_tick_out* out);
 
+/* Outputs of the last tick (settles a GW_TICK_DEFER tick first). */
+int  gw_tick_result(gw_ctx* ctx, gw_tick_out* out);
+
 /* CollectEntitySyncInfos for all spaces of the context; clears the flags. */
 int  gw_sync_collect(gw_ctx* ctx, uint32_t flags, gw_sync_out* out);
 
@@ -227,19 +236,21 @@ int  gw_sync_collect(gw_ctx* ctx, uint32_t flags, gw_sync_out* out);
  * full count even when it exceeds cap. */
 int  gw_neighbors(gw_ctx* ctx, uint32_t slot, uint32_t* buf, uint32_t cap, uint32_t* n);
 
-/* Per-stage device timings (HIP events on the library's stream), for
- * bench.py's roofline.  Stages of successive gw_tick / gw_sync_collect calls
- * accumulate (up to GW_MAX_STAGES) until gw_get_stage_times returns and
- * clears them, so recording adds no host sync to a call.  names[i] are static
- * strings. */
+/* Per-stage device timings (HIP events recorded around each stage on the
+ * library's stream), for bench.py's roofline.  The stages of successive
+ * gw_tick / gw_sync_collect calls are all kept until gw_get_stage_times,
+ * which synchronises once and returns per stage name the summed time, bytes
+ * and number of calls, then clears them; recording adds no host sync and no
+ * query to the calls being timed.  name[i] are static strings. */
 #define GW_MAX_STAGES 32
 typedef struct gw_stage_times {
     uint32_t n;
     const char* name[GW_MAX_STAGES];
-    double   us[GW_MAX_STAGES];
-    uint64_t bytes_alg[GW_MAX_STAGES];   /* algorithmic bytes of the stage      */
+    double   us[GW_MAX_STAGES];          /* summed over the calls               */
+    uint64_t bytes_alg[GW_MAX_STAGES];   /* algorithmic bytes, summed           */
+    uint32_t calls[GW_MAX_STAGES];       /* recorded instances of the stage     */
 } gw_stage_times;
-int  gw_set_profiling(gw_ctx* ctx, int enable);
+int  gw_set_profiling(gw_ctx* ctx, int enable);   /* 0 off, 1 every stage, 2 the "diff" stage only */
 int  gw_get_stage_times(gw_ctx* ctx, gw_stage_times* out);
 
 /* Total neighbour-list entries held (sum over slots of |InterestedIn|). */
@@ -259,7 +270,7 @@ int  gw_synchronize(gw_ctx* ctx);
 int  gw_set_stream(gw_ctx* ctx, void* hip_stream);
 
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 3
+#define GW_ABI_VERSION 5
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

@@ -321,3 +321,75 @@ def test_long_dense_run(ctx_factory):
             h.check_lists(sample=range(0, n, 7))
     h.check_lists()
     assert h.g.total_neighbors() == h.orcs[0].total_neighbors()
+
+
+def _oracle_events(o, ops):
+    assert o.tick(ops) == 0
+    e, l = o.events()
+    return e.copy(), l.copy()
+
+
+@pytest.mark.parametrize("dense", [False, True])
+def test_deferred_tick_with_collect(ctx_factory, dense):
+    """GW_TICK_DEFER: device ops, the tick returns without a host sync, the
+    collect's one sync settles it (records checked), then gw_tick_result gives
+    the tick's events.  dense: every mover sees thousands of candidates, so the
+    first tick overflows the own-event regions and the redo runs in the settle."""
+    if dense:
+        n = 6000
+        tr = T.SpaceTrace(n=n, capacity=n, d=100.0, bounds=(-1000, -1000, 1000, 1000),
+                          init_slots=np.arange(n, dtype=np.uint32),
+                          init_x=(np.arange(n) % 40).astype(np.float32), init_y=np.zeros(n, np.float32),
+                          init_z=(np.arange(n) // 40 % 40).astype(np.float32),
+                          init_yaw=np.zeros(n, np.float32), ticks=[], gates=np.ones(n, np.uint16))
+        for t in range(3):
+            ops = T.make_ops(n // 3)
+            ops["kind"] = T.OP_MOVED
+            ops["sync_flags"] = 3
+            ops["slot"] = np.arange(t, n, 3)[: n // 3]
+            ops["x"] = np.where(np.arange(n // 3) % 2 == 0, 150.0 + t, 10.0 + t)
+            ops["z"] = 7.0
+            tr.ticks.append(ops)
+    else:
+        tr = T.config2(ticks=4, n=30_000)
+    g = ctx_factory()
+    gpuaoi.load_space(g, tr)
+    o = pyorc.OracleSpace(tr.capacity, tr.d, pyorc.SEQRULE)
+    pyorc.load_trace(o, tr)
+    g.sync_collect(copy=False)
+    o.collect()
+    gates = tr.gates
+    for t in range(len(tr.ticks)):
+        ops = tr.ticks[t]
+        dev = g.dev_alloc(max(ops.nbytes, 1))
+        g.h2d(dev, ops)
+        g.submit_device(dev, len(ops))
+        r0 = g.tick(copy=False, defer=True)
+        assert r0.ops == len(ops) and r0.n_enter == 0          # nothing read back yet
+        rec = g.sync_collect()                                  # settles the tick
+        ee, ll = _oracle_events(o, ops)
+        exp = _sorted_records(o.collect(), gates)
+        assert rec.n_rec == len(exp)
+        assert _sorted_records(rec.records, gates).tobytes() == exp.tobytes()
+        r = g.tick_result()
+        assert (r.n_enter, r.n_leave) == (len(ee), len(ll))
+        e = np.zeros(r.n_enter, gpuaoi.EVENT_DTYPE)
+        l = np.zeros(r.n_leave, gpuaoi.EVENT_DTYPE)
+        if r.n_enter:
+            g.d2h(e, r.enter_dev)
+        if r.n_leave:
+            g.d2h(l, r.leave_dev)
+        assert e.tobytes() == ee.tobytes() and l.tobytes() == ll.tobytes()
+        g.synchronize()
+        g.dev_free(dev)
+    # a deferred tick followed by another tick (no collect) settles in order
+    if not dense:
+        for t in range(2):
+            ops = tr.ticks[t]
+            dev = g.dev_alloc(ops.nbytes)
+            g.h2d(dev, ops)
+            g.submit_device(dev, len(ops))
+            g.tick(copy=False, defer=True)
+            g.synchronize()
+            g.dev_free(dev)
+        g.tick_result()

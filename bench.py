@@ -62,6 +62,8 @@ def parse():
                     help="halo exchange backend (gloo: rehearsal of several ranks on one GPU)")
     ap.add_argument("--halo-cap", type=int, default=16384, help="halo entities per neighbour per tick")
     ap.add_argument("--device", type=int, default=None, help="force a device (rehearsals on one GPU)")
+    ap.add_argument("--sync-by-client", action="store_true",
+                    help="collect grouped per client (GW_SYNC_BY_CLIENT, the gate's regroup on the GPU)")
     ap.add_argument("--capacity", type=int, default=None,
                     help="slot capacity of the space (N=1: cost of a strip's id range at N ranks)")
     return ap.parse_args()
@@ -164,6 +166,7 @@ class SpaceRun:
         self.dev_ops = g.dev_alloc(ops_all.nbytes)
         g.h2d(self.dev_ops, ops_all)
         self.nbytes_tick = self.m * traces.OP_DTYPE.itemsize
+        self.by_client = a.sync_by_client
         self.parallelism = f"independent spaces x{ctl.ws} (no comm)" if ctl.ws > 1 else "single GPU"
         self.n_world = a.entities * (ctl.ws if ctl.ws > 1 else 1)
 
@@ -171,7 +174,7 @@ class SpaceRun:
         g = self.g
         g.submit_device(self.dev_ops + t * self.nbytes_tick, self.m)
         g.tick(copy=False, defer=True)       # no host sync: the collect's sync settles it
-        s = g.sync_collect(copy=False)
+        s = g.sync_collect(copy=False, by_client=self.by_client)
         r = g.tick_result()
         return r.movers, r, s
 

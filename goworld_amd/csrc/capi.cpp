@@ -119,6 +119,7 @@ struct gw_ctx {
     ScanCtx sc{};                  // single-pass scan state (prim.hpp)
     // sync / query scratch
     DevBuf fbits, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
+    DevBuf cl_slot, cl_off, h_cl_slot, h_cl_off;   // GW_SYNC_BY_CLIENT segments (device / pinned host)
     uint64_t rec_cap = 0;                // records the rec0 buffer holds (grows on overflow)
     uint32_t* scal32 = nullptr;    // small device scalars
 
@@ -562,9 +563,9 @@ void gw_shutdown(gw_ctx* c) {
                       &c->mir_cnt,
                       &c->enter_d, &c->leave_d, &c->scan_status, &c->rs_hist,
                       &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
-                      &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf};
+                      &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf, &c->cl_slot, &c->cl_off};
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
-    DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec};
+    DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
     void* ps[] = {c->halo, c->rflag, c->sc.ticket, c->ownbits, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->nbc, c->last_pos, c->last_aoi,
                   c->last_leave, c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->cstats, c->scal32, c->gsb[0],
@@ -1070,6 +1071,25 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         if (c->hcstats->overflow) return set_err(c, GW_ENOMEM, "sync record buffer overflowed twice");
     }
     gw_sync_record* recs = P<gw_sync_record>(c->rec0);
+    const bool by_client = (flags & GW_SYNC_BY_CLIENT) != 0;
+    // ---- per-client grouping: stable sort by watcher (the gate grouping below
+    // is stable too, so the order becomes (gate, watcher, entity)) ---------
+    if (by_client && R > 1) {
+        prof_begin(c, "sync_clients");
+        if ((rc = ensure(c, c->gk0, R * 4)) || (rc = ensure(c, c->gv0, R * 4)) || (rc = ensure(c, c->gk1, R * 4)) ||
+            (rc = ensure(c, c->gv1, R * 4)) || (rc = ensure(c, c->rec1, R * sizeof(gw_sync_record))))
+            return rc;
+        RadixTmp rt;
+        if ((rc = radix_tmp(c, R, rt))) return rc;
+        launch_watcher_keys(recs, R, P<uint32_t>(c->gk0), P<uint32_t>(c->gv0), c->st);
+        const int wsel = sort_u32_u32(P<uint32_t>(c->gk0), P<uint32_t>(c->gv0), P<uint32_t>(c->gk1),
+                                      P<uint32_t>(c->gv1), R, nullptr, 0, ceil_log2(C), rt, c->st);
+        launch_gather_records(recs, wsel ? P<uint32_t>(c->gv1) : P<uint32_t>(c->gv0), nullptr, R,
+                              P<gw_sync_record>(c->rec1), c->st);
+        std::swap(c->rec0, c->rec1);
+        recs = P<gw_sync_record>(c->rec0);
+        prof_end(c, R * (24 * 2 + 8 * 4));
+    }
     // ---- per-gate grouping (stable, keeps the entity order) -------------
     if (R && G > 2) {
         prof_begin(c, "sync_gates");
@@ -1103,12 +1123,41 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         // at most one gate id in use: every record belongs to the last gate
         for (uint32_t g = 0; g <= G; ++g) c->gate_off[g] = (g == G) ? R : 0;
     }
+    uint32_t n_clients = 0;
+    if (by_client && R) {
+        if ((rc = ensure(c, c->gk0, R * 4)) || (rc = ensure(c, c->gk1, R * 4)) ||
+            (rc = ensure(c, c->cl_slot, R * 4)) || (rc = ensure(c, c->cl_off, (R + 1) * 8)) ||
+            (rc = ensure_scan(c, R)))
+            return rc;
+        launch_client_segments(recs, R, P<uint32_t>(c->gk0), P<uint32_t>(c->gk1), c->scal32 + 1,
+                               P<uint32_t>(c->cl_slot), P<uint64_t>(c->cl_off), c->sc, c->st);
+        HIPCHK(hipMemcpyAsync(&n_clients, c->scal32 + 1, 4, hipMemcpyDeviceToHost, c->st));
+    }
     HIPCHK(hipEventRecord(c->ev_t1, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1);
     out->device_us = ms * 1000.0;
     out->n_rec = R;
+    if (by_client) {
+        out->n_clients = n_clients;
+        out->client_slot_dev = P<uint32_t>(c->cl_slot);
+        out->client_off_dev = P<uint64_t>(c->cl_off);
+        if (flags & GW_SYNC_COPY_TO_HOST) {
+            if ((rc = ensure_host(c, c->h_cl_slot, (size_t)std::max<uint32_t>(n_clients, 1) * 4)) ||
+                (rc = ensure_host(c, c->h_cl_off, ((size_t)n_clients + 1) * 8)))
+                return rc;
+            if (n_clients) {
+                HIPCHK(hipMemcpyAsync(c->h_cl_slot.p, c->cl_slot.p, (size_t)n_clients * 4, hipMemcpyDeviceToHost, c->st));
+                HIPCHK(hipMemcpyAsync(c->h_cl_off.p, c->cl_off.p, ((size_t)n_clients + 1) * 8, hipMemcpyDeviceToHost, c->st));
+                HIPCHK(hipStreamSynchronize(c->st));
+            } else {
+                *(uint64_t*)c->h_cl_off.p = 0;
+            }
+            out->client_slot = (const uint32_t*)c->h_cl_slot.p;
+            out->client_off = (const uint64_t*)c->h_cl_off.p;
+        }
+    }
     out->flagged = NF;
     out->rec_dev = recs;
     out->gate_off = c->gate_off.data();

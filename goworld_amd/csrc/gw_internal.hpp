@@ -234,6 +234,10 @@ void launch_route_halo(const World& w, const gw_op* ops, const unsigned long lon
                        int32_t* last_leave, uint32_t* rflag, HaloStats* hs, hipStream_t s);
 void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,
                        hipStream_t s);
+void launch_watcher_keys(const gw_sync_record* rec, uint64_t n, uint32_t* keys, uint32_t* vals, hipStream_t s);
+void launch_client_segments(const gw_sync_record* rec, uint64_t n, uint32_t* head, uint32_t* pos,
+                            uint32_t* n_clients, uint32_t* client_slot, uint64_t* client_off, ScanCtx& sc,
+                            hipStream_t s);
 void launch_fill_u32(uint32_t* p, uint32_t v, uint64_t n, hipStream_t s);
 void launch_fill_i32(int32_t* p, int32_t v, uint64_t n, hipStream_t s);
 

@@ -278,6 +278,50 @@ __global__ void __launch_bounds__(NT) k_gather_records(const gw_sync_record* __r
     uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
     if (r < n) out[r] = in[idx[r]];
 }
+// ---------------------------------------------------------------------------
+// Per-client grouping of the record stream (GateService.handleSyncPositionYaw
+// OnClients, GateService.go:350-375, done on the device): the keys of a stable
+// sort by watcher, then the client segments of the sorted stream (a flag per
+// first record of a watcher, scanned, compacted into slot + offset).
+__global__ void __launch_bounds__(NT) k_watcher_keys(const gw_sync_record* __restrict__ rec, uint64_t n,
+                                                     uint32_t* keys, uint32_t* vals) {
+    const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (r >= n) return;
+    keys[r] = rec[r].watcher;
+    vals[r] = (uint32_t)r;
+}
+void launch_watcher_keys(const gw_sync_record* rec, uint64_t n, uint32_t* keys, uint32_t* vals, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_watcher_keys, dim3(nblk(n, NT)), dim3(NT), 0, s, rec, n, keys, vals);
+}
+__global__ void __launch_bounds__(NT) k_client_heads(const gw_sync_record* __restrict__ rec, uint64_t n,
+                                                     uint32_t* head) {
+    const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (r >= n) return;
+    head[r] = (r == 0 || rec[r].watcher != rec[r - 1].watcher) ? 1u : 0u;
+}
+__global__ void __launch_bounds__(NT) k_client_segments(const gw_sync_record* __restrict__ rec, uint64_t n,
+                                                        const uint32_t* __restrict__ head,
+                                                        const uint32_t* __restrict__ pos, uint32_t* client_slot,
+                                                        uint64_t* client_off) {
+    const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (r >= n) return;
+    if (head[r]) {
+        client_slot[pos[r]] = rec[r].watcher;
+        client_off[pos[r]] = r;
+    }
+    if (r == n - 1) client_off[pos[r] + head[r]] = n;    // end of the last client
+}
+void launch_client_segments(const gw_sync_record* rec, uint64_t n, uint32_t* head, uint32_t* pos,
+                            uint32_t* n_clients, uint32_t* client_slot, uint64_t* client_off, ScanCtx& sc,
+                            hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_client_heads, dim3(nblk(n, NT)), dim3(NT), 0, s, rec, n, head);
+    scan_exclusive<uint32_t, uint32_t>(head, pos, n, nullptr, sc, n_clients, s);
+    hipLaunchKernelGGL(k_client_segments, dim3(nblk(n, NT)), dim3(NT), 0, s, rec, n, head, pos, client_slot,
+                       client_off);
+}
+
 void launch_gather_records(const gw_sync_record* in, const uint32_t* idx, const uint64_t* n_dev, uint64_t n_max,
                            gw_sync_record* out, hipStream_t s) {
     if (!n_max) return;

@@ -31,7 +31,7 @@ REC_DTYPE = np.dtype([("watcher", "<u4"), ("entity", "<u4"), ("x", "<f4"), ("y",
                       ("z", "<f4"), ("yaw", "<f4")])
 
 TICK_COPY_TO_HOST, TICK_NO_EVENTS, TICK_DEFER = 1, 2, 4
-SYNC_COPY_TO_HOST = 1
+SYNC_COPY_TO_HOST, SYNC_BY_CLIENT = 1, 2
 MAX_STAGES = 32
 
 _u64, _u32, _f64 = C.c_uint64, C.c_uint32, C.c_double
@@ -47,7 +47,9 @@ class TickOut(C.Structure):
 class SyncOut(C.Structure):
     _fields_ = [("rec", C.c_void_p), ("rec_dev", C.c_void_p), ("n_rec", _u64),
                 ("gate_off", C.POINTER(_u64)), ("n_gates", _u32), ("flagged", _u64),
-                ("bytes_alg", _u64), ("device_us", _f64)]
+                ("bytes_alg", _u64), ("device_us", _f64), ("n_clients", _u32),
+                ("client_slot", C.POINTER(_u32)), ("client_off", C.POINTER(_u64)),
+                ("client_slot_dev", C.c_void_p), ("client_off_dev", C.c_void_p)]
 
 
 class StageTimes(C.Structure):
@@ -149,6 +151,8 @@ class SyncResult:
     bytes_alg: int
     device_us: float
     rec_dev: int = 0
+    client_slot: np.ndarray | None = None     # by_client: watcher slot of each client segment
+    client_off: np.ndarray | None = None      # by_client: n_clients + 1 offsets into records
 
 
 class GpuAOI:
@@ -261,16 +265,24 @@ class GpuAOI:
         return TickResult(e, l, o.n_enter, o.n_leave, o.ops, o.movers, o.pairs_tested, o.nbr_old,
                           o.nbr_new, o.bytes_alg, o.device_us, o.enter_dev or 0, o.leave_dev or 0)
 
-    def sync_collect(self, copy: bool = True) -> SyncResult:
+    def sync_collect(self, copy: bool = True, by_client: bool = False) -> SyncResult:
+        """by_client: records grouped per client inside each gate (the gate's
+        regroup, GateService.go:350-375), with the client segment table."""
         o = SyncOut()
-        self._chk(lib().gw_sync_collect(self._h, SYNC_COPY_TO_HOST if copy else 0, C.byref(o)))
+        fl = (SYNC_COPY_TO_HOST if copy else 0) | (SYNC_BY_CLIENT if by_client else 0)
+        self._chk(lib().gw_sync_collect(self._h, fl, C.byref(o)))
         r = None
         if copy:
             r = np.zeros(o.n_rec, REC_DTYPE)
             if o.n_rec:
                 C.memmove(_p(r), o.rec, o.n_rec * 24)
         goff = np.array([o.gate_off[i] for i in range(o.n_gates + 1)], dtype=np.uint64)
-        return SyncResult(r, o.n_rec, goff, o.flagged, o.bytes_alg, o.device_us, o.rec_dev or 0)
+        res = SyncResult(r, o.n_rec, goff, o.flagged, o.bytes_alg, o.device_us, o.rec_dev or 0)
+        if by_client and copy:
+            n = o.n_clients
+            res.client_slot = np.ctypeslib.as_array(o.client_slot, (max(n, 1),))[:n].copy()
+            res.client_off = np.ctypeslib.as_array(o.client_off, (n + 1,)).copy()
+        return res
 
     def neighbors(self, slot: int) -> np.ndarray:
         n = _u32()

@@ -132,9 +132,16 @@ typedef struct gw_tick_out {
 
 /* gw_sync_collect flags */
 #define GW_SYNC_COPY_TO_HOST   1u
+#define GW_SYNC_BY_CLIENT      2u  /* also group the records per client inside each
+                                      gate, as GateService.handleSyncPositionYaw
+                                      OnClients does (GateService.go:350-375):
+                                      order (gate, watcher, entity); client_off
+                                      partitions rec, one segment per client
+                                      packet MT_SYNC_POSITION_YAW_ON_CLIENTS   */
 
 typedef struct gw_sync_out {
-    /* canonical order: sorted by (gate(watcher), entity, watcher) */
+    /* canonical order: sorted by (gate(watcher), entity, watcher); with
+     * GW_SYNC_BY_CLIENT by (gate(watcher), watcher, entity)                    */
     const gw_sync_record* rec;      /* host pointer (NULL unless COPY_TO_HOST) */
     const gw_sync_record* rec_dev;  /* device pointer, always valid            */
     uint64_t n_rec;
@@ -143,6 +150,13 @@ typedef struct gw_sync_out {
     uint64_t flagged;               /* entities whose syncInfoFlag was set      */
     uint64_t bytes_alg;
     double   device_us;
+    /* GW_SYNC_BY_CLIENT only: client segments of rec (the watcher slot of each
+     * segment; n_clients+1 offsets).  Host arrays with COPY_TO_HOST.          */
+    uint32_t n_clients;
+    const uint32_t* client_slot;
+    const uint64_t* client_off;
+    const uint32_t* client_slot_dev;
+    const uint64_t* client_off_dev;
 } gw_sync_out;
 
 typedef struct gw_ctx gw_ctx;
@@ -270,7 +284,7 @@ int  gw_synchronize(gw_ctx* ctx);
 int  gw_set_stream(gw_ctx* ctx, void* hip_stream);
 
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 5
+#define GW_ABI_VERSION 6
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

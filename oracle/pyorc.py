@@ -164,3 +164,38 @@ def load_trace(sp: OracleSpace, tr, flags: int = 3):
     sp.bulk_enter(tr.init_slots, tr.init_x, tr.init_y, tr.init_z, tr.init_yaw, flags)
     if tr.gates is not None:
         sp.set_clients(tr.gates)
+
+
+MT_SYNC_POSITION_YAW_ON_CLIENTS = 1502   # proto.go:107-109 (the value orc_encode_wire writes)
+_WIRE_REC = np.dtype([("cid", "S16"), ("data", "V32")])   # clientid[16] + eid[16] + x,y,z,yaw
+
+
+def split_wire(buf: bytes) -> list:
+    """The game->gate packets concatenated by OracleSpace.wire() (one per gate:
+    u16 msgtype, u16 gateid, 48-B records).  Records start with an ASCII
+    clientid, so a 0xDE byte (low byte of msgtype 1502) only starts a header."""
+    out, i = [], 0
+    while i < len(buf):
+        assert buf[i] == MT_SYNC_POSITION_YAW_ON_CLIENTS & 0xFF
+        j = i + 4
+        while j < len(buf) and buf[j] != MT_SYNC_POSITION_YAW_ON_CLIENTS & 0xFF:
+            j += 48
+        out.append(buf[i:j])
+        i = j
+    return out
+
+
+def gate_dispatch(packet: bytes) -> dict:
+    """GateService.handleSyncPositionYawOnClients (GateService.go:350-375)
+    restated on one game->gate packet: records split by clientid; a client's
+    data (eid + x,y,z,yaw, 32 B per record) is appended in packet order and
+    sent as one packet u16 MT_SYNC_POSITION_YAW_ON_CLIENTS + data.  Returns
+    {clientid: packet bytes} (the reference visits clients in Go map order, so
+    the client order is not part of the result)."""
+    mt = int(np.frombuffer(packet, "<u2", 1, 0)[0])
+    assert mt == MT_SYNC_POSITION_YAW_ON_CLIENTS
+    out = {}
+    for r in np.frombuffer(packet[4:], _WIRE_REC):       # skip msgtype and the useless gateid
+        out.setdefault(bytes(r["cid"]), [np.uint16(MT_SYNC_POSITION_YAW_ON_CLIENTS).tobytes()]).append(
+            bytes(r["data"]))
+    return {k: b"".join(v) for k, v in out.items()}

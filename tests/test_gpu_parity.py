@@ -393,3 +393,47 @@ def test_deferred_tick_with_collect(ctx_factory, dense):
             g.synchronize()
             g.dev_free(dev)
         g.tick_result()
+
+
+def test_sync_by_client_matches_gate_dispatch(ctx_factory):
+    """GW_SYNC_BY_CLIENT: records grouped per client inside each gate, order
+    (gate, watcher, entity), with the client segment table; the per-client
+    packets built from them equal the gate's dispatch (GateService.go:350-375,
+    restated in oracle/pyorc.gate_dispatch) of the oracle's game->gate packets."""
+    import struct
+    tr = T.config2(ticks=3, n=20_000)
+    tr.gates = np.where(np.arange(tr.capacity) % 7 == 6, 0, 1 + np.arange(tr.capacity) % 3).astype(np.uint16)
+    g = ctx_factory()
+    gpuaoi.load_space(g, tr)
+    o = pyorc.OracleSpace(tr.capacity, tr.d, pyorc.SEQRULE)
+    pyorc.load_trace(o, tr)
+    eid = [pyorc.fixed_uuid(i) for i in range(tr.capacity)]
+    cid = [pyorc.fixed_uuid(i | 0x80000000) for i in range(tr.capacity)]
+    for t in range(-1, len(tr.ticks)):
+        if t >= 0:
+            g.submit(tr.ticks[t])
+            g.tick(copy=False)
+            assert o.tick(tr.ticks[t]) == 0
+        r = g.sync_collect(by_client=True)
+        exp = o.collect()
+        exp = exp[np.lexsort((exp["entity"], exp["watcher"], tr.gates[exp["watcher"]]))]
+        assert r.records.tobytes() == exp.tobytes(), f"tick {t}: per-client records differ"
+        # client table: one segment per watcher, in stream order
+        w = r.records["watcher"]
+        heads = np.nonzero(np.r_[True, w[1:] != w[:-1]])[0] if len(w) else np.zeros(0, np.int64)
+        assert np.array_equal(r.client_off, np.r_[heads, len(w)].astype(np.uint64))
+        assert np.array_equal(r.client_slot, w[heads])
+        # gate_off still partitions the stream by gate
+        gsel = tr.gates[w]
+        for gid in range(len(r.gate_off) - 1):
+            assert np.all(gsel[r.gate_off[gid]:r.gate_off[gid + 1]] == gid)
+        if t == len(tr.ticks) - 1:
+            got = {}
+            for k in range(len(r.client_slot)):
+                seg = r.records[r.client_off[k]:r.client_off[k + 1]]
+                got[cid[int(r.client_slot[k])]] = struct.pack("<H", 1502) + b"".join(
+                    eid[int(e["entity"])] + struct.pack("<4f", e["x"], e["y"], e["z"], e["yaw"]) for e in seg)
+            want = {}
+            for pkt in pyorc.split_wire(o.wire()):
+                want.update(pyorc.gate_dispatch(pkt))
+            assert len(want) > 1000 and got == want

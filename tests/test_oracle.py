@@ -227,3 +227,45 @@ def test_net_events_cancel_transients():
     e, l = sp.events()
     raw_e, raw_l, _, _ = sp.raw_counts()
     assert len(e) == 0 and len(l) == 0 and raw_e == 2 and raw_l == 2
+
+
+def test_gate_dispatch_known_answer():
+    """GateService.handleSyncPositionYawOnClients (GateService.go:350-375): a
+    game->gate packet is split per clientid, each client's 32-B records kept
+    in packet order behind u16 MT_SYNC_POSITION_YAW_ON_CLIENTS."""
+    import struct
+
+    def rec(cid, eid, x):
+        return cid + eid + struct.pack("<4f", x, 0.0, 2 * x, 0.5)
+    A, B = b"A" * 16, b"B" * 16
+    pkt = struct.pack("<HH", 1502, 7) + rec(A, b"e" * 16, 1.0) + rec(B, b"f" * 16, 2.0) + rec(A, b"g" * 16, 3.0)
+    d = pyorc.gate_dispatch(pkt)
+    assert set(d) == {A, B}
+    assert d[A] == struct.pack("<H", 1502) + rec(A, b"e" * 16, 1.0)[16:] + rec(A, b"g" * 16, 3.0)[16:]
+    assert d[B] == struct.pack("<H", 1502) + rec(B, b"f" * 16, 2.0)[16:]
+    assert pyorc.split_wire(pkt + pkt) == [pkt, pkt]
+
+
+def test_gate_dispatch_of_oracle_wire_is_the_client_regroup():
+    """The oracle's game->gate packets dispatched by the gate restatement hold,
+    per client, the client's records in entity order (the canonical order the
+    GPU's per-client collect returns)."""
+    import struct
+    tr = T.config2(ticks=1, n=3000)
+    tr.gates = (1 + np.arange(tr.capacity) % 3).astype(np.uint16)
+    o = pyorc.OracleSpace(tr.capacity, tr.d, pyorc.SEQRULE)
+    pyorc.load_trace(o, tr)
+    o.collect()
+    assert o.tick(tr.ticks[0]) == 0
+    recs = o.collect()
+    got = {}
+    for pkt in pyorc.split_wire(o.wire()):
+        got.update(pyorc.gate_dispatch(pkt))
+    order = np.lexsort((recs["entity"], recs["watcher"]))
+    exp = {}
+    for r in recs[order]:
+        cid = pyorc.fixed_uuid(int(r["watcher"]) | 0x80000000)
+        exp.setdefault(cid, [struct.pack("<H", 1502)]).append(
+            pyorc.fixed_uuid(int(r["entity"])) + struct.pack("<4f", r["x"], r["y"], r["z"], r["yaw"]))
+    exp = {k: b"".join(v) for k, v in exp.items()}
+    assert len(got) > 100 and got == exp

@@ -60,7 +60,8 @@ def parse():
                     help="3: config #3 per GPU (weak); 5: the 16M uniform world of config #5 over N strips (strong)")
     ap.add_argument("--comm", choices=["nccl", "gloo"], default="nccl",
                     help="halo exchange backend (gloo: rehearsal of several ranks on one GPU)")
-    ap.add_argument("--halo-cap", type=int, default=16384, help="halo entities per neighbour per tick")
+    ap.add_argument("--halo-cap", type=int, default=4096, help="halo entities per neighbour per tick")
+    ap.add_argument("--halo-cap-load", type=int, default=16384, help="the same, for the ticks that load the world")
     ap.add_argument("--device", type=int, default=None, help="force a device (rehearsals on one GPU)")
     ap.add_argument("--sync-by-client", action="store_true",
                     help="collect grouped per client (GW_SYNC_BY_CLIENT, the gate's regroup on the GPU)")
@@ -212,7 +213,7 @@ class WorldRun:
         pg = None if a.comm == "nccl" else ctl.group
         cdev = dev if a.comm == "nccl" else torch.device("cpu")
         self.sr = sr = dworld.StripRank(eng, geom, r, n * ws, bounds, dev, pg=pg, comm_device=cdev,
-                                        halo_cap=a.halo_cap)
+                                        halo_cap=a.halo_cap, halo_cap_max=a.halo_cap_load)
         eng.set_clients(np.arange(n * ws, dtype=np.uint32), np.ones(n * ws, np.uint16))  # config #3: 1 gate, all clients
 
         def words(ops):
@@ -222,7 +223,7 @@ class WorldRun:
             return torch.from_numpy(dworld.ops_to_words(o).copy()).to(dev)
         enter = traces.enter_ops(tr.init_slots, tr.init_x, tr.init_y, tr.init_z, tr.init_yaw)
         for i in range(0, n, 1 << 18):
-            sr.step(words(enter[i:i + (1 << 18)]), copy=False, no_events=True)
+            sr.step(words(enter[i:i + (1 << 18)]), copy=False, cap=a.halo_cap_load, no_events=True)
         sr.collect(copy=False)
         self.m = len(tr.ticks[0])
         self.words = [words(t) for t in tr.ticks]              # resident in HBM

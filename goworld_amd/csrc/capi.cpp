@@ -699,11 +699,9 @@ int gw_route_halo(gw_ctx* c, const gw_op* dev_ops, const uint64_t* dev_stamps, u
     for (uint32_t d = 0; d < n_dst; ++d) {
         if (!dsts[d].rows && dsts[d].cap_entities) return GW_EINVAL;
         D.d[d] = HaloDst{dsts[d].x_lo, dsts[d].x_hi, dsts[d].rows, dsts[d].cap_entities};
-        if (dsts[d].cap_entities)
-            HIPCHK(hipMemsetAsync(dsts[d].rows, 0, (size_t)dsts[d].cap_entities * 3 * sizeof(gw_halo_row), c->st));
     }
-    HIPCHK(hipMemsetAsync(c->halo->cnt, 0, sizeof c->halo->cnt, c->st));
-    if (!n || !c->total_slots) return 0;
+    if (!c->total_slots) return set_err(c, GW_EINVAL, "no space");
+    // n == 0 still runs: the buffers must become all NOPs
     launch_route_halo(world(c), dev_ops, (const unsigned long long*)dev_stamps, n, max_step, D, c->last_pos,
                       c->last_aoi, c->last_leave, c->rflag, c->halo, c->st);
     HIPCHK(hipGetLastError());

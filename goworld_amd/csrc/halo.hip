@@ -10,8 +10,11 @@
 //   r2  OR of the sync flags of the ops after the last Leave (atomicOr)
 //   r3  the entity's last op writes up to 3 rows per destination, entities
 //       placed by one wave-aggregated atomic per wave and destination
-//   r4  reset of the per-slot scratch
-// Integer/byte work bound by latency of the per-slot gathers; no LDS or MFMA.
+//   r4  reset of the per-slot scratch; zero (NOP) rows past the entities
+//       placed, so no memset of the buffers is needed
+// The placement counters are zeroed by r1 of the next call (r4 of this one
+// has read them by then).  Integer/byte work bound by the latency of the
+// per-slot gathers; no LDS or MFMA.
 #include "dev_common.hpp"
 
 namespace gw {
@@ -28,6 +31,7 @@ __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, ui
                                                 int32_t* last_pos, int32_t* last_aoi, int32_t* last_leave,
                                                 HaloStats* hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i == 0) hs->cnt[0] = hs->cnt[1] = 0;         // placement counters of this call
     if (i >= n) return;
     const gw_op op = ops[i];
     if (op.kind == GW_OP_NOP) return;
@@ -136,16 +140,22 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
             continue;
         }
         gw_halo_row* r = dst.rows + (size_t)e * ROWS;
-        if (k0) put_row(r + 0, mk_op(k0, 0, s, nullptr), stamps[ll]);
-        if (k1) put_row(r + 1, mk_op(k1, 0, s, &oa), stamps[la]);
-        if (k2) put_row(r + 2, mk_op(k2, (uint8_t)f, s, &op_pos), stamps[i]);
+        const gw_op nop = mk_op(GW_OP_NOP, 0, 0, nullptr);
+        put_row(r + 0, k0 ? mk_op(k0, 0, s, nullptr) : nop, k0 ? stamps[ll] : 0ull);
+        put_row(r + 1, k1 ? mk_op(k1, 0, s, &oa) : nop, k1 ? stamps[la] : 0ull);
+        put_row(r + 2, k2 ? mk_op(k2, (uint8_t)f, s, &op_pos) : nop, k2 ? stamps[i] : 0ull);
     }
 }
 
 __global__ void __launch_bounds__(NT) k_route4(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
                                                 int32_t* last_pos, int32_t* last_aoi, int32_t* last_leave,
-                                                uint32_t* rflag) {
+                                                uint32_t* rflag, HaloDsts D, const HaloStats* __restrict__ hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    // rows past the placed entities become NOPs (thread i: row i of each buffer)
+    for (uint32_t d = 0; d < D.n; ++d) {
+        const uint64_t used = (uint64_t)min(hs->cnt[d], D.d[d].cap) * ROWS;
+        if (i >= used && i < (uint64_t)D.d[d].cap * ROWS) put_row(D.d[d].rows + i, mk_op(GW_OP_NOP, 0, 0, nullptr), 0ull);
+    }
     if (i >= n) return;
     const gw_op op = ops[i];
     if (!op_valid(op, cap)) return;
@@ -169,11 +179,14 @@ void launch_route_halo(const World& w, const gw_op* ops, const unsigned long lon
                        float max_step, const HaloDsts& D, int32_t* last_pos, int32_t* last_aoi,
                        int32_t* last_leave, uint32_t* rflag, HaloStats* hs, hipStream_t s) {
     const uint32_t nb = nblk1(n, NT);
+    uint64_t rows = 0;
+    for (uint32_t d = 0; d < D.n; ++d) rows = std::max<uint64_t>(rows, (uint64_t)D.d[d].cap * ROWS);
     hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, last_pos, last_aoi, last_leave, hs);
     hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, last_leave, rflag);
     hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, last_pos, last_aoi, last_leave,
                        rflag, max_step, D, hs);
-    hipLaunchKernelGGL(k_route4, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, last_pos, last_aoi, last_leave, rflag);
+    hipLaunchKernelGGL(k_route4, dim3(nblk1(std::max<uint64_t>(n, rows), NT)), dim3(NT), 0, s, ops, n, w.cap,
+                       last_pos, last_aoi, last_leave, rflag, D, hs);
 }
 
 void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,

@@ -165,11 +165,12 @@ class Router:
             t[slot] = -1
         return out
 
-    def route(self, words: torch.Tensor, stamps: torch.Tensor):
+    def route(self, words: torch.Tensor, stamps: torch.Tensor, cap: int | None = None):
         """Owned ops of one tick -> (send to left, send to right): NOP-padded
-        int32 row buffers (K * 3, 8) in gw_halo_row layout.  Updates the
-        routing state.  No host sync."""
+        int32 row buffers (cap * 3, 8) in gw_halo_row layout (cap <= K
+        entities).  Updates the routing state.  No host sync."""
         g, r = self.g, self.r
+        cap = self.K if cap is None else min(cap, self.K)
         m = words.shape[0]
         dev = self.dev
         kind = words[:, 0] & 0xFF
@@ -215,7 +216,7 @@ class Router:
             k2 = torch.where(now & ((new_f != 0) | (lp > la)), torch.full_like(kind, OP_SYNC), nop)
             sel = rep & ((k0 | k1 | k2) != 0)
             sends.append(self._pack(words, stamps, slot, sel, k0, ll.clamp(min=0), k1, la_c,
-                                    k2, lp_c, new_f, lany))
+                                    k2, lp_c, new_f, lany, cap))
         # routing state of the rows this rank owns (dummy row n absorbs the rest)
         s = torch.where(rep, slot, torch.full_like(slot, self.n))
         self.x[s] = new_x
@@ -223,10 +224,9 @@ class Router:
         self.pflags[s] = new_f
         return sends[0], sends[1]
 
-    def _pack(self, words, stamps, slot, sel, k0, i0, k1, i1, k2, i2, f2, i_last):
+    def _pack(self, words, stamps, slot, sel, k0, i0, k1, i1, k2, i2, f2, i_last, K):
         """Entity rows (row 0, 1, 2 of each selected entity) compacted into a
         buffer of K entities; unused rows are NOPs (all-zero)."""
-        K = self.K
         m = words.shape[0]
         pos = torch.cumsum(sel.to(torch.int64), 0) - 1
         self.overflow = torch.maximum(self.overflow, sel.sum() - K)
@@ -255,8 +255,7 @@ class Router:
 
     def receive(self, buf: torch.Tensor):
         """Ghost rows from a neighbour: updates the routing state."""
-        K = self.K
-        rows = buf.view(K, ROWS_PER_ENTITY, ROW_WORDS)
+        rows = buf.view(-1, ROWS_PER_ENTITY, ROW_WORDS)
         k1 = rows[:, 1, 0] & 0xFF
         k2 = rows[:, 2, 0] & 0xFF
         f2 = (rows[:, 2, 0] >> 8) & SIF_MASK
@@ -303,12 +302,13 @@ class HipRouter:
             else:
                 self.bufs.append(None)
 
-    def route(self, words: torch.Tensor, stamps: torch.Tensor):
+    def route(self, words: torch.Tensor, stamps: torch.Tensor, cap: int | None = None):
         if not self.dsts:
             return None, None            # a one-strip world has no neighbours
+        cap = self.K if cap is None else min(cap, self.K)
         self.g.route_halo(words.data_ptr(), stamps.data_ptr(), words.shape[0], float(self.geom.max_step),
-                          self.dsts)
-        return self.bufs[0], self.bufs[1]
+                          [(lo, hi, p, cap) for lo, hi, p, _ in self.dsts])
+        return tuple(None if b is None else b[:cap * ROWS_PER_ENTITY] for b in self.bufs)
 
     def receive(self, buf):
         pass                        # the engine's own state is the routing state
@@ -394,25 +394,30 @@ class StripRank:
     submit_rows / tick / collect)."""
 
     def __init__(self, engine, geom: Strips, rank: int, n_global: int, bounds, device,
-                 pg=None, comm_device=None, halo_cap: int = 1 << 14):
+                 pg=None, comm_device=None, halo_cap: int = 1 << 14, halo_cap_max: int | None = None):
+        """halo_cap: entities per neighbour per tick (steady state); a call may
+        ask for up to halo_cap_max (e.g. the ticks that load the population)."""
         self.e, self.g, self.r = engine, geom, rank
         self.dev = device
         self.pg = pg
         self.cdev = comm_device if comm_device is not None else device
-        self.router = engine.make_router(geom, rank, n_global, device, halo_cap)
+        self.cap = halo_cap
+        self.router = engine.make_router(geom, rank, n_global, device, max(halo_cap, halo_cap_max or 0))
         self.sid, base = engine.create_space(geom.d, n_global, bounds)
         if base != 0:
             raise ValueError("a strip rank holds one space per context (local slot = global id)")
         engine.set_ownership(self.sid, *geom.own_range_f32(rank))
         self.tick_no = 0
 
-    def submit(self, words: torch.Tensor):
+    def submit(self, words: torch.Tensor, cap: int | None = None):
         """Queue this rank's owned ops of one tick (int32 (m, 6) gw_op words on
-        the device, in call order), route and exchange the halo rows."""
+        the device, in call order), route and exchange the halo rows (cap:
+        entities per neighbour for this tick; every rank must pass the same)."""
         m = words.shape[0]
+        cap = min(self.cap if cap is None else cap, self.router.K)
         st = stamps_for(self.tick_no, self.r, self.g.ranks, m, self.dev)
-        sl, sr = self.router.route(words, st)
-        nrows = self.router.K * ROWS_PER_ENTITY
+        sl, sr = self.router.route(words, st, cap)
+        nrows = cap * ROWS_PER_ENTITY
         if self.g.ranks > 1:
             recvd = exchange(self.pg, self.r, self.g.ranks, sl, sr, nrows, self.dev, self.cdev)
         else:
@@ -426,8 +431,8 @@ class StripRank:
     def tick(self, copy=True, **kw):
         return self.e.tick(copy=copy, **kw)
 
-    def step(self, words: torch.Tensor, copy=True, **kw):
-        self.submit(words)
+    def step(self, words: torch.Tensor, copy=True, cap: int | None = None, **kw):
+        self.submit(words, cap)
         return self.tick(copy=copy, **kw)
 
     def collect(self, copy=True):

@@ -122,8 +122,10 @@ def test_dworld_gloo_oracle_ranks(world, tmp_path):
 
 
 @pytest.mark.gpu
-def test_dworld_gpu_two_ranks(tmp_path):
-    _check(2, _run_ranks(2, "hip", tmp_path, timeout=100))
+@pytest.mark.parametrize("world", [2, 3])
+def test_dworld_gpu_ranks(world, tmp_path):
+    """The HIP engine per rank (HipRouter + gw_route_halo), ranks sharing the GPU."""
+    _check(world, _run_ranks(world, "hip", tmp_path, timeout=100))
 
 
 def _canon_rows(buf, K):

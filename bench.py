@@ -150,6 +150,40 @@ def cpu_baseline(tr, seconds):
             "per_op_us": spent / done * 1e6}
 
 
+def cpu_baseline_mt(seconds, entities, side):
+    """Fairness point: oracle/gridmt.c, a multi-threaded (OpenMP)
+    uniform-grid CPU implementation of the same batched tick + collect, on the
+    host cores this job may use (OMP_NUM_THREADS; 16 per GPU on the box), over
+    config #3 ticks until the time budget is spent."""
+    from oracle import pyorc
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = min(threads, 16)
+    tr = traces.config3(ticks=8, seed=3, n=entities, side=side)
+    m = pyorc.GridMT(tr.capacity, tr.d, tr.bounds, threads=threads)
+    m.load(tr)
+    m.collect()                                       # the Enter flags (untimed)
+    done = ev = rec = 0
+    spent = 0.0
+    for ops in tr.ticks:
+        t = time.perf_counter()
+        assert m.tick(ops) == 0
+        e, l = m.events()
+        r = m.collect()
+        spent += time.perf_counter() - t
+        done += len(ops)
+        ev += len(e) + len(l)
+        rec += len(r)
+        if spent > seconds:
+            break
+    m.close()
+    steps = done // len(tr.ticks[0])
+    return {"value": done / spent, "unit": "updates/s", "cores": threads, "kind": "port",
+            "events_per_sec": ev / spent, "records_per_sec": rec / spent, "ms_per_step": spent / steps * 1e3,
+            "sample": f"{steps} full ticks of config #3 (tick + collect, canonical events and records) through "
+                      f"oracle/gridmt.c: OpenMP uniform grid, {threads} threads, the batched contract "
+                      f"(checked bit-exact against the oracle in tests/test_oracle.py)"}
+
+
 class SpaceRun:
     """N=1 (config #3) and --mode spaces: one independent space per GPU."""
 
@@ -356,6 +390,7 @@ def main():
     if not a.no_cpu_baseline and ws == 1 and a.config == 3:
         cb = cpu_baseline(traces.config3(ticks=1, seed=3, n=a.entities, side=a.side), a.cpu_seconds)
         line["cpu_baseline"] = cb
+        line["cpu_baseline_mt"] = cpu_baseline_mt(a.cpu_seconds, a.entities, a.side)
     print(json.dumps(line), flush=True)
     run.close()
 

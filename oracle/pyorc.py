@@ -199,3 +199,80 @@ def gate_dispatch(packet: bytes) -> dict:
         out.setdefault(bytes(r["cid"]), [np.uint16(MT_SYNC_POSITION_YAW_ON_CLIENTS).tobytes()]).append(
             bytes(r["data"]))
     return {k: b"".join(v) for k, v in out.items()}
+
+
+# ---------------------------------------------------------------------------
+# gridmt.c: multi-threaded uniform-grid CPU fairness baseline
+_GMT_PATH = os.path.join(_HERE, "build", "libgridmt.so")
+_gmt = None
+
+
+def gmt_lib():
+    global _gmt
+    if _gmt is None:
+        if not os.path.exists(_GMT_PATH):
+            build()
+        L = C.CDLL(_GMT_PATH)
+        vp, u32, u64, f32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_float
+        L.gmt_new.restype = vp
+        L.gmt_new.argtypes = [u32, f32, f32, f32, f32, f32, C.c_int]
+        L.gmt_free.argtypes = [vp]
+        L.gmt_set_clients.argtypes = [vp, vp]
+        L.gmt_load.argtypes = [vp, u32, vp, vp, vp, vp, vp]
+        L.gmt_tick.argtypes = [vp, vp, u32]
+        L.gmt_event_counts.argtypes = [vp, C.POINTER(u64), C.POINTER(u64)]
+        L.gmt_events_copy.argtypes = [vp, vp, vp]
+        L.gmt_collect.argtypes = [vp]
+        L.gmt_collect.restype = u64
+        L.gmt_records_copy.argtypes = [vp, vp]
+        L.gmt_threads.argtypes = [vp]
+        _gmt = L
+    return _gmt
+
+
+class GridMT:
+    """Multi-threaded (OpenMP) uniform-grid CPU implementation of the batched
+    tick + collect; threads = 0 uses OMP_NUM_THREADS / all cores."""
+
+    def __init__(self, capacity: int, d: float, bounds, threads: int = 0):
+        self._h = gmt_lib().gmt_new(capacity, d, *[float(b) for b in bounds], threads)
+        self.capacity = capacity
+
+    def close(self):
+        if self._h:
+            gmt_lib().gmt_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    @property
+    def threads(self) -> int:
+        return gmt_lib().gmt_threads(self._h)
+
+    def load(self, tr):
+        a = [np.ascontiguousarray(v, dtype=t) for v, t in
+             ((tr.init_slots, np.uint32), (tr.init_x, np.float32), (tr.init_y, np.float32),
+              (tr.init_z, np.float32), (tr.init_yaw, np.float32))]
+        assert gmt_lib().gmt_load(self._h, len(a[0]), *[_ptr(v) for v in a]) == 0
+        if tr.gates is not None:
+            gates = np.zeros(self.capacity, np.uint16)
+            gates[:len(tr.gates)] = tr.gates
+            gmt_lib().gmt_set_clients(self._h, _ptr(gates))
+
+    def tick(self, ops: np.ndarray) -> int:
+        ops = np.ascontiguousarray(ops)
+        return gmt_lib().gmt_tick(self._h, _ptr(ops), len(ops))
+
+    def events(self):
+        ne, nl = C.c_uint64(), C.c_uint64()
+        gmt_lib().gmt_event_counts(self._h, C.byref(ne), C.byref(nl))
+        e = np.zeros(ne.value, EVENT_DTYPE)
+        l = np.zeros(nl.value, EVENT_DTYPE)
+        gmt_lib().gmt_events_copy(self._h, _ptr(e), _ptr(l))
+        return e, l
+
+    def collect(self) -> np.ndarray:
+        n = gmt_lib().gmt_collect(self._h)
+        r = np.zeros(n, REC_DTYPE)
+        gmt_lib().gmt_records_copy(self._h, _ptr(r))
+        return r

@@ -437,3 +437,26 @@ def test_sync_by_client_matches_gate_dispatch(ctx_factory):
             for pkt in pyorc.split_wire(o.wire()):
                 want.update(pyorc.gate_dispatch(pkt))
             assert len(want) > 1000 and got == want
+
+
+def test_clients_change_between_tick_and_collect(ctx_factory):
+    """The collect takes a mover's count of neighbours with a client from the
+    diff's cache only while it is current: attaching / detaching clients after
+    the tick (GameClient set or cleared, GameClient.go:14-27) must be seen by
+    the next collect; flags accumulate over two ticks without a collect."""
+    tr = T.config2(ticks=4, n=20_000)
+    g = ctx_factory()
+    h = Harness(g, [tr])
+    h.check_collect()
+    rng = np.random.default_rng(5)
+    for t in range(len(tr.ticks)):
+        h.step(t)
+        if t % 2 == 0:
+            continue                          # two ticks' flags per collect
+        sel = rng.choice(tr.capacity, 3000, replace=False).astype(np.uint32)
+        newg = np.where(rng.random(3000) < 0.5, 0, 1 + rng.integers(0, 3, 3000)).astype(np.uint16)
+        g.set_clients(sel, newg)              # after the tick, before the collect
+        h.gates[sel] = newg
+        for s, gg in zip(sel.tolist(), newg.tolist()):
+            h.orcs[0].set_client(s, gg)
+        h.check_collect()

@@ -269,3 +269,27 @@ def test_gate_dispatch_of_oracle_wire_is_the_client_regroup():
             pyorc.fixed_uuid(int(r["entity"])) + struct.pack("<4f", r["x"], r["y"], r["z"], r["yaw"]))
     exp = {k: b"".join(v) for k, v in exp.items()}
     assert len(got) > 100 and got == exp
+
+
+@pytest.mark.parametrize("which", ["uniform", "adversarial", "churn"])
+def test_gridmt_equals_seqrule(which):
+    """The multi-threaded grid CPU baseline (oracle/gridmt.c) computes the
+    batched contract: events bit-exact with the SEQRULE engine, records the
+    same multiset, on uniform, rounding-edge and churn traces."""
+    if which == "uniform":
+        tr = T.config2(ticks=4, n=6000)
+    else:
+        tr = T.adversarial_trace(21 if which == "adversarial" else 22, n=500, ticks=8, churn=which == "churn")
+    o = pyorc.OracleSpace(tr.capacity, tr.d, pyorc.SEQRULE)
+    pyorc.load_trace(o, tr)
+    m = pyorc.GridMT(tr.capacity, tr.d, tr.bounds, threads=4)
+    m.load(tr)
+
+    def srt(r):
+        return r[np.lexsort((r["watcher"], r["entity"]))].tobytes()
+    assert srt(o.collect()) == srt(m.collect())
+    for ops in tr.ticks:
+        assert o.tick(ops) == 0 and m.tick(ops) == 0
+        (e0, l0), (e1, l1) = o.events(), m.events()
+        assert e0.tobytes() == e1.tobytes() and l0.tobytes() == l1.tobytes()
+        assert srt(o.collect()) == srt(m.collect())

@@ -99,6 +99,30 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
     }
 }
 
+// Restore path (Space.go:209-214, EntityManager.go:556-617): entity i enters
+// with stamp base + i, i.e. exactly as n Enter calls in index order; with no
+// neighbour lists there is nothing else to build (the grid is rebuilt next).
+__global__ void __launch_bounds__(NT) k_restore(World w, const uint32_t* __restrict__ slots,
+                                                const float4* __restrict__ xyzw, uint32_t n,
+                                                unsigned long long stamp_base, uint32_t flags) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slots[i];
+    const float4 p = xyzw[i];
+    AoiEnt a = w.aoi[s];
+    a.x = p.x;
+    a.z = p.z;
+    a.meta |= PRESENT_BIT;
+    w.aoi[s] = a;
+    w.pos[s] = p;
+    w.stamp[s] = stamp_base + i;
+    w.flags[s] |= flags;
+}
+void launch_restore(const World& w, const uint32_t* slots, const float4* xyzw, uint32_t n,
+                    unsigned long long stamp_base, uint32_t flags, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_restore, dim3(nblk(n, NT)), dim3(NT), 0, s, w, slots, xyzw, n, stamp_base, flags);
+}
+
 void tick_ops(const TickBufs& b, hipStream_t s) {
     hipLaunchKernelGGL(k_ops1, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_ops2, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);

@@ -636,6 +636,45 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
     return 0;
 }
 
+int gw_space_restore(gw_ctx* c, uint32_t sid, const uint32_t* slots, const float* x, const float* y,
+                     const float* z, const float* yaw, uint32_t n, uint8_t sync_flags) {
+    if (!c || (n && (!slots || !x || !y || !z || !yaw))) return GW_EINVAL;
+    if (int rs = settle(c)) return rs;
+    (void)hipSetDevice(c->dev);
+    if (sid >= c->spaces.size() || !c->spaces[sid].alive) return set_err(c, GW_ERANGE, "no space %u", sid);
+    if (!c->segs.empty()) return set_err(c, GW_ESTATE, "restore with ops pending: tick first");
+    if (!n) return 0;
+    const SpaceHost& sp = c->spaces[sid];
+    std::vector<uint8_t> seen;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t s = slots[i];
+        if (s < sp.base || s >= sp.base + sp.cap)
+            return set_err(c, GW_ERANGE, "restore %u: slot %u not in space %u", i, s, sid);
+        if (!(std::isfinite(x[i]) && std::isfinite(z[i])))
+            return set_err(c, GW_EINVAL, "restore %u: non-finite coordinates", i);
+        if (seen.empty()) seen.assign(sp.cap, 0);
+        if (seen[s - sp.base]++ || (c->validate && c->present_h[s]))
+            return set_err(c, GW_ESTATE, "restore %u: slot %u already in the space", i, s);
+    }
+    int rc;
+    std::vector<float4> p(n);
+    for (uint32_t i = 0; i < n; ++i) p[i] = make_float4(x[i], y[i], z[i], yaw[i]);
+    const size_t off = ((size_t)n * 4 + 15) & ~(size_t)15;     // float4 payload after the slots
+    if ((rc = ensure(c, c->qbuf, off + (size_t)n * 16))) return rc;
+    uint32_t* dslots = P<uint32_t>(c->qbuf);
+    float4* dp = (float4*)(P<uint8_t>(c->qbuf) + off);
+    HIPCHK(hipMemcpyAsync(dslots, slots, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(dp, p.data(), (size_t)n * 16, hipMemcpyHostToDevice, c->st));
+    launch_restore(world(c), dslots, dp, n, c->stamp_base, sync_flags, c->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->st));            // the host arrays are the caller's
+    c->stamp_base += n;
+    for (uint32_t i = 0; i < n; ++i) c->present_h[slots[i]] = 1;
+    ++c->epoch;                                      // neighbour counts cached by the diff are stale
+    c->grid_dirty = true;                            // rebuilt (one radix sort) before the next use
+    return 0;
+}
+
 int gw_space_destroy(gw_ctx* c, uint32_t sid) {
     if (!c) return GW_EINVAL;
     if (int rs = settle(c)) return rs;
@@ -747,7 +786,7 @@ int gw_set_clients(gw_ctx* c, const uint32_t* slots, const uint16_t* gates, uint
     HIPCHK(hipMemcpyAsync(c->gk0.p, slots, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemcpyAsync(c->gv0.p, gates, (size_t)n * 2, hipMemcpyHostToDevice, c->st));
     ++c->epoch;   // neighbour-with-client counts cached by the last tick are stale
-    launch_set_clients(world(c), P<uint32_t>(c->gk0), (const uint16_t*)c->gv0.p, n, c->st);
+    launch_set_clients(world(c), P<uint32_t>(c->gk0), (const uint16_t*)c->gv0.p, n, !c->grid_dirty, c->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;

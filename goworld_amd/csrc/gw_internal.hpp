@@ -195,7 +195,7 @@ void tick_diff(const TickBufs& b, hipStream_t s);                  // own + mirr
 void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s);   // canonical event arrays
 void tick_reset(const TickBufs& b, hipStream_t s);                 // after the host read the counts
 
-void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n,
+void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n, bool grid_ok,
                         hipStream_t s);
 // sync collect
 void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint32_t* fbits, ScanCtx& sc,
@@ -238,6 +238,8 @@ void launch_watcher_keys(const gw_sync_record* rec, uint64_t n, uint32_t* keys, 
 void launch_client_segments(const gw_sync_record* rec, uint64_t n, uint32_t* head, uint32_t* pos,
                             uint32_t* n_clients, uint32_t* client_slot, uint64_t* client_off, ScanCtx& sc,
                             hipStream_t s);
+void launch_restore(const World& w, const uint32_t* slots, const float4* xyzw, uint32_t n,
+                    unsigned long long stamp_base, uint32_t flags, hipStream_t s);
 void launch_fill_u32(uint32_t* p, uint32_t v, uint64_t n, hipStream_t s);
 void launch_fill_i32(int32_t* p, int32_t v, uint64_t n, hipStream_t s);
 

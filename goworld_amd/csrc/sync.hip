@@ -331,20 +331,27 @@ void launch_gather_records(const gw_sync_record* in, const uint32_t* idx, const 
 // ---------------------------------------------------------------------------
 // client attach / detach (GameClient.go:14-27): the gate copy in the grid entry
 // is patched too, so a collect after set_clients sees the new gates
+// gate[] always; the CLIENT_BIT of the slot's grid entry only while the grid
+// is current (grid_ok: a rebuild takes the bits from gate[] anyway, and gidx
+// of slots entered since the last build is not valid)
 __global__ void __launch_bounds__(NT) k_set_clients(World w, const uint32_t* slots, const uint16_t* gates,
-                                                    uint32_t n) {
+                                                    uint32_t n, int grid_ok) {
     uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i >= n || slots[i] >= w.cap) return;
     const uint32_t s = slots[i];
     w.gate[s] = gates[i];
-    if (w.aoi[s].meta & PRESENT_BIT) {
-        GEnt* g = w.gn + w.gidx[s];
-        if (g->slot == s) g->meta = (g->meta & ~CLIENT_BIT) | (gates[i] ? CLIENT_BIT : 0u);
+    if (grid_ok && (w.aoi[s].meta & PRESENT_BIT)) {
+        const uint32_t k = w.gidx[s];
+        if (k < w.cap) {
+            GEnt* g = w.gn + k;
+            if (g->slot == s) g->meta = (g->meta & ~CLIENT_BIT) | (gates[i] ? CLIENT_BIT : 0u);
+        }
     }
 }
-void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n, hipStream_t s) {
+void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n, bool grid_ok,
+                        hipStream_t s) {
     if (!n) return;
-    hipLaunchKernelGGL(k_set_clients, dim3(nblk(n, NT)), dim3(NT), 0, s, w, slots, gates, n);
+    hipLaunchKernelGGL(k_set_clients, dim3(nblk(n, NT)), dim3(NT), 0, s, w, slots, gates, n, grid_ok ? 1 : 0);
 }
 
 // InterestedIn(slot) (== InterestedBy): related slots, unordered

@@ -93,6 +93,7 @@ def lib():
         L.gw_set_clients.argtypes = [vp, vp, vp, _u32]
         L.gw_tick.argtypes = [vp, _u32, C.POINTER(TickOut)]
         L.gw_tick_result.argtypes = [vp, C.POINTER(TickOut)]
+        L.gw_space_restore.argtypes = [vp, _u32, vp, vp, vp, vp, vp, _u32, C.c_uint8]
         L.gw_sync_collect.argtypes = [vp, _u32, C.POINTER(SyncOut)]
         L.gw_neighbors.argtypes = [vp, _u32, vp, _u32, C.POINTER(_u32)]
         L.gw_set_profiling.argtypes = [vp, C.c_int]
@@ -118,7 +119,7 @@ EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_spa
             "gw_sync_collect", "gw_neighbors", "gw_set_profiling", "gw_get_stage_times",
             "gw_total_neighbors", "gw_device_alloc", "gw_device_free", "gw_memcpy_h2d",
             "gw_memcpy_d2h", "gw_synchronize", "gw_submit_device_stamped", "gw_space_set_ownership",
-            "gw_set_stream", "gw_route_halo", "gw_submit_device_rows", "gw_halo_status", "gw_tick_result"]
+            "gw_set_stream", "gw_route_halo", "gw_submit_device_rows", "gw_halo_status", "gw_tick_result", "gw_space_restore"]
 
 
 def _p(a: np.ndarray):
@@ -199,6 +200,12 @@ class GpuAOI:
 
     def destroy_space(self, sid: int):
         self._chk(lib().gw_space_destroy(self._h, sid))
+
+    def restore(self, sid: int, slots, x, y, z, yaw, flags: int = 3):
+        """Bulk Enter in index order without events (restore path, Space.go:209-214)."""
+        a = [np.ascontiguousarray(v, dtype=t) for v, t in
+             ((slots, np.uint32), (x, np.float32), (y, np.float32), (z, np.float32), (yaw, np.float32))]
+        self._chk(lib().gw_space_restore(self._h, sid, *[_p(v) for v in a], len(a[0]), flags))
 
     def submit(self, ops: np.ndarray):
         ops = np.ascontiguousarray(ops, dtype=OP_DTYPE)
@@ -328,18 +335,21 @@ class GpuAOI:
         self._chk(lib().gw_synchronize(self._h))
 
 
-def load_space(g: GpuAOI, tr, bounds=None, chunk: int = 1 << 21) -> tuple[int, int]:
-    """Create a space for a SpaceTrace and bulk-load its initial population.
-
-    The bulk load is Enter ops in trace order, flushed in chunks with
-    TICK_NO_EVENTS (the restore path, Space.go:209-214); ticks compose, so
-    chunking equals one sequential Enter stream."""
+def load_space(g: GpuAOI, tr, bounds=None, chunk: int = 1 << 21, via_ticks: bool = False) -> tuple[int, int]:
+    """Create a space for a SpaceTrace and bulk-load its initial population
+    (the restore path, Space.go:209-214): gw_space_restore, or (via_ticks)
+    Enter ops in trace order flushed in chunks with TICK_NO_EVENTS; both equal
+    one sequential Enter stream."""
     from .traces import enter_ops, with_global_slots
     sid, base = g.create_space(tr.d, tr.capacity, bounds if bounds is not None else tr.bounds)
-    ops = with_global_slots(enter_ops(tr.init_slots, tr.init_x, tr.init_y, tr.init_z, tr.init_yaw), base)
-    for i in range(0, len(ops), chunk):
-        g.submit(ops[i:i + chunk])
-        g.tick(copy=False, no_events=True)
+    if via_ticks:
+        ops = with_global_slots(enter_ops(tr.init_slots, tr.init_x, tr.init_y, tr.init_z, tr.init_yaw), base)
+        for i in range(0, len(ops), chunk):
+            g.submit(ops[i:i + chunk])
+            g.tick(copy=False, no_events=True)
+    else:
+        g.restore(sid, np.asarray(tr.init_slots, np.uint32) + np.uint32(base), tr.init_x, tr.init_y, tr.init_z,
+                  tr.init_yaw)
     if tr.gates is not None:
         nz = np.nonzero(tr.gates)[0]
         g.set_clients(nz.astype(np.uint32) + base, tr.gates[nz])

@@ -234,6 +234,16 @@ int  gw_submit_device_rows(gw_ctx* ctx, const gw_halo_row* dev_rows, uint32_t n)
  * then resets them). */
 int  gw_halo_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops);
 
+/* Restore / bulk load (Space.go:209-214 restoreEntity, EntityManager.go:
+ * 556-617 freeze/restore): entities slots[i] enter space
+ * space_id at (x, z) exactly as n Enter calls in index order would, without
+ * events (the restore path fires none), their syncInfoFlag ORed with
+ * sync_flags (GW_SIF_*; Space.enter sets both, Space.go:196).  One upload,
+ * one kernel and one grid rebuild instead of n ops and a tick.  No ops may be
+ * pending; slots must be absent and distinct (all-or-nothing). */
+int  gw_space_restore(gw_ctx* ctx, uint32_t space_id, const uint32_t* slots, const float* x, const float* y,
+                      const float* z, const float* yaw, uint32_t n, uint8_t sync_flags);
+
 /* Attach / detach clients: gate 0 = no client (GameClient nil). */
 int  gw_set_clients(gw_ctx* ctx, const uint32_t* slots, const uint16_t* gates, uint32_t n);
 
@@ -284,7 +294,7 @@ int  gw_synchronize(gw_ctx* ctx);
 int  gw_set_stream(gw_ctx* ctx, void* hip_stream);
 
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 6
+#define GW_ABI_VERSION 7
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

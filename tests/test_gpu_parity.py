@@ -460,3 +460,31 @@ def test_clients_change_between_tick_and_collect(ctx_factory):
         for s, gg in zip(sel.tolist(), newg.tolist()):
             h.orcs[0].set_client(s, gg)
         h.check_collect()
+
+
+def test_restore_equals_enter_ticks(ctx_factory):
+    """gw_space_restore (freeze/restore bulk path) leaves the
+    same state as the Enter ops flushed with TICK_NO_EVENTS: identical events,
+    records and neighbour lists over the following ticks; bad restores raise."""
+    tr = T.adversarial_trace(41, n=600, ticks=4)
+    outs = []
+    for via in (False, True):
+        g = ctx_factory()
+        sid, base = gpuaoi.load_space(g, tr, via_ticks=via)
+        seq = [g.sync_collect().records.tobytes()]
+        for ops in tr.ticks:
+            g.submit(ops)
+            r = g.tick()
+            seq.append((r.enter.tobytes(), r.leave.tobytes(), g.sync_collect().records.tobytes()))
+        seq.append([g.neighbors(s).tobytes() for s in range(0, tr.capacity, 7)])
+        outs.append(seq)
+        if not via:
+            with pytest.raises(gpuaoi.GwError):      # already present
+                g.restore(sid, [base], [0.0], [0.0], [0.0], [0.0])
+    assert outs[0] == outs[1]
+    g = ctx_factory()
+    sid, base = g.create_space(100.0, 8)
+    with pytest.raises(gpuaoi.GwError):              # duplicate slot in one restore
+        g.restore(sid, [base, base], [0.0, 1.0], [0.0, 0.0], [0.0, 0.0], [0.0, 0.0])
+    with pytest.raises(gpuaoi.GwError):              # outside the space
+        g.restore(sid, [base + 8], [0.0], [0.0], [0.0], [0.0])

@@ -32,19 +32,17 @@ def gpu():
 
 
 def canonical(recs: np.ndarray, gates: np.ndarray) -> np.ndarray:
-    """Records in (gate(watcher), entity, watcher) order.  One u64 key
-    (gate 16 | entity 24 | watcher 24 bits) sorted on the device: the 1M
-    config's load collect holds ~1.5e8 records."""
-    import torch
+    """Records in (gate(watcher), entity, watcher) order via one u64 key
+    (gate 16 | entity 24 | watcher 24 bits).  The GPU stream is already in
+    (gate, entity) order with only the watchers of an entity permuted, so the
+    stable (run-merging) sort is near linear even for the 1M config's load
+    collect (~1.5e8 records)."""
     if len(recs) == 0:
         return recs
     assert len(gates) <= 1 << 24
     key = (gates[recs["watcher"]].astype(np.uint64) << np.uint64(48)) | \
         (recs["entity"].astype(np.uint64) << np.uint64(24)) | recs["watcher"].astype(np.uint64)
-    kt = torch.from_numpy(key.view(np.int64)).to("cuda")          # keys < 2**63: order kept
-    order = torch.argsort(kt).cpu().numpy()
-    del kt
-    return recs[order]
+    return recs[np.argsort(key, kind="stable")]
 
 
 @pytest.mark.parametrize("name", G.SMALL)

@@ -121,6 +121,12 @@ struct gw_ctx {
     DevBuf fbits, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
     DevBuf cl_slot, cl_off, h_cl_slot, h_cl_off;   // GW_SYNC_BY_CLIENT segments (device / pinned host)
     uint64_t rec_cap = 0;                // records the rec0 buffer holds (grows on overflow)
+    // client messages (gw_client_events, gw_fanout): ping-pong + pinned host + gate offsets
+    struct MsgBufs {
+        DevBuf a, b, h;
+        std::vector<uint64_t> goff;
+    } m_create, m_destroy, m_fanout;
+    DevBuf m_flag, m_at, m_items, m_cnt, m_off;
     uint32_t* scal32 = nullptr;    // small device scalars
 
     // host mirror for validation of host-submitted ops
@@ -563,9 +569,12 @@ void gw_shutdown(gw_ctx* c) {
                       &c->mir_cnt,
                       &c->enter_d, &c->leave_d, &c->scan_status, &c->rs_hist,
                       &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
-                      &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf, &c->cl_slot, &c->cl_off};
+                      &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf, &c->cl_slot, &c->cl_off,
+                      &c->m_create.a, &c->m_create.b, &c->m_destroy.a, &c->m_destroy.b, &c->m_fanout.a,
+                      &c->m_fanout.b, &c->m_flag, &c->m_at, &c->m_items, &c->m_cnt, &c->m_off};
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
-    DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off};
+    DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off, &c->m_create.h,
+                    &c->m_destroy.h, &c->m_fanout.h};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
     void* ps[] = {c->halo, c->rflag, c->sc.ticket, c->ownbits, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->nbc, c->last_pos, c->last_aoi,
                   c->last_leave, c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->cstats, c->scal32, c->gsb[0],
@@ -1210,6 +1219,141 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         HIPCHK(hipStreamSynchronize(c->st));
         out->rec = (const gw_sync_record*)c->h_rec.p;
     }
+    return 0;
+}
+
+// ---- client messages -------------------------------
+// Stable grouping of R records of `words` u32 in m.a (first word = watcher):
+// by watcher first (by_watcher), then by gate(watcher); m.goff = gate offsets.
+static int group_msgs(gw_ctx* c, gw_ctx::MsgBufs& m, uint64_t R, int words, bool by_watcher) {
+    const uint32_t G = (uint32_t)c->max_gate + 1;
+    m.goff.assign((size_t)G + 1, 0);
+    if (!R) return 0;
+    int rc;
+    if ((rc = ensure(c, c->gk0, R * 4)) || (rc = ensure(c, c->gv0, R * 4)) || (rc = ensure(c, c->gk1, R * 4)) ||
+        (rc = ensure(c, c->gv1, R * 4)) || (rc = ensure(c, m.b, R * words * 4)))
+        return rc;
+    RadixTmp rt;
+    if ((rc = radix_tmp(c, R, rt))) return rc;
+    auto sort_by = [&](const uint16_t* gate, int bits) {
+        launch_msg_keys(P<uint32_t>(m.a), words, R, gate, P<uint32_t>(c->gk0), P<uint32_t>(c->gv0), c->st);
+        const int sel = sort_u32_u32(P<uint32_t>(c->gk0), P<uint32_t>(c->gv0), P<uint32_t>(c->gk1),
+                                     P<uint32_t>(c->gv1), R, nullptr, 0, bits, rt, c->st);
+        launch_msg_gather(P<uint32_t>(m.a), words, sel ? P<uint32_t>(c->gv1) : P<uint32_t>(c->gv0), R,
+                          P<uint32_t>(m.b), c->st);
+        std::swap(m.a, m.b);
+    };
+    if (by_watcher && R > 1) sort_by(nullptr, ceil_log2(c->total_slots));
+    if (G > 2) {
+        if ((rc = ensure(c, c->gate_hist, (size_t)65536 * 4))) return rc;
+        HIPCHK(hipMemsetAsync(c->gate_hist.p, 0, (size_t)G * 4, c->st));
+        launch_msg_gate_hist(P<uint32_t>(m.a), words, R, c->gate, P<uint32_t>(c->gate_hist), c->st);
+        std::vector<uint32_t> h(G);
+        HIPCHK(hipMemcpyAsync(h.data(), c->gate_hist.p, (size_t)G * 4, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        uint32_t nonzero = 0;
+        uint64_t acc = 0;
+        for (uint32_t g = 0; g < G; ++g) { nonzero += h[g] != 0; m.goff[g] = acc; acc += h[g]; }
+        m.goff[G] = acc;
+        if (nonzero > 1) sort_by(c->gate, ceil_log2(G));
+    } else {
+        for (uint32_t g = 0; g <= G; ++g) m.goff[g] = (g == G) ? R : 0;   // one gate id in use
+    }
+    return 0;
+}
+
+static int msg_out(gw_ctx* c, gw_ctx::MsgBufs& m, uint64_t R, int words, uint32_t flags, gw_msg_out* o) {
+    o->rec_dev = m.a.p;
+    o->n_rec = R;
+    o->gate_off = m.goff.data();
+    o->n_gates = (uint32_t)m.goff.size() - 1;
+    o->bytes_alg = R * words * 4;
+    if (flags & GW_MSG_COPY_TO_HOST) {
+        int rc;
+        if ((rc = ensure_host(c, m.h, std::max<uint64_t>(R, 1) * words * 4))) return rc;
+        if (R) HIPCHK(hipMemcpyAsync(m.h.p, m.a.p, R * words * 4, hipMemcpyDeviceToHost, c->st));
+        o->rec = m.h.p;
+    }
+    return 0;
+}
+
+int gw_client_events(gw_ctx* c, uint32_t flags, gw_msg_out* create, gw_msg_out* destroy) {
+    if (!c || !create || !destroy) return GW_EINVAL;
+    int rc;
+    if ((rc = settle(c))) return rc;
+    (void)hipSetDevice(c->dev);
+    memset(create, 0, sizeof *create);
+    memset(destroy, 0, sizeof *destroy);
+    HIPCHK(hipEventRecord(c->ev_t0, c->st));
+    const gw_tick_out& t = c->last_out;
+    const gw_event* evs[2] = {t.enter_dev, t.leave_dev};
+    const uint64_t ns[2] = {evs[0] ? t.n_enter : 0, evs[1] ? t.n_leave : 0};
+    gw_ctx::MsgBufs* ms[2] = {&c->m_create, &c->m_destroy};
+    gw_msg_out* outs[2] = {create, destroy};
+    for (int k = 0; k < 2; ++k) {
+        const uint64_t n = ns[k];
+        const int words = k == 0 ? 6 : 2;
+        gw_ctx::MsgBufs& m = *ms[k];
+        uint32_t R = 0;
+        if (n) {
+            if (n >= 0xffffffffull) return set_err(c, GW_ERANGE, "too many events (%llu)", (unsigned long long)n);
+            if ((rc = ensure(c, c->m_flag, n * 4)) || (rc = ensure(c, c->m_at, n * 4)) || (rc = ensure_scan(c, n)) ||
+                (rc = ensure(c, m.a, n * words * 4)))
+                return rc;
+            launch_event_client_flags(evs[k], n, c->gate, P<uint32_t>(c->m_flag), c->st);
+            scan_u32_u32(P<uint32_t>(c->m_flag), P<uint32_t>(c->m_at), n, nullptr, c->sc, c->scal32 + 2, c->st);
+            launch_event_client_write(evs[k], n, P<uint32_t>(c->m_flag), P<uint32_t>(c->m_at), c->pos,
+                                      P<uint32_t>(m.a), k == 0, c->st);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(&R, c->scal32 + 2, 4, hipMemcpyDeviceToHost, c->st));
+            HIPCHK(hipStreamSynchronize(c->st));
+        }
+        if ((rc = group_msgs(c, m, R, words, false)) || (rc = msg_out(c, m, R, words, flags, outs[k]))) return rc;
+        outs[k]->bytes_alg += n * 8;
+    }
+    HIPCHK(hipEventRecord(c->ev_t1, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    float ms_ = 0;
+    (void)hipEventElapsedTime(&ms_, c->ev_t0, c->ev_t1);
+    create->device_us = destroy->device_us = ms_ * 1000.0;
+    return 0;
+}
+
+int gw_fanout(gw_ctx* c, const uint32_t* slots, uint32_t n, uint32_t flags, gw_msg_out* out) {
+    if (!c || !out || (n && !slots)) return GW_EINVAL;
+    int rc;
+    if ((rc = settle(c))) return rc;
+    (void)hipSetDevice(c->dev);
+    memset(out, 0, sizeof *out);
+    for (uint32_t k = 0; k < n; ++k)
+        if (slots[k] >= c->total_slots) return set_err(c, GW_ERANGE, "fanout: slot %u out of range", slots[k]);
+    HIPCHK(hipEventRecord(c->ev_t0, c->st));
+    gw_ctx::MsgBufs& m = c->m_fanout;
+    uint64_t R = 0;
+    if (n) {
+        if ((rc = rebuild_grid(c))) return rc;
+        if ((rc = ensure(c, c->m_items, (size_t)n * 4)) || (rc = ensure(c, c->m_cnt, (size_t)n * 4)) ||
+            (rc = ensure(c, c->m_off, ((size_t)n + 1) * 8)) || (rc = ensure_scan(c, n)))
+            return rc;
+        HIPCHK(hipMemcpyAsync(c->m_items.p, slots, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
+        const World w = world(c);
+        launch_fanout(w, P<uint32_t>(c->m_items), n, P<uint32_t>(c->m_cnt), nullptr, nullptr, c->st);
+        uint64_t* tot = P<uint64_t>(c->m_off) + n;   // the total lands after the offsets
+        scan_u32_u64(P<uint32_t>(c->m_cnt), P<uint64_t>(c->m_off), n, nullptr, c->sc, tot, c->st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&R, tot, 8, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        if ((rc = ensure(c, m.a, std::max<uint64_t>(R, 1) * sizeof(gw_fanout_rec)))) return rc;
+        launch_fanout(w, P<uint32_t>(c->m_items), n, nullptr, P<uint64_t>(c->m_off), P<gw_fanout_rec>(m.a), c->st);
+        HIPCHK(hipGetLastError());
+    }
+    if ((rc = group_msgs(c, m, R, 3, true)) || (rc = msg_out(c, m, R, 3, flags, out))) return rc;
+    out->bytes_alg += (uint64_t)n * 4;
+    HIPCHK(hipEventRecord(c->ev_t1, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    float ms_ = 0;
+    (void)hipEventElapsedTime(&ms_, c->ev_t0, c->ev_t1);
+    out->device_us = ms_ * 1000.0;
     return 0;
 }
 

@@ -240,6 +240,19 @@ void launch_client_segments(const gw_sync_record* rec, uint64_t n, uint32_t* hea
                             hipStream_t s);
 void launch_restore(const World& w, const uint32_t* slots, const float4* xyzw, uint32_t n,
                     unsigned long long stamp_base, uint32_t flags, hipStream_t s);
+// client messages (sync.hip)
+void launch_event_client_flags(const gw_event* ev, uint64_t n, const uint16_t* gate, uint32_t* f, hipStream_t s);
+void launch_event_client_write(const gw_event* ev, uint64_t n, const uint32_t* f, const uint32_t* at,
+                               const float4* pos, uint32_t* out, bool create, hipStream_t s);
+// out == nullptr: counts per item into cnt; else deliveries at off[k]
+void launch_fanout(const World& w, const uint32_t* items, uint32_t n, uint32_t* cnt, const uint64_t* off,
+                   gw_fanout_rec* out, hipStream_t s);
+void launch_msg_keys(const uint32_t* rec, int words, uint64_t n, const uint16_t* gate, uint32_t* keys, uint32_t* vals,
+                     hipStream_t s);   // gate == nullptr: key = watcher
+void launch_msg_gate_hist(const uint32_t* rec, int words, uint64_t n, const uint16_t* gate, uint32_t* hist,
+                          hipStream_t s);
+void launch_msg_gather(const uint32_t* in, int words, const uint32_t* idx, uint64_t n, uint32_t* out,
+                       hipStream_t s);
 void launch_fill_u32(uint32_t* p, uint32_t v, uint64_t n, hipStream_t s);
 void launch_fill_i32(int32_t* p, int32_t v, uint64_t n, hipStream_t s);
 

@@ -399,6 +399,158 @@ void launch_fill_i32(int32_t* p, int32_t v, uint64_t n, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
+// Client messages.  Records are runs of W u32 words
+// whose first word is the receiving watcher slot.
+//
+// (a) AOI events -> client messages: Entity.interest / uninterest call
+// e.client.sendCreateEntity(other) / sendDestroyEntity(other), a no-op when the
+// watcher has no client (Entity.go:236-246, GameClient.go:37-59).  A flag per
+// canonical event, a scan, and a write pass that keeps the (watcher, target)
+// order; creates carry the target's position and yaw (GameClient.go:49-52).
+__global__ void __launch_bounds__(NT) k_event_client_flags(const gw_event* __restrict__ ev, uint64_t n,
+                                                           const uint16_t* __restrict__ gate, uint32_t* f) {
+    const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (r < n) f[r] = gate[ev[r].watcher] != 0 ? 1u : 0u;
+}
+__global__ void __launch_bounds__(NT) k_event_client_write(const gw_event* __restrict__ ev, uint64_t n,
+                                                           const uint32_t* __restrict__ f,
+                                                           const uint32_t* __restrict__ at,
+                                                           const float4* __restrict__ pos, uint32_t* out,
+                                                           int create) {
+    const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (r >= n || !f[r]) return;
+    const gw_event e = ev[r];
+    if (create) {
+        const float4 p = pos[e.target];
+        gw_sync_record m;
+        m.watcher = e.watcher; m.entity = e.target; m.x = p.x; m.y = p.y; m.z = p.z; m.yaw = p.w;
+        ((gw_sync_record*)out)[at[r]] = m;
+    } else {
+        ((gw_event*)out)[at[r]] = e;
+    }
+}
+void launch_event_client_flags(const gw_event* ev, uint64_t n, const uint16_t* gate, uint32_t* f, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_event_client_flags, dim3(nblk(n, NT)), dim3(NT), 0, s, ev, n, gate, f);
+}
+void launch_event_client_write(const gw_event* ev, uint64_t n, const uint32_t* f, const uint32_t* at,
+                               const float4* pos, uint32_t* out, bool create, hipStream_t s) {
+    if (n)
+        hipLaunchKernelGGL(k_event_client_write, dim3(nblk(n, NT)), dim3(NT), 0, s, ev, n, f, at, pos, out,
+                           create ? 1 : 0);
+}
+
+// (b) AllClients fan-out: CallAllClients and every AllClients attribute
+// notification send to e.client, then to n.client for n in e.InterestedBy
+// (Entity.go:743-749, 814-917).  Item k (entity items[k]) -> deliveries
+// {watcher, entity, k}: the own one first, then the related entities with a
+// client, from the current grid (one wave per item, like the collect).
+template <int U>
+__global__ void __launch_bounds__(NT) k_fanout_count(World w, const uint32_t* __restrict__ items, uint32_t n,
+                                                     uint32_t* cnt) {
+    const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
+    for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < n; k += stride) {
+        const uint32_t e = items[k];
+        uint32_t r = w.gate[e] ? 1u : 0u;
+        wave_neighbors<U>(w, e, [&](bool rel, uint32_t, uint32_t g) {
+            r += (uint32_t)popc64(wave_ballot(rel && g != 0));
+        });
+        if (lane_id() == 0) cnt[k] = r;
+    }
+}
+template <int U>
+__global__ void __launch_bounds__(NT) k_fanout_write(World w, const uint32_t* __restrict__ items, uint32_t n,
+                                                     const uint64_t* __restrict__ off, gw_fanout_rec* out) {
+    const uint64_t lt = lanemask_lt();
+    const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
+    for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < n; k += stride) {
+        const uint32_t e = items[k];
+        uint64_t at = off[k];
+        if (w.gate[e]) {
+            if (lane_id() == 0) {
+                gw_fanout_rec m;
+                m.watcher = e; m.entity = e; m.item = (uint32_t)k;
+                out[at] = m;
+            }
+            ++at;
+        }
+        wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
+            const bool take = rel && g != 0;
+            const uint64_t bt = wave_ballot(take);
+            if (take) {
+                gw_fanout_rec m;
+                m.watcher = ws; m.entity = e; m.item = (uint32_t)k;
+                out[at + (uint64_t)popc64(bt & lt)] = m;
+            }
+            at += (uint64_t)popc64(bt);
+        });
+    }
+}
+void launch_fanout(const World& w, const uint32_t* items, uint32_t n, uint32_t* cnt, const uint64_t* off,
+                   gw_fanout_rec* out, hipStream_t s) {
+    if (!n) return;
+    const dim3 g(std::min(nblk(n, NWAVE), SYNC_MAX_BLOCKS));
+    if (!out) hipLaunchKernelGGL(k_fanout_count<4>, g, dim3(NT), 0, s, w, items, n, cnt);
+    else hipLaunchKernelGGL(k_fanout_write<4>, g, dim3(NT), 0, s, w, items, n, off, out);
+}
+
+// (c) stable grouping of a message stream: keys (watcher, or gate(watcher)),
+// gather of W-word records by the sorted indices (one thread per output word)
+template <int W>
+__global__ void __launch_bounds__(NT) k_msg_keys(const uint32_t* __restrict__ rec, uint64_t n,
+                                                 const uint16_t* __restrict__ gate, uint32_t* keys, uint32_t* vals) {
+    const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t w = rec[r * W];
+    keys[r] = gate ? (uint32_t)gate[w] : w;
+    vals[r] = (uint32_t)r;
+}
+template <int W>
+__global__ void __launch_bounds__(NT) k_msg_gate_hist(const uint32_t* __restrict__ rec, uint64_t n,
+                                                      const uint16_t* __restrict__ gate, uint32_t* hist) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x; r < n; r += (uint64_t)gridDim.x * NT) {
+        const uint32_t g = gate[rec[r * W]];
+        if (g < 256) atomicAdd(&h[g], 1u); else atomicAdd(&hist[g], 1u);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+template <int W>
+__global__ void __launch_bounds__(NT) k_msg_gather(const uint32_t* __restrict__ in, const uint32_t* __restrict__ idx,
+                                                   uint64_t n, uint32_t* out) {
+    const uint64_t t = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (t >= n * W) return;
+    const uint64_t r = t / W;
+    out[t] = in[(uint64_t)idx[r] * W + (t - r * W)];
+}
+#define GW_MSG_W(words, stmt)                      \
+    switch (words) {                               \
+    case 2: { constexpr int W = 2; stmt; } break;  \
+    case 3: { constexpr int W = 3; stmt; } break;  \
+    default: { constexpr int W = 6; stmt; } break; \
+    }
+void launch_msg_keys(const uint32_t* rec, int words, uint64_t n, const uint16_t* gate, uint32_t* keys, uint32_t* vals,
+                     hipStream_t s) {
+    if (!n) return;
+    GW_MSG_W(words, hipLaunchKernelGGL(k_msg_keys<W>, dim3(nblk(n, NT)), dim3(NT), 0, s, rec, n, gate, keys, vals));
+}
+void launch_msg_gate_hist(const uint32_t* rec, int words, uint64_t n, const uint16_t* gate, uint32_t* hist,
+                          hipStream_t s) {
+    if (!n) return;
+    uint32_t nb = nblk1(n, NT * 16);
+    if (nb > 2048) nb = 2048;
+    GW_MSG_W(words, hipLaunchKernelGGL(k_msg_gate_hist<W>, dim3(nb), dim3(NT), 0, s, rec, n, gate, hist));
+}
+void launch_msg_gather(const uint32_t* in, int words, const uint32_t* idx, uint64_t n, uint32_t* out,
+                       hipStream_t s) {
+    if (!n) return;
+    GW_MSG_W(words, hipLaunchKernelGGL(k_msg_gather<W>, dim3(nblk(n * W, NT)), dim3(NT), 0, s, in, idx, n, out));
+}
+#undef GW_MSG_W
+
+// ---------------------------------------------------------------------------
 // primitive instantiations for the host code
 uint64_t radix_tile() { return RS_TILE; }
 uint64_t scan_tile() { return SCAN_TILE; }

@@ -30,7 +30,10 @@ EVENT_DTYPE = np.dtype([("watcher", "<u4"), ("target", "<u4")])
 REC_DTYPE = np.dtype([("watcher", "<u4"), ("entity", "<u4"), ("x", "<f4"), ("y", "<f4"),
                       ("z", "<f4"), ("yaw", "<f4")])
 
+FANOUT_DTYPE = np.dtype([("watcher", "<u4"), ("entity", "<u4"), ("item", "<u4")])
+
 TICK_COPY_TO_HOST, TICK_NO_EVENTS, TICK_DEFER = 1, 2, 4
+MSG_COPY_TO_HOST = 1
 SYNC_COPY_TO_HOST, SYNC_BY_CLIENT = 1, 2
 MAX_STAGES = 32
 
@@ -50,6 +53,11 @@ class SyncOut(C.Structure):
                 ("bytes_alg", _u64), ("device_us", _f64), ("n_clients", _u32),
                 ("client_slot", C.POINTER(_u32)), ("client_off", C.POINTER(_u64)),
                 ("client_slot_dev", C.c_void_p), ("client_off_dev", C.c_void_p)]
+
+
+class MsgOut(C.Structure):
+    _fields_ = [("rec", C.c_void_p), ("rec_dev", C.c_void_p), ("n_rec", _u64), ("gate_off", C.POINTER(_u64)),
+                ("n_gates", _u32), ("bytes_alg", _u64), ("device_us", _f64)]
 
 
 class StageTimes(C.Structure):
@@ -110,6 +118,8 @@ def lib():
         L.gw_route_halo.argtypes = [vp, vp, vp, _u32, C.c_float, C.POINTER(HaloDst), _u32]
         L.gw_submit_device_rows.argtypes = [vp, vp, _u32]
         L.gw_halo_status.argtypes = [vp, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64)]
+        L.gw_client_events.argtypes = [vp, _u32, C.POINTER(MsgOut), C.POINTER(MsgOut)]
+        L.gw_fanout.argtypes = [vp, vp, _u32, _u32, C.POINTER(MsgOut)]
         _lib = L
     return _lib
 
@@ -119,7 +129,8 @@ EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_spa
             "gw_sync_collect", "gw_neighbors", "gw_set_profiling", "gw_get_stage_times",
             "gw_total_neighbors", "gw_device_alloc", "gw_device_free", "gw_memcpy_h2d",
             "gw_memcpy_d2h", "gw_synchronize", "gw_submit_device_stamped", "gw_space_set_ownership",
-            "gw_set_stream", "gw_route_halo", "gw_submit_device_rows", "gw_halo_status", "gw_tick_result", "gw_space_restore"]
+            "gw_set_stream", "gw_route_halo", "gw_submit_device_rows", "gw_halo_status", "gw_tick_result", "gw_space_restore",
+            "gw_client_events", "gw_fanout"]
 
 
 def _p(a: np.ndarray):
@@ -154,6 +165,14 @@ class SyncResult:
     rec_dev: int = 0
     client_slot: np.ndarray | None = None     # by_client: watcher slot of each client segment
     client_off: np.ndarray | None = None      # by_client: n_clients + 1 offsets into records
+
+
+@dataclasses.dataclass
+class MsgResult:
+    records: np.ndarray
+    gate_off: np.ndarray
+    bytes_alg: int
+    device_us: float
 
 
 class GpuAOI:
@@ -290,6 +309,30 @@ class GpuAOI:
             res.client_slot = np.ctypeslib.as_array(o.client_slot, (max(n, 1),))[:n].copy()
             res.client_off = np.ctypeslib.as_array(o.client_off, (n + 1,)).copy()
         return res
+
+    @staticmethod
+    def _msgs(o: MsgOut, dtype) -> MsgResult:
+        r = np.zeros(o.n_rec, dtype)
+        if o.n_rec:
+            C.memmove(_p(r), o.rec, o.n_rec * dtype.itemsize)
+        goff = np.array([o.gate_off[i] for i in range(o.n_gates + 1)], dtype=np.uint64)
+        return MsgResult(r, goff, o.bytes_alg, o.device_us)
+
+    def client_events(self) -> tuple[MsgResult, MsgResult]:
+        """Client messages of the last tick's events (Entity.interest/uninterest,
+        Entity.go:236-246): creates (REC_DTYPE: watcher, target, target's x,y,z,yaw)
+        and destroys (EVENT_DTYPE), each grouped (gate, watcher, target)."""
+        cr, de = MsgOut(), MsgOut()
+        self._chk(lib().gw_client_events(self._h, MSG_COPY_TO_HOST, C.byref(cr), C.byref(de)))
+        return self._msgs(cr, REC_DTYPE), self._msgs(de, EVENT_DTYPE)
+
+    def fanout(self, slots) -> MsgResult:
+        """AllClients fan-out of calls on slots[k] (Entity.CallAllClients,
+        Entity.go:743-749): FANOUT_DTYPE records grouped (gate, watcher, call)."""
+        s = np.ascontiguousarray(slots, dtype=np.uint32)
+        o = MsgOut()
+        self._chk(lib().gw_fanout(self._h, _p(s), len(s), MSG_COPY_TO_HOST, C.byref(o)))
+        return self._msgs(o, FANOUT_DTYPE)
 
     def neighbors(self, slot: int) -> np.ndarray:
         n = _u32()

@@ -277,6 +277,52 @@ typedef struct gw_stage_times {
 int  gw_set_profiling(gw_ctx* ctx, int enable);   /* 0 off, 1 every stage, 2 the "diff" stage only */
 int  gw_get_stage_times(gw_ctx* ctx, gw_stage_times* out);
 
+/* ---- client messages ------------------------------
+ * Streams of messages to clients, each grouped by the receiving client's gate
+ * (gate_off partitions rec by gate id, n_gates = max gate id + 1) and, inside
+ * a gate, ordered by receiving watcher slot: one contiguous run per client, in
+ * the order the reference's calls reach that client.  Only watchers with a
+ * client receive anything (GameClient methods are no-ops on a nil client,
+ * GameClient.go:37-59).  Pointers stay valid until the next call of the same
+ * entry point. */
+#define GW_MSG_COPY_TO_HOST   1u
+
+typedef struct gw_msg_out {
+    const void* rec;              /* host (GW_MSG_COPY_TO_HOST), else NULL      */
+    const void* rec_dev;          /* device, always valid                       */
+    uint64_t n_rec;
+    const uint64_t* gate_off;     /* host: n_gates + 1 offsets into rec         */
+    uint32_t n_gates;
+    uint64_t bytes_alg;           /* records written (+ inputs read)            */
+    double   device_us;
+} gw_msg_out;
+
+/* Enter/leave events of the last gw_tick turned into the client messages
+ * Entity.interest / uninterest send (Entity.go:236-246):
+ *   create:  gw_sync_record {watcher, entity = target, x, y, z, yaw of the
+ *            target} = GameClient.sendCreateEntity(target, isPlayer=false)
+ *            -> MT_CREATE_ENTITY_ON_CLIENT (GameClient.go:37-53,
+ *            GoWorldConnection.go:138-153; the host adds type and the
+ *            msgpack'd AllClients attributes)
+ *   destroy: gw_event {watcher, target} = sendDestroyEntity(target)
+ *            -> MT_DESTROY_ENTITY_ON_CLIENT (GameClient.go:55-59)
+ * Order: (gate(watcher), watcher, target).  Positions are those at the flush. */
+int  gw_client_events(gw_ctx* ctx, uint32_t flags, gw_msg_out* create, gw_msg_out* destroy);
+
+/* AllClients fan-out: n calls, call k on entity slots[k] (Entity.CallAllClients
+ * Entity.go:743-749, and every AllClients attribute notification
+ * sendMap/ListAttr*ToClients, Entity.go:814-917) reach the entity's own client
+ * and the client of every n in InterestedBy (as of the last flush).  Output:
+ * gw_fanout_rec {watcher, entity, item = k}, order (gate(watcher), watcher, k),
+ * so each client's run lists its calls in call order.  Slots must be in range;
+ * an entity outside any AOI space reaches only its own client. */
+typedef struct gw_fanout_rec {
+    uint32_t watcher;     /* slot whose client receives the call                 */
+    uint32_t entity;      /* slots[item]                                          */
+    uint32_t item;        /* index of the call                                    */
+} gw_fanout_rec;
+int  gw_fanout(gw_ctx* ctx, const uint32_t* slots, uint32_t n, uint32_t flags, gw_msg_out* out);
+
 /* Total neighbour-list entries held (sum over slots of |InterestedIn|). */
 int  gw_total_neighbors(gw_ctx* ctx, uint64_t* out);
 
@@ -294,7 +340,7 @@ int  gw_synchronize(gw_ctx* ctx);
 int  gw_set_stream(gw_ctx* ctx, void* hip_stream);
 
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 7
+#define GW_ABI_VERSION 8
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

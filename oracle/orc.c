@@ -721,3 +721,78 @@ int orc_present(const orc_space* s, uint32_t slot) { return slot < s->cap ? s->p
 
 /* keep cmp_u64 referenced for future digest helpers */
 int orc__unused_cmp_u64(const void* a, const void* b) { return cmp_u64(a, b); }
+
+/* ------------------------------------------------------------------------ */
+/* Client messages, restated on the oracle's state.  */
+/* Order of every stream: (gate(watcher), watcher, ...), i.e. one run per     */
+/* client inside a gate; the reference sends them from Go map iteration, so  */
+/* only the per-client order is meaningful, and that is call order.          */
+static const orc_space* g_fs;    /* qsort context (single-threaded oracle) */
+static int cmp_gate_rec3(const void* a, const void* b) {
+    const uint32_t* x = (const uint32_t*)a; const uint32_t* y = (const uint32_t*)b;
+    uint32_t gx = g_fs->gate[x[0]], gy = g_fs->gate[y[0]];
+    if (gx != gy) return gx < gy ? -1 : 1;
+    if (x[0] != y[0]) return x[0] < y[0] ? -1 : 1;
+    if (x[2] != y[2]) return x[2] < y[2] ? -1 : 1;
+    return 0;
+}
+/* Entity.interest / uninterest (Entity.go:236-246) -> e.client.sendCreateEntity
+ * (other, false) with other's Position and yaw (GameClient.go:37-53) /
+ * sendDestroyEntity(other) (GameClient.go:55-59); a nil client sends nothing.
+ * Built from the tick's net events (already in (watcher, target) order), kept
+ * stable per gate by a counting pass over the gate ids.  out NULL: count. */
+static uint64_t client_msgs(const orc_space* s, const gw_event* ev, uint64_t n, gw_sync_record* cr, gw_event* de) {
+    uint64_t* at = (uint64_t*)calloc(65537, 8);
+    for (uint64_t i = 0; i < n; ++i) at[s->gate[ev[i].watcher] + 1]++;
+    at[1] = 0;                                   /* gate 0: no client, no message */
+    for (uint32_t g = 1; g <= 65535u; ++g) at[g + 1] += at[g];
+    const uint64_t k = at[65536];
+    if (cr || de) {
+        for (uint64_t i = 0; i < n; ++i) {       /* stable: events stay in (watcher, target) order */
+            uint32_t w = ev[i].watcher, t = ev[i].target, g = s->gate[w];
+            if (!g) continue;
+            uint64_t j = at[g]++;
+            if (cr) {
+                gw_sync_record r = {w, t, s->px[t], s->py[t], s->pz[t], s->pyaw[t]};
+                cr[j] = r;
+            } else {
+                de[j] = ev[i];
+            }
+        }
+    }
+    free(at);
+    return k;
+}
+uint64_t orc_client_creates(const orc_space* s, gw_sync_record* out) {
+    return client_msgs(s, s->enter, s->n_enter, out, NULL);
+}
+uint64_t orc_client_destroys(const orc_space* s, gw_event* out) {
+    return client_msgs(s, s->leave, s->n_leave, NULL, out);
+}
+/* Entity.CallAllClients (Entity.go:743-749) and the AllClients attribute
+ * notifications (Entity.go:814-917): e.client.call(...), then for neighbor in
+ * e.InterestedBy: neighbor.client.call(...).  Call k on slots[k] yields
+ * {watcher, entity, k} records (3 words); out NULL: count. */
+uint64_t orc_fanout(const orc_space* s, const uint32_t* slots, uint32_t n, uint32_t* out) {
+    uint64_t k = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t e = slots[i];
+        if (e >= s->cap) continue;
+        if (s->gate[e]) {
+            if (out) { out[3 * k] = e; out[3 * k + 1] = e; out[3 * k + 2] = i; }
+            ++k;
+        }
+        const vec32* by = s->by ? &s->by[e] : &s->nb[e];
+        for (uint32_t j = 0; j < by->n; ++j) {
+            uint32_t w = by->a[j];
+            if (!s->gate[w]) continue;
+            if (out) { out[3 * k] = w; out[3 * k + 1] = e; out[3 * k + 2] = i; }
+            ++k;
+        }
+    }
+    if (out && k) {
+        g_fs = s;
+        qsort(out, k, 12, cmp_gate_rec3);
+    }
+    return k;
+}

@@ -92,6 +92,12 @@ int      orc_present(const orc_space* s, uint32_t slot);
 /* Exact window test of the reference, for tests: other in [fl(c-d), fl(c+d)]
  * on both axes (go-aoi xzlist Mark bounds). */
 int orc_in_window(float cx, float cz, float d, float ox, float oz);
+/* client messages of the last tick / AllClients fan-out (SURVEY 8(f) ranks
+ * 2-3; orc.c has the reference citations); out NULL returns the count */
+uint64_t orc_client_creates(const orc_space* s, gw_sync_record* out);
+uint64_t orc_client_destroys(const orc_space* s, gw_event* out);
+uint64_t orc_fanout(const orc_space* s, const uint32_t* slots, uint32_t n, uint32_t* out);
+
 
 #ifdef __cplusplus
 }

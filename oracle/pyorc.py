@@ -21,6 +21,8 @@ EVENT_DTYPE = np.dtype([("watcher", "<u4"), ("target", "<u4")])
 REC_DTYPE = np.dtype([("watcher", "<u4"), ("entity", "<u4"), ("x", "<f4"), ("y", "<f4"),
                       ("z", "<f4"), ("yaw", "<f4")])
 
+FANOUT_DTYPE = np.dtype([("watcher", "<u4"), ("entity", "<u4"), ("item", "<u4")])
+
 _lib = None
 
 
@@ -59,6 +61,12 @@ def lib():
         L.orc_total_neighbors.argtypes = [vp]
         L.orc_present.argtypes = [vp, u32]
         L.orc_in_window.argtypes = [f32, f32, f32, f32, f32]
+        L.orc_client_creates.restype = u64
+        L.orc_client_creates.argtypes = [vp, vp]
+        L.orc_client_destroys.restype = u64
+        L.orc_client_destroys.argtypes = [vp, vp]
+        L.orc_fanout.restype = u64
+        L.orc_fanout.argtypes = [vp, vp, u32, vp]
         _lib = L
     return _lib
 
@@ -141,6 +149,25 @@ class OracleSpace:
 
     def total_neighbors(self) -> int:
         return lib().orc_total_neighbors(self._h)
+
+    def client_events(self):
+        """(creates, destroys) of the last tick: the sendCreateEntity /
+        sendDestroyEntity messages (GameClient.go:37-59), order (gate, watcher, target)."""
+        n = lib().orc_client_creates(self._h, None)
+        cr = np.zeros(n, REC_DTYPE)
+        lib().orc_client_creates(self._h, _ptr(cr))
+        n = lib().orc_client_destroys(self._h, None)
+        de = np.zeros(n, EVENT_DTYPE)
+        lib().orc_client_destroys(self._h, _ptr(de))
+        return cr, de
+
+    def fanout(self, slots) -> np.ndarray:
+        """CallAllClients deliveries (Entity.go:743-749), order (gate, watcher, call)."""
+        sl = np.ascontiguousarray(slots, dtype=np.uint32)
+        n = lib().orc_fanout(self._h, _ptr(sl), len(sl), None)
+        out = np.zeros(n, FANOUT_DTYPE)
+        lib().orc_fanout(self._h, _ptr(sl), len(sl), _ptr(out))
+        return out
 
     def present(self, slot: int) -> bool:
         return bool(lib().orc_present(self._h, slot))

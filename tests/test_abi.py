@@ -31,7 +31,9 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version_and_layouts():
-    assert gpuaoi.lib().gw_abi_version() == 7
+    assert gpuaoi.lib().gw_abi_version() == 8
+    assert gpuaoi.FANOUT_DTYPE.itemsize == 12
+    assert ctypes.sizeof(gpuaoi.MsgOut) == 7 * 8
     assert ctypes.sizeof(gpuaoi.HaloDst) == 24
     assert traces.OP_DTYPE.itemsize == 24
     assert gpuaoi.EVENT_DTYPE.itemsize == 8

@@ -488,3 +488,48 @@ def test_restore_equals_enter_ticks(ctx_factory):
         g.restore(sid, [base, base], [0.0, 1.0], [0.0, 0.0], [0.0, 0.0], [0.0, 0.0])
     with pytest.raises(gpuaoi.GwError):              # outside the space
         g.restore(sid, [base + 8], [0.0], [0.0], [0.0], [0.0])
+
+
+@pytest.mark.parametrize("which", ["config2_3gates", "adversarial_1gate"])
+def test_client_events_and_fanout_match_oracle(ctx_factory, which):
+    """SURVEY 8(f) ranks 2-3 on the device: the create/destroy client messages
+    of each tick's events (Entity.go:236-246, GameClient.go:37-59; creates carry
+    the target's position and yaw) and the AllClients fan-out of calls
+    (Entity.go:743-749), both bit-exact with the oracle's restatement, order
+    (gate, watcher, target / call), gate_off partitioning each stream."""
+    if which == "config2_3gates":
+        tr = T.config2(ticks=3, n=20_000)
+        tr.gates = np.where(np.arange(tr.capacity) % 7 == 6, 0, 1 + np.arange(tr.capacity) % 3).astype(np.uint16)
+    else:
+        tr = T.adversarial_trace(9, n=400, ticks=10)
+        tr.gates = (np.arange(tr.capacity) % 3 != 0).astype(np.uint16)
+    g = ctx_factory()
+    gpuaoi.load_space(g, tr)
+    o = pyorc.OracleSpace(tr.capacity, tr.d, pyorc.SEQRULE)
+    pyorc.load_trace(o, tr)
+    rng = np.random.default_rng(7)
+    n_cr = n_de = n_fo = 0
+    for t, ops in enumerate(tr.ticks):
+        g.submit(ops)
+        g.tick(copy=False)
+        assert o.tick(ops) == 0
+        cr, de = g.client_events()
+        ocr, ode = o.client_events()
+        assert cr.records.tobytes() == ocr.tobytes(), f"tick {t}: create messages differ"
+        assert de.records.tobytes() == ode.tobytes(), f"tick {t}: destroy messages differ"
+        calls = rng.integers(0, tr.capacity, 3000).astype(np.uint32)
+        f = g.fanout(calls)
+        assert f.records.tobytes() == o.fanout(calls).tobytes(), f"tick {t}: fan-out differs"
+        for res in (cr, de, f):
+            gsel = tr.gates[res.records["watcher"]]
+            assert res.gate_off[-1] == len(res.records)
+            for gid in range(len(res.gate_off) - 1):
+                assert np.all(gsel[res.gate_off[gid]:res.gate_off[gid + 1]] == gid)
+        n_cr += len(cr.records); n_de += len(de.records); n_fo += len(f.records)
+        if t % 3 == 2:
+            g.sync_collect(copy=False)
+            o.collect()
+    assert n_cr > 0 and n_de > 0 and n_fo > 1000
+    assert len(g.fanout(np.zeros(0, np.uint32)).records) == 0
+    with pytest.raises(gpuaoi.GwError):
+        g.fanout([tr.capacity + 5])

@@ -293,3 +293,68 @@ def test_gridmt_equals_seqrule(which):
         (e0, l0), (e1, l1) = o.events(), m.events()
         assert e0.tobytes() == e1.tobytes() and l0.tobytes() == l1.tobytes()
         assert srt(o.collect()) == srt(m.collect())
+
+
+# ---- client messages --------------------------------
+def test_client_messages_and_fanout_known_answer():
+    """Entity.interest/uninterest -> sendCreateEntity/sendDestroyEntity only to
+    watchers with a client (Entity.go:236-246, GameClient.go:37-59); creates
+    carry the target's position and yaw; CallAllClients reaches the own client
+    and every InterestedBy client (Entity.go:743-749).  Order (gate, watcher, ...)."""
+    sp = one()
+    sp.set_client(0, 2); sp.set_client(2, 1)            # slot 1 and 3: no client
+    sp.tick(np.concatenate([op(1, 0, 0, 0), op(1, 1, 50, 0)]))
+    assert sp.tick(np.concatenate([op(1, 2, 10, 10, y=3, yaw=0.5), op(1, 3, 1000, 1000)])) == 0
+    cr, de = sp.client_events()
+    assert len(de) == 0
+    assert [tuple(r) for r in cr.tolist()] == [(2, 0, 0.0, 0.0, 0.0, 0.0), (2, 1, 50.0, 0.0, 0.0, 0.0),
+                                              (0, 2, 10.0, 3.0, 10.0, 0.5)]
+    f = sp.fanout([2, 1, 3])
+    assert [tuple(r) for r in f.tolist()] == [(2, 2, 0), (2, 1, 1), (0, 2, 0), (0, 1, 1)]
+    assert sp.tick(op(3, 2)) == 0
+    cr, de = sp.client_events()
+    assert len(cr) == 0
+    assert [tuple(r) for r in de.tolist()] == [(2, 0), (2, 1), (0, 2)]
+    assert [tuple(r) for r in sp.fanout([2]).tolist()] == [(2, 2, 0)]   # left the space: own client only
+
+
+def _client_msgs_py(sp, enter, leave, gates, pos):
+    """Python restatement of the same rules on the net events (checker of the C one)."""
+    cr = [(int(w), int(t), *pos[t]) for w, t in enter.tolist() if gates[w]]
+    de = [(int(w), int(t)) for w, t in leave.tolist() if gates[w]]
+    key = lambda r: (gates[r[0]], r[0], r[1])
+    return sorted(cr, key=key), sorted(de, key=key)
+
+
+@pytest.mark.parametrize("mode", [pyorc.XZLIST, pyorc.SEQRULE])
+def test_client_messages_follow_events(mode):
+    tr = T.adversarial_trace(21, n=300, ticks=8)
+    gates = tr.gates = (np.arange(tr.capacity) % 4).astype(np.uint16)
+    sp = pyorc.OracleSpace(tr.capacity, tr.d, mode)
+    pyorc.load_trace(sp, tr)
+    pos = {}
+    for i, s in enumerate(tr.init_slots):
+        pos[int(s)] = (float(tr.init_x[i]), float(tr.init_y[i]), float(tr.init_z[i]), float(tr.init_yaw[i]))
+    rng = np.random.default_rng(3)
+    n_msgs = 0
+    for ops in tr.ticks:
+        assert sp.tick(ops) == 0
+        for o in ops.tolist():
+            if o[0] in (T.OP_ENTER, T.OP_MOVED, T.OP_SYNC):
+                pos[int(o[3])] = tuple(float(v) for v in o[4:8])
+        e, l = sp.events()
+        cr, de = sp.client_events()
+        wcr, wde = _client_msgs_py(sp, e, l, gates, pos)
+        assert [tuple(r) for r in cr.tolist()] == [tuple(np.float32(v) if i > 1 else v for i, v in enumerate(r))
+                                                   for r in wcr]
+        assert [tuple(r) for r in de.tolist()] == wde
+        n_msgs += len(cr) + len(de)
+        calls = rng.integers(0, tr.capacity, 50)
+        want = []
+        for k, s in enumerate(calls.tolist()):
+            if gates[s]:
+                want.append((s, s, k))
+            want += [(int(w), s, k) for w in sp.interested_by(s).tolist() if gates[w]]
+        want.sort(key=lambda r: (gates[r[0]], r[0], r[2]))
+        assert [tuple(r) for r in sp.fanout(calls).tolist()] == want
+    assert n_msgs > 100

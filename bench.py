@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--device", type=int, default=None, help="force a device (rehearsals on one GPU)")
     ap.add_argument("--sync-by-client", action="store_true",
                     help="collect grouped per client (GW_SYNC_BY_CLIENT, the gate's regroup on the GPU)")
+    ap.add_argument("--client-msgs", type=int, default=5,
+                    help="extra untimed ticks measuring gw_client_events + gw_fanout (N=1 config #3; 0 = off)")
     ap.add_argument("--capacity", type=int, default=None,
                     help="slot capacity of the space (N=1: cost of a strip's id range at N ranks)")
     return ap.parse_args()
@@ -276,12 +278,42 @@ class WorldRun:
         self.g.close()
 
 
+def client_msgs(run, t0, n):
+    """SURVEY 8(f) ranks 2-3, outside the headline step: after each of n more
+    ticks, gw_client_events (create/destroy messages of the tick's events) and
+    gw_fanout of one AllClients call per mover (e.g. an attribute change),
+    outputs left on the device; wall time per call (each ends in a host sync)."""
+    g = run.g
+    t_ev = t_fo = 0.0
+    n_cr = n_de = n_fo = n_calls = b_ev = b_fo = 0
+    for t in range(t0, t0 + n):
+        run.step(t)
+        calls = run.tr.ticks[t]["slot"]
+        g.synchronize()
+        c0 = time.perf_counter()
+        cr, de = g.client_events(copy=False)
+        c1 = time.perf_counter()
+        fo = g.fanout(calls, copy=False)
+        c2 = time.perf_counter()
+        t_ev += c1 - c0
+        t_fo += c2 - c1
+        n_cr += cr.n_rec; n_de += de.n_rec; n_fo += fo.n_rec; n_calls += len(calls)
+        b_ev += cr.bytes_alg + de.bytes_alg; b_fo += fo.bytes_alg
+    return {"ticks": n,
+            "client_events": {"avg_us": t_ev / n * 1e6, "creates_per_tick": n_cr / n, "destroys_per_tick": n_de / n,
+                              "msgs_per_sec": (n_cr + n_de) / t_ev, "GBps_alg": b_ev / t_ev / 1e9},
+            "fanout": {"avg_us": t_fo / n * 1e6, "calls_per_tick": n_calls / n, "deliveries_per_tick": n_fo / n,
+                       "deliveries_per_sec": n_fo / t_fo, "GBps_alg": b_fo / t_fo / 1e9},
+            "timing": "host wall clock around each call (one host sync inside each); not part of ms_per_step"}
+
+
 def main():
     a = parse()
     ctl = Ctl(a)
     ws, rank = ctl.ws, ctl.rank
     extra = 5 if a.profile_stages else 0         # untimed steps for the per-stage breakdown
-    ticks = a.warmup + a.steps + extra
+    cm = a.client_msgs if (ws == 1 and a.config == 3) else 0
+    ticks = a.warmup + a.steps + extra + cm
     t_load = time.perf_counter()
     world = (ws > 1 and a.mode == "world") or a.config == 5
     run = WorldRun(a, ctl, ticks) if world else SpaceRun(a, ctl, ticks)
@@ -321,10 +353,11 @@ def main():
                 dom_us, dom_bytes = us / calls, b / calls
         # per-stage breakdown: every stage timed over a few more (untimed) steps
         g.set_profiling(1)
-        for t in range(a.warmup + a.steps, ticks):
+        for t in range(a.warmup + a.steps, a.warmup + a.steps + extra):
             run.step(t)
         acc_stages()
         g.set_profiling(0)
+    client = client_msgs(run, a.warmup + a.steps + extra, cm) if cm else None
     mx = ctl.reduce([elapsed], "MAX")[0]
     sums = ctl.reduce([tot["ops"], tot["events"], tot["records"]], "SUM")
     if rank != 0:
@@ -387,6 +420,8 @@ def main():
             v["bytes_alg"] / max(v["avg_us"], 1e-9) / 1e3, 1)} for n, v in stages.items()}
     else:
         line["roofline"] = None
+    if client:
+        line["client_msgs"] = client
     if not a.no_cpu_baseline and ws == 1 and a.config == 3:
         cb = cpu_baseline(traces.config3(ticks=1, seed=3, n=a.entities, side=a.side), a.cpu_seconds)
         line["cpu_baseline"] = cb

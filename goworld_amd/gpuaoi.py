@@ -173,6 +173,8 @@ class MsgResult:
     gate_off: np.ndarray
     bytes_alg: int
     device_us: float
+    n_rec: int = 0
+    rec_dev: int = 0
 
 
 class GpuAOI:
@@ -312,26 +314,27 @@ class GpuAOI:
 
     @staticmethod
     def _msgs(o: MsgOut, dtype) -> MsgResult:
-        r = np.zeros(o.n_rec, dtype)
-        if o.n_rec:
+        r = np.zeros(o.n_rec if o.rec else 0, dtype)
+        if o.n_rec and o.rec:
             C.memmove(_p(r), o.rec, o.n_rec * dtype.itemsize)
         goff = np.array([o.gate_off[i] for i in range(o.n_gates + 1)], dtype=np.uint64)
-        return MsgResult(r, goff, o.bytes_alg, o.device_us)
+        return MsgResult(r, goff, o.bytes_alg, o.device_us, o.n_rec, o.rec_dev or 0)
 
-    def client_events(self) -> tuple[MsgResult, MsgResult]:
+    def client_events(self, copy: bool = True) -> tuple[MsgResult, MsgResult]:
         """Client messages of the last tick's events (Entity.interest/uninterest,
         Entity.go:236-246): creates (REC_DTYPE: watcher, target, target's x,y,z,yaw)
         and destroys (EVENT_DTYPE), each grouped (gate, watcher, target)."""
         cr, de = MsgOut(), MsgOut()
-        self._chk(lib().gw_client_events(self._h, MSG_COPY_TO_HOST, C.byref(cr), C.byref(de)))
+        fl = MSG_COPY_TO_HOST if copy else 0
+        self._chk(lib().gw_client_events(self._h, fl, C.byref(cr), C.byref(de)))
         return self._msgs(cr, REC_DTYPE), self._msgs(de, EVENT_DTYPE)
 
-    def fanout(self, slots) -> MsgResult:
+    def fanout(self, slots, copy: bool = True) -> MsgResult:
         """AllClients fan-out of calls on slots[k] (Entity.CallAllClients,
         Entity.go:743-749): FANOUT_DTYPE records grouped (gate, watcher, call)."""
         s = np.ascontiguousarray(slots, dtype=np.uint32)
         o = MsgOut()
-        self._chk(lib().gw_fanout(self._h, _p(s), len(s), MSG_COPY_TO_HOST, C.byref(o)))
+        self._chk(lib().gw_fanout(self._h, _p(s), len(s), MSG_COPY_TO_HOST if copy else 0, C.byref(o)))
         return self._msgs(o, FANOUT_DTYPE)
 
     def neighbors(self, slot: int) -> np.ndarray:

@@ -1179,11 +1179,16 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
                                P<uint32_t>(c->cl_slot), P<uint64_t>(c->cl_off), c->sc, c->st);
         HIPCHK(hipMemcpyAsync(&n_clients, c->scal32 + 1, 4, hipMemcpyDeviceToHost, c->st));
     }
-    HIPCHK(hipEventRecord(c->ev_t1, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1);
-    out->device_us = ms * 1000.0;
+    // the stream is synced again only for host outputs (records, client
+    // table): without them the caller may queue the next tick behind the
+    // collect's tail at once, and device_us stays 0 (as for gw_tick)
+    if ((flags & GW_SYNC_COPY_TO_HOST) || by_client) {
+        HIPCHK(hipEventRecord(c->ev_t1, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1);
+        out->device_us = ms * 1000.0;
+    }
     out->n_rec = R;
     if (by_client) {
         out->n_clients = n_clients;

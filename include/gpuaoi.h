@@ -149,7 +149,9 @@ typedef struct gw_sync_out {
     uint32_t n_gates;               /* max gate id + 1                          */
     uint64_t flagged;               /* entities whose syncInfoFlag was set      */
     uint64_t bytes_alg;
-    double   device_us;
+    double   device_us;             /* only with COPY_TO_HOST or BY_CLIENT (0
+                                       otherwise: the call returns without
+                                       waiting for its last kernels)           */
     /* GW_SYNC_BY_CLIENT only: client segments of rec (the watcher slot of each
      * segment; n_clients+1 offsets).  Host arrays with COPY_TO_HOST.          */
     uint32_t n_clients;

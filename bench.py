@@ -56,8 +56,10 @@ def parse():
                     help="1: HIP events around the dominant kernel's stage in the timed region (roofline) and "
                          "a per-stage breakdown over extra untimed steps; 0: none")
     ap.add_argument("--mode", choices=["world", "spaces"], default="world", help="N>1 regime")
-    ap.add_argument("--config", type=int, choices=[3, 5], default=3,
-                    help="3: config #3 per GPU (weak); 5: the 16M uniform world of config #5 over N strips (strong)")
+    ap.add_argument("--config", type=int, choices=[3, 4, 5], default=3,
+                    help="3: config #3 per GPU (weak); 4: config #4, 10k independent 1k-entity spaces, space s on "
+                         "GPU s mod N (strong); 5: the 16M uniform world of config #5 over N strips (strong)")
+    ap.add_argument("--spaces", type=int, default=10_000, help="config #4: number of spaces")
     ap.add_argument("--comm", choices=["nccl", "gloo"], default="nccl",
                     help="halo exchange backend (gloo: rehearsal of several ranks on one GPU)")
     ap.add_argument("--halo-cap", type=int, default=4096, help="halo entities per neighbour per tick")
@@ -220,6 +222,65 @@ class SpaceRun:
         self.g.close()
 
 
+class ManySpacesRun(SpaceRun):
+    """--config 4 (BASELINE config #4): `spaces` independent spaces of 1k entities (L = 1024, d = 100,
+    K ~ 38), space s on GPU s mod N (SpaceManager.go:11-31: a space never spans processes), no
+    collective; every space of a GPU is ticked and collected by the same launches.  The population
+    and the walk (10% movers per space per tick, +-4 on the 1/128 grid, reflected) are drawn per
+    rank with the seeded generators of goworld_amd/traces.py, vectorised over spaces."""
+
+    def __init__(self, a, ctl, ticks):
+        T = traces
+        mine = np.arange(ctl.rank, a.spaces, ctl.ws)
+        S, per, L, Q = len(mine), 1000, 1024.0, int(T.Q)
+        seed = 4_000_000 + ctl.rank
+        self.g = g = gpuaoi.GpuAOI(ctl.local)
+        bases = np.zeros(S, np.int64)
+        sids = []
+        for i in range(S):
+            sid, bases[i] = g.create_space(100.0, per, bounds=(-L / 2, -L / 2, L / 2, L / 2))
+            sids.append(sid)
+        n = S * per
+        lo, hi = -int(L / 2 * Q), int(L / 2 * Q)
+        kx = T.rand_int(T.stream_key(seed, 1), n, lo, hi)
+        kz = T.rand_int(T.stream_key(seed, 2), n, lo, hi)
+        yaw = (T.rand_f32(T.stream_key(seed, 3), n) * np.float32(2 * np.pi)).astype(np.float32)
+        slots = (bases[:, None] + np.arange(per)[None, :]).reshape(-1).astype(np.uint32)
+        for i in range(S):
+            sl = slice(i * per, (i + 1) * per)
+            g.restore(sids[i], slots[sl], kx[sl] / Q, np.zeros(per, np.float32), kz[sl] / Q, yaw[sl])
+        g.set_clients(slots, np.ones(n, np.uint16))          # every entity has a client, 1 gate
+        g.sync_collect(copy=False)                            # clear the Enter flags (untimed)
+        m = per // 10
+        coprime = np.array([1, 3, 7, 9, 11, 13, 17, 19, 21, 23], np.int64)
+        ops_all = []
+        for t in range(ticks):
+            o = T.rand_int(T.stream_key(seed, 100, t), S, 0, per)
+            p = coprime[T.rand_int(T.stream_key(seed, 101, t), S, 0, len(coprime))]
+            local = (o[:, None] + np.arange(m)[None, :] * p[:, None]) % per     # distinct within a space
+            idx = (np.arange(S)[:, None] * per + local).reshape(-1)
+            q = (T.rand_unit(T.stream_key(seed, 102, t), 2 * len(idx)) * 1025).astype(np.int64) - 512
+            kx[idx] = T._reflect_q(kx[idx] + q[:len(idx)], lo, hi)
+            kz[idx] = T._reflect_q(kz[idx] + q[len(idx):], lo, hi)
+            ops = T.make_ops(len(idx))
+            ops["kind"] = T.OP_MOVED
+            ops["sync_flags"] = T.SIF_NEIGHBOR | T.SIF_OWN
+            ops["slot"] = slots[idx]
+            ops["x"] = (kx[idx] / Q).astype(np.float32)
+            ops["z"] = (kz[idx] / Q).astype(np.float32)
+            ops["yaw"] = yaw[idx]
+            ops_all.append(ops)
+        self.m = len(ops_all[0])
+        ops_all = np.concatenate(ops_all)
+        self.dev_ops = g.dev_alloc(ops_all.nbytes)
+        g.h2d(self.dev_ops, ops_all)
+        self.nbytes_tick = self.m * T.OP_DTYPE.itemsize
+        self.by_client = a.sync_by_client
+        self.parallelism = f"{a.spaces} independent spaces, s -> GPU s mod {ctl.ws} ({S} on this GPU, no comm)"
+        self.n_world = a.spaces * per
+        self.tr = None
+
+
 class WorldRun:
     """--mode world, N>1 (or --config 5): one world of N strips (dworld.StripRank per rank)."""
 
@@ -316,7 +377,10 @@ def main():
     ticks = a.warmup + a.steps + extra + cm
     t_load = time.perf_counter()
     world = (ws > 1 and a.mode == "world") or a.config == 5
-    run = WorldRun(a, ctl, ticks) if world else SpaceRun(a, ctl, ticks)
+    if a.config == 4:
+        run = ManySpacesRun(a, ctl, ticks)
+    else:
+        run = WorldRun(a, ctl, ticks) if world else SpaceRun(a, ctl, ticks)
     t_load = time.perf_counter() - t_load
     g = run.g
 
@@ -364,7 +428,11 @@ def main():
         run.close()
         return
     K = a.steps
-    if a.config == 5:
+    if a.config == 4:
+        workload = (f"config #4: {a.spaces} independent AOI spaces x 1000 entities (uniform, L = 1024, AOI "
+                    f"distance 100), 10% movers per space per tick (step +-4), space s on GPU s mod {ws}, every "
+                    f"space of a GPU in one tick; step = gw_tick + gw_sync_collect")
+    elif a.config == 5:
         workload = (f"config #5: one 16M-entity uniform world space, L = 131072, AOI distance 100, 10% movers "
                     f"per tick (step +-4), decomposed into {ws} X-strip(s) of {131072 // ws} x 131072 (walkers "
                     f"reflect at strip borders); step = route + halo exchange + gw_tick + gw_sync_collect")
@@ -386,15 +454,15 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": mx / K * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if a.config == 5 else "weak",
+        "scaling": "strong" if a.config in (4, 5) else "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": ("synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #5)" if a.config == 5 else
+        "data": (f"synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #{a.config})" if a.config in (4, 5) else
                  "synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #3" + (" per strip)" if world else ")")),
         "config": {"workload": workload,
                    "entities_per_gpu": run.n_world // ws, "world_entities": run.n_world,
                    "movers_per_tick_per_gpu": run.m, "aoi_dist": 100.0,
-                   "world_side": 131072.0 if a.config == 5 else a.side, "gates": 1,
+                   "world_side": {4: 1024.0, 5: 131072.0}.get(a.config, a.side), "gates": 1,
                    "parallelism": run.parallelism},
         "events_per_sec": sums[1] / mx,
         "records_per_sec": sums[2] / mx,

@@ -491,8 +491,11 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     const uint64_t m = (uint64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
     if (m >= b.st->n_gm) return;
     const MEnt me = b.gm[m];
-    if (!(me.tags & TAG_PRIMARY)) return;
     const int ln = lane_id();
+    if (!(me.tags & TAG_PRIMARY)) {
+        if (ln == 0) b.mstat[m] = make_ulonglong2(0, 0);
+        return;
+    }
     const uint64_t lt = lanemask_lt();
     const World& w = b.w;
     const uint64_t reg = b.reg[m], cap = b.cand[m];
@@ -500,6 +503,7 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
         if (ln == 0) {
             atomicOr(&b.st->overflow, 1ull);
             b.mir_cnt[m] = 0;
+            b.mstat[m] = make_ulonglong2(0, 0);
         }
         return;
     }
@@ -546,27 +550,35 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
             if (base + 64u * u >= f.total) break;              // wave-uniform
             const Cand& e = cc[u];
             bool ev = false, lv = false, nmv = false;
+            bool t_ro = false, t_rn = false, t_cli = false, b_o = false, b_n = false;
             uint32_t key = 0;
             if (e.slot != A) {
                 nmv = (e.info & CAND_NONMOVER) != 0;
                 const bool iao = wo.has(e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, me.ox, me.oz);
                 const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, me.x, me.z);
                 bool ro = iao, rn = ian;
-                if (iao != ibo || ian != ibn) {
+                b_o = iao != ibo;
+                b_n = ian != ibn;
+                if (b_o || b_n) {
                     const unsigned long long sb = w.stamp[e.slot];
                     const unsigned long long sbo = nmv ? sb : w.prev[e.slot].ostamp;
-                    if (iao != ibo) { ro = resolve(iao, ibo, soA, sbo); ++c_band; }
-                    if (ian != ibn) { rn = resolve(ian, ibn, sA, sb); ++c_band; }
+                    if (b_o) ro = resolve(iao, ibo, soA, sbo);
+                    if (b_n) rn = resolve(ian, ibn, sA, sb);
                 }
                 const bool take = ((e.info & TAG_OLD) && ro) || ((e.info & TAG_NEW) && rn && !ro);
                 if (take) {
-                    c_old += ro; c_new += rn;
-                    c_cli += rn && (e.info & CAND_CLIENT) != 0;
+                    t_ro = ro; t_rn = rn;
+                    t_cli = rn && (e.info & CAND_CLIENT) != 0;
                     ev = ro != rn;
                     lv = ro;
                     key = (e.slot << 1) | (lv ? 1u : 0u);
                 }
             }
+            // statistics as wave-uniform ballot counts (no cross-lane sums at the end)
+            c_old += (uint32_t)popc64(wave_ballot(t_ro));
+            c_new += (uint32_t)popc64(wave_ballot(t_rn));
+            c_cli += (uint32_t)popc64(wave_ballot(t_cli));
+            c_band += (uint32_t)popc64(wave_ballot(b_o)) + (uint32_t)popc64(wave_ballot(b_n));
             const bool mev = ev && nmv && owned_x(P, e.x);
             ev = ev && ownA;
             // B has no op: (B,A) is B's event too: count it (no return value,
@@ -602,16 +614,37 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
             b.big[atomicAdd(&b.st->n_big, 1ull)] = (uint32_t)m;
         }
     }
-    const uint32_t so = wave_sum<uint32_t>(c_old), sn = wave_sum<uint32_t>(c_new), sb = wave_sum<uint32_t>(c_band);
-    const uint32_t scl = wave_sum<uint32_t>(c_cli);
+    const uint32_t so = c_old, sn = c_new, sb = c_band, scl = c_cli;
     if (ln == 0) {
         b.cnt64[A] = (unsigned long long)(n - nl) | ((unsigned long long)nl << 32);
         b.mir_cnt[m] = nm_;
         if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | scl;
-#ifndef GW_EXP_NO_SHARD
-        shard_add(b.st, blockIdx.x, SH_AOLD, (unsigned long long)so | ((unsigned long long)sn << 32));
-        shard_add(b.st, blockIdx.x, SH_BAND, sb);
-#endif
+        // per-mover statistics, summed by k_mover_stats (no atomics here: 2 per
+        // mover into 256 shards cost 25 us at config #3 and 180 us at config #4)
+        b.mstat[m] = make_ulonglong2((unsigned long long)so | ((unsigned long long)sn << 32), sb);
+    }
+}
+
+// A_old | A_new << 32 and band counts of every mover-grid entry, one shard per
+// block (STAT_SHARDS blocks, so no two blocks add to the same words)
+__global__ void __launch_bounds__(NT) k_mover_stats(TickBufs b) {
+    __shared__ unsigned long long red[2][NWAVE];
+    const uint64_t n = b.st->n_gm;
+    unsigned long long a = 0, c = 0;
+    for (uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x; m < n; m += (uint64_t)gridDim.x * NT) {
+        const ulonglong2 v = b.mstat[m];
+        a += v.x;
+        c += v.y;
+    }
+    a = wave_sum<unsigned long long>(a);
+    c = wave_sum<unsigned long long>(c);
+    if (lane_id() == 0) { red[0][threadIdx.x >> 6] = a; red[1][threadIdx.x >> 6] = c; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a = c = 0;
+        for (int i = 0; i < NWAVE; ++i) { a += red[0][i]; c += red[1][i]; }
+        shard_add(b.st, blockIdx.x, SH_AOLD, a);
+        shard_add(b.st, blockIdx.x, SH_BAND, c);
     }
 }
 
@@ -763,6 +796,7 @@ void tick_diff(const TickBufs& b, hipStream_t s) {
 void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint64_t nmax = 2ull * b.m;
     const uint32_t C = b.w.cap;
+    hipLaunchKernelGGL(k_mover_stats, dim3(STAT_SHARDS), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_big_own, dim3(64), dim3(NT), 0, s, b);
     scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.cnt64, b.off64, (uint64_t)C + 1, nullptr, sc,
                                        (uint64_t*)&b.st->ev_pk, s);

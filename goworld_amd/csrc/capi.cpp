@@ -113,7 +113,7 @@ struct gw_ctx {
     gw_tick_out last_out{};
 
     // grid + tick scratch
-    DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, cand, reg, own, big, bigseg;
+    DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, cand, reg, own, big, bigseg, mstat;
     DevBuf mir, mir_cnt;
     DevBuf off64, enter_d, leave_d, scan_status, rs_hist;
     ScanCtx sc{};                  // single-pass scan state (prim.hpp)
@@ -564,7 +564,7 @@ void gw_shutdown(gw_ctx* c) {
     (void)settle(c);
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->k0, &c->v0, &c->k1, &c->v1, &c->bigseg,
+    DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1, &c->bigseg,
                       &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->off64, &c->mir,
                       &c->mir_cnt,
                       &c->enter_d, &c->leave_d, &c->scan_status, &c->rs_hist,
@@ -993,6 +993,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     if ((rc = ensure(c, c->gm, M2 * sizeof(MEnt))) ||
         (rc = ensure(c, c->cand, M2 * 8)) || (rc = ensure(c, c->reg, M2 * 8)) ||
         (rc = ensure(c, c->mir_cnt, M2 * 4)) || (rc = ensure(c, c->big, M2 * 4)) ||
+        (rc = ensure(c, c->mstat, M2 * 16)) ||
         (rc = ensure(c, c->bigseg, (size_t)C * 4)) ||
         (rc = ensure(c, c->off64, ((size_t)C + 2) * 8)) ||
         (rc = ensure_scan(c, std::max<uint64_t>(std::max<uint64_t>(M2, (uint64_t)C + 1), (uint64_t)NC + 1))))
@@ -1014,6 +1015,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.gm_cnt = c->gm_cnt; b.gm_start = c->gm_start; b.gm = P<MEnt>(c->gm);
     b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg);
     b.mir_cnt = P<uint32_t>(c->mir_cnt); b.big = P<uint32_t>(c->big);
+    b.mstat = P<ulonglong2>(c->mstat);
     b.bigseg = P<uint32_t>(c->bigseg);
     b.ownbits = c->ownbits;
     b.cnt64 = c->cnt64; b.off64 = P<uint64_t>(c->off64);

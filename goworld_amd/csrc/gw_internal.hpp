@@ -171,6 +171,7 @@ struct TickBufs {
     uint64_t* mir;            // mirror events of op-less neighbours: watcher<<32 | mover<<1 | leave
     uint32_t* ownbits;        // [cap/32 + 1] touched op-less watchers to sort, zero between ticks
     uint32_t* mir_cnt;        // [2m] mirror events per entry
+    ulonglong2* mstat;        // [2m] A_old | A_new << 32, band count per entry (k_mover -> k_mover_stats)
     uint32_t* big;            // [2m] entries whose own events need the block sort
     uint32_t* bigseg;         // [cap] op-less watchers whose segments need the block sort
     // canonical events

@@ -533,3 +533,23 @@ def test_client_events_and_fanout_match_oracle(ctx_factory, which):
     assert len(g.fanout(np.zeros(0, np.uint32)).records) == 0
     with pytest.raises(gpuaoi.GwError):
         g.fanout([tr.capacity + 5])
+
+
+def test_tick_statistics_match_oracle(ctx_factory):
+    """gw_tick_out.movers / nbr_old / nbr_new (the A_old, A_new terms of the
+    SURVEY 8(d) algorithmic bytes) equal the oracle's list sizes: distinct
+    slots with an AOI op, and the sums of their neighbour-list lengths before
+    and after the tick."""
+    tr = T.adversarial_trace(31, n=300, ticks=6)
+    g = ctx_factory()
+    gpuaoi.load_space(g, tr)
+    o = pyorc.OracleSpace(tr.capacity, tr.d, pyorc.SEQRULE)
+    pyorc.load_trace(o, tr)
+    for ops in tr.ticks:
+        aoi = np.unique(ops["slot"][np.isin(ops["kind"], [T.OP_ENTER, T.OP_MOVED, T.OP_LEAVE])])
+        a_old = sum(len(o.neighbors(int(s))) for s in aoi)
+        assert o.tick(ops) == 0
+        a_new = sum(len(o.neighbors(int(s))) for s in aoi)
+        g.submit(ops)
+        r = g.tick()
+        assert (r.movers, r.nbr_old, r.nbr_new) == (len(aoi), a_old, a_new)

@@ -33,6 +33,24 @@ __device__ __forceinline__ T wave_incl_scan(T x) {
     return x;
 }
 
+// 32-bit inclusive scan on the DPP network (VALU lane moves; the shuffle
+// version above goes through ds_bpermute, an LDS round trip per step, which
+// sits on the latency chain of every per-mover / per-entity walk): row_shr
+// 1, 2, 4, 8 inside each 16-lane row, then row_bcast:15 into rows 1 and 3 and
+// row_bcast:31 into rows 2 and 3 (GFX9 broadcast modes).  Lanes a DPP move
+// does not write keep the identity 0.
+template <>
+__device__ __forceinline__ uint32_t wave_incl_scan<uint32_t>(uint32_t v) {
+    int x = (int)v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return (uint32_t)x;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T x) {
 #pragma unroll

@@ -51,6 +51,31 @@ __device__ __forceinline__ uint32_t wave_incl_scan<uint32_t>(uint32_t v) {
     return (uint32_t)x;
 }
 
+// 64-bit version: each DPP step moves both halves, then one 64-bit add
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long x, int ctrl_sel) {
+    const int lo = (int)(uint32_t)x, hi = (int)(uint32_t)(x >> 32);
+    int a, b;
+    switch (ctrl_sel) {
+    case 0: a = __builtin_amdgcn_update_dpp(0, lo, 0x111, 0xf, 0xf, false); b = __builtin_amdgcn_update_dpp(0, hi, 0x111, 0xf, 0xf, false); break;
+    case 1: a = __builtin_amdgcn_update_dpp(0, lo, 0x112, 0xf, 0xf, false); b = __builtin_amdgcn_update_dpp(0, hi, 0x112, 0xf, 0xf, false); break;
+    case 2: a = __builtin_amdgcn_update_dpp(0, lo, 0x114, 0xf, 0xf, false); b = __builtin_amdgcn_update_dpp(0, hi, 0x114, 0xf, 0xf, false); break;
+    case 3: a = __builtin_amdgcn_update_dpp(0, lo, 0x118, 0xf, 0xf, false); b = __builtin_amdgcn_update_dpp(0, hi, 0x118, 0xf, 0xf, false); break;
+    case 4: a = __builtin_amdgcn_update_dpp(0, lo, 0x142, 0xa, 0xf, false); b = __builtin_amdgcn_update_dpp(0, hi, 0x142, 0xa, 0xf, false); break;
+    default: a = __builtin_amdgcn_update_dpp(0, lo, 0x143, 0xc, 0xf, false); b = __builtin_amdgcn_update_dpp(0, hi, 0x143, 0xc, 0xf, false); break;
+    }
+    return ((unsigned long long)(uint32_t)b << 32) | (uint32_t)a;
+}
+template <>
+__device__ __forceinline__ unsigned long long wave_incl_scan<unsigned long long>(unsigned long long x) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x += dpp_u64(x, i);
+    return x;
+}
+template <>
+__device__ __forceinline__ unsigned long wave_incl_scan<unsigned long>(unsigned long x) {
+    return (unsigned long)wave_incl_scan<unsigned long long>((unsigned long long)x);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T x) {
 #pragma unroll

@@ -157,6 +157,27 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// v of lane l ^ j.  j <= 8 stays inside a 16-lane row and runs on the DPP
+// network (quad_perm for 1 and 2, row_shl / row_shr for 4 and 8: VALU moves);
+// 16 and 32 cross rows and go through ds_bpermute.  j is a compile-time
+// constant once the sorting network is unrolled.
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v, int j) {
+    const int x = (int)v;
+    if (j == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    if (j == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0x4e, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    if (j == 4) {
+        const int up = __builtin_amdgcn_update_dpp(0, x, 0x104, 0xf, 0xf, false);         // row_shl:4 (lane + 4)
+        const int dn = __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);         // row_shr:4 (lane - 4)
+        return (uint32_t)((lane_id() & 4) ? dn : up);
+    }
+    if (j == 8) {
+        const int up = __builtin_amdgcn_update_dpp(0, x, 0x108, 0xf, 0xf, false);
+        const int dn = __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+        return (uint32_t)((lane_id() & 8) ? dn : up);
+    }
+    return (uint32_t)__shfl_xor(x, j, 64);
+}
+
 // ascending bitonic sort of one value per lane across the wave (registers)
 __device__ __forceinline__ uint32_t wave_sort64(uint32_t v) {
     const int l = lane_id();
@@ -164,7 +185,7 @@ __device__ __forceinline__ uint32_t wave_sort64(uint32_t v) {
     for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
         for (int j = k >> 1; j > 0; j >>= 1) {
-            uint32_t o = __shfl_xor(v, j, 64);
+            uint32_t o = lane_xor(v, j);
             bool up = (l & k) == 0;
             bool lower = (l & j) == 0;
             uint32_t mn = v < o ? v : o, mx = v < o ? o : v;

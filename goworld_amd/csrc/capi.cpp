@@ -844,7 +844,9 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         HIPCHK(hipMemsetAsync(c->ownbits, 0, ((size_t)C / 32 + 1) * 4, c->st));
         DevStats* h = c->hstats;
         h->overflow = 0; h->n_big = 0; h->n_bigseg = 0; h->ev_pk = 0;
-        memset(h->shard, 0, sizeof h->shard);
+        for (int i = 0; i < STAT_SHARDS; ++i)      // the diff's shards restart; the mover count stays
+            for (int f = 0; f < SH_FIELDS; ++f)
+                if (f != SH_MOVERS) h->shard[i][f] = 0;
         HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
         prof_begin(c, "diff");
         tick_diff(b, c->st);
@@ -865,7 +867,8 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     c->h_present = hs.n_present;
     gw_tick_out o{};
     const uint64_t n_enter = hs.ev_pk & 0xffffffffull, n_leave = hs.ev_pk >> 32;
-    const uint64_t n_mov = hs.n_movers;
+    uint64_t n_mov = 0;
+    for (int i = 0; i < STAT_SHARDS; ++i) n_mov += hs.shard[i][SH_MOVERS];
     // candidates tested == the candidate bounds; a_old | a_new << 32 per shard
     const uint64_t pairs = hs.cand_total;
     uint64_t a_old = 0, a_new = 0;
@@ -877,7 +880,7 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         unsigned long long f0 = 0, f2 = 0;
         for (int i = 0; i < STAT_SHARDS; ++i) { f0 += hs.shard[i][0]; f2 += hs.shard[i][2]; }
         fprintf(stderr, "gw_tick: movers %llu gm %llu cand %llu ev %llu+%llu big %llu bigseg %llu bigcell %llu "
-                "seg_lane %llu seg_wave %llu\n", hs.n_movers, hs.n_gm, hs.cand_total, hs.ev_pk & 0xffffffffull,
+                "seg_lane %llu seg_wave %llu\n", (unsigned long long)n_mov, hs.n_gm, hs.cand_total, hs.ev_pk & 0xffffffffull,
                 hs.ev_pk >> 32, hs.n_big, hs.n_bigseg, hs.n_bigcell, f0, f2);
     }
     o.ops = M;

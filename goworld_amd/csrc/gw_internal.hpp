@@ -75,13 +75,14 @@ __device__ __forceinline__ bool owned_x(const SpaceP& P, float x) { return x >= 
 
 constexpr int STAT_SHARDS = 256;
 constexpr int SH_FIELDS = 4;
+constexpr int SH_MOVERS = 0;  // distinct slots with an AOI op (k_classify)
 constexpr int SH_AOLD = 1;    // a_old | a_new << 32 (per-shard sums stay below 2^32)
 constexpr int SH_BAND = 3;
 
 // Device-side counters of one tick / collect (read back once per call).
 struct DevStats {
     unsigned long long n_present;     // entities in the grid
-    unsigned long long n_movers;      // distinct slots with an AOI op this tick
+    unsigned long long n_movers;      // unused (movers are counted in shard[][SH_MOVERS])
     unsigned long long n_bigcell;     // dirty cells too large for one wave
     unsigned long long cand_total;    // sum of candidate bounds over movers
     unsigned long long n_gm;          // mover-grid entries

@@ -60,16 +60,32 @@ __global__ void __launch_bounds__(NT) k_ops1(TickBufs b) {
     }
     if (op.kind != GW_OP_LEAVE) atomicMax(&b.last_pos[op.slot], (int32_t)i);
     if (op.kind != GW_OP_SYNC) atomicMax(&b.last_aoi[op.slot], (int32_t)i);
-    if (op.kind == GW_OP_LEAVE) atomicMax(&b.last_leave[op.slot], (int32_t)i);
+    if (op.kind == GW_OP_LEAVE) {
+        atomicMax(&b.last_leave[op.slot], (int32_t)i);
+        for (int c = 0; c < 2; ++c)                     // the last Leave that clears bit c
+            if (!((op.sync_flags >> c) & 1)) atomicMax(&b.clr[2 * op.slot + c], (int32_t)i);
+    }
 }
 
-// a Leave clears syncInfoFlag (the entity leaves this space's sync set)
+// syncInfoFlag across a Leave.  Space.leave leaves the flag alone (Space.go:
+// 219-242); a Leave's sync_flags is the mask of pending bits the entity keeps
+// (all when it stays in the game in the nil space, none when it is destroyed
+// or enters another AOI space, whose Enter flags it anew).  In call order the
+// ops are f -> (f & mask) and f -> (f | bits); per bit c the result is: the
+// old bit unless some Leave cleared c, OR'd with the bits of the ops after the
+// last Leave that cleared c.  One thread per slot with a Leave (its last one)
+// clears here, k_ops3 ORs.
 __global__ void __launch_bounds__(NT) k_ops2(TickBufs b) {
     uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i >= b.m) return;
     gw_op op = b.ops[i];
     if (op.slot >= b.w.cap || op.kind != GW_OP_LEAVE) return;
-    if (b.last_leave[op.slot] == (int32_t)i) b.w.flags[op.slot] = 0;
+    const uint32_t s = op.slot;
+    if (b.last_leave[s] != (int32_t)i) return;
+    uint32_t keep = 0xffffffffu;
+    for (int c = 0; c < 2; ++c)
+        if (b.clr[2 * s + c] >= 0) keep &= ~(1u << c);
+    if (keep != 0xffffffffu) b.w.flags[s] &= keep;
 }
 
 __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
@@ -78,9 +94,14 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
         const gw_op op = b.ops[i];
         const uint32_t s = op.slot;
         if (s < b.w.cap && op.kind >= GW_OP_ENTER && op.kind <= GW_OP_SYNC) {
-            // syncInfoFlag |= bits of every call after the last Leave (Space.go:196,
-            // Entity.go:1199-1204, 1286)
-            if ((int32_t)i > b.last_leave[s] && op.sync_flags) atomicOr(&b.w.flags[s], (uint32_t)op.sync_flags);
+            // syncInfoFlag |= bits of every call after the last Leave that
+            // cleared them (Space.go:196, Entity.go:1199-1204, 1286)
+            if (op.kind != GW_OP_LEAVE && op.sync_flags) {
+                uint32_t bits = 0;
+                for (int c = 0; c < 2; ++c)
+                    if (((op.sync_flags >> c) & 1) && (int32_t)i > b.clr[2 * s + c]) bits |= 1u << c;
+                if (bits) atomicOr(&b.w.flags[s], bits);
+            }
             if (b.last_pos[s] == (int32_t)i) b.w.pos[s] = make_float4(op.x, op.y, op.z, op.yaw);
             if (b.last_aoi[s] == (int32_t)i) {
                 AoiEnt a = b.w.aoi[s];
@@ -817,6 +838,7 @@ __global__ void __launch_bounds__(NT) k_tick_reset(TickBufs b) {
             b.last_pos[s] = -1;
             b.last_aoi[s] = -1;
             b.last_leave[s] = -1;
+            b.clr[2 * s] = b.clr[2 * s + 1] = -1;
         }
     }
     if (i < b.st->n_gm) {

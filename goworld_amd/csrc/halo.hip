@@ -7,7 +7,8 @@
 // last collect).  Four light passes over the owned ops, O(ops), no host sync:
 //   r1  last AOI op / last payload op / last Leave per slot (atomicMax, as
 //       k_ops1 of the tick; the same per-slot arrays, left at -1 after r4)
-//   r2  OR of the sync flags of the ops after the last Leave (atomicOr)
+//   r2  OR of the sync bits of the ops after the last Leave clearing each bit
+//       (atomicOr; a Leave's sync_flags is the mask of bits it keeps, k_ops2)
 //   r3  the entity's last op writes up to 3 rows per destination, entities
 //       placed by one wave-aggregated atomic per wave and destination
 //   r4  reset of the per-slot scratch; zero (NOP) rows past the entities
@@ -29,7 +30,7 @@ __device__ __forceinline__ bool op_valid(const gw_op& op, uint32_t cap) {
 
 __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
                                                 int32_t* last_pos, int32_t* last_aoi, int32_t* last_leave,
-                                                HaloStats* hs) {
+                                                int32_t* clr, HaloStats* hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i == 0) hs->cnt[0] = hs->cnt[1] = 0;         // placement counters of this call
     if (i >= n) return;
@@ -41,16 +42,23 @@ __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, ui
     }
     if (op.kind != GW_OP_LEAVE) atomicMax(&last_pos[op.slot], (int32_t)i);
     if (op.kind != GW_OP_SYNC) atomicMax(&last_aoi[op.slot], (int32_t)i);
-    if (op.kind == GW_OP_LEAVE) atomicMax(&last_leave[op.slot], (int32_t)i);
+    if (op.kind == GW_OP_LEAVE) {
+        atomicMax(&last_leave[op.slot], (int32_t)i);
+        for (int c = 0; c < 2; ++c)
+            if (!((op.sync_flags >> c) & 1)) atomicMax(&clr[2 * op.slot + c], (int32_t)i);
+    }
 }
 
 __global__ void __launch_bounds__(NT) k_route2(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
-                                                const int32_t* __restrict__ last_leave, uint32_t* rflag) {
+                                                const int32_t* __restrict__ clr, uint32_t* rflag) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
     const gw_op op = ops[i];
-    if (!op_valid(op, cap) || !(op.sync_flags & SIF_ROUTED)) return;
-    if ((int32_t)i > last_leave[op.slot]) atomicOr(&rflag[op.slot], (uint32_t)(op.sync_flags & SIF_ROUTED));
+    if (!op_valid(op, cap) || op.kind == GW_OP_LEAVE || !(op.sync_flags & SIF_ROUTED)) return;
+    uint32_t bits = 0;
+    for (int c = 0; c < 2; ++c)
+        if (((op.sync_flags >> c) & 1) && (int32_t)i > clr[2 * op.slot + c]) bits |= 1u << c;
+    if (bits) atomicOr(&rflag[op.slot], bits);
 }
 
 __device__ __forceinline__ gw_op mk_op(uint8_t kind, uint8_t flags, uint32_t slot, const gw_op* payload) {
@@ -76,6 +84,7 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
                                                 uint32_t n, World w, const int32_t* __restrict__ last_pos,
                                                 const int32_t* __restrict__ last_aoi,
                                                 const int32_t* __restrict__ last_leave,
+                                                const int32_t* __restrict__ clr,
                                                 const uint32_t* __restrict__ rflag, float max_step, HaloDsts D,
                                                 HaloStats* hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
@@ -110,7 +119,12 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
             if (old_p && new_p && fabsf(new_x - old_x) > max_step) atomicAdd(&hs->bad_moves, 1ull);
         }
         if (lp >= 0) op_pos = ops[lp];
-        f = (((ll >= 0) ? 0u : w.flags[s]) | rflag[s]) & SIF_ROUTED;   // syncInfoFlag since the last Leave
+        // syncInfoFlag after the tick's ops (k_ops2 / k_ops3): old bits a Leave
+        // did not clear, OR'd with the bits set since the Leave that cleared them
+        uint32_t keep = 0;
+        for (int c = 0; c < 2; ++c)
+            if (clr[2 * s + c] < 0) keep |= 1u << c;
+        f = ((w.flags[s] & keep) | rflag[s]) & SIF_ROUTED;
     }
     for (uint32_t d = 0; d < D.n; ++d) {
         const HaloDst& dst = D.d[d];
@@ -149,7 +163,8 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
 
 __global__ void __launch_bounds__(NT) k_route4(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
                                                 int32_t* last_pos, int32_t* last_aoi, int32_t* last_leave,
-                                                uint32_t* rflag, HaloDsts D, const HaloStats* __restrict__ hs) {
+                                                int32_t* clr, uint32_t* rflag, HaloDsts D,
+                                                const HaloStats* __restrict__ hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     // rows past the placed entities become NOPs (thread i: row i of each buffer)
     for (uint32_t d = 0; d < D.n; ++d) {
@@ -162,6 +177,7 @@ __global__ void __launch_bounds__(NT) k_route4(const gw_op* __restrict__ ops, ui
     last_pos[op.slot] = -1;
     last_aoi[op.slot] = -1;
     last_leave[op.slot] = -1;
+    clr[2 * op.slot] = clr[2 * op.slot + 1] = -1;
     rflag[op.slot] = 0;
 }
 
@@ -177,16 +193,16 @@ __global__ void __launch_bounds__(NT) k_split_rows(const gw_halo_row* __restrict
 
 void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
                        float max_step, const HaloDsts& D, int32_t* last_pos, int32_t* last_aoi,
-                       int32_t* last_leave, uint32_t* rflag, HaloStats* hs, hipStream_t s) {
+                       int32_t* last_leave, int32_t* clr, uint32_t* rflag, HaloStats* hs, hipStream_t s) {
     const uint32_t nb = nblk1(n, NT);
     uint64_t rows = 0;
     for (uint32_t d = 0; d < D.n; ++d) rows = std::max<uint64_t>(rows, (uint64_t)D.d[d].cap * ROWS);
-    hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, last_pos, last_aoi, last_leave, hs);
-    hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, last_leave, rflag);
+    hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, last_pos, last_aoi, last_leave, clr, hs);
+    hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, clr, rflag);
     hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, last_pos, last_aoi, last_leave,
-                       rflag, max_step, D, hs);
+                       clr, rflag, max_step, D, hs);
     hipLaunchKernelGGL(k_route4, dim3(nblk1(std::max<uint64_t>(n, rows), NT)), dim3(NT), 0, s, ops, n, w.cap,
-                       last_pos, last_aoi, last_leave, rflag, D, hs);
+                       last_pos, last_aoi, last_leave, clr, rflag, D, hs);
 }
 
 void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,

@@ -3,8 +3,9 @@
 // primitive instantiations used by the host code.
 //
 // A flagged entity e's records are: its own client's (syncInfoFlag bit0 and e
-// has a client), then one per neighbour w with a client (bit1), neighbours in
-// grid order ((cell, slot): deterministic).  The neighbours are evaluated from
+// has a client; also after e left the space with the bit kept), then one per
+// neighbour w with a client (bit1, e present), neighbours in grid order
+// ((cell, slot): deterministic).  The neighbours are evaluated from
 // the current grid with the stamp-resolved relation (dev_common.hpp), so no
 // list is kept.  Count pass, scan, write pass; records land at their final
 // offsets, grouped by gate afterwards with a stable radix sort.
@@ -144,9 +145,12 @@ __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __re
             e = flagged[k];
             f = fbits[k];
             const AoiEnt a = w.aoi[e];
-            if ((a.meta & PRESENT_BIT) && owned_x(w.sp[a.meta & SPACE_MASK], a.x)) {
+            // an entity that left the space (into the nil space, keeping its
+            // flag) still syncs its own client (Entity.go:1221-1239); only a
+            // present one has neighbours
+            if (owned_x(w.sp[a.meta & SPACE_MASK], a.x)) {
                 if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) r = 1;
-                if (f & GW_SIF_NEIGHBOR_CLIENTS) {
+                if ((f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
                     const unsigned long long c = w.nbc[e];
                     if ((uint32_t)(c >> 32) == w.epoch) r += (uint32_t)c;   // counted by this tick's diff
                     else walk = true;
@@ -209,13 +213,13 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
             continue;
         }
         const AoiEnt a = w.aoi[e];
-        if (!(a.meta & PRESENT_BIT) || !owned_x(w.sp[a.meta & SPACE_MASK], a.x)) continue;
+        if (!owned_x(w.sp[a.meta & SPACE_MASK], a.x)) continue;
         const float4 p = w.pos[e];
         if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
             if (ln == 0) st_record_nt(rec + at, e, e, p);
             ++at;
         }
-        if (f & GW_SIF_NEIGHBOR_CLIENTS) {
+        if ((f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
             wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
                 const bool take = rel && g != 0;
                 const uint64_t bt = wave_ballot(take);

@@ -248,11 +248,13 @@ def config1(ticks: int = 1000, seed: int = 1, n: int = 1000, big_steps: bool = F
 
 
 def adversarial_trace(seed: int, n: int = 400, ticks: int = 30, d: float = 100.0,
-                      churn: bool = True) -> SpaceTrace:
+                      churn: bool = True, leave_masks: bool = False) -> SpaceTrace:
     """Non-dyadic float32 positions placed on the rounding edge of each other's
     windows (other.x == fl(c.x +- d) +- 1 ulp), so the rounded-bounds test is
     asymmetric and the seq rule decides.  With churn, ticks also contain
-    Leave / re-Enter / Sync ops and repeated ops on one slot."""
+    Leave / re-Enter / Sync ops and repeated ops on one slot.  leave_masks:
+    Leave ops carry a random keep-mask of pending sync bits (0..3; the entity
+    stays in the game in the nil space, Space.go:219-242) instead of 0."""
     d32 = np.float32(d)
     base_x = (rand_unit(stream_key(seed, 1), n) * 600 - 300).astype(np.float32)
     base_z = (rand_unit(stream_key(seed, 2), n) * 600 - 300).astype(np.float32)
@@ -295,7 +297,8 @@ def adversarial_trace(seed: int, n: int = 400, ticks: int = 30, d: float = 100.0
                 continue
             if churn and kinds_r[j] < 0.05:
                 present[a] = False
-                rows.append((OP_LEAVE, 0, a, x[a], z[a], yaw[a]))
+                mask = int(kinds_r[j] * 80) & 3 if leave_masks else 0
+                rows.append((OP_LEAVE, mask, a, x[a], z[a], yaw[a]))
             elif churn and kinds_r[j] < 0.10:
                 yaw[a] = np.float32(kinds_r[j] * 31)
                 rows.append((OP_SYNC, 3, a, x[a], z[a], yaw[a]))

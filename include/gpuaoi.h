@@ -77,7 +77,8 @@ extern "C" {
  * (the seq number of the batched-parity contract is the index of the op in
  * the tick's concatenated submission stream).  x,y,z,yaw are the entity's
  * Position and yaw after the op (for LEAVE they are ignored).  sync_flags is
- * ORed into the entity's syncInfoFlag; a LEAVE clears it. */
+ * ORed into the entity's syncInfoFlag; for a LEAVE it is the mask of pending
+ * bits the entity keeps (see the note before gw_space_restore). */
 typedef struct gw_op {
     uint8_t  kind;        /* GW_OP_*                                        */
     uint8_t  sync_flags;  /* GW_SIF_* bits set by this call                  */
@@ -140,8 +141,13 @@ typedef struct gw_tick_out {
                                       packet MT_SYNC_POSITION_YAW_ON_CLIENTS   */
 
 typedef struct gw_sync_out {
-    /* canonical order: sorted by (gate(watcher), entity, watcher); with
-     * GW_SYNC_BY_CLIENT by (gate(watcher), watcher, entity)                    */
+    /* Deterministic order.  Default: grouped by gate(watcher) (gate_off), and
+     * inside a gate by entity ascending; an entity's own-client record comes
+     * first, then its neighbours' records in grid order: (cell of the
+     * watcher's position, watcher slot) - the order the window walk visits
+     * them.  Only the gate grouping is a sort.  With GW_SYNC_BY_CLIENT: the
+     * canonical (gate(watcher), watcher, entity) order of SURVEY App. B.5,
+     * each client's records one contiguous segment (client_off).            */
     const gw_sync_record* rec;      /* host pointer (NULL unless COPY_TO_HOST) */
     const gw_sync_record* rec_dev;  /* device pointer, always valid            */
     uint64_t n_rec;
@@ -235,6 +241,14 @@ int  gw_submit_device_rows(gw_ctx* ctx, const gw_halo_row* dev_rows, uint32_t n)
 /* Counters accumulated by gw_route_halo since the last call (synchronises,
  * then resets them). */
 int  gw_halo_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops);
+
+/* (GW_OP_LEAVE: sync_flags is the mask of the entity's pending syncInfoFlag
+ * bits it keeps.  Space.leave leaves the flag alone (Space.go:219-242), so an
+ * entity that stays in the game in the nil space keeps them (pass 3) and the
+ * next collect still sends its own-client record at its last position
+ * (CollectEntitySyncInfos scans every entity, Entity.go:1221-1239); pass 0
+ * when it is destroyed (Entity.go:136-157) or enters another AOI space, whose
+ * Enter flags it anew.) */
 
 /* Restore / bulk load (Space.go:209-214 restoreEntity, EntityManager.go:
  * 556-617 freeze/restore): entities slots[i] enter space

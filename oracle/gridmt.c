@@ -242,7 +242,7 @@ int gmt_tick(gmt* g, const gw_op* ops, uint32_t n) {
         const gw_op* op = &ops[i];
         if (op->slot >= g->cap || op->kind < GW_OP_ENTER || op->kind > GW_OP_SYNC) { free(movers); return GW_EINVAL; }
         const uint32_t a = op->slot;
-        if (op->kind == GW_OP_LEAVE) g->flags[a] = 0;
+        if (op->kind == GW_OP_LEAVE) g->flags[a] &= op->sync_flags;   /* keep-mask (orc.c) */
         else {
             g->flags[a] |= op->sync_flags;
             g->px[a] = op->x; g->py[a] = op->y; g->pz[a] = op->z; g->pyaw[a] = op->yaw;
@@ -371,8 +371,8 @@ uint64_t gmt_collect(gmt* g) {
         const uint32_t e = fl[k];
         const uint32_t f = g->flags[e];
         uint64_t c = 0;
+        if ((f & GW_SIF_OWN_CLIENT) && g->gate[e]) ++c;       /* also after a Leave (orc.c) */
         if (g->present[e]) {
-            if ((f & GW_SIF_OWN_CLIENT) && g->gate[e]) ++c;
             if (f & GW_SIF_NEIGHBOR_CLIENTS) {
                 const float ex = g->x[e], ez = g->z[e];
                 const uint64_t se = g->stamp[e];
@@ -395,7 +395,7 @@ uint64_t gmt_collect(gmt* g) {
         uint64_t at = cnt[k];
         gw_sync_record r;
         r.entity = e; r.x = g->px[e]; r.y = g->py[e]; r.z = g->pz[e]; r.yaw = g->pyaw[e];
-        if (g->present[e] && (f & GW_SIF_OWN_CLIENT) && g->gate[e]) { r.watcher = e; g->rec[at++] = r; }
+        if ((f & GW_SIF_OWN_CLIENT) && g->gate[e]) { r.watcher = e; g->rec[at++] = r; }
         for (size_t j = 0; j < nb[k].n; ++j) { r.watcher = nb[k].a[j]; g->rec[at++] = r; }
         free(nb[k].a);
         g->flags[e] = 0;

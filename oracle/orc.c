@@ -572,7 +572,11 @@ int orc_tick(orc_space* s, const gw_op* ops, uint32_t n) {
         }
         if (rc) break;
         /* sync state and syncInfoFlag, in call order */
-        if (op->kind == GW_OP_LEAVE) { s->flags[a] = 0; }
+        /* Space.leave leaves syncInfoFlag alone (Space.go:219-242): a Leave's
+         * sync_flags is the mask of pending bits the entity keeps (3 = all: it
+         * stays in the game in the nil space; 0: destroyed / entering another
+         * AOI space, whose Enter flags it anew) */
+        if (op->kind == GW_OP_LEAVE) { s->flags[a] &= op->sync_flags; }
         else {
             s->flags[a] |= op->sync_flags;
             s->px[a] = op->x; s->py[a] = op->y; s->pz[a] = op->z; s->pyaw[a] = op->yaw;
@@ -640,8 +644,11 @@ uint64_t orc_collect(orc_space* s) {
         uint8_t f = s->flags[e];
         if (!f) continue;
         s->flags[e] = 0;
-        if (!s->present[e]) continue;
+        /* every entity of the game is scanned (Entity.go:1221-1239): one that
+         * left into the nil space still syncs its own client; it has no
+         * InterestedBy left */
         if ((f & GW_SIF_OWN_CLIENT) && s->gate[e]) push_rec(s, &cap, e, e);
+        if (!s->present[e]) continue;
         if (f & GW_SIF_NEIGHBOR_CLIENTS) {
             const vec32* by = s->by ? &s->by[e] : &s->nb[e];        /* e.InterestedBy */
             for (uint32_t j = 0; j < by->n; ++j)

@@ -19,6 +19,7 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from goworld_amd import dworld, traces as T  # noqa: E402
+import torch_router  # noqa: E402  (tests/, on sys.path as the script's dir)
 
 
 class OracleStrip:
@@ -31,10 +32,10 @@ class OracleStrip:
         self.words, self.stamps = [], []
 
     def make_router(self, geom, rank, n_global, device, halo_cap):
-        return dworld.Router(geom, rank, n_global, device, halo_cap)
+        return torch_router.Router(geom, rank, n_global, device, halo_cap)
 
     def submit_rows(self, rows):
-        self.submit(*dworld.split_rows(rows))
+        self.submit(*torch_router.split_rows(rows))
 
     def create_space(self, d, cap, bounds):
         self.o = self.pyorc.OracleSpace(cap, d, self.pyorc.SEQRULE)
@@ -80,7 +81,9 @@ class OracleStrip:
     def collect(self, copy=True):
         r = self.o.collect()
         ent = r["entity"]
-        keep = self.present[ent] & self._owned(self.x[ent])
+        # own records of leavers that kept their flag (the owner's copy; ghost
+        # copies had theirs cleared by the LEAVE row) are emitted too
+        keep = self._owned(self.x[ent]) & (self.present[ent] | (r["watcher"] == ent))
         return _Res(records=r[keep].copy())
 
 

@@ -16,6 +16,8 @@ import numpy as np
 import pytest
 
 from goworld_amd import dworld, traces as T
+
+import torch_router
 from oracle import pyorc
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -138,7 +140,7 @@ def _canon_rows(buf, K):
 @pytest.mark.gpu
 def test_hip_router_rows_match_torch_router():
     """gw_route_halo (halo.hip) writes, per neighbour, the same entity rows
-    as the torch statement of the protocol (dworld.Router), tick by tick, for
+    as the torch statement of the protocol (tests/torch_router.py), tick by tick, for
     the middle rank of a 3-strip world (order of entities aside)."""
     import torch
     from goworld_amd import gpuaoi
@@ -151,7 +153,7 @@ def test_hip_router_rows_match_torch_router():
         eng = dworld.HipStrip(g)
         eng.create_space(tr.d, tr.n, tr.bounds)
         hip = eng.make_router(geom, 1, tr.n, dev, K)
-        ref = dworld.Router(geom, 1, tr.n, dev, K)
+        ref = torch_router.Router(geom, 1, tr.n, dev, K)
         n_rows = 0
         for t in range(len(tr.ticks)):
             w = torch.from_numpy(dworld.ops_to_words(tr.rank_ops(t, 1)).copy()).to(dev)

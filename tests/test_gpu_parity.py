@@ -145,7 +145,7 @@ def test_tiny_hand_made(ctx_factory):
 
 @pytest.mark.parametrize("seed", [11, 12, 13])
 def test_adversarial_rounding_and_churn_vs_xzlist(ctx_factory, seed):
-    tr = T.adversarial_trace(seed, n=300, ticks=12)
+    tr = T.adversarial_trace(seed, n=300, ticks=12, leave_masks=seed == 13)   # 13: Leave keep-masks
     h = Harness(ctx_factory(), [tr], mode=pyorc.XZLIST)
     h.check_collect()
     for t in range(len(tr.ticks)):

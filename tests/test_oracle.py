@@ -53,6 +53,7 @@ def op(kind, slot, x=0.0, z=0.0, y=0.0, yaw=0.0, flags=3):
 @pytest.mark.parametrize("name,make", [
     ("adversarial", lambda: T.adversarial_trace(11, n=300, ticks=12)),
     ("adversarial_nochurn", lambda: T.adversarial_trace(12, n=250, ticks=10, churn=False)),
+    ("adversarial_leave_masks", lambda: T.adversarial_trace(13, n=300, ticks=12, leave_masks=True)),
     ("config1b", lambda: T.config1(ticks=30, n=300, big_steps=True)),
     ("config1", lambda: T.config1(ticks=20, n=300)),
     ("dyadic", lambda: T.dyadic_walk_trace(5, 1500, 1024.0, 100.0, 4)),
@@ -166,6 +167,39 @@ def test_own_client_record_rules():                          # (v)
     assert sorted(zip(r["watcher"], r["entity"])) == [(0, 1), (1, 1), (2, 1)]
     assert all(r["yaw"] == np.float32(2.0))
     assert len(sp.collect()) == 0         # flags cleared by the collect
+
+
+def test_leave_keeps_pending_flags_by_mask():
+    """Space.leave leaves syncInfoFlag alone (Space.go:219-242) and
+    CollectEntitySyncInfos scans every entity of the game (Entity.go:1221-1239):
+    an entity that moved and then left into the nil space in the same interval
+    still gets its own-client record (at its last position), and no neighbour
+    records (InterestedBy is empty).  A Leave op's sync_flags is the mask of
+    pending bits kept: 3 for the nil space, 0 when the entity is destroyed
+    (Entity.go:136-157) or enters another AOI space (whose Enter flags it)."""
+    for mode in MODES:
+        sp = one(mode=mode)
+        for s in range(3):
+            sp.set_client(s, 1)
+        sp.tick(np.concatenate([op(1, 0, 0, 0), op(1, 1, 1, 1), op(1, 2, 2, 2)]))
+        sp.collect()
+        # moved (own + neighbours), then left into the nil space keeping the flag
+        sp.tick(np.concatenate([op(2, 0, 5, 6, y=7, yaw=0.5, flags=3), op(3, 0, flags=3)]))
+        r = sp.collect()
+        assert sorted(zip(r["watcher"], r["entity"])) == [(0, 0)]
+        assert (r["x"][0], r["y"][0], r["z"][0], r["yaw"][0]) == (5, 7, 6, np.float32(0.5))
+        assert len(sp.collect()) == 0                      # cleared by the collect
+        # destroyed: nothing
+        sp.tick(np.concatenate([op(2, 1, 3, 3, flags=3), op(3, 1, flags=0)]))
+        assert len(sp.collect()) == 0
+        # a client-originated move (neighbour bit only) then nil space: nothing
+        sp.tick(np.concatenate([op(2, 2, 3, 3, flags=2), op(3, 2, flags=3)]))
+        assert len(sp.collect()) == 0
+        # keep-masks compose in call order: f & mask, f | bits
+        sp.tick(np.concatenate([op(1, 0, 0, 0, flags=2), op(3, 0, flags=1),    # -> 0
+                                op(1, 0, 1, 0, flags=1), op(3, 0, flags=3)]))  # -> 1
+        r = sp.collect()
+        assert sorted(zip(r["watcher"], r["entity"])) == [(0, 0)] and r["x"][0] == 1
 
 
 def test_distance_zero_and_inclusive_boundary():             # (vi)

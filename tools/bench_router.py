@@ -1,6 +1,6 @@
 """Per-tick cost of the decomposed-world routing on one GPU: 100k owned Moved
 ops of a config #3 strip (rank min(3, N-1) of an N-strip world); HipRouter
-(gw_route_halo) and the torch statement (dworld.Router).
+(gw_route_halo) and the torch statement (tests/torch_router.py).
 usage: python tools/bench_router.py [N]"""
 import os
 import sys
@@ -10,6 +10,9 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from goworld_amd import dworld, gpuaoi, traces as T  # noqa: E402
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+import torch_router  # noqa: E402
 
 ws = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 r, n, side, K = min(3, ws - 1), 1_000_000, 32768.0, 16384
@@ -31,7 +34,7 @@ g = gpuaoi.GpuAOI(0)
 eng = dworld.HipStrip(g)
 lo, hi = geom.ext(r)
 eng.create_space(tr.d, n * ws, (max(lo, x0), -side / 2, min(hi, x0 + ws * side), side / 2))
-routers = {"hip": eng.make_router(geom, r, n * ws, dev, K), "torch": dworld.Router(geom, r, n * ws, dev, K)}
+routers = {"hip": eng.make_router(geom, r, n * ws, dev, K), "torch": torch_router.Router(geom, r, n * ws, dev, K)}
 enter = T.enter_ops(tr.init_slots, tr.init_x, tr.init_y, tr.init_z, tr.init_yaw)
 tick = 0
 for i in range(0, n, 1 << 18):

@@ -51,7 +51,10 @@ def parse():
     ap.add_argument("--entities", type=int, default=1_000_000)
     ap.add_argument("--side", type=float, default=32768.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="multi-threaded CPU baseline time budget")
+    ap.add_argument("--cpu-st-max-seconds", type=float, default=240.0,
+                    help="guard on the single-thread baseline (it replays one full tick)")
+    ap.add_argument("--e2e-steps", type=int, default=3, help="untimed end-to-end steps (host in/out)")
     ap.add_argument("--profile-stages", type=int, default=1,
                     help="1: HIP events around the dominant kernel's stage in the timed region (roofline) and "
                          "a per-stage breakdown over extra untimed steps; 0: none")
@@ -114,44 +117,86 @@ class Ctl:
 
 
 STAGE_KERNEL = {"diff": "k_mover<2, 1>"}
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
+PMC_DIR = os.path.join(ROOT, "profiles")
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
-    (tools/gpu/pmc.sh: FETCH_SIZE*2 + WRITE_SIZE, the gfx950 correction of
-    MI355X_MICROARCH.md); PMC counters cannot be read inside the timed run."""
+def src_hash():
+    """Hash of the kernel sources (the PMC pass must come from this HEAD)."""
+    import hashlib
+    h = hashlib.sha256()
+    d = os.path.join(ROOT, "goworld_amd", "csrc")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".hpp", ".cpp")):
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(config):
+    """HBM bytes per launch per kernel from the committed rocprofv3 PMC pass of
+    this config (tools/gpu/pmc.sh: FETCH_SIZE*2 + WRITE_SIZE, the gfx950
+    correction of MI355X_MICROARCH.md), only if it was taken on these kernel
+    sources (src_hash); PMC counters cannot be read inside the timed run."""
+    path = os.path.join(PMC_DIR, f"pmc_config{config}.json")
     try:
-        import json as _j
-        d = _j.load(open(PMC_FILE))
-        return d[kernel]["hbm_bytes"], os.path.relpath(PMC_FILE, ROOT)
-    except (OSError, KeyError, ValueError):
-        return None, None
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None, "missing"
+    if d.get("src_hash") != src_hash():
+        return None, os.path.relpath(path, ROOT), "stale (taken on other kernel sources)"
+    return d.get("kernels", {}), os.path.relpath(path, ROOT), d.get("src_hash")
 
 
-def cpu_baseline(tr, seconds):
-    """Oracle XZList restatement (go-aoi algorithm + goworld glue), one thread,
-    replaying tick 0's ops one by one until the time budget is spent."""
+def cpu_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "cpus_allowed": allowed,
+            "GOMAXPROCS": "n/a (no Go toolchain: the go-aoi algorithm runs as its C restatement)"}
+
+
+def cpu_baseline(tr, max_seconds):
+    """Oracle XZList restatement (go-aoi v0.2.0 algorithm + goworld glue:
+    InterestedIn/By sets, create/destroy message counts), ONE thread, replaying
+    all of tick 0's ops one by one (the reference's single game goroutine,
+    GameService.go:77-190); max_seconds only guards against a pathological host."""
     from oracle import pyorc
     sp = pyorc.OracleSpace(tr.capacity, tr.d, pyorc.XZLIST)
     t0 = time.perf_counter()
     pyorc.load_trace(sp, tr)
     build_s = time.perf_counter() - t0
     ops = tr.ticks[0]
-    done, spent, chunk = 0, 0.0, 200
-    while spent < seconds and done < len(ops):
+    done, spent, chunk = 0, 0.0, 1000
+    raw_e = raw_l = net = 0
+    while done < len(ops) and spent < max_seconds:
         part = ops[done:done + chunk]
         t = time.perf_counter()
         rc = sp.tick(part)
         spent += time.perf_counter() - t
         assert rc == 0
+        re_, rl_, _, _ = sp.raw_counts()
+        e, l = sp.events()
+        raw_e += re_; raw_l += rl_; net += len(e) + len(l)
         done += len(part)
     sp.close()
+    full = done == len(ops)
     return {"value": done / spent, "unit": "updates/s", "cores": 1, "kind": "port",
-            "sample": f"{done} Moved ops of tick 0 of config #3 (1M entities), applied one by one through the "
-                      f"XZList restatement incl. InterestedIn/By glue and raw->net event reduction, "
-                      f"{spent:.1f}s timed; initial population bulk-built untimed ({build_s:.1f}s)",
-            "per_op_us": spent / done * 1e6}
+            "sample": (f"{'all' if full else 'first'} {done} Moved ops of tick 0 of config #3 (1M entities; "
+                       f"{'one full tick' if full else 'time guard hit'}), applied one by one through the C "
+                       f"restatement of go-aoi's XZList incl. InterestedIn/By glue, {spent:.1f}s on one core; "
+                       f"initial population bulk-built untimed ({build_s:.1f}s)"),
+            "per_op_us": spent / done * 1e6, "full_tick": full,
+            "raw_events_per_sec": (raw_e + raw_l) / spent, "net_events_per_sec": net / spent,
+            **cpu_info()}
 
 
 def cpu_baseline_mt(seconds, entities, side):
@@ -201,6 +246,7 @@ class SpaceRun:
         g.sync_collect(copy=False)                      # clear the Enter flags (untimed)
         # all ticks' ops resident in HBM before timing
         self.m = len(self.tr.ticks[0])
+        self.host_ticks = self.tr.ticks
         ops_all = np.concatenate(self.tr.ticks)
         self.dev_ops = g.dev_alloc(ops_all.nbytes)
         g.h2d(self.dev_ops, ops_all)
@@ -215,6 +261,17 @@ class SpaceRun:
         g.tick(copy=False, defer=True)       # no host sync: the collect's sync settles it
         s = g.sync_collect(copy=False, by_client=self.by_client)
         r = g.tick_result()
+        return r.movers, r, s
+
+    def step_e2e(self, t):
+        """The Go caller's game tick: host ops in (gw_submit: pageable host
+        memory, copied to the device), the canonical events and the sync
+        records out to pinned host buffers (GW_TICK_COPY_TO_HOST /
+        GW_SYNC_COPY_TO_HOST), i.e. PCIe both ways."""
+        g = self.g
+        g.submit(self.host_ticks[t])
+        r = g.tick(copy=True)
+        s = g.sync_collect(copy=True, by_client=self.by_client)
         return r.movers, r, s
 
     def close(self):
@@ -271,6 +328,7 @@ class ManySpacesRun(SpaceRun):
             ops["yaw"] = yaw[idx]
             ops_all.append(ops)
         self.m = len(ops_all[0])
+        self.host_ticks = ops_all
         ops_all = np.concatenate(ops_all)
         self.dev_ops = g.dev_alloc(ops_all.nbytes)
         g.h2d(self.dev_ops, ops_all)
@@ -374,9 +432,10 @@ def main():
     ws, rank = ctl.ws, ctl.rank
     extra = 5 if a.profile_stages else 0         # untimed steps for the per-stage breakdown
     cm = a.client_msgs if (ws == 1 and a.config == 3) else 0
-    ticks = a.warmup + a.steps + extra + cm
-    t_load = time.perf_counter()
     world = (ws > 1 and a.mode == "world") or a.config == 5
+    n_e2e = 0 if world else a.e2e_steps
+    ticks = a.warmup + a.steps + extra + cm + n_e2e
+    t_load = time.perf_counter()
     if a.config == 4:
         run = ManySpacesRun(a, ctl, ticks)
     else:
@@ -395,7 +454,8 @@ def main():
     for t in range(a.warmup):
         run.step(t)
     g.set_profiling(2 if a.profile_stages else 0)    # the dominant kernel's stage only
-    tot = dict(ops=0, events=0, records=0, bytes_alg=0)
+    tot = dict(ops=0, events=0, records=0, bytes_alg=0, mover_alg=0, a_nbr=0, cand=0, own_copy_alg=0,
+               sync_write_alg=0)
     ctl.barrier()
     g.synchronize()
     t0 = time.perf_counter()
@@ -405,6 +465,15 @@ def main():
         tot["events"] += r.n_enter + r.n_leave
         tot["records"] += s.n_rec
         tot["bytes_alg"] += r.bytes_alg + s.bytes_alg
+        ev = r.n_enter + r.n_leave
+        # SURVEY 8(d) terms per kernel: k_mover produces the neighbour-list
+        # terms and the net events, 4*(A_old+A_new) + 8*E; k_own_copy reads and
+        # writes the events (8*E each way); k_sync_write writes the records
+        tot["mover_alg"] += 4 * (r.nbr_old + r.nbr_new) + 8 * ev
+        tot["own_copy_alg"] += 16 * ev
+        tot["sync_write_alg"] += 24 * s.n_rec
+        tot["a_nbr"] += r.nbr_old + r.nbr_new
+        tot["cand"] += r.pairs_tested
     g.synchronize()
     t1 = time.perf_counter()
     ctl.barrier()
@@ -422,6 +491,21 @@ def main():
         acc_stages()
         g.set_profiling(0)
     client = client_msgs(run, a.warmup + a.steps + extra, cm) if cm else None
+    e2e = None
+    if n_e2e:
+        # end-to-end game ticks (host ops in, events + records out over PCIe),
+        # after the timed region; wall clock per step
+        t_e, e_ops = 0.0, 0
+        for t in range(a.warmup + a.steps + extra + cm, a.warmup + a.steps + extra + cm + n_e2e):
+            g.synchronize()
+            c0 = time.perf_counter()
+            upd, r, s_ = run.step_e2e(t)
+            t_e += time.perf_counter() - c0
+            e_ops += upd
+        e2e = {"ms_per_step": t_e / n_e2e * 1e3, "updates_per_sec": e_ops / t_e, "steps": n_e2e,
+               "what": "gw_submit(host ops) + gw_tick(COPY_TO_HOST) + gw_sync_collect(COPY_TO_HOST): the Go "
+                       "caller's tick, events and compact records copied to pinned host memory (PCIe); "
+                       "wall clock, untimed by the headline"}
     mx = ctl.reduce([elapsed], "MAX")[0]
     sums = ctl.reduce([tot["ops"], tot["events"], tot["records"]], "SUM")
     if rank != 0:
@@ -471,27 +555,46 @@ def main():
         "tick_hbm_frac": (tot["bytes_alg"] / K) / (mx / K) / (HBM_PEAK_GBS * 1e9),
         "load_s": t_load,
     }
+    if stage_us or dom_us:
+        # the dominant kernel: k_mover, alone in stage "diff", timed live by HIP
+        # events on the library's stream in every timed step.  achieved = its
+        # SURVEY 8(d) bytes per launch (4*(A_old+A_new) + 8*E: the neighbour-list
+        # and event terms it produces; A and E from gw_tick_out) / that duration
+        mover_alg = tot["mover_alg"] / K
+        ach = mover_alg / (dom_us * 1e-6) / 1e9
+        kern, psrc, pstamp = pmc_traffic(a.config if a.config != 5 or ws == 1 else None)
+        def traffic(k):
+            return (kern or {}).get(k, {}).get("hbm_bytes") if kern else None
+        mv = STAGE_KERNEL["diff"]
+        line["roofline"] = {"bound": "hbm", "kernel": mv, "achieved": ach, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic(mv),
+                            "traffic_unit": "bytes/launch", "traffic_source": psrc, "traffic_src_hash": pstamp,
+                            "bytes_alg_per_launch": mover_alg, "avg_us": dom_us,
+                            "bytes_alg_def": "SURVEY 8(d): 4*(A_old+A_new) + 8*(n_enter+n_leave) per tick",
+                            "impl_bytes_per_launch": 16 * tot["cand"] / K + 4 * tot["events"] / K,
+                            "impl_bytes_def": "16 B per candidate pair tested + 4 B per own event (what the "
+                                              "kernel actually reads; not the roofline numerator)",
+                            "timing": "HIP events around the kernel on its stream, every timed step"}
+        kt = {}
+        for k, alg in ((mv, mover_alg), ("k_own_copy", tot["own_copy_alg"] / K),
+                       ("k_sync_write<4>", tot["sync_write_alg"] / K)):
+            tr_ = traffic(k)
+            kt[k] = {"bytes_alg": alg, "traffic": tr_, "traffic_over_alg": (tr_ / alg) if (tr_ and alg) else None}
+        line["kernels"] = kt
     if stage_us:
         stages = {n: {"avg_us": stage_us[n] / stage_n[n], "bytes_alg": stage_bytes[n] / stage_n[n]}
                   for n in stage_us}
-        # the dominant kernel: k_mover, alone in stage "diff" (16 B per candidate tested + 4 B per
-        # own event), timed by HIP events on the library's stream
-        dom = "diff"
-        ach = dom_bytes / (dom_us * 1e-6) / 1e9
-        traffic, src = pmc_traffic(STAGE_KERNEL[dom])
-        line["roofline"] = {"bound": "hbm", "kernel": STAGE_KERNEL[dom], "achieved": ach, "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
-                            "traffic_unit": "bytes/launch", "traffic_source": src,
-                            "bytes_alg_per_launch": dom_bytes, "avg_us": dom_us,
-                            "timing": "HIP events around the kernel on its stream, every timed step"}
-        line["stages"] = {n: {"avg_us": round(v["avg_us"], 2), "GBps_alg": round(
+        line["stages"] = {n: {"avg_us": round(v["avg_us"], 2), "GBps_impl": round(
             v["bytes_alg"] / max(v["avg_us"], 1e-9) / 1e3, 1)} for n, v in stages.items()}
-    else:
+    if not (stage_us or dom_us):
         line["roofline"] = None
+    if e2e:
+        line["t_e2e"] = e2e
+        line["t_device_ms_per_step"] = mx / K * 1e3
     if client:
         line["client_msgs"] = client
     if not a.no_cpu_baseline and ws == 1 and a.config == 3:
-        cb = cpu_baseline(traces.config3(ticks=1, seed=3, n=a.entities, side=a.side), a.cpu_seconds)
+        cb = cpu_baseline(traces.config3(ticks=1, seed=3, n=a.entities, side=a.side), a.cpu_st_max_seconds)
         line["cpu_baseline"] = cb
         line["cpu_baseline_mt"] = cpu_baseline_mt(a.cpu_seconds, a.entities, a.side)
     print(json.dumps(line), flush=True)

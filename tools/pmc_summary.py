@@ -32,7 +32,26 @@ def summarize(path, last=3):
     return out
 
 
+def finalize(argv):
+    """Stamp a merged pass with the kernel-source hash bench.py checks and the
+    config it was taken on: {"src_hash", "config", "kernels": {...}}."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    src = argv[argv.index("--finalize") + 1]
+    cfg = int(argv[argv.index("--config") + 1])
+    out = argv[argv.index("--out") + 1]
+    kern = json.load(open(src))
+    json.dump({"src_hash": bench.src_hash(), "config": cfg,
+               "how": "rocprofv3 --pmc, one counter group per run (tools/gpu/pmc.sh), last 3 dispatches "
+                      "averaged; hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE (KB -> B; gfx950 correction of "
+                      "MI355X_MICROARCH.md)",
+               "kernels": kern}, open(out, "w"), indent=1, sort_keys=True)
+    print("wrote", out)
+
+
 def main(argv):
+    if "--finalize" in argv:
+        return finalize(argv)
     path = argv[1]
     js = argv[argv.index("--json") + 1] if "--json" in argv else None
     out = summarize(path)

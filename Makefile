@@ -5,8 +5,9 @@ ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
 LIBDIR   := goworld_amd/lib
 CSRC     := goworld_amd/csrc
-HDR      := $(CSRC)/prim.hpp $(CSRC)/gw_internal.hpp $(CSRC)/dev_common.hpp include/gpuaoi.h
-OBJ      := $(LIBDIR)/aoi.o $(LIBDIR)/sync.o $(LIBDIR)/halo.o $(LIBDIR)/capi.o
+HDR      := $(CSRC)/prim.hpp $(CSRC)/gw_internal.hpp $(CSRC)/dev_common.hpp $(CSRC)/ctx.hpp include/gpuaoi.h
+OBJ      := $(LIBDIR)/aoi.o $(LIBDIR)/sync.o $(LIBDIR)/halo.o $(LIBDIR)/capi.o $(LIBDIR)/world.o
+ROCM     ?= /opt/rocm
 
 all: $(LIBDIR)/libgpuaoi.so oracle
 
@@ -14,12 +15,12 @@ $(LIBDIR)/%.o: $(CSRC)/%.hip $(HDR)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIBDIR)/capi.o: $(CSRC)/capi.cpp $(HDR)
+$(LIBDIR)/%.o: $(CSRC)/%.cpp $(HDR)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 $(LIBDIR)/libgpuaoi.so: $(OBJ)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
 
 oracle:
 	$(MAKE) -s -C oracle

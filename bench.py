@@ -1,25 +1,27 @@
 #!/usr/bin/env python3
-"""Benchmark of the MI355X AOI + entity-sync hot path (BASELINE.json metric).
+"""Benchmark of the MI355X AOI + entity-sync hot path (BASELINE.json metric:
+entity AOI updates/s + enter/leave events/s, 1M-entity space, 1/2/4/8 GPU).
 
 A step = one game tick of the hot path over one batch of synthetic input:
-gw_tick (apply the tick's 100k Moved ops, update every neighbour list, emit the
-canonical enter/leave streams) + gw_sync_collect (CollectEntitySyncInfos:
-per-watcher position/yaw records).  Workload at N=1 is BASELINE config #3,
-the 1M-entity clustered-hotspot single space the metric is quoted on.
+gw_tick (apply the tick's Moved ops, update every relation, emit the canonical
+enter/leave streams) + gw_sync_collect (CollectEntitySyncInfos: per-watcher
+position/yaw records).
 
-N>1, --mode world (default): one world space decomposed into N X-strips, one
-per GPU (BASELINE config #5, goworld_amd/dworld.py): each strip has config
-#3's statistics (1M entities per strip by default, --entities 2000000 gives
-config #5's 16M at N=8), and each tick every rank routes its ops, exchanges
-its halo rows with both neighbours over RCCL (xGMI) and ticks its strip.
-Weak scaling.  Bench strips reflect their walkers at the strip borders
-(migration is covered by the parity tests, tests/test_dworld.py); the halo
-traffic of the border bands is real.
-N>1, --mode spaces: an independent 1M-entity space per GPU (spaces never span
-processes in the reference, SpaceManager.go:11-31): no data-path collective.
+N=1 (default): BASELINE config #3, the 1M-entity clustered-hotspot space the
+metric is quoted on, on one GPU.
+N>1 (default --mode world): the SAME 1M-entity space decomposed into N X-strips,
+one per GPU (strong scaling; goworld_amd/dworld.py over the library's
+gw_world_* path): each tick every rank routes its owned ops, exchanges halo rows
+with both neighbours over RCCL inside the library (xGMI) and ticks its strip;
+walkers cross strip borders (migration is part of the measured tick).
+Every run also measures config #5, the north star's 16M-entity world
+decomposed over the same N GPUs, under the "config5" key (--no-config5 skips).
+--mode spaces: an independent 1M space per GPU, no comm (weak scaling).
+--config 4 / 5: BASELINE config #4 (10k spaces x 1k) / #5 as the headline.
 
 Inputs (ops of every tick) are resident in HBM before the timed region;
-outputs stay in HBM (device-resident boundary).
+outputs stay in HBM (device-resident boundary); t_e2e reports the host-in /
+host-out tick separately.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
 N>1:  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -54,19 +56,27 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="multi-threaded CPU baseline time budget")
     ap.add_argument("--cpu-st-max-seconds", type=float, default=240.0,
                     help="guard on the single-thread baseline (it replays one full tick)")
-    ap.add_argument("--e2e-steps", type=int, default=3, help="untimed end-to-end steps (host in/out)")
+    ap.add_argument("--e2e-steps", type=int, default=4, help="untimed end-to-end steps (host in/out; the first is "
+                                                                 "a warm-up)")
     ap.add_argument("--profile-stages", type=int, default=1,
                     help="1: HIP events around the dominant kernel's stage in the timed region (roofline) and "
                          "a per-stage breakdown over extra untimed steps; 0: none")
-    ap.add_argument("--mode", choices=["world", "spaces"], default="world", help="N>1 regime")
+    ap.add_argument("--mode", choices=["world", "spaces"], default="world",
+                    help="N>1 with config 3: world = the 1M space decomposed over the N GPUs (strong); spaces = an "
+                         "independent 1M space per GPU, no comm (weak)")
     ap.add_argument("--config", type=int, choices=[3, 4, 5], default=3,
-                    help="3: config #3 per GPU (weak); 4: config #4, 10k independent 1k-entity spaces, space s on "
-                         "GPU s mod N (strong); 5: the 16M uniform world of config #5 over N strips (strong)")
+                    help="3: the metric's 1M clustered space (N=1: one GPU; N>1: decomposed over the N GPUs); "
+                         "4: config #4, 10k independent 1k-entity spaces, space s on GPU s mod N (strong); "
+                         "5: the 16M uniform world of config #5 over N strips (strong)")
     ap.add_argument("--spaces", type=int, default=10_000, help="config #4: number of spaces")
-    ap.add_argument("--comm", choices=["nccl", "gloo"], default="nccl",
-                    help="halo exchange backend (gloo: rehearsal of several ranks on one GPU)")
-    ap.add_argument("--halo-cap", type=int, default=4096, help="halo entities per neighbour per tick")
-    ap.add_argument("--halo-cap-load", type=int, default=16384, help="the same, for the ticks that load the world")
+    ap.add_argument("--comm", choices=["rccl", "gloo"], default="rccl",
+                    help="halo exchange: RCCL inside the library (gw_world_step) or gloo (rehearsal of several "
+                         "ranks on one GPU)")
+    ap.add_argument("--world-entities", type=int, default=16_000_000, help="config #5 world population")
+    ap.add_argument("--no-config5", dest="config5", action="store_false",
+                    help="skip the extra config #5 (16M decomposed world) measurement")
+    ap.add_argument("--warmup5", type=int, default=5)
+    ap.add_argument("--steps5", type=int, default=10, help="config #5 timed ticks (SURVEY 8(d): 10)")
     ap.add_argument("--device", type=int, default=None, help="force a device (rehearsals on one GPU)")
     ap.add_argument("--sync-by-client", action="store_true",
                     help="collect grouped per client (GW_SYNC_BY_CLIENT, the gate's regroup on the GPU)")
@@ -78,8 +88,9 @@ def parse():
 
 
 class Ctl:
-    """Control plane (barrier, max/sum of scalars) on a gloo group; the data
-    path (halo rows) uses the default group (RCCL) in world mode."""
+    """Control plane (barrier, max/sum of scalars, the RCCL id broadcast) on a
+    gloo group; the data path (halo rows) runs inside the library over its
+    own RCCL communicator."""
 
     def __init__(self, a):
         self.ws = int(os.environ.get("WORLD_SIZE", "1"))
@@ -87,20 +98,10 @@ class Ctl:
         self.local = int(os.environ.get("LOCAL_RANK", "0")) if a.device is None else a.device
         self.group = None
         if self.ws > 1:
-            import torch
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            if a.mode == "world" and a.comm == "nccl":
-                torch.cuda.set_device(self.local)
-                dist.init_process_group("nccl", rank=self.rank, world_size=self.ws,
-                                        device_id=torch.device("cuda", self.local))
-                self.group = dist.new_group(backend="gloo")
-                t = torch.ones(1, device=torch.device("cuda", self.local))
-                dist.all_reduce(t)            # bring up the RCCL communicator on all ranks
-                torch.cuda.synchronize()
-            else:
-                dist.init_process_group("gloo", rank=self.rank, world_size=self.ws)
-                self.group = dist.group.WORLD
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.ws)
+            self.group = dist.group.WORLD
             self.dist = dist
 
     def barrier(self):
@@ -115,18 +116,27 @@ class Ctl:
         self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op), group=self.group)
         return t.tolist()
 
+    def bcast_bytes(self, b: bytes) -> bytes:
+        if self.group is None:
+            return b
+        import torch
+        t = torch.tensor(list(b), dtype=torch.uint8)
+        self.dist.broadcast(t, src=0, group=self.group)
+        return bytes(t.tolist())
+
 
 STAGE_KERNEL = {"diff": "k_mover<2, 1>"}
 PMC_DIR = os.path.join(ROOT, "profiles")
 
 
 def src_hash():
-    """Hash of the kernel sources (the PMC pass must come from this HEAD)."""
+    """Hash of the device-code sources (kernels, their launchers and device
+    headers): the PMC pass must come from these exact kernels."""
     import hashlib
     h = hashlib.sha256()
     d = os.path.join(ROOT, "goworld_amd", "csrc")
     for f in sorted(os.listdir(d)):
-        if f.endswith((".hip", ".hpp", ".cpp")):
+        if f.endswith(".hip") or f in ("dev_common.hpp", "prim.hpp", "gw_internal.hpp"):
             h.update(f.encode())
             h.update(open(os.path.join(d, f), "rb").read())
     return h.hexdigest()[:16]
@@ -340,57 +350,80 @@ class ManySpacesRun(SpaceRun):
 
 
 class WorldRun:
-    """--mode world, N>1 (or --config 5): one world of N strips (dworld.StripRank per rank)."""
+    """One world decomposed into N X-strips, one per GPU (dworld.StripRank over
+    the library's gw_world_* path; halo rows over RCCL inside the library).
+    which = "c3": the metric's 1M-entity clustered space (config #3) as one
+    world over N strips; "c5": config #5, the 16M uniform world (L = 131072).
+    Both walks are global: entities cross strip borders and migrate between
+    ranks; every rank regenerates the same walk and keeps the ops of the
+    entities it owns at the start of each tick."""
 
-    def __init__(self, a, ctl, ticks):
+    def __init__(self, a, ctl, ticks, which):
         import torch
         from goworld_amd import dworld
         self.torch = torch
         dev = torch.device("cuda", ctl.local)
         torch.cuda.set_device(dev)
         ws, r = ctl.ws, ctl.rank
-        if a.config == 5:
-            # config #5: 16M uniform, L = 131072, strips of L / N, step +-4
-            tr = traces.config5_strip(r, ws, ticks=ticks)
-            n, side, side_z, max_step = tr.n, 131072.0 / ws, 131072.0, 4.0
+        if which == "c5":
+            n, side, max_step = a.world_entities, 131072.0, 4.0
+            walk = traces.WorldWalk(seed=5, n=n, side=side)
+            x0_all, z0_all, yaw0 = walk.x(), walk.z(), walk.yaw.copy()
+            gen = (walk.next_tick() for _ in range(ticks))
         else:
-            n, side = a.entities, a.side
-            tr = traces.config3(ticks=ticks, seed=3 + r, n=n, side=side)
-            side_z, max_step = side, 16.0                       # config #3 steps: +-4, hotspots +-16
-        x0 = -ws * side / 2
-        geom = dworld.Strips(x0, side, ws, tr.d, max_step)
-        off = np.float32(x0 + (r + 0.5) * side)                 # strip r's centre (exact in f32)
+            n, side, max_step = a.entities, a.side, 16.0         # config #3 steps: +-4, hotspots +-16
+            tr = traces.config3(ticks=ticks, seed=3, n=n, side=side)
+            x0_all, z0_all, yaw0 = tr.init_x, tr.init_z, tr.init_yaw
+            xcur = tr.init_x.copy()
+
+            def gen3():
+                for ops in tr.ticks:
+                    xb = xcur[ops["slot"]].copy()
+                    xcur[ops["slot"]] = ops["x"]
+                    yield ops, xb
+            gen = gen3()
+        geom = dworld.Strips(-side / 2, side / ws, ws, 100.0, max_step)
         lo, hi = geom.ext(r)
-        bounds = (max(lo, x0), -side_z / 2, min(hi, x0 + ws * side), side_z / 2)
-        self.n_world = n * ws
-        self.g = gpuaoi.GpuAOI(ctl.local)
-        eng = dworld.HipStrip(self.g)
-        pg = None if a.comm == "nccl" else ctl.group
-        cdev = dev if a.comm == "nccl" else torch.device("cpu")
-        self.sr = sr = dworld.StripRank(eng, geom, r, n * ws, bounds, dev, pg=pg, comm_device=cdev,
-                                        halo_cap=a.halo_cap, halo_cap_max=a.halo_cap_load)
-        eng.set_clients(np.arange(n * ws, dtype=np.uint32), np.ones(n * ws, np.uint16))  # config #3: 1 gate, all clients
+        bounds = (max(lo, -side / 2), -side / 2, min(hi, side / 2), side / 2)
+        self.n_world = n
+        self.g = g = gpuaoi.GpuAOI(ctl.local)
+        eng = dworld.HipStrip(g)
+        comm = "rccl" if (ws > 1 and a.comm == "rccl") else "torch"
+        if comm == "rccl":
+            g.comm_init(ctl.bcast_bytes(gpuaoi.comm_unique_id() if r == 0 else bytes(gpuaoi.COMM_ID_BYTES)), ws, r)
+        self.sr = sr = dworld.StripRank(eng, geom, r, n, bounds, dev, pg=ctl.group, comm=comm,
+                                        comm_device=torch.device("cpu"))
+        eng.set_clients(np.arange(n, dtype=np.uint32), np.ones(n, np.uint16))   # 1 gate, every entity a client
 
         def words(ops):
-            o = ops.copy()
-            o["slot"] += np.uint32(r * n)
-            o["x"] += off
-            return torch.from_numpy(dworld.ops_to_words(o).copy()).to(dev)
-        enter = traces.enter_ops(tr.init_slots, tr.init_x, tr.init_y, tr.init_z, tr.init_yaw)
-        for i in range(0, n, 1 << 18):
-            sr.step(words(enter[i:i + (1 << 18)]), copy=False, cap=a.halo_cap_load, no_events=True)
+            return torch.from_numpy(dworld.ops_to_words(ops).copy()).to(dev)
+        # load: every rank enters the entities it owns (routed to its neighbours
+        # as ghosts), in id order, in the same number of chunks on every rank
+        owner0 = geom.owner(x0_all)
+        mine = np.nonzero(owner0 == r)[0].astype(np.uint32)
+        chunk = 1 << 21
+        n_chunks = max(1, -(-int(np.bincount(owner0, minlength=ws).max()) // chunk))
+        enter = traces.enter_ops(mine, x0_all[mine], np.zeros(len(mine), np.float32), z0_all[mine], yaw0[mine])
+        for k in range(n_chunks):
+            sr.step(words(enter[k * chunk:(k + 1) * chunk]), copy=False, no_events=True)
         sr.collect(copy=False)
-        self.m = len(tr.ticks[0])
-        self.words = [words(t) for t in tr.ticks]              # resident in HBM
+        self.words, self.m_ticks, self.slots = [], [], []
+        for ops, xb in gen:
+            own = ops[geom.owner(xb) == r]
+            self.words.append(words(own))                    # resident in HBM
+            self.m_ticks.append(len(own))
+            self.slots.append(own["slot"])
+        self.m = int(np.mean(self.m_ticks))
         torch.cuda.synchronize()
-        self.parallelism = (f"decomposed world, {ws} X-strips, halo rows over {a.comm.upper()}" if ws > 1
+        self.parallelism = (f"decomposed world, {ws} X-strips of {side / ws:g} x {side:g}, halo rows over "
+                            f"{'RCCL (gw_world_step)' if comm == 'rccl' else 'gloo'}" if ws > 1
                             else "single GPU, one-strip world")
-        self.tr = tr
+        self.tr = None
 
     def step(self, t):
         self.sr.step(self.words[t], copy=False, defer=True)
         s = self.sr.collect(copy=False)
-        return self.m, self.sr.e.tick_result(), s
+        return self.m_ticks[t], self.sr.e.tick_result(), s
 
     def close(self):
         self.sr.check()
@@ -426,179 +459,218 @@ def client_msgs(run, t0, n):
             "timing": "host wall clock around each call (one host sync inside each); not part of ms_per_step"}
 
 
-def main():
-    a = parse()
-    ctl = Ctl(a)
-    ws, rank = ctl.ws, ctl.rank
-    extra = 5 if a.profile_stages else 0         # untimed steps for the per-stage breakdown
-    cm = a.client_msgs if (ws == 1 and a.config == 3) else 0
-    world = (ws > 1 and a.mode == "world") or a.config == 5
-    n_e2e = 0 if world else a.e2e_steps
-    ticks = a.warmup + a.steps + extra + cm + n_e2e
-    t_load = time.perf_counter()
-    if a.config == 4:
-        run = ManySpacesRun(a, ctl, ticks)
-    else:
-        run = WorldRun(a, ctl, ticks) if world else SpaceRun(a, ctl, ticks)
-    t_load = time.perf_counter() - t_load
+def measure(run, a, ctl, warmup, steps, profile, extra):
+    """W untimed steps, then exactly K steps bracketed by a barrier and a device
+    sync on both sides; HIP events around the dominant kernel's stage in every
+    timed step; a per-stage breakdown over `extra` more untimed steps."""
     g = run.g
-
-    stage_us, stage_bytes, stage_n = {}, {}, {}
-
-    def acc_stages():
-        for name, us, b, calls in g.stage_times():
-            stage_us[name] = stage_us.get(name, 0.0) + us
-            stage_bytes[name] = stage_bytes.get(name, 0) + b
-            stage_n[name] = stage_n.get(name, 0) + calls
-
-    for t in range(a.warmup):
+    for t in range(warmup):
         run.step(t)
-    g.set_profiling(2 if a.profile_stages else 0)    # the dominant kernel's stage only
-    tot = dict(ops=0, events=0, records=0, bytes_alg=0, mover_alg=0, a_nbr=0, cand=0, own_copy_alg=0,
-               sync_write_alg=0)
+    g.set_profiling(2 if profile else 0)    # the dominant kernel's stage only
+    tot = dict(ops=0, events=0, records=0, bytes_alg=0, mover_alg=0, cand=0, own_copy_alg=0, sync_write_alg=0)
     ctl.barrier()
     g.synchronize()
     t0 = time.perf_counter()
-    for t in range(a.warmup, a.warmup + a.steps):
+    for t in range(warmup, warmup + steps):
         upd, r, s = run.step(t)
+        ev = r.n_enter + r.n_leave
         tot["ops"] += upd
-        tot["events"] += r.n_enter + r.n_leave
+        tot["events"] += ev
         tot["records"] += s.n_rec
         tot["bytes_alg"] += r.bytes_alg + s.bytes_alg
-        ev = r.n_enter + r.n_leave
         # SURVEY 8(d) terms per kernel: k_mover produces the neighbour-list
         # terms and the net events, 4*(A_old+A_new) + 8*E; k_own_copy reads and
         # writes the events (8*E each way); k_sync_write writes the records
         tot["mover_alg"] += 4 * (r.nbr_old + r.nbr_new) + 8 * ev
         tot["own_copy_alg"] += 16 * ev
         tot["sync_write_alg"] += 24 * s.n_rec
-        tot["a_nbr"] += r.nbr_old + r.nbr_new
         tot["cand"] += r.pairs_tested
     g.synchronize()
     t1 = time.perf_counter()
     ctl.barrier()
-    elapsed = t1 - t0
-    dom_us = dom_bytes = None
-    if a.profile_stages:
-        # HIP events recorded live around the dominant kernel in the timed region, read back here
-        for name, us, b, calls in g.stage_times():
+    res = {"elapsed": t1 - t0, "tot": tot, "dom_us": None, "stages": {}}
+    if profile:
+        for name, us, b, calls in g.stage_times():       # HIP events read back here, after the timed region
             if name == "diff":
-                dom_us, dom_bytes = us / calls, b / calls
-        # per-stage breakdown: every stage timed over a few more (untimed) steps
+                res["dom_us"] = us / calls
         g.set_profiling(1)
-        for t in range(a.warmup + a.steps, a.warmup + a.steps + extra):
+        for t in range(warmup + steps, warmup + steps + extra):
             run.step(t)
-        acc_stages()
+        acc = {}
+        for name, us, b, calls in g.stage_times():
+            v = acc.setdefault(name, [0.0, 0, 0])
+            v[0] += us; v[1] += b; v[2] += calls
+        res["stages"] = {n: {"avg_us": v[0] / v[2], "bytes_impl": v[1] / v[2]} for n, v in acc.items()}
         g.set_profiling(0)
-    client = client_msgs(run, a.warmup + a.steps + extra, cm) if cm else None
-    e2e = None
-    if n_e2e:
-        # end-to-end game ticks (host ops in, events + records out over PCIe),
-        # after the timed region; wall clock per step
-        t_e, e_ops = 0.0, 0
-        for t in range(a.warmup + a.steps + extra + cm, a.warmup + a.steps + extra + cm + n_e2e):
-            g.synchronize()
-            c0 = time.perf_counter()
-            upd, r, s_ = run.step_e2e(t)
-            t_e += time.perf_counter() - c0
-            e_ops += upd
-        e2e = {"ms_per_step": t_e / n_e2e * 1e3, "updates_per_sec": e_ops / t_e, "steps": n_e2e,
-               "what": "gw_submit(host ops) + gw_tick(COPY_TO_HOST) + gw_sync_collect(COPY_TO_HOST): the Go "
-                       "caller's tick, events and compact records copied to pinned host memory (PCIe); "
-                       "wall clock, untimed by the headline"}
-    mx = ctl.reduce([elapsed], "MAX")[0]
+    mx = ctl.reduce([res["elapsed"]], "MAX")[0]
     sums = ctl.reduce([tot["ops"], tot["events"], tot["records"]], "SUM")
-    if rank != 0:
-        run.close()
-        return
-    K = a.steps
-    if a.config == 4:
-        workload = (f"config #4: {a.spaces} independent AOI spaces x 1000 entities (uniform, L = 1024, AOI "
-                    f"distance 100), 10% movers per space per tick (step +-4), space s on GPU s mod {ws}, every "
-                    f"space of a GPU in one tick; step = gw_tick + gw_sync_collect")
-    elif a.config == 5:
-        workload = (f"config #5: one 16M-entity uniform world space, L = 131072, AOI distance 100, 10% movers "
-                    f"per tick (step +-4), decomposed into {ws} X-strip(s) of {131072 // ws} x 131072 (walkers "
-                    f"reflect at strip borders); step = route + halo exchange + gw_tick + gw_sync_collect")
-    elif world:
-        workload = (f"config #5 shape: one world space of {ws} x {a.entities} entities decomposed into {ws} "
-                    f"X-strips of {a.side:g} x {a.side:g}, each with config #3 statistics (70% uniform + 30% in "
-                    f"64 Gaussian hotspots, 10% movers per tick), AOI distance 100; step = route + halo "
-                    f"exchange + gw_tick + gw_sync_collect on every rank")
-    else:
-        workload = ("config #3: single AOI space per GPU, 1M entities, 70% uniform + 30% in 64 "
-                    "Gaussian hotspots (sigma 200), 10% movers per tick (+-4 / hotspot +-16), "
-                    "AOI distance 100, world 32768^2; step = gw_tick + gw_sync_collect")
-    line = {
-        "metric": "entity AOI updates/sec + enter/leave events/sec, 1M-entity space, 1/2/4/8 GPU",
-        "value": sums[0] / mx,
-        "unit": "updates/s",
-        "n_gpus": ws,
-        "steps": K,
-        "warmup": a.warmup,
-        "ms_per_step": mx / K * 1e3,
-        "higher_is_better": True,
-        "scaling": "strong" if a.config in (4, 5) else "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": (f"synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #{a.config})" if a.config in (4, 5) else
-                 "synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #3" + (" per strip)" if world else ")")),
-        "config": {"workload": workload,
-                   "entities_per_gpu": run.n_world // ws, "world_entities": run.n_world,
-                   "movers_per_tick_per_gpu": run.m, "aoi_dist": 100.0,
-                   "world_side": {4: 1024.0, 5: 131072.0}.get(a.config, a.side), "gates": 1,
-                   "parallelism": run.parallelism},
-        "events_per_sec": sums[1] / mx,
-        "records_per_sec": sums[2] / mx,
-        "device_us_per_step": (sum(stage_us.values()) / extra) if stage_us else None,
-        "bytes_alg_per_step": tot["bytes_alg"] / K,
-        "tick_hbm_frac": (tot["bytes_alg"] / K) / (mx / K) / (HBM_PEAK_GBS * 1e9),
-        "load_s": t_load,
-    }
-    if stage_us or dom_us:
-        # the dominant kernel: k_mover, alone in stage "diff", timed live by HIP
-        # events on the library's stream in every timed step.  achieved = its
-        # SURVEY 8(d) bytes per launch (4*(A_old+A_new) + 8*E: the neighbour-list
-        # and event terms it produces; A and E from gw_tick_out) / that duration
+    res.update(max_elapsed=mx, sum_ops=sums[0], sum_events=sums[1], sum_records=sums[2])
+    return res
+
+
+def roofline_fields(res, K, config, ws):
+    """The dominant kernel (k_mover, alone in stage "diff", timed live by HIP
+    events on the library's stream in every timed step): achieved = its SURVEY
+    8(d) bytes per launch (4*(A_old+A_new) + 8*E, the neighbour-list and event
+    terms it produces, from gw_tick_out) / that duration."""
+    tot, dom_us = res["tot"], res["dom_us"]
+    out = {}
+    if dom_us:
         mover_alg = tot["mover_alg"] / K
         ach = mover_alg / (dom_us * 1e-6) / 1e9
-        kern, psrc, pstamp = pmc_traffic(a.config if a.config != 5 or ws == 1 else None)
+        kern, psrc, pstamp = pmc_traffic(config) if ws == 1 else (None, None, "n/a (N>1)")
+
         def traffic(k):
             return (kern or {}).get(k, {}).get("hbm_bytes") if kern else None
         mv = STAGE_KERNEL["diff"]
-        line["roofline"] = {"bound": "hbm", "kernel": mv, "achieved": ach, "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic(mv),
-                            "traffic_unit": "bytes/launch", "traffic_source": psrc, "traffic_src_hash": pstamp,
-                            "bytes_alg_per_launch": mover_alg, "avg_us": dom_us,
-                            "bytes_alg_def": "SURVEY 8(d): 4*(A_old+A_new) + 8*(n_enter+n_leave) per tick",
-                            "impl_bytes_per_launch": 16 * tot["cand"] / K + 4 * tot["events"] / K,
-                            "impl_bytes_def": "16 B per candidate pair tested + 4 B per own event (what the "
-                                              "kernel actually reads; not the roofline numerator)",
-                            "timing": "HIP events around the kernel on its stream, every timed step"}
+        out["roofline"] = {"bound": "hbm", "kernel": mv, "achieved": ach, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic(mv),
+                           "traffic_unit": "bytes/launch", "traffic_source": psrc, "traffic_src_hash": pstamp,
+                           "bytes_alg_per_launch": mover_alg, "avg_us": dom_us,
+                           "bytes_alg_def": "SURVEY 8(d): 4*(A_old+A_new) + 8*(n_enter+n_leave) per tick",
+                           "impl_bytes_per_launch": 16 * tot["cand"] / K + 4 * tot["events"] / K,
+                           "impl_bytes_def": "16 B per candidate pair tested + 4 B per own event (what the "
+                                             "kernel reads; not the roofline numerator)",
+                           "timing": "HIP events around the kernel on its stream, every timed step"}
         kt = {}
         for k, alg in ((mv, mover_alg), ("k_own_copy", tot["own_copy_alg"] / K),
                        ("k_sync_write<4>", tot["sync_write_alg"] / K)):
             tr_ = traffic(k)
             kt[k] = {"bytes_alg": alg, "traffic": tr_, "traffic_over_alg": (tr_ / alg) if (tr_ and alg) else None}
-        line["kernels"] = kt
-    if stage_us:
-        stages = {n: {"avg_us": stage_us[n] / stage_n[n], "bytes_alg": stage_bytes[n] / stage_n[n]}
-                  for n in stage_us}
-        line["stages"] = {n: {"avg_us": round(v["avg_us"], 2), "GBps_impl": round(
-            v["bytes_alg"] / max(v["avg_us"], 1e-9) / 1e3, 1)} for n, v in stages.items()}
-    if not (stage_us or dom_us):
-        line["roofline"] = None
+        out["kernels"] = kt
+    else:
+        out["roofline"] = None
+    if res["stages"]:
+        out["stages"] = {n: {"avg_us": round(v["avg_us"], 2),
+                             "GBps_impl": round(v["bytes_impl"] / max(v["avg_us"], 1e-9) / 1e3, 1)}
+                         for n, v in res["stages"].items()}
+    return out
+
+
+def main():
+    a = parse()
+    ctl = Ctl(a)
+    ws, rank = ctl.ws, ctl.rank
+    extra = 5 if a.profile_stages else 0         # untimed steps for the per-stage breakdown
+    if a.config == 4:
+        kind = "c4"
+    elif a.config == 5:
+        kind = "c5"
+    elif ws > 1 and a.mode == "world":
+        kind = "c3world"                            # the metric's 1M space decomposed over the N GPUs
+    else:
+        kind = "c3"                                 # N=1: the 1M space on one GPU (a one-strip world)
+    cm = a.client_msgs if (ws == 1 and kind == "c3") else 0
+    n_e2e = a.e2e_steps if kind in ("c3", "c4") else 0
+    W, K = a.warmup, a.steps
+    ticks = W + K + extra + cm + n_e2e
+    t_load = time.perf_counter()
+    if kind == "c4":
+        run = ManySpacesRun(a, ctl, ticks)
+    elif kind == "c5":
+        run = WorldRun(a, ctl, ticks, "c5")
+    elif kind == "c3world":
+        run = WorldRun(a, ctl, ticks, "c3")
+    else:
+        run = SpaceRun(a, ctl, ticks)
+    t_load = time.perf_counter() - t_load
+    g = run.g
+    res = measure(run, a, ctl, W, K, a.profile_stages, extra)
+    client = client_msgs(run, W + K + extra, cm) if cm else None
+    e2e = None
+    if n_e2e >= 2:
+        # end-to-end game ticks (host ops in, events + records out over PCIe),
+        # after the timed region; wall clock per step (the first one, which
+        # allocates the pinned host buffers, untimed)
+        t_e, e_ops = 0.0, 0
+        t_first = W + K + extra + cm
+        run.step_e2e(t_first)
+        for t in range(t_first + 1, t_first + n_e2e):
+            g.synchronize()
+            c0 = time.perf_counter()
+            upd, r, s_ = run.step_e2e(t)
+            t_e += time.perf_counter() - c0
+            e_ops += upd
+        e2e = {"ms_per_step": t_e / (n_e2e - 1) * 1e3, "updates_per_sec": e_ops / t_e, "steps": n_e2e - 1,
+               "what": "gw_submit(host ops) + gw_tick(COPY_TO_HOST) + gw_sync_collect(COPY_TO_HOST): the Go "
+                       "caller's tick, events and compact records copied to pinned host memory (PCIe); "
+                       "wall clock, untimed by the headline"}
+    parallelism, n_world, m_rank = run.parallelism, run.n_world, run.m
+    run.close()
+    # the north star's 16M decomposed world (config #5) at the same N, strong scaling
+    c5 = None
+    if a.config5 and kind in ("c3", "c3world"):
+        run5 = WorldRun(a, ctl, a.warmup5 + a.steps5 + (extra if a.profile_stages else 0), "c5")
+        r5 = measure(run5, a, ctl, a.warmup5, a.steps5, a.profile_stages, extra)
+        c5 = {"workload": "config #5: one 16M-entity uniform world space, L = 131072, AOI distance 100, 10% movers "
+                          f"per tick (+-4; walkers cross strip borders), decomposed into {ws} X-strip(s); step = "
+                          "route + RCCL halo exchange + gw_tick + gw_sync_collect on every rank",
+              "value": r5["sum_ops"] / r5["max_elapsed"], "unit": "updates/s",
+              "events_per_sec": r5["sum_events"] / r5["max_elapsed"],
+              "records_per_sec": r5["sum_records"] / r5["max_elapsed"],
+              "ms_per_step": r5["max_elapsed"] / a.steps5 * 1e3, "steps": a.steps5, "warmup": a.warmup5,
+              "scaling": "strong", "n_gpus": ws, "parallelism": run5.parallelism,
+              "roofline_frac": (roofline_fields(r5, a.steps5, 5, ws).get("roofline") or {}).get("frac")}
+        run5.close()
+    if rank != 0:
+        return
+    mx = res["max_elapsed"]
+    if kind == "c4":
+        workload = (f"config #4: {a.spaces} independent AOI spaces x 1000 entities (uniform, L = 1024, AOI "
+                    f"distance 100), 10% movers per space per tick (step +-4), space s on GPU s mod {ws}, every "
+                    f"space of a GPU in one tick; step = gw_tick + gw_sync_collect")
+    elif kind == "c5":
+        workload = c5 and c5["workload"] or (
+            f"config #5: one 16M-entity uniform world space, L = 131072, AOI distance 100, 10% movers per tick "
+            f"(+-4; walkers cross strip borders), decomposed into {ws} X-strip(s); step = route + RCCL halo "
+            f"exchange + gw_tick + gw_sync_collect on every rank")
+    elif kind == "c3world":
+        workload = (f"config #3 as one world: the 1M-entity clustered space (70% uniform + 30% in 64 Gaussian "
+                    f"hotspots, sigma 200; 10% movers per tick, +-4 / hotspot +-16; AOI distance 100; world "
+                    f"32768^2) decomposed into {ws} X-strips of {a.side / ws:g}, one per GPU (walkers cross "
+                    f"strip borders); step = route + RCCL halo exchange + gw_tick + gw_sync_collect")
+    else:
+        workload = ("config #3: single AOI space per GPU, 1M entities, 70% uniform + 30% in 64 "
+                    "Gaussian hotspots (sigma 200), 10% movers per tick (+-4 / hotspot +-16), "
+                    "AOI distance 100, world 32768^2; step = gw_tick + gw_sync_collect")
+    cfg_no = {"c3": 3, "c3world": 3, "c4": 4, "c5": 5}[kind]
+    line = {
+        "metric": "entity AOI updates/sec + enter/leave events/sec, 1M-entity space, 1/2/4/8 GPU",
+        "value": res["sum_ops"] / mx,
+        "unit": "updates/s",
+        "n_gpus": ws,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": mx / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak" if (ws > 1 and kind == "c3") else "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #{cfg_no})",
+        "config": {"workload": workload, "world_entities": n_world, "entities_per_gpu": n_world // ws,
+                   "movers_per_tick_per_gpu": m_rank, "aoi_dist": 100.0,
+                   "world_side": {4: 1024.0, 5: 131072.0}.get(cfg_no, a.side), "gates": 1,
+                   "parallelism": parallelism},
+        "events_per_sec": res["sum_events"] / mx,
+        "records_per_sec": res["sum_records"] / mx,
+        "device_us_per_step": (sum(v["avg_us"] for v in res["stages"].values())) if res["stages"] else None,
+        "bytes_alg_per_step": res["tot"]["bytes_alg"] / K,
+        "step_hbm_frac": (res["tot"]["bytes_alg"] / K) / (mx / K) / (HBM_PEAK_GBS * 1e9),
+        "load_s": t_load,
+    }
+    line.update(roofline_fields(res, K, cfg_no, ws))
     if e2e:
         line["t_e2e"] = e2e
         line["t_device_ms_per_step"] = mx / K * 1e3
     if client:
         line["client_msgs"] = client
-    if not a.no_cpu_baseline and ws == 1 and a.config == 3:
+    if c5:
+        line["config5"] = c5
+    if not a.no_cpu_baseline and ws == 1 and kind == "c3":
         cb = cpu_baseline(traces.config3(ticks=1, seed=3, n=a.entities, side=a.side), a.cpu_st_max_seconds)
         line["cpu_baseline"] = cb
         line["cpu_baseline_mt"] = cpu_baseline_mt(a.cpu_seconds, a.entities, a.side)
     print(json.dumps(line), flush=True)
-    run.close()
 
 
 if __name__ == "__main__":

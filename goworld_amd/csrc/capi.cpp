@@ -21,140 +21,15 @@
 #include <string>
 #include <vector>
 
-#include "gw_internal.hpp"
+#include "ctx.hpp"
 
 using namespace gw;
+using namespace gw::host;
 
-namespace {
 
-struct DevBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-};
 
-struct SpaceHost {
-    float d;
-    uint32_t cap, base;
-    SpaceP p;
-    bool alive;
-};
-
-struct OpSeg {            // submission order of a tick: host or device segment
-    bool host;
-    const gw_op* dev;
-    const uint64_t* stamps;   // explicit global stamps (device) or nullptr
-    uint32_t n;
-    size_t host_off;
-    const gw_halo_row* rows;  // halo rows (device): ops with inline stamps
-};
-
-struct Stage {
-    const char* name;
-    hipEvent_t a, b;
-    uint64_t bytes;
-};
-
-}  // namespace
-
-struct gw_ctx {
-    int dev = 0;
-    hipStream_t st = nullptr;
-    hipStream_t own_st = nullptr;   // the context's own stream (st may be a caller's)
-    std::string err;
-
-    std::vector<SpaceHost> spaces;
-    uint32_t total_slots = 0, slot_cap = 0, total_cells = 0;
-    uint16_t max_gate = 0;
-    unsigned long long stamp_base = 1;   // global op counter (stamp 0 = never)
-    uint32_t epoch = 1;                  // bumped by every tick and client change (World.nbc)
-    int cells_per_d = 2;                 // grid cells per AOI distance (GW_CELLS_PER_D)
-    int diff_u = 1, nb_u = 4;            // k_mover waves per block (GW_MOVER_WPB), sync chunks in flight (GW_NB_U)
-    bool grid_dirty = true;              // gn/gn_start must be rebuilt before queries
-    uint64_t h_present = 0;
-    uint64_t own_cap = 0;                // capacity of the own-event regions (grows on overflow)
-    bool cells_zero = false;             // dep / arr / gm_cnt hold zeros
-
-    // persistent device state (slot-indexed)
-    AoiEnt* aoi = nullptr;
-    PrevEnt* prev = nullptr;
-    unsigned long long* stamp = nullptr;
-    float4* pos = nullptr;
-    uint32_t* flags = nullptr;
-    uint16_t* gate = nullptr;
-    unsigned long long* cnt64 = nullptr;     // [slot_cap + 1], zero between ticks
-    unsigned long long* nbc = nullptr;       // [slot_cap] epoch<<32 | neighbours with a client
-    uint32_t* ownbits = nullptr;             // [slot_cap/32 + 1] zero between ticks
-    int32_t *last_pos = nullptr, *last_aoi = nullptr, *last_leave = nullptr;
-    int32_t* clr = nullptr;                   // [2 slot_cap] last Leave clearing each sync bit, -1 between ticks
-    uint32_t* rflag = nullptr;                // [slot_cap] halo routing scratch, zero between calls
-    HaloStats* halo = nullptr;                // halo routing counters (device)
-    GEnt* gnb[2] = {nullptr, nullptr};   // grid ping-pong (gnb[gcur] is current)
-    uint32_t* gsb[2] = {nullptr, nullptr};  // cell starts ping-pong
-    int gcur = 0;
-    uint32_t cells_cap = 0;              // words in each per-cell array
-    uint32_t *dep = nullptr, *arr = nullptr, *gm_cnt = nullptr, *cnt_new = nullptr, *dirty = nullptr,
-             *bigcell = nullptr, *gm_start = nullptr;
-    uint32_t* gidx = nullptr;
-    SpaceP* sp_dev = nullptr;
-    uint32_t sp_cap = 0;
-
-    DevStats* stats = nullptr;     // device (grid rebuild, tick)
-    DevStats* hstats = nullptr;    // pinned host
-    DevStats* cstats = nullptr;    // device (collect: a deferred tick's stats stay intact)
-    DevStats* hcstats = nullptr;   // pinned host
-
-    // a tick launched but not read back yet (GW_TICK_DEFER): settled by the
-    // next call that needs its results (the collect's one sync covers it)
-    struct Pending {
-        bool on = false, copied = false;
-        uint32_t M = 0, C = 0, NC = 0, flags = 0;
-        size_t s_grid = 0, s_movers = 0, s_diff = 0, s_events = 0;
-        TickBufs b{};
-    } pt;
-    gw_tick_out last_out{};
-
-    // grid + tick scratch
-    DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, cand, reg, own, big, bigseg, mstat;
-    DevBuf mir, mir_cnt;
-    DevBuf off64, enter_d, leave_d, scan_status, rs_hist;
-    ScanCtx sc{};                  // single-pass scan state (prim.hpp)
-    // sync / query scratch
-    DevBuf fbits, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
-    DevBuf cl_slot, cl_off, h_cl_slot, h_cl_off;   // GW_SYNC_BY_CLIENT segments (device / pinned host)
-    uint64_t rec_cap = 0;                // records the rec0 buffer holds (grows on overflow)
-    // client messages (gw_client_events, gw_fanout): ping-pong + pinned host + gate offsets
-    struct MsgBufs {
-        DevBuf a, b, h;
-        std::vector<uint64_t> goff;
-    } m_create, m_destroy, m_fanout;
-    DevBuf m_flag, m_at, m_items, m_cnt, m_off;
-    uint32_t* scal32 = nullptr;    // small device scalars
-
-    // host mirror for validation of host-submitted ops
-    std::vector<uint8_t> present_h;
-    std::vector<int32_t> space_of_h;   // slot -> space id (-1 none)
-    bool validate = true;
-
-    // pending ops
-    std::vector<gw_op> pend_host;
-    std::vector<OpSeg> segs;
-
-    // outputs
-    DevBuf h_enter, h_leave, h_rec;   // pinned host
-    std::vector<uint64_t> gate_off;
-
-    // profiling
-    int prof = 0;                      // 0 off, 1 every stage, 2 the "diff" stage only
-    bool prof_cur = false;             // the stage being recorded is on
-    std::vector<Stage> stages;
-    size_t nstage = 0;
-    hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
-    gw_stage_times last_times{};
-};
-
-static int settle(gw_ctx* c);   // finish a deferred tick (GW_TICK_DEFER)
-
-namespace {
+namespace gw {
+namespace host {
 
 int set_err(gw_ctx* c, int code, const char* fmt, ...) {
     char buf[512];
@@ -166,13 +41,6 @@ int set_err(gw_ctx* c, int code, const char* fmt, ...) {
     return code;
 }
 
-#define HIPCHK(expr)                                                                             \
-    do {                                                                                         \
-        hipError_t _e = (expr);                                                                  \
-        if (_e != hipSuccess)                                                                    \
-            return set_err(c, GW_EDEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
-                           __FILE__, __LINE__);                                                  \
-    } while (0)
 
 // (re)allocate scratch without preserving contents; callers only grow buffers
 // at points where the stream is idle (after a host sync)
@@ -212,6 +80,11 @@ int ensure_host(gw_ctx* c, DevBuf& b, size_t bytes) {
     return 0;
 }
 
+}  // namespace host
+}  // namespace gw
+
+namespace {
+
 template <typename T>
 int grow_preserve(gw_ctx* c, T*& p, size_t old_n, size_t new_n) {
     T* q = nullptr;
@@ -228,8 +101,6 @@ int grow_preserve(gw_ctx* c, T*& p, size_t old_n, size_t new_n) {
     return 0;
 }
 
-template <typename T>
-T* P(DevBuf& b) { return (T*)b.p; }
 
 int ceil_log2(uint64_t v) {   // bits needed to represent values in [0, v)
     int b = 1;
@@ -421,6 +292,12 @@ World world(gw_ctx* c) {
     return w;
 }
 
+}  // namespace
+
+World gw::host::world_of(gw_ctx* c) { return world(c); }
+
+namespace {
+
 // per-cell arrays for total_cells (+2); dep / arr / gm_cnt must hold zeros
 // between ticks (their counters return to zero inside a tick)
 int ensure_cells(gw_ctx* c) {
@@ -576,6 +453,9 @@ void gw_shutdown(gw_ctx* c) {
                       &c->m_create.a, &c->m_create.b, &c->m_destroy.a, &c->m_destroy.b, &c->m_fanout.a,
                       &c->m_fanout.b, &c->m_flag, &c->m_at, &c->m_items, &c->m_cnt, &c->m_off};
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
+    DevBuf* wb[] = {&c->wd.stamps, &c->wd.send[0], &c->wd.send[1], &c->wd.recv[0], &c->wd.recv[1], &c->wd.cnt};
+    for (DevBuf* b : wb) if (b->p) (void)hipFree(b->p);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off, &c->m_create.h,
                     &c->m_destroy.h, &c->m_fanout.h};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
@@ -928,7 +808,15 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     return 0;
 }
 
-static int settle(gw_ctx* c) { return finish_tick(c, nullptr); }
+}  // extern "C"
+
+namespace gw {
+namespace host {
+int settle(gw_ctx* c) { return finish_tick(c, nullptr); }
+}  // namespace host
+}  // namespace gw
+
+extern "C" {
 
 
 

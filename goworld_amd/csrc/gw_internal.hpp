@@ -234,7 +234,9 @@ struct HaloDsts {
 };
 void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
                        float max_step, const HaloDsts& D, int32_t* last_pos, int32_t* last_aoi,
-                       int32_t* last_leave, int32_t* clr, uint32_t* rflag, HaloStats* hs, hipStream_t s);
+                       int32_t* last_leave, int32_t* clr, uint32_t* rflag, HaloStats* hs, hipStream_t s,
+                       bool pad = true);
+void launch_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n, hipStream_t s);
 void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,
                        hipStream_t s);
 void launch_watcher_keys(const gw_sync_record* rec, uint64_t n, uint32_t* keys, uint32_t* vals, hipStream_t s);

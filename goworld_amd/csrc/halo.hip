@@ -193,16 +193,26 @@ __global__ void __launch_bounds__(NT) k_split_rows(const gw_halo_row* __restrict
 
 void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
                        float max_step, const HaloDsts& D, int32_t* last_pos, int32_t* last_aoi,
-                       int32_t* last_leave, int32_t* clr, uint32_t* rflag, HaloStats* hs, hipStream_t s) {
+                       int32_t* last_leave, int32_t* clr, uint32_t* rflag, HaloStats* hs, hipStream_t s,
+                       bool pad) {
     const uint32_t nb = nblk1(n, NT);
-    uint64_t rows = 0;
-    for (uint32_t d = 0; d < D.n; ++d) rows = std::max<uint64_t>(rows, (uint64_t)D.d[d].cap * ROWS);
+    uint64_t rows = 0;                                   // NOP padding up to the capacity (fixed-size exchanges)
+    if (pad)
+        for (uint32_t d = 0; d < D.n; ++d) rows = std::max<uint64_t>(rows, (uint64_t)D.d[d].cap * ROWS);
     hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, last_pos, last_aoi, last_leave, clr, hs);
     hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, clr, rflag);
     hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, last_pos, last_aoi, last_leave,
                        clr, rflag, max_step, D, hs);
     hipLaunchKernelGGL(k_route4, dim3(nblk1(std::max<uint64_t>(n, rows), NT)), dim3(NT), 0, s, ops, n, w.cap,
                        last_pos, last_aoi, last_leave, clr, rflag, D, hs);
+}
+
+__global__ void __launch_bounds__(NT) k_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i < n) p[i] = base + i;
+}
+void launch_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_iota_u64, dim3(nblk(n, NT)), dim3(NT), 0, s, p, base, n);
 }
 
 void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,

@@ -1,0 +1,293 @@
+// world.cpp — RCCL communicator of a context and the decomposed world
+// (include/gpuaoi.h gw_comm_* / gw_world_*).
+//
+// The reference keeps a space inside one game process (engine/entity/
+// SpaceManager.go:11-31); splitting one huge space into X-strips over GPUs is
+// new capability.  go-aoi's relation is a pure function of the two positions
+// and of which member made the later AOI call, so a strip needs no neighbour
+// lists from its neighbours, only the state of the entities near its borders:
+// the owner of an entity forwards the net effect of its ops of the tick as
+// halo rows (gw_route_halo, halo.hip) and every rank orders all ops by global
+// stamps.  Per tick on every rank, all on the context's stream:
+//   stamps (iota) -> route into send buffers sized for the worst case (n
+//   entities per side, so they cannot overflow) -> RCCL exchange of the two
+//   row counts -> one host sync -> RCCL exchange of exactly the used rows ->
+//   the tick's op stream = owned ops (stamped) + both neighbours' rows.
+// Point-to-point with <= 2 peers per rank (one xGMI link each); the volumes are
+// small (a few thousand entities x 96 B per border), so the exact-size second
+// round costs a host round trip but never sends padding.
+#include <cmath>
+#include <cstring>
+
+#include "ctx.hpp"
+
+using namespace gw;
+using namespace gw::host;
+
+namespace {
+
+constexpr uint64_t STAMP_STRIDE = 1ull << 26;   // stamp = 1 + (tick * ranks + rank) * 2^26 + op index
+constexpr uint32_t ROWS = 3;                    // rows per routed entity (gw_route_halo)
+
+#define NCCLCHK(expr)                                                                            \
+    do {                                                                                         \
+        ncclResult_t _r = (expr);                                                                \
+        if (_r != ncclSuccess)                                                                   \
+            return set_err(c, GW_EDEVICE, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(_r), \
+                           __FILE__, __LINE__);                                                  \
+    } while (0)
+
+// dworld.Strips geometry, in double like the Python statement, rounded to float32 where the device compares
+double strip_lo(const gw_world_geom& g, int r) { return r == 0 ? -INFINITY : (double)g.x0 + r * (double)g.strip_w; }
+double strip_hi(const gw_world_geom& g, int r) {
+    return r == (int)g.ranks - 1 ? INFINITY : (double)g.x0 + (r + 1) * (double)g.strip_w;
+}
+// smallest float32 >= v (x >= lo <=> x >= that float32 for float32 x); +-3e38 for the open ends
+float f32_ceil(double v, int side) {
+    if (!std::isfinite(v)) return side < 0 ? -3.0e38f : 3.0e38f;
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafterf(f, INFINITY);
+    return f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gw_comm_unique_id(void* id) {
+    if (!id) return GW_EINVAL;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return GW_EDEVICE;
+    memcpy(id, &u, sizeof u);
+    return 0;
+}
+
+int gw_comm_init(gw_ctx* c, const void* id, int nranks, int rank) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return GW_EINVAL;
+    if (c->comm) return set_err(c, GW_ESTATE, "communicator already initialised");
+    if (int rs = settle(c)) return rs;
+    (void)hipSetDevice(c->dev);
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    NCCLCHK(ncclCommInitRank(&c->comm, nranks, u, rank));
+    c->c_nranks = nranks;
+    c->c_rank = rank;
+    return 0;
+}
+
+int gw_comm_info(gw_ctx* c, int* nranks, int* rank) {
+    if (!c) return GW_EINVAL;
+    if (nranks) *nranks = c->comm ? c->c_nranks : 0;
+    if (rank) *rank = c->comm ? c->c_rank : 0;
+    return 0;
+}
+
+int gw_comm_exchange(gw_ctx* c, const gw_xfer* x, uint32_t n) {
+    if (!c || (n && !x)) return GW_EINVAL;
+    if (!c->comm) return set_err(c, GW_ESTATE, "no communicator (gw_comm_init)");
+    for (uint32_t i = 0; i < n; ++i)
+        if (x[i].peer < 0 || x[i].peer >= c->c_nranks || (x[i].send_bytes && !x[i].send) ||
+            (x[i].recv_bytes && !x[i].recv))
+            return set_err(c, GW_EINVAL, "bad transfer %u", i);
+    (void)hipSetDevice(c->dev);
+    NCCLCHK(ncclGroupStart());
+    for (uint32_t i = 0; i < n; ++i) {
+        if (x[i].send_bytes) {
+            ncclResult_t r = ncclSend(x[i].send, x[i].send_bytes, ncclUint8, x[i].peer, c->comm, c->st);
+            if (r != ncclSuccess) { (void)ncclGroupEnd(); NCCLCHK(r); }
+        }
+        if (x[i].recv_bytes) {
+            ncclResult_t r = ncclRecv(x[i].recv, x[i].recv_bytes, ncclUint8, x[i].peer, c->comm, c->st);
+            if (r != ncclSuccess) { (void)ncclGroupEnd(); NCCLCHK(r); }
+        }
+    }
+    NCCLCHK(ncclGroupEnd());
+    return 0;
+}
+
+int gw_comm_allreduce_u64(gw_ctx* c, uint64_t* dev, uint32_t n, int op) {
+    if (!c || (n && !dev) || (op != GW_RED_SUM && op != GW_RED_MAX)) return GW_EINVAL;
+    if (!c->comm) return set_err(c, GW_ESTATE, "no communicator (gw_comm_init)");
+    if (!n) return 0;
+    (void)hipSetDevice(c->dev);
+    NCCLCHK(ncclAllReduce(dev, dev, n, ncclUint64, op == GW_RED_SUM ? ncclSum : ncclMax, c->comm, c->st));
+    return 0;
+}
+
+int gw_world_create(gw_ctx* c, const gw_world_geom* g, uint32_t capacity, const float* bounds, uint32_t* space_id) {
+    if (!c || !g) return GW_EINVAL;
+    if (c->wd.on) return set_err(c, GW_ESTATE, "the context already holds a world strip");
+    if (g->ranks < 1 || g->rank >= g->ranks || !(g->strip_w > 0) || !(g->aoi_dist > 0) || !(g->max_step >= 0) ||
+        !std::isfinite(g->x0))
+        return set_err(c, GW_EINVAL, "bad world geometry");
+    WorldHost& W = c->wd;
+    W.g = *g;
+    W.h = (double)g->aoi_dist + 2.0 * g->max_step + 1.0 +
+          1e-5 * (std::fabs((double)g->x0) + g->ranks * (double)g->strip_w);
+    if (g->ranks > 2 && !(g->strip_w > W.h + g->max_step))
+        return set_err(c, GW_EINVAL, "strip width %g must exceed halo %g + max_step %g", g->strip_w, W.h,
+                       g->max_step);
+    uint32_t sid = 0, base = 0;
+    if (int rc = gw_space_create(c, g->aoi_dist, capacity, bounds, &sid, &base)) return rc;
+    if (base != 0) return set_err(c, GW_ESTATE, "a world strip must be the context's first space (slot = id)");
+    const int r = (int)g->rank;
+    if (int rc = gw_space_set_ownership(c, sid, f32_ceil(strip_lo(*g, r), -1), f32_ceil(strip_hi(*g, r), 1)))
+        return rc;
+    for (int side = 0; side < 2; ++side) {
+        const int nb = side == 0 ? r - 1 : r + 1;
+        W.nb[side] = (nb >= 0 && nb < (int)g->ranks) ? nb : -1;
+        if (W.nb[side] >= 0) {
+            W.ext_lo[side] = (float)(strip_lo(*g, nb) - W.h);
+            W.ext_hi[side] = (float)(strip_hi(*g, nb) + W.h);
+        }
+    }
+    W.sid = sid;
+    W.tick = 0;
+    W.on = true;
+    if (space_id) *space_id = sid;
+    return 0;
+}
+
+int gw_world_route(gw_ctx* c, const gw_op* ops, uint32_t n, const gw_halo_row* send[2], uint32_t send_rows[2]) {
+    if (!c || (n && !ops)) return GW_EINVAL;
+    WorldHost& W = c->wd;
+    if (!W.on) return set_err(c, GW_ESTATE, "no world strip (gw_world_create)");
+    if (W.routed) return set_err(c, GW_ESTATE, "tick already routed: gw_world_submit first");
+    if ((uint64_t)n >= STAMP_STRIDE) return set_err(c, GW_ERANGE, "too many ops in one tick for the stamp layout");
+    if (int rs = settle(c)) return rs;
+    (void)hipSetDevice(c->dev);
+    int rc;
+    const uint64_t cap_ent = std::max<uint64_t>(n, 1);   // an entity is routed at most once per side
+    if ((rc = ensure(c, W.stamps, (size_t)cap_ent * 8)) || (rc = ensure(c, W.cnt, 64))) return rc;
+    HaloDsts D{};
+    for (int side = 0; side < 2; ++side) {
+        if (W.nb[side] < 0) continue;
+        if ((rc = ensure(c, W.send[side], (size_t)cap_ent * ROWS * sizeof(gw_halo_row)))) return rc;
+        D.d[D.n++] = HaloDst{W.ext_lo[side], W.ext_hi[side], P<gw_halo_row>(W.send[side]), (uint32_t)cap_ent};
+    }
+    const unsigned long long base = 1 + (W.tick * W.g.ranks + W.g.rank) * STAMP_STRIDE;
+    launch_iota_u64(P<unsigned long long>(W.stamps), base, n, c->st);
+    launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->last_pos,
+                      c->last_aoi, c->last_leave, c->clr, c->rflag, c->halo, c->st, /*pad=*/false);
+    HIPCHK(hipGetLastError());
+    HaloStats hs{};
+    HIPCHK(hipMemcpyAsync(&hs, c->halo, sizeof hs, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    uint32_t k = 0;
+    for (int side = 0; side < 2; ++side) {
+        W.send_cnt[side] = 0;
+        if (W.nb[side] < 0) continue;
+        W.send_cnt[side] = std::min<uint32_t>(hs.cnt[k++], (uint32_t)cap_ent);
+    }
+    W.ops = ops;
+    W.n_ops = n;
+    W.routed = true;
+    for (int side = 0; side < 2; ++side) {
+        if (send) send[side] = W.nb[side] >= 0 ? P<gw_halo_row>(W.send[side]) : nullptr;
+        if (send_rows) send_rows[side] = W.send_cnt[side] * ROWS;
+    }
+    return 0;
+}
+
+int gw_world_submit(gw_ctx* c, const gw_halo_row* const recv[2], const uint32_t recv_rows[2]) {
+    if (!c) return GW_EINVAL;
+    WorldHost& W = c->wd;
+    if (!W.routed) return set_err(c, GW_ESTATE, "gw_world_route first");
+    W.routed = false;
+    ++W.tick;
+    if (int rc = gw_submit_device_stamped(c, W.ops, (const uint64_t*)W.stamps.p, W.n_ops)) return rc;
+    for (int side = 0; side < 2; ++side) {
+        const uint32_t nr = recv_rows ? recv_rows[side] : 0;
+        if (!nr) continue;
+        if (!recv || !recv[side]) return set_err(c, GW_EINVAL, "rows from side %d missing", side);
+        if (int rc = gw_submit_device_rows(c, recv[side], nr)) return rc;
+    }
+    return 0;
+}
+
+int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
+    if (!c) return GW_EINVAL;
+    WorldHost& W = c->wd;
+    if (!W.on) return set_err(c, GW_ESTATE, "no world strip (gw_world_create)");
+    const bool any_nb = W.nb[0] >= 0 || W.nb[1] >= 0;
+    if (any_nb && (!c->comm || c->c_nranks != (int)W.g.ranks || c->c_rank != (int)W.g.rank))
+        return set_err(c, GW_ESTATE, "world of %u ranks needs a matching communicator (gw_comm_init)", W.g.ranks);
+    if ((uint64_t)n >= STAMP_STRIDE) return set_err(c, GW_ERANGE, "too many ops in one tick for the stamp layout");
+    if (int rs = settle(c)) return rs;
+    (void)hipSetDevice(c->dev);
+    int rc;
+    const uint64_t cap_ent = std::max<uint64_t>(n, 1);
+    if ((rc = ensure(c, W.stamps, (size_t)cap_ent * 8)) || (rc = ensure(c, W.cnt, 64))) return rc;
+    HaloDsts D{};
+    for (int side = 0; side < 2; ++side) {
+        if (W.nb[side] < 0) continue;
+        if ((rc = ensure(c, W.send[side], (size_t)cap_ent * ROWS * sizeof(gw_halo_row)))) return rc;
+        D.d[D.n++] = HaloDst{W.ext_lo[side], W.ext_hi[side], P<gw_halo_row>(W.send[side]), (uint32_t)cap_ent};
+    }
+    const unsigned long long base = 1 + (W.tick * W.g.ranks + W.g.rank) * STAMP_STRIDE;
+    launch_iota_u64(P<unsigned long long>(W.stamps), base, n, c->st);
+    launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->last_pos,
+                      c->last_aoi, c->last_leave, c->clr, c->rflag, c->halo, c->st, /*pad=*/false);
+    HIPCHK(hipGetLastError());
+    uint32_t rcnt[2] = {0, 0};
+    if (any_nb) {
+        // round 1: the entity counts (u32) both ways; HaloStats.cnt[k] is the
+        // k-th destination of D, i.e. left first when both exist
+        uint32_t* dcnt = P<uint32_t>(W.cnt);         // [0..1] received from left / right
+        NCCLCHK(ncclGroupStart());
+        uint32_t k = 0;
+        for (int side = 0; side < 2; ++side) {
+            if (W.nb[side] < 0) continue;
+            ncclResult_t r1 = ncclSend(&c->halo->cnt[k++], 1, ncclUint32, W.nb[side], c->comm, c->st);
+            ncclResult_t r2 = ncclRecv(dcnt + side, 1, ncclUint32, W.nb[side], c->comm, c->st);
+            if (r1 != ncclSuccess || r2 != ncclSuccess) { (void)ncclGroupEnd(); NCCLCHK(r1 != ncclSuccess ? r1 : r2); }
+        }
+        NCCLCHK(ncclGroupEnd());
+        uint32_t h[4] = {0, 0, 0, 0};
+        HIPCHK(hipMemcpyAsync(h, dcnt, 8, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipMemcpyAsync(h + 2, c->halo->cnt, 8, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        k = 0;
+        for (int side = 0; side < 2; ++side) {
+            W.send_cnt[side] = 0;
+            if (W.nb[side] < 0) continue;
+            W.send_cnt[side] = std::min<uint32_t>(h[2 + k++], (uint32_t)cap_ent);
+            rcnt[side] = h[side];
+            if ((rc = ensure(c, W.recv[side], (size_t)std::max<uint32_t>(rcnt[side], 1) * ROWS * sizeof(gw_halo_row))))
+                return rc;
+        }
+        // round 2: exactly the used rows
+        NCCLCHK(ncclGroupStart());
+        for (int side = 0; side < 2; ++side) {
+            if (W.nb[side] < 0) continue;
+            ncclResult_t r1 = ncclSuccess, r2 = ncclSuccess;
+            if (W.send_cnt[side])
+                r1 = ncclSend(W.send[side].p, (size_t)W.send_cnt[side] * ROWS * sizeof(gw_halo_row), ncclUint8,
+                              W.nb[side], c->comm, c->st);
+            if (rcnt[side])
+                r2 = ncclRecv(W.recv[side].p, (size_t)rcnt[side] * ROWS * sizeof(gw_halo_row), ncclUint8, W.nb[side],
+                              c->comm, c->st);
+            if (r1 != ncclSuccess || r2 != ncclSuccess) { (void)ncclGroupEnd(); NCCLCHK(r1 != ncclSuccess ? r1 : r2); }
+        }
+        NCCLCHK(ncclGroupEnd());
+    }
+    W.ops = ops;
+    W.n_ops = n;
+    W.routed = true;
+    const gw_halo_row* recv[2] = {P<gw_halo_row>(W.recv[0]), P<gw_halo_row>(W.recv[1])};
+    const uint32_t rrows[2] = {rcnt[0] * ROWS, rcnt[1] * ROWS};
+    return gw_world_submit(c, recv, rrows);
+}
+
+int gw_world_status(gw_ctx* c, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops) {
+    if (!c) return GW_EINVAL;
+    if (int rs = settle(c)) return rs;
+    (void)hipSetDevice(c->dev);
+    if (c->comm && c->c_nranks > 1) {
+        // the three counters are the first three u64 of HaloStats
+        NCCLCHK(ncclAllReduce(c->halo, c->halo, 3, ncclUint64, ncclSum, c->comm, c->st));
+    }
+    return gw_halo_status(c, overflow, bad_moves, bad_ops);
+}
+
+}  // extern "C"

@@ -38,10 +38,13 @@ state before the tick is the routing state; four light passes over the owned
 ops, rows placed by wave-aggregated atomics into fixed-size NOP-padded
 buffers, no host sync).  tests/torch_router.py restates the same protocol in
 torch for the CPU tests' mock engine and as the row-for-row reference of the
-HIP rows.  The halo exchange is torch.distributed point-to-point (RCCL over
-xGMI with the nccl backend, gloo for the CPU tests); all AOI work is the HIP
-engine's, on torch's stream (gw_set_stream).  Local slots are the global
-entity ids (the local space's capacity is the world population).
+HIP rows.  The halo exchange runs inside the library over its RCCL
+communicator (gw_comm_init + gw_world_step: row counts, one host sync, then
+exactly the used rows, grouped ncclSend/ncclRecv with both neighbours on the
+context's stream over xGMI), or over a torch.distributed group for the CPU
+tests and one-GPU rehearsals (gloo, exchange_rows).  All AOI work is the HIP
+engine's.  Local slots are the global entity ids (the local space's capacity
+is the world population).
 """
 from __future__ import annotations
 
@@ -122,63 +125,49 @@ def words_to_ops(words: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(words, dtype=np.int32).reshape(-1).view(OP_DTYPE)
 
 
-class HipRouter:
-    """The routing on the GPU: gw_route_halo of the rank's engine context
-    writes the rows of both neighbours into persistent torch buffers."""
-
-    def __init__(self, g, geom: Strips, rank: int, device, halo_cap: int):
-        self.g, self.geom, self.r, self.K = g, geom, rank, halo_cap
-        self.bufs, self.dsts = [], []
-        for nb in (rank - 1, rank + 1):
-            if 0 <= nb < geom.ranks:
-                b = torch.zeros((halo_cap * ROWS_PER_ENTITY, ROW_WORDS), dtype=torch.int32, device=device)
-                lo, hi = geom.ext(nb)
-                self.bufs.append(b)
-                self.dsts.append((float(np.float32(lo)), float(np.float32(hi)), b.data_ptr(), halo_cap))
-            else:
-                self.bufs.append(None)
-
-    def route(self, words: torch.Tensor, stamps: torch.Tensor, cap: int | None = None):
-        if not self.dsts:
-            return None, None            # a one-strip world has no neighbours
-        cap = self.K if cap is None else min(cap, self.K)
-        self.g.route_halo(words.data_ptr(), stamps.data_ptr(), words.shape[0], float(self.geom.max_step),
-                          [(lo, hi, p, cap) for lo, hi, p, _ in self.dsts])
-        return tuple(None if b is None else b[:cap * ROWS_PER_ENTITY] for b in self.bufs)
-
-    def receive(self, buf):
-        pass                        # the engine's own state is the routing state
-
-    def collected(self):
-        pass
-
-    def status(self):
-        return self.g.halo_status()
-
-
-def exchange(pg, rank: int, ranks: int, send_left, send_right, nrows: int, device, comm_device):
-    """Halo exchange with both neighbours (point-to-point, one round)."""
+def exchange_rows(pg, rank: int, ranks: int, sends, device, comm_device):
+    """Host-transport halo exchange with both neighbours (torch.distributed
+    point-to-point; gloo for the CPU tests and the one-GPU rehearsals): the
+    row counts first, then exactly the used rows.  sends: [to_left, to_right]
+    int32 (rows, 8) tensors (None where there is no neighbour).  Returns the
+    received [from_left, from_right] on `device`."""
     import torch.distributed as dist
-    shape = (nrows, ROW_WORDS)
     mv = (lambda t: t) if comm_device == device else (lambda t: t.to(comm_device))
-    recv = {}
+    nbs = [(0, rank - 1), (1, rank + 1)]
+    nbs = [(side, nb) for side, nb in nbs if 0 <= nb < ranks]
+    cnt_in = {side: torch.zeros(1, dtype=torch.int64) for side, _ in nbs}
     ops = []
-    for nb, send in ((rank - 1, send_left), (rank + 1, send_right)):
-        if 0 <= nb < ranks:
-            recv[nb] = torch.empty(shape, dtype=torch.int32, device=comm_device)
-            ops.append(dist.P2POp(dist.isend, mv(send).contiguous(), nb, group=pg))
-            ops.append(dist.P2POp(dist.irecv, recv[nb], nb, group=pg))
+    for side, nb in nbs:
+        rows = 0 if sends[side] is None else int(sends[side].shape[0])
+        ops.append(dist.P2POp(dist.isend, torch.tensor([rows], dtype=torch.int64), nb, group=pg))
+        ops.append(dist.P2POp(dist.irecv, cnt_in[side], nb, group=pg))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    recv = [None, None]
+    ops = []
+    for side, nb in nbs:
+        n_in = int(cnt_in[side].item())
+        if sends[side] is not None and sends[side].shape[0]:
+            ops.append(dist.P2POp(dist.isend, mv(sends[side]).contiguous(), nb, group=pg))
+        if n_in:
+            recv[side] = torch.empty((n_in, ROW_WORDS), dtype=torch.int32, device=comm_device)
+            ops.append(dist.P2POp(dist.irecv, recv[side], nb, group=pg))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
     back = (lambda t: t) if comm_device == device else (lambda t: t.to(device))
-    return [back(recv[nb]) for nb in (rank - 1, rank + 1) if nb in recv]
+    return [None if r is None else back(r) for r in recv]
 
 
 class HipStrip:
-    """Engine adapter: a gpuaoi.GpuAOI context sharing one stream with torch
-    (made torch's current stream), so routing kernels, collectives and AOI
-    kernels are ordered without host syncs.  Routing: HipRouter."""
+    """Engine adapter over the library's decomposed world (gw_world_*): a
+    gpuaoi.GpuAOI context sharing one stream with torch (made torch's current
+    stream), so routing kernels, exchanges and AOI kernels are ordered without
+    host syncs beyond the library's own.  comm="rccl": the exchange runs inside
+    the library over its RCCL communicator (gw_world_step); otherwise the rows
+    travel over the caller's torch.distributed group (gw_world_route ->
+    exchange_rows -> gw_world_submit)."""
 
     def __init__(self, g):
         self.g = g
@@ -187,27 +176,41 @@ class HipStrip:
         torch.cuda.set_stream(self.stream)
         g.set_stream(self.stream.cuda_stream)
 
-    def create_space(self, d, cap, bounds):
-        return self.g.create_space(d, cap, bounds)
-
-    def set_ownership(self, sid, lo, hi):
-        self.g.set_ownership(sid, lo, hi)
+    def create_world(self, geom: Strips, rank: int, n_global: int, bounds):
+        return self.g.world_create(geom.x0, geom.w, geom.d, geom.max_step, geom.ranks, rank, n_global, bounds)
 
     def set_clients(self, slots, gates):
         self.g.set_clients(slots, gates)
 
-    def make_router(self, geom, rank, n_global, device, halo_cap):
-        return HipRouter(self.g, geom, rank, device, halo_cap)
+    def step(self, words: torch.Tensor):
+        words = words.contiguous()
+        self._keep.append(words)                # alive until the tick has consumed it
+        self.g.world_step(words.data_ptr(), words.shape[0])
 
-    def submit(self, words: torch.Tensor, stamps: torch.Tensor):
-        words, stamps = words.contiguous(), stamps.contiguous()
-        self._keep += [words, stamps]        # alive until the tick has consumed them
-        self.g.submit_device_stamped(words.data_ptr(), stamps.data_ptr(), words.shape[0])
+    def route(self, words: torch.Tensor, stamps=None):
+        words = words.contiguous()
+        self._keep.append(words)
+        out = []
+        for ptr, rows in self.g.world_route(words.data_ptr(), words.shape[0]):
+            if not ptr:
+                out.append(None)
+                continue
+            buf = np.zeros((rows, ROW_WORDS), np.int32)
+            if rows:
+                self.g.d2h(buf, ptr)
+            out.append(torch.from_numpy(buf))
+        return out
 
-    def submit_rows(self, rows: torch.Tensor):
-        rows = rows.contiguous()
-        self._keep.append(rows)
-        self.g.submit_device_rows(rows.data_ptr(), rows.shape[0])
+    def submit(self, words: torch.Tensor, stamps, recvd):
+        rows = []
+        for r in recvd:
+            if r is None or r.shape[0] == 0:
+                rows.append((0, 0))
+                continue
+            r = r.to(device=torch.device("cuda", torch.cuda.current_device()), dtype=torch.int32).contiguous()
+            self._keep.append(r)
+            rows.append((r.data_ptr(), r.shape[0]))
+        self.g.world_submit(rows)
 
     def tick(self, copy=True, no_events=False, defer=False):
         res = self.g.tick(copy=copy, no_events=no_events, defer=defer)
@@ -223,64 +226,63 @@ class HipStrip:
         self._keep = []
         return res
 
+    def collected(self):
+        pass
+
+    def status(self):
+        return self.g.world_status()
+
 
 class StripRank:
     """One rank of a decomposed world.  `engine` follows HipStrip's interface
-    (make_router / create_space / set_ownership / set_clients / submit /
-    submit_rows / tick / collect)."""
+    (create_world / set_clients / route / submit / [step] / tick / collect /
+    status); comm = "rccl" (HIP engine: exchange inside the library) or
+    "torch" (exchange_rows over the process group `pg`)."""
 
     def __init__(self, engine, geom: Strips, rank: int, n_global: int, bounds, device,
-                 pg=None, comm_device=None, halo_cap: int = 1 << 14, halo_cap_max: int | None = None):
-        """halo_cap: entities per neighbour per tick (steady state); a call may
-        ask for up to halo_cap_max (e.g. the ticks that load the population)."""
+                 pg=None, comm: str = "torch", comm_device=None):
         self.e, self.g, self.r = engine, geom, rank
         self.dev = device
         self.pg = pg
+        self.comm = comm
         self.cdev = comm_device if comm_device is not None else device
-        self.cap = halo_cap
-        self.router = engine.make_router(geom, rank, n_global, device, max(halo_cap, halo_cap_max or 0))
-        self.sid, base = engine.create_space(geom.d, n_global, bounds)
-        if base != 0:
-            raise ValueError("a strip rank holds one space per context (local slot = global id)")
-        engine.set_ownership(self.sid, *geom.own_range_f32(rank))
+        self.sid = engine.create_world(geom, rank, n_global, bounds)
         self.tick_no = 0
 
-    def submit(self, words: torch.Tensor, cap: int | None = None):
+    def submit(self, words: torch.Tensor):
         """Queue this rank's owned ops of one tick (int32 (m, 6) gw_op words on
-        the device, in call order), route and exchange the halo rows (cap:
-        entities per neighbour for this tick; every rank must pass the same)."""
+        the device, in call order): route, exchange the halo rows with both
+        neighbours, queue own ops + received rows."""
         m = words.shape[0]
-        cap = min(self.cap if cap is None else cap, self.router.K)
-        st = stamps_for(self.tick_no, self.r, self.g.ranks, m, self.dev)
-        sl, sr = self.router.route(words, st, cap)
-        nrows = cap * ROWS_PER_ENTITY
-        if self.g.ranks > 1:
-            recvd = exchange(self.pg, self.r, self.g.ranks, sl, sr, nrows, self.dev, self.cdev)
+        if self.comm == "rccl":
+            self.e.step(words)
         else:
-            recvd = []
-        self.e.submit(words, st)
-        for buf in recvd:
-            self.router.receive(buf)
-            self.e.submit_rows(buf)
+            st = stamps_for(self.tick_no, self.r, self.g.ranks, m, self.dev)
+            sends = self.e.route(words, st)
+            if self.g.ranks > 1:
+                recvd = exchange_rows(self.pg, self.r, self.g.ranks, sends, self.dev, self.cdev)
+            else:
+                recvd = [None, None]
+            self.e.submit(words, st, recvd)
         self.tick_no += 1
 
     def tick(self, copy=True, **kw):
         return self.e.tick(copy=copy, **kw)
 
-    def step(self, words: torch.Tensor, copy=True, cap: int | None = None, **kw):
-        self.submit(words, cap)
+    def step(self, words: torch.Tensor, copy=True, **kw):
+        self.submit(words)
         return self.tick(copy=copy, **kw)
 
     def collect(self, copy=True):
         res = self.e.collect(copy=copy)
-        self.router.collected()
+        self.e.collected()
         return res
 
     def check(self):
         """Host check of the contract counters (one sync; call outside timed loops)."""
-        ov, bad, bad_ops = self.router.status()
+        ov, bad, bad_ops = self.e.status()
         if ov > 0:
-            raise RuntimeError(f"halo buffers overflowed by {ov} entities (raise halo_cap)")
+            raise RuntimeError(f"halo buffers overflowed by {ov} entities")
         if bad:
             raise RuntimeError(f"{bad} owned entities moved more than max_step in one tick")
         if bad_ops:

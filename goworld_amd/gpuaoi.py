@@ -70,6 +70,20 @@ class HaloDst(C.Structure):
                 ("reserved", _u32)]
 
 
+class Xfer(C.Structure):
+    _fields_ = [("peer", C.c_int32), ("reserved", _u32), ("send", C.c_void_p), ("send_bytes", _u64),
+                ("recv", C.c_void_p), ("recv_bytes", _u64)]
+
+
+class WorldGeom(C.Structure):
+    _fields_ = [("x0", C.c_float), ("strip_w", C.c_float), ("aoi_dist", C.c_float), ("max_step", C.c_float),
+                ("ranks", _u32), ("rank", _u32)]
+
+
+COMM_ID_BYTES = 128
+RED_SUM, RED_MAX = 0, 1
+
+
 class GwError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"gpuaoi error {code}: {msg}")
@@ -120,6 +134,16 @@ def lib():
         L.gw_halo_status.argtypes = [vp, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64)]
         L.gw_client_events.argtypes = [vp, _u32, C.POINTER(MsgOut), C.POINTER(MsgOut)]
         L.gw_fanout.argtypes = [vp, vp, _u32, _u32, C.POINTER(MsgOut)]
+        L.gw_comm_unique_id.argtypes = [vp]
+        L.gw_comm_init.argtypes = [vp, vp, C.c_int, C.c_int]
+        L.gw_comm_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.gw_comm_exchange.argtypes = [vp, C.POINTER(Xfer), _u32]
+        L.gw_comm_allreduce_u64.argtypes = [vp, vp, _u32, C.c_int]
+        L.gw_world_create.argtypes = [vp, C.POINTER(WorldGeom), _u32, vp, C.POINTER(_u32)]
+        L.gw_world_step.argtypes = [vp, vp, _u32]
+        L.gw_world_route.argtypes = [vp, vp, _u32, C.POINTER(vp * 2), C.POINTER(_u32 * 2)]
+        L.gw_world_submit.argtypes = [vp, C.POINTER(vp * 2), C.POINTER(_u32 * 2)]
+        L.gw_world_status.argtypes = [vp, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64)]
         _lib = L
     return _lib
 
@@ -130,7 +154,18 @@ EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_spa
             "gw_total_neighbors", "gw_device_alloc", "gw_device_free", "gw_memcpy_h2d",
             "gw_memcpy_d2h", "gw_synchronize", "gw_submit_device_stamped", "gw_space_set_ownership",
             "gw_set_stream", "gw_route_halo", "gw_submit_device_rows", "gw_halo_status", "gw_tick_result", "gw_space_restore",
-            "gw_client_events", "gw_fanout"]
+            "gw_client_events", "gw_fanout", "gw_comm_unique_id", "gw_comm_init", "gw_comm_info",
+            "gw_comm_exchange", "gw_comm_allreduce_u64", "gw_world_create", "gw_world_step", "gw_world_route",
+            "gw_world_submit", "gw_world_status"]
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId (rank 0); distribute the bytes to every rank (any channel)."""
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    rc = lib().gw_comm_unique_id(C.cast(buf, C.c_void_p))
+    if rc:
+        raise GwError(rc, "gw_comm_unique_id failed")
+    return buf.raw
 
 
 def _p(a: np.ndarray):
@@ -379,6 +414,55 @@ class GpuAOI:
 
     def synchronize(self):
         self._chk(lib().gw_synchronize(self._h))
+
+    # ---- RCCL communicator (library-internal data-path collectives) -------
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        buf = C.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        self._chk(lib().gw_comm_init(self._h, C.cast(buf, C.c_void_p), nranks, rank))
+
+    def comm_info(self) -> tuple[int, int]:
+        n, r = C.c_int(), C.c_int()
+        self._chk(lib().gw_comm_info(self._h, C.byref(n), C.byref(r)))
+        return n.value, r.value
+
+    def comm_exchange(self, xfers):
+        """xfers: list of (peer, send_ptr, send_bytes, recv_ptr, recv_bytes) (device memory)."""
+        arr = (Xfer * max(1, len(xfers)))(*[Xfer(p, 0, C.c_void_p(sp), sb, C.c_void_p(rp), rb)
+                                             for p, sp, sb, rp, rb in xfers])
+        self._chk(lib().gw_comm_exchange(self._h, arr, len(xfers)))
+
+    def comm_allreduce_u64(self, dev_ptr: int, n: int, op: int = RED_SUM):
+        self._chk(lib().gw_comm_allreduce_u64(self._h, C.c_void_p(dev_ptr), n, op))
+
+    # ---- decomposed world ----------------------------------------------------
+    def world_create(self, x0, strip_w, d, max_step, ranks, rank, capacity, bounds) -> int:
+        geom = WorldGeom(x0, strip_w, d, max_step, ranks, rank)
+        barr = (C.c_float * 4)(*[float(v) for v in bounds])
+        sid = _u32()
+        self._chk(lib().gw_world_create(self._h, C.byref(geom), capacity, C.cast(barr, C.c_void_p), C.byref(sid)))
+        self.spaces.append((sid.value, 0, capacity))
+        return sid.value
+
+    def world_step(self, dev_ops: int, n: int):
+        """Route + RCCL exchange + queue this rank's tick (then tick / sync_collect)."""
+        self._chk(lib().gw_world_step(self._h, C.c_void_p(dev_ops), n))
+
+    def world_route(self, dev_ops: int, n: int):
+        """-> ((left_ptr, left_rows), (right_ptr, right_rows)) device rows to send (ptr 0 = no neighbour)."""
+        ptrs, rows = (C.c_void_p * 2)(), (_u32 * 2)()
+        self._chk(lib().gw_world_route(self._h, C.c_void_p(dev_ops), n, C.byref(ptrs), C.byref(rows)))
+        return [(ptrs[i] or 0, rows[i]) for i in range(2)]
+
+    def world_submit(self, recv):
+        """recv: [(left_ptr, left_rows), (right_ptr, right_rows)] received rows (device)."""
+        ptrs = (C.c_void_p * 2)(*[C.c_void_p(p or None) for p, _ in recv])
+        rows = (_u32 * 2)(*[n for _, n in recv])
+        self._chk(lib().gw_world_submit(self._h, C.byref(ptrs), C.byref(rows)))
+
+    def world_status(self) -> tuple[int, int, int]:
+        v = [_u64() for _ in range(3)]
+        self._chk(lib().gw_world_status(self._h, *[C.byref(x) for x in v]))
+        return tuple(x.value for x in v)
 
 
 def load_space(g: GpuAOI, tr, bounds=None, chunk: int = 1 << 21, via_ticks: bool = False) -> tuple[int, int]:

@@ -204,6 +204,59 @@ def config5_strip(rank: int, ranks: int, ticks: int = 20, seed: int = 5,
                              side_z=side)
 
 
+class WorldWalk:
+    """Config #5 as ONE world: n entities uniform on the 1/128
+    grid in [-side/2, side/2)^2, each tick `move_frac` of them (a fixed random
+    permutation walked in windows, so movers are distinct within a tick) step
+    +-step on both axes, reflected at the WORLD borders only, so entities
+    cross strip borders and migrate between ranks.  Every rank regenerates the
+    same walk and keeps the ops of the entities it owns at the start of the
+    tick (the strip of their x then), in the world's op order."""
+
+    def __init__(self, seed: int = 5, n: int = 16_000_000, side: float = 131072.0, d: float = 100.0,
+                 move_frac: float = 0.10, step: float = 4.0):
+        self.n, self.side, self.d = n, side, d
+        self.half_q = int(side / 2 * Q)
+        self.seed = seed
+        self.kx = rand_int(stream_key(seed, 1), n, -self.half_q, self.half_q)
+        self.kz = rand_int(stream_key(seed, 2), n, -self.half_q, self.half_q)
+        self.yaw = (rand_f32(stream_key(seed, 10), n) * np.float32(2 * math.pi)).astype(np.float32)
+        self.perm = np.argsort(rand_u64(stream_key(seed, 3), n), kind="stable").astype(np.uint32)
+        self.m = int(round(n * move_frac))
+        self.step_q = int(step * Q)
+        self.t = 0
+
+    def x(self) -> np.ndarray:
+        return (self.kx / Q).astype(np.float32)
+
+    def z(self) -> np.ndarray:
+        return (self.kz / Q).astype(np.float32)
+
+    def next_tick(self):
+        """(ops of the whole world in call order, x of every mover before the tick)."""
+        t, n, m = self.t, self.n, self.m
+        start = (t * m) % n
+        idx = np.arange(start, start + m) % n
+        movers = self.perm[idx]
+        x_before = (self.kx[movers] / Q).astype(np.float32)
+        sq = self.step_q
+        dx = (rand_unit(stream_key(self.seed, 101, t), m) * (2 * sq + 1)).astype(np.int64) - sq
+        dz = (rand_unit(stream_key(self.seed, 102, t), m) * (2 * sq + 1)).astype(np.int64) - sq
+        self.kx[movers] = _reflect_q(self.kx[movers] + dx, -self.half_q, self.half_q)
+        self.kz[movers] = _reflect_q(self.kz[movers] + dz, -self.half_q, self.half_q)
+        self.yaw[movers] = rand_f32(stream_key(self.seed, 103, t), m) * np.float32(2 * math.pi)
+        from_client = rand_unit(stream_key(self.seed, 104, t), m) < 0.5
+        ops = make_ops(m)
+        ops["kind"] = OP_MOVED
+        ops["sync_flags"] = np.where(from_client, SIF_NEIGHBOR, SIF_NEIGHBOR | SIF_OWN)
+        ops["slot"] = movers
+        ops["x"] = (self.kx[movers] / Q).astype(np.float32)
+        ops["z"] = (self.kz[movers] / Q).astype(np.float32)
+        ops["yaw"] = self.yaw[movers]
+        self.t += 1
+        return ops, x_before
+
+
 def config4_space(space: int, ticks: int = 20, seed: int = 4, n: int = 1000) -> SpaceTrace:
     """#4: one of the 10k independent spaces (1k entities, L=1024, d=100)."""
     return dyadic_walk_trace(seed * 1_000_003 + space, n, 1024.0, 100.0, ticks, 0.10, 512)
@@ -469,3 +522,30 @@ def strip_world_trace(seed: int, n: int, ranks: int, strip_w: float, height: flo
                 own[k] = enter_owner[i]
         tr.ticks.append((allops, own))
     return tr
+
+
+def walk_strip_trace(seed: int, n: int, side: float, ranks: int, ticks: int) -> StripTrace:
+    """A config #5-shaped decomposed world at test scale: WorldWalk (uniform,
+    dyadic, 10% movers per tick stepping +-4, reflected at the world border)
+    shifted to [0, side)^2 and cut into `ranks` strips of side / ranks; tick 0
+    enters everyone (id order), later ticks are the walk; each op tagged with
+    the strip of the entity's x at the start of the tick."""
+    w = WorldWalk(seed=seed, n=n, side=side)
+    half = np.float32(side / 2)
+    strip_w = side / ranks
+
+    def owner(xs):
+        return np.clip(np.floor(np.asarray(xs, np.float64) / strip_w).astype(np.int64), 0, ranks - 1)
+    gates = np.where(np.arange(n) % 5 == 4, 0, 1 + np.arange(n) % 3).astype(np.uint16)
+    tr = StripTrace(n=n, d=w.d, ranks=ranks, strip_w=float(strip_w), max_step=4.0,
+                    bounds=(0.0, 0.0, float(side), float(side)), gates=gates, ticks=[])
+    x0 = w.x() + half
+    ops = enter_ops(np.arange(n, dtype=np.uint32), x0, np.zeros(n, np.float32), w.z() + half, w.yaw.copy())
+    tr.ticks.append((ops, owner(x0)))
+    for _ in range(1, ticks):
+        ops, xb = w.next_tick()
+        ops["x"] += half
+        ops["z"] += half
+        tr.ticks.append((ops, owner(xb + half)))
+    return tr
+

@@ -355,8 +355,71 @@ int  gw_synchronize(gw_ctx* ctx);
  * restores the context's own stream.  Drains the previous stream first. */
 int  gw_set_stream(gw_ctx* ctx, void* hip_stream);
 
+/* ---- RCCL communicator (one per context: one process per GPU) -----------
+ * The data-path collectives of a decomposed world run inside the library on
+ * the context's stream (RCCL over xGMI), so a Go host drives them through the
+ * same C ABI.  Rank 0 makes the id, the host distributes it (any channel),
+ * every rank calls gw_comm_init (blocking until all have joined). */
+#define GW_COMM_ID_BYTES 128
+int  gw_comm_unique_id(void* id /* GW_COMM_ID_BYTES */);
+int  gw_comm_init(gw_ctx* ctx, const void* id, int nranks, int rank);
+int  gw_comm_info(gw_ctx* ctx, int* nranks, int* rank);      /* 0 ranks: no communicator */
+
+/* One transfer of a grouped point-to-point exchange (bytes, device memory). */
+typedef struct gw_xfer {
+    int32_t     peer;
+    uint32_t    reserved;
+    const void* send;  uint64_t send_bytes;   /* 0: nothing to send to peer   */
+    void*       recv;  uint64_t recv_bytes;   /* 0: nothing to receive        */
+} gw_xfer;
+/* ncclGroupStart; ncclSend / ncclRecv per transfer; ncclGroupEnd, on the
+ * context's stream (asynchronous; the peer may be this rank itself). */
+int  gw_comm_exchange(gw_ctx* ctx, const gw_xfer* x, uint32_t n);
+#define GW_RED_SUM 0
+#define GW_RED_MAX 1
+/* In-place ncclAllReduce of n u64 device words on the context's stream. */
+int  gw_comm_allreduce_u64(gw_ctx* ctx, uint64_t* dev, uint32_t n, int op);
+
+/* ---- decomposed world: one space split into X-strips, one per context ----
+ * Strip r owns entities with x in [x0 + r*w, x0 + (r+1)*w) (strip 0 and the
+ * last one extend to -inf / +inf) and holds, in one local space whose slots
+ * are the global entity ids, every entity within h = d + 2*max_step + 1 +
+ * 1e-5*(|x0| + ranks*w) of it (owned + ghosts).  Per tick:
+ * the owned ops get global stamps 1 + (tick*ranks + rank)*2^26 + i, their net
+ * effect is routed to both neighbours as halo rows (gw_route_halo's rows),
+ * the row counts and then exactly the rows are exchanged, and the owned ops
+ * plus the received rows form the tick's op stream.  Events are emitted only
+ * for owned watchers, records only for owned entities. */
+typedef struct gw_world_geom {
+    float    x0;         /* strip r covers [x0 + r*strip_w, x0 + (r+1)*strip_w)   */
+    float    strip_w;    /* strip width                                         */
+    float    aoi_dist;   /* d (EnableAOI)                                       */
+    float    max_step;   /* max |dx| of a present owned entity per tick         */
+    uint32_t ranks, rank;
+} gw_world_geom;
+/* bounds: the grid of the local space (its held x-range and the world's z). */
+int  gw_world_create(gw_ctx* ctx, const gw_world_geom* geom, uint32_t capacity, const float* bounds,
+                     uint32_t* space_id);
+/* One tick with the exchange over the context's communicator (ranks > 1
+ * needs gw_comm_init): route, count exchange, one host sync, exact row
+ * exchange, queue (then gw_tick / gw_sync_collect as usual).  dev_ops: this
+ * rank's owned ops of the tick in call order, valid until the tick. */
+int  gw_world_step(gw_ctx* ctx, const gw_op* dev_ops, uint32_t n);
+/* The same tick with the exchange done by the caller (another transport):
+ * gw_world_route writes the rows (one host sync) and returns the rows per
+ * neighbour (entities * 3 rows; send[0] left, send[1] right, NULL if none);
+ * the caller sends them, receives the neighbours' rows and calls
+ * gw_world_submit with them (device memory, valid until the tick). */
+int  gw_world_route(gw_ctx* ctx, const gw_op* dev_ops, uint32_t n, const gw_halo_row* send[2],
+                    uint32_t send_rows[2]);
+int  gw_world_submit(gw_ctx* ctx, const gw_halo_row* const recv[2], const uint32_t recv_rows[2]);
+/* Contract counters since the last call, summed over ranks when a
+ * communicator exists: halo overflows (0 by construction), owned entities
+ * that moved more than max_step, ops with an invalid slot or kind. */
+int  gw_world_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops);
+
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 8
+#define GW_ABI_VERSION 9
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

@@ -31,34 +31,43 @@ class OracleStrip:
         self.pyorc = pyorc
         self.words, self.stamps = [], []
 
-    def make_router(self, geom, rank, n_global, device, halo_cap):
-        return torch_router.Router(geom, rank, n_global, device, halo_cap)
+    def create_world(self, geom, rank, n_global, bounds):
+        self.router = torch_router.Router(geom, rank, n_global, torch.device("cpu"), n_global)
+        self.o = self.pyorc.OracleSpace(n_global, geom.d, self.pyorc.SEQRULE)
+        self.x = np.zeros(n_global, np.float32)
+        self.present = np.zeros(n_global, bool)
+        self.lo, self.hi = (np.float32(v) for v in geom.own_range_f32(rank))
+        return 0
 
-    def submit_rows(self, rows):
-        self.submit(*torch_router.split_rows(rows))
+    def route(self, words, stamps):
+        return self.router.route_exact(words, stamps)
 
-    def create_space(self, d, cap, bounds):
-        self.o = self.pyorc.OracleSpace(cap, d, self.pyorc.SEQRULE)
-        self.x = np.zeros(cap, np.float32)
-        self.present = np.zeros(cap, bool)
-        return 0, 0
+    def submit(self, words, stamps, recvd=()):
+        self.words.append(words.cpu().numpy())
+        self.stamps.append(stamps.cpu().numpy())
+        for rows in recvd:
+            if rows is None:
+                continue
+            self.router.receive(rows)
+            w, s = torch_router.split_rows(rows)
+            self.words.append(w.cpu().numpy())
+            self.stamps.append(s.cpu().numpy())
 
-    def set_ownership(self, sid, lo, hi):
-        self.lo, self.hi = np.float32(lo), np.float32(hi)
+    def collected(self):
+        self.router.collected()
+
+    def status(self):
+        return self.router.status()
 
     def set_clients(self, slots, gates):
         for s, g in zip(np.asarray(slots).tolist(), np.asarray(gates).tolist()):
             if g:
                 self.o.set_client(int(s), int(g))
 
-    def submit(self, words, stamps):
-        self.words.append(words.cpu().numpy())
-        self.stamps.append(stamps.cpu().numpy())
-
     def _owned(self, xs):
         return (xs >= self.lo) & (xs < self.hi)
 
-    def tick(self, copy=True):
+    def tick(self, copy=True, no_events=False):
         w = np.concatenate(self.words)
         s = np.concatenate(self.stamps)
         self.words, self.stamps = [], []
@@ -107,11 +116,15 @@ def main():
     ap.add_argument("--max-step", type=float, default=8.0)
     ap.add_argument("--ticks", type=int, default=12)
     ap.add_argument("--collect-every", type=int, default=3)
-    ap.add_argument("--halo-cap", type=int, default=512)
+    ap.add_argument("--trace", choices=["strip", "walk"], default="strip")
+    ap.add_argument("--side", type=float, default=36864.0, help="walk: world side")
     a = ap.parse_args()
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{a.port}", rank=a.rank,
                             world_size=a.world)
-    tr = T.strip_world_trace(a.seed, a.n, a.world, a.strip_w, a.height, a.d, a.ticks, a.max_step)
+    if a.trace == "walk":
+        tr = T.walk_strip_trace(a.seed, a.n, a.side, a.world, a.ticks)
+    else:
+        tr = T.strip_world_trace(a.seed, a.n, a.world, a.strip_w, a.height, a.d, a.ticks, a.max_step)
     geom = dworld.Strips(0.0, tr.strip_w, a.world, tr.d, tr.max_step)
     if a.engine == "oracle":
         eng, dev = OracleStrip(), torch.device("cpu")
@@ -120,12 +133,15 @@ def main():
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
         eng = dworld.HipStrip(gpuaoi.GpuAOI(0))
-    sr = dworld.StripRank(eng, geom, a.rank, a.n, tr.bounds, dev, comm_device=torch.device("cpu"),
-                          halo_cap=a.halo_cap)
+    sr = dworld.StripRank(eng, geom, a.rank, a.n, tr.bounds, dev, comm="torch", comm_device=torch.device("cpu"))
     eng.set_clients(np.arange(a.n, dtype=np.uint32), tr.gates)
     out = {}
     for t in range(len(tr.ticks)):
         w = torch.from_numpy(dworld.ops_to_words(tr.rank_ops(t, a.rank)).copy()).to(dev)
+        if a.trace == "walk" and t == 0:
+            sr.step(w, copy=False, no_events=True)      # the load: no events, its records discarded
+            sr.collect(copy=False)
+            continue
         res = sr.step(w)
         out[f"enter_{t}"], out[f"leave_{t}"] = res.enter, res.leave
         if (t + 1) % a.collect_every == 0 or t == len(tr.ticks) - 1:

@@ -33,7 +33,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_ranks(world, engine, tmp_path, timeout=240):
+def _run_ranks(world, engine, tmp_path, timeout=240, args=None, collect_every=COLLECT_EVERY):
     port = _free_port()
     procs, outs = [], []
     env = dict(os.environ, OMP_NUM_THREADS="1")
@@ -42,8 +42,8 @@ def _run_ranks(world, engine, tmp_path, timeout=240):
         outs.append(out)
         cmd = [sys.executable, os.path.join(HERE, "dworld_worker.py"), "--rank", str(r), "--world", str(world),
                "--port", str(port), "--out", out, "--engine", engine,
-               "--collect-every", str(COLLECT_EVERY)]
-        for k, v in TRACE.items():
+               "--collect-every", str(collect_every)]
+        for k, v in (TRACE if args is None else args).items():
             cmd += [f"--{k.replace('_', '-')}", str(v)]
         procs.append(subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
@@ -130,40 +130,156 @@ def test_dworld_gpu_ranks(world, tmp_path):
     _check(world, _run_ranks(world, "hip", tmp_path, timeout=100))
 
 
-def _canon_rows(buf, K):
-    rows = buf.view(K, 3, 8).cpu().numpy()
+WALK_SMALL = dict(trace="walk", seed=9, n=20000, side=6144.0, ticks=5)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dworld_gloo_oracle_walk(world, tmp_path):
+    """Config #5 shape at test scale: a uniform walk whose entities cross strip
+    borders every tick; the union of the ranks' outputs equals one global
+    oracle space (dyadic positions: the windows are symmetric)."""
+    res = _run_ranks(world, "oracle", tmp_path, args=WALK_SMALL, collect_every=1)
+    tr = T.walk_strip_trace(WALK_SMALL["seed"], WALK_SMALL["n"], WALK_SMALL["side"], world, WALK_SMALL["ticks"])
+    o = pyorc.OracleSpace(tr.n, tr.d, pyorc.SEQRULE)
+    o.set_clients(tr.gates)
+    assert o.tick(tr.global_ops(0)) == 0
+    o.collect()
+    n_ev = 0
+    for t in range(1, len(tr.ticks)):
+        assert o.tick(tr.global_ops(t)) == 0
+        e, l = o.events()
+        for name, exp in (("enter", e), ("leave", l)):
+            got = np.concatenate([r[f"{name}_{t}"] for r in res])
+            assert _sort_ev(got).tobytes() == _sort_ev(exp).tobytes(), f"tick {t}: {name} events differ"
+            n_ev += len(exp)
+        exp = o.collect()
+        got = np.concatenate([r[f"rec_{t}"] for r in res])
+        assert _sort_rec(got).tobytes() == _sort_rec(exp).tobytes(), f"tick {t}: records differ"
+    assert n_ev > 1000
+
+
+@pytest.mark.gpu
+def test_dworld_gpu_walk_1m_equals_single_context(tmp_path):
+    """SURVEY 4 item 4 at config #5 density: a 1M-entity world decomposed into
+    3 strips (3 HIP-engine processes on the one GPU, rows over gloo through
+    the library's gw_world_route / gw_world_submit) equals a single-context
+    HIP run of the same world, tick by tick: the union of the ranks' owned
+    events and records (entities migrate across borders every tick)."""
+    from goworld_amd import gpuaoi
+    args = dict(trace="walk", seed=11, n=1_000_000, side=32768.0, ticks=4)
+    res = _run_ranks(3, "hip", tmp_path, timeout=110, args=args, collect_every=1)
+    tr = T.walk_strip_trace(args["seed"], args["n"], args["side"], 3, args["ticks"])
+    with gpuaoi.GpuAOI(0) as g:
+        sid, base = g.create_space(tr.d, tr.n, tr.bounds)
+        g.set_clients(np.arange(tr.n, dtype=np.uint32), tr.gates)
+        g.submit(tr.global_ops(0))
+        g.tick(copy=False, no_events=True)
+        g.sync_collect(copy=False)
+        n_ev = n_rec = 0
+        for t in range(1, len(tr.ticks)):
+            g.submit(tr.global_ops(t))
+            r = g.tick()
+            for name, exp in (("enter", r.enter), ("leave", r.leave)):
+                got = np.concatenate([x[f"{name}_{t}"] for x in res])
+                assert len(got) == len(exp), (t, name, len(got), len(exp))
+                assert _sort_ev(got).tobytes() == _sort_ev(exp).tobytes(), f"tick {t}: {name} events differ"
+                n_ev += len(exp)
+            exp = g.sync_collect().records
+            got = np.concatenate([x[f"rec_{t}"] for x in res])
+            assert len(got) == len(exp), (t, len(got), len(exp))
+            assert _sort_rec(got).tobytes() == _sort_rec(exp).tobytes(), f"tick {t}: records differ"
+            n_rec += len(exp)
+    assert n_ev > 100_000 and n_rec > 1_000_000
+
+
+@pytest.mark.gpu
+def test_rccl_self_exchange_and_allreduce():
+    """The library's RCCL communicator on the one GPU (a 1-rank communicator):
+    a grouped send/recv to itself moves the bytes, the all-reduce of one rank
+    is the identity, and a one-strip world ticked by gw_world_step (its RCCL
+    path with no neighbours) equals the plain space."""
+    import torch
+    from goworld_amd import gpuaoi
+    with gpuaoi.GpuAOI(0) as g:
+        g.comm_init(gpuaoi.comm_unique_id(), 1, 0)
+        assert g.comm_info() == (1, 0)
+        src = np.arange(1 << 16, dtype=np.uint32)
+        a, b = g.dev_alloc(src.nbytes), g.dev_alloc(src.nbytes)
+        g.h2d(a, src)
+        g.comm_exchange([(0, a, src.nbytes, b, src.nbytes)])
+        back = np.zeros_like(src)
+        g.d2h(back, b)
+        assert np.array_equal(back, src)
+        v = np.array([5, 7, 1 << 40], np.uint64)
+        g.h2d(a, v)
+        g.comm_allreduce_u64(a, 3, gpuaoi.RED_MAX)
+        g.synchronize()
+        w = np.zeros(3, np.uint64)
+        g.d2h(w, a)
+        assert np.array_equal(w, v)
+        g.dev_free(a)
+        g.dev_free(b)
+    tr = T.walk_strip_trace(13, 30000, 8192.0, 1, 4)
+    outs = []
+    for path in ("world", "plain"):
+        with gpuaoi.GpuAOI(0) as g:
+            if path == "world":
+                g.comm_init(gpuaoi.comm_unique_id(), 1, 0)
+                g.world_create(0.0, 8192.0, tr.d, tr.max_step, 1, 0, tr.n, tr.bounds)
+            else:
+                g.create_space(tr.d, tr.n, tr.bounds)
+            g.set_clients(np.arange(tr.n, dtype=np.uint32), tr.gates)
+            seq = []
+            for t in range(len(tr.ticks)):
+                ops = tr.global_ops(t)
+                if path == "world":
+                    dev = torch.from_numpy(ops.view(np.uint8).copy()).to("cuda:0")
+                    torch.cuda.synchronize()               # the copy ran on torch's stream
+                    g.world_step(dev.data_ptr(), len(ops))
+                    r = g.tick()
+                    del dev
+                else:
+                    g.submit(ops)
+                    r = g.tick()
+                seq.append((r.enter.tobytes(), r.leave.tobytes(), g.sync_collect().records.tobytes()))
+            outs.append(seq)
+    assert outs[0] == outs[1]
+
+
+def _canon_rows(buf):
+    rows = buf.reshape(-1, 3, 8).cpu().numpy()
     used = rows[np.any(rows[:, :, 0] & 0xFF, axis=1)]
+    assert len(used) == len(rows), "exact-size rows must not carry NOP padding"
     slot = used[:, :, 1].max(axis=1)
     return used[np.argsort(slot, kind="stable")]
 
 
 @pytest.mark.gpu
 def test_hip_router_rows_match_torch_router():
-    """gw_route_halo (halo.hip) writes, per neighbour, the same entity rows
-    as the torch statement of the protocol (tests/torch_router.py), tick by tick, for
-    the middle rank of a 3-strip world (order of entities aside)."""
+    """gw_world_route (gw_route_halo rows, exact size) writes, per neighbour,
+    the same entity rows as the torch statement of the protocol
+    (tests/torch_router.py), tick by tick, for the middle rank of a 3-strip
+    world (order of entities aside)."""
     import torch
     from goworld_amd import gpuaoi
     tr = T.strip_world_trace(TRACE["seed"], TRACE["n"], 3, TRACE["strip_w"], TRACE["height"],
                              TRACE["d"], TRACE["ticks"], TRACE["max_step"])
     geom = dworld.Strips(0.0, tr.strip_w, 3, tr.d, tr.max_step)
     dev = torch.device("cuda:0")
-    K = 512
     with gpuaoi.GpuAOI(0) as g:
         eng = dworld.HipStrip(g)
-        eng.create_space(tr.d, tr.n, tr.bounds)
-        hip = eng.make_router(geom, 1, tr.n, dev, K)
-        ref = torch_router.Router(geom, 1, tr.n, dev, K)
+        eng.create_world(geom, 1, tr.n, tr.bounds)
+        ref = torch_router.Router(geom, 1, tr.n, dev, tr.n)
         n_rows = 0
         for t in range(len(tr.ticks)):
             w = torch.from_numpy(dworld.ops_to_words(tr.rank_ops(t, 1)).copy()).to(dev)
             st = dworld.stamps_for(t, 1, 3, w.shape[0], dev)
-            for side, (a, b) in enumerate(zip(hip.route(w, st), ref.route(w, st))):
-                ca, cb = _canon_rows(a, K), _canon_rows(b, K)
+            for side, (a, b) in enumerate(zip(eng.route(w, st), ref.route_exact(w, st))):
+                ca, cb = _canon_rows(a), _canon_rows(b)
                 assert ca.shape == cb.shape, (t, side, ca.shape, cb.shape)
                 assert ca.tobytes() == cb.tobytes(), f"tick {t} side {side}: halo rows differ"
                 n_rows += len(ca)
-            eng.submit(w, st)
+            eng.submit(w, st, [None, None])
             eng.tick(copy=False)
             if t % 3 == 2:
                 eng.collect(copy=False)
@@ -171,10 +287,10 @@ def test_hip_router_rows_match_torch_router():
         assert n_rows > 300
         # no overflow; the same move-bound violations (entities that come back
         # after ticks owned elsewhere, whose ghost rows this lone rank never got)
-        assert hip.status() == ref.status()
+        assert eng.status() == ref.status()
         # invalid slots are counted, never followed
         bad = w.clone()
         bad[:, 1] = tr.n + 5
-        hip.route(bad, st)
-        assert hip.status()[2] == bad.shape[0]
+        eng.route(bad)
+        assert eng.status()[2] == bad.shape[0]
         torch.cuda.synchronize()

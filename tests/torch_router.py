@@ -97,6 +97,7 @@ class Router:
         moved = rep & has_aoi & old_p & new_p
         self.bad_moves += (moved & ((new_x - old_x).abs() > g.max_step)).sum()
         sends = []
+        self.last_used = []
         for nb in (r - 1, r + 1):
             if nb < 0 or nb >= g.ranks:
                 sends.append(None)
@@ -120,6 +121,12 @@ class Router:
         self.present[s] = new_p
         self.pflags[s] = new_f
         return sends[0], sends[1]
+
+    def route_exact(self, words: torch.Tensor, stamps: torch.Tensor):
+        """route() trimmed to the used rows (the exact-size exchange)."""
+        sends = list(self.route(words, stamps))
+        used = iter(self.last_used)
+        return [None if b is None else b[:next(used) * ROWS_PER_ENTITY] for b in sends]
 
     def _pack(self, words, stamps, slot, sel, k0, i0, k1, i1, k2, i2, f2, i_last, K):
         """Entity rows (row 0, 1, 2 of each selected entity) compacted into a
@@ -148,6 +155,7 @@ class Router:
         rows = rows * (torch.stack([k0, k1, k2], 1) != 0).to(torch.int32).unsqueeze(2)
         buf = torch.zeros((K + 1, ROWS_PER_ENTITY, ROW_WORDS), dtype=torch.int32, device=self.dev)
         buf.index_copy_(0, dst, rows)   # duplicates only at the trash row K
+        self.last_used.append(int(min(int(sel.sum()), K)))
         return buf[:K].reshape(-1, ROW_WORDS)
 
     def receive(self, buf: torch.Tensor):

@@ -280,8 +280,8 @@ class SpaceRun:
         GW_SYNC_COPY_TO_HOST), i.e. PCIe both ways."""
         g = self.g
         g.submit(self.host_ticks[t])
-        r = g.tick(copy=True)
-        s = g.sync_collect(copy=True, by_client=self.by_client)
+        r = g.tick(copy=True, view=True)
+        s = g.sync_collect(copy=True, by_client=self.by_client, view=True)
         return r.movers, r, s
 
     def close(self):
@@ -560,6 +560,12 @@ def main():
         kind = "c3world"                            # the metric's 1M space decomposed over the N GPUs
     else:
         kind = "c3"                                 # N=1: the 1M space on one GPU (a one-strip world)
+    if kind in ("c5", "c3world") or (a.config5 and kind in ("c3", "c3world")):
+        # torch (decomposed-world runs) brings its own HIP runtime: it must
+        # initialise before the library's runtime does, in this process
+        import torch
+        torch.cuda.set_device(ctl.local)
+        torch.zeros(1, device=torch.device("cuda", ctl.local))
     cm = a.client_msgs if (ws == 1 and kind == "c3") else 0
     n_e2e = a.e2e_steps if kind in ("c3", "c4") else 0
     W, K = a.warmup, a.steps

@@ -17,17 +17,20 @@
 //            old and new relation of every candidate and emits own events,
 //            sorted
 //   mirror   the relation is symmetric, so an own event (A,B) of a mover with
-//            an op-less B is also B's event (B,A): the mover counts it into
-//            B's packed counter (no return value) and keeps (B, A) for later
-//   events   scan of the per-watcher counts -> canonical offsets; movers copy
-//            their sorted own events; each mirror event counts its watcher's
-//            counter back down (the returned value is its rank in the
-//            segment, the last one lists the watcher for the sort); the
-//            listed segments are sorted by target in registers
-// Outputs are placed by scans; the atomics are histogram/cursor updates, one
-// counter increment per mirror event (spread over watchers), wave-aggregated
-// list appends and per-shard statistics.  No MFMA: compare and gather work
-// bound by L2/HBM latency and bandwidth.
+//            an op-less B is also B's event (B,A): the mover keeps (B, A) in
+//            its region (no atomics: device-scope atomics run memory-side on a
+//            multi-XCD part, so a count per mirror event cost more than the
+//            event itself)
+//   events   movers in slot order (bitmap compaction), their own and mirror
+//            events flattened into one array (key = leave<<wbits | watcher,
+//            value = target), one stable LSD radix sort by key: mirror events
+//            enter the sort in mover-slot order and own events target-sorted,
+//            so the result is the canonical (watcher, target) order, enters
+//            then leaves, written as gw_event by the last pass
+// Outputs are placed by scans and sorts; the atomics left are histogram /
+// cursor updates of the grid, one bitmap OR per mover and per-shard
+// statistics.  No MFMA: compare and gather work bound by L2/HBM latency and
+// bandwidth.
 #include "dev_common.hpp"
 
 namespace gw {
@@ -514,7 +517,11 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     const MEnt me = b.gm[m];
     const int ln = lane_id();
     if (!(me.tags & TAG_PRIMARY)) {
-        if (ln == 0) b.mstat[m] = make_ulonglong2(0, 0);
+        if (ln == 0) {
+            b.mstat[m] = make_ulonglong2(0, 0);
+            b.ownc[m] = 0;
+            b.mirc[m] = 0;
+        }
         return;
     }
     const uint64_t lt = lanemask_lt();
@@ -523,7 +530,8 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     if (reg + cap > b.own_cap) {                      // region past the buffers: the host redoes the diff
         if (ln == 0) {
             atomicOr(&b.st->overflow, 1ull);
-            b.mir_cnt[m] = 0;
+            b.ownc[m] = 0;
+            b.mirc[m] = 0;
             b.mstat[m] = make_ulonglong2(0, 0);
         }
         return;
@@ -540,7 +548,7 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     const Rects R = mover_rects(P, po, me.ox, me.oz, pn, me.x, me.z);
     uint32_t* out = b.own + reg;
     uint64_t* mir = b.mir + reg;
-    uint32_t n = 0, nl = 0, nm_ = 0;
+    uint32_t n = 0, nl = 0, nm_ = 0, nml = 0;
     uint32_t c_old = 0, c_new = 0, c_band = 0, c_cli = 0;
     Flat f = flat_build<2>(P, R, w.gn_start, b.gm_start);
     for (uint32_t base = 0; base < f.total; base += 64u * DIFF_U) {
@@ -600,13 +608,10 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
             c_new += (uint32_t)popc64(wave_ballot(t_rn));
             c_cli += (uint32_t)popc64(wave_ballot(t_cli));
             c_band += (uint32_t)popc64(wave_ballot(b_o)) + (uint32_t)popc64(wave_ballot(b_n));
+            // B has no op: (B,A) is B's event too (kept in A's region; the
+            // events stage places it)
             const bool mev = ev && nmv && owned_x(P, e.x);
             ev = ev && ownA;
-            // B has no op: (B,A) is B's event too: count it (no return value,
-            // so the candidate loop never waits on the atomic)
-#ifndef GW_EXP_NO_MIR_ATOMIC
-            if (mev) atomicAdd(&b.cnt64[e.slot], lv ? (1ull << 32) : 1ull);
-#endif
             const uint64_t be = wave_ballot(ev), bl = wave_ballot(ev && lv), bm = wave_ballot(mev);
             const uint32_t at = n + (uint32_t)popc64(be & lt);
             if (ev && at < cap) out[at] = key;
@@ -615,6 +620,7 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
             n += (uint32_t)popc64(be);
             nl += (uint32_t)popc64(bl);
             nm_ += (uint32_t)popc64(bm);
+            nml += (uint32_t)popc64(wave_ballot(mev && lv));
         }
     }
     // sort the own events by (target, kind)
@@ -637,8 +643,12 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     }
     const uint32_t so = c_old, sn = c_new, sb = c_band, scl = c_cli;
     if (ln == 0) {
-        b.cnt64[A] = (unsigned long long)(n - nl) | ((unsigned long long)nl << 32);
-        b.mir_cnt[m] = nm_;
+        b.ownc[m] = (unsigned long long)(n - nl) | ((unsigned long long)nl << 32);
+        b.mirc[m] = (unsigned long long)(nm_ - nml) | ((unsigned long long)nml << 32);
+        if (n | nm_) {                                     // listed for the events stage (slot order)
+            atomicOr(&b.movbit[A >> 5], 1u << (A & 31u));
+            b.gmi[A] = (uint32_t)m;
+        }
         if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | scl;
         // per-mover statistics, summed by k_mover_stats (no atomics here: 2 per
         // mover into 256 shards cost 25 us at config #3 and 180 us at config #4)
@@ -674,7 +684,7 @@ __global__ void __launch_bounds__(NT) k_big_own(TickBufs b) {
     const uint64_t nb = b.st->n_big;
     for (uint64_t k = blockIdx.x; k < nb; k += gridDim.x) {
         const uint32_t m = b.big[k];
-        const uint64_t c = b.cnt64[b.gm[m].slot];
+        const uint64_t c = b.ownc[m];
         const uint32_t n = (uint32_t)(lo32(c) + hi32(c));
         bitonic_inplace<NT>(b.own + b.reg[m], n, (int)threadIdx.x, [](uint32_t v) { return v; },
                             [] { __syncthreads(); });
@@ -682,127 +692,127 @@ __global__ void __launch_bounds__(NT) k_big_own(TickBufs b) {
     }
 }
 
-// movers copy their sorted own events into the canonical arrays and scatter
-// their mirror events to the op-less watchers' segments.  Loads are issued in
-// independent batches ahead of the stores (vmcnt retires in issue order).
-__global__ void __launch_bounds__(NT) k_own_copy(TickBufs b) {
-    const uint64_t m = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
-    if (m >= b.st->n_gm) return;
-    const MEnt me = b.gm[m];
-    if (!(me.tags & TAG_PRIMARY)) return;
+// ---------------------------------------------------------------------------
+// events stage.  (1) movers with events in slot order: compaction of the
+// mover bitmap (one 32-slot word per thread, striped tiles, decoupled
+// look-back; words are cleared as they are read).
+template <int IPT>
+__global__ void __launch_bounds__(NT) k_bits_list(uint32_t* __restrict__ bits, uint64_t nwords,
+                                                  uint32_t* __restrict__ list, unsigned long long* __restrict__ status,
+                                                  unsigned long long* __restrict__ ticket, unsigned long long tbase,
+                                                  uint32_t tag, unsigned long long* total) {
+    __shared__ uint32_t lds[IPT * NWAVE];
+    __shared__ uint32_t s_tile, s_prefix;
+    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tbase);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t t0 = (uint64_t)tile * (IPT * NT);
+    uint32_t wv[IPT], c[IPT];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
+        wv[j] = i < nwords ? bits[i] : 0u;
+        c[j] = (uint32_t)__popc(wv[j]);
+    }
+    uint32_t tot;
+    tile_excl_scan_striped<uint32_t, IPT>(c, lds, tot);
+    if (threadIdx.x < 64) {
+        const uint32_t excl = scan_lookback<uint32_t>(status, tile, tag, tot);
+        if (threadIdx.x == 0) s_prefix = excl;
+    }
+    __syncthreads();
+    const uint32_t pre = s_prefix;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        if (!wv[j]) continue;
+        const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
+        uint32_t v = wv[j], at = pre + c[j];
+        while (v) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(v);
+            v &= v - 1;
+            list[at++] = (uint32_t)(i * 32 + bit);
+        }
+        bits[i] = 0;
+    }
+    if (tile == gridDim.x - 1 && threadIdx.x == 0) *total = pre + tot;
+}
+
+// (2) per listed mover: all its events (own + mirror), packed enters | leaves<<32,
+// and what the flatten needs of it in one 16-B record + its region offset
+__global__ void __launch_bounds__(NT) k_mover_counts(TickBufs b) {
+    const uint64_t k = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= b.st->n_mlist) return;
+    const uint32_t A = b.mlist[k];
+    const uint32_t m = b.gmi[A];
+    const uint64_t oc = b.ownc[m], mc = b.mirc[m];
+    b.mcnt[k] = oc + mc;
+    b.minfo[k] = make_uint4(A, (uint32_t)(lo32(oc) + hi32(oc)), (uint32_t)(lo32(mc) + hi32(mc)), 0u);
+    b.mreg[k] = b.reg[m];
+}
+
+// (3) the listed movers' events flattened at their scanned offsets, in list
+// (slot) order: own events (watcher A, target-sorted), then the mirror events
+// (watcher W, target A).  Keys carry the leave bit above the slot bits.  A
+// lane per mover (64 movers per wave; K ~ 40 gives a few events each), movers
+// with more than FLAT_LANE events afterwards by the whole wave.
+constexpr uint32_t FLAT_LANE = 32;
+__device__ __forceinline__ void flat_put(const TickBufs& b, uint64_t at, uint32_t key, uint32_t val) {
+    b.fk0[at] = key;
+    b.fv0[at] = val;
+}
+__global__ void __launch_bounds__(NT) k_flatten(TickBufs b) {
+    const uint64_t nl_ = b.st->n_mlist;
     const int ln = lane_id();
-    const uint64_t lt = lanemask_lt();
-    const uint32_t A = me.slot;
-    const uint64_t reg = b.reg[m], capm = b.cand[m];
-    const uint32_t nmr = b.mir_cnt[m];
-    const uint64_t c = b.cnt64[A];
-    const uint64_t off = b.off64[A];
-    if (reg + capm > b.own_cap) return;               // overflowed region (k_mover): nothing was written
-    const uint32_t n = (uint32_t)(lo32(c) + hi32(c));
-    // first chunks of both streams in flight together
-    const uint32_t* own = b.own + reg;
-    uint32_t key = (ln < (int)n) ? own[ln] : 0u;
-    uint64_t mv = (ln < (int)nmr) ? b.mir[reg + ln] : 0ull;
-    uint64_t moff = (ln < (int)nmr) ? b.off64[hi32(mv)] : 0ull;
-    if (n) {
-        uint32_t ie = 0, il = 0;
-        for (uint32_t base = 0; base < n; base += 64) {
-            const uint32_t j = base + ln;
-            const bool v = j < n;
-            if (base) key = v ? own[j] : 0u;
-            const bool lv = v && (key & 1u), en = v && !(key & 1u);
-            const uint64_t be = wave_ballot(en), bl = wave_ballot(lv);
-            gw_event ev; ev.watcher = A; ev.target = key >> 1;
-            if (en) { uint64_t at = lo32(off) + ie + popc64(be & lt); if (at < b.ev_cap) b.enter[at] = ev; }
-            if (lv) { uint64_t at = hi32(off) + il + popc64(bl & lt); if (at < b.ev_cap) b.leave[at] = ev; }
-            ie += (uint32_t)popc64(be);
-            il += (uint32_t)popc64(bl);
-        }
-        if (ln == 0) b.cnt64[A] = 0;
+    const uint64_t E = lo32(b.st->ev_pk) + hi32(b.st->ev_pk);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (E > b.ev_cap) atomicOr(&b.st->overflow, 1ull);
+        b.st->n_sort = E > b.ev_cap ? 0 : E;              // nothing is sorted on overflow (the host redoes)
     }
-    // mirror events: the watcher's counter (its full count after the scan) is
-    // counted back down, the returned value is the event's rank in the
-    // segment and the event that reaches zero marks the segment's owner
-    for (uint32_t base = 0; base < nmr; base += 64) {
-        const uint32_t j = base + ln;
-        if (base && j < nmr) {
-            mv = b.mir[reg + j];
-            moff = b.off64[hi32(mv)];
+    if (E > b.ev_cap) return;
+    const uint64_t k0 = ((uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6)) * 64;
+    if (k0 >= nl_) return;
+    const uint64_t k = k0 + ln;
+    const bool valid = k < nl_;
+    uint4 mi = make_uint4(0, 0, 0, 0);
+    uint64_t at = 0, reg = 0;
+    if (valid) {
+        mi = b.minfo[k];
+        const uint64_t off = b.moff[k];
+        at = lo32(off) + hi32(off);
+        reg = b.mreg[k];
+    }
+    const uint32_t lvb = 1u << b.wbits;
+    const uint32_t A = mi.x, n = mi.y, nm = mi.z;
+    const bool small = n + nm <= FLAT_LANE;
+    if (valid && small) {
+        for (uint32_t j = 0; j < n; ++j) {
+            const uint32_t e = b.own[reg + j];
+            flat_put(b, at + j, ((e & 1u) ? lvb : 0u) | A, e >> 1);
         }
-        if (j < nmr) {
-            const uint32_t W = (uint32_t)hi32(mv), al = (uint32_t)lo32(mv);
-            const unsigned long long inc = (al & 1u) ? (1ull << 32) : 1ull;
-            const unsigned long long o = atomicSub(&b.cnt64[W], inc);
-            gw_event ev; ev.watcher = W; ev.target = al >> 1;
-            if (al & 1u) { uint64_t at = hi32(moff) + hi32(o) - 1; if (at < b.ev_cap) b.leave[at] = ev; }
-            else { uint64_t at = lo32(moff) + lo32(o) - 1; if (at < b.ev_cap) b.enter[at] = ev; }
-            // the last event of the watcher marks it for the sort: one bit per
-        // slot, so no two owners contend on a counter
-        if (o == inc) atomicOr(&b.ownbits[W >> 5], 1u << (W & 31u));
+        for (uint32_t j = 0; j < nm; ++j) {
+            const uint64_t e = b.mir[reg + j];
+            flat_put(b, at + n + j, ((e & 1u) ? lvb : 0u) | (uint32_t)hi32(e), (uint32_t)(lo32(e) >> 1));
         }
     }
-}
-
-// Touched op-less watchers: their segments are ordered by target (the ranks
-// came from atomics).  The mirror event whose count-down reached zero set the
-// watcher's bit in ownbits; a thread per bit sorts its watcher's segments of
-// up to REG_SORT targets in registers (bitonic network, indices fixed at
-// compile time) and hands longer ones to the block sort; the first lane of a
-// word clears it.
-constexpr int REG_SORT = 16;
-template <int N>
-__device__ __forceinline__ void reg_sort(uint32_t (&v)[N]) {
-#pragma unroll
-    for (int k = 2; k <= N; k <<= 1)
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1)
-#pragma unroll
-            for (int i = 0; i < N; ++i) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const bool up = (i & k) == 0;
-                    const uint32_t a = v[i], c = v[l];
-                    if ((a > c) == up) { v[i] = c; v[l] = a; }
-                }
-            }
-}
-__device__ __forceinline__ void lane_sort_segment(gw_event* seg, uint32_t n) {
-    uint32_t v[REG_SORT];
-#pragma unroll
-    for (int i = 0; i < REG_SORT; ++i) v[i] = i < (int)n ? seg[i].target : 0xffffffffu;
-    reg_sort<REG_SORT>(v);
-#pragma unroll
-    for (int i = 0; i < REG_SORT; ++i)
-        if (i < (int)n) seg[i].target = v[i];
-}
-__global__ void __launch_bounds__(NT) k_seg_fix(TickBufs b) {
-    const uint32_t W = blockIdx.x * NT + threadIdx.x;     // one thread per slot bit
-    if (W >= b.w.cap) return;
-    const uint32_t bits = b.ownbits[W >> 5];
-    if ((W & 31u) == 0 && bits) b.ownbits[W >> 5] = 0;    // lanes of one word share a wave: all read first
-    if (!((bits >> (W & 31u)) & 1u)) return;
-    const uint64_t o0 = b.off64[W], o1 = b.off64[W + 1];
-    const uint32_t ne = (uint32_t)(lo32(o1) - lo32(o0)), nl = (uint32_t)(hi32(o1) - hi32(o0));
-    if (ne > (uint32_t)REG_SORT || nl > (uint32_t)REG_SORT) {
-        b.bigseg[atomicAdd(&b.st->n_bigseg, 1ull)] = W;                      // rare
-        return;
-    }
-    if (ne > 1 && lo32(o0) + ne <= b.ev_cap) lane_sort_segment(b.enter + lo32(o0), ne);
-    if (nl > 1 && hi32(o0) + nl <= b.ev_cap) lane_sort_segment(b.leave + hi32(o0), nl);
-}
-
-// block sort of op-less segments longer than REG_SORT (by target)
-__global__ void __launch_bounds__(NT) k_big_seg(TickBufs b) {
-    const uint64_t nb = b.st->n_bigseg;
-    for (uint64_t k = blockIdx.x; k < nb; k += gridDim.x) {
-        const uint32_t B = b.bigseg[k];
-        const uint64_t o0 = b.off64[B], o1 = b.off64[B + 1];
-        auto key = [](const gw_event& e) { return e.target; };
-        auto sy = [] { __syncthreads(); };
-        const uint32_t ne = (uint32_t)(lo32(o1) - lo32(o0)), nl = (uint32_t)(hi32(o1) - hi32(o0));
-        if (lo32(o0) + ne <= b.ev_cap) bitonic_inplace<NT>(b.enter + lo32(o0), ne, (int)threadIdx.x, key, sy);
-        if (hi32(o0) + nl <= b.ev_cap) bitonic_inplace<NT>(b.leave + hi32(o0), nl, (int)threadIdx.x, key, sy);
-        __syncthreads();
+    uint64_t bigm = wave_ballot(valid && !small);
+    while (bigm) {                                          // the whole wave per large mover
+        const int q = __builtin_ctzll(bigm);
+        bigm &= bigm - 1;
+        const uint32_t qA = (uint32_t)__builtin_amdgcn_readlane((int)A, q);
+        const uint32_t qn = (uint32_t)__builtin_amdgcn_readlane((int)n, q);
+        const uint32_t qm = (uint32_t)__builtin_amdgcn_readlane((int)nm, q);
+        const uint64_t qat = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(at >> 32), q) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)at, q);
+        const uint64_t qreg = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(reg >> 32), q) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)reg, q);
+        for (uint32_t j = ln; j < qn; j += 64) {
+            const uint32_t e = b.own[qreg + j];
+            flat_put(b, qat + j, ((e & 1u) ? lvb : 0u) | qA, e >> 1);
+        }
+        for (uint32_t j = ln; j < qm; j += 64) {
+            const uint64_t e = b.mir[qreg + j];
+            flat_put(b, qat + qn + j, ((e & 1u) ? lvb : 0u) | (uint32_t)hi32(e), (uint32_t)(lo32(e) >> 1));
+        }
     }
 }
 
@@ -816,14 +826,29 @@ void tick_diff(const TickBufs& b, hipStream_t s) {
 }
 void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint64_t nmax = 2ull * b.m;
-    const uint32_t C = b.w.cap;
     hipLaunchKernelGGL(k_mover_stats, dim3(STAT_SHARDS), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_big_own, dim3(64), dim3(NT), 0, s, b);
-    scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.cnt64, b.off64, (uint64_t)C + 1, nullptr, sc,
+    // movers in slot order
+    const uint64_t nwords = (uint64_t)b.w.cap / 32 + 1;
+    const uint64_t tile = (uint64_t)SCAN_IPT * NT;
+    const uint32_t nb = nblk1(nwords, (uint32_t)tile);
+    if (sc.tag >= SCAN_TAG_MAX) {
+        (void)hipMemsetAsync(sc.status, 0, sc.max_tiles * SCAN_WORDS * 8, s);
+        sc.tag = 0;
+    }
+    ++sc.tag;
+    hipLaunchKernelGGL(k_bits_list<SCAN_IPT>, dim3(nb), dim3(NT), 0, s, b.movbit, nwords, b.mlist, sc.status,
+                       sc.ticket, sc.tbase, sc.tag, &b.st->n_mlist);
+    sc.tbase += nb;
+    const uint64_t* nml = (const uint64_t*)&b.st->n_mlist;
+    hipLaunchKernelGGL(k_mover_counts, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
+    scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.mcnt, (uint64_t*)b.moff, b.m, nml, sc,
                                        (uint64_t*)&b.st->ev_pk, s);
-    hipLaunchKernelGGL(k_own_copy, dim3(nblk1(nmax, NWAVE)), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_seg_fix, dim3(nblk1(C, NT)), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_big_seg, dim3(64), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_flatten, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
+    // one stable sort by (leave, watcher); the last pass writes gw_event
+    radix_sort2(b.fk0, b.fv0, b.fk1, b.fv1, b.ev_cap, (const uint64_t*)&b.st->n_sort, 0, b.wbits + 1, b.rtable, sc,
+                s, b.ev, (1u << b.wbits) - 1u);
+    (void)nmax;
 }
 
 // ---------------------------------------------------------------------------

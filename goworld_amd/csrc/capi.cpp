@@ -200,9 +200,9 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->pos, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->flags, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->gate, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->cnt64, oc ? oc + 1 : 0, (size_t)nc + 1))) return rc;
     if ((rc = grow_preserve(c, c->nbc, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->ownbits, 0, (size_t)nc / 32 + 1))) return rc;
+    if ((rc = grow_preserve(c, c->movbit, 0, (size_t)nc / 32 + 1))) return rc;
+    if ((rc = grow_preserve(c, c->gmi, 0, (size_t)nc))) return rc;
     if ((rc = grow_preserve(c, c->last_pos, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_aoi, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_leave, oc, nc))) return rc;
@@ -219,9 +219,8 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     HIPCHK(hipMemsetAsync(c->flags + oc, 0, n * 4, c->st));
     HIPCHK(hipMemsetAsync(c->rflag + oc, 0, n * 4, c->st));
     HIPCHK(hipMemsetAsync(c->gate + oc, 0, n * 2, c->st));
-    HIPCHK(hipMemsetAsync(c->cnt64 + oc, 0, (n + 1) * 8, c->st));
     HIPCHK(hipMemsetAsync(c->nbc + oc, 0, n * 8, c->st));
-    HIPCHK(hipMemsetAsync(c->ownbits, 0, ((size_t)nc / 32 + 1) * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->movbit, 0, ((size_t)nc / 32 + 1) * 4, c->st));
     launch_fill_i32(c->last_pos + oc, -1, n, c->st);
     launch_fill_i32(c->last_aoi + oc, -1, n, c->st);
     launch_fill_i32(c->last_leave + oc, -1, n, c->st);
@@ -444,11 +443,11 @@ void gw_shutdown(gw_ctx* c) {
     (void)settle(c);
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1, &c->bigseg,
-                      &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->off64, &c->mir,
-                      &c->mir_cnt,
-                      &c->enter_d, &c->leave_d, &c->scan_status, &c->rs_hist,
-                      &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
+    DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1,
+                      &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
+                      &c->mcnt, &c->moff, &c->minfo, &c->mreg, &c->fk0, &c->fv0, &c->fk1, &c->fv1, &c->ev_d, &c->rtable,
+                      &c->scan_status, &c->rs_hist,
+                      &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec_big, &c->rec0, &c->rec1,
                       &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf, &c->cl_slot, &c->cl_off,
                       &c->m_create.a, &c->m_create.b, &c->m_destroy.a, &c->m_destroy.b, &c->m_fanout.a,
                       &c->m_fanout.b, &c->m_flag, &c->m_at, &c->m_items, &c->m_cnt, &c->m_off};
@@ -459,7 +458,7 @@ void gw_shutdown(gw_ctx* c) {
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off, &c->m_create.h,
                     &c->m_destroy.h, &c->m_fanout.h};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
-    void* ps[] = {c->halo, c->rflag, c->sc.ticket, c->ownbits, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->cnt64, c->nbc, c->last_pos, c->last_aoi,
+    void* ps[] = {c->halo, c->rflag, c->sc.ticket, c->movbit, c->gmi, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->nbc, c->last_pos, c->last_aoi,
                   c->last_leave, c->clr, c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->cstats, c->scal32, c->gsb[0],
                   c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->bigcell, c->gm_start};
     for (void* p : ps) if (p) (void)hipFree(p);
@@ -686,9 +685,12 @@ int gw_set_clients(gw_ctx* c, const uint32_t* slots, const uint16_t* gates, uint
 
 static int ensure_events(gw_ctx* c) {
     int r;
+    const uint64_t tiles = (c->ev_cap + radix2_tile() - 1) / radix2_tile() + 1;
     if ((r = ensure(c, c->own, c->own_cap * 4)) || (r = ensure(c, c->mir, c->own_cap * 8)) ||
-        (r = ensure(c, c->enter_d, 2 * c->own_cap * sizeof(gw_event))) ||
-        (r = ensure(c, c->leave_d, 2 * c->own_cap * sizeof(gw_event))))
+        (r = ensure(c, c->fk0, c->ev_cap * 4)) || (r = ensure(c, c->fv0, c->ev_cap * 4)) ||
+        (r = ensure(c, c->fk1, c->ev_cap * 4)) || (r = ensure(c, c->fv1, c->ev_cap * 4)) ||
+        (r = ensure(c, c->ev_d, c->ev_cap * sizeof(gw_event))) || (r = ensure(c, c->rtable, tiles * 256 * 4)) ||
+        (r = ensure_scan(c, tiles * 256)))
         return r;
     return 0;
 }
@@ -696,8 +698,11 @@ static int ensure_events(gw_ctx* c) {
 static void bind_events(gw_ctx* c, TickBufs& b) {
     b.own_cap = c->own_cap;
     b.own = P<uint32_t>(c->own); b.mir = P<uint64_t>(c->mir);
-    b.enter = P<gw_event>(c->enter_d); b.leave = P<gw_event>(c->leave_d);
-    b.ev_cap = 2 * c->own_cap;
+    b.fk0 = P<uint32_t>(c->fk0); b.fv0 = P<uint32_t>(c->fv0);
+    b.fk1 = P<uint32_t>(c->fk1); b.fv1 = P<uint32_t>(c->fv1);
+    b.ev = P<gw_event>(c->ev_d);
+    b.ev_cap = c->ev_cap;
+    b.rtable = P<uint32_t>(c->rtable);
 }
 
 // Second half of a tick: read the statistics (one host sync, or none when a
@@ -712,21 +717,25 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     p.on = false;
     (void)hipSetDevice(c->dev);
     TickBufs b = p.b;
-    const uint32_t M = p.M, C = p.C, NC = p.NC, flags = p.flags;
+    const uint32_t M = p.M, NC = p.NC, flags = p.flags;
     size_t s_grid = p.s_grid, s_movers = p.s_movers, s_diff = p.s_diff, s_events = p.s_events;
     int rc;
     if (p.copied) HIPCHK(hipStreamSynchronize(c->st));
     else if ((rc = read_stats(c))) return rc;
-    if (c->hstats->overflow) {
-        // the own-event regions did not fit: grow to the exact bound, clear the
-        // per-watcher counters and rerun diff + events (their inputs are intact)
-        c->own_cap = c->hstats->cand_total + c->hstats->cand_total / 4 + 4096;
+    // the own-event regions or the event buffers did not fit: grow to the
+    // exact bounds and rerun diff + events (their inputs are intact; the mover
+    // bitmap was cleared by the list pass).  A region overflow hides the events
+    // of the movers it stopped, so the event count is only exact on the next
+    // attempt: up to three.
+    for (int attempt = 0; c->hstats->overflow; ++attempt) {
+        if (attempt == 3) return set_err(c, GW_ENOMEM, "event buffers overflowed three times");
+        const uint64_t E = (c->hstats->ev_pk & 0xffffffffull) + (c->hstats->ev_pk >> 32);
+        if (c->hstats->cand_total > c->own_cap) c->own_cap = c->hstats->cand_total + c->hstats->cand_total / 4 + 4096;
+        if (E > c->ev_cap) c->ev_cap = E + E / 4 + 4096;
         if ((rc = ensure_events(c))) return rc;
         bind_events(c, b);
-        HIPCHK(hipMemsetAsync(c->cnt64, 0, ((size_t)C + 1) * 8, c->st));
-        HIPCHK(hipMemsetAsync(c->ownbits, 0, ((size_t)C / 32 + 1) * 4, c->st));
         DevStats* h = c->hstats;
-        h->overflow = 0; h->n_big = 0; h->n_bigseg = 0; h->ev_pk = 0;
+        h->overflow = 0; h->n_big = 0; h->ev_pk = 0; h->n_mlist = 0; h->n_sort = 0;
         for (int i = 0; i < STAT_SHARDS; ++i)      // the diff's shards restart; the mover count stays
             for (int f = 0; f < SH_FIELDS; ++f)
                 if (f != SH_MOVERS) h->shard[i][f] = 0;
@@ -739,7 +748,6 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         s_events = prof_end(c, 0);
         HIPCHK(hipGetLastError());
         if ((rc = read_stats(c))) return rc;
-        if (c->hstats->overflow) return set_err(c, GW_ENOMEM, "event regions overflowed twice");
     }
     prof_begin(c, "reset");
     tick_reset(b, c->st);                            // asynchronous: the next call orders behind it
@@ -762,17 +770,17 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     if (getenv("GW_DEBUG_STATS")) {
         unsigned long long f0 = 0, f2 = 0;
         for (int i = 0; i < STAT_SHARDS; ++i) { f0 += hs.shard[i][0]; f2 += hs.shard[i][2]; }
-        fprintf(stderr, "gw_tick: movers %llu gm %llu cand %llu ev %llu+%llu big %llu bigseg %llu bigcell %llu "
-                "seg_lane %llu seg_wave %llu\n", (unsigned long long)n_mov, hs.n_gm, hs.cand_total, hs.ev_pk & 0xffffffffull,
-                hs.ev_pk >> 32, hs.n_big, hs.n_bigseg, hs.n_bigcell, f0, f2);
+        fprintf(stderr, "gw_tick: movers %llu gm %llu cand %llu ev %llu+%llu big %llu mlist %llu bigcell %llu "
+                "f0 %llu f2 %llu\n", (unsigned long long)n_mov, hs.n_gm, hs.cand_total, hs.ev_pk & 0xffffffffull,
+                hs.ev_pk >> 32, hs.n_big, hs.n_mlist, hs.n_bigcell, f0, f2);
     }
     o.ops = M;
     o.movers = n_mov;
     o.pairs_tested = pairs;
     o.nbr_old = a_old;
     o.nbr_new = a_new;
-    o.enter_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->enter_d);
-    o.leave_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->leave_d);
+    o.enter_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->ev_d);
+    o.leave_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->ev_d) + (hs.ev_pk & 0xffffffffull);
     o.n_enter = n_enter;
     o.n_leave = n_leave;
     // SURVEY 8(d) algorithmic bytes of the AOI part (records are counted by gw_sync_collect)
@@ -785,13 +793,16 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         // diff: candidates (16 B grid / 32 B mover grid; counted at 16 B) + own events (4 B)
         prof_set_bytes(c, s_diff, 16ull * pairs + 4ull * n_evt);
         // events: per-watcher counts and offsets (16 B per slot) + events (8 B) + own copies (4 B)
-        prof_set_bytes(c, s_events, 16ull * (C + 1) + 12ull * n_evt);
+        // events: flatten (read 4-8 B, write 8 B) + three sort passes (read 12 B, write 8 B) per event
+        prof_set_bytes(c, s_events, 76ull * n_evt);
     }
     if ((flags & GW_TICK_COPY_TO_HOST) && !(flags & GW_TICK_NO_EVENTS)) {
         if ((rc = ensure_host(c, c->h_enter, std::max<uint64_t>(n_enter, 1) * sizeof(gw_event)))) return rc;
         if ((rc = ensure_host(c, c->h_leave, std::max<uint64_t>(n_leave, 1) * sizeof(gw_event)))) return rc;
-        if (n_enter) HIPCHK(hipMemcpyAsync(c->h_enter.p, c->enter_d.p, n_enter * sizeof(gw_event), hipMemcpyDeviceToHost, c->st));
-        if (n_leave) HIPCHK(hipMemcpyAsync(c->h_leave.p, c->leave_d.p, n_leave * sizeof(gw_event), hipMemcpyDeviceToHost, c->st));
+        if (n_enter) HIPCHK(hipMemcpyAsync(c->h_enter.p, c->ev_d.p, n_enter * sizeof(gw_event), hipMemcpyDeviceToHost, c->st));
+        if (n_leave)
+            HIPCHK(hipMemcpyAsync(c->h_leave.p, P<gw_event>(c->ev_d) + n_enter, n_leave * sizeof(gw_event),
+                                  hipMemcpyDeviceToHost, c->st));
         HIPCHK(hipStreamSynchronize(c->st));
         o.enter = (const gw_event*)c->h_enter.p;
         o.leave = (const gw_event*)c->h_leave.p;
@@ -884,13 +895,15 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     const uint64_t M2 = 2ull * M;
     // ---- buffers (event regions sized from the last tick; grown on overflow)
     c->own_cap = std::max<uint64_t>(c->own_cap, 64ull * M + 4096);
+    c->ev_cap = std::max<uint64_t>(c->ev_cap, 48ull * M + 4096);
     if ((rc = ensure(c, c->gm, M2 * sizeof(MEnt))) ||
         (rc = ensure(c, c->cand, M2 * 8)) || (rc = ensure(c, c->reg, M2 * 8)) ||
-        (rc = ensure(c, c->mir_cnt, M2 * 4)) || (rc = ensure(c, c->big, M2 * 4)) ||
+        (rc = ensure(c, c->ownc, M2 * 8)) || (rc = ensure(c, c->mirc, M2 * 8)) || (rc = ensure(c, c->big, M2 * 4)) ||
         (rc = ensure(c, c->mstat, M2 * 16)) ||
-        (rc = ensure(c, c->bigseg, (size_t)C * 4)) ||
-        (rc = ensure(c, c->off64, ((size_t)C + 2) * 8)) ||
-        (rc = ensure_scan(c, std::max<uint64_t>(std::max<uint64_t>(M2, (uint64_t)C + 1), (uint64_t)NC + 1))))
+        (rc = ensure(c, c->mlist, (size_t)M * 4)) || (rc = ensure(c, c->mcnt, (size_t)M * 8)) ||
+        (rc = ensure(c, c->moff, (size_t)M * 8)) || (rc = ensure(c, c->minfo, (size_t)M * 16)) ||
+        (rc = ensure(c, c->mreg, (size_t)M * 8)) ||
+        (rc = ensure_scan(c, std::max<uint64_t>(std::max<uint64_t>(M2, (uint64_t)C / 32 + 2), (uint64_t)NC + 1))))
         return rc;
     if ((rc = ensure_events(c))) return rc;
     reset_stats_host(c);
@@ -909,11 +922,14 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.dep = c->dep; b.arr = c->arr; b.cnt_new = c->cnt_new; b.bigcell = c->bigcell;
     b.gm_cnt = c->gm_cnt; b.gm_start = c->gm_start; b.gm = P<MEnt>(c->gm);
     b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg);
-    b.mir_cnt = P<uint32_t>(c->mir_cnt); b.big = P<uint32_t>(c->big);
+    b.ownc = P<unsigned long long>(c->ownc); b.mirc = P<unsigned long long>(c->mirc);
+    b.big = P<uint32_t>(c->big);
     b.mstat = P<ulonglong2>(c->mstat);
-    b.bigseg = P<uint32_t>(c->bigseg);
-    b.ownbits = c->ownbits;
-    b.cnt64 = c->cnt64; b.off64 = P<uint64_t>(c->off64);
+    b.movbit = c->movbit; b.gmi = c->gmi;
+    b.mlist = P<uint32_t>(c->mlist);
+    b.mcnt = P<unsigned long long>(c->mcnt); b.moff = P<unsigned long long>(c->moff);
+    b.minfo = P<uint4>(c->minfo); b.mreg = P<unsigned long long>(c->mreg);
+    b.wbits = ceil_log2(C);
     bind_events(c, b);
 
     prof_begin(c, "ops");
@@ -976,6 +992,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     DevStats* st = c->cstats;
     if ((rc = ensure(c, c->fbits, (size_t)C * 4)) || (rc = ensure(c, c->flagged, (size_t)C * 4)) ||
         (rc = ensure(c, c->rec_cnt, (size_t)C * 4)) || (rc = ensure(c, c->rec_off, (size_t)C * 8)) ||
+        (rc = ensure(c, c->rec_big, (size_t)C * 4)) ||
         (rc = ensure_scan(c, C)))
         return rc;
     // records land in a buffer sized from the last collect; if it was too
@@ -995,7 +1012,8 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     size_t s_count = prof_end(c, 0);
     prof_begin(c, "sync_write");
     launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint64_t>(c->rec_off),
-                      P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
+                      P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, P<uint32_t>(c->rec_big),
+                      c->st);
     size_t s_write = prof_end(c, 0);
     HIPCHK(hipGetLastError());
     if ((rc = read_cstats(c))) return rc;                // the one host sync
@@ -1007,8 +1025,11 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         if ((rc = ensure(c, c->rec0, c->rec_cap * sizeof(gw_sync_record)))) return rc;
         c->hcstats->overflow = 0;
         HIPCHK(hipMemcpyAsync(c->cstats, c->hcstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
+        c->hcstats->n_big = 0;
+        HIPCHK(hipMemcpyAsync(c->cstats, c->hcstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
         launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint64_t>(c->rec_off),
-                          P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
+                          P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st,
+                          P<uint32_t>(c->rec_big), c->st);
         HIPCHK(hipGetLastError());
         if ((rc = read_cstats(c))) return rc;
         if (c->hcstats->overflow) return set_err(c, GW_ENOMEM, "sync record buffer overflowed twice");

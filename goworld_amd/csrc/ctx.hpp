@@ -97,9 +97,9 @@ struct gw_ctx {
     float4* pos = nullptr;
     uint32_t* flags = nullptr;
     uint16_t* gate = nullptr;
-    unsigned long long* cnt64 = nullptr;     // [slot_cap + 1], zero between ticks
     unsigned long long* nbc = nullptr;       // [slot_cap] epoch<<32 | neighbours with a client
-    uint32_t* ownbits = nullptr;             // [slot_cap/32 + 1] zero between ticks
+    uint32_t* movbit = nullptr;              // [slot_cap/32 + 1] movers of the tick, zero between ticks
+    uint32_t* gmi = nullptr;                 // [slot_cap] primary mover-grid entry of a mover
     int32_t *last_pos = nullptr, *last_aoi = nullptr, *last_leave = nullptr;
     int32_t* clr = nullptr;                   // [2 slot_cap] last Leave clearing each sync bit, -1 between ticks
     uint32_t* rflag = nullptr;                // [slot_cap] halo routing scratch, zero between calls
@@ -130,12 +130,13 @@ struct gw_ctx {
     gw_tick_out last_out{};
 
     // grid + tick scratch
-    DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, cand, reg, own, big, bigseg, mstat;
-    DevBuf mir, mir_cnt;
-    DevBuf off64, enter_d, leave_d, scan_status, rs_hist;
+    DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, cand, reg, own, big, mstat;
+    DevBuf mir, ownc, mirc, mlist, mcnt, moff, minfo, mreg, fk0, fv0, fk1, fv1, ev_d, rtable;
+    DevBuf scan_status, rs_hist;
+    uint64_t ev_cap = 0;                 // events the flatten/sort buffers hold (grows on overflow)
     ScanCtx sc{};                  // single-pass scan state (prim.hpp)
     // sync / query scratch
-    DevBuf fbits, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
+    DevBuf fbits, flagged, rec_cnt, rec_off, rec_big, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
     DevBuf cl_slot, cl_off, h_cl_slot, h_cl_off;   // GW_SYNC_BY_CLIENT segments (device / pinned host)
     uint64_t rec_cap = 0;                // records the rec0 buffer holds (grows on overflow)
     // client messages (gw_client_events, gw_fanout): ping-pong + pinned host + gate offsets

@@ -205,8 +205,9 @@ __device__ __forceinline__ void bitonic_inplace(T* a, uint32_t n, int t, KeyF ke
     const uint32_t P2 = next_pow2(n);
     for (uint32_t k = 2; k <= P2; k <<= 1) {
         const uint32_t h = k >> 1;
+        const int lh = __builtin_ctz(h);                 // powers of two: shifts, no integer division
         for (uint32_t i = t; i < (P2 >> 1); i += TPM) {
-            const uint32_t lo = (i / h) * k + (i % h);
+            const uint32_t lo = ((i >> lh) << (lh + 1)) | (i & (h - 1));
             const uint32_t hi = lo ^ (k - 1);
             if (hi < n) {
                 T x = a[lo], y = a[hi];
@@ -215,8 +216,9 @@ __device__ __forceinline__ void bitonic_inplace(T* a, uint32_t n, int t, KeyF ke
         }
         sync();
         for (uint32_t j = h >> 1; j > 0; j >>= 1) {
+            const int lj = __builtin_ctz(j);
             for (uint32_t i = t; i < (P2 >> 1); i += TPM) {
-                const uint32_t lo = (i / j) * (2 * j) + (i % j);
+                const uint32_t lo = ((i >> lj) << (lj + 1)) | (i & (j - 1));
                 const uint32_t hi = lo + j;
                 if (hi < n) {
                     T x = a[lo], y = a[hi];

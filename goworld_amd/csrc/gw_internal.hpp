@@ -88,7 +88,8 @@ struct DevStats {
     unsigned long long n_gm;          // mover-grid entries
     unsigned long long ev_pk;         // sum of (enters | leaves<<32) over watchers
     unsigned long long n_big;         // own-event segments left for the block sort
-    unsigned long long n_bigseg;      // op-less segments left for the block sort
+    unsigned long long n_mlist;       // movers with events (slot-ordered list)
+    unsigned long long n_sort;        // events flattened for the sort (min(E, ev_cap))
     unsigned long long overflow;      // event regions exceeded their capacity
     unsigned long long bad_ops;
     unsigned long long flagged;       // sync: flagged entities
@@ -111,6 +112,7 @@ struct RadixTmp {
     ScanCtx* sc;
 };
 uint64_t radix_tile();            // keys per radix block
+uint64_t radix2_tile();           // keys per tile of radix_sort2
 uint64_t scan_tile();             // elements per scan tile
 uint64_t scan_words();            // status words per scan tile
 void scan_u32_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
@@ -169,19 +171,26 @@ struct TickBufs {
     uint64_t* cand;           // [2m] candidate bound (0 unless TAG_PRIMARY)
     uint64_t* reg;            // [2m] exclusive scan of cand
     uint64_t own_cap;         // capacity of own / mir
-    uint32_t* own;            // own events (target<<1 | leave)
+    uint32_t* own;            // own events (target<<1 | leave), sorted by target per mover
     uint64_t* mir;            // mirror events of op-less neighbours: watcher<<32 | mover<<1 | leave
-    uint32_t* ownbits;        // [cap/32 + 1] touched op-less watchers to sort, zero between ticks
-    uint32_t* mir_cnt;        // [2m] mirror events per entry
+    unsigned long long* ownc; // [2m] own enters | leaves<<32 per entry
+    unsigned long long* mirc; // [2m] mirror enters | leaves<<32 per entry
     ulonglong2* mstat;        // [2m] A_old | A_new << 32, band count per entry (k_mover -> k_mover_stats)
     uint32_t* big;            // [2m] entries whose own events need the block sort
-    uint32_t* bigseg;         // [cap] op-less watchers whose segments need the block sort
-    // canonical events
-    unsigned long long* cnt64;  // [cap+1] enters | leaves<<32 per watcher, zero between ticks
-    uint64_t* off64;          // [cap+1]
-    gw_event* enter;
-    gw_event* leave;
-    uint64_t ev_cap;          // capacity of enter and of leave
+    // canonical events: movers in slot order, their events flattened, one
+    // stable radix sort by (leave, watcher) -> (watcher, target) order
+    uint32_t* movbit;         // [cap/32 + 1] movers, zero between ticks
+    uint32_t* gmi;            // [cap] primary mover-grid entry of a mover slot
+    uint32_t* mlist;          // [m] movers in slot order
+    unsigned long long* mcnt; // [m] all events of a listed mover (enters | leaves<<32)
+    unsigned long long* moff; // [m] exclusive scan of mcnt
+    uint4* minfo;             // [m] listed mover: slot, own events, mirror events
+    unsigned long long* mreg; // [m] its region offset
+    uint32_t *fk0, *fv0, *fk1, *fv1;   // [ev_cap] flattened events: key leave<<wbits | watcher, value target
+    gw_event* ev;             // [ev_cap] canonical events, enters then leaves
+    uint64_t ev_cap;
+    uint32_t* rtable;         // radix digit table (256 per tile)
+    int wbits;                // bits of a slot
     int diff_u;               // candidate chunks of 64 in flight per k_mover iteration
 };
 
@@ -207,7 +216,7 @@ void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* 
                        uint32_t nf_max, uint32_t* cnt, hipStream_t s);
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
-                       uint64_t rec_cap, DevStats* st, hipStream_t s);
+                       uint64_t rec_cap, DevStats* st, uint32_t* big, hipStream_t s);
 void launch_gate_hist(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,
                       uint32_t* hist /*65536*/, hipStream_t s);
 void launch_gate_keys(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,

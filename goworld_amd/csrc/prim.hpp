@@ -393,4 +393,174 @@ inline int radix_sort(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n_max, 
     return cur;
 }
 
+// ---------------------------------------------------------------------------
+// Stable LSD radix sort of (u32 key, u32 value) pairs, 8-bit digits, tiles of
+// 4096 pairs with LDS-staged coalesced scatter.  Per pass: an upsweep writes
+// the per-tile digit counts (digit-major table), one device scan turns them
+// into global offsets, and the downsweep ranks the tile in LDS and writes each
+// digit's run of the tile contiguously.  Ranking is wave-private (no barrier
+// inside the loop): wave w owns the tile's w-th quarter in input order, ranks
+// each 64-key chunk by match-any over the 8 digit bits (8 ballots) against a
+// wave-private LDS histogram; the waves' counts are then prefix-summed per
+// digit, so the order within a digit is the input order (stable).  The last
+// pass may write gw_event {key & mask, value} instead of the two arrays.
+constexpr int RS2_IPT = 16;
+constexpr int RS2_TILE = NT * RS2_IPT;              // 4096
+constexpr int RS2_WAVE_KEYS = RS2_TILE / NWAVE;     // 1024 per wave
+constexpr int RS2_CHUNKS = RS2_WAVE_KEYS / 64;      // 16
+
+template <int TILE_ = RS2_TILE>   // a template: the header is included by several translation units
+__global__ void __launch_bounds__(NT) k_rs2_hist(const uint32_t* __restrict__ keys, const uint64_t* n_dev,
+                                                 uint64_t n_max, int shift, uint32_t* __restrict__ table,
+                                                 uint32_t ntiles) {
+    // wave-private histograms fed by match-any leaders (sorted inputs make
+    // LDS atomics on one bin serialise): no atomics at all
+    __shared__ uint32_t h[NWAVE][RS_RADIX];
+    const int t = threadIdx.x, w = t >> 6, ln = lane_id();
+#pragma unroll
+    for (int k = 0; k < NWAVE; ++k) h[k][t] = 0;
+    __syncthreads();
+    const uint64_t n = load_n(n_max, n_dev);
+    const uint64_t wbase = (uint64_t)blockIdx.x * RS2_TILE + (uint64_t)w * RS2_WAVE_KEYS;
+    uint32_t key[RS2_CHUNKS];
+#pragma unroll
+    for (int c = 0; c < RS2_CHUNKS; ++c) {
+        const uint64_t i = wbase + (uint64_t)c * 64 + ln;
+        key[c] = i < n ? keys[i] : 0u;
+    }
+    uint32_t* hw = h[w];
+#pragma unroll
+    for (int c = 0; c < RS2_CHUNKS; ++c) {
+        const bool valid = wbase + (uint64_t)c * 64 + ln < n;
+        const uint32_t d = (key[c] >> shift) & 255u;
+        uint64_t peers = wave_ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = wave_ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t old = valid ? hw[d] : 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (valid && (peers & lanemask_lt()) == 0) hw[d] = old + (uint32_t)popc64(peers);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < NWAVE; ++k) tot += h[k][t];
+    table[(uint64_t)t * ntiles + blockIdx.x] = tot;
+}
+
+template <int TILE_ = RS2_TILE>
+__global__ void __launch_bounds__(NT) k_rs2_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                    gw_event* __restrict__ aos, uint32_t aos_mask,
+                                                    const uint64_t* n_dev, uint64_t n_max, int shift,
+                                                    const uint32_t* __restrict__ table, uint32_t ntiles) {
+    __shared__ uint32_t whist[NWAVE][RS_RADIX];
+    __shared__ uint32_t tstart[RS_RADIX], gbase[RS_RADIX], red[NWAVE];
+    __shared__ uint32_t sk[RS2_TILE], sv[RS2_TILE];
+    const uint64_t n = load_n(n_max, n_dev);
+    const uint64_t base = (uint64_t)blockIdx.x * RS2_TILE;
+    if (base >= n) return;                                   // block-uniform
+    const int t = threadIdx.x, w = t >> 6, ln = lane_id();
+    const uint64_t lt = lanemask_lt();
+#pragma unroll
+    for (int k = 0; k < NWAVE; ++k) whist[k][t] = 0;
+    gbase[t] = table[(uint64_t)t * ntiles + blockIdx.x];
+    __syncthreads();
+    uint32_t key[RS2_CHUNKS], val[RS2_CHUNKS], rk[RS2_CHUNKS];
+    const uint64_t wbase = base + (uint64_t)w * RS2_WAVE_KEYS;
+#pragma unroll
+    for (int c = 0; c < RS2_CHUNKS; ++c) {                   // loads first: all in flight together
+        const uint64_t i = wbase + (uint64_t)c * 64 + ln;
+        key[c] = i < n ? kin[i] : 0u;
+        val[c] = i < n ? vin[i] : 0u;
+    }
+    uint32_t* hw = whist[w];
+#pragma unroll
+    for (int c = 0; c < RS2_CHUNKS; ++c) {
+        const uint64_t i = wbase + (uint64_t)c * 64 + ln;
+        const bool valid = i < n;
+        const uint32_t d = (key[c] >> shift) & 255u;
+        uint64_t peers = wave_ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = wave_ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t r = (uint32_t)popc64(peers & lt);
+        const uint32_t old = valid ? hw[d] : 0u;             // same-digit lanes read the same count
+        __builtin_amdgcn_wave_barrier();
+        if (valid && r == 0) hw[d] = old + (uint32_t)popc64(peers);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        rk[c] = valid ? old + r : 0xffffffffu;
+    }
+    __syncthreads();
+    {   // thread t = digit t: prefix over the waves, then the tile's digit starts
+        uint32_t run = 0;
+#pragma unroll
+        for (int k = 0; k < NWAVE; ++k) { const uint32_t v = whist[k][t]; whist[k][t] = run; run += v; }
+        uint32_t tot;
+        const uint32_t pre = block_excl_scan<uint32_t>(run, red, tot);
+        tstart[t] = pre;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < RS2_CHUNKS; ++c) {
+        if (rk[c] == 0xffffffffu) continue;
+        const uint32_t d = (key[c] >> shift) & 255u;
+        const uint32_t pos = tstart[d] + hw[d] + rk[c];
+        sk[pos] = key[c];
+        sv[pos] = val[c];
+    }
+    __syncthreads();
+    const uint32_t tn = (uint32_t)min<uint64_t>((uint64_t)RS2_TILE, n - base);
+    for (uint32_t i = t; i < tn; i += NT) {                  // each digit's run of the tile is contiguous
+        const uint32_t k = sk[i], v = sv[i];
+        const uint32_t d = (k >> shift) & 255u;
+        const uint32_t dst = gbase[d] + (i - tstart[d]);
+        if (aos) {
+            gw_event e;
+            e.watcher = k & aos_mask;
+            e.target = v;
+            aos[dst] = e;
+        } else {
+            kout[dst] = k;
+            vout[dst] = v;
+        }
+    }
+}
+
+inline uint64_t radix2_tiles(uint64_t n_max) { return (n_max + RS2_TILE - 1) / RS2_TILE; }
+
+// Sorts (k0,v0) by bits [lo_bit, hi_bit) with (k1,v1) as ping-pong; table holds
+// 256 * radix2_tiles(n_max) words.  With aos, the last pass writes gw_event
+// {key & aos_mask, value} there (and the return value is meaningless).
+// Returns 0 if the result is in (k0,v0), 1 if in (k1,v1).
+inline int radix_sort2(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
+                       int lo_bit, int hi_bit, uint32_t* table, ScanCtx& sc, hipStream_t st,
+                       gw_event* aos = nullptr, uint32_t aos_mask = 0xffffffffu) {
+    const uint32_t nt = (uint32_t)radix2_tiles(n_max);
+    if (nt == 0) return 0;
+    int cur = 0;
+    for (int shift = lo_bit; shift < hi_bit; shift += 8) {
+        const bool last = shift + 8 >= hi_bit;
+        uint32_t* ki = cur ? k1 : k0; uint32_t* ko = cur ? k0 : k1;
+        uint32_t* vi = cur ? v1 : v0; uint32_t* vo = cur ? v0 : v1;
+        hipLaunchKernelGGL(k_rs2_hist<>, dim3(nt), dim3(NT), 0, st, ki, n_dev, n_max, shift, table, nt);
+        scan_exclusive<uint32_t, uint32_t>(table, table, (uint64_t)RS_RADIX * nt, nullptr, sc, (uint32_t*)nullptr, st);
+        hipLaunchKernelGGL(k_rs2_scatter<>, dim3(nt), dim3(NT), 0, st, ki, vi, ko, vo, last ? aos : nullptr, aos_mask,
+                           n_dev, n_max, shift, table, nt);
+        cur ^= 1;
+    }
+    return cur;
+}
+
 }  // namespace gw

@@ -172,6 +172,13 @@ def _p(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
 
 
+def _host_view(ptr, n: int, dtype) -> np.ndarray:
+    """A numpy view (no copy) of n records at a library-owned host pointer."""
+    if not n or not ptr:
+        return np.zeros(0, dtype)
+    return np.frombuffer((C.c_uint8 * (n * dtype.itemsize)).from_address(ptr), dtype=dtype)
+
+
 @dataclasses.dataclass
 class TickResult:
     enter: np.ndarray | None
@@ -301,13 +308,19 @@ class GpuAOI:
         g = np.ascontiguousarray(gates, dtype=np.uint16)
         self._chk(lib().gw_set_clients(self._h, _p(s), _p(g), len(s)))
 
-    def tick(self, copy: bool = True, no_events: bool = False, defer: bool = False) -> TickResult:
+    def tick(self, copy: bool = True, no_events: bool = False, defer: bool = False, view: bool = False) -> TickResult:
         """defer (device-resident ops, copy=False): launch without a host sync;
-        the result holds only `ops` until tick_result() (or the next collect)."""
+        the result holds only `ops` until tick_result() (or the next collect).
+        view (with copy): the event arrays are views of the library's pinned
+        host buffers (valid until the next tick), as a Go caller reads them."""
         o = TickOut()
         fl = (TICK_COPY_TO_HOST if copy else 0) | (TICK_NO_EVENTS if no_events else 0) | \
             (TICK_DEFER if defer and not copy else 0)
         self._chk(lib().gw_tick(self._h, fl, C.byref(o)))
+        if view and copy and not no_events:
+            return TickResult(_host_view(o.enter, o.n_enter, EVENT_DTYPE), _host_view(o.leave, o.n_leave, EVENT_DTYPE),
+                              o.n_enter, o.n_leave, o.ops, o.movers, o.pairs_tested, o.nbr_old, o.nbr_new,
+                              o.bytes_alg, o.device_us, o.enter_dev or 0, o.leave_dev or 0)
         return self._tick_result(o, copy, no_events)
 
     def tick_result(self) -> TickResult:
@@ -328,14 +341,17 @@ class GpuAOI:
         return TickResult(e, l, o.n_enter, o.n_leave, o.ops, o.movers, o.pairs_tested, o.nbr_old,
                           o.nbr_new, o.bytes_alg, o.device_us, o.enter_dev or 0, o.leave_dev or 0)
 
-    def sync_collect(self, copy: bool = True, by_client: bool = False) -> SyncResult:
+    def sync_collect(self, copy: bool = True, by_client: bool = False, view: bool = False) -> SyncResult:
         """by_client: records grouped per client inside each gate (the gate's
-        regroup, GateService.go:350-375), with the client segment table."""
+        regroup, GateService.go:350-375), with the client segment table.
+        view (with copy): records are a view of the pinned host buffer."""
         o = SyncOut()
         fl = (SYNC_COPY_TO_HOST if copy else 0) | (SYNC_BY_CLIENT if by_client else 0)
         self._chk(lib().gw_sync_collect(self._h, fl, C.byref(o)))
         r = None
-        if copy:
+        if copy and view:
+            r = _host_view(o.rec, o.n_rec, REC_DTYPE)
+        elif copy:
             r = np.zeros(o.n_rec, REC_DTYPE)
             if o.n_rec:
                 C.memmove(_p(r), o.rec, o.n_rec * 24)

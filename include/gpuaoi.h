@@ -141,12 +141,9 @@ typedef struct gw_tick_out {
                                       packet MT_SYNC_POSITION_YAW_ON_CLIENTS   */
 
 typedef struct gw_sync_out {
-    /* Deterministic order.  Default: grouped by gate(watcher) (gate_off), and
-     * inside a gate by entity ascending; an entity's own-client record comes
-     * first, then its neighbours' records in grid order: (cell of the
-     * watcher's position, watcher slot) - the order the window walk visits
-     * them.  Only the gate grouping is a sort.  With GW_SYNC_BY_CLIENT: the
-     * canonical (gate(watcher), watcher, entity) order of SURVEY App. B.5,
+    /* Canonical order: sorted by (gate(watcher), entity, watcher), gate_off
+     * partitioning the stream by gate id (each gate's packet one slice); with
+     * GW_SYNC_BY_CLIENT by (gate(watcher), watcher, entity),
      * each client's records one contiguous segment (client_off).            */
     const gw_sync_record* rec;      /* host pointer (NULL unless COPY_TO_HOST) */
     const gw_sync_record* rec_dev;  /* device pointer, always valid            */

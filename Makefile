@@ -6,10 +6,10 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-f
 LIBDIR   := goworld_amd/lib
 CSRC     := goworld_amd/csrc
 HDR      := $(CSRC)/prim.hpp $(CSRC)/gw_internal.hpp $(CSRC)/dev_common.hpp $(CSRC)/ctx.hpp include/gpuaoi.h
-OBJ      := $(LIBDIR)/aoi.o $(LIBDIR)/sync.o $(LIBDIR)/halo.o $(LIBDIR)/capi.o $(LIBDIR)/world.o
+OBJ      := $(LIBDIR)/aoi.o $(LIBDIR)/sync.o $(LIBDIR)/halo.o $(LIBDIR)/capi.o $(LIBDIR)/world.o $(LIBDIR)/wire.o
 ROCM     ?= /opt/rocm
 
-all: $(LIBDIR)/libgpuaoi.so oracle
+all: $(LIBDIR)/libgpuaoi.so $(LIBDIR)/c_harness oracle
 
 $(LIBDIR)/%.o: $(CSRC)/%.hip $(HDR)
 	@mkdir -p $(LIBDIR)
@@ -21,6 +21,10 @@ $(LIBDIR)/%.o: $(CSRC)/%.cpp $(HDR)
 
 $(LIBDIR)/libgpuaoi.so: $(OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+
+# plain-C caller of the ABI (tests/test_c_harness.py): gcc, no HIP headers
+$(LIBDIR)/c_harness: tests/c_harness.c include/gpuaoi.h $(LIBDIR)/libgpuaoi.so
+	gcc -O2 -std=c99 -Wall -Iinclude -o $@ tests/c_harness.c -L$(LIBDIR) -lgpuaoi -Wl,-rpath,'$$ORIGIN'
 
 oracle:
 	$(MAKE) -s -C oracle

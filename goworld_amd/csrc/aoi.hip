@@ -752,13 +752,21 @@ __global__ void __launch_bounds__(NT) k_mover_counts(TickBufs b) {
 
 // (3) the listed movers' events flattened at their scanned offsets, in list
 // (slot) order: own events (watcher A, target-sorted), then the mirror events
-// (watcher W, target A).  Keys carry the leave bit above the slot bits.  A
-// lane per mover (64 movers per wave; K ~ 40 gives a few events each), movers
-// with more than FLAT_LANE events afterwards by the whole wave.
-constexpr uint32_t FLAT_LANE = 32;
-__device__ __forceinline__ void flat_put(const TickBufs& b, uint64_t at, uint32_t key, uint32_t val) {
-    b.fk0[at] = key;
-    b.fv0[at] = val;
+// (watcher W, target A).  Keys carry the leave bit above the slot bits.  One
+// wave per 64 output positions (every wave independent): chunk_first[c] is
+// the mover whose events hold position 64c; lane i loads mover first + i, and
+// lane p finds its mover by a binary search over those movers' ends (7
+// shuffles), so loads and stores are runs of consecutive addresses whatever
+// the per-mover counts.
+__global__ void __launch_bounds__(NT) k_chunk_first(TickBufs b) {
+    const uint64_t k = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= b.st->n_mlist) return;
+    if (lo32(b.st->ev_pk) + hi32(b.st->ev_pk) > b.ev_cap) return;   // overflow: nothing is flattened (redo)
+    const uint64_t off = b.moff[k];
+    const uint64_t at = lo32(off) + hi32(off);
+    const uint4 mi = b.minfo[k];
+    const uint64_t end = at + mi.y + mi.z;
+    for (uint64_t c = (at + 63) >> 6; (c << 6) < end; ++c) b.chunk_first[c] = (uint32_t)k;
 }
 __global__ void __launch_bounds__(NT) k_flatten(TickBufs b) {
     const uint64_t nl_ = b.st->n_mlist;
@@ -769,51 +777,52 @@ __global__ void __launch_bounds__(NT) k_flatten(TickBufs b) {
         b.st->n_sort = E > b.ev_cap ? 0 : E;              // nothing is sorted on overflow (the host redoes)
     }
     if (E > b.ev_cap) return;
-    const uint64_t k0 = ((uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6)) * 64;
-    if (k0 >= nl_) return;
-    const uint64_t k = k0 + ln;
-    const bool valid = k < nl_;
+    const uint64_t c = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
+    if ((c << 6) >= E) return;
+    const uint32_t q0 = b.chunk_first[c];
+    const uint64_t k = (uint64_t)q0 + ln;
+    uint64_t at = ~0ull, end = ~0ull, reg = 0;
     uint4 mi = make_uint4(0, 0, 0, 0);
-    uint64_t at = 0, reg = 0;
-    if (valid) {
-        mi = b.minfo[k];
+    if (k < nl_) {
         const uint64_t off = b.moff[k];
-        at = lo32(off) + hi32(off);
+        mi = b.minfo[k];
         reg = b.mreg[k];
+        at = lo32(off) + hi32(off);
+        end = at + mi.y + mi.z;
     }
+    const uint64_t p = (c << 6) + ln;
+    // first lane q whose mover ends after p (ends ascend with the lane)
+    uint32_t lo = 0, hi = 64;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {                           // [lo, hi) of 64 closes in 7 halvings
+        const uint32_t mid = min((lo + hi) >> 1, 63u);
+        const uint64_t e = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(end >> 32), (int)mid, 64) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)end, (int)mid, 64);
+        if (lo < hi) {
+            if (e <= p) lo = mid + 1; else hi = mid;
+        }
+    }
+    const int q = (int)min(lo, 63u);
+    const uint64_t qat = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(at >> 32), q, 64) << 32) |
+                         (uint32_t)__shfl((int)(uint32_t)at, q, 64);
+    const uint64_t qreg = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(reg >> 32), q, 64) << 32) |
+                          (uint32_t)__shfl((int)(uint32_t)reg, q, 64);
+    const uint32_t qA = (uint32_t)__shfl((int)mi.x, q, 64), qn = (uint32_t)__shfl((int)mi.y, q, 64);
+    if (p >= E) return;
+    const uint32_t j = (uint32_t)(p - qat);                 // index inside mover q's events
     const uint32_t lvb = 1u << b.wbits;
-    const uint32_t A = mi.x, n = mi.y, nm = mi.z;
-    const bool small = n + nm <= FLAT_LANE;
-    if (valid && small) {
-        for (uint32_t j = 0; j < n; ++j) {
-            const uint32_t e = b.own[reg + j];
-            flat_put(b, at + j, ((e & 1u) ? lvb : 0u) | A, e >> 1);
-        }
-        for (uint32_t j = 0; j < nm; ++j) {
-            const uint64_t e = b.mir[reg + j];
-            flat_put(b, at + n + j, ((e & 1u) ? lvb : 0u) | (uint32_t)hi32(e), (uint32_t)(lo32(e) >> 1));
-        }
+    uint32_t key, val;
+    if (j < qn) {
+        const uint32_t e = b.own[qreg + j];
+        key = ((e & 1u) ? lvb : 0u) | qA;
+        val = e >> 1;
+    } else {
+        const uint64_t e = b.mir[qreg + (j - qn)];
+        key = ((e & 1u) ? lvb : 0u) | (uint32_t)hi32(e);
+        val = (uint32_t)(lo32(e) >> 1);
     }
-    uint64_t bigm = wave_ballot(valid && !small);
-    while (bigm) {                                          // the whole wave per large mover
-        const int q = __builtin_ctzll(bigm);
-        bigm &= bigm - 1;
-        const uint32_t qA = (uint32_t)__builtin_amdgcn_readlane((int)A, q);
-        const uint32_t qn = (uint32_t)__builtin_amdgcn_readlane((int)n, q);
-        const uint32_t qm = (uint32_t)__builtin_amdgcn_readlane((int)nm, q);
-        const uint64_t qat = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(at >> 32), q) << 32) |
-                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)at, q);
-        const uint64_t qreg = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(reg >> 32), q) << 32) |
-                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)reg, q);
-        for (uint32_t j = ln; j < qn; j += 64) {
-            const uint32_t e = b.own[qreg + j];
-            flat_put(b, qat + j, ((e & 1u) ? lvb : 0u) | qA, e >> 1);
-        }
-        for (uint32_t j = ln; j < qm; j += 64) {
-            const uint64_t e = b.mir[qreg + j];
-            flat_put(b, qat + qn + j, ((e & 1u) ? lvb : 0u) | (uint32_t)hi32(e), (uint32_t)(lo32(e) >> 1));
-        }
-    }
+    b.fk0[p] = key;
+    b.fv0[p] = val;
 }
 
 void tick_diff(const TickBufs& b, hipStream_t s) {
@@ -844,10 +853,11 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     hipLaunchKernelGGL(k_mover_counts, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
     scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.mcnt, (uint64_t*)b.moff, b.m, nml, sc,
                                        (uint64_t*)&b.st->ev_pk, s);
-    hipLaunchKernelGGL(k_flatten, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_chunk_first, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_flatten, dim3(nblk1((b.ev_cap + 63) / 64, NWAVE)), dim3(NT), 0, s, b);
     // one stable sort by (leave, watcher); the last pass writes gw_event
-    radix_sort2(b.fk0, b.fv0, b.fk1, b.fv1, b.ev_cap, (const uint64_t*)&b.st->n_sort, 0, b.wbits + 1, b.rtable, sc,
-                s, b.ev, (1u << b.wbits) - 1u);
+    radix_sort2(b.fk0, b.fv0, b.fk1, b.fv1, b.ev_cap, (const uint64_t*)&b.st->n_sort, 0, b.wbits + 1, b.rtable, s,
+                b.ev, (1u << b.wbits) - 1u);
     (void)nmax;
 }
 

@@ -203,6 +203,8 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->nbc, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->movbit, 0, (size_t)nc / 32 + 1))) return rc;
     if ((rc = grow_preserve(c, c->gmi, 0, (size_t)nc))) return rc;
+    if ((rc = grow_preserve(c, c->eid_dev, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->cid_dev, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_pos, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_aoi, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->last_leave, oc, nc))) return rc;
@@ -221,6 +223,8 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     HIPCHK(hipMemsetAsync(c->gate + oc, 0, n * 2, c->st));
     HIPCHK(hipMemsetAsync(c->nbc + oc, 0, n * 8, c->st));
     HIPCHK(hipMemsetAsync(c->movbit, 0, ((size_t)nc / 32 + 1) * 4, c->st));
+    HIPCHK(hipMemsetAsync(c->eid_dev + oc, 0, n * 16, c->st));
+    HIPCHK(hipMemsetAsync(c->cid_dev + oc, 0, n * 16, c->st));
     launch_fill_i32(c->last_pos + oc, -1, n, c->st);
     launch_fill_i32(c->last_aoi + oc, -1, n, c->st);
     launch_fill_i32(c->last_leave + oc, -1, n, c->st);
@@ -228,6 +232,8 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     HIPCHK(hipStreamSynchronize(c->st));
     c->slot_cap = nc;
     c->present_h.resize(nc, 0);
+    c->eid_h.resize(nc, gw::host::Id16{0, 0});
+    c->syncing_h.resize(nc, 0);
     c->space_of_h.resize(nc, -1);
     c->grid_dirty = true;
     return 0;
@@ -445,14 +451,18 @@ void gw_shutdown(gw_ctx* c) {
     if (c->st) (void)hipStreamSynchronize(c->st);
     DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1,
                       &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
-                      &c->mcnt, &c->moff, &c->minfo, &c->mreg, &c->fk0, &c->fv0, &c->fk1, &c->fv1, &c->ev_d, &c->rtable,
+                      &c->mcnt, &c->moff, &c->minfo, &c->mreg, &c->chunk_first, &c->fk0, &c->fv0, &c->fk1, &c->fv1, &c->ev_d, &c->rtable,
                       &c->scan_status, &c->rs_hist,
-                      &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec_big, &c->rec0, &c->rec1,
+                      &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
                       &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf, &c->cl_slot, &c->cl_off,
                       &c->m_create.a, &c->m_create.b, &c->m_destroy.a, &c->m_destroy.b, &c->m_fanout.a,
                       &c->m_fanout.b, &c->m_flag, &c->m_at, &c->m_items, &c->m_cnt, &c->m_off};
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
-    DevBuf* wb[] = {&c->wd.stamps, &c->wd.send[0], &c->wd.send[1], &c->wd.recv[0], &c->wd.recv[1], &c->wd.cnt};
+    DevBuf* wb[] = {&c->wd.stamps, &c->wd.send[0], &c->wd.send[1], &c->wd.recv[0], &c->wd.recv[1], &c->wd.cnt,
+                    &c->wire_d, &c->wire_tab, &c->id_up};
+    if (c->wire_h.p) (void)hipHostFree(c->wire_h.p);
+    if (c->eid_dev) (void)hipFree(c->eid_dev);
+    if (c->cid_dev) (void)hipFree(c->cid_dev);
     for (DevBuf* b : wb) if (b->p) (void)hipFree(b->p);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off, &c->m_create.h,
@@ -685,12 +695,12 @@ int gw_set_clients(gw_ctx* c, const uint32_t* slots, const uint16_t* gates, uint
 
 static int ensure_events(gw_ctx* c) {
     int r;
-    const uint64_t tiles = (c->ev_cap + radix2_tile() - 1) / radix2_tile() + 1;
     if ((r = ensure(c, c->own, c->own_cap * 4)) || (r = ensure(c, c->mir, c->own_cap * 8)) ||
         (r = ensure(c, c->fk0, c->ev_cap * 4)) || (r = ensure(c, c->fv0, c->ev_cap * 4)) ||
         (r = ensure(c, c->fk1, c->ev_cap * 4)) || (r = ensure(c, c->fv1, c->ev_cap * 4)) ||
-        (r = ensure(c, c->ev_d, c->ev_cap * sizeof(gw_event))) || (r = ensure(c, c->rtable, tiles * 256 * 4)) ||
-        (r = ensure_scan(c, tiles * 256)))
+        (r = ensure(c, c->ev_d, c->ev_cap * sizeof(gw_event))) ||
+        (r = ensure(c, c->chunk_first, (c->ev_cap / 64 + 1) * 4)) ||
+        (r = ensure(c, c->rtable, radix2_scratch(c->ev_cap) * 4 + 64)))
         return r;
     return 0;
 }
@@ -701,6 +711,7 @@ static void bind_events(gw_ctx* c, TickBufs& b) {
     b.fk0 = P<uint32_t>(c->fk0); b.fv0 = P<uint32_t>(c->fv0);
     b.fk1 = P<uint32_t>(c->fk1); b.fv1 = P<uint32_t>(c->fv1);
     b.ev = P<gw_event>(c->ev_d);
+    b.chunk_first = P<uint32_t>(c->chunk_first);
     b.ev_cap = c->ev_cap;
     b.rtable = P<uint32_t>(c->rtable);
 }
@@ -992,7 +1003,6 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     DevStats* st = c->cstats;
     if ((rc = ensure(c, c->fbits, (size_t)C * 4)) || (rc = ensure(c, c->flagged, (size_t)C * 4)) ||
         (rc = ensure(c, c->rec_cnt, (size_t)C * 4)) || (rc = ensure(c, c->rec_off, (size_t)C * 8)) ||
-        (rc = ensure(c, c->rec_big, (size_t)C * 4)) ||
         (rc = ensure_scan(c, C)))
         return rc;
     // records land in a buffer sized from the last collect; if it was too
@@ -1012,8 +1022,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     size_t s_count = prof_end(c, 0);
     prof_begin(c, "sync_write");
     launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint64_t>(c->rec_off),
-                      P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, P<uint32_t>(c->rec_big),
-                      c->st);
+                      P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
     size_t s_write = prof_end(c, 0);
     HIPCHK(hipGetLastError());
     if ((rc = read_cstats(c))) return rc;                // the one host sync
@@ -1025,11 +1034,8 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         if ((rc = ensure(c, c->rec0, c->rec_cap * sizeof(gw_sync_record)))) return rc;
         c->hcstats->overflow = 0;
         HIPCHK(hipMemcpyAsync(c->cstats, c->hcstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
-        c->hcstats->n_big = 0;
-        HIPCHK(hipMemcpyAsync(c->cstats, c->hcstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
         launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint64_t>(c->rec_off),
-                          P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st,
-                          P<uint32_t>(c->rec_big), c->st);
+                          P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
         HIPCHK(hipGetLastError());
         if ((rc = read_cstats(c))) return rc;
         if (c->hcstats->overflow) return set_err(c, GW_ENOMEM, "sync record buffer overflowed twice");
@@ -1129,6 +1135,8 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     }
     out->flagged = NF;
     out->rec_dev = recs;
+    c->last_rec = recs;
+    c->last_R = R;
     out->gate_off = c->gate_off.data();
     out->n_gates = G;
     out->bytes_alg = 24ull * R;

@@ -5,7 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "gw_internal.hpp"
@@ -56,6 +58,23 @@ struct WorldHost {
     uint32_t n_ops = 0;
     bool routed = false;
 };
+
+// a 16-byte EntityID as a hash-map key
+struct Id16 {
+    uint64_t a, b;
+    bool operator==(const Id16& o) const { return a == o.a && b == o.b; }
+};
+struct Id16Hash {
+    size_t operator()(const Id16& k) const {
+        uint64_t h = k.a * 0x9E3779B97F4A7C15ull ^ (k.b + 0x632BE59BD9B4E019ull + (k.a << 6) + (k.a >> 2));
+        return (size_t)(h ^ (h >> 29));
+    }
+};
+inline Id16 id16(const void* p) {
+    Id16 k;
+    memcpy(&k, p, 16);
+    return k;
+}
 
 }  // namespace host
 }  // namespace gw
@@ -131,12 +150,12 @@ struct gw_ctx {
 
     // grid + tick scratch
     DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, cand, reg, own, big, mstat;
-    DevBuf mir, ownc, mirc, mlist, mcnt, moff, minfo, mreg, fk0, fv0, fk1, fv1, ev_d, rtable;
+    DevBuf mir, ownc, mirc, mlist, mcnt, moff, minfo, mreg, chunk_first, fk0, fv0, fk1, fv1, ev_d, rtable;
     DevBuf scan_status, rs_hist;
     uint64_t ev_cap = 0;                 // events the flatten/sort buffers hold (grows on overflow)
     ScanCtx sc{};                  // single-pass scan state (prim.hpp)
     // sync / query scratch
-    DevBuf fbits, flagged, rec_cnt, rec_off, rec_big, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
+    DevBuf fbits, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
     DevBuf cl_slot, cl_off, h_cl_slot, h_cl_off;   // GW_SYNC_BY_CLIENT segments (device / pinned host)
     uint64_t rec_cap = 0;                // records the rec0 buffer holds (grows on overflow)
     // client messages (gw_client_events, gw_fanout): ping-pong + pinned host + gate offsets
@@ -167,6 +186,18 @@ struct gw_ctx {
     size_t nstage = 0;
     hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
     gw_stage_times last_times{};
+
+    // ids, client-sync decode, wire encode (wire.cpp)
+    std::unordered_map<gw::host::Id16, uint32_t, gw::host::Id16Hash> id_slot;   // entity id -> slot
+    std::vector<gw::host::Id16> eid_h;       // [slot_cap] entity id of a slot (zero = none)
+    std::vector<uint8_t> syncing_h;          // [slot_cap] SetClientSyncing
+    uint4* eid_dev = nullptr;                // [slot_cap] 16-B entity ids
+    uint4* cid_dev = nullptr;                // [slot_cap] 16-B client ids
+    const gw_sync_record* last_rec = nullptr;   // records of the last collect (device)
+    uint64_t last_R = 0;
+    DevBuf wire_d, wire_h, wire_tab, id_up;
+    std::vector<uint16_t> wire_gate;
+    std::vector<uint64_t> wire_off;
 
     // RCCL communicator and decomposed world (world.cpp)
     ncclComm_t comm = nullptr;

@@ -113,6 +113,7 @@ struct RadixTmp {
 };
 uint64_t radix_tile();            // keys per radix block
 uint64_t radix2_tile();           // keys per tile of radix_sort2
+uint64_t radix2_scratch(uint64_t n_max);   // u32 scratch words of radix_sort2
 uint64_t scan_tile();             // elements per scan tile
 uint64_t scan_words();            // status words per scan tile
 void scan_u32_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
@@ -186,10 +187,11 @@ struct TickBufs {
     unsigned long long* moff; // [m] exclusive scan of mcnt
     uint4* minfo;             // [m] listed mover: slot, own events, mirror events
     unsigned long long* mreg; // [m] its region offset
+    uint32_t* chunk_first;    // [ev_cap / 64] listed mover holding flat position 64c
     uint32_t *fk0, *fv0, *fk1, *fv1;   // [ev_cap] flattened events: key leave<<wbits | watcher, value target
     gw_event* ev;             // [ev_cap] canonical events, enters then leaves
     uint64_t ev_cap;
-    uint32_t* rtable;         // radix digit table (256 per tile)
+    uint32_t* rtable;         // radix_sort2 scratch
     int wbits;                // bits of a slot
     int diff_u;               // candidate chunks of 64 in flight per k_mover iteration
 };
@@ -216,7 +218,7 @@ void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* 
                        uint32_t nf_max, uint32_t* cnt, hipStream_t s);
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
-                       uint64_t rec_cap, DevStats* st, uint32_t* big, hipStream_t s);
+                       uint64_t rec_cap, DevStats* st, hipStream_t s);
 void launch_gate_hist(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,
                       uint32_t* hist /*65536*/, hipStream_t s);
 void launch_gate_keys(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,
@@ -268,6 +270,15 @@ void launch_msg_gate_hist(const uint32_t* rec, int words, uint64_t n, const uint
 void launch_msg_gather(const uint32_t* in, int words, const uint32_t* idx, uint64_t n, uint32_t* out,
                        hipStream_t s);
 void launch_fill_u32(uint32_t* p, uint32_t v, uint64_t n, hipStream_t s);
+// ids and the wire encode (sync.hip)
+void launch_put16(uint4* table, const uint32_t* slots, const uint4* vals, uint32_t n, hipStream_t s);
+struct WirePacket {              // one gate's packet of the wire encode
+    uint64_t rec0, nrec;         // its records in the collect's stream
+    uint64_t byte_off;           // packet offset in the output
+    uint32_t gate, pad;
+};
+void launch_wire_encode(const gw_sync_record* rec, uint64_t R, const WirePacket* pk, uint32_t npk,
+                        const uint4* eid, const uint4* cid, uint32_t* out, hipStream_t s);
 void launch_fill_i32(int32_t* p, int32_t v, uint64_t n, hipStream_t s);
 
 }  // namespace gw

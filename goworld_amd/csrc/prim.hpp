@@ -394,84 +394,103 @@ inline int radix_sort(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n_max, 
 }
 
 // ---------------------------------------------------------------------------
-// Stable LSD radix sort of (u32 key, u32 value) pairs, 8-bit digits, tiles of
-// 4096 pairs with LDS-staged coalesced scatter.  Per pass: an upsweep writes
-// the per-tile digit counts (digit-major table), one device scan turns them
-// into global offsets, and the downsweep ranks the tile in LDS and writes each
-// digit's run of the tile contiguously.  Ranking is wave-private (no barrier
-// inside the loop): wave w owns the tile's w-th quarter in input order, ranks
-// each 64-key chunk by match-any over the 8 digit bits (8 ballots) against a
-// wave-private LDS histogram; the waves' counts are then prefix-summed per
-// digit, so the order within a digit is the input order (stable).  The last
-// pass may write gw_event {key & mask, value} instead of the two arrays.
-constexpr int RS2_IPT = 16;
-constexpr int RS2_TILE = NT * RS2_IPT;              // 4096
-constexpr int RS2_WAVE_KEYS = RS2_TILE / NWAVE;     // 1024 per wave
-constexpr int RS2_CHUNKS = RS2_WAVE_KEYS / 64;      // 16
+// Stable LSD radix sort of (u32 key, u32 value) pairs, 8-bit digits, ONE kernel
+// per pass ("onesweep"): the digit counts of every pass are order-independent,
+// so one upfront pass over the keys gives each pass's global digit bases; a
+// pass then ranks its 4096-pair tile in LDS, publishes the tile's per-digit
+// counts and gets the counts of all earlier tiles by a decoupled look-back per
+// digit (thread d follows digit d back through the tiles' status words until
+// an inclusive prefix; tiles take tickets in dispatch order, so every tile it
+// waits on is running), and writes each digit's run of the tile contiguously
+// from LDS.  Ranking is wave-private (no barrier inside the loop): wave w owns
+// the tile's w-th quarter in input order and ranks each 64-key chunk by
+// match-any over the 8 digit bits (8 ballots) against a wave-private LDS
+// histogram; the waves' counts are then prefix-summed per digit, so the order
+// within a digit is the input order (stable).  The last pass may write
+// gw_event {key & mask, value} instead of the two arrays.
+constexpr int RS2_NT = 512;                          // 8 waves per tile: short serial ranking loops
+constexpr int RS2_NW = RS2_NT / 64;
+constexpr int RS2_TILE = 4096;
+constexpr int RS2_WAVE_KEYS = RS2_TILE / RS2_NW;     // 512 per wave
+constexpr int RS2_CHUNKS = RS2_WAVE_KEYS / 64;      // 8
+constexpr int RS2_MAX_PASSES = 4;
+constexpr int RS2_GBLOCKS = 256;                    // blocks of the upfront histogram
+constexpr uint32_t OS_AGG = 1u << 30, OS_INC = 2u << 30, OS_VAL = (1u << 30) - 1;
 
-template <int TILE_ = RS2_TILE>   // a template: the header is included by several translation units
-__global__ void __launch_bounds__(NT) k_rs2_hist(const uint32_t* __restrict__ keys, const uint64_t* n_dev,
-                                                 uint64_t n_max, int shift, uint32_t* __restrict__ table,
-                                                 uint32_t ntiles) {
-    // wave-private histograms fed by match-any leaders (sorted inputs make
-    // LDS atomics on one bin serialise): no atomics at all
-    __shared__ uint32_t h[NWAVE][RS_RADIX];
-    const int t = threadIdx.x, w = t >> 6, ln = lane_id();
+// per-block digit counts of every pass (wave-private LDS copies: the top
+// digit of a key has few distinct values, so one shared copy would serialise
+// its bins' atomics; grid-stride)
+template <int TILE_ = RS2_TILE>   // templates: the header is included by several translation units
+__global__ void __launch_bounds__(NT) k_os_hist(const uint32_t* __restrict__ keys, const uint64_t* n_dev,
+                                                uint64_t n_max, int lo_bit, int passes, uint32_t* __restrict__ part) {
+    __shared__ uint32_t h[NWAVE][RS2_MAX_PASSES][RS_RADIX];
+    const int w = threadIdx.x >> 6;
 #pragma unroll
-    for (int k = 0; k < NWAVE; ++k) h[k][t] = 0;
+    for (int q = 0; q < NWAVE; ++q)
+#pragma unroll
+        for (int p = 0; p < RS2_MAX_PASSES; ++p) h[q][p][threadIdx.x] = 0;
     __syncthreads();
     const uint64_t n = load_n(n_max, n_dev);
-    const uint64_t wbase = (uint64_t)blockIdx.x * RS2_TILE + (uint64_t)w * RS2_WAVE_KEYS;
-    uint32_t key[RS2_CHUNKS];
-#pragma unroll
-    for (int c = 0; c < RS2_CHUNKS; ++c) {
-        const uint64_t i = wbase + (uint64_t)c * 64 + ln;
-        key[c] = i < n ? keys[i] : 0u;
-    }
-    uint32_t* hw = h[w];
-#pragma unroll
-    for (int c = 0; c < RS2_CHUNKS; ++c) {
-        const bool valid = wbase + (uint64_t)c * 64 + ln < n;
-        const uint32_t d = (key[c] >> shift) & 255u;
-        uint64_t peers = wave_ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bb = wave_ballot(bit);
-            peers &= bit ? bb : ~bb;
-        }
-        const uint32_t old = valid ? hw[d] : 0u;
-        __builtin_amdgcn_wave_barrier();
-        if (valid && (peers & lanemask_lt()) == 0) hw[d] = old + (uint32_t)popc64(peers);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * NT) {
+        const uint32_t k = keys[i];
+        for (int p = 0; p < passes; ++p) atomicAdd(&h[w][p][(k >> (lo_bit + 8 * p)) & 255u], 1u);
     }
     __syncthreads();
+    for (int p = 0; p < passes; ++p) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < NWAVE; ++q) v += h[q][p][threadIdx.x];
+        part[((uint64_t)p * RS_RADIX + threadIdx.x) * gridDim.x + blockIdx.x] = v;
+    }
+}
+// global digit bases per pass: block p, thread d sums digit d over the
+// partial histograms (independent loads, batched), then an exclusive scan
+// over the digits
+template <int TILE_ = RS2_TILE>
+__global__ void __launch_bounds__(NT) k_os_bases(const uint32_t* __restrict__ part, uint32_t nblocks,
+                                                 uint32_t* __restrict__ gbase) {
+    __shared__ uint32_t red[NWAVE];
+    const uint32_t p = blockIdx.x, d = threadIdx.x;
+    const uint32_t* q = part + ((uint64_t)p * RS_RADIX + d) * nblocks;
+    uint32_t acc[16] = {};
+    for (uint32_t b = 0; b < nblocks; b += 16) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc[u] += (b + u < nblocks) ? q[b + u] : 0u;
+    }
     uint32_t tot = 0;
 #pragma unroll
-    for (int k = 0; k < NWAVE; ++k) tot += h[k][t];
-    table[(uint64_t)t * ntiles + blockIdx.x] = tot;
+    for (int u = 0; u < 16; ++u) tot += acc[u];
+    uint32_t all;
+    gbase[p * RS_RADIX + d] = block_excl_scan<uint32_t>(tot, red, all);
+}
+
+__device__ __forceinline__ uint32_t os_ld(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void os_st(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int TILE_ = RS2_TILE>
-__global__ void __launch_bounds__(NT) k_rs2_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+__global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                     gw_event* __restrict__ aos, uint32_t aos_mask,
                                                     const uint64_t* n_dev, uint64_t n_max, int shift,
-                                                    const uint32_t* __restrict__ table, uint32_t ntiles) {
-    __shared__ uint32_t whist[NWAVE][RS_RADIX];
-    __shared__ uint32_t tstart[RS_RADIX], gbase[RS_RADIX], red[NWAVE];
+                                                    const uint32_t* __restrict__ gbase, uint32_t* __restrict__ status,
+                                                    unsigned long long* __restrict__ ticket) {
+    __shared__ uint32_t whist[RS2_NW][RS_RADIX];
+    __shared__ uint32_t tstart[RS_RADIX], gofs[RS_RADIX], red[RS_RADIX / 64];
     __shared__ uint32_t sk[RS2_TILE], sv[RS2_TILE];
-    const uint64_t n = load_n(n_max, n_dev);
-    const uint64_t base = (uint64_t)blockIdx.x * RS2_TILE;
-    if (base >= n) return;                                   // block-uniform
+    __shared__ uint32_t s_tile;
     const int t = threadIdx.x, w = t >> 6, ln = lane_id();
-    const uint64_t lt = lanemask_lt();
-#pragma unroll
-    for (int k = 0; k < NWAVE; ++k) whist[k][t] = 0;
-    gbase[t] = table[(uint64_t)t * ntiles + blockIdx.x];
+    if (t == 0) s_tile = (uint32_t)atomicAdd(ticket, 1ull);
+    for (int i = t; i < RS2_NW * RS_RADIX; i += RS2_NT) (&whist[0][0])[i] = 0;
     __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t n = load_n(n_max, n_dev);
+    const uint64_t base = (uint64_t)tile * RS2_TILE;
+    if (base >= n) return;                                   // block-uniform; no later tile waits on it
+    const uint64_t lt = lanemask_lt();
     uint32_t key[RS2_CHUNKS], val[RS2_CHUNKS], rk[RS2_CHUNKS];
     const uint64_t wbase = base + (uint64_t)w * RS2_WAVE_KEYS;
 #pragma unroll
@@ -503,13 +522,32 @@ __global__ void __launch_bounds__(NT) k_rs2_scatter(const uint32_t* __restrict__
         rk[c] = valid ? old + r : 0xffffffffu;
     }
     __syncthreads();
-    {   // thread t = digit t: prefix over the waves, then the tile's digit starts
-        uint32_t run = 0;
+    uint32_t run = 0, inc = 0;
+    if (t < RS_RADIX) {
+        // thread t = digit t: prefix over the waves, then the tile's global
+        // offset for the digit by a look-back over earlier tiles
 #pragma unroll
-        for (int k = 0; k < NWAVE; ++k) { const uint32_t v = whist[k][t]; whist[k][t] = run; run += v; }
-        uint32_t tot;
-        const uint32_t pre = block_excl_scan<uint32_t>(run, red, tot);
-        tstart[t] = pre;
+        for (int k = 0; k < RS2_NW; ++k) { const uint32_t v = whist[k][t]; whist[k][t] = run; run += v; }
+        uint32_t* my = status + (uint64_t)tile * RS_RADIX + t;
+        os_st(my, (tile == 0 ? OS_INC : OS_AGG) | run);
+        uint32_t excl = 0;
+        for (int64_t j = (int64_t)tile - 1; j >= 0; --j) {
+            uint32_t v;
+            do { v = os_ld(status + (uint64_t)j * RS_RADIX + t); } while (!(v & (OS_AGG | OS_INC)));
+            excl += v & OS_VAL;
+            if (v & OS_INC) break;
+        }
+        if (tile) os_st(my, OS_INC | (excl + run));
+        gofs[t] = gbase[t] + excl;
+        inc = wave_incl_scan<uint32_t>(run);                 // the tile's digit starts: a scan over 256 digits
+        if (ln == 63) red[w] = inc;
+    }
+    __syncthreads();
+    if (t < RS_RADIX) {
+        uint32_t pre = 0;
+#pragma unroll
+        for (int k = 0; k < RS_RADIX / 64; ++k) pre += (k < w) ? red[k] : 0u;
+        tstart[t] = pre + inc - run;
     }
     __syncthreads();
 #pragma unroll
@@ -522,10 +560,10 @@ __global__ void __launch_bounds__(NT) k_rs2_scatter(const uint32_t* __restrict__
     }
     __syncthreads();
     const uint32_t tn = (uint32_t)min<uint64_t>((uint64_t)RS2_TILE, n - base);
-    for (uint32_t i = t; i < tn; i += NT) {                  // each digit's run of the tile is contiguous
+    for (uint32_t i = t; i < tn; i += RS2_NT) {              // each digit's run of the tile is contiguous
         const uint32_t k = sk[i], v = sv[i];
         const uint32_t d = (k >> shift) & 255u;
-        const uint32_t dst = gbase[d] + (i - tstart[d]);
+        const uint32_t dst = gofs[d] + (i - tstart[d]);
         if (aos) {
             gw_event e;
             e.watcher = k & aos_mask;
@@ -539,25 +577,38 @@ __global__ void __launch_bounds__(NT) k_rs2_scatter(const uint32_t* __restrict__
 }
 
 inline uint64_t radix2_tiles(uint64_t n_max) { return (n_max + RS2_TILE - 1) / RS2_TILE; }
+// scratch words radix_sort2 needs for n_max pairs
+inline uint64_t radix2_scratch_words(uint64_t n_max) {
+    return (uint64_t)RS2_MAX_PASSES * RS_RADIX * (RS2_GBLOCKS + 1 + radix2_tiles(n_max)) + 2 * RS2_MAX_PASSES;
+}
 
-// Sorts (k0,v0) by bits [lo_bit, hi_bit) with (k1,v1) as ping-pong; table holds
-// 256 * radix2_tiles(n_max) words.  With aos, the last pass writes gw_event
+// Sorts (k0,v0) by bits [lo_bit, hi_bit) (at most 32 bits) with (k1,v1) as
+// ping-pong; scratch holds radix2_scratch_words(n_max) u32 (no clearing
+// needed by the caller).  With aos, the last pass writes gw_event
 // {key & aos_mask, value} there (and the return value is meaningless).
 // Returns 0 if the result is in (k0,v0), 1 if in (k1,v1).
 inline int radix_sort2(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
-                       int lo_bit, int hi_bit, uint32_t* table, ScanCtx& sc, hipStream_t st,
+                       int lo_bit, int hi_bit, uint32_t* scratch, hipStream_t st,
                        gw_event* aos = nullptr, uint32_t aos_mask = 0xffffffffu) {
-    const uint32_t nt = (uint32_t)radix2_tiles(n_max);
-    if (nt == 0) return 0;
+    const uint64_t nt = radix2_tiles(n_max);
+    if (nt == 0 || hi_bit <= lo_bit) return 0;
+    const int passes = (hi_bit - lo_bit + 7) / 8;
+    uint32_t* part = scratch;                                             // [P][256][GBLOCKS]
+    uint32_t* gbase = part + (uint64_t)RS2_MAX_PASSES * RS_RADIX * RS2_GBLOCKS;   // [P][256]
+    unsigned long long* tickets = (unsigned long long*)(gbase + RS2_MAX_PASSES * RS_RADIX);   // [P]
+    uint32_t* status = (uint32_t*)(tickets + RS2_MAX_PASSES);            // [P][tiles][256]
+    // tickets and the status words of the passes used start at zero
+    (void)hipMemsetAsync(tickets, 0, RS2_MAX_PASSES * 8 + (uint64_t)passes * RS_RADIX * nt * 4, st);
+    hipLaunchKernelGGL(k_os_hist<>, dim3(RS2_GBLOCKS), dim3(NT), 0, st, k0, n_dev, n_max, lo_bit, passes, part);
+    hipLaunchKernelGGL(k_os_bases<>, dim3(passes), dim3(NT), 0, st, part, (uint32_t)RS2_GBLOCKS, gbase);
     int cur = 0;
-    for (int shift = lo_bit; shift < hi_bit; shift += 8) {
-        const bool last = shift + 8 >= hi_bit;
+    for (int p = 0; p < passes; ++p) {
+        const bool last = p == passes - 1;
         uint32_t* ki = cur ? k1 : k0; uint32_t* ko = cur ? k0 : k1;
         uint32_t* vi = cur ? v1 : v0; uint32_t* vo = cur ? v0 : v1;
-        hipLaunchKernelGGL(k_rs2_hist<>, dim3(nt), dim3(NT), 0, st, ki, n_dev, n_max, shift, table, nt);
-        scan_exclusive<uint32_t, uint32_t>(table, table, (uint64_t)RS_RADIX * nt, nullptr, sc, (uint32_t*)nullptr, st);
-        hipLaunchKernelGGL(k_rs2_scatter<>, dim3(nt), dim3(NT), 0, st, ki, vi, ko, vo, last ? aos : nullptr, aos_mask,
-                           n_dev, n_max, shift, table, nt);
+        hipLaunchKernelGGL(k_os_pass<>, dim3((uint32_t)nt), dim3(RS2_NT), 0, st, ki, vi, ko, vo, last ? aos : nullptr,
+                           aos_mask, n_dev, n_max, lo_bit + 8 * p, gbase + p * RS_RADIX,
+                           status + (uint64_t)p * RS_RADIX * nt, tickets + p);
         cur ^= 1;
     }
     return cur;

@@ -3,12 +3,12 @@
 // primitive instantiations used by the host code.
 //
 // A flagged entity e's records are: its own client's (syncInfoFlag bit0 and e
-// has a client; also after e left the space with the bit kept) and one per
-// neighbour w with a client (bit1, e present), all in watcher order.  The neighbours are evaluated from
+// has a client; also after e left the space with the bit kept), then one per
+// neighbour w with a client (bit1, e present), neighbours in the order the
+// window walk visits them: grid order ((cell of w, w): deterministic).  The neighbours are evaluated from
 // the current grid with the stamp-resolved relation (dev_common.hpp), so no
 // list is kept.  Count pass, scan, write pass; records land at their final
-// offsets in (entity, watcher) order, grouped by gate afterwards with a stable
-// radix sort.
+// offsets, grouped by gate afterwards with a stable radix sort.
 #include "dev_common.hpp"
 
 namespace gw {
@@ -192,23 +192,14 @@ __device__ __forceinline__ void st_record_nt(gw_sync_record* r, uint32_t watcher
     __builtin_nontemporal_store(((unsigned long long)__float_as_uint(p.w) << 32) | __float_as_uint(p.z), q + 2);
 }
 
-// Writes e's records at rec_off[k] in watcher order (nothing if the buffer is
-// too small: the host grows it and reruns this pass).  The window walk visits
-// watchers in grid order, so they are staged in the wave's LDS (the own-client
-// record included, watcher = e), sorted there (registers up to 64, bitonic in
-// LDS up to SYNC_LDS) and written in order; an entity with more records is
-// written in walk order and listed for the block sort (k_sync_bigsort).  With
-// the stable gate grouping after it the stream is in the canonical (gate,
-// entity, watcher) order.
-constexpr uint32_t SYNC_LDS = 1024;
+// writes e's records at rec_off[k] (nothing if the buffer is too small: the
+// host grows it and reruns this pass)
 template <int U>
 __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __restrict__ flagged,
                                                    const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
                                                    uint32_t nf_max, const uint64_t* __restrict__ rec_off,
                                                    const uint32_t* __restrict__ cnt, gw_sync_record* rec,
-                                                   uint64_t rec_cap, DevStats* st, uint32_t* big) {
-    __shared__ uint32_t lds[NWAVE * SYNC_LDS];
-    uint32_t* L = lds + (threadIdx.x >> 6) * SYNC_LDS;
+                                                   uint64_t rec_cap, DevStats* st) {
     const uint64_t nf = load_n(nf_max, nf_dev);
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
@@ -216,88 +207,42 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
     for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < nf; k += stride) {
         const uint32_t e = flagged[k];
         const uint32_t f = fbits[k];
-        const uint64_t at0 = rec_off[k];
-        const uint32_t c = cnt[k];
-        if (at0 + c > rec_cap) {
+        uint64_t at = rec_off[k];
+        if (at + cnt[k] > rec_cap) {
             if (ln == 0) atomicOr(&st->overflow, 1ull);
             continue;
         }
-        if (!c) continue;
         const AoiEnt a = w.aoi[e];
+        if (!owned_x(w.sp[a.meta & SPACE_MASK], a.x)) continue;
         const float4 p = w.pos[e];
-        const bool own = (f & GW_SIF_OWN_CLIENT) && w.gate[e];
-        const bool walk = (f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT);
-        if (c > SYNC_LDS) {                                   // rare: walk order, sorted by k_sync_bigsort
-            uint64_t at = at0;
-            if (own) {
-                if (ln == 0) st_record_nt(rec + at, e, e, p);
-                ++at;
-            }
-            if (walk)
-                wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
-                    const bool take = rel && g != 0;
-                    const uint64_t bt = wave_ballot(take);
-                    if (take) st_record_nt(rec + at + (uint64_t)popc64(bt & lt), ws, e, p);
-                    at += (uint64_t)popc64(bt);
-                });
-            if (ln == 0) big[atomicAdd(&st->n_big, 1ull)] = (uint32_t)k;
-            continue;
+        if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
+            if (ln == 0) st_record_nt(rec + at, e, e, p);
+            ++at;
         }
-        uint32_t n = 0;
-        if (own) {
-            if (ln == 0) L[0] = e;
-            n = 1;
-        }
-        if (walk)
+        if ((f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
             wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
                 const bool take = rel && g != 0;
                 const uint64_t bt = wave_ballot(take);
-                const uint32_t pos = n + (uint32_t)popc64(bt & lt);
-                if (take && pos < SYNC_LDS) L[pos] = ws;
-                n += (uint32_t)popc64(bt);
+                if (take) st_record_nt(rec + at + (uint64_t)popc64(bt & lt), ws, e, p);
+                at += (uint64_t)popc64(bt);
             });
-        wave_sync();
-        if (n <= 64) {
-            uint32_t v = ln < (int)n ? L[ln] : 0xffffffffu;
-            v = wave_sort64(v);
-            if (ln < (int)n) st_record_nt(rec + at0 + ln, v, e, p);
-        } else {
-            bitonic_inplace<64>(L, n, ln, [](uint32_t v) { return v; }, [] { wave_sync(); });
-            for (uint32_t i = ln; i < n; i += 64) st_record_nt(rec + at0 + i, L[i], e, p);
         }
-        wave_sync();                                          // L is reused by the next entity
     }
 }
-
-// entities with more than SYNC_LDS records: one block sorts the records of
-// one entity by watcher, in place
-__global__ void __launch_bounds__(NT) k_sync_bigsort(const uint64_t* __restrict__ rec_off,
-                                                     const uint32_t* __restrict__ cnt, gw_sync_record* rec,
-                                                     const DevStats* st, const uint32_t* __restrict__ big) {
-    const uint64_t nb = st->n_big;
-    for (uint64_t q = blockIdx.x; q < nb; q += gridDim.x) {
-        const uint32_t k = big[q];
-        bitonic_inplace<NT>(rec + rec_off[k], cnt[k], (int)threadIdx.x,
-                            [](const gw_sync_record& r) { return r.watcher; }, [] { __syncthreads(); });
-        __syncthreads();
-    }
-}
-
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
-                       uint64_t rec_cap, DevStats* st, uint32_t* big, hipStream_t s) {
+                       uint64_t rec_cap, DevStats* st, hipStream_t s) {
     if (!nf_max) return;
     const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
     if (w.nb_u >= 8)
         hipLaunchKernelGGL(k_sync_write<8>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st, big);
+                           rec_cap, st);
     else if (w.nb_u <= 2)
         hipLaunchKernelGGL(k_sync_write<2>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st, big);
+                           rec_cap, st);
     else
         hipLaunchKernelGGL(k_sync_write<4>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st, big);
-    hipLaunchKernelGGL(k_sync_bigsort, dim3(64), dim3(NT), 0, s, rec_off, cnt, rec, st, big);
+                           rec_cap, st);
 }
 
 // per-gate record histogram: LDS buckets for gates < 256, global atomics above
@@ -614,9 +559,60 @@ void launch_msg_gather(const uint32_t* in, int words, const uint32_t* idx, uint6
 #undef GW_MSG_W
 
 // ---------------------------------------------------------------------------
+// ids (16-B values per slot) and the game->gate wire encode (Entity.go:
+// 1210-1266): per gate with records, u16 1502, u16 gateid, then 48-B records
+// clientid(watcher) eid(entity) f32 x y z yaw, all little-endian.  One thread
+// per output dword (coalesced stores): record r's packet by a binary search
+// over the packets' first records, dword j of the record from the client id
+// (j < 4), the entity id (j < 8) or the payload.
+__global__ void __launch_bounds__(NT) k_put16(uint4* table, const uint32_t* __restrict__ slots,
+                                              const uint4* __restrict__ vals, uint32_t n) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i < n) table[slots[i]] = vals[i];
+}
+void launch_put16(uint4* table, const uint32_t* slots, const uint4* vals, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_put16, dim3(nblk(n, NT)), dim3(NT), 0, s, table, slots, vals, n);
+}
+__global__ void __launch_bounds__(NT) k_wire_encode(const gw_sync_record* __restrict__ rec, uint64_t R,
+                                                    const WirePacket* __restrict__ pk, uint32_t npk,
+                                                    const uint4* __restrict__ eid, const uint4* __restrict__ cid,
+                                                    uint32_t* __restrict__ out) {
+    const uint64_t t = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (t < npk) out[pk[t].byte_off / 4] = 1502u | (pk[t].gate << 16);   // packet headers
+    const uint64_t r = t / 12;
+    if (r >= R) return;
+    const uint32_t j = (uint32_t)(t - r * 12);
+    uint32_t lo = 0, hi = npk;                               // last packet with rec0 <= r
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pk[mid].rec0 <= r) lo = mid; else hi = mid;
+    }
+    const WirePacket p = pk[lo];
+    const gw_sync_record e = rec[r];
+    uint32_t v;
+    if (j < 4) {
+        const uint4 c = cid[e.watcher];
+        v = j == 0 ? c.x : j == 1 ? c.y : j == 2 ? c.z : c.w;
+    } else if (j < 8) {
+        const uint4 c = eid[e.entity];
+        v = j == 4 ? c.x : j == 5 ? c.y : j == 6 ? c.z : c.w;
+    } else {
+        const float f = j == 8 ? e.x : j == 9 ? e.y : j == 10 ? e.z : e.yaw;
+        v = __float_as_uint(f);
+    }
+    out[(p.byte_off + 4) / 4 + (r - p.rec0) * 12 + j] = v;
+}
+void launch_wire_encode(const gw_sync_record* rec, uint64_t R, const WirePacket* pk, uint32_t npk,
+                        const uint4* eid, const uint4* cid, uint32_t* out, hipStream_t s) {
+    const uint64_t threads = std::max<uint64_t>(R * 12, npk);
+    if (threads) hipLaunchKernelGGL(k_wire_encode, dim3(nblk(threads, NT)), dim3(NT), 0, s, rec, R, pk, npk, eid, cid, out);
+}
+
+// ---------------------------------------------------------------------------
 // primitive instantiations for the host code
 uint64_t radix_tile() { return RS_TILE; }
 uint64_t radix2_tile() { return RS2_TILE; }
+uint64_t radix2_scratch(uint64_t n_max) { return radix2_scratch_words(n_max); }
 uint64_t scan_tile() { return SCAN_TILE; }
 uint64_t scan_words() { return SCAN_WORDS; }
 void scan_u32_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,

@@ -84,6 +84,11 @@ COMM_ID_BYTES = 128
 RED_SUM, RED_MAX = 0, 1
 
 
+class WireOut(C.Structure):
+    _fields_ = [("bytes", C.c_void_p), ("bytes_dev", C.c_void_p), ("n_bytes", _u64), ("n_packets", _u32),
+                ("gate", C.POINTER(C.c_uint16)), ("off", C.POINTER(_u64)), ("device_us", _f64)]
+
+
 class GwError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"gpuaoi error {code}: {msg}")
@@ -144,6 +149,12 @@ def lib():
         L.gw_world_route.argtypes = [vp, vp, _u32, C.POINTER(vp * 2), C.POINTER(_u32 * 2)]
         L.gw_world_submit.argtypes = [vp, C.POINTER(vp * 2), C.POINTER(_u32 * 2)]
         L.gw_world_status.argtypes = [vp, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64)]
+        L.gw_set_entity_ids.argtypes = [vp, vp, vp, _u32]
+        L.gw_clear_entity_ids.argtypes = [vp, vp, _u32]
+        L.gw_set_client_ids.argtypes = [vp, vp, vp, _u32]
+        L.gw_set_client_syncing.argtypes = [vp, vp, vp, _u32]
+        L.gw_submit_client_sync.argtypes = [vp, vp, _u32, C.POINTER(_u32), C.POINTER(_u32)]
+        L.gw_sync_encode_wire.argtypes = [vp, _u32, C.POINTER(WireOut)]
         _lib = L
     return _lib
 
@@ -156,7 +167,8 @@ EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_spa
             "gw_set_stream", "gw_route_halo", "gw_submit_device_rows", "gw_halo_status", "gw_tick_result", "gw_space_restore",
             "gw_client_events", "gw_fanout", "gw_comm_unique_id", "gw_comm_init", "gw_comm_info",
             "gw_comm_exchange", "gw_comm_allreduce_u64", "gw_world_create", "gw_world_step", "gw_world_route",
-            "gw_world_submit", "gw_world_status"]
+            "gw_world_submit", "gw_world_status", "gw_set_entity_ids", "gw_clear_entity_ids", "gw_set_client_ids",
+            "gw_set_client_syncing", "gw_submit_client_sync", "gw_sync_encode_wire"]
 
 
 def comm_unique_id() -> bytes:
@@ -430,6 +442,44 @@ class GpuAOI:
 
     def synchronize(self):
         self._chk(lib().gw_synchronize(self._h))
+
+    # ---- ids, client-sync decode, wire encode -------
+    def set_entity_ids(self, slots, ids: bytes):
+        s = np.ascontiguousarray(slots, dtype=np.uint32)
+        b = np.frombuffer(bytes(ids), np.uint8)
+        assert len(b) == 16 * len(s)
+        self._chk(lib().gw_set_entity_ids(self._h, _p(s), _p(b), len(s)))
+
+    def clear_entity_ids(self, slots):
+        s = np.ascontiguousarray(slots, dtype=np.uint32)
+        self._chk(lib().gw_clear_entity_ids(self._h, _p(s), len(s)))
+
+    def set_client_ids(self, slots, ids: bytes):
+        s = np.ascontiguousarray(slots, dtype=np.uint32)
+        b = np.frombuffer(bytes(ids), np.uint8)
+        assert len(b) == 16 * len(s)
+        self._chk(lib().gw_set_client_ids(self._h, _p(s), _p(b), len(s)))
+
+    def set_client_syncing(self, slots, on):
+        s = np.ascontiguousarray(slots, dtype=np.uint32)
+        o = np.ascontiguousarray(on, dtype=np.uint8)
+        self._chk(lib().gw_set_client_syncing(self._h, _p(s), _p(o), len(s)))
+
+    def submit_client_sync(self, payload: bytes) -> tuple[int, int]:
+        """MT_SYNC_POSITION_YAW_FROM_CLIENT payload (32-B records) -> (applied, left to the caller)."""
+        b = np.frombuffer(bytes(payload), np.uint8)
+        assert len(b) % 32 == 0
+        ap, tc = _u32(), _u32()
+        self._chk(lib().gw_submit_client_sync(self._h, _p(b), len(b) // 32, C.byref(ap), C.byref(tc)))
+        return ap.value, tc.value
+
+    def encode_wire(self, copy: bool = True):
+        """-> (bytes or None, [(gate, offset, length)], n_bytes, device_us) of the last collect's packets."""
+        o = WireOut()
+        self._chk(lib().gw_sync_encode_wire(self._h, 1 if copy else 0, C.byref(o)))
+        pk = [(o.gate[k], o.off[k], o.off[k + 1] - o.off[k]) for k in range(o.n_packets)]
+        data = C.string_at(o.bytes, o.n_bytes) if (copy and o.n_bytes) else (b"" if copy else None)
+        return data, pk, o.n_bytes, o.device_us
 
     # ---- RCCL communicator (library-internal data-path collectives) -------
     def comm_init(self, uid: bytes, nranks: int, rank: int):

@@ -141,10 +141,15 @@ typedef struct gw_tick_out {
                                       packet MT_SYNC_POSITION_YAW_ON_CLIENTS   */
 
 typedef struct gw_sync_out {
-    /* Canonical order: sorted by (gate(watcher), entity, watcher), gate_off
-     * partitioning the stream by gate id (each gate's packet one slice); with
-     * GW_SYNC_BY_CLIENT by (gate(watcher), watcher, entity),
-     * each client's records one contiguous segment (client_off).            */
+    /* Deterministic order.  Default: grouped by gate(watcher) (gate_off; each
+     * gate's packet is one slice), inside a gate by entity ascending; an
+     * entity's own-client record first, then its neighbours' records in the
+     * order the window walk visits them, i.e. by (grid cell of the watcher's
+     * position, watcher slot) - the reference emits them in Go map order, so
+     * any fixed order is equivalent and this one costs no sort.  With
+     * GW_SYNC_BY_CLIENT: the canonical (gate(watcher), watcher, entity) order
+     * of SURVEY App. B.5, each client's records one contiguous segment
+     * (client_off).                                                          */
     const gw_sync_record* rec;      /* host pointer (NULL unless COPY_TO_HOST) */
     const gw_sync_record* rec_dev;  /* device pointer, always valid            */
     uint64_t n_rec;
@@ -352,6 +357,49 @@ int  gw_synchronize(gw_ctx* ctx);
  * restores the context's own stream.  Drains the previous stream first. */
 int  gw_set_stream(gw_ctx* ctx, void* hip_stream);
 
+/* ---- ids, client-sync decode and the wire encode (host boundary rows) -----
+ * EntityID and ClientID are 16-byte strings (engine/common/types.go:9;
+ * uuid/uuid.go:27-59).  The context keeps the entity id and the client id of
+ * each slot, a host table entity id -> slot for the decode, and the entity's
+ * SetClientSyncing flag (Entity.go:437-440). */
+#define GW_ID_BYTES 16
+int  gw_set_entity_ids(gw_ctx* ctx, const uint32_t* slots, const void* ids /* n*16 */, uint32_t n);
+int  gw_clear_entity_ids(gw_ctx* ctx, const uint32_t* slots, uint32_t n);    /* entity destroyed */
+int  gw_set_client_ids(gw_ctx* ctx, const uint32_t* slots, const void* ids /* n*16 */, uint32_t n);
+int  gw_set_client_syncing(gw_ctx* ctx, const uint32_t* slots, const uint8_t* on, uint32_t n);
+
+/* GameService.HandleSyncPositionYawFromClient (GameService.go:395-407): the
+ * payload of one MT_SYNC_POSITION_YAW_FROM_CLIENT packet, n records of
+ * eid[16] f32 x y z yaw (little-endian, 32 B each), each in order as
+ * entity.OnSyncPositionYawFromClient (EntityManager.go:450-459): a record of
+ * an unknown entity is dropped; one whose entity syncs from its client
+ * (Entity.go:430-435) becomes setPositionYaw(fromClient=true): a Moved op
+ * with syncInfoFlag NEIGHBOR (Entity.go:1189-1205) appended to the tick like
+ * gw_submit - if the entity is in an AOI space of this context at that point
+ * of the call order; otherwise it is left to the caller (*to_caller counts
+ * those: an entity outside AOI spaces keeps the reference path).  *applied:
+ * records turned into ops. */
+int  gw_submit_client_sync(gw_ctx* ctx, const void* payload, uint32_t n_records, uint32_t* applied,
+                           uint32_t* to_caller);
+
+/* The game->gate sync packets of the last gw_sync_collect (Entity.go:1210-1266):
+ * per gate with records, u16 MT_SYNC_POSITION_YAW_ON_CLIENTS (1502), u16
+ * gateid, then per record clientid(watcher)[16] eid(entity)[16] f32 x y z yaw
+ * (48 B, little-endian), records in the collect's order.  Encoded on the
+ * device; `bytes` is one buffer holding the packets back to back, packet k of
+ * gate gate[k] at [off[k], off[k+1]).  Pointers valid until the next call. */
+#define GW_WIRE_COPY_TO_HOST 1u
+typedef struct gw_wire_out {
+    const uint8_t* bytes;         /* host (GW_WIRE_COPY_TO_HOST), else NULL     */
+    const uint8_t* bytes_dev;     /* device, always valid                       */
+    uint64_t n_bytes;
+    uint32_t n_packets;
+    const uint16_t* gate;         /* host: n_packets gate ids                   */
+    const uint64_t* off;          /* host: n_packets + 1 byte offsets           */
+    double device_us;
+} gw_wire_out;
+int  gw_sync_encode_wire(gw_ctx* ctx, uint32_t flags, gw_wire_out* out);
+
 /* ---- RCCL communicator (one per context: one process per GPU) -----------
  * The data-path collectives of a decomposed world run inside the library on
  * the context's stream (RCCL over xGMI), so a Go host drives them through the
@@ -416,7 +464,7 @@ int  gw_world_submit(gw_ctx* ctx, const gw_halo_row* const recv[2], const uint32
 int  gw_world_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops);
 
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 9
+#define GW_ABI_VERSION 10
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

@@ -1,0 +1,150 @@
+"""The drop-in boundary driven from plain C (tests/c_harness.c, gcc, linked
+against libgpuaoi.so): a golden fixture replayed through the ABI in the Go
+shim's call order, with the client position records decoded by
+gw_submit_client_sync (GameService.go:395-407) and the game->gate packets
+encoded by gw_sync_encode_wire (Entity.go:1210-1266).
+
+Checked against the fixture (made by the oracle, tests/golden/): every tick's
+canonical events byte for byte, and the wire bytes: each packet's header
+(u16 1502, u16 gate), 48-B records with GenFixedUUID client / entity ids and
+the payload floats; re-ordered into the fixture's canonical record order the
+packets must hash to the fixture's wire_sha (the oracle's own encoding).
+The library emits an entity's neighbour records in grid order, the reference
+in Go map order, so only the order inside an entity may differ."""
+import hashlib
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import golden_data as G
+from goworld_amd import gpuaoi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "goworld_amd", "lib", "c_harness")
+
+
+def _write_input(path, fx):
+    tr = fx.trace
+    with open(path, "wb") as f:
+        f.write(b"GWH1")
+        f.write(struct.pack("<If4fII", tr.capacity, tr.d, *tr.bounds, len(tr.init_slots), len(tr.ticks)))
+        init = np.zeros(len(tr.init_slots), [("slot", "<u4"), ("x", "<f4"), ("y", "<f4"), ("z", "<f4"),
+                                              ("yaw", "<f4")])
+        init["slot"], init["x"], init["y"], init["z"], init["yaw"] = (tr.init_slots, tr.init_x, tr.init_y,
+                                                                       tr.init_z, tr.init_yaw)
+        f.write(init.tobytes())
+        f.write(np.asarray(tr.gates, np.uint16).tobytes())
+        for ops in tr.ticks:
+            f.write(struct.pack("<I", len(ops)))
+            f.write(np.ascontiguousarray(ops).tobytes())
+
+
+def _read_output(path, ticks):
+    b = open(path, "rb").read()
+    p = 0
+    out = []
+
+    def take(n):
+        nonlocal p
+        v = b[p:p + n]
+        p += n
+        return v
+    for _ in range(ticks):
+        ne = struct.unpack("<Q", take(8))[0]
+        e = np.frombuffer(take(8 * ne), G.EVENT_DTYPE)
+        nl = struct.unpack("<Q", take(8))[0]
+        l = np.frombuffer(take(8 * nl), G.EVENT_DTYPE)
+        nw = struct.unpack("<Q", take(8))[0]
+        wire = take(nw)
+        npk = struct.unpack("<I", take(4))[0]
+        pk = [struct.unpack("<IQ", take(12)) for _ in range(npk)]
+        out.append((e, l, wire, pk))
+    applied = struct.unpack("<I", take(4))[0]
+    assert p == len(b)
+    return out, applied
+
+
+def _parse_wire(wire, pk, n_slots):
+    """Packets -> records (watcher, entity, x, y, z, yaw), checking the layout."""
+    eid = {pyorc_uuid(i): i for i in range(n_slots)}
+    cid = {pyorc_uuid(i | 0x80000000): i for i in range(n_slots)}
+    recs = []
+    ends = [o for _, o in pk[1:]] + [len(wire)]
+    for (gate, off), end in zip(pk, ends):
+        mt, g = struct.unpack_from("<HH", wire, off)
+        assert mt == 1502 and g == gate                     # MT_SYNC_POSITION_YAW_ON_CLIENTS, gate id
+        assert (end - off - 4) % 48 == 0
+        for q in range(off + 4, end, 48):
+            w, e = cid[wire[q:q + 16]], eid[wire[q + 16:q + 32]]
+            recs.append((w, e) + struct.unpack_from("<4f", wire, q + 32))
+    a = np.zeros(len(recs), G.REC_DTYPE)
+    if recs:
+        arr = np.array(recs, dtype=object)
+        for i, k in enumerate(["watcher", "entity", "x", "y", "z", "yaw"]):
+            a[k] = arr[:, i].astype(a.dtype[k])
+    return a
+
+
+def pyorc_uuid(v):
+    from oracle import pyorc
+    return pyorc.fixed_uuid(v)
+
+
+def _encode_like_oracle(recs, gates):
+    """The oracle's game->gate bytes (orc_encode_wire) of canonical records."""
+    out = bytearray()
+    i = 0
+    while i < len(recs):
+        g = int(gates[recs["watcher"][i]])
+        j = i
+        while j < len(recs) and gates[recs["watcher"][j]] == g:
+            j += 1
+        out += struct.pack("<HH", 1502, g)
+        for r in recs[i:j]:
+            out += pyorc_uuid(int(r["watcher"]) | 0x80000000) + pyorc_uuid(int(r["entity"]))
+            out += struct.pack("<4f", r["x"], r["y"], r["z"], r["yaw"])
+        i = j
+    return bytes(out)
+
+
+def test_harness_is_built_and_fails_loudly_without_a_device(tmp_path):
+    assert os.path.exists(HARNESS), "build with make (gcc links tests/c_harness.c against libgpuaoi.so)"
+    import torch
+    if torch.cuda.is_available():
+        return
+    fx = G.Fixture("cfg1_walk")
+    _write_input(tmp_path / "in.bin", fx)
+    r = subprocess.run([HARNESS, str(tmp_path / "in.bin"), str(tmp_path / "out.bin")], capture_output=True, text=True)
+    assert r.returncode != 0 and "gw_init" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cfg1_walk", "dyadic_hot_2k", "adversarial_s11"])
+def test_c_harness_replays_golden_through_the_abi(tmp_path, name):
+    fx = G.Fixture(name)
+    tr = fx.trace
+    _write_input(tmp_path / "in.bin", fx)
+    r = subprocess.run([HARNESS, str(tmp_path / "in.bin"), str(tmp_path / "out.bin")], capture_output=True,
+                       text=True, timeout=100)
+    assert r.returncode == 0, r.stderr
+    out, applied = _read_output(tmp_path / "out.bin", fx.ticks)
+    n_client = sum(int(np.sum((ops["kind"] == 2) & (ops["sync_flags"] == 2))) for ops in tr.ticks)
+    assert applied == n_client                              # every client record decoded into a Moved op
+    if name == "cfg1_walk":
+        assert applied > 1000
+    for t, (e, l, wire, pk) in enumerate(out):
+        ee, ll = fx.events(t)
+        assert e.tobytes() == ee.tobytes() and l.tobytes() == ll.tobytes(), f"{name} tick {t}: events"
+        recs = _parse_wire(wire, pk, tr.capacity)
+        assert len(recs) == fx.n_rec(t)
+        canon = G.canonical_records(recs, tr.gates)
+        assert G.sha(canon) == fx.rec_sha(t), f"{name} tick {t}: records"
+        assert hashlib.sha256(_encode_like_oracle(canon, tr.gates)).hexdigest() == fx.wire_sha(t), \
+            f"{name} tick {t}: wire bytes"
+        # inside a gate packet: entities ascending, the own record first
+        for (gate, off), end in zip(pk, [o for _, o in pk[1:]] + [len(wire)]):
+            seg = _parse_wire(wire[off:end], [(gate, 0)], tr.capacity)
+            assert np.all(np.diff(seg["entity"].astype(np.int64)) >= 0)

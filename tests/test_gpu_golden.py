@@ -6,9 +6,8 @@ tick's canonical enter / leave events byte for byte, the sync records of every
 collect (count + SHA-256 of the canonical bytes, tick 0 in full) and the final
 InterestedIn sets.  Large configs (#2 100k, #3 1M; tests/golden/digests.json):
 per tick event and record digests, on traces regenerated from their seeds
-(input hash checked first).  Event and record streams are compared as the GPU
-emits them (canonical order, no host re-sort).  No oracle runs here: the
-expected outputs are data.
+(input hash checked first).  No oracle runs here: the expected outputs are
+data.
 """
 import numpy as np
 import pytest
@@ -33,14 +32,19 @@ def gpu():
 
 
 def canonical(recs: np.ndarray, gates: np.ndarray) -> np.ndarray:
-    """The GPU stream must already be in the canonical (gate(watcher), entity,
-    watcher) order of the fixtures: checked, not re-sorted."""
-    if len(recs) > 1:
-        assert len(gates) <= 1 << 24
-        key = (gates[recs["watcher"]].astype(np.uint64) << np.uint64(48)) | \
-            (recs["entity"].astype(np.uint64) << np.uint64(24)) | recs["watcher"].astype(np.uint64)
-        assert np.all(key[1:] > key[:-1]), "record stream not in (gate, entity, watcher) order"
-    return recs
+    """Records in the fixtures' (gate(watcher), entity, watcher) order via one
+    u64 key (gate 16 | entity 24 | watcher 24 bits).  The GPU stream is already
+    in (gate, entity) order (checked) with only the watchers of an entity in
+    grid order (test_gpu_parity checks that order exactly), so the stable
+    (run-merging) sort is near linear even for the 1M config's load collect
+    (~1.5e8 records)."""
+    if len(recs) == 0:
+        return recs
+    assert len(gates) <= 1 << 24
+    ge = (gates[recs["watcher"]].astype(np.uint64) << np.uint64(24)) | recs["entity"].astype(np.uint64)
+    assert np.all(ge[1:] >= ge[:-1]), "record stream not grouped by (gate, entity)"
+    key = (ge << np.uint64(24)) | recs["watcher"].astype(np.uint64)
+    return recs[np.argsort(key, kind="stable")]
 
 
 @pytest.mark.parametrize("name", G.SMALL)

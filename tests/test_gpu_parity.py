@@ -2,10 +2,11 @@
 same seeded traces — bit-exact events, sync records and neighbour lists.
 
 Event and sync-record streams are compared byte for byte as the GPU emits them:
-both are in the canonical orders of SURVEY App. B.5 ((watcher, target);
-(gate, entity, watcher), or (gate, watcher, entity) with GW_SYNC_BY_CLIENT),
-which the oracle produces by sorting (the reference's own order is Go map
-order, i.e. random).
+events in the canonical (watcher, target) order; records in the documented
+order (gate, entity, own record first, then the watchers in the window walk's
+grid order), predicted here from the oracle's records and the grid geometry,
+or (gate, watcher, entity) with GW_SYNC_BY_CLIENT (the reference's own order is
+Go map order, i.e. random).
 
 The oracle engines are equal to each other on every trace (test_oracle.py), so
 the GPU is checked against ORC_SEQRULE for speed and against ORC_XZLIST (the
@@ -42,13 +43,34 @@ def _sorted_records(recs, gates_of):
     return recs[order]
 
 
+def grid_cells(tr, x, z, cells_per_d=2):
+    """The library's uniform-grid cell of positions (x, z) of one space, as
+    gw_space_create / dev_common.hpp cell_of compute it (float32)."""
+    b = [float(v) for v in tr.bounds]
+    d = float(tr.d)
+    ex, ez = b[2] - b[0], b[3] - b[1]
+    maxabs = max(abs(b[0]), abs(b[2]), abs(b[1]), abs(b[3]))
+    span = 2.0 * d + 4e-6 * (maxabs + d) + 1e-3
+    cs = max(max(d / cells_per_d, max(ex, ez) / 8192.0), span / 9.0)
+    inv = np.float32(1.0 / cs)
+    W, H = max(1, int(np.ceil(ex / cs))), max(1, int(np.ceil(ez / cs)))
+
+    def cellc(v, o, lim):
+        f = np.floor((np.asarray(v, np.float32) - np.float32(o)) * inv)
+        return np.clip(f, 0, lim - 1).astype(np.int64)
+    return cellc(z, b[1], H) * W + cellc(x, b[0], W)
+
+
 class Harness:
-    """One GPU context with several spaces, each mirrored by an oracle space."""
+    """One GPU context with several spaces, each mirrored by an oracle space.
+    Positions are tracked from the ops to predict the record stream's exact
+    order (the walk's grid order)."""
 
     def __init__(self, g, trs, mode=pyorc.SEQRULE):
         self.g, self.trs = g, trs
         self.orcs, self.bases = [], []
         cap_total = 0
+        self.x, self.z = [], []
         for tr in trs:
             sid, base = gpuaoi.load_space(g, tr)
             o = pyorc.OracleSpace(tr.capacity, tr.d, mode)
@@ -56,22 +78,38 @@ class Harness:
             self.orcs.append(o)
             self.bases.append(base)
             cap_total = base + tr.capacity
+            x = np.zeros(tr.capacity, np.float32)
+            z = np.zeros(tr.capacity, np.float32)
+            x[tr.init_slots], z[tr.init_slots] = tr.init_x, tr.init_z
+            self.x.append(x)
+            self.z.append(z)
         self.gates = np.zeros(cap_total, np.uint16)
         for tr, b in zip(trs, self.bases):
             if tr.gates is not None:
                 self.gates[b:b + tr.capacity] = tr.gates
 
+    def track(self, i, ops):
+        aoi = np.isin(ops["kind"], [T.OP_ENTER, T.OP_MOVED])
+        self.x[i][ops["slot"][aoi]] = ops["x"][aoi]
+        self.z[i][ops["slot"][aoi]] = ops["z"][aoi]
+
     def check_collect(self):
         r = self.g.sync_collect()
-        exp = []
-        for o, b in zip(self.orcs, self.bases):
+        exp, keys = [], []
+        for i, (o, b, tr) in enumerate(zip(self.orcs, self.bases, self.trs)):
             e = o.collect()
+            cell = grid_cells(tr, self.x[i][e["watcher"]], self.z[i][e["watcher"]])
+            own = e["watcher"] == e["entity"]
             e["watcher"] += b
             e["entity"] += b
             exp.append(e)
-        exp = _sorted_records(np.concatenate(exp) if exp else np.zeros(0, pyorc.REC_DTYPE), self.gates)
+            keys.append(np.where(own, -1, cell))
+        exp = np.concatenate(exp) if exp else np.zeros(0, pyorc.REC_DTYPE)
+        cell = np.concatenate(keys) if keys else np.zeros(0, np.int64)
+        # the documented stream order: (gate, entity, own record first, then the
+        # watchers' (grid cell, slot)) - compared raw, no host re-sort of the GPU output
+        exp = exp[np.lexsort((exp["watcher"], cell, exp["entity"], self.gates[exp["watcher"]]))]
         assert r.n_rec == len(exp)
-        # the raw stream: canonical (gate, entity, watcher) order, no host re-sort
         assert r.records.tobytes() == exp.tobytes(), "sync records differ"
         assert r.gate_off[0] == 0 and r.gate_off[-1] == len(exp)
         for gid in range(len(r.gate_off) - 1):
@@ -83,8 +121,9 @@ class Harness:
         self.g.submit(np.concatenate(ops))
         res = self.g.tick()
         ee, ll = [], []
-        for tr, o, b in zip(self.trs, self.orcs, self.bases):
+        for i, (tr, o, b) in enumerate(zip(self.trs, self.orcs, self.bases)):
             assert o.tick(tr.ticks[t]) == 0
+            self.track(i, tr.ticks[t])
             e, l = o.events()
             e = e.copy(); l = l.copy()
             for a in (e, l):
@@ -128,7 +167,7 @@ def test_tiny_hand_made(ctx_factory):
     rec = g.sync_collect().records
     gates = np.zeros(base + 8, np.uint16)
     gates[base:base + 4] = 1
-    assert rec.tobytes() == _sorted_records(o.collect(), gates[base:]).tobytes()
+    assert _sorted_records(rec, gates).tobytes() == _sorted_records(o.collect(), gates[base:]).tobytes()
 
 
 @pytest.mark.parametrize("seed", [11, 12, 13])
@@ -358,7 +397,7 @@ def test_deferred_tick_with_collect(ctx_factory, dense):
         ee, ll = _oracle_events(o, ops)
         exp = _sorted_records(o.collect(), gates)
         assert rec.n_rec == len(exp)
-        assert rec.records.tobytes() == exp.tobytes()
+        assert _sorted_records(rec.records, gates).tobytes() == exp.tobytes()
         r = g.tick_result()
         assert (r.n_enter, r.n_leave) == (len(ee), len(ll))
         e = np.zeros(r.n_enter, gpuaoi.EVENT_DTYPE)

@@ -768,17 +768,11 @@ __global__ void __launch_bounds__(NT) k_chunk_first(TickBufs b) {
     const uint64_t end = at + mi.y + mi.z;
     for (uint64_t c = (at + 63) >> 6; (c << 6) < end; ++c) b.chunk_first[c] = (uint32_t)k;
 }
-__global__ void __launch_bounds__(NT) k_flatten(TickBufs b) {
+// element p = 64c + lane of the flat list (wave-uniform c; every lane runs
+// the shuffles); false past E
+__device__ __forceinline__ bool flat_elem(const TickBufs& b, uint64_t c, uint64_t E, uint32_t& key, uint32_t& val) {
     const uint64_t nl_ = b.st->n_mlist;
     const int ln = lane_id();
-    const uint64_t E = lo32(b.st->ev_pk) + hi32(b.st->ev_pk);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (E > b.ev_cap) atomicOr(&b.st->overflow, 1ull);
-        b.st->n_sort = E > b.ev_cap ? 0 : E;              // nothing is sorted on overflow (the host redoes)
-    }
-    if (E > b.ev_cap) return;
-    const uint64_t c = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
-    if ((c << 6) >= E) return;
     const uint32_t q0 = b.chunk_first[c];
     const uint64_t k = (uint64_t)q0 + ln;
     uint64_t at = ~0ull, end = ~0ull, reg = 0;
@@ -808,10 +802,9 @@ __global__ void __launch_bounds__(NT) k_flatten(TickBufs b) {
     const uint64_t qreg = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(reg >> 32), q, 64) << 32) |
                           (uint32_t)__shfl((int)(uint32_t)reg, q, 64);
     const uint32_t qA = (uint32_t)__shfl((int)mi.x, q, 64), qn = (uint32_t)__shfl((int)mi.y, q, 64);
-    if (p >= E) return;
+    if (p >= E) return false;
     const uint32_t j = (uint32_t)(p - qat);                 // index inside mover q's events
     const uint32_t lvb = 1u << b.wbits;
-    uint32_t key, val;
     if (j < qn) {
         const uint32_t e = b.own[qreg + j];
         key = ((e & 1u) ? lvb : 0u) | qA;
@@ -821,8 +814,318 @@ __global__ void __launch_bounds__(NT) k_flatten(TickBufs b) {
         key = ((e & 1u) ? lvb : 0u) | (uint32_t)hi32(e);
         val = (uint32_t)(lo32(e) >> 1);
     }
-    b.fk0[p] = key;
-    b.fv0[p] = val;
+    return true;
+}
+
+// flat list: (key, value) arrays for the general sort, or one u64
+// (leave<<wbits | watcher) << wbits | target per event for the bucket path
+__global__ void __launch_bounds__(NT) k_flatten(TickBufs b) {
+    const uint64_t E = lo32(b.st->ev_pk) + hi32(b.st->ev_pk);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (E > b.ev_cap) atomicOr(&b.st->overflow, 1ull);
+        b.st->n_sort = E > b.ev_cap ? 0 : E;              // nothing is sorted on overflow (the host redoes)
+    }
+    if (E > b.ev_cap) return;
+    const uint64_t c = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
+    if ((c << 6) >= E) return;
+    uint32_t key, val;
+    if (!flat_elem(b, c, E, key, val)) return;
+    const uint64_t p = (c << 6) + lane_id();
+    if (b.ev_full) {
+        b.fk0[p] = key;
+        b.fv0[p] = val;
+    } else {
+        b.bk_a[p] = ((uint64_t)key << b.wbits) | val;      // (leave, watcher, target)
+    }
+}
+
+// (4) bucket path.  Events are keyed by the full (leave, watcher, target) —
+// unique within a tick — so no pass needs to be stable: the flat list is
+// cut into tiles; each tile counts its events per bucket (a range of
+// (leave, watcher)); one exclusive scan of the bucket-major count table gives
+// every (bucket, tile) its offset; each tile stages its events by bucket in
+// LDS and writes runs; each bucket (a few thousand events) is then sorted in
+// LDS and written as gw_event.  Two passes over the events instead of three
+// stable radix passes with look-back.  A bucket larger than the LDS sort is
+// reported (overflow + bk_max) and the host redoes the tick on the general
+// sort.
+//
+// Bucket bounds are quantiles of the previous tick's (leave, watcher) keys
+// (k_bk_split), so skewed slot ranges (hotspot entities in adjacent slots)
+// still give buckets of about the mean size; bucket(k) = #{bounds <= k},
+// found through a 2^12-cell table of bound counts (A[x] = #{bounds < x <<
+// lsh}) and a binary search inside the cell (usually empty).
+// Flat entries: bucket << 54 | (leave<<wbits | watcher) << wbits | target
+// (wbits <= 26, or the host takes the general sort).
+constexpr int BK_LUT_BITS = 12;
+constexpr int BK_KEY_SHIFT = 54;
+
+struct BkLut {
+    uint32_t sp[1 << BK_MAXBITS];
+    uint16_t a[(1 << BK_LUT_BITS) + 1];
+};
+__device__ __forceinline__ void bk_lut_build(const TickBufs& b, BkLut& L, uint32_t NB, int& lsh) {
+    const uint32_t stride = BK_NSPLIT / NB;
+    for (uint32_t i = threadIdx.x; i + 1 < NB; i += blockDim.x) L.sp[i] = b.bk_split[(i + 1) * stride];
+    const int kb = b.wbits + 1;
+    const int lb = min(kb, BK_LUT_BITS);
+    lsh = kb - lb;
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x <= (1u << lb); x += blockDim.x) {
+        const uint64_t v = (uint64_t)x << lsh;                 // count bounds < v
+        uint32_t lo = 0, hi = NB - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((uint64_t)L.sp[mid] < v) lo = mid + 1; else hi = mid;
+        }
+        L.a[x] = (uint16_t)lo;
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ uint32_t bk_bucket(const BkLut& L, int lsh, uint32_t key) {
+    const uint32_t x = key >> lsh;
+    uint32_t lo = L.a[x], hi = L.a[x + 1];
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.sp[mid] <= key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(BK_NT) k_bk_count(TickBufs b) {
+    __shared__ uint32_t h[1 << BK_MAXBITS];
+    __shared__ BkLut lut;
+    const int t = threadIdx.x;
+    const uint32_t NB = 1u << b.bk_bits;
+    for (uint32_t i = t; i < NB; i += BK_NT) h[i] = 0;
+    const uint64_t n = b.st->n_sort;
+    const uint64_t base = (uint64_t)blockIdx.x * BK_TILE;
+    if (base < n) {                                         // block-uniform
+        int lsh;
+        bk_lut_build(b, lut, NB, lsh);                      // (syncs)
+        const int W = b.wbits;
+        constexpr int IPT = BK_TILE / BK_NT;
+        uint64_t k[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint64_t i = base + (uint64_t)j * BK_NT + t;
+            k[j] = i < n ? b.bk_a[i] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint64_t i = base + (uint64_t)j * BK_NT + t;
+            if (i < n) {
+                const uint32_t q = bk_bucket(lut, lsh, (uint32_t)(k[j] >> W));
+                b.bk_id[i] = (uint16_t)q;
+                atomicAdd(&h[q], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < NB; i += BK_NT) b.bk_cnt[(uint64_t)i * b.bk_tiles + blockIdx.x] = h[i];
+}
+
+// exclusive scan of one value per thread over a block of NTH threads
+template <int NTH>
+__device__ __forceinline__ uint32_t bk_block_excl(uint32_t v, uint32_t* red) {
+    const int t = threadIdx.x, w = t >> 6, ln = lane_id();
+    const uint32_t inc = wave_incl_scan<uint32_t>(v);
+    if (ln == 63) red[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+#pragma unroll
+    for (int k = 0; k < NTH / 64; ++k) pre += (k < w) ? red[k] : 0u;
+    return pre + inc - v;
+}
+
+__global__ void __launch_bounds__(BK_NT) k_bucket_scatter(TickBufs b) {
+    __shared__ uint64_t stg[BK_TILE];
+    __shared__ uint32_t h[1 << BK_MAXBITS], go[1 << BK_MAXBITS];
+    __shared__ uint32_t red[BK_NT / 64];
+    const int t = threadIdx.x;
+    const uint64_t n = b.st->n_sort;
+    const uint64_t base = (uint64_t)blockIdx.x * BK_TILE;
+    if (base >= n) return;                                  // block-uniform
+    const uint32_t NB = 1u << b.bk_bits;
+    if (t < (int)NB) h[t] = 0;
+    __syncthreads();
+    constexpr int IPT = BK_TILE / BK_NT;
+    uint64_t k[IPT];
+    uint32_t r[IPT], q[IPT];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t i = base + (uint64_t)j * BK_NT + t;
+        k[j] = i < n ? b.bk_a[i] : 0ull;
+        q[j] = i < n ? b.bk_id[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t i = base + (uint64_t)j * BK_NT + t;
+        k[j] |= (uint64_t)q[j] << BK_KEY_SHIFT;             // the bucket rides in the staged key
+        r[j] = i < n ? atomicAdd(&h[q[j]], 1u) : 0u;
+    }
+    __syncthreads();
+    const uint32_t cnt = t < (int)NB ? h[t] : 0u;
+    const uint32_t toff = bk_block_excl<BK_NT>(cnt, red);
+    if (t < (int)NB) {
+        h[t] = toff;
+        go[t] = b.bk_cnt[(uint64_t)t * b.bk_tiles + blockIdx.x] - toff;   // mod 2^32: dst = go + staged index
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t i = base + (uint64_t)j * BK_NT + t;
+        if (i < n) stg[h[q[j]] + r[j]] = k[j];
+    }
+    __syncthreads();
+    const uint32_t tn = (uint32_t)min<uint64_t>((uint64_t)BK_TILE, n - base);
+    for (uint32_t i = t; i < tn; i += BK_NT) {              // each bucket's run of the tile is contiguous
+        const uint64_t v = stg[i];
+        b.bk_b[go[(uint32_t)(v >> BK_KEY_SHIFT)] + i] = v & ((1ull << BK_KEY_SHIFT) - 1);
+    }
+}
+
+// One bucket per block: a counting sort of its events by bin = (leave,
+// watcher - floor) >> bsh into at most BK_HBINS bins (bsh = 0 unless the
+// bucket spans a wide, sparse key range).  A short bin (<= BK_SHORT events,
+// the common case) places each event at the bin start + the bin's events
+// with a smaller (leave, watcher, target) key; a longer bin (a moving
+// hotspot watcher's own events) is sorted in place by one wave (bitonic) and
+// written as a run.
+template <int MODE>
+__global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
+    __shared__ uint64_t L[BK_LCAP];
+    __shared__ uint32_t hb[BK_HBINS];
+    __shared__ uint32_t red[BK_SNT / 64];
+    __shared__ uint2 longs[BK_LCAP / (BK_SHORT + 1) + 1];
+    __shared__ uint32_t n_long;
+    constexpr int CH = BK_LCAP / BK_SNT;                    // max keys per thread
+    const uint32_t bk = blockIdx.x;
+    const uint32_t NB = 1u << b.bk_bits;
+    const uint64_t T = b.bk_tiles;
+    const uint64_t n_all = b.st->n_sort;
+    const uint64_t s = b.bk_cnt[(uint64_t)bk * T];
+    const uint64_t e = bk + 1 < NB ? b.bk_cnt[(uint64_t)(bk + 1) * T] : n_all;
+    if (e <= s) return;
+    const uint32_t n = (uint32_t)(e - s);
+    const int t = threadIdx.x, w = t >> 6, ln = lane_id();
+    if (n > BK_LCAP) {                                      // too large for LDS: the host redoes on the general sort
+        if (t == 0) {
+            atomicOr(&b.st->overflow, 1ull);
+            atomicMax(&b.st->bk_max, (unsigned long long)n);
+        }
+        return;
+    }
+    // the bucket's range of (leave, watcher): [lo, hi_max)
+    const uint32_t stride = BK_NSPLIT / NB;
+    const uint32_t W = (uint32_t)b.wbits;
+    const uint32_t lo = bk ? b.bk_split[bk * stride] : 0u;
+    const uint32_t hi_max = bk + 1 < NB ? b.bk_split[(bk + 1) * stride] : (2u << W);
+    const uint32_t span = hi_max - lo;
+    int bsh = 0;
+    while (((span - 1) >> bsh) >= (uint32_t)BK_HBINS) ++bsh;
+    const uint32_t nbins = ((span - 1) >> bsh) + 1;
+    const uint64_t lo64 = (uint64_t)lo << W;
+    const int bsw = bsh + (int)W;                           // bin = (key - lo<<W) >> (W + bsh)
+    for (uint32_t i = t; i < nbins; i += BK_SNT) hb[i] = 0;
+    if (t == 0) n_long = 0;
+    __syncthreads();
+    uint64_t key[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        const uint32_t i = (uint32_t)t + (uint32_t)k * BK_SNT;
+        key[k] = i < n ? b.bk_b[s + i] - lo64 : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        const uint32_t i = (uint32_t)t + (uint32_t)k * BK_SNT;
+        if (i < n) atomicAdd(&hb[(uint32_t)(key[k] >> bsw)], 1u);
+    }
+    __syncthreads();
+    constexpr int PER = BK_HBINS / BK_SNT;                  // consecutive bins per thread
+    uint32_t c[PER], sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = (uint32_t)t * PER + q;
+        c[q] = i < nbins ? hb[i] : 0u;
+        sum += c[q];
+    }
+    uint32_t run = bk_block_excl<BK_SNT>(sum, red);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = (uint32_t)t * PER + q;
+        if (i < nbins) hb[i] = run;
+        if (c[q] > (uint32_t)BK_SHORT) longs[atomicAdd(&n_long, 1u)] = make_uint2(run, c[q]);
+        run += c[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        const uint32_t i = (uint32_t)t + (uint32_t)k * BK_SNT;
+        if (i < n) L[atomicAdd(&hb[(uint32_t)(key[k] >> bsw)], 1u)] = key[k];
+    }
+    __syncthreads();                                        // hb[x] = end of bin x = start of bin x + 1
+    const uint32_t wm = (1u << W) - 1u;
+    if (MODE == 1) {                                        // (timing probe: placement only)
+        for (uint32_t i = t; i < n; i += BK_SNT) {
+            const uint64_t v = L[i] + lo64;
+            gw_event ev;
+            ev.watcher = (uint32_t)(v >> W) & wm;
+            ev.target = (uint32_t)v & wm;
+            b.ev[s + i] = ev;
+        }
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        const uint32_t i = (uint32_t)t + (uint32_t)k * BK_SNT;
+        if (i >= n) continue;
+        const uint32_t x = (uint32_t)(key[k] >> bsw);
+        const uint32_t r0 = x ? hb[x - 1] : 0u, r1 = hb[x];
+        if (r1 - r0 > (uint32_t)BK_SHORT) continue;        // a wave sorts the long bins
+        uint32_t r = r0;
+        for (uint32_t j = r0; j < r1; ++j) r += L[j] < key[k];
+        const uint64_t v = key[k] + lo64;
+        gw_event ev;
+        ev.watcher = (uint32_t)(v >> W) & wm;
+        ev.target = (uint32_t)v & wm;
+        b.ev[s + r] = ev;
+    }
+    const uint32_t nl = n_long;
+    for (uint32_t q = (uint32_t)w; q < nl; q += BK_SNT / 64) {
+        const uint2 g = longs[q];
+        uint64_t* R = L + g.x;
+        bitonic_inplace<64>(R, g.y, ln, [](uint64_t v) { return v; }, [] { wave_sync(); });
+        for (uint32_t i = (uint32_t)ln; i < g.y; i += 64) {
+            const uint64_t v = R[i] + lo64;
+            gw_event ev;
+            ev.watcher = (uint32_t)(v >> W) & wm;
+            ev.target = (uint32_t)v & wm;
+            b.ev[s + g.x + i] = ev;
+        }
+        wave_sync();
+    }
+}
+
+// quantiles of this tick's sorted (leave, watcher) keys: the next tick's
+// bucket bounds (BK_NSPLIT of them; a tick with fewer buckets takes every
+// (BK_NSPLIT / NB)-th).  Kept when the tick overflowed or had no events.
+__global__ void __launch_bounds__(NT) k_bk_split(TickBufs b) {
+    const uint64_t E = lo32(b.st->ev_pk) + hi32(b.st->ev_pk), ne = lo32(b.st->ev_pk);
+    if (E == 0 || E > b.ev_cap || b.st->overflow) return;
+    const uint32_t lvb = 1u << b.wbits;
+    for (uint32_t j = 1 + threadIdx.x; j < BK_NSPLIT; j += NT) {
+        const uint64_t p = (uint64_t)j * E / BK_NSPLIT;
+        b.bk_split[j] = (p >= ne ? lvb : 0u) | b.ev[p].watcher;
+    }
+}
+// uniform bounds over the key range [0, 2^(wbits+1))
+__global__ void __launch_bounds__(NT) k_bk_split_init(uint32_t* sp, int wbits) {
+    for (uint32_t j = threadIdx.x; j < BK_NSPLIT; j += NT)
+        sp[j] = (uint32_t)(((uint64_t)j << (wbits + 1)) / BK_NSPLIT);
+}
+void launch_bk_split_init(uint32_t* sp, int wbits, hipStream_t s) {
+    hipLaunchKernelGGL(k_bk_split_init, dim3(1), dim3(NT), 0, s, sp, wbits);
 }
 
 void tick_diff(const TickBufs& b, hipStream_t s) {
@@ -854,10 +1157,23 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.mcnt, (uint64_t*)b.moff, b.m, nml, sc,
                                        (uint64_t*)&b.st->ev_pk, s);
     hipLaunchKernelGGL(k_chunk_first, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_flatten, dim3(nblk1((b.ev_cap + 63) / 64, NWAVE)), dim3(NT), 0, s, b);
-    // one stable sort by (leave, watcher); the last pass writes gw_event
-    radix_sort2(b.fk0, b.fv0, b.fk1, b.fv1, b.ev_cap, (const uint64_t*)&b.st->n_sort, 0, b.wbits + 1, b.rtable, s,
-                b.ev, (1u << b.wbits) - 1u);
+    if (!b.ev_full) {
+        const uint32_t NB = 1u << b.bk_bits;
+        hipLaunchKernelGGL(k_flatten, dim3(nblk1((b.ev_cap + 63) / 64, NWAVE)), dim3(NT), 0, s, b);
+        hipLaunchKernelGGL(k_bk_count, dim3(b.bk_tiles), dim3(BK_NT), 0, s, b);
+        scan_exclusive<uint32_t, uint32_t>(b.bk_cnt, b.bk_cnt, (uint64_t)NB * b.bk_tiles, nullptr, sc,
+                                           (uint32_t*)nullptr, s);
+        hipLaunchKernelGGL(k_bucket_scatter, dim3(b.bk_tiles), dim3(BK_NT), 0, s, b);
+        static const int probe = getenv("GW_BK_PROBE") ? atoi(getenv("GW_BK_PROBE")) : 0;
+        if (probe == 1) hipLaunchKernelGGL(k_bucket_sort<1>, dim3(NB), dim3(BK_SNT), 0, s, b);
+        else hipLaunchKernelGGL(k_bucket_sort<0>, dim3(NB), dim3(BK_SNT), 0, s, b);
+    } else {
+        hipLaunchKernelGGL(k_flatten, dim3(nblk1((b.ev_cap + 63) / 64, NWAVE)), dim3(NT), 0, s, b);
+        // one stable sort by (leave, watcher); the last pass writes gw_event
+        radix_sort2(b.fk0, b.fv0, b.fk1, b.fv1, b.ev_cap, (const uint64_t*)&b.st->n_sort, 0, b.wbits + 1,
+                    b.rtable, s, b.ev, (1u << b.wbits) - 1u);
+    }
+    hipLaunchKernelGGL(k_bk_split, dim3(1), dim3(NT), 0, s, b);
     (void)nmax;
 }
 

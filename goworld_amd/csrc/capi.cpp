@@ -451,7 +451,7 @@ void gw_shutdown(gw_ctx* c) {
     if (c->st) (void)hipStreamSynchronize(c->st);
     DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1,
                       &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
-                      &c->mcnt, &c->moff, &c->minfo, &c->mreg, &c->chunk_first, &c->fk0, &c->fv0, &c->fk1, &c->fv1, &c->ev_d, &c->rtable,
+                      &c->mcnt, &c->moff, &c->minfo, &c->mreg, &c->chunk_first, &c->bk_a, &c->bk_b, &c->bk_id, &c->bk_cnt, &c->bk_split, &c->ev_d, &c->rtable,
                       &c->scan_status, &c->rs_hist,
                       &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
                       &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf, &c->cl_slot, &c->cl_off,
@@ -696,20 +696,41 @@ int gw_set_clients(gw_ctx* c, const uint32_t* slots, const uint16_t* gates, uint
 static int ensure_events(gw_ctx* c) {
     int r;
     if ((r = ensure(c, c->own, c->own_cap * 4)) || (r = ensure(c, c->mir, c->own_cap * 8)) ||
-        (r = ensure(c, c->fk0, c->ev_cap * 4)) || (r = ensure(c, c->fv0, c->ev_cap * 4)) ||
-        (r = ensure(c, c->fk1, c->ev_cap * 4)) || (r = ensure(c, c->fv1, c->ev_cap * 4)) ||
+        (r = ensure(c, c->bk_a, c->ev_cap * 8)) || (r = ensure(c, c->bk_b, c->ev_cap * 8)) ||
+        (r = ensure(c, c->bk_id, c->ev_cap * 2)) ||
         (r = ensure(c, c->ev_d, c->ev_cap * sizeof(gw_event))) ||
         (r = ensure(c, c->chunk_first, (c->ev_cap / 64 + 1) * 4)) ||
         (r = ensure(c, c->rtable, radix2_scratch(c->ev_cap) * 4 + 64)))
         return r;
+    const uint64_t tiles = (c->ev_cap + BK_TILE - 1) / BK_TILE;
+    if ((r = ensure(c, c->bk_cnt, (tiles << BK_MAXBITS) * 4)) || (r = ensure_scan(c, tiles << BK_MAXBITS)) ||
+        (r = ensure(c, c->bk_split, BK_NSPLIT * 4)))
+        return r;
     return 0;
+}
+
+// buckets for the expected event count: mean about BK_MEAN; the general sort
+// when even the most buckets would average over BK_LCAP / 2, or for a while
+// after a bucket overflowed
+static void choose_buckets(gw_ctx* c, TickBufs& b, bool full = false) {
+    const uint64_t est = std::max<uint64_t>(c->ev_est, 1);
+    int bits = 1;
+    while (bits < BK_MAXBITS && (est >> bits) > BK_MEAN) ++bits;
+    bits = std::min(bits, b.wbits + 1);
+    b.bk_bits = bits;
+    b.ev_full = full || c->ev_full_ticks > 0 || (est >> bits) > (uint64_t)BK_LCAP / 2 || b.wbits > 26;
 }
 
 static void bind_events(gw_ctx* c, TickBufs& b) {
     b.own_cap = c->own_cap;
     b.own = P<uint32_t>(c->own); b.mir = P<uint64_t>(c->mir);
-    b.fk0 = P<uint32_t>(c->fk0); b.fv0 = P<uint32_t>(c->fv0);
-    b.fk1 = P<uint32_t>(c->fk1); b.fv1 = P<uint32_t>(c->fv1);
+    b.bk_a = P<uint64_t>(c->bk_a); b.bk_b = P<uint64_t>(c->bk_b);
+    b.fk0 = P<uint32_t>(c->bk_a); b.fv0 = b.fk0 + c->ev_cap;
+    b.fk1 = P<uint32_t>(c->bk_b); b.fv1 = b.fk1 + c->ev_cap;
+    b.bk_cnt = P<uint32_t>(c->bk_cnt);
+    b.bk_id = P<uint16_t>(c->bk_id);
+    b.bk_split = P<uint32_t>(c->bk_split);
+    b.bk_tiles = (uint32_t)((c->ev_cap + BK_TILE - 1) / BK_TILE);
     b.ev = P<gw_event>(c->ev_d);
     b.chunk_first = P<uint32_t>(c->chunk_first);
     b.ev_cap = c->ev_cap;
@@ -743,10 +764,17 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         const uint64_t E = (c->hstats->ev_pk & 0xffffffffull) + (c->hstats->ev_pk >> 32);
         if (c->hstats->cand_total > c->own_cap) c->own_cap = c->hstats->cand_total + c->hstats->cand_total / 4 + 4096;
         if (E > c->ev_cap) c->ev_cap = E + E / 4 + 4096;
+        // a bucket outgrew the LDS sort: this attempt on the general sort (its
+        // output gives the next tick quantile bounds); twice running, the
+        // general sort for a while
+        const bool bk_over = c->hstats->bk_max != 0;
+        if (bk_over && ++c->bk_overflows >= 2) c->ev_full_ticks = 16;
+        c->ev_est = std::max(c->ev_est, E);
         if ((rc = ensure_events(c))) return rc;
         bind_events(c, b);
+        choose_buckets(c, b, bk_over || b.ev_full);
         DevStats* h = c->hstats;
-        h->overflow = 0; h->n_big = 0; h->ev_pk = 0; h->n_mlist = 0; h->n_sort = 0;
+        h->overflow = 0; h->n_big = 0; h->ev_pk = 0; h->n_mlist = 0; h->n_sort = 0; h->bk_max = 0;
         for (int i = 0; i < STAT_SHARDS; ++i)      // the diff's shards restart; the mover count stays
             for (int f = 0; f < SH_FIELDS; ++f)
                 if (f != SH_MOVERS) h->shard[i][f] = 0;
@@ -769,6 +797,9 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     c->h_present = hs.n_present;
     gw_tick_out o{};
     const uint64_t n_enter = hs.ev_pk & 0xffffffffull, n_leave = hs.ev_pk >> 32;
+    if (!(flags & GW_TICK_NO_EVENTS)) c->ev_est = n_enter + n_leave;   // sizes the next tick's buckets
+    if (c->ev_full_ticks > 0) --c->ev_full_ticks;
+    if (!b.ev_full) c->bk_overflows = 0;
     uint64_t n_mov = 0;
     for (int i = 0; i < STAT_SHARDS; ++i) n_mov += hs.shard[i][SH_MOVERS];
     // candidates tested == the candidate bounds; a_old | a_new << 32 per shard
@@ -942,6 +973,12 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.minfo = P<uint4>(c->minfo); b.mreg = P<unsigned long long>(c->mreg);
     b.wbits = ceil_log2(C);
     bind_events(c, b);
+    if (!c->ev_est) c->ev_est = 16ull * M;
+    choose_buckets(c, b);
+    if (c->bk_split_w != b.wbits) {                  // slot bits changed: uniform bounds until a tick's quantiles
+        launch_bk_split_init(b.bk_split, b.wbits, c->st);
+        c->bk_split_w = b.wbits;
+    }
 
     prof_begin(c, "ops");
     tick_ops(b, c->st);

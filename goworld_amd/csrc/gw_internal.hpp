@@ -91,6 +91,7 @@ struct DevStats {
     unsigned long long n_mlist;       // movers with events (slot-ordered list)
     unsigned long long n_sort;        // events flattened for the sort (min(E, ev_cap))
     unsigned long long overflow;      // event regions exceeded their capacity
+    unsigned long long bk_max;        // largest event bucket too big for the LDS sort (0: none)
     unsigned long long bad_ops;
     unsigned long long flagged;       // sync: flagged entities
     unsigned long long rec_total;     // sync: records
@@ -188,13 +189,33 @@ struct TickBufs {
     uint4* minfo;             // [m] listed mover: slot, own events, mirror events
     unsigned long long* mreg; // [m] its region offset
     uint32_t* chunk_first;    // [ev_cap / 64] listed mover holding flat position 64c
-    uint32_t *fk0, *fv0, *fk1, *fv1;   // [ev_cap] flattened events: key leave<<wbits | watcher, value target
+    uint32_t *fk0, *fv0, *fk1, *fv1;   // [ev_cap] general sort: key leave<<wbits | watcher, value target
+                                       // (aliases of bk_a / bk_b)
+    uint64_t *bk_a, *bk_b;    // [ev_cap] bucket path: (leave<<wbits | watcher) << 32 | target
+    uint16_t* bk_id;          // [ev_cap] bucket of each flat event
+    uint32_t* bk_cnt;         // [NB * bk_tiles] per (bucket, tile) counts, scanned in place
+    uint32_t bk_tiles;        // tiles of BK_TILE flat positions covering ev_cap
+    uint32_t* bk_split;       // [BK_NSPLIT] bucket bounds: quantiles of the last tick's keys
+    int bk_bits;              // log2 of the bucket count (<= BK_MAXBITS, <= wbits + 1)
+    int ev_full;              // 1: general stable radix sort instead of the bucket path
     gw_event* ev;             // [ev_cap] canonical events, enters then leaves
     uint64_t ev_cap;
     uint32_t* rtable;         // radix_sort2 scratch
     int wbits;                // bits of a slot
     int diff_u;               // candidate chunks of 64 in flight per k_mover iteration
 };
+
+// events bucket path (aoi.hip k_flat_count / k_bucket_scatter / k_bucket_sort)
+constexpr int BK_NT = 1024;           // threads of the tile kernels
+constexpr int BK_TILE = 8192;         // flat positions per tile
+constexpr int BK_MAXBITS = 10;        // at most 1024 buckets (one per tile thread)
+constexpr int BK_LCAP = 8192;         // events a bucket may hold (LDS sort)
+constexpr int BK_SNT = 512;           // threads of the bucket sort
+constexpr int BK_HBINS = 3072;        // bins of the counting sort inside a bucket
+constexpr int BK_SHORT = 16;          // longer bins are sorted by a wave
+constexpr uint64_t BK_MEAN = 2048;    // target mean bucket size when choosing bk_bits
+constexpr uint32_t BK_NSPLIT = 1u << BK_MAXBITS;   // quantile table size
+void launch_bk_split_init(uint32_t* sp, int wbits, hipStream_t s);
 
 // ---- launchers --------------------------------------------------------------
 // full rebuild of the grid (spaces created, first use): stable radix sort of

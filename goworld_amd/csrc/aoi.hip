@@ -600,7 +600,7 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
                     t_cli = rn && (e.info & CAND_CLIENT) != 0;
                     ev = ro != rn;
                     lv = ro;
-                    key = (e.slot << 1) | (lv ? 1u : 0u);
+                    key = (lv ? 0x80000000u : 0u) | e.slot;      // own events sort as (leave, target)
                 }
             }
             // statistics as wave-uniform ballot counts (no cross-lane sums at the end)
@@ -746,8 +746,26 @@ __global__ void __launch_bounds__(NT) k_mover_counts(TickBufs b) {
     const uint32_t m = b.gmi[A];
     const uint64_t oc = b.ownc[m], mc = b.mirc[m];
     b.mcnt[k] = oc + mc;
-    b.minfo[k] = make_uint4(A, (uint32_t)(lo32(oc) + hi32(oc)), (uint32_t)(lo32(mc) + hi32(mc)), 0u);
+    const uint32_t nm = (uint32_t)(lo32(mc) + hi32(mc));
+    b.minfo[k] = make_uint4(A, (uint32_t)lo32(oc), (uint32_t)hi32(oc), nm);
     b.mreg[k] = b.reg[m];
+    // bucket path: items = one per nonempty own run (enters, leaves) + one per mirror event
+    b.icnt[k] = (lo32(oc) ? 1u : 0u) + (hi32(oc) ? 1u : 0u) + nm;
+}
+// bucket path: the event totals (the general path takes them from the scan of mcnt)
+__global__ void __launch_bounds__(NT) k_event_totals(TickBufs b) {
+    __shared__ unsigned long long red[NWAVE];
+    const uint64_t n = b.st->n_mlist;
+    unsigned long long a = 0;
+    for (uint64_t k = (uint64_t)blockIdx.x * NT + threadIdx.x; k < n; k += (uint64_t)gridDim.x * NT) a += b.mcnt[k];
+    a = wave_sum<unsigned long long>(a);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a = 0;
+        for (int i = 0; i < NWAVE; ++i) a += red[i];
+        if (a) atomicAdd(&b.st->ev_pk, a);
+    }
 }
 
 // (3) the listed movers' events flattened at their scanned offsets, in list
@@ -765,7 +783,15 @@ __global__ void __launch_bounds__(NT) k_chunk_first(TickBufs b) {
     const uint64_t off = b.moff[k];
     const uint64_t at = lo32(off) + hi32(off);
     const uint4 mi = b.minfo[k];
-    const uint64_t end = at + mi.y + mi.z;
+    const uint64_t end = at + mi.y + mi.z + mi.w;
+    for (uint64_t c = (at + 63) >> 6; (c << 6) < end; ++c) b.chunk_first[c] = (uint32_t)k;
+}
+__global__ void __launch_bounds__(NT) k_chunk_first_items(TickBufs b) {
+    const uint64_t k = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= b.st->n_mlist) return;
+    if (lo32(b.st->ev_pk) + hi32(b.st->ev_pk) > b.ev_cap) return;   // overflow: nothing is flattened (redo)
+    const uint64_t at = b.ioff[k];
+    const uint64_t end = at + b.icnt[k];
     for (uint64_t c = (at + 63) >> 6; (c << 6) < end; ++c) b.chunk_first[c] = (uint32_t)k;
 }
 // element p = 64c + lane of the flat list (wave-uniform c; every lane runs
@@ -782,7 +808,7 @@ __device__ __forceinline__ bool flat_elem(const TickBufs& b, uint64_t c, uint64_
         mi = b.minfo[k];
         reg = b.mreg[k];
         at = lo32(off) + hi32(off);
-        end = at + mi.y + mi.z;
+        end = at + mi.y + mi.z + mi.w;
     }
     const uint64_t p = (c << 6) + ln;
     // first lane q whose mover ends after p (ends ascend with the lane)
@@ -801,14 +827,14 @@ __device__ __forceinline__ bool flat_elem(const TickBufs& b, uint64_t c, uint64_
                          (uint32_t)__shfl((int)(uint32_t)at, q, 64);
     const uint64_t qreg = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(reg >> 32), q, 64) << 32) |
                           (uint32_t)__shfl((int)(uint32_t)reg, q, 64);
-    const uint32_t qA = (uint32_t)__shfl((int)mi.x, q, 64), qn = (uint32_t)__shfl((int)mi.y, q, 64);
+    const uint32_t qA = (uint32_t)__shfl((int)mi.x, q, 64), qn = (uint32_t)__shfl((int)(mi.y + mi.z), q, 64);
     if (p >= E) return false;
     const uint32_t j = (uint32_t)(p - qat);                 // index inside mover q's events
     const uint32_t lvb = 1u << b.wbits;
     if (j < qn) {
         const uint32_t e = b.own[qreg + j];
-        key = ((e & 1u) ? lvb : 0u) | qA;
-        val = e >> 1;
+        key = ((e >> 31) ? lvb : 0u) | qA;
+        val = e & 0x7fffffffu;
     } else {
         const uint64_t e = b.mir[qreg + (j - qn)];
         key = ((e & 1u) ? lvb : 0u) | (uint32_t)hi32(e);
@@ -831,12 +857,72 @@ __global__ void __launch_bounds__(NT) k_flatten(TickBufs b) {
     uint32_t key, val;
     if (!flat_elem(b, c, E, key, val)) return;
     const uint64_t p = (c << 6) + lane_id();
-    if (b.ev_full) {
-        b.fk0[p] = key;
-        b.fv0[p] = val;
-    } else {
-        b.bk_a[p] = ((uint64_t)key << b.wbits) | val;      // (leave, watcher, target)
+    b.fk0[p] = key;
+    b.fv0[p] = val;
+}
+
+// Bucket path items (u64): a mirror event (leave, watcher W, target A) is
+// (leave<<wbits | W) << wbits | A; an own run of mover A (all its enters, or
+// all its leaves; a mover's own events are sorted by (leave, target)) is
+// BK_RUN | (leave<<wbits | A) << wbits | k (k: its listed-mover index).  A
+// (leave, watcher) key holds one run (the watcher moved) or mirror events
+// only (it did not), so items sort by their masked key and runs expand to
+// their events at output time.
+constexpr int BK_RUN_BIT = 53;
+constexpr uint64_t BK_RUN = 1ull << BK_RUN_BIT;
+__global__ void __launch_bounds__(NT) k_flat_items(TickBufs b) {
+    const uint64_t E = lo32(b.st->ev_pk) + hi32(b.st->ev_pk);
+    const uint64_t NI = b.st->n_items;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (E > b.ev_cap) atomicOr(&b.st->overflow, 1ull);
+        b.st->n_sort = E > b.ev_cap ? 0 : NI;
     }
+    if (E > b.ev_cap) return;
+    const uint64_t c = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
+    if ((c << 6) >= NI) return;
+    const int ln = lane_id();
+    const uint64_t nl_ = b.st->n_mlist;
+    const uint32_t q0 = b.chunk_first[c];
+    const uint64_t k = (uint64_t)q0 + ln;
+    uint32_t at = 0xffffffffu, end = 0xffffffffu;
+    uint4 mi = make_uint4(0, 0, 0, 0);
+    uint64_t reg = 0;
+    if (k < nl_) {
+        at = b.ioff[k];
+        end = at + b.icnt[k];
+        mi = b.minfo[k];
+        reg = b.mreg[k];
+    }
+    const uint32_t p = (uint32_t)((c << 6) + ln);
+    uint32_t lo = 0, hi = 64;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+        const uint32_t mid = min((lo + hi) >> 1, 63u);
+        const uint32_t e = (uint32_t)__shfl((int)end, (int)mid, 64);
+        if (lo < hi) {
+            if (e <= p) lo = mid + 1; else hi = mid;
+        }
+    }
+    const int q = (int)min(lo, 63u);
+    const uint32_t qat = (uint32_t)__shfl((int)at, q, 64);
+    const uint64_t qreg = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(reg >> 32), q, 64) << 32) |
+                          (uint32_t)__shfl((int)(uint32_t)reg, q, 64);
+    const uint32_t qA = (uint32_t)__shfl((int)mi.x, q, 64);
+    const uint32_t qe = (uint32_t)__shfl((int)mi.y, q, 64), ql = (uint32_t)__shfl((int)mi.z, q, 64);
+    if (p >= NI) return;
+    const uint32_t W = (uint32_t)b.wbits;
+    const uint32_t lvb = 1u << W;
+    const uint32_t j = p - qat;
+    const uint32_t nr = (qe ? 1u : 0u) + (ql ? 1u : 0u);
+    uint64_t item;
+    if (j < nr) {
+        const bool leave = (j == 1) || !qe;
+        item = BK_RUN | ((uint64_t)((leave ? lvb : 0u) | qA) << W) | (q0 + (uint32_t)q);
+    } else {
+        const uint64_t e = b.mir[qreg + (j - nr)];
+        item = ((uint64_t)(((e & 1u) ? lvb : 0u) | (uint32_t)hi32(e)) << W) | (uint32_t)(lo32(e) >> 1);
+    }
+    b.bk_a[p] = item;
 }
 
 // (4) bucket path.  Events are keyed by the full (leave, watcher, target) —
@@ -892,18 +978,28 @@ __device__ __forceinline__ uint32_t bk_bucket(const BkLut& L, int lsh, uint32_t 
     return lo;
 }
 
+// events an item stands for (a run: its mover's enters or leaves)
+__device__ __forceinline__ uint32_t bk_weight(const TickBufs& b, uint64_t item) {
+    if (!(item & BK_RUN)) return 1u;
+    const uint32_t W = (uint32_t)b.wbits;
+    const uint4 mi = b.minfo[(uint32_t)item & ((1u << W) - 1u)];
+    return ((item >> (2 * W)) & 1u) ? mi.z : mi.y;
+}
+
+// per (bucket, tile): items | events << 32
 __global__ void __launch_bounds__(BK_NT) k_bk_count(TickBufs b) {
-    __shared__ uint32_t h[1 << BK_MAXBITS];
+    __shared__ uint32_t h[1 << BK_MAXBITS], hw[1 << BK_MAXBITS];
     __shared__ BkLut lut;
     const int t = threadIdx.x;
     const uint32_t NB = 1u << b.bk_bits;
-    for (uint32_t i = t; i < NB; i += BK_NT) h[i] = 0;
+    for (uint32_t i = t; i < NB; i += BK_NT) h[i] = hw[i] = 0;
     const uint64_t n = b.st->n_sort;
     const uint64_t base = (uint64_t)blockIdx.x * BK_TILE;
     if (base < n) {                                         // block-uniform
         int lsh;
         bk_lut_build(b, lut, NB, lsh);                      // (syncs)
         const int W = b.wbits;
+        const uint64_t km = (1ull << (2 * W + 1)) - 1;
         constexpr int IPT = BK_TILE / BK_NT;
         uint64_t k[IPT];
 #pragma unroll
@@ -911,18 +1007,26 @@ __global__ void __launch_bounds__(BK_NT) k_bk_count(TickBufs b) {
             const uint64_t i = base + (uint64_t)j * BK_NT + t;
             k[j] = i < n ? b.bk_a[i] : 0ull;
         }
+        uint32_t wt[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint64_t i = base + (uint64_t)j * BK_NT + t;
+            wt[j] = i < n ? bk_weight(b, k[j]) : 0u;
+        }
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
             const uint64_t i = base + (uint64_t)j * BK_NT + t;
             if (i < n) {
-                const uint32_t q = bk_bucket(lut, lsh, (uint32_t)(k[j] >> W));
+                const uint32_t q = bk_bucket(lut, lsh, (uint32_t)((k[j] & km) >> W));
                 b.bk_id[i] = (uint16_t)q;
                 atomicAdd(&h[q], 1u);
+                atomicAdd(&hw[q], wt[j]);
             }
         }
     }
     __syncthreads();
-    for (uint32_t i = t; i < NB; i += BK_NT) b.bk_cnt[(uint64_t)i * b.bk_tiles + blockIdx.x] = h[i];
+    for (uint32_t i = t; i < NB; i += BK_NT)
+        b.bk_cnt[(uint64_t)i * b.bk_tiles + blockIdx.x] = (unsigned long long)h[i] | ((unsigned long long)hw[i] << 32);
 }
 
 // exclusive scan of one value per thread over a block of NTH threads
@@ -969,7 +1073,7 @@ __global__ void __launch_bounds__(BK_NT) k_bucket_scatter(TickBufs b) {
     const uint32_t toff = bk_block_excl<BK_NT>(cnt, red);
     if (t < (int)NB) {
         h[t] = toff;
-        go[t] = b.bk_cnt[(uint64_t)t * b.bk_tiles + blockIdx.x] - toff;   // mod 2^32: dst = go + staged index
+        go[t] = (uint32_t)b.bk_cnt[(uint64_t)t * b.bk_tiles + blockIdx.x] - toff;   // mod 2^32: dst = go + staged index
     }
     __syncthreads();
 #pragma unroll
@@ -985,28 +1089,32 @@ __global__ void __launch_bounds__(BK_NT) k_bucket_scatter(TickBufs b) {
     }
 }
 
-// One bucket per block: a counting sort of its events by bin = (leave,
-// watcher - floor) >> bsh into at most BK_HBINS bins (bsh = 0 unless the
-// bucket spans a wide, sparse key range).  A short bin (<= BK_SHORT events,
-// the common case) places each event at the bin start + the bin's events
-// with a smaller (leave, watcher, target) key; a longer bin (a moving
-// hotspot watcher's own events) is sorted in place by one wave (bitonic) and
-// written as a run.
-template <int MODE>
+// One bucket per block.  Its items are counting-sorted by bin = (leave,
+// watcher - floor) >> bsh (at most BK_HBINS bins; bsh = 0 unless the bucket
+// spans a wide, sparse key range) and each bin is sorted in place by the
+// masked key (a thread for <= BK_SHORT items, else a wave); the items' event
+// counts are then prefix-summed in that order (the bucket's base comes from
+// the scanned count table), mirror events are written by their lane and own
+// runs are copied from the mover's own-event region by a wave.
 __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
     __shared__ uint64_t L[BK_LCAP];
     __shared__ uint32_t hb[BK_HBINS];
     __shared__ uint32_t red[BK_SNT / 64];
-    __shared__ uint2 longs[BK_LCAP / (BK_SHORT + 1) + 1];
-    __shared__ uint32_t n_long;
-    constexpr int CH = BK_LCAP / BK_SNT;                    // max keys per thread
+    __shared__ uint16_t longs[BK_LCAP / (BK_SHORT + 1) + 1];   // bins sorted by a wave
+    __shared__ uint4 runs[BK_RUNS];                            // (dst, src, len, watcher)
+    __shared__ uint32_t n_long, n_runs;
+    constexpr int NWV = BK_SNT / 64;
+    constexpr int CH = BK_LCAP / BK_SNT;                    // max items per thread
+    constexpr int WCH = BK_LCAP / BK_SNT;                   // max chunks of 64 per wave
     const uint32_t bk = blockIdx.x;
     const uint32_t NB = 1u << b.bk_bits;
     const uint64_t T = b.bk_tiles;
     const uint64_t n_all = b.st->n_sort;
-    const uint64_t s = b.bk_cnt[(uint64_t)bk * T];
-    const uint64_t e = bk + 1 < NB ? b.bk_cnt[(uint64_t)(bk + 1) * T] : n_all;
+    const unsigned long long c0 = b.bk_cnt[(uint64_t)bk * T];
+    const uint64_t s = lo32(c0);
+    const uint64_t e = bk + 1 < NB ? lo32(b.bk_cnt[(uint64_t)(bk + 1) * T]) : n_all;
     if (e <= s) return;
+    const uint32_t wbase = (uint32_t)hi32(c0);              // events of the earlier buckets
     const uint32_t n = (uint32_t)(e - s);
     const int t = threadIdx.x, w = t >> 6, ln = lane_id();
     if (n > BK_LCAP) {                                      // too large for LDS: the host redoes on the general sort
@@ -1016,7 +1124,6 @@ __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
         }
         return;
     }
-    // the bucket's range of (leave, watcher): [lo, hi_max)
     const uint32_t stride = BK_NSPLIT / NB;
     const uint32_t W = (uint32_t)b.wbits;
     const uint32_t lo = bk ? b.bk_split[bk * stride] : 0u;
@@ -1025,21 +1132,21 @@ __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
     int bsh = 0;
     while (((span - 1) >> bsh) >= (uint32_t)BK_HBINS) ++bsh;
     const uint32_t nbins = ((span - 1) >> bsh) + 1;
-    const uint64_t lo64 = (uint64_t)lo << W;
-    const int bsw = bsh + (int)W;                           // bin = (key - lo<<W) >> (W + bsh)
+    const uint64_t km = (1ull << (2 * W + 1)) - 1;          // (leave, watcher, target) bits
     for (uint32_t i = t; i < nbins; i += BK_SNT) hb[i] = 0;
-    if (t == 0) n_long = 0;
+    if (t == 0) n_long = n_runs = 0;
     __syncthreads();
     uint64_t key[CH];
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
         const uint32_t i = (uint32_t)t + (uint32_t)k * BK_SNT;
-        key[k] = i < n ? b.bk_b[s + i] - lo64 : 0ull;
+        key[k] = i < n ? b.bk_b[s + i] : 0ull;
     }
+#define BK_BIN(v) ((uint32_t)((((v) & km) >> W) - lo) >> bsh)
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
         const uint32_t i = (uint32_t)t + (uint32_t)k * BK_SNT;
-        if (i < n) atomicAdd(&hb[(uint32_t)(key[k] >> bsw)], 1u);
+        if (i < n) atomicAdd(&hb[BK_BIN(key[k])], 1u);
     }
     __syncthreads();
     constexpr int PER = BK_HBINS / BK_SNT;                  // consecutive bins per thread
@@ -1051,59 +1158,161 @@ __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
         sum += c[q];
     }
     uint32_t run = bk_block_excl<BK_SNT>(sum, red);
+    uint32_t bstart[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = (uint32_t)t * PER + q;
+        bstart[q] = run;
         if (i < nbins) hb[i] = run;
-        if (c[q] > (uint32_t)BK_SHORT) longs[atomicAdd(&n_long, 1u)] = make_uint2(run, c[q]);
+        if (c[q] > (uint32_t)BK_SHORT) longs[atomicAdd(&n_long, 1u)] = (uint16_t)i;
         run += c[q];
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
         const uint32_t i = (uint32_t)t + (uint32_t)k * BK_SNT;
-        if (i < n) L[atomicAdd(&hb[(uint32_t)(key[k] >> bsw)], 1u)] = key[k];
+        if (i < n) L[atomicAdd(&hb[BK_BIN(key[k])], 1u)] = key[k];
     }
-    __syncthreads();                                        // hb[x] = end of bin x = start of bin x + 1
-    const uint32_t wm = (1u << W) - 1u;
-    if (MODE == 1) {                                        // (timing probe: placement only)
-        for (uint32_t i = t; i < n; i += BK_SNT) {
-            const uint64_t v = L[i] + lo64;
-            gw_event ev;
-            ev.watcher = (uint32_t)(v >> W) & wm;
-            ev.target = (uint32_t)v & wm;
-            b.ev[s + i] = ev;
-        }
-        return;
-    }
+#undef BK_BIN
+    __syncthreads();
+    // each bin in place by the masked key: short ones by the thread owning them
 #pragma unroll
-    for (int k = 0; k < CH; ++k) {
-        const uint32_t i = (uint32_t)t + (uint32_t)k * BK_SNT;
-        if (i >= n) continue;
-        const uint32_t x = (uint32_t)(key[k] >> bsw);
-        const uint32_t r0 = x ? hb[x - 1] : 0u, r1 = hb[x];
-        if (r1 - r0 > (uint32_t)BK_SHORT) continue;        // a wave sorts the long bins
-        uint32_t r = r0;
-        for (uint32_t j = r0; j < r1; ++j) r += L[j] < key[k];
-        const uint64_t v = key[k] + lo64;
-        gw_event ev;
-        ev.watcher = (uint32_t)(v >> W) & wm;
-        ev.target = (uint32_t)v & wm;
-        b.ev[s + r] = ev;
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t len = c[q];
+        if (len < 2 || len > (uint32_t)BK_SHORT) continue;
+        uint64_t* R = L + bstart[q];
+        for (uint32_t a = 1; a < len; ++a) {
+            const uint64_t v = R[a];
+            uint32_t j = a;
+            while (j > 0 && (R[j - 1] & km) > (v & km)) { R[j] = R[j - 1]; --j; }
+            R[j] = v;
+        }
     }
     const uint32_t nl = n_long;
-    for (uint32_t q = (uint32_t)w; q < nl; q += BK_SNT / 64) {
-        const uint2 g = longs[q];
-        uint64_t* R = L + g.x;
-        bitonic_inplace<64>(R, g.y, ln, [](uint64_t v) { return v; }, [] { wave_sync(); });
-        for (uint32_t i = (uint32_t)ln; i < g.y; i += 64) {
-            const uint64_t v = R[i] + lo64;
-            gw_event ev;
-            ev.watcher = (uint32_t)(v >> W) & wm;
-            ev.target = (uint32_t)v & wm;
-            b.ev[s + g.x + i] = ev;
+    for (uint32_t q = (uint32_t)w; q < nl; q += NWV) {
+        const uint32_t x = longs[q];
+        const uint32_t g0 = x ? hb[x - 1] : 0u, gn = hb[x] - g0;
+        uint64_t* R = L + g0;
+        if (gn <= 64) {                                     // in registers
+            uint64_t v = ln < (int)gn ? R[ln] : ~0ull;
+            const uint64_t sk = ln < (int)gn ? ((v & km) << 10) | (uint64_t)ln : ~0ull;   // masked key, then lane
+            const uint64_t o = wave_sort64_u64(sk);
+            const int from = (int)(o & 1023u);
+            const uint64_t moved = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), from & 63, 64) << 32) |
+                                   (uint32_t)__shfl((int)(uint32_t)v, from & 63, 64);
+            wave_sync();
+            if (ln < (int)gn) R[ln] = moved;
+        } else {
+            bitonic_inplace<64>(R, gn, ln, [km](uint64_t v) { return v & km; }, [] { wave_sync(); });
         }
         wave_sync();
+    }
+    __syncthreads();
+    // event offsets: the items' weights prefix-summed in sorted order (wave w
+    // takes [w*seg, (w+1)*seg) in chunks of 64); the runs' mover records are
+    // loaded for all chunks at once
+    const uint32_t seg = (((n + NWV - 1) / NWV) + 63) & ~63u;
+    const uint32_t w0 = (uint32_t)w * seg;
+    const uint32_t wm = (1u << W) - 1u;
+    uint64_t v[WCH];
+    uint32_t off[WCH], aux[WCH];
+#pragma unroll
+    for (int cc = 0; cc < WCH; ++cc) {
+        const uint32_t i = w0 + (uint32_t)cc * 64 + ln;
+        v[cc] = (cc * 64 < (int)seg && i < n) ? L[i] : 0ull;
+    }
+    uint4 mi[WCH];
+#pragma unroll
+    for (int cc = 0; cc < WCH; ++cc) {
+        mi[cc] = make_uint4(0, 0, 0, 0);
+        aux[cc] = 0;
+        if (v[cc] & BK_RUN) {
+            const uint32_t k = (uint32_t)v[cc] & wm;
+            mi[cc] = b.minfo[k];
+            aux[cc] = (uint32_t)b.mreg[k];
+        }
+    }
+    uint32_t carry = 0;
+#pragma unroll
+    for (int cc = 0; cc < WCH; ++cc) {
+        off[cc] = 0;
+        if (cc * 64 >= (int)seg) continue;                  // wave-uniform
+        const uint32_t i = w0 + (uint32_t)cc * 64 + ln;
+        const bool leave = ((v[cc] >> (2 * W)) & 1u) != 0;
+        const uint32_t wt = i >= n ? 0u : !(v[cc] & BK_RUN) ? 1u : (leave ? mi[cc].z : mi[cc].y);
+        const uint32_t inc = wave_incl_scan<uint32_t>(wt);
+        off[cc] = carry + inc - wt;
+        carry += (uint32_t)__shfl((int)inc, 63, 64);
+    }
+    if (ln == 63) red[w] = carry;
+    __syncthreads();
+    uint32_t wpre = wbase;
+    for (int k = 0; k < w; ++k) wpre += red[k];
+#pragma unroll
+    for (int cc = 0; cc < WCH; ++cc) {
+        if (cc * 64 >= (int)seg) continue;
+        const uint32_t i = w0 + (uint32_t)cc * 64 + ln;
+        if (i >= n) continue;
+        const uint32_t dst = wpre + off[cc];
+        if (!(v[cc] & BK_RUN)) {
+            gw_event ev;
+            ev.watcher = (uint32_t)(v[cc] >> W) & wm;
+            ev.target = (uint32_t)v[cc] & wm;
+            b.ev[dst] = ev;
+        } else {
+            const bool leave = ((v[cc] >> (2 * W)) & 1u) != 0;
+            const uint32_t len = leave ? mi[cc].z : mi[cc].y;
+            const uint32_t src = aux[cc] + (leave ? mi[cc].y : 0u);
+            const uint32_t q = atomicAdd(&n_runs, 1u);
+            if (q < (uint32_t)BK_RUNS) {
+                runs[q] = make_uint4(dst, src, len, mi[cc].x);
+            } else {                                        // list full: this lane copies
+                for (uint32_t j = 0; j < len; ++j) {
+                    gw_event ev;
+                    ev.watcher = mi[cc].x;
+                    ev.target = b.own[src + j] & 0x7fffffffu;
+                    b.ev[dst + j] = ev;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // own runs, flattened over the block: run prefix sums in hb (free now),
+    // each thread copies every 512th event (binary search for its run)
+    const uint32_t nr = min(n_runs, (uint32_t)BK_RUNS);
+    const uint32_t rl = (uint32_t)t < nr ? runs[t].z : 0u;  // BK_RUNS == BK_SNT: one run per thread
+    const uint32_t rpre = bk_block_excl<BK_SNT>(rl, red);
+    if ((uint32_t)t < nr) hb[t] = rpre;
+    if (t == BK_SNT - 1) hb[BK_RUNS] = rpre + rl;
+    __syncthreads();
+    const uint32_t tot = hb[BK_RUNS];
+    constexpr int CU = 4;
+    for (uint32_t e0 = (uint32_t)t; e0 < tot; e0 += CU * BK_SNT) {
+        uint32_t tg[CU], dd[CU], ww[CU];
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+            const uint32_t e1 = e0 + (uint32_t)u * BK_SNT;
+            dd[u] = 0xffffffffu;
+            if (e1 >= tot) continue;
+            uint32_t lo_ = 0, hi_ = nr;                     // last run with prefix <= e1
+            while (hi_ - lo_ > 1) {
+                const uint32_t mid = (lo_ + hi_) >> 1;
+                if (hb[mid] <= e1) lo_ = mid; else hi_ = mid;
+            }
+            const uint4 r = runs[lo_];
+            const uint32_t j = e1 - hb[lo_];
+            tg[u] = b.own[r.y + j];
+            dd[u] = r.x + j;
+            ww[u] = r.w;
+        }
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+            if (dd[u] == 0xffffffffu) continue;
+            gw_event ev;
+            ev.watcher = ww[u];
+            ev.target = tg[u] & 0x7fffffffu;
+            b.ev[dd[u]] = ev;
+        }
     }
 }
 
@@ -1154,20 +1363,21 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     sc.tbase += nb;
     const uint64_t* nml = (const uint64_t*)&b.st->n_mlist;
     hipLaunchKernelGGL(k_mover_counts, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
-    scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.mcnt, (uint64_t*)b.moff, b.m, nml, sc,
-                                       (uint64_t*)&b.st->ev_pk, s);
-    hipLaunchKernelGGL(k_chunk_first, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
     if (!b.ev_full) {
         const uint32_t NB = 1u << b.bk_bits;
-        hipLaunchKernelGGL(k_flatten, dim3(nblk1((b.ev_cap + 63) / 64, NWAVE)), dim3(NT), 0, s, b);
+        hipLaunchKernelGGL(k_event_totals, dim3(64), dim3(NT), 0, s, b);
+        scan_exclusive<uint32_t, uint32_t>(b.icnt, b.ioff, b.m, nml, sc, (uint32_t*)&b.st->n_items, s);
+        hipLaunchKernelGGL(k_chunk_first_items, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
+        hipLaunchKernelGGL(k_flat_items, dim3(nblk1((b.ev_cap + 63) / 64, NWAVE)), dim3(NT), 0, s, b);
         hipLaunchKernelGGL(k_bk_count, dim3(b.bk_tiles), dim3(BK_NT), 0, s, b);
-        scan_exclusive<uint32_t, uint32_t>(b.bk_cnt, b.bk_cnt, (uint64_t)NB * b.bk_tiles, nullptr, sc,
-                                           (uint32_t*)nullptr, s);
+        scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.bk_cnt, (uint64_t*)b.bk_cnt,
+                                           (uint64_t)NB * b.bk_tiles, nullptr, sc, (uint64_t*)nullptr, s);
         hipLaunchKernelGGL(k_bucket_scatter, dim3(b.bk_tiles), dim3(BK_NT), 0, s, b);
-        static const int probe = getenv("GW_BK_PROBE") ? atoi(getenv("GW_BK_PROBE")) : 0;
-        if (probe == 1) hipLaunchKernelGGL(k_bucket_sort<1>, dim3(NB), dim3(BK_SNT), 0, s, b);
-        else hipLaunchKernelGGL(k_bucket_sort<0>, dim3(NB), dim3(BK_SNT), 0, s, b);
+        hipLaunchKernelGGL(k_bucket_sort, dim3(NB), dim3(BK_SNT), 0, s, b);
     } else {
+        scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.mcnt, (uint64_t*)b.moff, b.m, nml, sc,
+                                           (uint64_t*)&b.st->ev_pk, s);
+        hipLaunchKernelGGL(k_chunk_first, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
         hipLaunchKernelGGL(k_flatten, dim3(nblk1((b.ev_cap + 63) / 64, NWAVE)), dim3(NT), 0, s, b);
         // one stable sort by (leave, watcher); the last pass writes gw_event
         radix_sort2(b.fk0, b.fv0, b.fk1, b.fv1, b.ev_cap, (const uint64_t*)&b.st->n_sort, 0, b.wbits + 1,

@@ -451,7 +451,7 @@ void gw_shutdown(gw_ctx* c) {
     if (c->st) (void)hipStreamSynchronize(c->st);
     DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1,
                       &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
-                      &c->mcnt, &c->moff, &c->minfo, &c->mreg, &c->chunk_first, &c->bk_a, &c->bk_b, &c->bk_id, &c->bk_cnt, &c->bk_split, &c->ev_d, &c->rtable,
+                      &c->mcnt, &c->moff, &c->minfo, &c->icnt, &c->ioff, &c->mreg, &c->chunk_first, &c->bk_a, &c->bk_b, &c->bk_id, &c->bk_cnt, &c->bk_split, &c->ev_d, &c->rtable,
                       &c->scan_status, &c->rs_hist,
                       &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
                       &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf, &c->cl_slot, &c->cl_off,
@@ -703,7 +703,7 @@ static int ensure_events(gw_ctx* c) {
         (r = ensure(c, c->rtable, radix2_scratch(c->ev_cap) * 4 + 64)))
         return r;
     const uint64_t tiles = (c->ev_cap + BK_TILE - 1) / BK_TILE;
-    if ((r = ensure(c, c->bk_cnt, (tiles << BK_MAXBITS) * 4)) || (r = ensure_scan(c, tiles << BK_MAXBITS)) ||
+    if ((r = ensure(c, c->bk_cnt, (tiles << BK_MAXBITS) * 8)) || (r = ensure_scan(c, tiles << BK_MAXBITS)) ||
         (r = ensure(c, c->bk_split, BK_NSPLIT * 4)))
         return r;
     return 0;
@@ -713,7 +713,8 @@ static int ensure_events(gw_ctx* c) {
 // when even the most buckets would average over BK_LCAP / 2, or for a while
 // after a bucket overflowed
 static void choose_buckets(gw_ctx* c, TickBufs& b, bool full = false) {
-    const uint64_t est = std::max<uint64_t>(c->ev_est, 1);
+    // items (own runs + mirror events) of the last tick, else about half the events
+    const uint64_t est = std::max<uint64_t>(c->it_est ? c->it_est : c->ev_est / 2, 1);
     int bits = 1;
     while (bits < BK_MAXBITS && (est >> bits) > BK_MEAN) ++bits;
     bits = std::min(bits, b.wbits + 1);
@@ -727,7 +728,7 @@ static void bind_events(gw_ctx* c, TickBufs& b) {
     b.bk_a = P<uint64_t>(c->bk_a); b.bk_b = P<uint64_t>(c->bk_b);
     b.fk0 = P<uint32_t>(c->bk_a); b.fv0 = b.fk0 + c->ev_cap;
     b.fk1 = P<uint32_t>(c->bk_b); b.fv1 = b.fk1 + c->ev_cap;
-    b.bk_cnt = P<uint32_t>(c->bk_cnt);
+    b.bk_cnt = P<unsigned long long>(c->bk_cnt);
     b.bk_id = P<uint16_t>(c->bk_id);
     b.bk_split = P<uint32_t>(c->bk_split);
     b.bk_tiles = (uint32_t)((c->ev_cap + BK_TILE - 1) / BK_TILE);
@@ -774,7 +775,7 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         bind_events(c, b);
         choose_buckets(c, b, bk_over || b.ev_full);
         DevStats* h = c->hstats;
-        h->overflow = 0; h->n_big = 0; h->ev_pk = 0; h->n_mlist = 0; h->n_sort = 0; h->bk_max = 0;
+        h->overflow = 0; h->n_big = 0; h->ev_pk = 0; h->n_mlist = 0; h->n_sort = 0; h->bk_max = 0; h->n_items = 0;
         for (int i = 0; i < STAT_SHARDS; ++i)      // the diff's shards restart; the mover count stays
             for (int f = 0; f < SH_FIELDS; ++f)
                 if (f != SH_MOVERS) h->shard[i][f] = 0;
@@ -797,7 +798,10 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     c->h_present = hs.n_present;
     gw_tick_out o{};
     const uint64_t n_enter = hs.ev_pk & 0xffffffffull, n_leave = hs.ev_pk >> 32;
-    if (!(flags & GW_TICK_NO_EVENTS)) c->ev_est = n_enter + n_leave;   // sizes the next tick's buckets
+    if (!(flags & GW_TICK_NO_EVENTS)) {                // sizes the next tick's buckets
+        c->ev_est = n_enter + n_leave;
+        if (!b.ev_full) c->it_est = hs.n_items;
+    }
     if (c->ev_full_ticks > 0) --c->ev_full_ticks;
     if (!b.ev_full) c->bk_overflows = 0;
     uint64_t n_mov = 0;
@@ -813,8 +817,9 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         unsigned long long f0 = 0, f2 = 0;
         for (int i = 0; i < STAT_SHARDS; ++i) { f0 += hs.shard[i][0]; f2 += hs.shard[i][2]; }
         fprintf(stderr, "gw_tick: movers %llu gm %llu cand %llu ev %llu+%llu big %llu mlist %llu bigcell %llu "
-                "f0 %llu f2 %llu\n", (unsigned long long)n_mov, hs.n_gm, hs.cand_total, hs.ev_pk & 0xffffffffull,
-                hs.ev_pk >> 32, hs.n_big, hs.n_mlist, hs.n_bigcell, f0, f2);
+                "f0 %llu f2 %llu bits %d full %d items %llu\n",
+                (unsigned long long)n_mov, hs.n_gm, hs.cand_total, hs.ev_pk & 0xffffffffull,
+                hs.ev_pk >> 32, hs.n_big, hs.n_mlist, hs.n_bigcell, f0, f2, b.bk_bits, b.ev_full, hs.n_items);
     }
     o.ops = M;
     o.movers = n_mov;
@@ -944,7 +949,8 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         (rc = ensure(c, c->mstat, M2 * 16)) ||
         (rc = ensure(c, c->mlist, (size_t)M * 4)) || (rc = ensure(c, c->mcnt, (size_t)M * 8)) ||
         (rc = ensure(c, c->moff, (size_t)M * 8)) || (rc = ensure(c, c->minfo, (size_t)M * 16)) ||
-        (rc = ensure(c, c->mreg, (size_t)M * 8)) ||
+        (rc = ensure(c, c->mreg, (size_t)M * 8)) || (rc = ensure(c, c->icnt, (size_t)M * 4)) ||
+        (rc = ensure(c, c->ioff, (size_t)M * 4)) ||
         (rc = ensure_scan(c, std::max<uint64_t>(std::max<uint64_t>(M2, (uint64_t)C / 32 + 2), (uint64_t)NC + 1))))
         return rc;
     if ((rc = ensure_events(c))) return rc;
@@ -971,6 +977,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.mlist = P<uint32_t>(c->mlist);
     b.mcnt = P<unsigned long long>(c->mcnt); b.moff = P<unsigned long long>(c->moff);
     b.minfo = P<uint4>(c->minfo); b.mreg = P<unsigned long long>(c->mreg);
+    b.icnt = P<uint32_t>(c->icnt); b.ioff = P<uint32_t>(c->ioff);
     b.wbits = ceil_log2(C);
     bind_events(c, b);
     if (!c->ev_est) c->ev_est = 16ull * M;

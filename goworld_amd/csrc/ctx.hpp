@@ -150,10 +150,11 @@ struct gw_ctx {
 
     // grid + tick scratch
     DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, cand, reg, own, big, mstat;
-    DevBuf mir, ownc, mirc, mlist, mcnt, moff, minfo, mreg, chunk_first, bk_a, bk_b, bk_id, bk_cnt, bk_split, ev_d, rtable;
+    DevBuf mir, ownc, mirc, mlist, mcnt, moff, minfo, icnt, ioff, mreg, chunk_first, bk_a, bk_b, bk_id, bk_cnt, bk_split, ev_d, rtable;
     DevBuf scan_status, rs_hist;
     uint64_t ev_cap = 0;                 // events the flatten/sort buffers hold (grows on overflow)
     uint64_t ev_est = 0;                 // events expected this tick (last tick's count): sizes the buckets
+    uint64_t it_est = 0;                 // bucket-path items of the last tick
     int ev_full_ticks = 0;               // ticks left on the general sort after a bucket overflowed
     int bk_overflows = 0;                // consecutive ticks whose buckets overflowed
     int bk_split_w = -1;                 // slot bits the bucket bounds were made for

@@ -89,7 +89,8 @@ struct DevStats {
     unsigned long long ev_pk;         // sum of (enters | leaves<<32) over watchers
     unsigned long long n_big;         // own-event segments left for the block sort
     unsigned long long n_mlist;       // movers with events (slot-ordered list)
-    unsigned long long n_sort;        // events flattened for the sort (min(E, ev_cap))
+    unsigned long long n_sort;        // events (general sort) / items (bucket path) flattened
+    unsigned long long n_items;       // bucket path: items of the listed movers
     unsigned long long overflow;      // event regions exceeded their capacity
     unsigned long long bk_max;        // largest event bucket too big for the LDS sort (0: none)
     unsigned long long bad_ops;
@@ -186,14 +187,16 @@ struct TickBufs {
     uint32_t* mlist;          // [m] movers in slot order
     unsigned long long* mcnt; // [m] all events of a listed mover (enters | leaves<<32)
     unsigned long long* moff; // [m] exclusive scan of mcnt
-    uint4* minfo;             // [m] listed mover: slot, own events, mirror events
+    uint4* minfo;             // [m] listed mover: slot, own enters, own leaves, mirror events
+    uint32_t* icnt;           // [m] bucket path: items of a listed mover (own runs + mirror events)
+    uint32_t* ioff;           // [m] exclusive scan of icnt
     unsigned long long* mreg; // [m] its region offset
     uint32_t* chunk_first;    // [ev_cap / 64] listed mover holding flat position 64c
     uint32_t *fk0, *fv0, *fk1, *fv1;   // [ev_cap] general sort: key leave<<wbits | watcher, value target
                                        // (aliases of bk_a / bk_b)
     uint64_t *bk_a, *bk_b;    // [ev_cap] bucket path: (leave<<wbits | watcher) << 32 | target
     uint16_t* bk_id;          // [ev_cap] bucket of each flat event
-    uint32_t* bk_cnt;         // [NB * bk_tiles] per (bucket, tile) counts, scanned in place
+    unsigned long long* bk_cnt;   // [NB * bk_tiles] per (bucket, tile) items | events<<32, scanned in place
     uint32_t bk_tiles;        // tiles of BK_TILE flat positions covering ev_cap
     uint32_t* bk_split;       // [BK_NSPLIT] bucket bounds: quantiles of the last tick's keys
     int bk_bits;              // log2 of the bucket count (<= BK_MAXBITS, <= wbits + 1)
@@ -209,10 +212,11 @@ struct TickBufs {
 constexpr int BK_NT = 1024;           // threads of the tile kernels
 constexpr int BK_TILE = 8192;         // flat positions per tile
 constexpr int BK_MAXBITS = 10;        // at most 1024 buckets (one per tile thread)
-constexpr int BK_LCAP = 8192;         // events a bucket may hold (LDS sort)
+constexpr int BK_LCAP = 7168;         // items a bucket may hold (LDS sort)
 constexpr int BK_SNT = 512;           // threads of the bucket sort
-constexpr int BK_HBINS = 3072;        // bins of the counting sort inside a bucket
+constexpr int BK_HBINS = 2048;        // bins of the counting sort inside a bucket
 constexpr int BK_SHORT = 16;          // longer bins are sorted by a wave
+constexpr int BK_RUNS = 512;          // own runs a bucket copies block-wide (more: by their lane); == BK_SNT
 constexpr uint64_t BK_MEAN = 2048;    // target mean bucket size when choosing bk_bits
 constexpr uint32_t BK_NSPLIT = 1u << BK_MAXBITS;   // quantile table size
 void launch_bk_split_init(uint32_t* sp, int wbits, hipStream_t s);

@@ -199,6 +199,64 @@ def run_digest(tr) -> dict:
                 nbr_total=int(o.total_neighbors()))
 
 
+def multi_digest_configs():
+    return [("config4_10k", lambda: [T.config4_space(s, ticks=2) for s in range(10_000)])]
+
+
+def run_multi_digest(trs) -> dict:
+    """Independent spaces in one context, loaded and collected once (that
+    collect is not digested: 3.5e8 records), then ticked: each space through
+    ORC_SEQRULE and gridmt (must agree), outputs shifted to global slots (space i's slots
+    start at the sum of the earlier capacities) and merged in the canonical
+    orders: events by (watcher, target) = the spaces' arrays back to back;
+    records by (gate(watcher), entity, watcher)."""
+    bases = np.cumsum([0] + [tr.capacity for tr in trs])
+    gates = np.concatenate([tr.gates for tr in trs])
+    n_ticks = len(trs[0].ticks)
+    acc = [dict(e=[], l=[], r=[]) for _ in range(n_ticks)]
+    nbr = 0
+    for i, tr in enumerate(trs):
+        o = pyorc.OracleSpace(tr.capacity, tr.d, pyorc.SEQRULE)
+        pyorc.load_trace(o, tr)
+        g = pyorc.GridMT(tr.capacity, tr.d, tr.bounds)
+        g.load(tr)
+        o.collect()                      # the load's own collect is not part of the digest
+        g.collect()
+        b = np.uint32(bases[i])
+        for t, ops in enumerate(tr.ticks):
+            assert o.tick(ops) == 0 and g.tick(ops) == 0
+            e, l = o.events()
+            ge, gl = g.events()
+            assert ge.tobytes() == e.tobytes() and gl.tobytes() == l.tobytes(), f"space {i} tick {t}"
+            r = o.collect()
+            g.collect()
+            for a, k in ((e, "e"), (l, "l")):
+                a = a.copy()
+                a["watcher"] += b
+                a["target"] += b
+                acc[t][k].append(a)
+            r = r.copy()
+            r["watcher"] += b
+            r["entity"] += b
+            acc[t]["r"].append(r)
+        nbr += int(o.total_neighbors())
+        if i % 1000 == 0:
+            print(f"  space {i}", flush=True)
+    ticks = []
+    for t in range(n_ticks):
+        e = np.concatenate(acc[t]["e"])
+        l = np.concatenate(acc[t]["l"])
+        r = np.concatenate(acc[t]["r"])
+        r = r[np.lexsort((r["watcher"], r["entity"], gates[r["watcher"]]))]
+        ticks.append(dict(n_enter=len(e), n_leave=len(l), n_rec=len(r),
+                          enter_sha=sha(e), leave_sha=sha(l), rec_sha=sha(r)))
+        print(f"  tick {t}: {len(e)} enter, {len(l)} leave, {len(r)} records", flush=True)
+    h = hashlib.sha256()
+    for tr in trs:
+        h.update(bytes.fromhex(trace_input_sha(tr)))
+    return dict(input_sha=h.hexdigest(), ticks=ticks, nbr_total=nbr, spaces=len(trs))
+
+
 def main(argv):
     only = set(argv[1:])
     for name, tr, brute in small_fixtures():
@@ -206,7 +264,8 @@ def main(argv):
             continue
         print(f"{name}: N={tr.n}, {len(tr.ticks)} ticks", flush=True)
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **run_small(tr, brute))
-    if only and not any(n in only for n, _, _ in digest_configs()):
+    digest_names = [n for n, _, _ in digest_configs()] + [n for n, _ in multi_digest_configs()]
+    if only and not any(n in only for n in digest_names):
         return
     out = {"_note": "SHA-256 of canonical outputs (tests/golden/make_golden.py); "
                     "records in (gate(watcher), entity, watcher) order"}
@@ -215,6 +274,11 @@ def main(argv):
             continue
         print(f"{name}", flush=True)
         out[name] = run_digest(make())
+    for name, make in multi_digest_configs():
+        if only and name not in only:
+            continue
+        print(f"{name}", flush=True)
+        out[name] = run_multi_digest(make())
     path = os.path.join(HERE, "digests.json")
     if only and os.path.exists(path):
         with open(path) as f:

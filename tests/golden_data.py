@@ -109,3 +109,17 @@ DIGEST_TRACES = {
     "config2_100k": lambda: T.config2(ticks=3),
     "config3_1m": lambda: T.config3(ticks=2),
 }
+
+
+# config #4: 10k independent spaces of 1k entities in ONE context (slots of
+# space i at [1000 i, 1000 (i + 1))); digests over the whole context's outputs
+MULTI_DIGEST_TRACES = {
+    "config4_10k": lambda: [T.config4_space(s, ticks=2) for s in range(10_000)],
+}
+
+
+def multi_input_sha(trs) -> str:
+    h = hashlib.sha256()
+    for tr in trs:
+        h.update(bytes.fromhex(trace_input_sha(tr)))
+    return h.hexdigest()

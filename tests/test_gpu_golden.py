@@ -4,9 +4,9 @@ Small fixtures (tests/golden/*.npz: config #1 walks, rounding-edge churn
 traces, a dyadic hotspot trace with 3 gates and client-less entities): every
 tick's canonical enter / leave events byte for byte, the sync records of every
 collect (count + SHA-256 of the canonical bytes, tick 0 in full) and the final
-InterestedIn sets.  Large configs (#2 100k, #3 1M; tests/golden/digests.json):
-per tick event and record digests, on traces regenerated from their seeds
-(input hash checked first).  No oracle runs here: the expected outputs are
+InterestedIn sets.  Large configs (#2 100k, #3 1M, #4 10k spaces x 1k in one context;
+tests/golden/digests.json): per tick event and record digests, on traces
+regenerated from their seeds (input hash checked first).  No oracle runs here: the expected outputs are
 data.
 """
 import numpy as np
@@ -14,6 +14,7 @@ import pytest
 
 import golden_data as G
 from goworld_amd import gpuaoi
+from goworld_amd import traces as T
 
 pytestmark = pytest.mark.gpu
 
@@ -92,4 +93,39 @@ def test_large_config_digests(gpu, name):
         del recs
     if "nbr_total" in d:
         assert g.total_neighbors() == d["nbr_total"]
+    g.close()
+
+
+@pytest.mark.parametrize("name", list(G.MULTI_DIGEST_TRACES))
+def test_many_spaces_config4_digests(gpu, name):
+    """Config #4 at its workload: 10k spaces x 1k entities in one context, every
+    tick one gw_tick over all of them; per tick the digests of the whole
+    context's canonical events and records (tests/golden/digests.json, from
+    per-space ORC_SEQRULE + gridmt runs merged in global slot order)."""
+    d = G.digests()[name]
+    trs = G.MULTI_DIGEST_TRACES[name]()
+    assert G.multi_input_sha(trs) == d["input_sha"], "trace generator changed (not a parity failure)"
+    assert len(trs) == d["spaces"]
+    g = gpu()
+    bases = []
+    for tr in trs:
+        _, base = gpuaoi.load_space(g, tr)
+        bases.append(base)
+    assert bases == list(np.cumsum([0] + [tr.capacity for tr in trs[:-1]]))
+    gates = np.concatenate([tr.gates for tr in trs])
+    g.sync_collect()                                  # the load's collect (not digested)
+    for t in range(len(trs[0].ticks)):
+        exp = d["ticks"][t]
+        ops = np.concatenate([T.with_global_slots(tr.ticks[t], b) for tr, b in zip(trs, bases)])
+        g.submit(ops)
+        res = g.tick()
+        assert (res.n_enter, res.n_leave) == (exp["n_enter"], exp["n_leave"])
+        assert G.sha(res.enter) == exp["enter_sha"] and G.sha(res.leave) == exp["leave_sha"]
+        r = g.sync_collect()
+        assert r.n_rec == exp["n_rec"]
+        recs = canonical(r.records, gates)
+        del r
+        assert G.sha(recs) == exp["rec_sha"], f"{name} tick {t}: records"
+        del recs
+    assert g.total_neighbors() == d["nbr_total"]
     g.close()

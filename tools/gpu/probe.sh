@@ -7,3 +7,4 @@ kt=$(find gpurun_out/probe_$m -name '*kernel_trace.csv' | head -1)
 python3 tools/prof_summary.py "$kt" 5 | grep -E "k_bucket|k_bk|k_flatten|gpu-busy"
 rm -f "$kt"
 done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_golden.py -x -v --timeout 280 --timeout-method thread -k "config4 or large" > gpurun_out/t_c4.log 2>&1; tail -5 gpurun_out/t_c4.log

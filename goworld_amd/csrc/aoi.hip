@@ -875,7 +875,11 @@ __global__ void __launch_bounds__(NT) k_flat_items(TickBufs b) {
     const uint64_t NI = b.st->n_items;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (E > b.ev_cap) atomicOr(&b.st->overflow, 1ull);
-        b.st->n_sort = E > b.ev_cap ? 0 : NI;
+        const uint64_t n = E > b.ev_cap ? 0 : NI;
+        b.st->n_sort = n;
+        const uint64_t T = (n + BK_TILE - 1) / BK_TILE;      // tiles in use: the count table's stride
+        b.st->bk_tiles = T;
+        b.st->bk_cells = T << b.bk_bits;
     }
     if (E > b.ev_cap) return;
     const uint64_t c = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
@@ -994,8 +998,10 @@ __global__ void __launch_bounds__(BK_NT) k_bk_count(TickBufs b) {
     const uint32_t NB = 1u << b.bk_bits;
     for (uint32_t i = t; i < NB; i += BK_NT) h[i] = hw[i] = 0;
     const uint64_t n = b.st->n_sort;
+    const uint64_t T = b.st->bk_tiles;
+    if (blockIdx.x >= T) return;                            // block-uniform
     const uint64_t base = (uint64_t)blockIdx.x * BK_TILE;
-    if (base < n) {                                         // block-uniform
+    {
         int lsh;
         bk_lut_build(b, lut, NB, lsh);                      // (syncs)
         const int W = b.wbits;
@@ -1026,7 +1032,7 @@ __global__ void __launch_bounds__(BK_NT) k_bk_count(TickBufs b) {
     }
     __syncthreads();
     for (uint32_t i = t; i < NB; i += BK_NT)
-        b.bk_cnt[(uint64_t)i * b.bk_tiles + blockIdx.x] = (unsigned long long)h[i] | ((unsigned long long)hw[i] << 32);
+        b.bk_cnt[(uint64_t)i * T + blockIdx.x] = (unsigned long long)h[i] | ((unsigned long long)hw[i] << 32);
 }
 
 // exclusive scan of one value per thread over a block of NTH threads
@@ -1073,7 +1079,7 @@ __global__ void __launch_bounds__(BK_NT) k_bucket_scatter(TickBufs b) {
     const uint32_t toff = bk_block_excl<BK_NT>(cnt, red);
     if (t < (int)NB) {
         h[t] = toff;
-        go[t] = (uint32_t)b.bk_cnt[(uint64_t)t * b.bk_tiles + blockIdx.x] - toff;   // mod 2^32: dst = go + staged index
+        go[t] = (uint32_t)b.bk_cnt[(uint64_t)t * b.st->bk_tiles + blockIdx.x] - toff;   // mod 2^32: dst = go + staged index
     }
     __syncthreads();
 #pragma unroll
@@ -1108,8 +1114,9 @@ __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
     constexpr int WCH = BK_LCAP / BK_SNT;                   // max chunks of 64 per wave
     const uint32_t bk = blockIdx.x;
     const uint32_t NB = 1u << b.bk_bits;
-    const uint64_t T = b.bk_tiles;
+    const uint64_t T = b.st->bk_tiles;
     const uint64_t n_all = b.st->n_sort;
+    if (n_all == 0) return;
     const unsigned long long c0 = b.bk_cnt[(uint64_t)bk * T];
     const uint64_t s = lo32(c0);
     const uint64_t e = bk + 1 < NB ? lo32(b.bk_cnt[(uint64_t)(bk + 1) * T]) : n_all;
@@ -1158,11 +1165,9 @@ __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
         sum += c[q];
     }
     uint32_t run = bk_block_excl<BK_SNT>(sum, red);
-    uint32_t bstart[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = (uint32_t)t * PER + q;
-        bstart[q] = run;
         if (i < nbins) hb[i] = run;
         if (c[q] > (uint32_t)BK_SHORT) longs[atomicAdd(&n_long, 1u)] = (uint16_t)i;
         run += c[q];
@@ -1175,19 +1180,30 @@ __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
     }
 #undef BK_BIN
     __syncthreads();
-    // each bin in place by the masked key: short ones by the thread owning them
+    // each bin in place by the masked key.  Short bins: an item's place = the
+    // bin start + the bin's items with a smaller key (keys are unique), all
+    // read before any is written back
+    uint32_t pos[CH];
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const uint32_t len = c[q];
-        if (len < 2 || len > (uint32_t)BK_SHORT) continue;
-        uint64_t* R = L + bstart[q];
-        for (uint32_t a = 1; a < len; ++a) {
-            const uint64_t v = R[a];
-            uint32_t j = a;
-            while (j > 0 && (R[j - 1] & km) > (v & km)) { R[j] = R[j - 1]; --j; }
-            R[j] = v;
-        }
+    for (int k = 0; k < CH; ++k) {
+        pos[k] = 0xffffffffu;
+        const uint32_t i = (uint32_t)t + (uint32_t)k * BK_SNT;
+        if (i >= n) continue;
+        const uint32_t x = (uint32_t)((((key[k]) & km) >> W) - lo) >> bsh;
+        const uint32_t r0 = x ? hb[x - 1] : 0u, r1 = hb[x];
+        if (r1 - r0 > (uint32_t)BK_SHORT) continue;        // a wave sorts the long bins
+        const uint64_t kk = key[k] & km;
+        uint32_t r = r0, j = r0;
+        for (; j + 4 <= r1; j += 4)
+            r += (uint32_t)((L[j] & km) < kk) + (uint32_t)((L[j + 1] & km) < kk) +
+                 (uint32_t)((L[j + 2] & km) < kk) + (uint32_t)((L[j + 3] & km) < kk);
+        for (; j < r1; ++j) r += (uint32_t)((L[j] & km) < kk);
+        pos[k] = r;
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CH; ++k)
+        if (pos[k] != 0xffffffffu) L[pos[k]] = key[k];
     const uint32_t nl = n_long;
     for (uint32_t q = (uint32_t)w; q < nl; q += NWV) {
         const uint32_t x = longs[q];
@@ -1371,7 +1387,8 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
         hipLaunchKernelGGL(k_flat_items, dim3(nblk1((b.ev_cap + 63) / 64, NWAVE)), dim3(NT), 0, s, b);
         hipLaunchKernelGGL(k_bk_count, dim3(b.bk_tiles), dim3(BK_NT), 0, s, b);
         scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.bk_cnt, (uint64_t*)b.bk_cnt,
-                                           (uint64_t)NB * b.bk_tiles, nullptr, sc, (uint64_t*)nullptr, s);
+                                           (uint64_t)NB * b.bk_tiles, (const uint64_t*)&b.st->bk_cells, sc,
+                                           (uint64_t*)nullptr, s);
         hipLaunchKernelGGL(k_bucket_scatter, dim3(b.bk_tiles), dim3(BK_NT), 0, s, b);
         hipLaunchKernelGGL(k_bucket_sort, dim3(NB), dim3(BK_SNT), 0, s, b);
     } else {

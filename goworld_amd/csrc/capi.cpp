@@ -775,7 +775,7 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         bind_events(c, b);
         choose_buckets(c, b, bk_over || b.ev_full);
         DevStats* h = c->hstats;
-        h->overflow = 0; h->n_big = 0; h->ev_pk = 0; h->n_mlist = 0; h->n_sort = 0; h->bk_max = 0; h->n_items = 0;
+        h->overflow = 0; h->n_big = 0; h->ev_pk = 0; h->n_mlist = 0; h->n_sort = 0; h->bk_max = 0; h->n_items = 0; h->bk_tiles = 0; h->bk_cells = 0;
         for (int i = 0; i < STAT_SHARDS; ++i)      // the diff's shards restart; the mover count stays
             for (int f = 0; f < SH_FIELDS; ++f)
                 if (f != SH_MOVERS) h->shard[i][f] = 0;

@@ -91,6 +91,8 @@ struct DevStats {
     unsigned long long n_mlist;       // movers with events (slot-ordered list)
     unsigned long long n_sort;        // events (general sort) / items (bucket path) flattened
     unsigned long long n_items;       // bucket path: items of the listed movers
+    unsigned long long bk_tiles;      // bucket path: tiles in use (count table stride)
+    unsigned long long bk_cells;      // bucket path: count table entries in use
     unsigned long long overflow;      // event regions exceeded their capacity
     unsigned long long bk_max;        // largest event bucket too big for the LDS sort (0: none)
     unsigned long long bad_ops;

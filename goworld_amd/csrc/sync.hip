@@ -192,6 +192,21 @@ __device__ __forceinline__ void st_record_nt(gw_sync_record* r, uint32_t watcher
     __builtin_nontemporal_store(((unsigned long long)__float_as_uint(p.w) << 32) | __float_as_uint(p.z), q + 2);
 }
 
+// The neighbour records of one entity leave through a per-wave LDS buffer
+// (SW_BUF records): once 64 are staged they are written as 3 x 64 contiguous
+// 8-B non-temporal stores (512 B per instruction) instead of one strided
+// 8-B store per record field.
+constexpr int SW_BUF = 128;
+__device__ __forceinline__ void sw_flush64(unsigned long long* buf, unsigned long long* dst, uint32_t n_rec) {
+    const int ln = lane_id();
+    const uint32_t words = 3 * n_rec;
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) {
+        const uint32_t i = j * 64 + (uint32_t)ln;
+        if (i < words) __builtin_nontemporal_store(buf[i], dst + i);
+    }
+}
+
 // writes e's records at rec_off[k] (nothing if the buffer is too small: the
 // host grows it and reruns this pass)
 template <int U>
@@ -200,6 +215,8 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
                                                    uint32_t nf_max, const uint64_t* __restrict__ rec_off,
                                                    const uint32_t* __restrict__ cnt, gw_sync_record* rec,
                                                    uint64_t rec_cap, DevStats* st) {
+    __shared__ unsigned long long sbuf[NWAVE][3 * SW_BUF];
+    unsigned long long* buf = sbuf[threadIdx.x >> 6];
     const uint64_t nf = load_n(nf_max, nf_dev);
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
@@ -220,12 +237,35 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
             ++at;
         }
         if ((f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
+            const unsigned long long pxy = ((unsigned long long)__float_as_uint(p.y) << 32) | __float_as_uint(p.x);
+            const unsigned long long pzw = ((unsigned long long)__float_as_uint(p.w) << 32) | __float_as_uint(p.z);
+            uint32_t nb = 0;                                   // staged records (wave-uniform)
             wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
                 const bool take = rel && g != 0;
                 const uint64_t bt = wave_ballot(take);
-                if (take) st_record_nt(rec + at + (uint64_t)popc64(bt & lt), ws, e, p);
-                at += (uint64_t)popc64(bt);
+                if (take) {
+                    unsigned long long* r = buf + 3 * (nb + (uint32_t)popc64(bt & lt));
+                    r[0] = ((unsigned long long)e << 32) | ws;
+                    r[1] = pxy;
+                    r[2] = pzw;
+                }
+                nb += (uint32_t)popc64(bt);
+                if (nb >= 64) {
+                    wave_sync();
+                    sw_flush64(buf, (unsigned long long*)(rec + at), 64);
+                    at += 64;
+                    nb -= 64;
+                    wave_sync();
+                    for (uint32_t i = (uint32_t)ln; i < 3 * nb; i += 64) buf[i] = buf[192 + i];
+                    wave_sync();
+                }
             });
+            if (nb) {
+                wave_sync();
+                sw_flush64(buf, (unsigned long long*)(rec + at), nb);
+                at += nb;
+                wave_sync();
+            }
         }
     }
 }

@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--mode", choices=["world", "spaces"], default="world",
                     help="N>1 with config 3: world = the 1M space decomposed over the N GPUs (strong); spaces = an "
                          "independent 1M space per GPU, no comm (weak)")
-    ap.add_argument("--config", type=int, choices=[3, 4, 5], default=3,
+    ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=3,
                     help="3: the metric's 1M clustered space (N=1: one GPU; N>1: decomposed over the N GPUs); "
                          "4: config #4, 10k independent 1k-entity spaces, space s on GPU s mod N (strong); "
                          "5: the 16M uniform world of config #5 over N strips (strong)")
@@ -247,7 +247,10 @@ class SpaceRun:
     """N=1 (config #3) and --mode spaces: one independent space per GPU."""
 
     def __init__(self, a, ctl, ticks):
-        self.tr = traces.config3(ticks=ticks, seed=3 + ctl.rank, n=a.entities, side=a.side)
+        if a.config == 2:                               # BASELINE config #2: 100k uniform, L = 10240
+            self.tr = traces.config2(ticks=ticks, seed=2 + ctl.rank)
+        else:
+            self.tr = traces.config3(ticks=ticks, seed=3 + ctl.rank, n=a.entities, side=a.side)
         if a.capacity:
             self.tr.capacity = max(a.capacity, a.entities)
             self.tr.gates = np.concatenate([self.tr.gates, np.zeros(self.tr.capacity - a.entities, np.uint16)])
@@ -263,7 +266,7 @@ class SpaceRun:
         self.nbytes_tick = self.m * traces.OP_DTYPE.itemsize
         self.by_client = a.sync_by_client
         self.parallelism = f"independent spaces x{ctl.ws} (no comm)" if ctl.ws > 1 else "single GPU"
-        self.n_world = a.entities * (ctl.ws if ctl.ws > 1 else 1)
+        self.n_world = self.tr.n * (ctl.ws if ctl.ws > 1 else 1)
 
     def step(self, t):
         g = self.g
@@ -467,7 +470,7 @@ def measure(run, a, ctl, warmup, steps, profile, extra):
     for t in range(warmup):
         run.step(t)
     g.set_profiling(2 if profile else 0)    # the dominant kernel's stage only
-    tot = dict(ops=0, events=0, records=0, bytes_alg=0, mover_alg=0, cand=0, own_copy_alg=0, sync_write_alg=0)
+    tot = dict(ops=0, events=0, records=0, bytes_alg=0, mover_alg=0, cand=0, events_alg=0, sync_write_alg=0)
     ctl.barrier()
     g.synchronize()
     t0 = time.perf_counter()
@@ -479,10 +482,10 @@ def measure(run, a, ctl, warmup, steps, profile, extra):
         tot["records"] += s.n_rec
         tot["bytes_alg"] += r.bytes_alg + s.bytes_alg
         # SURVEY 8(d) terms per kernel: k_mover produces the neighbour-list
-        # terms and the net events, 4*(A_old+A_new) + 8*E; k_own_copy reads and
-        # writes the events (8*E each way); k_sync_write writes the records
+        # terms and the net events, 4*(A_old+A_new) + 8*E; k_bucket_sort writes
+        # the canonical event arrays (8*E); k_sync_write writes the records
         tot["mover_alg"] += 4 * (r.nbr_old + r.nbr_new) + 8 * ev
-        tot["own_copy_alg"] += 16 * ev
+        tot["events_alg"] += 8 * ev
         tot["sync_write_alg"] += 24 * s.n_rec
         tot["cand"] += r.pairs_tested
     g.synchronize()
@@ -533,7 +536,7 @@ def roofline_fields(res, K, config, ws):
                                              "kernel reads; not the roofline numerator)",
                            "timing": "HIP events around the kernel on its stream, every timed step"}
         kt = {}
-        for k, alg in ((mv, mover_alg), ("k_own_copy", tot["own_copy_alg"] / K),
+        for k, alg in ((mv, mover_alg), ("k_bucket_sort", tot["events_alg"] / K),
                        ("k_sync_write<4>", tot["sync_write_alg"] / K)):
             tr_ = traffic(k)
             kt[k] = {"bytes_alg": alg, "traffic": tr_, "traffic_over_alg": (tr_ / alg) if (tr_ and alg) else None}
@@ -552,7 +555,9 @@ def main():
     ctl = Ctl(a)
     ws, rank = ctl.ws, ctl.rank
     extra = 5 if a.profile_stages else 0         # untimed steps for the per-stage breakdown
-    if a.config == 4:
+    if a.config == 2:
+        kind = "c2"                                 # config #2 (100k uniform), one space per GPU
+    elif a.config == 4:
         kind = "c4"
     elif a.config == 5:
         kind = "c5"
@@ -567,7 +572,7 @@ def main():
         torch.cuda.set_device(ctl.local)
         torch.zeros(1, device=torch.device("cuda", ctl.local))
     cm = a.client_msgs if (ws == 1 and kind == "c3") else 0
-    n_e2e = a.e2e_steps if kind in ("c3", "c4") else 0
+    n_e2e = a.e2e_steps if kind in ("c2", "c3", "c4") else 0
     W, K = a.warmup, a.steps
     ticks = W + K + extra + cm + n_e2e
     t_load = time.perf_counter()
@@ -630,6 +635,9 @@ def main():
             f"config #5: one 16M-entity uniform world space, L = 131072, AOI distance 100, 10% movers per tick "
             f"(+-4; walkers cross strip borders), decomposed into {ws} X-strip(s); step = route + RCCL halo "
             f"exchange + gw_tick + gw_sync_collect on every rank")
+    elif kind == "c2":
+        workload = ("config #2: single AOI space per GPU, 100k uniform-random entities, L = 10240, AOI distance "
+                    "100, 10% movers per tick (+-4); step = gw_tick + gw_sync_collect")
     elif kind == "c3world":
         workload = (f"config #3 as one world: the 1M-entity clustered space (70% uniform + 30% in 64 Gaussian "
                     f"hotspots, sigma 200; 10% movers per tick, +-4 / hotspot +-16; AOI distance 100; world "
@@ -639,7 +647,7 @@ def main():
         workload = ("config #3: single AOI space per GPU, 1M entities, 70% uniform + 30% in 64 "
                     "Gaussian hotspots (sigma 200), 10% movers per tick (+-4 / hotspot +-16), "
                     "AOI distance 100, world 32768^2; step = gw_tick + gw_sync_collect")
-    cfg_no = {"c3": 3, "c3world": 3, "c4": 4, "c5": 5}[kind]
+    cfg_no = {"c2": 2, "c3": 3, "c3world": 3, "c4": 4, "c5": 5}[kind]
     line = {
         "metric": "entity AOI updates/sec + enter/leave events/sec, 1M-entity space, 1/2/4/8 GPU",
         "value": res["sum_ops"] / mx,
@@ -649,13 +657,13 @@ def main():
         "warmup": W,
         "ms_per_step": mx / K * 1e3,
         "higher_is_better": True,
-        "scaling": "weak" if (ws > 1 and kind == "c3") else "strong",
+        "scaling": "weak" if (ws > 1 and kind in ("c2", "c3")) else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #{cfg_no})",
         "config": {"workload": workload, "world_entities": n_world, "entities_per_gpu": n_world // ws,
                    "movers_per_tick_per_gpu": m_rank, "aoi_dist": 100.0,
-                   "world_side": {4: 1024.0, 5: 131072.0}.get(cfg_no, a.side), "gates": 1,
+                   "world_side": {2: 10240.0, 4: 1024.0, 5: 131072.0}.get(cfg_no, a.side), "gates": 1,
                    "parallelism": parallelism},
         "events_per_sec": res["sum_events"] / mx,
         "records_per_sec": res["sum_records"] / mx,

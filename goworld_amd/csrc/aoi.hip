@@ -868,7 +868,7 @@ __global__ void __launch_bounds__(NT) k_flatten(TickBufs b) {
 // (leave, watcher) key holds one run (the watcher moved) or mirror events
 // only (it did not), so items sort by their masked key and runs expand to
 // their events at output time.
-constexpr int BK_RUN_BIT = 53;
+constexpr int BK_RUN_BIT = BK_KEY_BITS;               // just above the (leave, watcher, target) bits
 constexpr uint64_t BK_RUN = 1ull << BK_RUN_BIT;
 __global__ void __launch_bounds__(NT) k_flat_items(TickBufs b) {
     const uint64_t E = lo32(b.st->ev_pk) + hi32(b.st->ev_pk);
@@ -948,7 +948,9 @@ __global__ void __launch_bounds__(NT) k_flat_items(TickBufs b) {
 // Flat entries: bucket << 54 | (leave<<wbits | watcher) << wbits | target
 // (wbits <= 26, or the host takes the general sort).
 constexpr int BK_LUT_BITS = 12;
-constexpr int BK_KEY_SHIFT = 54;
+// staged keys carry their bucket above the run bit (the scatter strips it)
+constexpr int BK_KEY_SHIFT = 64 - BK_MAXBITS;
+static_assert(BK_RUN_BIT < BK_KEY_SHIFT, "run bit below the staged bucket bits");
 
 struct BkLut {
     uint32_t sp[1 << BK_MAXBITS];
@@ -1057,7 +1059,7 @@ __global__ void __launch_bounds__(BK_NT) k_bucket_scatter(TickBufs b) {
     const uint64_t base = (uint64_t)blockIdx.x * BK_TILE;
     if (base >= n) return;                                  // block-uniform
     const uint32_t NB = 1u << b.bk_bits;
-    if (t < (int)NB) h[t] = 0;
+    for (uint32_t i = t; i < NB; i += BK_NT) h[i] = 0;
     __syncthreads();
     constexpr int IPT = BK_TILE / BK_NT;
     uint64_t k[IPT];
@@ -1075,11 +1077,25 @@ __global__ void __launch_bounds__(BK_NT) k_bucket_scatter(TickBufs b) {
         r[j] = i < n ? atomicAdd(&h[q[j]], 1u) : 0u;
     }
     __syncthreads();
-    const uint32_t cnt = t < (int)NB ? h[t] : 0u;
-    const uint32_t toff = bk_block_excl<BK_NT>(cnt, red);
-    if (t < (int)NB) {
-        h[t] = toff;
-        go[t] = (uint32_t)b.bk_cnt[(uint64_t)t * b.st->bk_tiles + blockIdx.x] - toff;   // mod 2^32: dst = go + staged index
+    // thread t: buckets [t*BPT, (t+1)*BPT)
+    constexpr int BPT = (1 << BK_MAXBITS) / BK_NT;
+    uint32_t cb[BPT], csum = 0;
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) {
+        const uint32_t i = (uint32_t)t * BPT + u;
+        cb[u] = i < NB ? h[i] : 0u;
+        csum += cb[u];
+    }
+    uint32_t toff = bk_block_excl<BK_NT>(csum, red);
+    const uint64_t T = b.st->bk_tiles;
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) {
+        const uint32_t i = (uint32_t)t * BPT + u;
+        if (i < NB) {
+            h[i] = toff;
+            go[i] = (uint32_t)b.bk_cnt[(uint64_t)i * T + blockIdx.x] - toff;   // mod 2^32: dst = go + staged index
+        }
+        toff += cb[u];
     }
     __syncthreads();
 #pragma unroll
@@ -1091,7 +1107,9 @@ __global__ void __launch_bounds__(BK_NT) k_bucket_scatter(TickBufs b) {
     const uint32_t tn = (uint32_t)min<uint64_t>((uint64_t)BK_TILE, n - base);
     for (uint32_t i = t; i < tn; i += BK_NT) {              // each bucket's run of the tile is contiguous
         const uint64_t v = stg[i];
-        b.bk_b[go[(uint32_t)(v >> BK_KEY_SHIFT)] + i] = v & ((1ull << BK_KEY_SHIFT) - 1);
+        const uint32_t dst = go[(uint32_t)(v >> BK_KEY_SHIFT)] + i;
+        if (dst < n) b.bk_b[dst] = v & ((1ull << BK_KEY_SHIFT) - 1);
+        else atomicOr(&b.st->overflow, 2ull);              // (inconsistent counts: never by construction)
     }
 }
 
@@ -1270,6 +1288,10 @@ __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
         const uint32_t i = w0 + (uint32_t)cc * 64 + ln;
         if (i >= n) continue;
         const uint32_t dst = wpre + off[cc];
+        if (dst >= b.ev_cap) {                              // (never by construction; no wild writes)
+            atomicOr(&b.st->overflow, 2ull);
+            continue;
+        }
         if (!(v[cc] & BK_RUN)) {
             gw_event ev;
             ev.watcher = (uint32_t)(v[cc] >> W) & wm;
@@ -1279,6 +1301,10 @@ __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
             const bool leave = ((v[cc] >> (2 * W)) & 1u) != 0;
             const uint32_t len = leave ? mi[cc].z : mi[cc].y;
             const uint32_t src = aux[cc] + (leave ? mi[cc].y : 0u);
+            if (dst + len > b.ev_cap) {
+                atomicOr(&b.st->overflow, 2ull);
+                continue;
+            }
             const uint32_t q = atomicAdd(&n_runs, 1u);
             if (q < (uint32_t)BK_RUNS) {
                 runs[q] = make_uint4(dst, src, len, mi[cc].x);

@@ -719,7 +719,7 @@ static void choose_buckets(gw_ctx* c, TickBufs& b, bool full = false) {
     while (bits < BK_MAXBITS && (est >> bits) > BK_MEAN) ++bits;
     bits = std::min(bits, b.wbits + 1);
     b.bk_bits = bits;
-    b.ev_full = full || c->ev_full_ticks > 0 || (est >> bits) > (uint64_t)BK_LCAP / 2 || b.wbits > 26;
+    b.ev_full = full || c->ev_full_ticks > 0 || (est >> bits) > (uint64_t)BK_LCAP / 2 || b.wbits > BK_MAX_WBITS;
 }
 
 static void bind_events(gw_ctx* c, TickBufs& b) {

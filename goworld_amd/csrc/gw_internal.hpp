@@ -213,7 +213,7 @@ struct TickBufs {
 // events bucket path (aoi.hip k_flat_count / k_bucket_scatter / k_bucket_sort)
 constexpr int BK_NT = 1024;           // threads of the tile kernels
 constexpr int BK_TILE = 8192;         // flat positions per tile
-constexpr int BK_MAXBITS = 10;        // at most 1024 buckets (one per tile thread)
+constexpr int BK_MAXBITS = 12;        // at most 4096 buckets
 constexpr int BK_LCAP = 7168;         // items a bucket may hold (LDS sort)
 constexpr int BK_SNT = 512;           // threads of the bucket sort
 constexpr int BK_HBINS = 2048;        // bins of the counting sort inside a bucket
@@ -221,6 +221,11 @@ constexpr int BK_SHORT = 16;          // longer bins are sorted by a wave
 constexpr int BK_RUNS = 512;          // own runs a bucket copies block-wide (more: by their lane); == BK_SNT
 constexpr uint64_t BK_MEAN = 2048;    // target mean bucket size when choosing bk_bits
 constexpr uint32_t BK_NSPLIT = 1u << BK_MAXBITS;   // quantile table size
+// item bits: (leave, watcher, target) = 2*wbits + 1 <= BK_KEY_BITS, then the
+// run flag, then (staged only) the bucket in the top BK_MAXBITS bits
+constexpr int BK_KEY_BITS = 51;
+constexpr int BK_MAX_WBITS = (BK_KEY_BITS - 1) / 2;   // 25: larger contexts take the general sort
+static_assert(BK_KEY_BITS + 1 + BK_MAXBITS <= 64, "item layout");
 void launch_bk_split_init(uint32_t* sp, int wbits, hipStream_t s);
 
 // ---- launchers --------------------------------------------------------------

@@ -509,11 +509,12 @@ constexpr uint32_t CAND_CLIENT = 1u << 30;
 
 // WPB waves per block: a block keeps its LDS until its slowest wave ends, so
 // small blocks keep more waves resident when hotspot movers run long
-template <int DIFF_U, int WPB>
-__global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[WPB * SORT_LDS];
-    const uint64_t m = (uint64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
-    if (m >= b.st->n_gm) return;
+// One mover-grid entry m by one wave.  GN / GS: the current grid entries and
+// row starts (global, or LDS copies of the space's range in small-space
+// mode, indexed by global position either way); lds: SCAP sort slots per wave.
+template <int DIFF_U, uint32_t SCAP>
+__device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_t* lds, const GEnt* GN,
+                                          const uint32_t* GS, const uint32_t* MS) {
     const MEnt me = b.gm[m];
     const int ln = lane_id();
     if (!(me.tags & TAG_PRIMARY)) {
@@ -550,7 +551,7 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     uint64_t* mir = b.mir + reg;
     uint32_t n = 0, nl = 0, nm_ = 0, nml = 0;
     uint32_t c_old = 0, c_new = 0, c_band = 0, c_cli = 0;
-    Flat f = flat_build<2>(P, R, w.gn_start, b.gm_start);
+    Flat f = flat_build<2>(P, R, GS, MS);
     for (uint32_t base = 0; base < f.total; base += 64u * DIFF_U) {
         uint32_t idx[DIFF_U], kd[DIFF_U];
         flat_map<DIFF_U, 2>(f, base, idx, kd);
@@ -561,7 +562,7 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
             cc[u].slot = A;                                    // invalid unless loaded below
             if (idx[u] != ~0u) {
                 if (kd[u] == 0) {
-                    const GEnt e = w.gn[idx[u]];
+                    const GEnt e = GN[idx[u]];
                     cc[u].x = cc[u].ox = e.x;
                     cc[u].z = cc[u].oz = e.z;
                     cc[u].slot = (e.meta & MOVER_BIT) ? A : e.slot;   // movers come from gm
@@ -630,8 +631,8 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
             uint32_t v = ln < (int)n ? out[ln] : 0xffffffffu;
             v = wave_sort64(v);
             if (ln < (int)n) out[ln] = v;
-        } else if (n <= SORT_LDS) {
-            uint32_t* L = lds + (threadIdx.x >> 6) * SORT_LDS;
+        } else if (n <= SCAP) {
+            uint32_t* L = lds + (threadIdx.x >> 6) * SCAP;
             wave_sync();
             for (uint32_t i = ln; i < n; i += 64) L[i] = out[i];
             wave_sync();
@@ -653,6 +654,48 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
         // per-mover statistics, summed by k_mover_stats (no atomics here: 2 per
         // mover into 256 shards cost 25 us at config #3 and 180 us at config #4)
         b.mstat[m] = make_ulonglong2((unsigned long long)so | ((unsigned long long)sn << 32), sb);
+    }
+}
+
+// WPB waves per block: a block keeps its LDS until its slowest wave ends, so
+// small blocks keep more waves resident when hotspot movers run long
+template <int DIFF_U, int WPB>
+__global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[WPB * SORT_LDS];
+    const uint64_t m = (uint64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+    if (m >= b.st->n_gm) return;
+    mover_one<DIFF_U, SORT_LDS>(b, m, lds, b.w.gn, b.w.gn_start, b.gm_start);
+}
+
+// Small-space mode (every space's grid fits in LDS: config #4's 10k spaces of
+// 1k): one block per space copies the space's grid entries and the row
+// starts of both grids into LDS, then its waves walk the space's mover-grid
+// entries with every grid candidate and row start read from LDS (mover-grid
+// candidates, ~10 % of them, stay global).
+constexpr uint32_t SMALL_SORT = 256;    // own events sorted in LDS up to this many (more: block sort)
+template <int DIFF_U>
+__global__ void __launch_bounds__(NT) k_mover_small(TickBufs b) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * SMALL_SORT];
+    extern __shared__ uint4 dyn_lds[];
+    const uint32_t s = blockIdx.x;
+    const SpaceP P = b.w.sp[s];
+    const uint32_t cb = P.cell_base, nc = (uint32_t)(P.W * P.H);
+    const uint32_t m0 = b.gm_start[cb], m1 = b.gm_start[cb + nc];
+    if (m0 >= m1) return;                                   // block-uniform: no movers here
+    const uint32_t g0 = b.w.gn_start[cb], g1 = b.w.gn_start[cb + nc];
+    GEnt* G = (GEnt*)dyn_lds;
+    uint32_t* S = (uint32_t*)(G + b.small_ents);
+    uint32_t* MS = S + nc + 1;
+    const uint32_t ng = min(g1 - g0, b.small_ents);        // (host guarantee: g1 - g0 <= small_ents)
+    for (uint32_t i = threadIdx.x; i < ng; i += NT) G[i] = b.w.gn[g0 + i];
+    for (uint32_t i = threadIdx.x; i <= nc; i += NT) {
+        S[i] = b.w.gn_start[cb + i];
+        MS[i] = b.gm_start[cb + i];
+    }
+    __syncthreads();
+    for (uint32_t m = m0 + (threadIdx.x >> 6); m < m1; m += NWAVE) {
+        mover_one<DIFF_U, SMALL_SORT>(b, m, lds, G - g0, S - cb, MS - cb);
+        wave_sync();
     }
 }
 
@@ -1381,6 +1424,11 @@ void launch_bk_split_init(uint32_t* sp, int wbits, hipStream_t s) {
 
 void tick_diff(const TickBufs& b, hipStream_t s) {
     const uint64_t nmax = 2ull * b.m;
+    if (b.small_ents) {                    // small-space mode: a block per space
+        const size_t lds = (size_t)b.small_ents * sizeof(GEnt) + 2 * ((size_t)b.small_cells + 1) * 4;
+        hipLaunchKernelGGL((k_mover_small<2>), dim3(b.n_spaces), dim3(NT), lds, s, b);
+        return;
+    }
     switch (b.diff_u) {                    // GW_MOVER_WPB: waves per k_mover block
     case 2: hipLaunchKernelGGL((k_mover<2, 2>), dim3(nblk1(nmax, 2)), dim3(128), 0, s, b); break;
     case 4: hipLaunchKernelGGL((k_mover<2, 4>), dim3(nblk1(nmax, 4)), dim3(256), 0, s, b); break;

@@ -451,7 +451,7 @@ void gw_shutdown(gw_ctx* c) {
     if (c->st) (void)hipStreamSynchronize(c->st);
     DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1,
                       &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
-                      &c->mcnt, &c->moff, &c->minfo, &c->icnt, &c->ioff, &c->mreg, &c->chunk_first, &c->bk_a, &c->bk_b, &c->bk_id, &c->bk_cnt, &c->bk_split, &c->ev_d, &c->rtable,
+                      &c->mcnt, &c->moff, &c->minfo, &c->icnt, &c->ioff, &c->mreg, &c->chunk_first, &c->srange, &c->bk_a, &c->bk_b, &c->bk_id, &c->bk_cnt, &c->bk_split, &c->ev_d, &c->rtable,
                       &c->scan_status, &c->rs_hist,
                       &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
                       &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf, &c->cl_slot, &c->cl_off,
@@ -722,6 +722,22 @@ static void choose_buckets(gw_ctx* c, TickBufs& b, bool full = false) {
     b.ev_full = full || c->ev_full_ticks > 0 || (est >> bits) > (uint64_t)BK_LCAP / 2 || b.wbits > BK_MAX_WBITS;
 }
 
+// small-space mode: every space's grid (entries + row starts of both grids)
+// fits in SMALL_LDS_MAX bytes of LDS, and there are many spaces
+static void small_mode(gw_ctx* c, TickBufs& b) {
+    uint32_t me = 0, mc = 0;
+    for (auto& sp : c->spaces)
+        if (sp.alive) {
+            me = std::max(me, sp.cap);
+            mc = std::max(mc, (uint32_t)(sp.p.W * sp.p.H));
+        }
+    static const bool on = !getenv("GW_SMALL") || atoi(getenv("GW_SMALL")) != 0;
+    b.n_spaces = (uint32_t)c->spaces.size();
+    const bool small = on && b.n_spaces >= 2 && (size_t)me * sizeof(GEnt) + 2 * ((size_t)mc + 1) * 4 <= SMALL_LDS_MAX;
+    b.small_ents = small ? me : 0;
+    b.small_cells = small ? mc : 0;
+}
+
 static void bind_events(gw_ctx* c, TickBufs& b) {
     b.own_cap = c->own_cap;
     b.own = P<uint32_t>(c->own); b.mir = P<uint64_t>(c->mir);
@@ -979,6 +995,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.minfo = P<uint4>(c->minfo); b.mreg = P<unsigned long long>(c->mreg);
     b.icnt = P<uint32_t>(c->icnt); b.ioff = P<uint32_t>(c->ioff);
     b.wbits = ceil_log2(C);
+    small_mode(c, b);
     bind_events(c, b);
     if (!c->ev_est) c->ev_est = 16ull * M;
     choose_buckets(c, b);
@@ -1065,8 +1082,33 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
                  (uint64_t*)&st->rec_total, c->st);
     size_t s_count = prof_end(c, 0);
     prof_begin(c, "sync_write");
-    launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint64_t>(c->rec_off),
-                      P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
+    // small-space mode: every space's grid fits in LDS (config #4's many small spaces)
+    uint32_t max_ents = 0, max_cells = 0;
+    for (auto& sp : c->spaces)
+        if (sp.alive) {
+            max_ents = std::max(max_ents, sp.cap);
+            max_cells = std::max(max_cells, (uint32_t)(sp.p.W * sp.p.H));
+        }
+    const uint32_t n_sp = (uint32_t)c->spaces.size();
+    static const bool small_on = !getenv("GW_SMALL") || atoi(getenv("GW_SMALL")) != 0;
+    const bool small = small_on && n_sp >= 2 &&
+                       (size_t)max_ents * sizeof(GEnt) + ((size_t)max_cells + 1) * 4 <= SMALL_LDS_MAX;
+    auto write_pass = [&]() {
+        if (small)
+            launch_sync_write_small(w, n_sp, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), P<uint64_t>(c->rec_off),
+                                    P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st,
+                                    P<uint32_t>(c->srange), P<uint32_t>(c->srange) + n_sp, max_ents, max_cells, c->st);
+        else
+            launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint64_t>(c->rec_off),
+                              P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
+    };
+    if (small) {
+        if ((rc = ensure(c, c->srange, (size_t)n_sp * 8))) return rc;
+        HIPCHK(hipMemsetAsync(c->srange.p, 0, (size_t)n_sp * 8, c->st));
+        launch_space_ranges(w, P<uint32_t>(c->flagged), nf, C, P<uint32_t>(c->srange), P<uint32_t>(c->srange) + n_sp,
+                            c->st);
+    }
+    write_pass();
     size_t s_write = prof_end(c, 0);
     HIPCHK(hipGetLastError());
     if ((rc = read_cstats(c))) return rc;                // the one host sync
@@ -1078,8 +1120,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         if ((rc = ensure(c, c->rec0, c->rec_cap * sizeof(gw_sync_record)))) return rc;
         c->hcstats->overflow = 0;
         HIPCHK(hipMemcpyAsync(c->cstats, c->hcstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
-        launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint64_t>(c->rec_off),
-                          P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
+        write_pass();
         HIPCHK(hipGetLastError());
         if ((rc = read_cstats(c))) return rc;
         if (c->hcstats->overflow) return set_err(c, GW_ENOMEM, "sync record buffer overflowed twice");

@@ -101,27 +101,28 @@ __device__ __forceinline__ Flat flat_build(const SpaceP& P, const Rects& R, cons
 }
 
 // Maps the lane's candidates k = B + 64u + lane (u < U) to (grid, index);
-// idx = ~0 past the end.  Ranges wholly before B + 64U are dropped from live.
+// idx = ~0 past the end.  Each lane finds its range by a binary search over
+// the ranges' exclusive prefixes (the largest range j with pre[j] <= k; empty
+// ranges share their successor's prefix and lose the tie), 6 shuffle steps
+// per chunk instead of a serial walk over every live range with readlanes
+// (a VALU cost per range that dominated the walk for short candidate lists).
 template <int U, int NK>
 __device__ __forceinline__ void flat_map(Flat& f, uint32_t B, uint32_t (&idx)[U], uint32_t (&kind)[U]) {
     const int ln = lane_id();
-    const uint32_t end = B + 64u * U;
 #pragma unroll
-    for (int u = 0; u < U; ++u) { idx[u] = ~0u; kind[u] = 0; }
-    uint64_t m = f.live;
-    while (m) {
-        const int j = __builtin_ctzll(m);
-        const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)f.pre, j);
-        if (sp >= end) break;
-        const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)f.len, j);
-        const uint32_t ss = (uint32_t)__builtin_amdgcn_readlane((int)f.start, j);
+    for (int u = 0; u < U; ++u) {
+        const uint32_t k = B + 64u * u + (uint32_t)ln;
+        uint32_t lo = 0;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t r = B + 64u * u + (uint32_t)ln - sp;
-            if (r < sl) { idx[u] = ss + r; kind[u] = NK == 2 ? (uint32_t)(j & 1) : 0u; }
+        for (int step = 32; step; step >>= 1) {
+            const uint32_t c = lo + (uint32_t)step;
+            const uint32_t p = (uint32_t)__shfl((int)f.pre, (int)min(c, 63u), 64);
+            if (c < 64u && p <= k) lo = c;
         }
-        if (sp + sl <= end) f.live &= ~(1ull << j);
-        m &= m - 1;
+        const uint32_t ss = (uint32_t)__shfl((int)f.start, (int)lo, 64);
+        const uint32_t sp = (uint32_t)__shfl((int)f.pre, (int)lo, 64);
+        idx[u] = k < f.total ? ss + (k - sp) : ~0u;
+        kind[u] = NK == 2 ? (lo & 1u) : 0u;
     }
 }
 

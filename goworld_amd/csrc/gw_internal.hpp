@@ -207,6 +207,9 @@ struct TickBufs {
     uint64_t ev_cap;
     uint32_t* rtable;         // radix_sort2 scratch
     int wbits;                // bits of a slot
+    uint32_t n_spaces;        // spaces of the context (dead ones included)
+    uint32_t small_ents;      // small-space mode: max entries per space (0: off)
+    uint32_t small_cells;     //   and max cells per space
     int diff_u;               // candidate chunks of 64 in flight per k_mover iteration
 };
 
@@ -244,6 +247,14 @@ void tick_reset(const TickBufs& b, hipStream_t s);                 // after the 
 void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n, bool grid_ok,
                         hipStream_t s);
 // sync collect
+void launch_space_ranges(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
+                         uint32_t* sfirst, uint32_t* slast, hipStream_t s);
+void launch_sync_write_small(const World& w, uint32_t n_spaces, const uint32_t* flagged, const uint32_t* fbits,
+                             const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec, uint64_t rec_cap,
+                             DevStats* st, const uint32_t* sfirst, const uint32_t* slast, uint32_t max_ents,
+                             uint32_t max_cells, hipStream_t s);
+// small-space mode: every space's grid (entries + row starts) in this many LDS bytes at most
+constexpr size_t SMALL_LDS_MAX = 48 * 1024;
 void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint32_t* fbits, ScanCtx& sc,
                          uint32_t* total, hipStream_t s);
 void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,

@@ -269,6 +269,132 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
         }
     }
 }
+// ---------------------------------------------------------------------------
+// Small-space mode (every space's grid fits in LDS, e.g. config #4's 10k
+// spaces of 1k): one block per space loads the space's grid entries and row
+// starts into LDS once, then its waves write the records of the space's
+// flagged entities (a contiguous range of the slot-ordered flagged list) with
+// every candidate read from LDS: the per-entity chain of dependent global
+// loads shrinks to the entity's own state.
+__global__ void __launch_bounds__(NT) k_space_ranges(World w, const uint32_t* __restrict__ flagged,
+                                                     const uint64_t* nf_dev, uint32_t nf_max,
+                                                     uint32_t* __restrict__ sfirst, uint32_t* __restrict__ slast) {
+    const uint64_t nf = load_n(nf_max, nf_dev);
+    const uint64_t k = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= nf) return;
+    const uint32_t s = w.aoi[flagged[k]].meta & SPACE_MASK;
+    const uint32_t sp = k ? (w.aoi[flagged[k - 1]].meta & SPACE_MASK) : 0xffffffffu;
+    const uint32_t sn = k + 1 < nf ? (w.aoi[flagged[k + 1]].meta & SPACE_MASK) : 0xffffffffu;
+    if (sp != s) sfirst[s] = (uint32_t)k;
+    if (sn != s) slast[s] = (uint32_t)(k + 1);
+}
+
+template <int NB_U, typename F>
+__device__ __forceinline__ void wave_neighbors_lds(const World& w, uint32_t e, const AoiEnt& a, const SpaceP& P,
+                                                   const GEnt* G, uint32_t g0, const uint32_t* S, F f) {
+    const float d = P.d;
+    const Win we = win_of(a.x, a.z, d);
+    Rects R;
+    R.n = 1;
+    R.r[0] = search_rect(P, a.x, a.z);
+    Flat fl = flat_build<1>(P, R, S - P.cell_base, nullptr);   // S[c - cell_base] = gn_start[c]
+    unsigned long long se = 0;
+    bool have_se = false;
+    for (uint32_t base = 0; base < fl.total; base += 64u * NB_U) {
+        uint32_t idx[NB_U], kd[NB_U];
+        flat_map<NB_U, 1>(fl, base, idx, kd);
+#pragma unroll
+        for (int u = 0; u < NB_U; ++u) {
+            if (base + 64u * u >= fl.total) break;            // wave-uniform
+            bool rel = false;
+            GEnt g;
+            g.slot = e;
+            g.meta = 0;
+            if (idx[u] != ~0u) g = G[idx[u] - g0];
+            if (g.slot != e) {
+                const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
+                rel = ia;
+                if (ia != ib) {
+                    if (!have_se) { se = w.stamp[e]; have_se = true; }
+                    rel = resolve(ia, ib, se, w.stamp[g.slot]);
+                }
+            }
+            f(rel, g.slot, (g.meta & CLIENT_BIT) ? 1u : 0u);
+        }
+    }
+}
+
+template <int U>
+__global__ void __launch_bounds__(NT) k_sync_write_small(World w, const uint32_t* __restrict__ flagged,
+                                                         const uint32_t* __restrict__ fbits,
+                                                         const uint64_t* __restrict__ rec_off,
+                                                         const uint32_t* __restrict__ cnt, gw_sync_record* rec,
+                                                         uint64_t rec_cap, DevStats* st,
+                                                         const uint32_t* __restrict__ sfirst,
+                                                         const uint32_t* __restrict__ slast, uint32_t max_ents) {
+    extern __shared__ uint4 dyn_lds[];
+    const uint32_t s = blockIdx.x;
+    const uint32_t lo = sfirst[s], hi = slast[s];
+    if (lo >= hi) return;                                   // block-uniform
+    const SpaceP P = w.sp[s];
+    const uint32_t cb = P.cell_base, nc = (uint32_t)(P.W * P.H);
+    const uint32_t g0 = w.gn_start[cb], g1 = w.gn_start[cb + nc];
+    GEnt* G = (GEnt*)dyn_lds;
+    uint32_t* S = (uint32_t*)(G + max_ents);
+    const uint32_t ng = min(g1 - g0, max_ents);             // (host guarantee: g1 - g0 <= max_ents)
+    for (uint32_t i = threadIdx.x; i < ng; i += NT) G[i] = w.gn[g0 + i];
+    for (uint32_t i = threadIdx.x; i <= nc; i += NT) S[i] = w.gn_start[cb + i];
+    __syncthreads();
+    const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
+    for (uint32_t k = lo + (threadIdx.x >> 6); k < hi; k += NWAVE) {
+        const uint32_t e = flagged[k];
+        const uint32_t f = fbits[k];
+        uint64_t at = rec_off[k];
+        if (at + cnt[k] > rec_cap) {
+            if (ln == 0) atomicOr(&st->overflow, 1ull);
+            continue;
+        }
+        const AoiEnt a = w.aoi[e];
+        if (!owned_x(P, a.x)) continue;
+        const float4 p = w.pos[e];
+        if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
+            if (ln == 0) st_record_nt(rec + at, e, e, p);
+            ++at;
+        }
+        if ((f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
+            wave_neighbors_lds<U>(w, e, a, P, G, g0, S, [&](bool rel, uint32_t ws, uint32_t g) {
+                const bool take = rel && g != 0;
+                const uint64_t bt = wave_ballot(take);
+                if (take) st_record_nt(rec + at + (uint64_t)popc64(bt & lt), ws, e, p);
+                at += (uint64_t)popc64(bt);
+            });
+        }
+    }
+}
+
+void launch_space_ranges(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
+                         uint32_t* sfirst, uint32_t* slast, hipStream_t s) {
+    if (nf_max) hipLaunchKernelGGL(k_space_ranges, dim3(nblk1(nf_max, NT)), dim3(NT), 0, s, w, flagged, nf_dev, nf_max,
+                                   sfirst, slast);
+}
+void launch_sync_write_small(const World& w, uint32_t n_spaces, const uint32_t* flagged, const uint32_t* fbits,
+                             const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec, uint64_t rec_cap,
+                             DevStats* st, const uint32_t* sfirst, const uint32_t* slast, uint32_t max_ents,
+                             uint32_t max_cells, hipStream_t s) {
+    if (!n_spaces) return;
+    const size_t lds = (size_t)max_ents * sizeof(GEnt) + ((size_t)max_cells + 1) * 4;
+    if (w.nb_u >= 8)
+        hipLaunchKernelGGL(k_sync_write_small<8>, dim3(n_spaces), dim3(NT), lds, s, w, flagged, fbits, rec_off, cnt,
+                           rec, rec_cap, st, sfirst, slast, max_ents);
+    else if (w.nb_u <= 2)
+        hipLaunchKernelGGL(k_sync_write_small<2>, dim3(n_spaces), dim3(NT), lds, s, w, flagged, fbits, rec_off, cnt,
+                           rec, rec_cap, st, sfirst, slast, max_ents);
+    else
+        hipLaunchKernelGGL(k_sync_write_small<4>, dim3(n_spaces), dim3(NT), lds, s, w, flagged, fbits, rec_off, cnt,
+                           rec, rec_cap, st, sfirst, slast, max_ents);
+}
+
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
                        uint64_t rec_cap, DevStats* st, hipStream_t s) {

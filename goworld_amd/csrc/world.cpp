@@ -226,8 +226,9 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
     }
     const unsigned long long base = 1 + (W.tick * W.g.ranks + W.g.rank) * STAMP_STRIDE;
     launch_iota_u64(P<unsigned long long>(W.stamps), base, n, c->st);
-    launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->last_pos,
-                      c->last_aoi, c->last_leave, c->clr, c->rflag, c->halo, c->st, /*pad=*/false);
+    if (D.n)                                          // a one-strip world has nobody to route to
+        launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->last_pos,
+                          c->last_aoi, c->last_leave, c->clr, c->rflag, c->halo, c->st, /*pad=*/false);
     HIPCHK(hipGetLastError());
     uint32_t rcnt[2] = {0, 0};
     if (any_nb) {

@@ -17,7 +17,7 @@ def summarize(path, last=3):
     rows = list(csv.DictReader(open(path)))
     by = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in rows:
-        k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("gw::", "")
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("gw::", "")
         by[k][r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     out = {}
     for k, cs in by.items():

@@ -111,6 +111,12 @@ __device__ __forceinline__ void flat_map(Flat& f, uint32_t B, uint32_t (&idx)[U]
     const int ln = lane_id();
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+        idx[u] = ~0u;
+        kind[u] = 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (B + 64u * u >= f.total) break;                  // wave-uniform: chunk past the end
         const uint32_t k = B + 64u * u + (uint32_t)ln;
         uint32_t lo = 0;
 #pragma unroll
@@ -123,6 +129,31 @@ __device__ __forceinline__ void flat_map(Flat& f, uint32_t B, uint32_t (&idx)[U]
         const uint32_t sp = (uint32_t)__shfl((int)f.pre, (int)lo, 64);
         idx[u] = k < f.total ? ss + (k - sp) : ~0u;
         kind[u] = NK == 2 ? (lo & 1u) : 0u;
+    }
+}
+
+// The same by walking the live ranges with readlanes (cheaper in VALU when a
+// chunk overlaps few ranges: the collect's long hotspot windows at config #3)
+template <int U, int NK>
+__device__ __forceinline__ void flat_map_walk(Flat& f, uint32_t B, uint32_t (&idx)[U], uint32_t (&kind)[U]) {
+    const int ln = lane_id();
+    const uint32_t end = B + 64u * U;
+#pragma unroll
+    for (int u = 0; u < U; ++u) { idx[u] = ~0u; kind[u] = 0; }
+    uint64_t m = f.live;
+    while (m) {
+        const int j = __builtin_ctzll(m);
+        const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)f.pre, j);
+        if (sp >= end) break;
+        const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)f.len, j);
+        const uint32_t ss = (uint32_t)__builtin_amdgcn_readlane((int)f.start, j);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t r = B + 64u * u + (uint32_t)ln - sp;
+            if (r < sl) { idx[u] = ss + r; kind[u] = NK == 2 ? (uint32_t)(j & 1) : 0u; }
+        }
+        if (sp + sl <= end) f.live &= ~(1ull << j);
+        m &= m - 1;
     }
 }
 

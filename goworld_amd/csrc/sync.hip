@@ -32,7 +32,7 @@ __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) 
     bool have_se = false;
     for (uint32_t base = 0; base < fl.total; base += 64u * NB_U) {
         uint32_t idx[NB_U], kd[NB_U];
-        flat_map<NB_U, 1>(fl, base, idx, kd);
+        flat_map_walk<NB_U, 1>(fl, base, idx, kd);
         GEnt gg[NB_U];
 #pragma unroll
         for (int u = 0; u < NB_U; ++u) {
@@ -373,6 +373,128 @@ __global__ void __launch_bounds__(NT) k_sync_write_small(World w, const uint32_t
     }
 }
 
+// The same with two entities per wave (a half-wave each): with short
+// candidate lists (config #4: ~80) the per-entity setup dominates a wave's
+// VALU, and a half-wave still covers a list in 2-3 chunks of 32.  Rows of a
+// window (<= 11) fit a half-wave; the row scan is the wave scan minus lane
+// 31's prefix for the upper half; a lane finds its range by a 5-step search
+// over its half's prefixes; record slots come from the half's ballot bits.
+__global__ void __launch_bounds__(NT) k_sync_write_small2(World w, const uint32_t* __restrict__ flagged,
+                                                          const uint32_t* __restrict__ fbits,
+                                                          const uint64_t* __restrict__ rec_off,
+                                                          const uint32_t* __restrict__ cnt, gw_sync_record* rec,
+                                                          uint64_t rec_cap, DevStats* st,
+                                                          const uint32_t* __restrict__ sfirst,
+                                                          const uint32_t* __restrict__ slast, uint32_t max_ents) {
+    extern __shared__ uint4 dyn_lds[];
+    const uint32_t s = blockIdx.x;
+    const uint32_t lo = sfirst[s], hi = slast[s];
+    if (lo >= hi) return;                                   // block-uniform
+    const SpaceP P = w.sp[s];
+    const uint32_t cb = P.cell_base, nc = (uint32_t)(P.W * P.H);
+    const uint32_t g0 = w.gn_start[cb], g1 = w.gn_start[cb + nc];
+    GEnt* G = (GEnt*)dyn_lds;
+    uint32_t* S = (uint32_t*)(G + max_ents);
+    const uint32_t ng = min(g1 - g0, max_ents);
+    for (uint32_t i = threadIdx.x; i < ng; i += NT) G[i] = w.gn[g0 + i];
+    for (uint32_t i = threadIdx.x; i <= nc; i += NT) S[i] = w.gn_start[cb + i];
+    __syncthreads();
+    const int ln = lane_id();
+    const uint32_t half = (uint32_t)ln >> 5, hl = (uint32_t)ln & 31u, hb = half << 5;
+    const uint64_t hmask = half ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+    const uint64_t lt = lanemask_lt();
+    const float d = P.d;
+    for (uint32_t k0 = lo + (threadIdx.x >> 6) * 2; k0 < hi; k0 += NWAVE * 2) {
+        const uint32_t k = k0 + half;
+        const bool valid = k < hi;
+        uint32_t e = 0, f = 0, c = 0;
+        uint64_t at = 0;
+        if (valid) {
+            e = flagged[k];
+            f = fbits[k];
+            at = rec_off[k];
+            c = cnt[k];
+        }
+        bool walk = false;
+        AoiEnt a;
+        a.x = a.z = 0.0f;
+        a.meta = 0;
+        float4 p = make_float4(0, 0, 0, 0);
+        if (valid) {
+            if (at + c > rec_cap) {
+                if (hl == 0) atomicOr(&st->overflow, 1ull);
+            } else {
+                a = w.aoi[e];
+                if (owned_x(P, a.x)) {
+                    p = w.pos[e];
+                    if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
+                        if (hl == 0) st_record_nt(rec + at, e, e, p);
+                        ++at;
+                    }
+                    walk = (f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT);
+                }
+            }
+        }
+        // the half's row ranges (lane hl: row hl of its window), then its scan
+        uint32_t rs = 0, rl = 0;
+        const Win we = win_of(a.x, a.z, d);
+        if (walk) {
+            const Rect r = search_rect(P, a.x, a.z);
+            const int nr = r.z1 - r.z0 + 1;
+            if ((int)hl < nr) {
+                const uint32_t base = (uint32_t)(r.z0 + (int)hl) * (uint32_t)P.W;   // local cell index
+                rs = S[base + (uint32_t)r.x0];
+                rl = S[base + (uint32_t)r.x1 + 1] - rs;
+            }
+        }
+        const uint32_t inc64 = wave_incl_scan<uint32_t>(rl);
+        const uint32_t lo31 = (uint32_t)__builtin_amdgcn_readlane((int)inc64, 31);
+        const uint32_t inc = half ? inc64 - lo31 : inc64;
+        const uint32_t pre = inc - rl;
+        const uint32_t tot0 = lo31, tot1 = (uint32_t)__builtin_amdgcn_readlane((int)inc64, 63) - lo31;
+        const uint32_t total = half ? tot1 : tot0;
+        const uint32_t tmax = max(tot0, tot1);
+        const unsigned long long pxy = ((unsigned long long)__float_as_uint(p.y) << 32) | __float_as_uint(p.x);
+        const unsigned long long pzw = ((unsigned long long)__float_as_uint(p.w) << 32) | __float_as_uint(p.z);
+        unsigned long long se = 0;
+        bool have_se = false;
+        for (uint32_t B = 0; B < tmax; B += 32) {             // wave-uniform
+            const uint32_t kk = B + hl;
+            uint32_t l2 = 0;
+#pragma unroll
+            for (int step = 16; step; step >>= 1) {
+                const uint32_t cc = l2 + (uint32_t)step;
+                const uint32_t pv = (uint32_t)__shfl((int)pre, (int)(hb + min(cc, 31u)), 64);
+                if (cc < 32u && pv <= kk) l2 = cc;
+            }
+            const uint32_t ss = (uint32_t)__shfl((int)rs, (int)(hb + l2), 64);
+            const uint32_t sp = (uint32_t)__shfl((int)pre, (int)(hb + l2), 64);
+            bool take = false;
+            GEnt g;
+            g.slot = e;
+            g.meta = 0;
+            if (kk < total) g = G[ss + (kk - sp) - g0];
+            if (kk < total && g.slot != e && (g.meta & CLIENT_BIT)) {
+                const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
+                bool rel = ia;
+                if (ia != ib) {
+                    if (!have_se) { se = w.stamp[e]; have_se = true; }
+                    rel = resolve(ia, ib, se, w.stamp[g.slot]);
+                }
+                take = rel;
+            }
+            const uint64_t bt = wave_ballot(take) & hmask;
+            if (take) {
+                unsigned long long* q = (unsigned long long*)(rec + at + (uint64_t)popc64(bt & lt));
+                __builtin_nontemporal_store(((unsigned long long)e << 32) | g.slot, q);
+                __builtin_nontemporal_store(pxy, q + 1);
+                __builtin_nontemporal_store(pzw, q + 2);
+            }
+            at += (uint64_t)popc64(bt);
+        }
+    }
+}
+
 void launch_space_ranges(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
                          uint32_t* sfirst, uint32_t* slast, hipStream_t s) {
     if (nf_max) hipLaunchKernelGGL(k_space_ranges, dim3(nblk1(nf_max, NT)), dim3(NT), 0, s, w, flagged, nf_dev, nf_max,
@@ -384,6 +506,12 @@ void launch_sync_write_small(const World& w, uint32_t n_spaces, const uint32_t* 
                              uint32_t max_cells, hipStream_t s) {
     if (!n_spaces) return;
     const size_t lds = (size_t)max_ents * sizeof(GEnt) + ((size_t)max_cells + 1) * 4;
+    static const bool halves = !getenv("GW_SYNC_HALVES") || atoi(getenv("GW_SYNC_HALVES")) != 0;
+    if (halves) {
+        hipLaunchKernelGGL(k_sync_write_small2, dim3(n_spaces), dim3(NT), lds, s, w, flagged, fbits, rec_off, cnt,
+                           rec, rec_cap, st, sfirst, slast, max_ents);
+        return;
+    }
     if (w.nb_u >= 8)
         hipLaunchKernelGGL(k_sync_write_small<8>, dim3(n_spaces), dim3(NT), lds, s, w, flagged, fbits, rec_off, cnt,
                            rec, rec_cap, st, sfirst, slast, max_ents);

@@ -667,6 +667,189 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     mover_one<DIFF_U, SORT_LDS>(b, m, lds, b.w.gn, b.w.gn_start, b.gm_start);
 }
 
+// Two mover-grid entries per wave (a half-wave each), small-space mode: with
+// ~80 candidates per mover the per-mover setup dominates a wave's VALU.  A
+// half holds <= 16 row ranges x 2 grids; the row scan is the wave scan minus
+// lane 31's prefix for the upper half; a lane finds its range by a 5-step
+// search over its half's prefixes; ballots are masked per half; own events
+// (<= 32) are sorted inside the half in registers, more go to the block sort.
+// Returns false (nothing done) when either entry needs more rows: the caller
+// then runs both through mover_one.
+template <int HU>
+__device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint64_t m_end, const SpaceP& P,
+                                           const GEnt* GN, const uint32_t* GS, const uint32_t* MS) {
+    const int ln = lane_id();
+    const uint32_t half = (uint32_t)ln >> 5, hl = (uint32_t)ln & 31u, hb = half << 5;
+    const uint64_t hmask = half ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+    const uint64_t lt = lanemask_lt();
+    const uint64_t m = m0 + half;
+    const bool valid = m < m_end;
+    MEnt me;
+    me.tags = 0;
+    me.x = me.z = me.ox = me.oz = qnan();
+    me.slot = 0; me.client = 0; me.space = 0;
+    if (valid) me = b.gm[m];
+    const bool prim = valid && (me.tags & TAG_PRIMARY);
+    const bool pn = me.x == me.x, po = me.ox == me.ox;
+    Rects R;
+    R.n = 0;
+    if (prim) R = mover_rects(P, po, me.ox, me.oz, pn, me.x, me.z);
+    int rows = 0;
+    for (int q = 0; q < R.n; ++q) rows += R.r[q].z1 - R.r[q].z0 + 1;
+    if (wave_ballot(rows > 16)) return false;              // wave-uniform
+    const World& w = b.w;
+    uint64_t reg = 0, cap = 0;
+    bool go = prim;
+    if (prim) {
+        reg = b.reg[m];
+        cap = b.cand[m];
+        if (reg + cap > b.own_cap) {                        // region past the buffers: the host redoes the diff
+            if (hl == 0) atomicOr(&b.st->overflow, 1ull);
+            go = false;
+        }
+    }
+    const uint32_t A = me.slot;
+    const float d = P.d;
+    const bool ownA = owned_x(P, pn ? me.x : me.ox);
+    unsigned long long sA = 0, soA = 0;
+    if (go) { sA = w.stamp[A]; soA = w.prev[A].ostamp; }
+    const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
+    // this half's row ranges: lane hl = row hl/2 of the rects, grid hl%2
+    uint32_t rs = 0, rl = 0;
+    if (go) {
+        const int row = (int)(hl >> 1), kind = (int)(hl & 1u);
+        const int nr0 = R.n > 0 ? R.r[0].z1 - R.r[0].z0 + 1 : 0;
+        const int nr1 = R.n > 1 ? R.r[1].z1 - R.r[1].z0 + 1 : 0;
+        if (row < nr0 + nr1) {
+            const bool first = row < nr0;
+            const int x0 = first ? R.r[0].x0 : R.r[1].x0;
+            const int x1 = first ? R.r[0].x1 : R.r[1].x1;
+            const int cz = first ? R.r[0].z0 + row : R.r[1].z0 + (row - nr0);
+            const uint32_t base = P.cell_base + (uint32_t)cz * (uint32_t)P.W;
+            const uint32_t* st = kind ? MS : GS;
+            rs = st[base + x0];
+            rl = st[base + x1 + 1] - rs;
+        }
+    }
+    const uint32_t inc64 = wave_incl_scan<uint32_t>(rl);
+    const uint32_t lo31 = (uint32_t)__builtin_amdgcn_readlane((int)inc64, 31);
+    const uint32_t inc = half ? inc64 - lo31 : inc64;
+    const uint32_t pre = inc - rl;
+    const uint32_t tot0 = lo31, tot1 = (uint32_t)__builtin_amdgcn_readlane((int)inc64, 63) - lo31;
+    const uint32_t total = half ? tot1 : tot0;
+    const uint32_t tmax = max(tot0, tot1);
+    uint32_t* out = b.own + reg;
+    uint64_t* mir = b.mir + reg;
+    uint32_t n = 0, nl = 0, nm_ = 0, nml = 0;
+    uint32_t c_old = 0, c_new = 0, c_band = 0, c_cli = 0;
+    for (uint32_t base = 0; base < tmax; base += 32u * HU) {   // wave-uniform
+        Cand cc[HU];
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+            cc[u].info = 0;
+            cc[u].slot = A;
+            if (base + 32u * u >= tmax) continue;            // wave-uniform
+            const uint32_t kk = base + 32u * u + hl;
+            uint32_t l2 = 0;
+#pragma unroll
+            for (int step = 16; step; step >>= 1) {
+                const uint32_t c2 = l2 + (uint32_t)step;
+                const uint32_t pv = (uint32_t)__shfl((int)pre, (int)(hb + min(c2, 31u)), 64);
+                if (c2 < 32u && pv <= kk) l2 = c2;
+            }
+            const uint32_t ss = (uint32_t)__shfl((int)rs, (int)(hb + l2), 64);
+            const uint32_t sp = (uint32_t)__shfl((int)pre, (int)(hb + l2), 64);
+            if (kk < total) {
+                const uint32_t idx = ss + (kk - sp);
+                if ((l2 & 1u) == 0) {
+                    const GEnt e = GN[idx];
+                    cc[u].x = cc[u].ox = e.x;
+                    cc[u].z = cc[u].oz = e.z;
+                    cc[u].slot = (e.meta & MOVER_BIT) ? A : e.slot;
+                    cc[u].info = TAG_OLD | TAG_NEW | (e.meta & CLIENT_BIT ? CAND_CLIENT : 0u) | CAND_NONMOVER;
+                } else {
+                    const MEnt e = b.gm[idx];
+                    cc[u].x = e.x; cc[u].z = e.z; cc[u].ox = e.ox; cc[u].oz = e.oz;
+                    cc[u].slot = e.slot;
+                    cc[u].info = e.tags | (e.client ? CAND_CLIENT : 0u);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+            if (base + 32u * u >= tmax) break;               // wave-uniform
+            const Cand& e = cc[u];
+            bool ev = false, lv = false, nmv = false;
+            bool t_ro = false, t_rn = false, t_cli = false, b_o = false, b_n = false;
+            uint32_t key = 0;
+            if (go && e.slot != A) {
+                nmv = (e.info & CAND_NONMOVER) != 0;
+                const bool iao = wo.has(e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, me.ox, me.oz);
+                const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, me.x, me.z);
+                bool ro = iao, rn = ian;
+                b_o = iao != ibo;
+                b_n = ian != ibn;
+                if (b_o || b_n) {
+                    const unsigned long long sb = w.stamp[e.slot];
+                    const unsigned long long sbo = nmv ? sb : w.prev[e.slot].ostamp;
+                    if (b_o) ro = resolve(iao, ibo, soA, sbo);
+                    if (b_n) rn = resolve(ian, ibn, sA, sb);
+                }
+                const bool take = ((e.info & TAG_OLD) && ro) || ((e.info & TAG_NEW) && rn && !ro);
+                if (take) {
+                    t_ro = ro; t_rn = rn;
+                    t_cli = rn && (e.info & CAND_CLIENT) != 0;
+                    ev = ro != rn;
+                    lv = ro;
+                    key = (lv ? 0x80000000u : 0u) | e.slot;
+                }
+            }
+            c_old += (uint32_t)popc64(wave_ballot(t_ro) & hmask);
+            c_new += (uint32_t)popc64(wave_ballot(t_rn) & hmask);
+            c_cli += (uint32_t)popc64(wave_ballot(t_cli) & hmask);
+            c_band += (uint32_t)popc64(wave_ballot(b_o) & hmask) + (uint32_t)popc64(wave_ballot(b_n) & hmask);
+            const bool mev = ev && nmv && owned_x(P, e.x);
+            ev = ev && ownA;
+            const uint64_t be = wave_ballot(ev) & hmask, bl = wave_ballot(ev && lv) & hmask;
+            const uint64_t bm = wave_ballot(mev) & hmask;
+            const uint32_t at = n + (uint32_t)popc64(be & lt);
+            if (ev && at < cap) out[at] = key;
+            const uint32_t atm = nm_ + (uint32_t)popc64(bm & lt);
+            if (mev && atm < cap) mir[atm] = ((uint64_t)e.slot << 32) | (A << 1) | (lv ? 1u : 0u);
+            n += (uint32_t)popc64(be);
+            nl += (uint32_t)popc64(bl);
+            nm_ += (uint32_t)popc64(bm);
+            nml += (uint32_t)popc64(wave_ballot(mev && lv) & hmask);
+        }
+    }
+    // own events by (leave, target): <= 32 in registers inside the half, more by the block sort
+    const bool reg_sort = go && n > 1 && n <= 32;
+    if (wave_ballot(reg_sort)) {
+        wave_sync();
+        uint32_t v = (reg_sort && hl < n) ? out[hl] : 0xffffffffu;
+        v = half_sort32(v);
+        if (reg_sort && hl < n) out[hl] = v;
+    }
+    if (go && n > 32 && hl == 0) b.big[atomicAdd(&b.st->n_big, 1ull)] = (uint32_t)m;
+    if (valid && hl == 0) {
+        if (!go) {
+            b.mstat[m] = make_ulonglong2(0, 0);
+            b.ownc[m] = 0;
+            b.mirc[m] = 0;
+        } else {
+            b.ownc[m] = (unsigned long long)(n - nl) | ((unsigned long long)nl << 32);
+            b.mirc[m] = (unsigned long long)(nm_ - nml) | ((unsigned long long)nml << 32);
+            if (n | nm_) {
+                atomicOr(&b.movbit[A >> 5], 1u << (A & 31u));
+                b.gmi[A] = (uint32_t)m;
+            }
+            if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | c_cli;
+            b.mstat[m] = make_ulonglong2((unsigned long long)c_old | ((unsigned long long)c_new << 32), c_band);
+        }
+    }
+    return true;
+}
+
 // Small-space mode (every space's grid fits in LDS: config #4's 10k spaces of
 // 1k): one block per space copies the space's grid entries and the row
 // starts of both grids into LDS, then its waves walk the space's mover-grid
@@ -693,6 +876,17 @@ __global__ void __launch_bounds__(NT) k_mover_small(TickBufs b) {
         MS[i] = b.gm_start[cb + i];
     }
     __syncthreads();
+    if (b.small_halves) {
+        for (uint32_t m = m0 + (threadIdx.x >> 6) * 2; m < m1; m += NWAVE * 2) {
+            if (!mover_half<3>(b, m, m1, P, G - g0, S - cb, MS - cb)) {
+                mover_one<DIFF_U, SMALL_SORT>(b, m, lds, G - g0, S - cb, MS - cb);
+                wave_sync();
+                if (m + 1 < m1) mover_one<DIFF_U, SMALL_SORT>(b, m + 1, lds, G - g0, S - cb, MS - cb);
+            }
+            wave_sync();
+        }
+        return;
+    }
     for (uint32_t m = m0 + (threadIdx.x >> 6); m < m1; m += NWAVE) {
         mover_one<DIFF_U, SMALL_SORT>(b, m, lds, G - g0, S - cb, MS - cb);
         wave_sync();

@@ -736,6 +736,8 @@ static void small_mode(gw_ctx* c, TickBufs& b) {
     const bool small = on && b.n_spaces >= 2 && (size_t)me * sizeof(GEnt) + 2 * ((size_t)mc + 1) * 4 <= SMALL_LDS_MAX;
     b.small_ents = small ? me : 0;
     b.small_cells = small ? mc : 0;
+    static const bool halves = !getenv("GW_MOVER_HALVES") || atoi(getenv("GW_MOVER_HALVES")) != 0;
+    b.small_halves = halves ? 1 : 0;
 }
 
 static void bind_events(gw_ctx* c, TickBufs& b) {

@@ -244,6 +244,23 @@ __device__ __forceinline__ uint64_t wave_sort64_u64(uint64_t v) {
     return v;
 }
 
+// ascending bitonic sort of one value per lane inside each 32-lane half
+__device__ __forceinline__ uint32_t half_sort32(uint32_t v) {
+    const int l = lane_id() & 31;                     // both halves end ascending
+#pragma unroll
+    for (int k = 2; k <= 32; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t o = lane_xor(v, j);
+            const bool up = (l & k) == 0;
+            const bool lower = (l & j) == 0;
+            const uint32_t mn = v < o ? v : o, mx = v < o ? o : v;
+            v = (lower == up) ? mn : mx;
+        }
+    }
+    return v;
+}
+
 // In-place ascending sort of a[0, n) by a group of TPM threads with the
 // all-ascending bitonic network (first step of each merge compares mirrored
 // partners i ^ (k-1)).  Every exchange moves the smaller key to the lower

@@ -210,6 +210,7 @@ struct TickBufs {
     uint32_t n_spaces;        // spaces of the context (dead ones included)
     uint32_t small_ents;      // small-space mode: max entries per space (0: off)
     uint32_t small_cells;     //   and max cells per space
+    int small_halves;         //   two movers per wave (GW_MOVER_HALVES, default on)
     int diff_u;               // candidate chunks of 64 in flight per k_mover iteration
 };
 

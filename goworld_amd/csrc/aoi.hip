@@ -61,12 +61,12 @@ __global__ void __launch_bounds__(NT) k_ops1(TickBufs b) {
         atomicAdd(&b.st->bad_ops, 1ull);
         return;
     }
-    if (op.kind != GW_OP_LEAVE) atomicMax(&b.last_pos[op.slot], (int32_t)i);
-    if (op.kind != GW_OP_SYNC) atomicMax(&b.last_aoi[op.slot], (int32_t)i);
+    if (op.kind != GW_OP_LEAVE) atomicMax(&b.ol[op.slot].pos, (int32_t)i);
+    if (op.kind != GW_OP_SYNC) atomicMax(&b.ol[op.slot].aoi, (int32_t)i);
     if (op.kind == GW_OP_LEAVE) {
-        atomicMax(&b.last_leave[op.slot], (int32_t)i);
+        atomicMax(&b.ol[op.slot].leave, (int32_t)i);
         for (int c = 0; c < 2; ++c)                     // the last Leave that clears bit c
-            if (!((op.sync_flags >> c) & 1)) atomicMax(&b.clr[2 * op.slot + c], (int32_t)i);
+            if (!((op.sync_flags >> c) & 1)) atomicMax(&b.ol[op.slot].clr[c], (int32_t)i);
     }
 }
 
@@ -84,10 +84,10 @@ __global__ void __launch_bounds__(NT) k_ops2(TickBufs b) {
     gw_op op = b.ops[i];
     if (op.slot >= b.w.cap || op.kind != GW_OP_LEAVE) return;
     const uint32_t s = op.slot;
-    if (b.last_leave[s] != (int32_t)i) return;
+    if (b.ol[s].leave != (int32_t)i) return;
     uint32_t keep = 0xffffffffu;
     for (int c = 0; c < 2; ++c)
-        if (b.clr[2 * s + c] >= 0) keep &= ~(1u << c);
+        if (b.ol[s].clr[c] >= 0) keep &= ~(1u << c);
     if (keep != 0xffffffffu) b.w.flags[s] &= keep;
 }
 
@@ -102,11 +102,11 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
             if (op.kind != GW_OP_LEAVE && op.sync_flags) {
                 uint32_t bits = 0;
                 for (int c = 0; c < 2; ++c)
-                    if (((op.sync_flags >> c) & 1) && (int32_t)i > b.clr[2 * s + c]) bits |= 1u << c;
+                    if (((op.sync_flags >> c) & 1) && (int32_t)i > b.ol[s].clr[c]) bits |= 1u << c;
                 if (bits) atomicOr(&b.w.flags[s], bits);
             }
-            if (b.last_pos[s] == (int32_t)i) b.w.pos[s] = make_float4(op.x, op.y, op.z, op.yaw);
-            if (b.last_aoi[s] == (int32_t)i) {
+            if (b.ol[s].pos == (int32_t)i) b.w.pos[s] = make_float4(op.x, op.y, op.z, op.yaw);
+            if (b.ol[s].aoi == (int32_t)i) {
                 AoiEnt a = b.w.aoi[s];
                 PrevEnt p;
                 const bool was = (a.meta & PRESENT_BIT) != 0;
@@ -229,7 +229,7 @@ __device__ __forceinline__ MoverCells mover_cells(const World& w, uint32_t A) {
 __device__ __forceinline__ bool op_mover(const TickBufs& b, uint32_t i, uint32_t& s) {
     const gw_op op = b.ops[i];
     s = op.slot;
-    return s < b.w.cap && op.kind >= GW_OP_ENTER && op.kind <= GW_OP_LEAVE && b.last_aoi[s] == (int32_t)i;
+    return s < b.w.cap && op.kind >= GW_OP_ENTER && op.kind <= GW_OP_LEAVE && b.ol[s].aoi == (int32_t)i;
 }
 
 // per mover: mover-grid histogram; a mover staying in its cell is patched in
@@ -1681,10 +1681,10 @@ __global__ void __launch_bounds__(NT) k_tick_reset(TickBufs b) {
     if (i < b.m) {
         const uint32_t s = b.ops[i].slot;
         if (s < b.w.cap) {
-            b.last_pos[s] = -1;
-            b.last_aoi[s] = -1;
-            b.last_leave[s] = -1;
-            b.clr[2 * s] = b.clr[2 * s + 1] = -1;
+            OpLast z;
+            z.pos = z.aoi = z.leave = z.pad0 = -1;
+            z.clr[0] = z.clr[1] = z.pad1[0] = z.pad1[1] = -1;
+            b.ol[s] = z;
         }
     }
     if (i < b.st->n_gm) {

@@ -205,10 +205,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->gmi, 0, (size_t)nc))) return rc;
     if ((rc = grow_preserve(c, c->eid_dev, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->cid_dev, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->last_pos, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->last_aoi, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->last_leave, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->clr, 2 * (size_t)oc, 2 * (size_t)nc))) return rc;
+    if ((rc = grow_preserve(c, c->ol, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->rflag, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->gnb[0], 0, nc))) return rc;    // rebuilt (grid_dirty)
     if ((rc = grow_preserve(c, c->gnb[1], 0, nc))) return rc;
@@ -225,10 +222,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     HIPCHK(hipMemsetAsync(c->movbit, 0, ((size_t)nc / 32 + 1) * 4, c->st));
     HIPCHK(hipMemsetAsync(c->eid_dev + oc, 0, n * 16, c->st));
     HIPCHK(hipMemsetAsync(c->cid_dev + oc, 0, n * 16, c->st));
-    launch_fill_i32(c->last_pos + oc, -1, n, c->st);
-    launch_fill_i32(c->last_aoi + oc, -1, n, c->st);
-    launch_fill_i32(c->last_leave + oc, -1, n, c->st);
-    launch_fill_i32(c->clr + 2 * (size_t)oc, -1, 2 * n, c->st);
+    launch_fill_i32((int32_t*)(c->ol + oc), -1, n * (sizeof(OpLast) / 4), c->st);
     HIPCHK(hipStreamSynchronize(c->st));
     c->slot_cap = nc;
     c->present_h.resize(nc, 0);
@@ -468,8 +462,8 @@ void gw_shutdown(gw_ctx* c) {
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off, &c->m_create.h,
                     &c->m_destroy.h, &c->m_fanout.h};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
-    void* ps[] = {c->halo, c->rflag, c->sc.ticket, c->movbit, c->gmi, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->nbc, c->last_pos, c->last_aoi,
-                  c->last_leave, c->clr, c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->cstats, c->scal32, c->gsb[0],
+    void* ps[] = {c->halo, c->rflag, c->sc.ticket, c->movbit, c->gmi, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->nbc, c->ol,
+                  c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->cstats, c->scal32, c->gsb[0],
                   c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->bigcell, c->gm_start};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
@@ -642,8 +636,8 @@ int gw_route_halo(gw_ctx* c, const gw_op* dev_ops, const uint64_t* dev_stamps, u
     }
     if (!c->total_slots) return set_err(c, GW_EINVAL, "no space");
     // n == 0 still runs: the buffers must become all NOPs
-    launch_route_halo(world(c), dev_ops, (const unsigned long long*)dev_stamps, n, max_step, D, c->last_pos,
-                      c->last_aoi, c->last_leave, c->clr, c->rflag, c->halo, c->st);
+    launch_route_halo(world(c), dev_ops, (const unsigned long long*)dev_stamps, n, max_step, D, c->ol, c->rflag,
+                      c->halo, c->st);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -981,8 +975,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.ops = ops; b.m = M; b.stamp_base = c->stamp_base;
     b.stamps = stamps;
     b.diff_u = c->diff_u;
-    b.last_pos = c->last_pos; b.last_aoi = c->last_aoi; b.last_leave = c->last_leave;
-    b.clr = c->clr;
+    b.ol = c->ol;
     b.st = st;
     b.gn_nxt = c->gnb[c->gcur ^ 1]; b.start_nxt = c->gsb[c->gcur ^ 1];
     b.dep = c->dep; b.arr = c->arr; b.cnt_new = c->cnt_new; b.bigcell = c->bigcell;

@@ -119,8 +119,7 @@ struct gw_ctx {
     unsigned long long* nbc = nullptr;       // [slot_cap] epoch<<32 | neighbours with a client
     uint32_t* movbit = nullptr;              // [slot_cap/32 + 1] movers of the tick, zero between ticks
     uint32_t* gmi = nullptr;                 // [slot_cap] primary mover-grid entry of a mover
-    int32_t *last_pos = nullptr, *last_aoi = nullptr, *last_leave = nullptr;
-    int32_t* clr = nullptr;                   // [2 slot_cap] last Leave clearing each sync bit, -1 between ticks
+    gw::OpLast* ol = nullptr;                // [slot_cap] per-op dedupe state, -1 between ticks
     uint32_t* rflag = nullptr;                // [slot_cap] halo routing scratch, zero between calls
     HaloStats* halo = nullptr;                // halo routing counters (device)
     GEnt* gnb[2] = {nullptr, nullptr};   // grid ping-pong (gnb[gcur] is current)

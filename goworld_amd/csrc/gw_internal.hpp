@@ -35,6 +35,16 @@ struct alignas(16) PrevEnt {
     unsigned long long ostamp;
 };
 
+// Per-slot op dedupe state of one tick, one 32-B record (a tick's op touches
+// one line for all of it): the index of the slot's last op that sets the sync
+// payload (non-Leave), its last AOI op, its last Leave, and per sync bit the
+// last Leave that cleared it; -1 between ticks.
+struct alignas(32) OpLast {
+    int32_t pos, aoi, leave, pad0;
+    int32_t clr[2];
+    int32_t pad1[2];
+};
+
 // Entry of the grid (cell-sorted, slot order inside a cell), 16 B.
 struct alignas(16) GEnt {
     float x, z;
@@ -158,8 +168,7 @@ struct TickBufs {
     const unsigned long long* stamps;   // explicit global stamps (nullptr: stamp_base + index)
     uint32_t m;               // ops in the stream
     unsigned long long stamp_base;
-    int32_t *last_pos, *last_aoi, *last_leave;
-    int32_t* clr;             // [2 cap] per slot and sync bit: the last Leave clearing it (-1 between ticks)
+    OpLast* ol;               // [cap] per-slot op dedupe state of the tick (-1 between ticks)
     DevStats* st;
     // incremental grid: gn -> gn_nxt
     GEnt* gn_nxt;             // [cap]
@@ -288,8 +297,7 @@ struct HaloDsts {
     uint32_t n;
 };
 void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
-                       float max_step, const HaloDsts& D, int32_t* last_pos, int32_t* last_aoi,
-                       int32_t* last_leave, int32_t* clr, uint32_t* rflag, HaloStats* hs, hipStream_t s,
+                       float max_step, const HaloDsts& D, OpLast* ol, uint32_t* rflag, HaloStats* hs, hipStream_t s,
                        bool pad = true);
 void launch_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n, hipStream_t s);
 void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,

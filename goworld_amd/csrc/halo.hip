@@ -29,8 +29,7 @@ __device__ __forceinline__ bool op_valid(const gw_op& op, uint32_t cap) {
 }
 
 __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
-                                                int32_t* last_pos, int32_t* last_aoi, int32_t* last_leave,
-                                                int32_t* clr, HaloStats* hs) {
+                                                OpLast* ol, HaloStats* hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i == 0) hs->cnt[0] = hs->cnt[1] = 0;         // placement counters of this call
     if (i >= n) return;
@@ -40,24 +39,24 @@ __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, ui
         atomicAdd(&hs->bad_ops, 1ull);
         return;
     }
-    if (op.kind != GW_OP_LEAVE) atomicMax(&last_pos[op.slot], (int32_t)i);
-    if (op.kind != GW_OP_SYNC) atomicMax(&last_aoi[op.slot], (int32_t)i);
+    if (op.kind != GW_OP_LEAVE) atomicMax(&ol[op.slot].pos, (int32_t)i);
+    if (op.kind != GW_OP_SYNC) atomicMax(&ol[op.slot].aoi, (int32_t)i);
     if (op.kind == GW_OP_LEAVE) {
-        atomicMax(&last_leave[op.slot], (int32_t)i);
+        atomicMax(&ol[op.slot].leave, (int32_t)i);
         for (int c = 0; c < 2; ++c)
-            if (!((op.sync_flags >> c) & 1)) atomicMax(&clr[2 * op.slot + c], (int32_t)i);
+            if (!((op.sync_flags >> c) & 1)) atomicMax(&ol[op.slot].clr[c], (int32_t)i);
     }
 }
 
 __global__ void __launch_bounds__(NT) k_route2(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
-                                                const int32_t* __restrict__ clr, uint32_t* rflag) {
+                                                const OpLast* __restrict__ ol, uint32_t* rflag) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
     const gw_op op = ops[i];
     if (!op_valid(op, cap) || op.kind == GW_OP_LEAVE || !(op.sync_flags & SIF_ROUTED)) return;
     uint32_t bits = 0;
     for (int c = 0; c < 2; ++c)
-        if (((op.sync_flags >> c) & 1) && (int32_t)i > clr[2 * op.slot + c]) bits |= 1u << c;
+        if (((op.sync_flags >> c) & 1) && (int32_t)i > ol[op.slot].clr[c]) bits |= 1u << c;
     if (bits) atomicOr(&rflag[op.slot], bits);
 }
 
@@ -81,10 +80,7 @@ __device__ __forceinline__ void put_row(gw_halo_row* r, const gw_op& o, unsigned
 }
 
 __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, const unsigned long long* __restrict__ stamps,
-                                                uint32_t n, World w, const int32_t* __restrict__ last_pos,
-                                                const int32_t* __restrict__ last_aoi,
-                                                const int32_t* __restrict__ last_leave,
-                                                const int32_t* __restrict__ clr,
+                                                uint32_t n, World w, const OpLast* __restrict__ ol,
                                                 const uint32_t* __restrict__ rflag, float max_step, HaloDsts D,
                                                 HaloStats* hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
@@ -96,9 +92,9 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
         const gw_op op = ops[i];
         if (op_valid(op, w.cap)) {
             s = op.slot;
-            la = last_aoi[s];
-            ll = last_leave[s];
-            lp = last_pos[s];
+            la = ol[s].aoi;
+            ll = ol[s].leave;
+            lp = ol[s].pos;
             rep = (int32_t)i == max(lp, ll);          // the entity's last op
         }
     }
@@ -123,7 +119,7 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
         // did not clear, OR'd with the bits set since the Leave that cleared them
         uint32_t keep = 0;
         for (int c = 0; c < 2; ++c)
-            if (clr[2 * s + c] < 0) keep |= 1u << c;
+            if (ol[s].clr[c] < 0) keep |= 1u << c;
         f = ((w.flags[s] & keep) | rflag[s]) & SIF_ROUTED;
     }
     for (uint32_t d = 0; d < D.n; ++d) {
@@ -162,8 +158,7 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
 }
 
 __global__ void __launch_bounds__(NT) k_route4(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
-                                                int32_t* last_pos, int32_t* last_aoi, int32_t* last_leave,
-                                                int32_t* clr, uint32_t* rflag, HaloDsts D,
+                                                OpLast* ol, uint32_t* rflag, HaloDsts D,
                                                 const HaloStats* __restrict__ hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     // rows past the placed entities become NOPs (thread i: row i of each buffer)
@@ -174,10 +169,10 @@ __global__ void __launch_bounds__(NT) k_route4(const gw_op* __restrict__ ops, ui
     if (i >= n) return;
     const gw_op op = ops[i];
     if (!op_valid(op, cap)) return;
-    last_pos[op.slot] = -1;
-    last_aoi[op.slot] = -1;
-    last_leave[op.slot] = -1;
-    clr[2 * op.slot] = clr[2 * op.slot + 1] = -1;
+    OpLast z;
+    z.pos = z.aoi = z.leave = z.pad0 = -1;
+    z.clr[0] = z.clr[1] = z.pad1[0] = z.pad1[1] = -1;
+    ol[op.slot] = z;
     rflag[op.slot] = 0;
 }
 
@@ -192,19 +187,17 @@ __global__ void __launch_bounds__(NT) k_split_rows(const gw_halo_row* __restrict
 }  // namespace
 
 void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
-                       float max_step, const HaloDsts& D, int32_t* last_pos, int32_t* last_aoi,
-                       int32_t* last_leave, int32_t* clr, uint32_t* rflag, HaloStats* hs, hipStream_t s,
+                       float max_step, const HaloDsts& D, OpLast* ol, uint32_t* rflag, HaloStats* hs, hipStream_t s,
                        bool pad) {
     const uint32_t nb = nblk1(n, NT);
     uint64_t rows = 0;                                   // NOP padding up to the capacity (fixed-size exchanges)
     if (pad)
         for (uint32_t d = 0; d < D.n; ++d) rows = std::max<uint64_t>(rows, (uint64_t)D.d[d].cap * ROWS);
-    hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, last_pos, last_aoi, last_leave, clr, hs);
-    hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, clr, rflag);
-    hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, last_pos, last_aoi, last_leave,
-                       clr, rflag, max_step, D, hs);
+    hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, hs);
+    hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, rflag);
+    hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, ol, rflag, max_step, D, hs);
     hipLaunchKernelGGL(k_route4, dim3(nblk1(std::max<uint64_t>(n, rows), NT)), dim3(NT), 0, s, ops, n, w.cap,
-                       last_pos, last_aoi, last_leave, clr, rflag, D, hs);
+                       ol, rflag, D, hs);
 }
 
 __global__ void __launch_bounds__(NT) k_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n) {

@@ -167,8 +167,8 @@ int gw_world_route(gw_ctx* c, const gw_op* ops, uint32_t n, const gw_halo_row* s
     }
     const unsigned long long base = 1 + (W.tick * W.g.ranks + W.g.rank) * STAMP_STRIDE;
     launch_iota_u64(P<unsigned long long>(W.stamps), base, n, c->st);
-    launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->last_pos,
-                      c->last_aoi, c->last_leave, c->clr, c->rflag, c->halo, c->st, /*pad=*/false);
+    launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->ol, c->rflag,
+                      c->halo, c->st, /*pad=*/false);
     HIPCHK(hipGetLastError());
     HaloStats hs{};
     HIPCHK(hipMemcpyAsync(&hs, c->halo, sizeof hs, hipMemcpyDeviceToHost, c->st));
@@ -227,8 +227,8 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
     const unsigned long long base = 1 + (W.tick * W.g.ranks + W.g.rank) * STAMP_STRIDE;
     launch_iota_u64(P<unsigned long long>(W.stamps), base, n, c->st);
     if (D.n)                                          // a one-strip world has nobody to route to
-        launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->last_pos,
-                          c->last_aoi, c->last_leave, c->clr, c->rflag, c->halo, c->st, /*pad=*/false);
+        launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->ol,
+                          c->rflag, c->halo, c->st, /*pad=*/false);
     HIPCHK(hipGetLastError());
     uint32_t rcnt[2] = {0, 0};
     if (any_nb) {

@@ -1,0 +1,169 @@
+"""GPU: the host boundary rows through the C ABI.
+
+a13 — gw_submit_client_sync decodes MT_SYNC_POSITION_YAW_FROM_CLIENT payloads
+(GameService.go:395-407): a record of an unknown entity id is dropped
+(EntityManager.go:450-455), one of an entity that does not sync from its client
+is ignored (Entity.go:430-435), one of an entity not in an AOI space of the
+context is left to the caller, every other one becomes a Moved op with sync
+flags NEIGHBOR (setPositionYaw(fromClient=true), Entity.go:1189-1205) at its
+place in the call order.  Checked by running the equivalent op stream through
+the oracle: events and records identical.
+
+a14 — gw_sync_encode_wire writes the game->gate packets (Entity.go:1210-1266):
+one packet per gate with records, u16 1502 + u16 gate, then 48-B records of
+clientid(watcher) eid(entity) x y z yaw; compared with the oracle's own
+encoding of the same collect after putting each entity's neighbour records in
+the canonical order (the only order freedom: Go map iteration)."""
+import struct
+
+import numpy as np
+import pytest
+
+import golden_data as G
+from goworld_amd import gpuaoi
+from goworld_amd import traces as T
+from oracle import pyorc
+
+pytestmark = pytest.mark.gpu
+
+
+def _ids(n, tag=0):
+    return b"".join(pyorc.fixed_uuid(i | tag) for i in range(n))
+
+
+def _canon(recs, gates):
+    return G.canonical_records(recs, gates)
+
+
+def _setup(tr):
+    g = gpuaoi.GpuAOI(0)
+    sid, base = gpuaoi.load_space(g, tr)
+    slots = np.arange(tr.capacity, dtype=np.uint32) + base
+    g.set_entity_ids(slots, _ids(tr.capacity))
+    g.set_client_ids(slots, _ids(tr.capacity, 0x80000000))
+    o = pyorc.OracleSpace(tr.capacity, tr.d, pyorc.SEQRULE)
+    pyorc.load_trace(o, tr)
+    g.sync_collect()
+    o.collect()
+    return g, o, base
+
+
+def test_client_sync_decode_matches_op_stream():
+    tr = T.dyadic_walk_trace(41, 1500, 1024.0, 100.0, 3, move_frac=0.3, hot_frac=0.3, n_hot=3, gate_count=2,
+                             client_frac=0.8)
+    g, o, base = _setup(tr)
+    rng = np.random.default_rng(5)
+    syncing = rng.random(tr.capacity) < 0.75
+    g.set_client_syncing(np.arange(tr.capacity, dtype=np.uint32) + base, syncing.astype(np.uint8))
+    try:
+        for t, ops in enumerate(tr.ticks):
+            # every op of the tick as a client record (some twice), plus records
+            # of unknown ids; the oracle gets the ops the decode must produce
+            recs, expect = [], []
+            for op in ops:
+                s = int(op["slot"])
+                for rep in range(1 + (s % 7 == 0)):
+                    x, z = float(op["x"]) + rep * 0.5, float(op["z"])
+                    recs.append(pyorc.fixed_uuid(s) + struct.pack("<4f", x, 0.0, z, float(op["yaw"])))
+                    if syncing[s]:
+                        e = np.zeros(1, T.OP_DTYPE)
+                        e["kind"] = T.OP_MOVED
+                        e["sync_flags"] = 2
+                        e["slot"] = s
+                        e["x"], e["y"], e["z"], e["yaw"] = x, 0.0, z, op["yaw"]
+                        expect.append(e)
+                if s % 11 == 0:                               # an id nobody registered
+                    recs.append(pyorc.fixed_uuid(0x40000000 | s) + struct.pack("<4f", 1, 2, 3, 4))
+            applied, left = g.submit_client_sync(b"".join(recs))
+            assert left == 0
+            assert applied == len(expect)
+            r = g.tick()
+            exp_ops = np.concatenate(expect) if expect else T.make_ops(0)
+            assert o.tick(exp_ops) == 0
+            ee, ll = o.events()
+            assert r.enter.tobytes() == ee.tobytes() and r.leave.tobytes() == ll.tobytes(), f"tick {t} events"
+            got = g.sync_collect().records
+            exp = o.collect()
+            got_c = _canon(got.copy(), tr.gates)
+            got_c["watcher"] -= base
+            got_c["entity"] -= base
+            assert got_c.tobytes() == exp.tobytes(), f"tick {t} records"
+    finally:
+        g.close()
+        o.close()
+
+
+def test_client_sync_outside_space_and_cleared_ids():
+    tr = T.config1(ticks=1, n=200)
+    g, o, base = _setup(tr)
+    try:
+        s_left, s_gone = 5, 7
+        g.set_client_syncing(np.arange(tr.capacity, dtype=np.uint32) + base, np.ones(tr.capacity, np.uint8))
+        lv = T.make_ops(1)
+        lv["kind"] = T.OP_LEAVE
+        lv["slot"] = s_left + base
+        lv["sync_flags"] = 3
+        g.submit(lv)
+        g.tick()
+        g.clear_entity_ids(np.array([s_gone + base], np.uint32))
+        pay = (pyorc.fixed_uuid(s_left) + struct.pack("<4f", 1, 0, 1, 0) +
+               pyorc.fixed_uuid(s_gone) + struct.pack("<4f", 1, 0, 1, 0) +
+               pyorc.fixed_uuid(9) + struct.pack("<4f", float(tr.init_x[9]) + 1, 0, float(tr.init_z[9]), 0))
+        applied, left = g.submit_client_sync(pay)
+        assert (applied, left) == (1, 1)     # 9 applied; 5 is in no AOI space here; 7's id is gone
+    finally:
+        g.close()
+        o.close()
+
+
+def test_wire_encode_matches_oracle_bytes():
+    tr = T.dyadic_walk_trace(43, 1200, 1024.0, 100.0, 2, move_frac=0.4, gate_count=3, client_frac=0.7)
+    g, o, base = _setup(tr)
+    assert base == 0
+    try:
+        for t, ops in enumerate(tr.ticks):
+            g.submit(ops)
+            g.tick()
+            assert o.tick(ops) == 0
+            o.events()
+            recs = g.sync_collect().records
+            exp = o.collect()
+            data, pk, nb, _ = g.encode_wire()
+            assert nb == len(data) == sum(4 + 48 * n for n in np.bincount(tr.gates[recs["watcher"]])[1:] if n)
+            gates_out = [p[0] for p in pk]
+            assert gates_out == sorted(set(int(x) for x in tr.gates[recs["watcher"]]))
+            # per packet: header, then the records of the collect in order, as bytes
+            ent = {pyorc.fixed_uuid(i): i for i in range(tr.capacity)}
+            cli = {pyorc.fixed_uuid(i | 0x80000000): i for i in range(tr.capacity)}
+            got = []
+            for gate, off, ln in pk:
+                assert struct.unpack_from("<HH", data, off) == (1502, gate)
+                for q in range(off + 4, off + ln, 48):
+                    w, e = cli[data[q:q + 16]], ent[data[q + 16:q + 32]]
+                    got.append((w, e) + struct.unpack_from("<4f", data, q + 32))
+            arr = np.zeros(len(got), G.REC_DTYPE)
+            for i, k in enumerate(["watcher", "entity", "x", "y", "z", "yaw"]):
+                arr[k] = [r[i] for r in got]
+            assert arr.tobytes() == recs.tobytes()            # the wire carries the collect's records in order
+            assert _canon(arr, tr.gates).tobytes() == exp.tobytes()
+            # the oracle's wire bytes are the canonical records encoded the same way
+            assert G.sha(o.wire()) == G.sha(_encode(exp, tr.gates))
+    finally:
+        g.close()
+        o.close()
+
+
+def _encode(recs, gates):
+    out = bytearray()
+    i = 0
+    while i < len(recs):
+        gt = int(gates[recs["watcher"][i]])
+        j = i
+        while j < len(recs) and gates[recs["watcher"][j]] == gt:
+            j += 1
+        out += struct.pack("<HH", 1502, gt)
+        for r in recs[i:j]:
+            out += pyorc.fixed_uuid(int(r["watcher"]) | 0x80000000) + pyorc.fixed_uuid(int(r["entity"]))
+            out += struct.pack("<4f", r["x"], r["y"], r["z"], r["yaw"])
+        i = j
+    return bytes(out)

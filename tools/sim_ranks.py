@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Per-rank cost of a decomposed world at R ranks, measured on ONE GPU.
+
+The driver runs the real N-GPU bench (one process per GPU, halo rows over RCCL
+inside the library).  This tool rehearses it on a single MI355X: R world
+contexts (gw_world_create, one X-strip each) live in one process on the same
+device, the halo rows move between them by pointer (rank r+1's send buffer is
+rank r's receive buffer: gw_world_route -> gw_world_submit, no copy), and every
+rank's step is run ALONE on the GPU and timed with a device sync on both
+sides:
+
+    step_r = gw_world_route (4 routing kernels + its host sync)
+           + gw_tick + gw_sync_collect (one host sync)
+
+so step_r is what rank r costs on its own GPU, minus the RCCL transfer (two
+grouped send/recv rounds with <= 2 peers; its bytes are reported).  The
+projected N-GPU step is max_r step_r + the exchange; projected throughput =
+all ranks' updates / that.  The same world at R = 1 gives the baseline of the
+projected speedup.  Workloads: config #5 (16M uniform world, L = 131072) and
+the metric's 1M clustered space (config #3 as one world).
+
+usage: python tools/sim_ranks.py [--which c5|c3] [--ranks 1,2,4,8] [--steps 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from goworld_amd import dworld, gpuaoi, traces  # noqa: E402
+
+
+def world_ticks(which, ticks, n):
+    """(n, side, max_step, x0, z0, yaw0, [(ops, x_before)] per tick)."""
+    if which == "c5":
+        side, max_step = 131072.0, 4.0
+        walk = traces.WorldWalk(seed=5, n=n, side=side)
+        x0, z0, yaw0 = walk.x(), walk.z(), walk.yaw.copy()
+        tk = [walk.next_tick() for _ in range(ticks)]
+    else:
+        side, max_step = 32768.0, 16.0
+        tr = traces.config3(ticks=ticks, seed=3, n=n, side=side)
+        x0, z0, yaw0 = tr.init_x, tr.init_z, tr.init_yaw
+        xcur = tr.init_x.copy()
+        tk = []
+        for ops in tr.ticks:
+            xb = xcur[ops["slot"]].copy()
+            xcur[ops["slot"]] = ops["x"]
+            tk.append((ops, xb))
+    return side, max_step, x0, z0, yaw0, tk
+
+
+class SimWorld:
+    def __init__(self, R, n, side, max_step, x0, z0, yaw0, tk, device=0):
+        self.R = R
+        self.geom = geom = dworld.Strips(-side / 2, side / R, R, 100.0, max_step)
+        self.g = []
+        for r in range(R):
+            g = gpuaoi.GpuAOI(device)
+            lo, hi = geom.ext(r)
+            bounds = (max(lo, -side / 2), -side / 2, min(hi, side / 2), side / 2)
+            g.world_create(geom.x0, geom.w, geom.d, geom.max_step, R, r, n, bounds)
+            g.set_clients(np.arange(n, dtype=np.uint32), np.ones(n, np.uint16))
+            self.g.append(g)
+        self.bufs = []
+        owner0 = geom.owner(x0)
+        chunk = 1 << 21
+        n_chunks = max(1, -(-int(np.bincount(owner0, minlength=R).max()) // chunk))
+        enters = []
+        for r in range(R):
+            mine = np.nonzero(owner0 == r)[0].astype(np.uint32)
+            enters.append(traces.enter_ops(mine, x0[mine], np.zeros(len(mine), np.float32), z0[mine], yaw0[mine]))
+        for k in range(n_chunks):                 # load: owned Enters, routed to the neighbours as ghosts
+            parts = [e[k * chunk:(k + 1) * chunk] for e in enters]
+            self._route_submit([self._upload(r, p) for r, p in enumerate(parts)], [len(p) for p in parts])
+            for g in self.g:
+                g.tick(copy=False, no_events=True)
+        for g in self.g:
+            g.sync_collect(copy=False)
+        self.ticks = []                           # per tick: [(dev_ptr, m)] per rank, resident in HBM
+        for ops, xb in tk:
+            own = geom.owner(xb)
+            self.ticks.append([(self._upload(r, ops[own == r]), int((own == r).sum())) for r in range(R)])
+
+    def _upload(self, r, ops):
+        ops = np.ascontiguousarray(ops)
+        p = self.g[r].dev_alloc(max(ops.nbytes, 64))
+        if ops.nbytes:
+            self.g[r].h2d(p, ops)
+        self.bufs.append((r, p))
+        return p
+
+    def _route_submit(self, ptrs, ms, times=None):
+        if self.R == 1:                           # one strip: gw_world_step stamps and queues, no routing
+            t0 = time.perf_counter()
+            self.g[0].world_step(ptrs[0], ms[0])
+            if times is not None:
+                times[0] += time.perf_counter() - t0
+            return 0
+        sends = []
+        for r, g in enumerate(self.g):
+            g.synchronize()
+            t0 = time.perf_counter()
+            sends.append(g.world_route(ptrs[r], ms[r]))
+            if times is not None:
+                times[r] += time.perf_counter() - t0
+        rows = 0
+        for r, g in enumerate(self.g):
+            left = sends[r - 1][1] if r > 0 else (0, 0)           # left neighbour's rows to its right
+            right = sends[r + 1][0] if r + 1 < self.R else (0, 0)
+            rows += left[1] + right[1]
+            g.world_submit([left, right])
+        return rows
+
+    def step(self, t):
+        """One tick of every rank; returns (per-rank seconds, updates, events, records, halo rows)."""
+        times = [0.0] * self.R
+        ptrs = [p for p, _ in self.ticks[t]]
+        ms = [m for _, m in self.ticks[t]]
+        rows = self._route_submit(ptrs, ms, times)
+        upd = ev = rec = 0
+        for r, g in enumerate(self.g):
+            g.synchronize()
+            t0 = time.perf_counter()
+            g.tick(copy=False, defer=True)
+            s = g.sync_collect(copy=False)
+            times[r] += time.perf_counter() - t0
+            res = g.tick_result()
+            upd += ms[r]
+            ev += res.n_enter + res.n_leave
+            rec += s.n_rec
+        return times, upd, ev, rec, rows
+
+    def close(self):
+        for r, g in enumerate(self.g):
+            ov, bad, bad_ops = g.world_status()
+            if ov or bad or bad_ops:
+                raise RuntimeError(f"rank {r}: contract counters {ov} {bad} {bad_ops}")
+        for r, p in self.bufs:
+            self.g[r].dev_free(p)
+        for g in self.g:
+            g.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--which", choices=["c5", "c3"], default="c5")
+    ap.add_argument("--ranks", default="1,2,4,8")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--entities", type=int, default=None)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    n = a.entities or (16_000_000 if a.which == "c5" else 1_000_000)
+    ticks = a.warmup + a.steps
+    t0 = time.perf_counter()
+    side, max_step, x0, z0, yaw0, tk = world_ticks(a.which, ticks, n)
+    print(f"# {a.which}: {n} entities, {ticks} ticks generated in {time.perf_counter() - t0:.1f}s", flush=True)
+    out = []
+    base = None
+    for R in [int(v) for v in a.ranks.split(",")]:
+        t0 = time.perf_counter()
+        w = SimWorld(R, n, side, max_step, x0, z0, yaw0, tk)
+        load = time.perf_counter() - t0
+        for t in range(a.warmup):
+            w.step(t)
+        per = np.zeros(R)
+        upd = ev = rec = rows = 0
+        for t in range(a.warmup, ticks):
+            ts, u, e, rc, rw = w.step(t)
+            per += np.array(ts)
+            upd += u; ev += e; rec += rc; rows += rw
+        w.close()
+        per_ms = per / a.steps * 1e3
+        step_ms = float(per_ms.max())
+        row_bytes = rows / a.steps * 32            # gw_halo_row = 32 B
+        line = {"which": a.which, "ranks": R, "entities": n, "steps": a.steps,
+                "rank_ms": [round(v, 4) for v in per_ms.tolist()], "max_rank_ms": step_ms,
+                "mean_rank_ms": float(per_ms.mean()),
+                "updates_per_step": upd / a.steps, "events_per_step": ev / a.steps,
+                "records_per_step": rec / a.steps, "halo_bytes_per_step_all_ranks": row_bytes,
+                "projected_updates_per_sec_excl_exchange": upd / a.steps / (step_ms * 1e-3),
+                "projected_events_per_sec_excl_exchange": ev / a.steps / (step_ms * 1e-3),
+                "load_s": round(load, 1)}
+        if base is None and R == 1:
+            base = line
+        if base is not None:
+            line["projected_speedup_vs_1_excl_exchange"] = base["max_rank_ms"] / step_ms
+        print(json.dumps(line), flush=True)
+        out.append(line)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

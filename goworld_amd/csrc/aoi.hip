@@ -88,27 +88,38 @@ __global__ void __launch_bounds__(NT) k_ops2(TickBufs b) {
     uint32_t keep = 0xffffffffu;
     for (int c = 0; c < 2; ++c)
         if (b.ol[s].clr[c] >= 0) keep &= ~(1u << c);
-    if (keep != 0xffffffffu) b.w.flags[s] &= keep;
+    if (keep != 0xffffffffu) atomicAnd(&b.w.flags[flag_word(s)], ~((~keep & 3u) << flag_sh(s)));
 }
 
+__device__ __forceinline__ void classify_mover(const TickBufs& b, uint32_t A, const AoiEnt& a, const PrevEnt& p);
+
+// Per op: the syncInfoFlag bits, the sync payload of the slot's last
+// non-Leave op; the slot's last AOI op saves the pre-tick position and stamp
+// (PrevEnt), takes its stamp, updates the AOI state and classifies the mover
+// for the incremental grid (state in registers: no second pass re-reading the
+// op, the dedupe record and the slot state)
 __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    bool mv = false;
+    uint32_t s = 0;
+    AoiEnt a;
+    PrevEnt p;
     if (i < b.m) {
         const gw_op op = b.ops[i];
-        const uint32_t s = op.slot;
+        s = op.slot;
         if (s < b.w.cap && op.kind >= GW_OP_ENTER && op.kind <= GW_OP_SYNC) {
+            const OpLast ol = b.ol[s];
             // syncInfoFlag |= bits of every call after the last Leave that
             // cleared them (Space.go:196, Entity.go:1199-1204, 1286)
             if (op.kind != GW_OP_LEAVE && op.sync_flags) {
                 uint32_t bits = 0;
                 for (int c = 0; c < 2; ++c)
-                    if (((op.sync_flags >> c) & 1) && (int32_t)i > b.ol[s].clr[c]) bits |= 1u << c;
-                if (bits) atomicOr(&b.w.flags[s], bits);
+                    if (((op.sync_flags >> c) & 1) && (int32_t)i > ol.clr[c]) bits |= 1u << c;
+                if (bits) atomicOr(&b.w.flags[flag_word(s)], bits << flag_sh(s));
             }
-            if (b.ol[s].pos == (int32_t)i) b.w.pos[s] = make_float4(op.x, op.y, op.z, op.yaw);
-            if (b.ol[s].aoi == (int32_t)i) {
-                AoiEnt a = b.w.aoi[s];
-                PrevEnt p;
+            if (ol.pos == (int32_t)i) b.w.pos[s] = make_float4(op.x, op.y, op.z, op.yaw);
+            if (ol.aoi == (int32_t)i) {                 // the slot's mover entry (never a SYNC op)
+                a = b.w.aoi[s];
                 const bool was = (a.meta & PRESENT_BIT) != 0;
                 p.ox = was ? a.x : qnan();
                 p.oz = was ? a.z : qnan();
@@ -118,9 +129,15 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
                 if (op.kind == GW_OP_LEAVE) a.meta &= ~PRESENT_BIT;
                 else { a.x = op.x; a.z = op.z; a.meta |= PRESENT_BIT; }
                 b.w.aoi[s] = a;
+                mv = true;
             }
         }
     }
+    // mover count: one add per wave into a private-ish shard (a per-block add
+    // to one counter serialised ~4k atomics at 1M ops: ~100 us at config #4)
+    const uint32_t nw = (uint32_t)popc64(wave_ballot(mv));
+    if (lane_id() == 0 && nw) shard_add(b.st, blockIdx.x * NWAVE + (threadIdx.x >> 6), SH_MOVERS, nw);
+    if (mv) classify_mover(b, s, a, p);
 }
 
 // Restore path (Space.go:209-214, EntityManager.go:556-617): entity i enters
@@ -140,7 +157,7 @@ __global__ void __launch_bounds__(NT) k_restore(World w, const uint32_t* __restr
     w.aoi[s] = a;
     w.pos[s] = p;
     w.stamp[s] = stamp_base + i;
-    w.flags[s] |= flags;
+    if (flags & 3u) atomicOr(&w.flags[flag_word(s)], (flags & 3u) << flag_sh(s));
 }
 void launch_restore(const World& w, const uint32_t* slots, const float4* xyzw, uint32_t n,
                     unsigned long long stamp_base, uint32_t flags, hipStream_t s) {
@@ -177,8 +194,15 @@ __global__ void __launch_bounds__(NT) k_grid_fill(World w, const uint32_t* __res
         e.x = a.x; e.z = a.z; e.slot = s;
         e.meta = key | (w.gate[s] ? CLIENT_BIT : 0u);
         w.gn[i] = e;
-        w.gidx[s] = i;
     }
+}
+// gidx = offset of the slot's entry inside its cell (stays valid while the
+// cell shifts as a block; rewritten only where the cell is re-merged)
+__global__ void __launch_bounds__(NT) k_grid_rel(World w) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i >= w.gn_start[w.ncells]) return;
+    const GEnt e = w.gn[i];
+    w.gidx[e.slot] = i - w.gn_start[e.meta & CELL_MASK];
 }
 // gn_start[c] = first index with key >= c (binary search over the sorted keys)
 __global__ void __launch_bounds__(NT) k_grid_starts(World w, const uint32_t* __restrict__ keys, DevStats* st) {
@@ -202,6 +226,7 @@ void grid_rebuild(const World& w, DevStats* st, uint32_t* k0, uint32_t* v0, uint
     const uint32_t* slots = r ? v1 : v0;
     hipLaunchKernelGGL(k_grid_fill, dim3(nblk1(C, NT)), dim3(NT), 0, s, w, keys, slots);
     hipLaunchKernelGGL(k_grid_starts, dim3(nblk1((uint64_t)w.ncells + 1, NT)), dim3(NT), 0, s, w, keys, st);
+    hipLaunchKernelGGL(k_grid_rel, dim3(nblk1(C, NT)), dim3(NT), 0, s, w);
 }
 
 // ---------------------------------------------------------------------------
@@ -233,31 +258,26 @@ __device__ __forceinline__ bool op_mover(const TickBufs& b, uint32_t i, uint32_t
 }
 
 // per mover: mover-grid histogram; a mover staying in its cell is patched in
-// place, the others count as a departure / an arrival of their cells
-__global__ void __launch_bounds__(NT) k_classify(TickBufs b) {
-    const uint32_t i = blockIdx.x * NT + threadIdx.x;
-    uint32_t A = 0;
-    const bool mv = i < b.m && op_mover(b, i, A);
-    // mover count: one add per wave into a private-ish shard (a per-block add
-    // to one counter serialised ~4k atomics at 1M ops: ~100 us at config #4)
-    const uint32_t nw = (uint32_t)popc64(wave_ballot(mv));
-    if (lane_id() == 0 && nw) shard_add(b.st, blockIdx.x * NWAVE + (threadIdx.x >> 6), SH_MOVERS, nw);
-    if (mv) {
-        const MoverCells mc = mover_cells(b.w, A);
-        if (mc.co != NO_CELL) atomicAdd(&b.gm_cnt[mc.co], 1u);
-        if (mc.cn != NO_CELL && mc.cn != mc.co) atomicAdd(&b.gm_cnt[mc.cn], 1u);
-        if (mc.co != NO_CELL && mc.co == mc.cn) {
-            GEnt e;
-            e.x = mc.a.x; e.z = mc.a.z; e.slot = mc.A;
-            e.meta = mc.cn | (b.w.gate[mc.A] ? CLIENT_BIT : 0u) | MOVER_BIT;
-            b.w.gn[b.w.gidx[mc.A]] = e;
-        } else {
-            if (mc.co != NO_CELL) {
-                atomicAdd(&b.dep[mc.co], 1u);
-                b.w.gn[b.w.gidx[mc.A]].slot = DEPARTED;
-            }
-            if (mc.cn != NO_CELL) atomicAdd(&b.arr[mc.cn], 1u);
+// place, the others count as a departure / an arrival of their cells (called
+// by k_ops3 with the slot's state after the tick and before it)
+__device__ __forceinline__ void classify_mover(const TickBufs& b, uint32_t A, const AoiEnt& a, const PrevEnt& p) {
+    const SpaceP P = b.w.sp[a.meta & SPACE_MASK];
+    uint32_t co = NO_CELL, cn = NO_CELL;
+    if (p.ox == p.ox) co = cell_of(P, p.ox, p.oz);
+    if (a.meta & PRESENT_BIT) cn = cell_of(P, a.x, a.z);
+    if (co != NO_CELL) atomicAdd(&b.gm_cnt[co], 1u);
+    if (cn != NO_CELL && cn != co) atomicAdd(&b.gm_cnt[cn], 1u);
+    if (co != NO_CELL && co == cn) {
+        GEnt e;
+        e.x = a.x; e.z = a.z; e.slot = A;
+        e.meta = cn | (b.w.gate[A] ? CLIENT_BIT : 0u) | MOVER_BIT;
+        b.w.gn[b.w.gn_start[co] + b.w.gidx[A]] = e;
+    } else {
+        if (co != NO_CELL) {
+            atomicAdd(&b.dep[co], 1u);
+            b.w.gn[b.w.gn_start[co] + b.w.gidx[A]].slot = DEPARTED;
         }
+        if (cn != NO_CELL) atomicAdd(&b.arr[cn], 1u);
     }
 }
 
@@ -307,16 +327,17 @@ __global__ void __launch_bounds__(NT) k_place(TickBufs b) {
 }
 
 // clean cells move as a block: new index = start_nxt + offset in the cell
+// (grid-stride over the present entries: the grid is sized by the slot
+// capacity, a world strip holds a fraction of it)
 __global__ void __launch_bounds__(NT) k_grid_copy(TickBufs b) {
-    const uint32_t i = blockIdx.x * NT + threadIdx.x;
-    if (i >= b.w.gn_start[b.w.ncells]) return;
-    const GEnt e = b.w.gn[i];
-    if (e.slot == DEPARTED) return;
-    const uint32_t c = e.meta & CELL_MASK;
-    if (b.dep[c] & CELL_DIRTY) return;
-    const uint32_t at = b.start_nxt[c] + (i - b.w.gn_start[c]);
-    b.gn_nxt[at] = e;
-    b.w.gidx[e.slot] = at;
+    const uint32_t n = b.w.gn_start[b.w.ncells];
+    for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < n; i += gridDim.x * NT) {
+        const GEnt e = b.w.gn[i];
+        if (e.slot == DEPARTED) continue;
+        const uint32_t c = e.meta & CELL_MASK;
+        if (b.dep[c] & CELL_DIRTY) continue;
+        b.gn_nxt[b.start_nxt[c] + (i - b.w.gn_start[c])] = e;   // gidx (offset in the cell) unchanged
+    }
 }
 
 // Dirty cells: the kept entries (already in slot order) merge with the
@@ -371,13 +392,13 @@ __global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) {
             if (keep) {
                 const uint32_t at = sn + k0 + (uint32_t)popc64(bm & lt) + below;
                 b.gn_nxt[at] = e;
-                b.w.gidx[e.slot] = at;
+                b.w.gidx[e.slot] = at - sn;
             }
             k0 += (uint32_t)popc64(bm);
         }
         if (ln < (int)narr) {
             b.gn_nxt[sn + arank] = ar;
-            b.w.gidx[ar.slot] = sn + arank;
+            b.w.gidx[ar.slot] = arank;
         }
         if (ln == 0) b.dep[c] = 0;
     }
@@ -406,7 +427,7 @@ __global__ void __launch_bounds__(NT) k_grid_bigcell(TickBufs b) {
         __syncthreads();
         bitonic_inplace<NT>(b.gn_nxt + sn, nn, (int)threadIdx.x, [](const GEnt& e) { return e.slot; },
                             [] { __syncthreads(); });
-        for (uint32_t j = threadIdx.x; j < nn; j += NT) b.w.gidx[b.gn_nxt[sn + j].slot] = sn + j;
+        for (uint32_t j = threadIdx.x; j < nn; j += NT) b.w.gidx[b.gn_nxt[sn + j].slot] = j;
         if (threadIdx.x == 0) b.dep[c] = 0;
         __syncthreads();
     }
@@ -414,7 +435,6 @@ __global__ void __launch_bounds__(NT) k_grid_bigcell(TickBufs b) {
 
 void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint32_t NC = b.w.ncells;
-    hipLaunchKernelGGL(k_classify, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_cellcnt, dim3(nblk1((uint64_t)NC + 1, NT)), dim3(NT), 0, s, b);
     // totals land in the low words of the (zeroed, little-endian) 64-bit counters
     scan_exclusive<uint32_t, uint32_t>(b.cnt_new, b.start_nxt, (uint64_t)NC + 1, nullptr, sc,
@@ -422,7 +442,7 @@ void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     scan_exclusive<uint32_t, uint32_t>(b.gm_cnt, b.gm_start, (uint64_t)NC + 1, nullptr, sc,
                                        (uint32_t*)&b.st->n_gm, s);
     hipLaunchKernelGGL(k_place, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_grid_copy, dim3(nblk1(b.w.cap, NT)), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_grid_copy, dim3(std::min<uint32_t>(nblk1(b.w.cap, NT), 16384)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_grid_dirty, dim3(nblk1((uint64_t)NC, DIRTY_SPAN * NWAVE)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_grid_bigcell, dim3(64), dim3(NT), 0, s, b);
 }
@@ -507,14 +527,23 @@ struct Cand {
 constexpr uint32_t CAND_NONMOVER = 1u << 31;
 constexpr uint32_t CAND_CLIENT = 1u << 30;
 
-// WPB waves per block: a block keeps its LDS until its slowest wave ends, so
-// small blocks keep more waves resident when hotspot movers run long
-// One mover-grid entry m by one wave.  GN / GS: the current grid entries and
-// row starts (global, or LDS copies of the space's range in small-space
-// mode, indexed by global position either way); lds: SCAP sort slots per wave.
-template <int DIFF_U, uint32_t SCAP>
-__device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_t* lds, const GEnt* GN,
-                                          const uint32_t* GS, const uint32_t* MS) {
+// Where a walk reads its candidates: the row starts of both grids (Flat of a
+// mover's rectangles) and the entries, in HBM or, in small-space mode, LDS
+// copies indexed like HBM.
+struct GlobalSrc {
+    const GEnt* GN;
+    const uint32_t* GS;
+    const uint32_t* MS;
+    const MEnt* GM;
+    __device__ __forceinline__ Flat flat(const SpaceP& P, const Rects& R) const { return flat_build<2>(P, R, GS, MS); }
+    __device__ __forceinline__ GEnt gn(uint32_t i) const { return GN[i]; }
+    __device__ __forceinline__ MEnt gm(uint32_t i) const { return GM[i]; }
+};
+
+// One mover-grid entry m by one wave, candidates from S; lds: SCAP sort slots
+// per wave.
+template <int DIFF_U, uint32_t SCAP, class Src>
+__device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_t* lds, const Src& S) {
     const MEnt me = b.gm[m];
     const int ln = lane_id();
     if (!(me.tags & TAG_PRIMARY)) {
@@ -551,10 +580,14 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     uint64_t* mir = b.mir + reg;
     uint32_t n = 0, nl = 0, nm_ = 0, nml = 0;
     uint32_t c_old = 0, c_new = 0, c_band = 0, c_cli = 0;
-    Flat f = flat_build<2>(P, R, GS, MS);
+    Flat f = S.flat(P, R);
+    // long ranges (crowded rows): walk the live ranges with readlanes, a chunk
+    // overlaps one or two of them; short ones: the shuffle binary search
+    const bool walk = f.total >= (uint32_t)popc64(f.live) * b.walk_min;
     for (uint32_t base = 0; base < f.total; base += 64u * DIFF_U) {
         uint32_t idx[DIFF_U], kd[DIFF_U];
-        flat_map<DIFF_U, 2>(f, base, idx, kd);
+        if (walk) flat_map_walk<DIFF_U, 2>(f, base, idx, kd);
+        else flat_map<DIFF_U, 2>(f, base, idx, kd);
         Cand cc[DIFF_U];
 #pragma unroll
         for (int u = 0; u < DIFF_U; ++u) {
@@ -562,13 +595,13 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             cc[u].slot = A;                                    // invalid unless loaded below
             if (idx[u] != ~0u) {
                 if (kd[u] == 0) {
-                    const GEnt e = GN[idx[u]];
+                    const GEnt e = S.gn(idx[u]);
                     cc[u].x = cc[u].ox = e.x;
                     cc[u].z = cc[u].oz = e.z;
                     cc[u].slot = (e.meta & MOVER_BIT) ? A : e.slot;   // movers come from gm
                     cc[u].info = TAG_OLD | TAG_NEW | (e.meta & CLIENT_BIT ? CAND_CLIENT : 0u) | CAND_NONMOVER;
                 } else {
-                    const MEnt e = b.gm[idx[u]];
+                    const MEnt e = S.gm(idx[u]);
                     cc[u].x = e.x; cc[u].z = e.z; cc[u].ox = e.ox; cc[u].oz = e.oz;
                     cc[u].slot = e.slot;
                     cc[u].info = e.tags | (e.client ? CAND_CLIENT : 0u);
@@ -664,7 +697,7 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[WPB * SORT_LDS];
     const uint64_t m = (uint64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
     if (m >= b.st->n_gm) return;
-    mover_one<DIFF_U, SORT_LDS>(b, m, lds, b.w.gn, b.w.gn_start, b.gm_start);
+    mover_one<DIFF_U, SORT_LDS>(b, m, lds, GlobalSrc{b.w.gn, b.w.gn_start, b.gm_start, b.gm});
 }
 
 // Two mover-grid entries per wave (a half-wave each), small-space mode: with
@@ -879,16 +912,17 @@ __global__ void __launch_bounds__(NT) k_mover_small(TickBufs b) {
     if (b.small_halves) {
         for (uint32_t m = m0 + (threadIdx.x >> 6) * 2; m < m1; m += NWAVE * 2) {
             if (!mover_half<3>(b, m, m1, P, G - g0, S - cb, MS - cb)) {
-                mover_one<DIFF_U, SMALL_SORT>(b, m, lds, G - g0, S - cb, MS - cb);
+                const GlobalSrc src{G - g0, S - cb, MS - cb, b.gm};
+                mover_one<DIFF_U, SMALL_SORT>(b, m, lds, src);
                 wave_sync();
-                if (m + 1 < m1) mover_one<DIFF_U, SMALL_SORT>(b, m + 1, lds, G - g0, S - cb, MS - cb);
+                if (m + 1 < m1) mover_one<DIFF_U, SMALL_SORT>(b, m + 1, lds, src);
             }
             wave_sync();
         }
         return;
     }
     for (uint32_t m = m0 + (threadIdx.x >> 6); m < m1; m += NWAVE) {
-        mover_one<DIFF_U, SMALL_SORT>(b, m, lds, G - g0, S - cb, MS - cb);
+        mover_one<DIFF_U, SMALL_SORT>(b, m, lds, GlobalSrc{G - g0, S - cb, MS - cb, b.gm});
         wave_sync();
     }
 }
@@ -1689,7 +1723,10 @@ __global__ void __launch_bounds__(NT) k_tick_reset(TickBufs b) {
     }
     if (i < b.st->n_gm) {
         const MEnt e = b.gm[i];
-        if (e.tags & TAG_NEW) b.w.gn[b.w.gidx[e.slot]].meta &= ~MOVER_BIT;
+        if (e.tags & TAG_NEW) {                 // the new grid (b.w after the tick)
+            const uint32_t c = cell_of(b.w.sp[e.space], e.x, e.z);
+            b.w.gn[b.w.gn_start[c] + b.w.gidx[e.slot]].meta &= ~MOVER_BIT;
+        }
     }
 }
 void tick_reset(const TickBufs& b, hipStream_t s) {

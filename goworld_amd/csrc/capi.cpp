@@ -428,6 +428,7 @@ int gw_init(int device_id, gw_ctx** out) {
         if (const char* e = getenv("GW_CELLS_PER_D")) c->cells_per_d = std::min(4, std::max(1, atoi(e)));
         if (const char* e = getenv("GW_MOVER_WPB")) c->diff_u = atoi(e);
         if (const char* e = getenv("GW_NB_U")) c->nb_u = atoi(e);
+        if (const char* e = getenv("GW_WALK_MIN")) c->walk_min = (uint32_t)std::max(0, atoi(e));
     } while (0);
     if (rc) {
         (void)hipGetLastError();
@@ -975,6 +976,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.ops = ops; b.m = M; b.stamp_base = c->stamp_base;
     b.stamps = stamps;
     b.diff_u = c->diff_u;
+    b.walk_min = c->walk_min;
     b.ol = c->ol;
     b.st = st;
     b.gn_nxt = c->gnb[c->gcur ^ 1]; b.start_nxt = c->gsb[c->gcur ^ 1];
@@ -1000,10 +1002,10 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     }
 
     prof_begin(c, "ops");
+    c->cells_zero = false;                           // counters are in flight until the grid stage ends
     tick_ops(b, c->st);
     prof_end(c, (uint64_t)M * 24);
     prof_begin(c, "grid");
-    c->cells_zero = false;                           // counters are in flight until the grid stage ends
     tick_grid(b, c->sc, c->st);
     c->cells_zero = true;
     size_t s_grid = prof_end(c, 0);

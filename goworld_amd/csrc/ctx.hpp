@@ -151,6 +151,7 @@ struct gw_ctx {
     DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, cand, reg, own, big, mstat;
     DevBuf mir, ownc, mirc, mlist, mcnt, moff, minfo, icnt, ioff, mreg, chunk_first, srange, bk_a, bk_b, bk_id, bk_cnt, bk_split, ev_d, rtable;
     DevBuf scan_status, rs_hist;
+    uint32_t walk_min = 32;              // GW_WALK_MIN: TickBufs.walk_min (0: always walk)
     uint64_t ev_cap = 0;                 // events the flatten/sort buffers hold (grows on overflow)
     uint64_t ev_est = 0;                 // events expected this tick (last tick's count): sizes the buckets
     uint64_t it_est = 0;                 // bucket-path items of the last tick

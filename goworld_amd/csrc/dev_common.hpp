@@ -18,6 +18,12 @@ static inline uint32_t gstride(uint64_t n, uint32_t per) {   // grid of a grid-s
 }
 
 __device__ __forceinline__ uint64_t lo32(uint64_t v) { return v & 0xffffffffull; }
+
+// syncInfoFlag of slot s: 2 bits at flag_sh(s) of word flag_word(s) (the
+// collect's compaction reads cap/16 words instead of a word per slot)
+__device__ __forceinline__ uint32_t flag_word(uint32_t s) { return s >> 4; }
+__device__ __forceinline__ uint32_t flag_sh(uint32_t s) { return (s & 15u) * 2u; }
+__device__ __forceinline__ uint32_t flag_get(const uint32_t* f, uint32_t s) { return (f[flag_word(s)] >> flag_sh(s)) & 3u; }
 __device__ __forceinline__ uint64_t hi32(uint64_t v) { return v >> 32; }
 __device__ __forceinline__ float qnan() { return __builtin_nanf(""); }
 

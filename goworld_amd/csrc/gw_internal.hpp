@@ -85,7 +85,7 @@ __device__ __forceinline__ bool owned_x(const SpaceP& P, float x) { return x >= 
 
 constexpr int STAT_SHARDS = 256;
 constexpr int SH_FIELDS = 4;
-constexpr int SH_MOVERS = 0;  // distinct slots with an AOI op (k_classify)
+constexpr int SH_MOVERS = 0;  // distinct slots with an AOI op (k_ops3)
 constexpr int SH_AOLD = 1;    // a_old | a_new << 32 (per-shard sums stay below 2^32)
 constexpr int SH_BAND = 3;
 
@@ -148,11 +148,11 @@ struct World {
     PrevEnt* prev;
     unsigned long long* stamp; // global stamp of the slot's last AOI op
     float4* pos;               // x, y, z, yaw (sync payload)
-    uint32_t* flags;           // syncInfoFlag
+    uint32_t* flags;           // syncInfoFlag, packed: 2 bits per slot, 16 slots per word (flag_word / flag_sh)
     uint16_t* gate;            // client gate, 0 = no client
     GEnt* gn;                  // [cap] current grid, n_present entries
     uint32_t* gn_start;        // [ncells+1] first entry of each cell
-    uint32_t* gidx;            // [cap] index of the slot in gn
+    uint32_t* gidx;            // [cap] offset of the slot's entry inside its cell's range of gn
     // |{w related to e : w has a client}| as of the end of tick `epoch`
     // (epoch<<32 | count), written for every present mover by the diff; a
     // collect right after that tick takes it instead of walking e's window
@@ -221,6 +221,7 @@ struct TickBufs {
     uint32_t small_cells;     //   and max cells per space
     int small_halves;         //   two movers per wave (GW_MOVER_HALVES, default on)
     int diff_u;               // candidate chunks of 64 in flight per k_mover iteration
+    uint32_t walk_min;        // mean candidates per row range from which a walk maps chunks by readlanes
 };
 
 // events bucket path (aoi.hip k_flat_count / k_bucket_scatter / k_bucket_sort)

@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
         uint32_t keep = 0;
         for (int c = 0; c < 2; ++c)
             if (ol[s].clr[c] < 0) keep |= 1u << c;
-        f = ((w.flags[s] & keep) | rflag[s]) & SIF_ROUTED;
+        f = ((flag_get(w.flags, s) & keep) | rflag[s]) & SIF_ROUTED;
     }
     for (uint32_t d = 0; d < D.n; ++d) {
         const HaloDst& dst = D.d[d];

@@ -59,11 +59,11 @@ __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) 
 
 // ---------------------------------------------------------------------------
 // flagged entities in slot order, by a one-launch stream compaction (decoupled
-// look-back, prim.hpp): flagged[k] = slot, fbits[k] = its syncInfoFlag.  The
-// flags are cleared here, so the write pass reads fbits and can be rerun
-// after the record buffer overflowed.
+// look-back, prim.hpp) of the packed flag words (16 slots each): flagged[k] =
+// slot, fbits[k] = its syncInfoFlag.  The flags are cleared here, so the write
+// pass reads fbits and can be rerun after the record buffer overflowed.
 template <int IPT>
-__global__ void __launch_bounds__(NT) k_flag_compact1(uint32_t* __restrict__ flags, uint32_t cap,
+__global__ void __launch_bounds__(NT) k_flag_compact1(uint32_t* __restrict__ flags, uint32_t nwords,
                                                       uint32_t* __restrict__ flagged, uint32_t* __restrict__ fbits,
                                                       unsigned long long* __restrict__ status,
                                                       unsigned long long* __restrict__ ticket,
@@ -78,8 +78,8 @@ __global__ void __launch_bounds__(NT) k_flag_compact1(uint32_t* __restrict__ fla
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {       // striped: coalesced loads
         const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
-        f[j] = i < cap ? flags[i] : 0u;
-        c[j] = f[j] != 0;
+        f[j] = i < nwords ? flags[i] : 0u;
+        c[j] = (uint32_t)__popc((f[j] | (f[j] >> 1)) & 0x55555555u);   // slots with a bit set
     }
     uint32_t tot;
     tile_excl_scan_striped<uint32_t, IPT>(c, lds, tot);
@@ -93,8 +93,14 @@ __global__ void __launch_bounds__(NT) k_flag_compact1(uint32_t* __restrict__ fla
     for (int j = 0; j < IPT; ++j) {
         if (f[j]) {
             const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
-            flagged[pre + c[j]] = (uint32_t)i;
-            fbits[pre + c[j]] = f[j];
+            uint32_t m = (f[j] | (f[j] >> 1)) & 0x55555555u, at = pre + c[j];
+            while (m) {
+                const uint32_t b2 = (uint32_t)__builtin_ctz(m);
+                m &= m - 1;
+                flagged[at] = (uint32_t)(i * 16 + (b2 >> 1));
+                fbits[at] = (f[j] >> b2) & 3u;
+                ++at;
+            }
             flags[i] = 0;
         }
     }
@@ -103,9 +109,10 @@ __global__ void __launch_bounds__(NT) k_flag_compact1(uint32_t* __restrict__ fla
 
 void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint32_t* fbits, ScanCtx& sc,
                          uint32_t* total, hipStream_t s) {
-    const bool big = cap > SCAN_BIG;
+    const uint32_t nwords = (cap + 15) / 16;
+    const bool big = nwords > SCAN_BIG;
     const uint64_t tile = big ? 2 * SCAN_TILE : SCAN_TILE;
-    uint32_t nb = (uint32_t)((cap + tile - 1) / tile);
+    uint32_t nb = (uint32_t)((nwords + tile - 1) / tile);
     if (nb == 0) nb = 1;
     if (sc.tag >= SCAN_TAG_MAX) {
         (void)hipMemsetAsync(sc.status, 0, sc.max_tiles * SCAN_WORDS * 8, s);
@@ -113,10 +120,10 @@ void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint3
     }
     ++sc.tag;
     if (big)
-        hipLaunchKernelGGL(k_flag_compact1<2 * SCAN_IPT>, dim3(nb), dim3(NT), 0, s, flags, cap, flagged, fbits,
+        hipLaunchKernelGGL(k_flag_compact1<2 * SCAN_IPT>, dim3(nb), dim3(NT), 0, s, flags, nwords, flagged, fbits,
                            sc.status, sc.ticket, sc.tbase, sc.tag, total);
     else
-        hipLaunchKernelGGL(k_flag_compact1<SCAN_IPT>, dim3(nb), dim3(NT), 0, s, flags, cap, flagged, fbits,
+        hipLaunchKernelGGL(k_flag_compact1<SCAN_IPT>, dim3(nb), dim3(NT), 0, s, flags, nwords, flagged, fbits,
                            sc.status, sc.ticket, sc.tbase, sc.tag, total);
     sc.tbase += nb;
 }
@@ -642,8 +649,9 @@ __global__ void __launch_bounds__(NT) k_set_clients(World w, const uint32_t* slo
     if (i >= n || slots[i] >= w.cap) return;
     const uint32_t s = slots[i];
     w.gate[s] = gates[i];
-    if (grid_ok && (w.aoi[s].meta & PRESENT_BIT)) {
-        const uint32_t k = w.gidx[s];
+    const AoiEnt a = w.aoi[s];
+    if (grid_ok && (a.meta & PRESENT_BIT)) {
+        const uint32_t k = w.gn_start[cell_of(w.sp[a.meta & SPACE_MASK], a.x, a.z)] + w.gidx[s];
         if (k < w.cap) {
             GEnt* g = w.gn + k;
             if (g->slot == s) g->meta = (g->meta & ~CLIENT_BIT) | (gates[i] ? CLIENT_BIT : 0u);

@@ -91,7 +91,8 @@ __global__ void __launch_bounds__(NT) k_ops2(TickBufs b) {
     if (keep != 0xffffffffu) atomicAnd(&b.w.flags[flag_word(s)], ~((~keep & 3u) << flag_sh(s)));
 }
 
-__device__ __forceinline__ void classify_mover(const TickBufs& b, uint32_t A, const AoiEnt& a, const PrevEnt& p);
+__device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, uint32_t A, const AoiEnt& a,
+                                                const PrevEnt& p);
 
 // Per op: the syncInfoFlag bits, the sync payload of the slot's last
 // non-Leave op; the slot's last AOI op saves the pre-tick position and stamp
@@ -137,7 +138,9 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
     // to one counter serialised ~4k atomics at 1M ops: ~100 us at config #4)
     const uint32_t nw = (uint32_t)popc64(wave_ballot(mv));
     if (lane_id() == 0 && nw) shard_add(b.st, blockIdx.x * NWAVE + (threadIdx.x >> 6), SH_MOVERS, nw);
-    if (mv) classify_mover(b, s, a, p);
+    uint2 cc = make_uint2(NO_CELL, NO_CELL);
+    if (mv) cc = classify_mover(b, i, s, a, p);
+    if (i < b.m) b.mcell[i] = cc;               // k_place reads the movers back coalesced
 }
 
 // Restore path (Space.go:209-214, EntityManager.go:556-617): entity i enters
@@ -231,46 +234,36 @@ void grid_rebuild(const World& w, DevStats* st, uint32_t* k0, uint32_t* v0, uint
 
 // ---------------------------------------------------------------------------
 // incremental grid.  co / cn: the mover's cell before / after the tick
-// (NO_CELL when absent).  co is the cell its pre-tick grid entry sits in.
-struct MoverCells {
-    uint32_t A, co, cn;
-    AoiEnt a;
-    PrevEnt p;
-};
-__device__ __forceinline__ MoverCells mover_cells(const World& w, uint32_t A) {
-    MoverCells m;
-    m.A = A;
-    m.a = w.aoi[A];
-    m.p = w.prev[A];
-    const SpaceP P = w.sp[m.a.meta & SPACE_MASK];
-    m.co = m.cn = NO_CELL;
-    if (m.p.ox == m.p.ox) m.co = cell_of(P, m.p.ox, m.p.oz);
-    if (m.a.meta & PRESENT_BIT) m.cn = cell_of(P, m.a.x, m.a.z);
-    return m;
-}
-
-// op i is slot s's mover entry when it is s's last AOI op (no list: a
-// single-address list counter serialises across the chip)
-__device__ __forceinline__ bool op_mover(const TickBufs& b, uint32_t i, uint32_t& s) {
-    const gw_op op = b.ops[i];
-    s = op.slot;
-    return s < b.w.cap && op.kind >= GW_OP_ENTER && op.kind <= GW_OP_LEAVE && b.ol[s].aoi == (int32_t)i;
-}
+// (NO_CELL when absent).  co is the cell its pre-tick grid entry sits in.  A
+// mover is slot s's last AOI op (no list: a single-address list counter
+// serialises across the chip).
 
 // per mover: mover-grid histogram; a mover staying in its cell is patched in
 // place, the others count as a departure / an arrival of their cells (called
-// by k_ops3 with the slot's state after the tick and before it)
-__device__ __forceinline__ void classify_mover(const TickBufs& b, uint32_t A, const AoiEnt& a, const PrevEnt& p) {
+// by k_ops3, op i, with the slot's state after the tick and before it).  The
+// mover's mover-grid entry (tags aside) goes to mtmp[i] and its cells are
+// returned for mcell[i], so k_place reads them coalesced.
+__device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, uint32_t A, const AoiEnt& a,
+                                                const PrevEnt& p) {
     const SpaceP P = b.w.sp[a.meta & SPACE_MASK];
     uint32_t co = NO_CELL, cn = NO_CELL;
     if (p.ox == p.ox) co = cell_of(P, p.ox, p.oz);
     if (a.meta & PRESENT_BIT) cn = cell_of(P, a.x, a.z);
+    const bool cl = b.w.gate[A] != 0;
+    if (co != NO_CELL || cn != NO_CELL) {
+        const bool pn = cn != NO_CELL;
+        MEnt m;
+        m.x = pn ? a.x : qnan(); m.z = pn ? a.z : qnan();
+        m.ox = p.ox; m.oz = p.oz;
+        m.slot = A; m.tags = 0; m.client = cl ? 1u : 0u; m.space = a.meta & SPACE_MASK;
+        b.mtmp[i] = m;
+    }
     if (co != NO_CELL) atomicAdd(&b.gm_cnt[co], 1u);
     if (cn != NO_CELL && cn != co) atomicAdd(&b.gm_cnt[cn], 1u);
     if (co != NO_CELL && co == cn) {
         GEnt e;
         e.x = a.x; e.z = a.z; e.slot = A;
-        e.meta = cn | (b.w.gate[A] ? CLIENT_BIT : 0u) | MOVER_BIT;
+        e.meta = cn | (cl ? CLIENT_BIT : 0u) | MOVER_BIT;
         b.w.gn[b.w.gn_start[co] + b.w.gidx[A]] = e;
     } else {
         if (co != NO_CELL) {
@@ -279,6 +272,7 @@ __device__ __forceinline__ void classify_mover(const TickBufs& b, uint32_t A, co
         }
         if (cn != NO_CELL) atomicAdd(&b.arr[cn], 1u);
     }
+    return make_uint2(co, cn);
 }
 
 // per cell: entries after the tick; cells with departures or arrivals are
@@ -300,29 +294,26 @@ __global__ void __launch_bounds__(NT) k_cellcnt(TickBufs b) {
 // and, for an arrival, its grid entry behind the kept entries of the new cell
 __global__ void __launch_bounds__(NT) k_place(TickBufs b) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
-    uint32_t A = 0;
-    if (i < b.m && op_mover(b, i, A)) {
-        const MoverCells mc = mover_cells(b.w, A);
-        const bool cl = b.w.gate[mc.A] != 0;
-        const bool pn = mc.cn != NO_CELL;
-        MEnt e;
-        e.x = pn ? mc.a.x : qnan(); e.z = pn ? mc.a.z : qnan();
-        e.ox = mc.p.ox; e.oz = mc.p.oz;
-        e.slot = mc.A; e.client = cl ? 1u : 0u; e.space = mc.a.meta & SPACE_MASK;
-        if (mc.co != NO_CELL) {
-            e.tags = TAG_OLD | (mc.cn == mc.co ? TAG_NEW | TAG_PRIMARY : 0u) | (pn ? 0u : TAG_PRIMARY);
-            b.gm[b.gm_start[mc.co] + atomicSub(&b.gm_cnt[mc.co], 1u) - 1u] = e;
-        }
-        if (pn && mc.cn != mc.co) {
-            e.tags = TAG_NEW | TAG_PRIMARY;
-            b.gm[b.gm_start[mc.cn] + atomicSub(&b.gm_cnt[mc.cn], 1u) - 1u] = e;
-            const uint32_t kept = (b.w.gn_start[mc.cn + 1] - b.w.gn_start[mc.cn]) - (b.dep[mc.cn] & ~CELL_DIRTY);
-            const uint32_t at = b.start_nxt[mc.cn] + kept + atomicSub(&b.arr[mc.cn], 1u) - 1u;
-            GEnt g;
-            g.x = mc.a.x; g.z = mc.a.z; g.slot = mc.A;
-            g.meta = mc.cn | (cl ? CLIENT_BIT : 0u) | MOVER_BIT;
-            b.gn_nxt[at] = g;
-        }
+    if (i >= b.m) return;
+    const uint2 cc = b.mcell[i];
+    const uint32_t co = cc.x, cn = cc.y;
+    if (co == NO_CELL && cn == NO_CELL) return;             // not a mover, or absent before and after
+    MEnt e = b.mtmp[i];
+    const bool cl = e.client != 0;
+    const bool pn = cn != NO_CELL;
+    if (co != NO_CELL) {
+        e.tags = TAG_OLD | (cn == co ? TAG_NEW | TAG_PRIMARY : 0u) | (pn ? 0u : TAG_PRIMARY);
+        b.gm[b.gm_start[co] + atomicSub(&b.gm_cnt[co], 1u) - 1u] = e;
+    }
+    if (pn && cn != co) {
+        e.tags = TAG_NEW | TAG_PRIMARY;
+        b.gm[b.gm_start[cn] + atomicSub(&b.gm_cnt[cn], 1u) - 1u] = e;
+        const uint32_t kept = (b.w.gn_start[cn + 1] - b.w.gn_start[cn]) - (b.dep[cn] & ~CELL_DIRTY);
+        const uint32_t at = b.start_nxt[cn] + kept + atomicSub(&b.arr[cn], 1u) - 1u;
+        GEnt g;
+        g.x = e.x; g.z = e.z; g.slot = e.slot;
+        g.meta = cn | (cl ? CLIENT_BIT : 0u) | MOVER_BIT;
+        b.gn_nxt[at] = g;
     }
 }
 
@@ -659,7 +650,14 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     }
     // sort the own events by (target, kind)
     if (n > 1) {
-        if (n <= 64) {
+        if (n <= b.rank_sort) {                    // a few events: place each by its rank
+            wave_sync();
+            const uint32_t v = ln < (int)n ? out[ln] : 0xffffffffu;
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < n; ++j) r += (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j) < v ? 1u : 0u;
+            wave_sync();
+            if (ln < (int)n) out[r] = v;
+        } else if (n <= 64) {
             wave_sync();
             uint32_t v = ln < (int)n ? out[ln] : 0xffffffffu;
             v = wave_sort64(v);
@@ -684,7 +682,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             b.gmi[A] = (uint32_t)m;
         }
         if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | scl;
-        // per-mover statistics, summed by k_mover_stats (no atomics here: 2 per
+        // per-mover statistics, summed by k_mover_post (no atomics here: 2 per
         // mover into 256 shards cost 25 us at config #3 and 180 us at config #4)
         b.mstat[m] = make_ulonglong2((unsigned long long)so | ((unsigned long long)sn << 32), sb);
     }
@@ -860,8 +858,22 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     if (wave_ballot(reg_sort)) {
         wave_sync();
         uint32_t v = (reg_sort && hl < n) ? out[hl] : 0xffffffffu;
-        v = half_sort32(v);
-        if (reg_sort && hl < n) out[hl] = v;
+        const uint32_t n2 = reg_sort ? n : 0u;
+        const uint32_t nmax = max((uint32_t)__builtin_amdgcn_readlane((int)n2, 0),
+                                  (uint32_t)__builtin_amdgcn_readlane((int)n2, 32));
+        if (nmax <= b.rank_sort) {                  // a few events per half: place each by its rank
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < nmax; ++j) {
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)v, 32 + (int)j);
+                r += (half ? hi : lo) < v ? 1u : 0u;
+            }
+            wave_sync();
+            if (reg_sort && hl < n) out[r] = v;
+        } else {
+            v = half_sort32(v);
+            if (reg_sort && hl < n) out[hl] = v;
+        }
     }
     if (go && n > 32 && hl == 0) b.big[atomicAdd(&b.st->n_big, 1ull)] = (uint32_t)m;
     if (valid && hl == 0) {
@@ -929,11 +941,26 @@ __global__ void __launch_bounds__(NT) k_mover_small(TickBufs b) {
 
 // A_old | A_new << 32 and band counts of every mover-grid entry, one shard per
 // block (STAT_SHARDS blocks, so no two blocks add to the same words)
-__global__ void __launch_bounds__(NT) k_mover_stats(TickBufs b) {
+// Blocks [0, STAT_SHARDS) sum the statistics; the others block-sort the own
+// events of movers with too many for LDS (k_mover listed them in big[]): one
+// launch for both small jobs.
+__global__ void __launch_bounds__(NT) k_mover_post(TickBufs b) {
+    if (blockIdx.x >= (uint32_t)STAT_SHARDS) {              // block-uniform role
+        const uint64_t nb = b.st->n_big;
+        for (uint64_t k = blockIdx.x - STAT_SHARDS; k < nb; k += gridDim.x - STAT_SHARDS) {
+            const uint32_t m = b.big[k];
+            const uint64_t c = b.ownc[m];
+            const uint32_t n = (uint32_t)(lo32(c) + hi32(c));
+            bitonic_inplace<NT>(b.own + b.reg[m], n, (int)threadIdx.x, [](uint32_t v) { return v; },
+                                [] { __syncthreads(); });
+            __syncthreads();
+        }
+        return;
+    }
     __shared__ unsigned long long red[2][NWAVE];
     const uint64_t n = b.st->n_gm;
     unsigned long long a = 0, c = 0;
-    for (uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x; m < n; m += (uint64_t)gridDim.x * NT) {
+    for (uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x; m < n; m += (uint64_t)STAT_SHARDS * NT) {
         const ulonglong2 v = b.mstat[m];
         a += v.x;
         c += v.y;
@@ -950,18 +977,6 @@ __global__ void __launch_bounds__(NT) k_mover_stats(TickBufs b) {
     }
 }
 
-// block sort of a mover's own events too many for LDS
-__global__ void __launch_bounds__(NT) k_big_own(TickBufs b) {
-    const uint64_t nb = b.st->n_big;
-    for (uint64_t k = blockIdx.x; k < nb; k += gridDim.x) {
-        const uint32_t m = b.big[k];
-        const uint64_t c = b.ownc[m];
-        const uint32_t n = (uint32_t)(lo32(c) + hi32(c));
-        bitonic_inplace<NT>(b.own + b.reg[m], n, (int)threadIdx.x, [](uint32_t v) { return v; },
-                            [] { __syncthreads(); });
-        __syncthreads();
-    }
-}
 
 // ---------------------------------------------------------------------------
 // events stage.  (1) movers with events in slot order: compaction of the
@@ -1212,7 +1227,7 @@ __global__ void __launch_bounds__(NT) k_flat_items(TickBufs b) {
 // sort.
 //
 // Bucket bounds are quantiles of the previous tick's (leave, watcher) keys
-// (k_bk_split), so skewed slot ranges (hotspot entities in adjacent slots)
+// (bk_split_next), so skewed slot ranges (hotspot entities in adjacent slots)
 // still give buckets of about the mean size; bucket(k) = #{bounds <= k},
 // found through a 2^12-cell table of bound counts (A[x] = #{bounds < x <<
 // lsh}) and a binary search inside the cell (usually empty).
@@ -1632,7 +1647,7 @@ __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
 // quantiles of this tick's sorted (leave, watcher) keys: the next tick's
 // bucket bounds (BK_NSPLIT of them; a tick with fewer buckets takes every
 // (BK_NSPLIT / NB)-th).  Kept when the tick overflowed or had no events.
-__global__ void __launch_bounds__(NT) k_bk_split(TickBufs b) {
+__device__ __forceinline__ void bk_split_next(const TickBufs& b) {
     const uint64_t E = lo32(b.st->ev_pk) + hi32(b.st->ev_pk), ne = lo32(b.st->ev_pk);
     if (E == 0 || E > b.ev_cap || b.st->overflow) return;
     const uint32_t lvb = 1u << b.wbits;
@@ -1665,8 +1680,7 @@ void tick_diff(const TickBufs& b, hipStream_t s) {
 }
 void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint64_t nmax = 2ull * b.m;
-    hipLaunchKernelGGL(k_mover_stats, dim3(STAT_SHARDS), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_big_own, dim3(64), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_mover_post, dim3(STAT_SHARDS + 64), dim3(NT), 0, s, b);
     // movers in slot order
     const uint64_t nwords = (uint64_t)b.w.cap / 32 + 1;
     const uint64_t tile = (uint64_t)SCAN_IPT * NT;
@@ -1702,7 +1716,6 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
         radix_sort2(b.fk0, b.fv0, b.fk1, b.fv1, b.ev_cap, (const uint64_t*)&b.st->n_sort, 0, b.wbits + 1,
                     b.rtable, s, b.ev, (1u << b.wbits) - 1u);
     }
-    hipLaunchKernelGGL(k_bk_split, dim3(1), dim3(NT), 0, s, b);
     (void)nmax;
 }
 
@@ -1712,6 +1725,7 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
 // mover-grid entry i)
 __global__ void __launch_bounds__(NT) k_tick_reset(TickBufs b) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (blockIdx.x == 0) bk_split_next(b);   // the next tick's bucket bounds (its own launch cost 5-8 us)
     if (i < b.m) {
         const uint32_t s = b.ops[i].slot;
         if (s < b.w.cap) {

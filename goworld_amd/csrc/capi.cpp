@@ -429,6 +429,7 @@ int gw_init(int device_id, gw_ctx** out) {
         if (const char* e = getenv("GW_MOVER_WPB")) c->diff_u = atoi(e);
         if (const char* e = getenv("GW_NB_U")) c->nb_u = atoi(e);
         if (const char* e = getenv("GW_WALK_MIN")) c->walk_min = (uint32_t)std::max(0, atoi(e));
+        if (const char* e = getenv("GW_RANK_SORT")) c->rank_sort = (uint32_t)std::max(0, atoi(e));
     } while (0);
     if (rc) {
         (void)hipGetLastError();
@@ -562,6 +563,7 @@ int gw_space_restore(gw_ctx* c, uint32_t sid, const uint32_t* slots, const float
     HIPCHK(hipMemcpyAsync(dslots, slots, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemcpyAsync(dp, p.data(), (size_t)n * 16, hipMemcpyHostToDevice, c->st));
     launch_restore(world(c), dslots, dp, n, c->stamp_base, sync_flags, c->st);
+    c->flag_bound += n;
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->st));            // the host arrays are the caller's
     c->stamp_base += n;
@@ -814,6 +816,11 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     if (!(flags & GW_TICK_NO_EVENTS)) {                // sizes the next tick's buckets
         c->ev_est = n_enter + n_leave;
         if (!b.ev_full) c->it_est = hs.n_items;
+        // the launches of the event stage (flatten chunks, bucket tiles) scale
+        // with ev_cap: after a burst, come back down to twice the need (the
+        // buffers keep their size; an overflow grows it again)
+        const uint64_t want = std::max<uint64_t>(48ull * M + 4096, 2 * (n_enter + n_leave) + 4096);
+        if (c->ev_cap > 2 * want) c->ev_cap = want;
     }
     if (c->ev_full_ticks > 0) --c->ev_full_ticks;
     if (!b.ev_full) c->bk_overflows = 0;
@@ -953,10 +960,17 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     }
     const uint32_t NC = c->total_cells;
     const uint64_t M2 = 2ull * M;
+    c->flag_bound += M;                              // an op may flag its slot
     // ---- buffers (event regions sized from the last tick; grown on overflow)
-    c->own_cap = std::max<uint64_t>(c->own_cap, 64ull * M + 4096);
-    c->ev_cap = std::max<uint64_t>(c->ev_cap, 48ull * M + 4096);
-    if ((rc = ensure(c, c->gm, M2 * sizeof(MEnt))) ||
+    // a NO_EVENTS tick (bulk load / restore path) only updates the state: no
+    // diff, no event stage, and its op count does not size the event buffers
+    const bool ev_on = !(flags & GW_TICK_NO_EVENTS);
+    if (ev_on) {
+        c->own_cap = std::max<uint64_t>(c->own_cap, 64ull * M + 4096);
+        c->ev_cap = std::max<uint64_t>(c->ev_cap, 48ull * M + 4096);
+    }
+    if ((rc = ensure(c, c->gm, M2 * sizeof(MEnt))) || (rc = ensure(c, c->mtmp, (size_t)M * sizeof(MEnt))) ||
+        (rc = ensure(c, c->mcell, (size_t)M * 8)) ||
         (rc = ensure(c, c->cand, M2 * 8)) || (rc = ensure(c, c->reg, M2 * 8)) ||
         (rc = ensure(c, c->ownc, M2 * 8)) || (rc = ensure(c, c->mirc, M2 * 8)) || (rc = ensure(c, c->big, M2 * 4)) ||
         (rc = ensure(c, c->mstat, M2 * 16)) ||
@@ -977,11 +991,13 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.stamps = stamps;
     b.diff_u = c->diff_u;
     b.walk_min = c->walk_min;
+    b.rank_sort = c->rank_sort;
     b.ol = c->ol;
     b.st = st;
     b.gn_nxt = c->gnb[c->gcur ^ 1]; b.start_nxt = c->gsb[c->gcur ^ 1];
     b.dep = c->dep; b.arr = c->arr; b.cnt_new = c->cnt_new; b.bigcell = c->bigcell;
     b.gm_cnt = c->gm_cnt; b.gm_start = c->gm_start; b.gm = P<MEnt>(c->gm);
+    b.mtmp = P<MEnt>(c->mtmp); b.mcell = P<uint2>(c->mcell);
     b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg);
     b.ownc = P<unsigned long long>(c->ownc); b.mirc = P<unsigned long long>(c->mirc);
     b.big = P<uint32_t>(c->big);
@@ -1012,13 +1028,13 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     c->gcur ^= 1;                                    // the new grid is current from here on
     b.w = world(c);
     prof_begin(c, "movers");
-    tick_movers(b, c->sc, c->st);
+    if (ev_on) tick_movers(b, c->sc, c->st);
     size_t s_movers = prof_end(c, 0);
     prof_begin(c, "diff");
-    tick_diff(b, c->st);
+    if (ev_on) tick_diff(b, c->st);
     size_t s_diff = prof_end(c, 0);
     prof_begin(c, "events");
-    tick_events(b, c->sc, c->st);
+    if (ev_on) tick_events(b, c->sc, c->st);
     size_t s_events = prof_end(c, 0);
     HIPCHK(hipGetLastError());
     c->segs.clear();
@@ -1068,14 +1084,18 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     c->rec_cap = std::max<uint64_t>(c->rec_cap, 4ull * C + 1024);
     if ((rc = ensure(c, c->rec0, c->rec_cap * sizeof(gw_sync_record)))) return rc;
     const World w = world(c);
+    // only slots with an op or a restore since the last collect can be flagged:
+    // the passes over the flagged list are sized by that bound, not the slots
+    const uint32_t NFM = (uint32_t)std::min<uint64_t>(C, std::max<uint64_t>(c->flag_bound, 1));
+    c->flag_bound = 0;
     prof_begin(c, "sync_flagged");
     launch_flag_compact(c->flags, C, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), c->sc, (uint32_t*)&st->flagged,
                         c->st);
     prof_end(c, (uint64_t)C * 4 * 2);
     const uint64_t* nf = (const uint64_t*)&st->flagged;
     prof_begin(c, "sync_count");
-    launch_sync_count(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint32_t>(c->rec_cnt), c->st);
-    scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), C, nf, c->sc,
+    launch_sync_count(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint32_t>(c->rec_cnt), c->st);
+    scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), NFM, nf, c->sc,
                  (uint64_t*)&st->rec_total, c->st);
     size_t s_count = prof_end(c, 0);
     prof_begin(c, "sync_write");
@@ -1096,13 +1116,13 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
                                     P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st,
                                     P<uint32_t>(c->srange), P<uint32_t>(c->srange) + n_sp, max_ents, max_cells, c->st);
         else
-            launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, C, P<uint64_t>(c->rec_off),
+            launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint64_t>(c->rec_off),
                               P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
     };
     if (small) {
         if ((rc = ensure(c, c->srange, (size_t)n_sp * 8))) return rc;
         HIPCHK(hipMemsetAsync(c->srange.p, 0, (size_t)n_sp * 8, c->st));
-        launch_space_ranges(w, P<uint32_t>(c->flagged), nf, C, P<uint32_t>(c->srange), P<uint32_t>(c->srange) + n_sp,
+        launch_space_ranges(w, P<uint32_t>(c->flagged), nf, NFM, P<uint32_t>(c->srange), P<uint32_t>(c->srange) + n_sp,
                             c->st);
     }
     write_pass();

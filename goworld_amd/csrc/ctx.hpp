@@ -148,10 +148,11 @@ struct gw_ctx {
     gw_tick_out last_out{};
 
     // grid + tick scratch
-    DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, cand, reg, own, big, mstat;
+    DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, mtmp, mcell, cand, reg, own, big, mstat;
     DevBuf mir, ownc, mirc, mlist, mcnt, moff, minfo, icnt, ioff, mreg, chunk_first, srange, bk_a, bk_b, bk_id, bk_cnt, bk_split, ev_d, rtable;
     DevBuf scan_status, rs_hist;
     uint32_t walk_min = 32;              // GW_WALK_MIN: TickBufs.walk_min (0: always walk)
+    uint32_t rank_sort = 12;             // GW_RANK_SORT: TickBufs.rank_sort
     uint64_t ev_cap = 0;                 // events the flatten/sort buffers hold (grows on overflow)
     uint64_t ev_est = 0;                 // events expected this tick (last tick's count): sizes the buckets
     uint64_t it_est = 0;                 // bucket-path items of the last tick
@@ -163,6 +164,7 @@ struct gw_ctx {
     DevBuf fbits, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
     DevBuf cl_slot, cl_off, h_cl_slot, h_cl_off;   // GW_SYNC_BY_CLIENT segments (device / pinned host)
     uint64_t rec_cap = 0;                // records the rec0 buffer holds (grows on overflow)
+    uint64_t flag_bound = 0;             // ops + restored slots since the last collect (>= flagged slots)
     // client messages (gw_client_events, gw_fanout): ping-pong + pinned host + gate offsets
     struct MsgBufs {
         DevBuf a, b, h;

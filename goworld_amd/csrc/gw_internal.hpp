@@ -181,6 +181,8 @@ struct TickBufs {
     uint32_t* gm_cnt;         // [ncells+1]
     uint32_t* gm_start;       // [ncells+1]
     MEnt* gm;                 // [2m]
+    MEnt* mtmp;               // [m] op i's mover-grid entry (tags aside) when op i is a mover (k_ops3 -> k_place)
+    uint2* mcell;             // [m] its old / new cell (NO_CELL: none), NO_CELL twice for other ops
     // diff (indexed by mover-grid entry)
     uint64_t* cand;           // [2m] candidate bound (0 unless TAG_PRIMARY)
     uint64_t* reg;            // [2m] exclusive scan of cand
@@ -222,6 +224,7 @@ struct TickBufs {
     int small_halves;         //   two movers per wave (GW_MOVER_HALVES, default on)
     int diff_u;               // candidate chunks of 64 in flight per k_mover iteration
     uint32_t walk_min;        // mean candidates per row range from which a walk maps chunks by readlanes
+    uint32_t rank_sort;       // own events sorted by rank (readlanes) up to this many, more by a network
 };
 
 // events bucket path (aoi.hip k_flat_count / k_bucket_scatter / k_bucket_sort)

@@ -1651,7 +1651,7 @@ __device__ __forceinline__ void bk_split_next(const TickBufs& b) {
     const uint64_t E = lo32(b.st->ev_pk) + hi32(b.st->ev_pk), ne = lo32(b.st->ev_pk);
     if (E == 0 || E > b.ev_cap || b.st->overflow) return;
     const uint32_t lvb = 1u << b.wbits;
-    for (uint32_t j = 1 + threadIdx.x; j < BK_NSPLIT; j += NT) {
+    for (uint32_t j = 1 + blockIdx.x * NT + threadIdx.x; j < BK_NSPLIT; j += gridDim.x * NT) {   // 1 per thread
         const uint64_t p = (uint64_t)j * E / BK_NSPLIT;
         b.bk_split[j] = (p >= ne ? lvb : 0u) | b.ev[p].watcher;
     }
@@ -1725,7 +1725,7 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
 // mover-grid entry i)
 __global__ void __launch_bounds__(NT) k_tick_reset(TickBufs b) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
-    if (blockIdx.x == 0) bk_split_next(b);   // the next tick's bucket bounds (its own launch cost 5-8 us)
+    bk_split_next(b);                        // the next tick's bucket bounds (its own launch cost 5-8 us)
     if (i < b.m) {
         const uint32_t s = b.ops[i].slot;
         if (s < b.w.cap) {

@@ -53,7 +53,7 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t v, uint32_t* lis
 // ---------------------------------------------------------------------------
 // ops: last-op dedupe per slot (seq = index in the tick's op stream)
 __global__ void __launch_bounds__(NT) k_ops1(TickBufs b) {
-    uint32_t i = blockIdx.x * NT + threadIdx.x;
+    const uint32_t i = b.op0 + blockIdx.x * NT + threadIdx.x;
     if (i >= b.m) return;
     gw_op op = b.ops[i];
     if (op.kind == GW_OP_NOP) return;
@@ -61,12 +61,13 @@ __global__ void __launch_bounds__(NT) k_ops1(TickBufs b) {
         atomicAdd(&b.st->bad_ops, 1ull);
         return;
     }
-    if (op.kind != GW_OP_LEAVE) atomicMax(&b.ol[op.slot].pos, (int32_t)i);
-    if (op.kind != GW_OP_SYNC) atomicMax(&b.ol[op.slot].aoi, (int32_t)i);
+    const unsigned long long v = ol_put(b.ol_tag, i);
+    if (op.kind != GW_OP_LEAVE) atomicMax(&b.ol[op.slot].pos, v);
+    if (op.kind != GW_OP_SYNC) atomicMax(&b.ol[op.slot].aoi, v);
     if (op.kind == GW_OP_LEAVE) {
-        atomicMax(&b.ol[op.slot].leave, (int32_t)i);
+        atomicMax(&b.ol[op.slot].leave, v);
         for (int c = 0; c < 2; ++c)                     // the last Leave that clears bit c
-            if (!((op.sync_flags >> c) & 1)) atomicMax(&b.ol[op.slot].clr[c], (int32_t)i);
+            if (!((op.sync_flags >> c) & 1)) atomicMax(&b.ol[op.slot].clr[c], v);
     }
 }
 
@@ -76,21 +77,8 @@ __global__ void __launch_bounds__(NT) k_ops1(TickBufs b) {
 // or enters another AOI space, whose Enter flags it anew).  In call order the
 // ops are f -> (f & mask) and f -> (f | bits); per bit c the result is: the
 // old bit unless some Leave cleared c, OR'd with the bits of the ops after the
-// last Leave that cleared c.  One thread per slot with a Leave (its last one)
-// clears here, k_ops3 ORs.
-__global__ void __launch_bounds__(NT) k_ops2(TickBufs b) {
-    uint32_t i = blockIdx.x * NT + threadIdx.x;
-    if (i >= b.m) return;
-    gw_op op = b.ops[i];
-    if (op.slot >= b.w.cap || op.kind != GW_OP_LEAVE) return;
-    const uint32_t s = op.slot;
-    if (b.ol[s].leave != (int32_t)i) return;
-    uint32_t keep = 0xffffffffu;
-    for (int c = 0; c < 2; ++c)
-        if (b.ol[s].clr[c] >= 0) keep &= ~(1u << c);
-    if (keep != 0xffffffffu) atomicAnd(&b.w.flags[flag_word(s)], ~((~keep & 3u) << flag_sh(s)));
-}
-
+// last Leave that cleared c.  The slot's last Leave clears in k_ops3, every
+// op's bits after it are OR'd in by k_place (a later launch: clear, then OR).
 __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, uint32_t A, const AoiEnt& a,
                                                 const PrevEnt& p);
 
@@ -102,21 +90,31 @@ __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, u
 __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     bool mv = false;
-    uint32_t s = 0;
+    uint32_t s = 0, fbits = 0;
     AoiEnt a;
     PrevEnt p;
     if (i < b.m) {
         const gw_op op = b.ops[i];
         s = op.slot;
         if (s < b.w.cap && op.kind >= GW_OP_ENTER && op.kind <= GW_OP_SYNC) {
-            const OpLast ol = b.ol[s];
+            const OpLast o = b.ol[s];
+            struct { int32_t pos, aoi, leave, clr[2]; } ol;
+            ol.pos = ol_get(o.pos, b.ol_tag);
+            ol.aoi = ol_get(o.aoi, b.ol_tag);
+            ol.leave = ol_get(o.leave, b.ol_tag);
+            ol.clr[0] = ol_get(o.clr[0], b.ol_tag);
+            ol.clr[1] = ol_get(o.clr[1], b.ol_tag);
             // syncInfoFlag |= bits of every call after the last Leave that
-            // cleared them (Space.go:196, Entity.go:1199-1204, 1286)
+            // cleared them (Space.go:196, Entity.go:1199-1204, 1286): OR'd in
+            // by k_place, after the slot's last Leave cleared its bits here
             if (op.kind != GW_OP_LEAVE && op.sync_flags) {
-                uint32_t bits = 0;
                 for (int c = 0; c < 2; ++c)
-                    if (((op.sync_flags >> c) & 1) && (int32_t)i > ol.clr[c]) bits |= 1u << c;
-                if (bits) atomicOr(&b.w.flags[flag_word(s)], bits << flag_sh(s));
+                    if (((op.sync_flags >> c) & 1) && (int32_t)i > ol.clr[c]) fbits |= 1u << c;
+            } else if (op.kind == GW_OP_LEAVE && ol.leave == (int32_t)i) {
+                uint32_t clear = 0;
+                for (int c = 0; c < 2; ++c)
+                    if (ol.clr[c] >= 0) clear |= 1u << c;
+                if (clear) atomicAnd(&b.w.flags[flag_word(s)], ~(clear << flag_sh(s)));
             }
             if (ol.pos == (int32_t)i) b.w.pos[s] = make_float4(op.x, op.y, op.z, op.yaw);
             if (ol.aoi == (int32_t)i) {                 // the slot's mover entry (never a SYNC op)
@@ -140,7 +138,7 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
     if (lane_id() == 0 && nw) shard_add(b.st, blockIdx.x * NWAVE + (threadIdx.x >> 6), SH_MOVERS, nw);
     uint2 cc = make_uint2(NO_CELL, NO_CELL);
     if (mv) cc = classify_mover(b, i, s, a, p);
-    if (i < b.m) b.mcell[i] = cc;               // k_place reads the movers back coalesced
+    if (i < b.m) b.mcell[i] = make_uint4(cc.x, cc.y, s, fbits);   // k_place reads them back coalesced
 }
 
 // Restore path (Space.go:209-214, EntityManager.go:556-617): entity i enters
@@ -168,8 +166,7 @@ void launch_restore(const World& w, const uint32_t* slots, const float4* xyzw, u
 }
 
 void tick_ops(const TickBufs& b, hipStream_t s) {
-    hipLaunchKernelGGL(k_ops1, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_ops2, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
+    if (b.m > b.op0) hipLaunchKernelGGL(k_ops1, dim3(nblk(b.m - b.op0, NT)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_ops3, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
 }
 
@@ -295,7 +292,8 @@ __global__ void __launch_bounds__(NT) k_cellcnt(TickBufs b) {
 __global__ void __launch_bounds__(NT) k_place(TickBufs b) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i >= b.m) return;
-    const uint2 cc = b.mcell[i];
+    const uint4 cc = b.mcell[i];
+    if (cc.w) atomicOr(&b.w.flags[flag_word(cc.z)], cc.w << flag_sh(cc.z));   // op i's syncInfoFlag bits
     const uint32_t co = cc.x, cn = cc.y;
     if (co == NO_CELL && cn == NO_CELL) return;             // not a mover, or absent before and after
     MEnt e = b.mtmp[i];
@@ -539,7 +537,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     const int ln = lane_id();
     if (!(me.tags & TAG_PRIMARY)) {
         if (ln == 0) {
-            b.mstat[m] = make_ulonglong2(0, 0);
+            b.mstat[m] = 0;
             b.ownc[m] = 0;
             b.mirc[m] = 0;
         }
@@ -553,7 +551,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             atomicOr(&b.st->overflow, 1ull);
             b.ownc[m] = 0;
             b.mirc[m] = 0;
-            b.mstat[m] = make_ulonglong2(0, 0);
+            b.mstat[m] = 0;
         }
         return;
     }
@@ -570,7 +568,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     uint32_t* out = b.own + reg;
     uint64_t* mir = b.mir + reg;
     uint32_t n = 0, nl = 0, nm_ = 0, nml = 0;
-    uint32_t c_old = 0, c_new = 0, c_band = 0, c_cli = 0;
+    uint32_t c_old = 0, c_new = 0, c_cli = 0;
     Flat f = S.flat(P, R);
     // long ranges (crowded rows): walk the live ranges with readlanes, a chunk
     // overlaps one or two of them; short ones: the shuffle binary search
@@ -632,7 +630,6 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             c_old += (uint32_t)popc64(wave_ballot(t_ro));
             c_new += (uint32_t)popc64(wave_ballot(t_rn));
             c_cli += (uint32_t)popc64(wave_ballot(t_cli));
-            c_band += (uint32_t)popc64(wave_ballot(b_o)) + (uint32_t)popc64(wave_ballot(b_n));
             // B has no op: (B,A) is B's event too (kept in A's region; the
             // events stage places it)
             const bool mev = ev && nmv && owned_x(P, e.x);
@@ -673,7 +670,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             b.big[atomicAdd(&b.st->n_big, 1ull)] = (uint32_t)m;
         }
     }
-    const uint32_t so = c_old, sn = c_new, sb = c_band, scl = c_cli;
+    const uint32_t so = c_old, sn = c_new, scl = c_cli;
     if (ln == 0) {
         b.ownc[m] = (unsigned long long)(n - nl) | ((unsigned long long)nl << 32);
         b.mirc[m] = (unsigned long long)(nm_ - nml) | ((unsigned long long)nml << 32);
@@ -684,7 +681,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
         if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | scl;
         // per-mover statistics, summed by k_mover_post (no atomics here: 2 per
         // mover into 256 shards cost 25 us at config #3 and 180 us at config #4)
-        b.mstat[m] = make_ulonglong2((unsigned long long)so | ((unsigned long long)sn << 32), sb);
+        b.mstat[m] = (unsigned long long)so | ((unsigned long long)sn << 32);
     }
 }
 
@@ -772,7 +769,7 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     uint32_t* out = b.own + reg;
     uint64_t* mir = b.mir + reg;
     uint32_t n = 0, nl = 0, nm_ = 0, nml = 0;
-    uint32_t c_old = 0, c_new = 0, c_band = 0, c_cli = 0;
+    uint32_t c_old = 0, c_new = 0, c_cli = 0;
     for (uint32_t base = 0; base < tmax; base += 32u * HU) {   // wave-uniform
         Cand cc[HU];
 #pragma unroll
@@ -838,7 +835,6 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
             c_old += (uint32_t)popc64(wave_ballot(t_ro) & hmask);
             c_new += (uint32_t)popc64(wave_ballot(t_rn) & hmask);
             c_cli += (uint32_t)popc64(wave_ballot(t_cli) & hmask);
-            c_band += (uint32_t)popc64(wave_ballot(b_o) & hmask) + (uint32_t)popc64(wave_ballot(b_n) & hmask);
             const bool mev = ev && nmv && owned_x(P, e.x);
             ev = ev && ownA;
             const uint64_t be = wave_ballot(ev) & hmask, bl = wave_ballot(ev && lv) & hmask;
@@ -878,7 +874,7 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     if (go && n > 32 && hl == 0) b.big[atomicAdd(&b.st->n_big, 1ull)] = (uint32_t)m;
     if (valid && hl == 0) {
         if (!go) {
-            b.mstat[m] = make_ulonglong2(0, 0);
+            b.mstat[m] = 0;
             b.ownc[m] = 0;
             b.mirc[m] = 0;
         } else {
@@ -889,7 +885,7 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
                 b.gmi[A] = (uint32_t)m;
             }
             if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | c_cli;
-            b.mstat[m] = make_ulonglong2((unsigned long long)c_old | ((unsigned long long)c_new << 32), c_band);
+            b.mstat[m] = (unsigned long long)c_old | ((unsigned long long)c_new << 32);
         }
     }
     return true;
@@ -939,7 +935,7 @@ __global__ void __launch_bounds__(NT) k_mover_small(TickBufs b) {
     }
 }
 
-// A_old | A_new << 32 and band counts of every mover-grid entry, one shard per
+// A_old | A_new << 32 of every mover-grid entry, one shard per
 // block (STAT_SHARDS blocks, so no two blocks add to the same words)
 // Blocks [0, STAT_SHARDS) sum the statistics; the others block-sort the own
 // events of movers with too many for LDS (k_mover listed them in big[]): one
@@ -957,23 +953,19 @@ __global__ void __launch_bounds__(NT) k_mover_post(TickBufs b) {
         }
         return;
     }
-    __shared__ unsigned long long red[2][NWAVE];
+    __shared__ unsigned long long red[NWAVE];
     const uint64_t n = b.st->n_gm;
-    unsigned long long a = 0, c = 0;
+    unsigned long long a = 0;
     for (uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x; m < n; m += (uint64_t)STAT_SHARDS * NT) {
-        const ulonglong2 v = b.mstat[m];
-        a += v.x;
-        c += v.y;
+        a += b.mstat[m];
     }
     a = wave_sum<unsigned long long>(a);
-    c = wave_sum<unsigned long long>(c);
-    if (lane_id() == 0) { red[0][threadIdx.x >> 6] = a; red[1][threadIdx.x >> 6] = c; }
+    if (lane_id() == 0) red[threadIdx.x >> 6] = a;
     __syncthreads();
     if (threadIdx.x == 0) {
-        a = c = 0;
-        for (int i = 0; i < NWAVE; ++i) { a += red[0][i]; c += red[1][i]; }
+        a = 0;
+        for (int i = 0; i < NWAVE; ++i) a += red[i];
         shard_add(b.st, blockIdx.x, SH_AOLD, a);
-        shard_add(b.st, blockIdx.x, SH_BAND, c);
     }
 }
 
@@ -1647,9 +1639,9 @@ __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
 // quantiles of this tick's sorted (leave, watcher) keys: the next tick's
 // bucket bounds (BK_NSPLIT of them; a tick with fewer buckets takes every
 // (BK_NSPLIT / NB)-th).  Kept when the tick overflowed or had no events.
-__device__ __forceinline__ void bk_split_next(const TickBufs& b) {
-    const uint64_t E = lo32(b.st->ev_pk) + hi32(b.st->ev_pk), ne = lo32(b.st->ev_pk);
-    if (E == 0 || E > b.ev_cap || b.st->overflow) return;
+__device__ __forceinline__ void bk_split_next(const TickBufs& b, const ResetArgs& r) {
+    const uint64_t E = lo32(r.ev_pk) + hi32(r.ev_pk), ne = lo32(r.ev_pk);
+    if (E == 0 || E > b.ev_cap || r.overflow) return;
     const uint32_t lvb = 1u << b.wbits;
     for (uint32_t j = 1 + blockIdx.x * NT + threadIdx.x; j < BK_NSPLIT; j += gridDim.x * NT) {   // 1 per thread
         const uint64_t p = (uint64_t)j * E / BK_NSPLIT;
@@ -1723,19 +1715,17 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
 // after the tick: per-op dedupe state of every op's slot back to -1 (thread
 // i: op i); MOVER bits cleared at the movers' new grid entries (thread i:
 // mover-grid entry i)
-__global__ void __launch_bounds__(NT) k_tick_reset(TickBufs b) {
+// The tick's counters come by value (read by the host already), so block 0
+// can zero the device statistics for the next tick (no reset copy at its
+// start).
+__global__ void __launch_bounds__(NT) k_tick_reset(TickBufs b, ResetArgs r) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
-    bk_split_next(b);                        // the next tick's bucket bounds (its own launch cost 5-8 us)
-    if (i < b.m) {
-        const uint32_t s = b.ops[i].slot;
-        if (s < b.w.cap) {
-            OpLast z;
-            z.pos = z.aoi = z.leave = z.pad0 = -1;
-            z.clr[0] = z.clr[1] = z.pad1[0] = z.pad1[1] = -1;
-            b.ol[s] = z;
-        }
+    bk_split_next(b, r);                     // the next tick's bucket bounds (its own launch cost 5-8 us)
+    if (blockIdx.x == 0) {
+        unsigned long long* z = (unsigned long long*)b.st;
+        for (uint32_t k = threadIdx.x; k < sizeof(DevStats) / 8; k += NT) z[k] = 0;
     }
-    if (i < b.st->n_gm) {
+    if (i < r.n_gm) {
         const MEnt e = b.gm[i];
         if (e.tags & TAG_NEW) {                 // the new grid (b.w after the tick)
             const uint32_t c = cell_of(b.w.sp[e.space], e.x, e.z);
@@ -1743,8 +1733,8 @@ __global__ void __launch_bounds__(NT) k_tick_reset(TickBufs b) {
         }
     }
 }
-void tick_reset(const TickBufs& b, hipStream_t s) {
-    hipLaunchKernelGGL(k_tick_reset, dim3(nblk1(2ull * b.m, NT)), dim3(NT), 0, s, b);
+void tick_reset(const TickBufs& b, const ResetArgs& r, hipStream_t s) {
+    hipLaunchKernelGGL(k_tick_reset, dim3(nblk1(2ull * b.m, NT)), dim3(NT), 0, s, b, r);
 }
 
 }  // namespace gw

@@ -80,6 +80,17 @@ int ensure_host(gw_ctx* c, DevBuf& b, size_t bytes) {
     return 0;
 }
 
+// a new op-dedupe session (OpLast words are tagged with it; after 2^32 - 1
+// sessions the records are zeroed once and the tags restart)
+int next_ol_tag(gw_ctx* c, uint32_t* tag) {
+    if (++c->ol_tag == 0) {
+        if (c->ol && c->slot_cap) HIPCHK(hipMemsetAsync(c->ol, 0, (size_t)c->slot_cap * sizeof(OpLast), c->st));
+        c->ol_tag = 1;
+    }
+    *tag = c->ol_tag;
+    return 0;
+}
+
 }  // namespace host
 }  // namespace gw
 
@@ -205,7 +216,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->gmi, 0, (size_t)nc))) return rc;
     if ((rc = grow_preserve(c, c->eid_dev, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->cid_dev, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->ol, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->ol, oc, nc))) return rc;     // new records: zero (session 0 is never used)
     if ((rc = grow_preserve(c, c->rflag, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->gnb[0], 0, nc))) return rc;    // rebuilt (grid_dirty)
     if ((rc = grow_preserve(c, c->gnb[1], 0, nc))) return rc;
@@ -222,7 +233,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     HIPCHK(hipMemsetAsync(c->movbit, 0, ((size_t)nc / 32 + 1) * 4, c->st));
     HIPCHK(hipMemsetAsync(c->eid_dev + oc, 0, n * 16, c->st));
     HIPCHK(hipMemsetAsync(c->cid_dev + oc, 0, n * 16, c->st));
-    launch_fill_i32((int32_t*)(c->ol + oc), -1, n * (sizeof(OpLast) / 4), c->st);
+    HIPCHK(hipMemsetAsync(c->ol + oc, 0, n * sizeof(OpLast), c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     c->slot_cap = nc;
     c->present_h.resize(nc, 0);
@@ -343,6 +354,7 @@ int rebuild_grid(gw_ctx* c) {
     if ((rc = radix_tmp(c, C, rt))) return rc;
     reset_stats_host(c);
     HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
+    c->stats_zero = false;
     if (C)
         grid_rebuild(world(c), c->stats, P<uint32_t>(c->k0), P<uint32_t>(c->v0), P<uint32_t>(c->k1),
                      P<uint32_t>(c->v1), rt, ceil_log2((uint64_t)c->total_cells + 1), c->st);
@@ -423,6 +435,7 @@ int gw_init(int device_id, gw_ctx** out) {
         (void)hipMemset(c->sc.ticket, 0, 8);
         memset(c->hstats, 0, sizeof(DevStats));
         (void)hipMemset(c->stats, 0, sizeof(DevStats));
+        (void)hipMemset(c->cstats, 0, sizeof(DevStats));
         (void)hipEventCreate(&c->ev_t0);
         (void)hipEventCreate(&c->ev_t1);
         if (const char* e = getenv("GW_CELLS_PER_D")) c->cells_per_d = std::min(4, std::max(1, atoi(e)));
@@ -639,8 +652,11 @@ int gw_route_halo(gw_ctx* c, const gw_op* dev_ops, const uint64_t* dev_stamps, u
     }
     if (!c->total_slots) return set_err(c, GW_EINVAL, "no space");
     // n == 0 still runs: the buffers must become all NOPs
-    launch_route_halo(world(c), dev_ops, (const unsigned long long*)dev_stamps, n, max_step, D, c->ol, c->rflag,
-                      c->halo, c->st);
+    int rc;
+    uint32_t tag = 0;
+    if ((rc = next_ol_tag(c, &tag))) return rc;
+    launch_route_halo(world(c), dev_ops, (const unsigned long long*)dev_stamps, n, max_step, D, c->ol, tag,
+                      c->rflag, c->halo, c->st);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -805,7 +821,11 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         if ((rc = read_stats(c))) return rc;
     }
     prof_begin(c, "reset");
-    tick_reset(b, c->st);                            // asynchronous: the next call orders behind it
+    {                                                // asynchronous: the next call orders behind it
+        const DevStats& h = *c->hstats;
+        tick_reset(b, ResetArgs{h.n_gm, h.ev_pk, h.overflow}, c->st);
+        c->stats_zero = true;                        // the reset zeroed the device statistics
+    }
     prof_end(c, (uint64_t)M * 24);
     HIPCHK(hipEventRecord(c->ev_t1, c->st));
     HIPCHK(hipGetLastError());
@@ -970,10 +990,10 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         c->ev_cap = std::max<uint64_t>(c->ev_cap, 48ull * M + 4096);
     }
     if ((rc = ensure(c, c->gm, M2 * sizeof(MEnt))) || (rc = ensure(c, c->mtmp, (size_t)M * sizeof(MEnt))) ||
-        (rc = ensure(c, c->mcell, (size_t)M * 8)) ||
+        (rc = ensure(c, c->mcell, (size_t)M * 16)) ||
         (rc = ensure(c, c->cand, M2 * 8)) || (rc = ensure(c, c->reg, M2 * 8)) ||
         (rc = ensure(c, c->ownc, M2 * 8)) || (rc = ensure(c, c->mirc, M2 * 8)) || (rc = ensure(c, c->big, M2 * 4)) ||
-        (rc = ensure(c, c->mstat, M2 * 16)) ||
+        (rc = ensure(c, c->mstat, M2 * 8)) ||
         (rc = ensure(c, c->mlist, (size_t)M * 4)) || (rc = ensure(c, c->mcnt, (size_t)M * 8)) ||
         (rc = ensure(c, c->moff, (size_t)M * 8)) || (rc = ensure(c, c->minfo, (size_t)M * 16)) ||
         (rc = ensure(c, c->mreg, (size_t)M * 8)) || (rc = ensure(c, c->icnt, (size_t)M * 4)) ||
@@ -982,12 +1002,25 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         return rc;
     if ((rc = ensure_events(c))) return rc;
     reset_stats_host(c);
-    HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
+    if (!c->stats_zero)                              // else the last tick's reset pass zeroed them
+        HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
+    c->stats_zero = false;
     DevStats* st = c->stats;
 
     TickBufs b{};
     b.w = world(c);
     b.ops = ops; b.m = M; b.stamp_base = c->stamp_base;
+    b.ol_tag = 0;
+    if (c->wd.ol_pre) {                               // the world's routing deduped its ops already
+        const uint32_t k = c->wd.ol_pre;
+        c->wd.ol_pre = 0;
+        const OpSeg& s0 = c->segs[0];
+        if (!s0.host && !s0.rows && s0.dev == c->wd.ops && s0.n == k) {
+            b.op0 = k;                                // same session: its dedupe words are this tick's
+            b.ol_tag = c->wd.kept_tag;
+        }
+    }
+    if (!b.ol_tag && (rc = next_ol_tag(c, &b.ol_tag))) return rc;
     b.stamps = stamps;
     b.diff_u = c->diff_u;
     b.walk_min = c->walk_min;
@@ -997,11 +1030,11 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.gn_nxt = c->gnb[c->gcur ^ 1]; b.start_nxt = c->gsb[c->gcur ^ 1];
     b.dep = c->dep; b.arr = c->arr; b.cnt_new = c->cnt_new; b.bigcell = c->bigcell;
     b.gm_cnt = c->gm_cnt; b.gm_start = c->gm_start; b.gm = P<MEnt>(c->gm);
-    b.mtmp = P<MEnt>(c->mtmp); b.mcell = P<uint2>(c->mcell);
+    b.mtmp = P<MEnt>(c->mtmp); b.mcell = P<uint4>(c->mcell);
     b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg);
     b.ownc = P<unsigned long long>(c->ownc); b.mirc = P<unsigned long long>(c->mirc);
     b.big = P<uint32_t>(c->big);
-    b.mstat = P<ulonglong2>(c->mstat);
+    b.mstat = P<unsigned long long>(c->mstat);
     b.movbit = c->movbit; b.gmi = c->gmi;
     b.mlist = P<uint32_t>(c->mlist);
     b.mcnt = P<unsigned long long>(c->mcnt); b.moff = P<unsigned long long>(c->moff);
@@ -1072,9 +1105,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     }
     if (c->grid_dirty && (rc = settle(c))) return rc;
     if ((rc = rebuild_grid(c))) return rc;
-    memset(c->hcstats, 0, sizeof(DevStats));
-    HIPCHK(hipMemcpyAsync(c->cstats, c->hcstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
-    DevStats* st = c->cstats;
+    DevStats* st = c->cstats;                        // its overflow flag is zeroed by the compaction
     if ((rc = ensure(c, c->fbits, (size_t)C * 4)) || (rc = ensure(c, c->flagged, (size_t)C * 4)) ||
         (rc = ensure(c, c->rec_cnt, (size_t)C * 4)) || (rc = ensure(c, c->rec_off, (size_t)C * 8)) ||
         (rc = ensure_scan(c, C)))
@@ -1089,8 +1120,8 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     const uint32_t NFM = (uint32_t)std::min<uint64_t>(C, std::max<uint64_t>(c->flag_bound, 1));
     c->flag_bound = 0;
     prof_begin(c, "sync_flagged");
-    launch_flag_compact(c->flags, C, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), c->sc, (uint32_t*)&st->flagged,
-                        c->st);
+    launch_flag_compact(c->flags, C, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), c->sc, &st->flagged,
+                        &st->overflow, c->st);
     prof_end(c, (uint64_t)C * 4 * 2);
     const uint64_t* nf = (const uint64_t*)&st->flagged;
     prof_begin(c, "sync_count");

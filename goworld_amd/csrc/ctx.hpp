@@ -57,6 +57,9 @@ struct WorldHost {
     const gw_op* ops = nullptr;     // this tick's owned ops (caller's device memory)
     uint32_t n_ops = 0;
     bool routed = false;
+    uint32_t kept = 0;              // routed ops whose dedupe session (k_route1 = k_ops1) the tick ...
+    uint32_t ol_pre = 0;            // ... reuses once submitted: the next tick's first ol_pre ops (gw_tick)
+    uint32_t kept_tag = 0;          // that session
 };
 
 // a 16-byte EntityID as a hash-map key
@@ -119,7 +122,8 @@ struct gw_ctx {
     unsigned long long* nbc = nullptr;       // [slot_cap] epoch<<32 | neighbours with a client
     uint32_t* movbit = nullptr;              // [slot_cap/32 + 1] movers of the tick, zero between ticks
     uint32_t* gmi = nullptr;                 // [slot_cap] primary mover-grid entry of a mover
-    gw::OpLast* ol = nullptr;                // [slot_cap] per-op dedupe state, -1 between ticks
+    gw::OpLast* ol = nullptr;                // [slot_cap] per-op dedupe state (session-tagged words)
+    uint32_t ol_tag = 0;                     // last dedupe session handed out (next_ol_tag)
     uint32_t* rflag = nullptr;                // [slot_cap] halo routing scratch, zero between calls
     HaloStats* halo = nullptr;                // halo routing counters (device)
     GEnt* gnb[2] = {nullptr, nullptr};   // grid ping-pong (gnb[gcur] is current)
@@ -133,6 +137,7 @@ struct gw_ctx {
     uint32_t sp_cap = 0;
 
     DevStats* stats = nullptr;     // device (grid rebuild, tick)
+    bool stats_zero = true;        // stats is all zero (the last tick's reset pass, or init)
     DevStats* hstats = nullptr;    // pinned host
     DevStats* cstats = nullptr;    // device (collect: a deferred tick's stats stay intact)
     DevStats* hcstats = nullptr;   // pinned host
@@ -218,6 +223,7 @@ int set_err(gw_ctx* c, int code, const char* fmt, ...);
 int ensure(gw_ctx* c, DevBuf& b, size_t bytes);
 int ensure_host(gw_ctx* c, DevBuf& b, size_t bytes);
 int settle(gw_ctx* c);
+int next_ol_tag(gw_ctx* c, uint32_t* tag);
 World world_of(gw_ctx* c);
 template <typename T>
 T* P(DevBuf& b) { return (T*)b.p; }

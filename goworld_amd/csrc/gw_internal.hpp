@@ -35,15 +35,22 @@ struct alignas(16) PrevEnt {
     unsigned long long ostamp;
 };
 
-// Per-slot op dedupe state of one tick, one 32-B record (a tick's op touches
-// one line for all of it): the index of the slot's last op that sets the sync
-// payload (non-Leave), its last AOI op, its last Leave, and per sync bit the
-// last Leave that cleared it; -1 between ticks.
-struct alignas(32) OpLast {
-    int32_t pos, aoi, leave, pad0;
-    int32_t clr[2];
-    int32_t pad1[2];
+// Per-slot op dedupe state, one 64-B record (a tick's op touches one line for
+// all of it): the index of the slot's last op that sets the sync payload
+// (non-Leave), its last AOI op, its last Leave, and per sync bit the last
+// Leave that cleared it.  Each word is tag << 32 | op index, tag = the dedupe
+// session (a tick, or a routing call whose tick reuses it); u64 atomicMax
+// lets a newer session's index replace an older one and a word of an older
+// session reads as -1 (ol_get), so nothing is reset between ticks.
+struct alignas(64) OpLast {
+    unsigned long long pos, aoi, leave, clr[2], pad[3];
 };
+__device__ __forceinline__ unsigned long long ol_put(uint32_t tag, uint32_t i) {
+    return ((unsigned long long)tag << 32) | i;
+}
+__device__ __forceinline__ int32_t ol_get(unsigned long long v, uint32_t tag) {
+    return (uint32_t)(v >> 32) == tag ? (int32_t)(uint32_t)v : -1;
+}
 
 // Entry of the grid (cell-sorted, slot order inside a cell), 16 B.
 struct alignas(16) GEnt {
@@ -87,7 +94,6 @@ constexpr int STAT_SHARDS = 256;
 constexpr int SH_FIELDS = 4;
 constexpr int SH_MOVERS = 0;  // distinct slots with an AOI op (k_ops3)
 constexpr int SH_AOLD = 1;    // a_old | a_new << 32 (per-shard sums stay below 2^32)
-constexpr int SH_BAND = 3;
 
 // Device-side counters of one tick / collect (read back once per call).
 struct DevStats {
@@ -167,8 +173,10 @@ struct TickBufs {
     const gw_op* ops;
     const unsigned long long* stamps;   // explicit global stamps (nullptr: stamp_base + index)
     uint32_t m;               // ops in the stream
+    uint32_t op0;             // ops [0, op0) were deduped into ol by the world's routing (k_ops1 starts here)
     unsigned long long stamp_base;
-    OpLast* ol;               // [cap] per-slot op dedupe state of the tick (-1 between ticks)
+    OpLast* ol;               // [cap] per-slot op dedupe state (words of this tick's session ol_tag)
+    uint32_t ol_tag;          // the tick's dedupe session
     DevStats* st;
     // incremental grid: gn -> gn_nxt
     GEnt* gn_nxt;             // [cap]
@@ -182,7 +190,7 @@ struct TickBufs {
     uint32_t* gm_start;       // [ncells+1]
     MEnt* gm;                 // [2m]
     MEnt* mtmp;               // [m] op i's mover-grid entry (tags aside) when op i is a mover (k_ops3 -> k_place)
-    uint2* mcell;             // [m] its old / new cell (NO_CELL: none), NO_CELL twice for other ops
+    uint4* mcell;             // [m] op i: old / new cell of its mover (NO_CELL: none), slot, syncInfoFlag bits to OR
     // diff (indexed by mover-grid entry)
     uint64_t* cand;           // [2m] candidate bound (0 unless TAG_PRIMARY)
     uint64_t* reg;            // [2m] exclusive scan of cand
@@ -191,7 +199,7 @@ struct TickBufs {
     uint64_t* mir;            // mirror events of op-less neighbours: watcher<<32 | mover<<1 | leave
     unsigned long long* ownc; // [2m] own enters | leaves<<32 per entry
     unsigned long long* mirc; // [2m] mirror enters | leaves<<32 per entry
-    ulonglong2* mstat;        // [2m] A_old | A_new << 32, band count per entry (k_mover -> k_mover_stats)
+    unsigned long long* mstat;   // [2m] A_old | A_new << 32 per entry (k_mover -> k_mover_post)
     uint32_t* big;            // [2m] entries whose own events need the block sort
     // canonical events: movers in slot order, their events flattened, one
     // stable radix sort by (leave, watcher) -> (watcher, target) order
@@ -256,7 +264,11 @@ void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s);     // gn -> gn_n
 void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s);   // b.w: the new grid
 void tick_diff(const TickBufs& b, hipStream_t s);                  // own + mirror events per mover
 void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s);   // canonical event arrays
-void tick_reset(const TickBufs& b, hipStream_t s);                 // after the host read the counts
+// after the host read the counts (given by value); zeroes the tick's DevStats
+struct ResetArgs {
+    unsigned long long n_gm, ev_pk, overflow;
+};
+void tick_reset(const TickBufs& b, const ResetArgs& r, hipStream_t s);
 
 void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n, bool grid_ok,
                         hipStream_t s);
@@ -269,8 +281,10 @@ void launch_sync_write_small(const World& w, uint32_t n_spaces, const uint32_t* 
                              uint32_t max_cells, hipStream_t s);
 // small-space mode: every space's grid (entries + row starts) in this many LDS bytes at most
 constexpr size_t SMALL_LDS_MAX = 48 * 1024;
+// also zeroes *ovf, the write passes' overflow flag (the collect's only
+// accumulated counter: no reset copy of the collect's DevStats)
 void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint32_t* fbits, ScanCtx& sc,
-                         uint32_t* total, hipStream_t s);
+                         unsigned long long* total, unsigned long long* ovf, hipStream_t s);
 void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, uint32_t* cnt, hipStream_t s);
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
@@ -300,9 +314,10 @@ struct HaloDsts {
     HaloDst d[2];
     uint32_t n;
 };
+// ol_tag: the routing's dedupe session (a tick that reuses it passes the same tag)
 void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
-                       float max_step, const HaloDsts& D, OpLast* ol, uint32_t* rflag, HaloStats* hs, hipStream_t s,
-                       bool pad = true);
+                       float max_step, const HaloDsts& D, OpLast* ol, uint32_t ol_tag, uint32_t* rflag, HaloStats* hs,
+                       hipStream_t s, bool pad = true);
 void launch_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n, hipStream_t s);
 void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,
                        hipStream_t s);

@@ -8,7 +8,7 @@
 //   r1  last AOI op / last payload op / last Leave per slot (atomicMax, as
 //       k_ops1 of the tick; the same per-slot arrays, left at -1 after r4)
 //   r2  OR of the sync bits of the ops after the last Leave clearing each bit
-//       (atomicOr; a Leave's sync_flags is the mask of bits it keeps, k_ops2)
+//       (atomicOr; a Leave's sync_flags is the mask of bits it keeps, as the tick)
 //   r3  the entity's last op writes up to 3 rows per destination, entities
 //       placed by one wave-aggregated atomic per wave and destination
 //   r4  reset of the per-slot scratch; zero (NOP) rows past the entities
@@ -29,7 +29,7 @@ __device__ __forceinline__ bool op_valid(const gw_op& op, uint32_t cap) {
 }
 
 __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
-                                                OpLast* ol, HaloStats* hs) {
+                                                OpLast* ol, uint32_t tag, HaloStats* hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i == 0) hs->cnt[0] = hs->cnt[1] = 0;         // placement counters of this call
     if (i >= n) return;
@@ -39,24 +39,25 @@ __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, ui
         atomicAdd(&hs->bad_ops, 1ull);
         return;
     }
-    if (op.kind != GW_OP_LEAVE) atomicMax(&ol[op.slot].pos, (int32_t)i);
-    if (op.kind != GW_OP_SYNC) atomicMax(&ol[op.slot].aoi, (int32_t)i);
+    const unsigned long long v = ol_put(tag, i);
+    if (op.kind != GW_OP_LEAVE) atomicMax(&ol[op.slot].pos, v);
+    if (op.kind != GW_OP_SYNC) atomicMax(&ol[op.slot].aoi, v);
     if (op.kind == GW_OP_LEAVE) {
-        atomicMax(&ol[op.slot].leave, (int32_t)i);
+        atomicMax(&ol[op.slot].leave, v);
         for (int c = 0; c < 2; ++c)
-            if (!((op.sync_flags >> c) & 1)) atomicMax(&ol[op.slot].clr[c], (int32_t)i);
+            if (!((op.sync_flags >> c) & 1)) atomicMax(&ol[op.slot].clr[c], v);
     }
 }
 
 __global__ void __launch_bounds__(NT) k_route2(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
-                                                const OpLast* __restrict__ ol, uint32_t* rflag) {
+                                                const OpLast* __restrict__ ol, uint32_t tag, uint32_t* rflag) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
     const gw_op op = ops[i];
     if (!op_valid(op, cap) || op.kind == GW_OP_LEAVE || !(op.sync_flags & SIF_ROUTED)) return;
     uint32_t bits = 0;
     for (int c = 0; c < 2; ++c)
-        if (((op.sync_flags >> c) & 1) && (int32_t)i > ol[op.slot].clr[c]) bits |= 1u << c;
+        if (((op.sync_flags >> c) & 1) && (int32_t)i > ol_get(ol[op.slot].clr[c], tag)) bits |= 1u << c;
     if (bits) atomicOr(&rflag[op.slot], bits);
 }
 
@@ -80,7 +81,7 @@ __device__ __forceinline__ void put_row(gw_halo_row* r, const gw_op& o, unsigned
 }
 
 __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, const unsigned long long* __restrict__ stamps,
-                                                uint32_t n, World w, const OpLast* __restrict__ ol,
+                                                uint32_t n, World w, const OpLast* __restrict__ ol, uint32_t tag,
                                                 const uint32_t* __restrict__ rflag, float max_step, HaloDsts D,
                                                 HaloStats* hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
@@ -92,9 +93,9 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
         const gw_op op = ops[i];
         if (op_valid(op, w.cap)) {
             s = op.slot;
-            la = ol[s].aoi;
-            ll = ol[s].leave;
-            lp = ol[s].pos;
+            la = ol_get(ol[s].aoi, tag);
+            ll = ol_get(ol[s].leave, tag);
+            lp = ol_get(ol[s].pos, tag);
             rep = (int32_t)i == max(lp, ll);          // the entity's last op
         }
     }
@@ -115,11 +116,11 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
             if (old_p && new_p && fabsf(new_x - old_x) > max_step) atomicAdd(&hs->bad_moves, 1ull);
         }
         if (lp >= 0) op_pos = ops[lp];
-        // syncInfoFlag after the tick's ops (k_ops2 / k_ops3): old bits a Leave
+        // syncInfoFlag after the tick's ops (k_ops3 / k_place): old bits a Leave
         // did not clear, OR'd with the bits set since the Leave that cleared them
         uint32_t keep = 0;
         for (int c = 0; c < 2; ++c)
-            if (ol[s].clr[c] < 0) keep |= 1u << c;
+            if (ol_get(ol[s].clr[c], tag) < 0) keep |= 1u << c;
         f = ((flag_get(w.flags, s) & keep) | rflag[s]) & SIF_ROUTED;
     }
     for (uint32_t d = 0; d < D.n; ++d) {
@@ -158,8 +159,7 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
 }
 
 __global__ void __launch_bounds__(NT) k_route4(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
-                                                OpLast* ol, uint32_t* rflag, HaloDsts D,
-                                                const HaloStats* __restrict__ hs) {
+                                                uint32_t* rflag, HaloDsts D, const HaloStats* __restrict__ hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     // rows past the placed entities become NOPs (thread i: row i of each buffer)
     for (uint32_t d = 0; d < D.n; ++d) {
@@ -168,12 +168,7 @@ __global__ void __launch_bounds__(NT) k_route4(const gw_op* __restrict__ ops, ui
     }
     if (i >= n) return;
     const gw_op op = ops[i];
-    if (!op_valid(op, cap)) return;
-    OpLast z;
-    z.pos = z.aoi = z.leave = z.pad0 = -1;
-    z.clr[0] = z.clr[1] = z.pad1[0] = z.pad1[1] = -1;
-    ol[op.slot] = z;
-    rflag[op.slot] = 0;
+    if (op_valid(op, cap)) rflag[op.slot] = 0;     // (the dedupe words age out with their session tag)
 }
 
 __global__ void __launch_bounds__(NT) k_split_rows(const gw_halo_row* __restrict__ rows, uint32_t n,
@@ -187,17 +182,17 @@ __global__ void __launch_bounds__(NT) k_split_rows(const gw_halo_row* __restrict
 }  // namespace
 
 void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
-                       float max_step, const HaloDsts& D, OpLast* ol, uint32_t* rflag, HaloStats* hs, hipStream_t s,
-                       bool pad) {
+                       float max_step, const HaloDsts& D, OpLast* ol, uint32_t ol_tag, uint32_t* rflag, HaloStats* hs,
+                       hipStream_t s, bool pad) {
     const uint32_t nb = nblk1(n, NT);
     uint64_t rows = 0;                                   // NOP padding up to the capacity (fixed-size exchanges)
     if (pad)
         for (uint32_t d = 0; d < D.n; ++d) rows = std::max<uint64_t>(rows, (uint64_t)D.d[d].cap * ROWS);
-    hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, hs);
-    hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, rflag);
-    hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, ol, rflag, max_step, D, hs);
+    hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, ol_tag, hs);
+    hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, ol_tag, rflag);
+    hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, ol, ol_tag, rflag, max_step, D, hs);
     hipLaunchKernelGGL(k_route4, dim3(nblk1(std::max<uint64_t>(n, rows), NT)), dim3(NT), 0, s, ops, n, w.cap,
-                       ol, rflag, D, hs);
+                       rflag, D, hs);
 }
 
 __global__ void __launch_bounds__(NT) k_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n) {

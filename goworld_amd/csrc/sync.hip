@@ -67,9 +67,11 @@ __global__ void __launch_bounds__(NT) k_flag_compact1(uint32_t* __restrict__ fla
                                                       uint32_t* __restrict__ flagged, uint32_t* __restrict__ fbits,
                                                       unsigned long long* __restrict__ status,
                                                       unsigned long long* __restrict__ ticket,
-                                                      unsigned long long tbase, uint32_t tag, uint32_t* total) {
+                                                      unsigned long long tbase, uint32_t tag,
+                                                      unsigned long long* total, unsigned long long* ovf) {
     __shared__ uint32_t lds[IPT * NWAVE];
     __shared__ uint32_t s_tile, s_prefix;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ovf = 0;
     if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tbase);
     __syncthreads();
     const uint32_t tile = s_tile;
@@ -104,11 +106,11 @@ __global__ void __launch_bounds__(NT) k_flag_compact1(uint32_t* __restrict__ fla
             flags[i] = 0;
         }
     }
-    if (tile == gridDim.x - 1 && threadIdx.x == 0) *total = pre + tot;
+    if (tile == gridDim.x - 1 && threadIdx.x == 0) *total = pre + tot;   // all 64 bits (no reset copy)
 }
 
 void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint32_t* fbits, ScanCtx& sc,
-                         uint32_t* total, hipStream_t s) {
+                         unsigned long long* total, unsigned long long* ovf, hipStream_t s) {
     const uint32_t nwords = (cap + 15) / 16;
     const bool big = nwords > SCAN_BIG;
     const uint64_t tile = big ? 2 * SCAN_TILE : SCAN_TILE;
@@ -121,10 +123,10 @@ void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint3
     ++sc.tag;
     if (big)
         hipLaunchKernelGGL(k_flag_compact1<2 * SCAN_IPT>, dim3(nb), dim3(NT), 0, s, flags, nwords, flagged, fbits,
-                           sc.status, sc.ticket, sc.tbase, sc.tag, total);
+                           sc.status, sc.ticket, sc.tbase, sc.tag, total, ovf);
     else
         hipLaunchKernelGGL(k_flag_compact1<SCAN_IPT>, dim3(nb), dim3(NT), 0, s, flags, nwords, flagged, fbits,
-                           sc.status, sc.ticket, sc.tbase, sc.tag, total);
+                           sc.status, sc.ticket, sc.tbase, sc.tag, total, ovf);
     sc.tbase += nb;
 }
 

@@ -153,6 +153,7 @@ int gw_world_route(gw_ctx* c, const gw_op* ops, uint32_t n, const gw_halo_row* s
     WorldHost& W = c->wd;
     if (!W.on) return set_err(c, GW_ESTATE, "no world strip (gw_world_create)");
     if (W.routed) return set_err(c, GW_ESTATE, "tick already routed: gw_world_submit first");
+    if (W.ol_pre) return set_err(c, GW_ESTATE, "the last routed world tick was not ticked (gw_tick first)");
     if ((uint64_t)n >= STAMP_STRIDE) return set_err(c, GW_ERANGE, "too many ops in one tick for the stamp layout");
     if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
@@ -167,9 +168,13 @@ int gw_world_route(gw_ctx* c, const gw_op* ops, uint32_t n, const gw_halo_row* s
     }
     const unsigned long long base = 1 + (W.tick * W.g.ranks + W.g.rank) * STAMP_STRIDE;
     launch_iota_u64(P<unsigned long long>(W.stamps), base, n, c->st);
-    launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->ol, c->rflag,
-                      c->halo, c->st, /*pad=*/false);
+    uint32_t tag = 0;
+    if ((rc = next_ol_tag(c, &tag))) return rc;      // the tick reuses this session (gw_world_submit)
+    launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->ol, tag,
+                      c->rflag, c->halo, c->st, /*pad=*/false);
     HIPCHK(hipGetLastError());
+    W.kept = n;
+    W.kept_tag = tag;
     HaloStats hs{};
     HIPCHK(hipMemcpyAsync(&hs, c->halo, sizeof hs, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
@@ -195,7 +200,12 @@ int gw_world_submit(gw_ctx* c, const gw_halo_row* const recv[2], const uint32_t 
     if (!W.routed) return set_err(c, GW_ESTATE, "gw_world_route first");
     W.routed = false;
     ++W.tick;
-    if (int rc = gw_submit_device_stamped(c, W.ops, (const uint64_t*)W.stamps.p, W.n_ops)) return rc;
+    if (int rc = gw_submit_device_stamped(c, W.ops, (const uint64_t*)W.stamps.p, W.n_ops)) {
+        W.kept = 0;                                   // (the session's words age out)
+        return rc;
+    }
+    W.ol_pre = W.kept;                   // the tick's stream starts with the routed ops (gw_tick checks)
+    W.kept = 0;
     for (int side = 0; side < 2; ++side) {
         const uint32_t nr = recv_rows ? recv_rows[side] : 0;
         if (!nr) continue;
@@ -209,6 +219,7 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
     if (!c) return GW_EINVAL;
     WorldHost& W = c->wd;
     if (!W.on) return set_err(c, GW_ESTATE, "no world strip (gw_world_create)");
+    if (W.ol_pre) return set_err(c, GW_ESTATE, "the last routed world tick was not ticked (gw_tick first)");
     const bool any_nb = W.nb[0] >= 0 || W.nb[1] >= 0;
     if (any_nb && (!c->comm || c->c_nranks != (int)W.g.ranks || c->c_rank != (int)W.g.rank))
         return set_err(c, GW_ESTATE, "world of %u ranks needs a matching communicator (gw_comm_init)", W.g.ranks);
@@ -226,9 +237,14 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
     }
     const unsigned long long base = 1 + (W.tick * W.g.ranks + W.g.rank) * STAMP_STRIDE;
     launch_iota_u64(P<unsigned long long>(W.stamps), base, n, c->st);
-    if (D.n)                                          // a one-strip world has nobody to route to
-        launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->ol,
+    if (D.n) {                                        // a one-strip world has nobody to route to
+        uint32_t tag = 0;
+        if ((rc = next_ol_tag(c, &tag))) return rc;  // the tick reuses this session (gw_world_submit)
+        launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->ol, tag,
                           c->rflag, c->halo, c->st, /*pad=*/false);
+        W.kept = n;
+        W.kept_tag = tag;
+    }
     HIPCHK(hipGetLastError());
     uint32_t rcnt[2] = {0, 0};
     if (any_nb) {

@@ -425,11 +425,10 @@ __global__ void __launch_bounds__(NT) k_grid_bigcell(TickBufs b) {
 void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint32_t NC = b.w.ncells;
     hipLaunchKernelGGL(k_cellcnt, dim3(nblk1((uint64_t)NC + 1, NT)), dim3(NT), 0, s, b);
-    // totals land in the low words of the (zeroed, little-endian) 64-bit counters
-    scan_exclusive<uint32_t, uint32_t>(b.cnt_new, b.start_nxt, (uint64_t)NC + 1, nullptr, sc,
-                                       (uint32_t*)&b.st->n_present, s);
-    scan_exclusive<uint32_t, uint32_t>(b.gm_cnt, b.gm_start, (uint64_t)NC + 1, nullptr, sc,
-                                       (uint32_t*)&b.st->n_gm, s);
+    // both cell scans in one launch; totals land in the low words of the
+    // (zeroed, little-endian) 64-bit counters
+    scan_pair32(b.cnt_new, b.gm_cnt, b.start_nxt, b.gm_start, (uint64_t)NC + 1, sc, (uint32_t*)&b.st->n_present,
+                (uint32_t*)&b.st->n_gm, s);
     hipLaunchKernelGGL(k_place, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_grid_copy, dim3(std::min<uint32_t>(nblk1(b.w.cap, NT), 16384)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_grid_dirty, dim3(nblk1((uint64_t)NC, DIRTY_SPAN * NWAVE)), dim3(NT), 0, s, b);
@@ -953,19 +952,24 @@ __global__ void __launch_bounds__(NT) k_mover_post(TickBufs b) {
         }
         return;
     }
-    __shared__ unsigned long long red[NWAVE];
+    // A_old | A_new << 32 into this block's shard; the tick's enters | leaves
+    // << 32 (own + mirror events of every entry) into ev_pk, one add per block
+    __shared__ unsigned long long red[2][NWAVE];
     const uint64_t n = b.st->n_gm;
-    unsigned long long a = 0;
+    unsigned long long a = 0, e = 0;
     for (uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x; m < n; m += (uint64_t)STAT_SHARDS * NT) {
         a += b.mstat[m];
+        e += b.ownc[m] + b.mirc[m];
     }
     a = wave_sum<unsigned long long>(a);
-    if (lane_id() == 0) red[threadIdx.x >> 6] = a;
+    e = wave_sum<unsigned long long>(e);
+    if (lane_id() == 0) { red[0][threadIdx.x >> 6] = a; red[1][threadIdx.x >> 6] = e; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        a = 0;
-        for (int i = 0; i < NWAVE; ++i) a += red[i];
+        a = e = 0;
+        for (int i = 0; i < NWAVE; ++i) { a += red[0][i]; e += red[1][i]; }
         shard_add(b.st, blockIdx.x, SH_AOLD, a);
+        if (e) atomicAdd(&b.st->ev_pk, e);
     }
 }
 
@@ -1031,20 +1035,6 @@ __global__ void __launch_bounds__(NT) k_mover_counts(TickBufs b) {
     b.icnt[k] = (lo32(oc) ? 1u : 0u) + (hi32(oc) ? 1u : 0u) + nm;
 }
 // bucket path: the event totals (the general path takes them from the scan of mcnt)
-__global__ void __launch_bounds__(NT) k_event_totals(TickBufs b) {
-    __shared__ unsigned long long red[NWAVE];
-    const uint64_t n = b.st->n_mlist;
-    unsigned long long a = 0;
-    for (uint64_t k = (uint64_t)blockIdx.x * NT + threadIdx.x; k < n; k += (uint64_t)gridDim.x * NT) a += b.mcnt[k];
-    a = wave_sum<unsigned long long>(a);
-    if (lane_id() == 0) red[threadIdx.x >> 6] = a;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        a = 0;
-        for (int i = 0; i < NWAVE; ++i) a += red[i];
-        if (a) atomicAdd(&b.st->ev_pk, a);
-    }
-}
 
 // (3) the listed movers' events flattened at their scanned offsets, in list
 // (slot) order: own events (watcher A, target-sorted), then the mirror events
@@ -1689,7 +1679,6 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     hipLaunchKernelGGL(k_mover_counts, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
     if (!b.ev_full) {
         const uint32_t NB = 1u << b.bk_bits;
-        hipLaunchKernelGGL(k_event_totals, dim3(64), dim3(NT), 0, s, b);
         scan_exclusive<uint32_t, uint32_t>(b.icnt, b.ioff, b.m, nml, sc, (uint32_t*)&b.st->n_items, s);
         hipLaunchKernelGGL(k_chunk_first_items, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
         hipLaunchKernelGGL(k_flat_items, dim3(nblk1((b.ev_cap + 63) / 64, NWAVE)), dim3(NT), 0, s, b);

@@ -217,7 +217,6 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->eid_dev, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->cid_dev, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->ol, oc, nc))) return rc;     // new records: zero (session 0 is never used)
-    if ((rc = grow_preserve(c, c->rflag, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->gnb[0], 0, nc))) return rc;    // rebuilt (grid_dirty)
     if ((rc = grow_preserve(c, c->gnb[1], 0, nc))) return rc;
     if ((rc = grow_preserve(c, c->gidx, 0, nc))) return rc;
@@ -227,7 +226,6 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     HIPCHK(hipMemsetAsync(c->stamp + oc, 0, n * 8, c->st));
     HIPCHK(hipMemsetAsync(c->pos + oc, 0, n * sizeof(float4), c->st));
     HIPCHK(hipMemsetAsync(c->flags + oc, 0, n * 4, c->st));
-    HIPCHK(hipMemsetAsync(c->rflag + oc, 0, n * 4, c->st));
     HIPCHK(hipMemsetAsync(c->gate + oc, 0, n * 2, c->st));
     HIPCHK(hipMemsetAsync(c->nbc + oc, 0, n * 8, c->st));
     HIPCHK(hipMemsetAsync(c->movbit, 0, ((size_t)nc / 32 + 1) * 4, c->st));
@@ -477,7 +475,7 @@ void gw_shutdown(gw_ctx* c) {
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off, &c->m_create.h,
                     &c->m_destroy.h, &c->m_fanout.h};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
-    void* ps[] = {c->halo, c->rflag, c->sc.ticket, c->movbit, c->gmi, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->nbc, c->ol,
+    void* ps[] = {c->halo, c->sc.ticket, c->movbit, c->gmi, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->nbc, c->ol,
                   c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->cstats, c->scal32, c->gsb[0],
                   c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->bigcell, c->gm_start};
     for (void* p : ps) if (p) (void)hipFree(p);
@@ -656,7 +654,7 @@ int gw_route_halo(gw_ctx* c, const gw_op* dev_ops, const uint64_t* dev_stamps, u
     uint32_t tag = 0;
     if ((rc = next_ol_tag(c, &tag))) return rc;
     launch_route_halo(world(c), dev_ops, (const unsigned long long*)dev_stamps, n, max_step, D, c->ol, tag,
-                      c->rflag, c->halo, c->st);
+                      c->halo, c->st);
     HIPCHK(hipGetLastError());
     return 0;
 }

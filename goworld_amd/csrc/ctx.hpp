@@ -124,7 +124,6 @@ struct gw_ctx {
     uint32_t* gmi = nullptr;                 // [slot_cap] primary mover-grid entry of a mover
     gw::OpLast* ol = nullptr;                // [slot_cap] per-op dedupe state (session-tagged words)
     uint32_t ol_tag = 0;                     // last dedupe session handed out (next_ol_tag)
-    uint32_t* rflag = nullptr;                // [slot_cap] halo routing scratch, zero between calls
     HaloStats* halo = nullptr;                // halo routing counters (device)
     GEnt* gnb[2] = {nullptr, nullptr};   // grid ping-pong (gnb[gcur] is current)
     uint32_t* gsb[2] = {nullptr, nullptr};  // cell starts ping-pong

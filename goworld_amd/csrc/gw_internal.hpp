@@ -43,7 +43,9 @@ struct alignas(16) PrevEnt {
 // lets a newer session's index replace an older one and a word of an older
 // session reads as -1 (ol_get), so nothing is reset between ticks.
 struct alignas(64) OpLast {
-    unsigned long long pos, aoi, leave, clr[2], pad[3];
+    unsigned long long pos, aoi, leave, clr[2];
+    unsigned long long rb[2];   // routing (halo.hip r2): sync bit c set since the last Leave clearing it (tag only)
+    unsigned long long pad;
 };
 __device__ __forceinline__ unsigned long long ol_put(uint32_t tag, uint32_t i) {
     return ((unsigned long long)tag << 32) | i;
@@ -314,10 +316,12 @@ struct HaloDsts {
     HaloDst d[2];
     uint32_t n;
 };
-// ol_tag: the routing's dedupe session (a tick that reuses it passes the same tag)
+// ol_tag: the routing's dedupe session (a tick that reuses it passes the same tag).
+// stamps_out != nullptr: the first pass also writes stamps_out[i] = stamp_base + i
+// (then `stamps` may be stamps_out); pad: NOP rows up to each buffer's capacity
 void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
-                       float max_step, const HaloDsts& D, OpLast* ol, uint32_t ol_tag, uint32_t* rflag, HaloStats* hs,
-                       hipStream_t s, bool pad = true);
+                       float max_step, const HaloDsts& D, OpLast* ol, uint32_t ol_tag, HaloStats* hs, hipStream_t s,
+                       bool pad = true, unsigned long long* stamps_out = nullptr, unsigned long long stamp_base = 0);
 void launch_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n, hipStream_t s);
 void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,
                        hipStream_t s);

@@ -4,18 +4,19 @@
 // net effect those ops have on a neighbour's copy (goworld_amd/dworld.py
 // module doc).  The entity state before the tick IS the
 // routing state: AoiEnt (x, present), flags (sync flags pending since the
-// last collect).  Four light passes over the owned ops, O(ops), no host sync:
-//   r1  last AOI op / last payload op / last Leave per slot (atomicMax, as
-//       k_ops1 of the tick; the same per-slot arrays, left at -1 after r4)
-//   r2  OR of the sync bits of the ops after the last Leave clearing each bit
-//       (atomicOr; a Leave's sync_flags is the mask of bits it keeps, as the tick)
+// last collect).  Three light passes over the owned ops, O(ops), no host sync:
+//   r1  last AOI op / last payload op / last Leave per slot (u64 atomicMax
+//       into the session-tagged OpLast words, exactly k_ops1 of the tick,
+//       which reuses them); the ops' stamps in the world path
+//   r2  the sync bits of the ops after the last Leave clearing each bit (a
+//       Leave's sync_flags is the mask of bits it keeps, as in the tick),
+//       one session-tagged word per bit in the same record
 //   r3  the entity's last op writes up to 3 rows per destination, entities
 //       placed by one wave-aggregated atomic per wave and destination
-//   r4  reset of the per-slot scratch; zero (NOP) rows past the entities
-//       placed, so no memset of the buffers is needed
-// The placement counters are zeroed by r1 of the next call (r4 of this one
-// has read them by then).  Integer/byte work bound by the latency of the
-// per-slot gathers; no LDS or MFMA.
+//   r4  (fixed-size buffers only) zero (NOP) rows past the entities placed
+// Nothing is reset afterwards: the words age out with their session tag.  The
+// placement counters are zeroed by r1 of the next call.  Integer/byte work
+// bound by the latency of the per-slot gathers; no LDS or MFMA.
 #include "dev_common.hpp"
 
 namespace gw {
@@ -29,10 +30,12 @@ __device__ __forceinline__ bool op_valid(const gw_op& op, uint32_t cap) {
 }
 
 __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
-                                                OpLast* ol, uint32_t tag, HaloStats* hs) {
+                                                OpLast* ol, uint32_t tag, HaloStats* hs,
+                                                unsigned long long* stamps_out, unsigned long long stamp_base) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i == 0) hs->cnt[0] = hs->cnt[1] = 0;         // placement counters of this call
     if (i >= n) return;
+    if (stamps_out) stamps_out[i] = stamp_base + i;
     const gw_op op = ops[i];
     if (op.kind == GW_OP_NOP) return;
     if (!op_valid(op, cap)) {
@@ -50,15 +53,14 @@ __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, ui
 }
 
 __global__ void __launch_bounds__(NT) k_route2(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
-                                                const OpLast* __restrict__ ol, uint32_t tag, uint32_t* rflag) {
+                                                OpLast* ol, uint32_t tag) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
     const gw_op op = ops[i];
     if (!op_valid(op, cap) || op.kind == GW_OP_LEAVE || !(op.sync_flags & SIF_ROUTED)) return;
-    uint32_t bits = 0;
-    for (int c = 0; c < 2; ++c)
-        if (((op.sync_flags >> c) & 1) && (int32_t)i > ol_get(ol[op.slot].clr[c], tag)) bits |= 1u << c;
-    if (bits) atomicOr(&rflag[op.slot], bits);
+    for (int c = 0; c < 2; ++c)                      // every writer stores the same word: no atomic
+        if (((op.sync_flags >> c) & 1) && (int32_t)i > ol_get(ol[op.slot].clr[c], tag))
+            ol[op.slot].rb[c] = ol_put(tag, 1);
 }
 
 __device__ __forceinline__ gw_op mk_op(uint8_t kind, uint8_t flags, uint32_t slot, const gw_op* payload) {
@@ -82,8 +84,7 @@ __device__ __forceinline__ void put_row(gw_halo_row* r, const gw_op& o, unsigned
 
 __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, const unsigned long long* __restrict__ stamps,
                                                 uint32_t n, World w, const OpLast* __restrict__ ol, uint32_t tag,
-                                                const uint32_t* __restrict__ rflag, float max_step, HaloDsts D,
-                                                HaloStats* hs) {
+                                                float max_step, HaloDsts D, HaloStats* hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     // every lane reaches the wave-aggregated appends below
     bool rep = false;
@@ -118,10 +119,12 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
         if (lp >= 0) op_pos = ops[lp];
         // syncInfoFlag after the tick's ops (k_ops3 / k_place): old bits a Leave
         // did not clear, OR'd with the bits set since the Leave that cleared them
-        uint32_t keep = 0;
-        for (int c = 0; c < 2; ++c)
+        uint32_t keep = 0, rbits = 0;
+        for (int c = 0; c < 2; ++c) {
             if (ol_get(ol[s].clr[c], tag) < 0) keep |= 1u << c;
-        f = ((flag_get(w.flags, s) & keep) | rflag[s]) & SIF_ROUTED;
+            if (ol_get(ol[s].rb[c], tag) >= 0) rbits |= 1u << c;
+        }
+        f = ((flag_get(w.flags, s) & keep) | rbits) & SIF_ROUTED;
     }
     for (uint32_t d = 0; d < D.n; ++d) {
         const HaloDst& dst = D.d[d];
@@ -158,17 +161,14 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
     }
 }
 
-__global__ void __launch_bounds__(NT) k_route4(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
-                                                uint32_t* rflag, HaloDsts D, const HaloStats* __restrict__ hs) {
+// zero (NOP) rows past the entities placed (fixed-size exchanges), so no
+// memset of the buffers is needed; thread i: row i of each buffer
+__global__ void __launch_bounds__(NT) k_route4(HaloDsts D, const HaloStats* __restrict__ hs) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
-    // rows past the placed entities become NOPs (thread i: row i of each buffer)
     for (uint32_t d = 0; d < D.n; ++d) {
         const uint64_t used = (uint64_t)min(hs->cnt[d], D.d[d].cap) * ROWS;
         if (i >= used && i < (uint64_t)D.d[d].cap * ROWS) put_row(D.d[d].rows + i, mk_op(GW_OP_NOP, 0, 0, nullptr), 0ull);
     }
-    if (i >= n) return;
-    const gw_op op = ops[i];
-    if (op_valid(op, cap)) rflag[op.slot] = 0;     // (the dedupe words age out with their session tag)
 }
 
 __global__ void __launch_bounds__(NT) k_split_rows(const gw_halo_row* __restrict__ rows, uint32_t n,
@@ -182,17 +182,16 @@ __global__ void __launch_bounds__(NT) k_split_rows(const gw_halo_row* __restrict
 }  // namespace
 
 void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
-                       float max_step, const HaloDsts& D, OpLast* ol, uint32_t ol_tag, uint32_t* rflag, HaloStats* hs,
-                       hipStream_t s, bool pad) {
+                       float max_step, const HaloDsts& D, OpLast* ol, uint32_t ol_tag, HaloStats* hs, hipStream_t s,
+                       bool pad, unsigned long long* stamps_out, unsigned long long stamp_base) {
     const uint32_t nb = nblk1(n, NT);
     uint64_t rows = 0;                                   // NOP padding up to the capacity (fixed-size exchanges)
     if (pad)
         for (uint32_t d = 0; d < D.n; ++d) rows = std::max<uint64_t>(rows, (uint64_t)D.d[d].cap * ROWS);
-    hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, ol_tag, hs);
-    hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, ol_tag, rflag);
-    hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, ol, ol_tag, rflag, max_step, D, hs);
-    hipLaunchKernelGGL(k_route4, dim3(nblk1(std::max<uint64_t>(n, rows), NT)), dim3(NT), 0, s, ops, n, w.cap,
-                       rflag, D, hs);
+    hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, ol_tag, hs, stamps_out, stamp_base);
+    hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, ol_tag);
+    hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, ol, ol_tag, max_step, D, hs);
+    if (rows) hipLaunchKernelGGL(k_route4, dim3(nblk1(rows, NT)), dim3(NT), 0, s, D, hs);
 }
 
 __global__ void __launch_bounds__(NT) k_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n) {

@@ -269,6 +269,65 @@ __global__ void __launch_bounds__(NT) k_scan1(const TI* in, TO* out, uint64_t n_
 }
 
 // host launcher; sc.status must hold SCAN_WORDS * ceil(n_max / SCAN_TILE) words
+// Two u32 arrays of the same length scanned by one launch: element i packs
+// a[i] | b[i] << 32 into a u64 (each sum stays below 2^32, so the halves never
+// carry into each other), one look-back chain, the halves unpacked on store.
+template <int IPT>
+__global__ void __launch_bounds__(NT) k_scan_pair32(const uint32_t* a, const uint32_t* b, uint32_t* oa, uint32_t* ob,
+                                                    uint64_t n, unsigned long long* __restrict__ status,
+                                                    unsigned long long* __restrict__ ticket, unsigned long long tbase,
+                                                    uint32_t tag, uint32_t* total_a, uint32_t* total_b) {
+    __shared__ unsigned long long lds[IPT * NWAVE];
+    __shared__ uint32_t s_tile;
+    __shared__ unsigned long long s_prefix;
+    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tbase);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t t0 = (uint64_t)tile * (IPT * NT);
+    unsigned long long v[IPT];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
+        v[j] = i < n ? ((unsigned long long)a[i] | ((unsigned long long)b[i] << 32)) : 0ull;
+    }
+    unsigned long long tot;
+    tile_excl_scan_striped<unsigned long long, IPT>(v, lds, tot);
+    if (threadIdx.x < 64) {
+        const unsigned long long excl = scan_lookback<unsigned long long>(status, tile, tag, tot);
+        if (threadIdx.x == 0) s_prefix = excl;
+    }
+    __syncthreads();
+    const unsigned long long pre = s_prefix;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
+        if (i < n) {
+            const unsigned long long x = pre + v[j];
+            oa[i] = (uint32_t)x;
+            ob[i] = (uint32_t)(x >> 32);
+        }
+    }
+    if (tile == gridDim.x - 1 && threadIdx.x == 0) {
+        *total_a = (uint32_t)(pre + tot);
+        *total_b = (uint32_t)((pre + tot) >> 32);
+    }
+}
+
+inline void scan_pair32(const uint32_t* a, const uint32_t* b, uint32_t* oa, uint32_t* ob, uint64_t n, ScanCtx& sc,
+                        uint32_t* total_a, uint32_t* total_b, hipStream_t st) {
+    const uint64_t tile = SCAN_TILE;
+    uint32_t nb = (uint32_t)((n + tile - 1) / tile);
+    if (nb == 0) nb = 1;
+    if (sc.tag >= SCAN_TAG_MAX) {
+        (void)hipMemsetAsync(sc.status, 0, sc.max_tiles * SCAN_WORDS * 8, st);
+        sc.tag = 0;
+    }
+    ++sc.tag;
+    hipLaunchKernelGGL((k_scan_pair32<SCAN_IPT>), dim3(nb), dim3(NT), 0, st, a, b, oa, ob, n, sc.status, sc.ticket,
+                       sc.tbase, sc.tag, total_a, total_b);
+    sc.tbase += nb;
+}
+
 template <typename TI, typename TO>
 inline void scan_exclusive(const TI* in, TO* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
                            TO* total_dev, hipStream_t st) {

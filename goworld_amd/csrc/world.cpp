@@ -167,11 +167,10 @@ int gw_world_route(gw_ctx* c, const gw_op* ops, uint32_t n, const gw_halo_row* s
         D.d[D.n++] = HaloDst{W.ext_lo[side], W.ext_hi[side], P<gw_halo_row>(W.send[side]), (uint32_t)cap_ent};
     }
     const unsigned long long base = 1 + (W.tick * W.g.ranks + W.g.rank) * STAMP_STRIDE;
-    launch_iota_u64(P<unsigned long long>(W.stamps), base, n, c->st);
     uint32_t tag = 0;
     if ((rc = next_ol_tag(c, &tag))) return rc;      // the tick reuses this session (gw_world_submit)
     launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->ol, tag,
-                      c->rflag, c->halo, c->st, /*pad=*/false);
+                      c->halo, c->st, /*pad=*/false, P<unsigned long long>(W.stamps), base);   // stamps by r1
     HIPCHK(hipGetLastError());
     W.kept = n;
     W.kept_tag = tag;
@@ -236,12 +235,12 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
         D.d[D.n++] = HaloDst{W.ext_lo[side], W.ext_hi[side], P<gw_halo_row>(W.send[side]), (uint32_t)cap_ent};
     }
     const unsigned long long base = 1 + (W.tick * W.g.ranks + W.g.rank) * STAMP_STRIDE;
-    launch_iota_u64(P<unsigned long long>(W.stamps), base, n, c->st);
+    if (!D.n) launch_iota_u64(P<unsigned long long>(W.stamps), base, n, c->st);
     if (D.n) {                                        // a one-strip world has nobody to route to
         uint32_t tag = 0;
         if ((rc = next_ol_tag(c, &tag))) return rc;  // the tick reuses this session (gw_world_submit)
         launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->ol, tag,
-                          c->rflag, c->halo, c->st, /*pad=*/false);
+                          c->halo, c->st, /*pad=*/false, P<unsigned long long>(W.stamps), base);   // stamps by r1
         W.kept = n;
         W.kept_tag = tag;
     }

@@ -334,7 +334,7 @@ __global__ void __launch_bounds__(NT) k_grid_copy(TickBufs b) {
 // moves up by the arrivals with a smaller slot, an arrival lands after the
 // kept entries and arrivals with a smaller slot.  A wave scans the flags of
 // DIRTY_SPAN cells and merges its dirty ones; cells with more than 64
-// arrivals go to the block path.
+// arrivals are compacted and sorted by the wave (bitonic, in place).
 constexpr uint32_t DIRTY_SPAN = 16;
 __global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) {
     const int ln = lane_id();
@@ -350,8 +350,22 @@ __global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) {
         const uint32_t sn = b.start_nxt[c], nn = b.start_nxt[c + 1] - sn;
         const uint32_t kept = old - (b.dep[c] & ~CELL_DIRTY);
         const uint32_t narr = nn - kept;
-        if (narr > 64) {
-            if (ln == 0) b.bigcell[atomicAdd(&b.st->n_bigcell, 1ull)] = c;   // rare
+        if (narr > 64) {                          // rare: compact the kept entries, sort the cell
+            uint32_t run = 0;
+            for (uint32_t base = 0; base < old; base += 64) {
+                const uint32_t i = base + ln;
+                GEnt e;
+                e.slot = DEPARTED;
+                if (i < old) e = b.w.gn[so + i];
+                const bool keep = i < old && e.slot != DEPARTED;
+                const uint64_t bm = wave_ballot(keep);
+                if (keep) b.gn_nxt[sn + run + (uint32_t)popc64(bm & lt)] = e;   // arrivals sit behind `kept`
+                run += (uint32_t)popc64(bm);
+            }
+            wave_sync();
+            bitonic_inplace<64>(b.gn_nxt + sn, nn, ln, [](const GEnt& e) { return e.slot; }, [] { wave_sync(); });
+            for (uint32_t j = (uint32_t)ln; j < nn; j += 64) b.w.gidx[b.gn_nxt[sn + j].slot] = j;
+            if (ln == 0) b.dep[c] = 0;
             continue;
         }
         // arrivals: one per lane, read before any write of the cell's new range
@@ -393,34 +407,6 @@ __global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) {
     }
 }
 
-// dirty cells with more than 64 arrivals: block compaction + bitonic in place
-__global__ void __launch_bounds__(NT) k_grid_bigcell(TickBufs b) {
-    __shared__ uint32_t lds[NWAVE];
-    const uint64_t nb = b.st->n_bigcell;
-    for (uint64_t k = blockIdx.x; k < nb; k += gridDim.x) {
-        const uint32_t c = b.bigcell[k];
-        const uint32_t so = b.w.gn_start[c], old = b.w.gn_start[c + 1] - so;
-        const uint32_t sn = b.start_nxt[c], nn = b.start_nxt[c + 1] - sn;
-        uint32_t run = 0;
-        for (uint32_t base = 0; base < old; base += NT) {
-            const uint32_t i = base + threadIdx.x;
-            GEnt e;
-            e.slot = DEPARTED;
-            if (i < old) e = b.w.gn[so + i];
-            const uint32_t keep = (i < old && e.slot != DEPARTED) ? 1u : 0u;
-            uint32_t tot;
-            const uint32_t pre = block_excl_scan<uint32_t>(keep, lds, tot);
-            if (keep) b.gn_nxt[sn + run + pre] = e;
-            run += tot;
-        }
-        __syncthreads();
-        bitonic_inplace<NT>(b.gn_nxt + sn, nn, (int)threadIdx.x, [](const GEnt& e) { return e.slot; },
-                            [] { __syncthreads(); });
-        for (uint32_t j = threadIdx.x; j < nn; j += NT) b.w.gidx[b.gn_nxt[sn + j].slot] = j;
-        if (threadIdx.x == 0) b.dep[c] = 0;
-        __syncthreads();
-    }
-}
 
 void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint32_t NC = b.w.ncells;
@@ -432,7 +418,6 @@ void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     hipLaunchKernelGGL(k_place, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_grid_copy, dim3(std::min<uint32_t>(nblk1(b.w.cap, NT), 16384)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_grid_dirty, dim3(nblk1((uint64_t)NC, DIRTY_SPAN * NWAVE)), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_grid_bigcell, dim3(64), dim3(NT), 0, s, b);
 }
 
 // ---------------------------------------------------------------------------

@@ -313,7 +313,7 @@ int ensure_cells(gw_ctx* c) {
     if (c->cells_cap < need) {
         const uint32_t nc = std::max(need, c->cells_cap + c->cells_cap / 2);
         uint32_t** arrs[] = {&c->gsb[0], &c->gsb[1], &c->dep, &c->arr, &c->gm_cnt, &c->cnt_new, &c->dirty,
-                             &c->bigcell, &c->gm_start};
+                             &c->gm_start};
         HIPCHK(hipStreamSynchronize(c->st));
         for (uint32_t** a : arrs) {
             if (*a) HIPCHK(hipFree(*a));
@@ -477,7 +477,7 @@ void gw_shutdown(gw_ctx* c) {
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
     void* ps[] = {c->halo, c->sc.ticket, c->movbit, c->gmi, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->nbc, c->ol,
                   c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->cstats, c->scal32, c->gsb[0],
-                  c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->bigcell, c->gm_start};
+                  c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->gm_start};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->hcstats) (void)hipHostFree(c->hcstats);
@@ -854,10 +854,10 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     if (getenv("GW_DEBUG_STATS")) {
         unsigned long long f0 = 0, f2 = 0;
         for (int i = 0; i < STAT_SHARDS; ++i) { f0 += hs.shard[i][0]; f2 += hs.shard[i][2]; }
-        fprintf(stderr, "gw_tick: movers %llu gm %llu cand %llu ev %llu+%llu big %llu mlist %llu bigcell %llu "
+        fprintf(stderr, "gw_tick: movers %llu gm %llu cand %llu ev %llu+%llu big %llu mlist %llu "
                 "f0 %llu f2 %llu bits %d full %d items %llu\n",
                 (unsigned long long)n_mov, hs.n_gm, hs.cand_total, hs.ev_pk & 0xffffffffull,
-                hs.ev_pk >> 32, hs.n_big, hs.n_mlist, hs.n_bigcell, f0, f2, b.bk_bits, b.ev_full, hs.n_items);
+                hs.ev_pk >> 32, hs.n_big, hs.n_mlist, f0, f2, b.bk_bits, b.ev_full, hs.n_items);
     }
     o.ops = M;
     o.movers = n_mov;
@@ -1026,7 +1026,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.ol = c->ol;
     b.st = st;
     b.gn_nxt = c->gnb[c->gcur ^ 1]; b.start_nxt = c->gsb[c->gcur ^ 1];
-    b.dep = c->dep; b.arr = c->arr; b.cnt_new = c->cnt_new; b.bigcell = c->bigcell;
+    b.dep = c->dep; b.arr = c->arr; b.cnt_new = c->cnt_new;
     b.gm_cnt = c->gm_cnt; b.gm_start = c->gm_start; b.gm = P<MEnt>(c->gm);
     b.mtmp = P<MEnt>(c->mtmp); b.mcell = P<uint4>(c->mcell);
     b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg);

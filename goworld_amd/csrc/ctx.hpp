@@ -130,7 +130,7 @@ struct gw_ctx {
     int gcur = 0;
     uint32_t cells_cap = 0;              // words in each per-cell array
     uint32_t *dep = nullptr, *arr = nullptr, *gm_cnt = nullptr, *cnt_new = nullptr, *dirty = nullptr,
-             *bigcell = nullptr, *gm_start = nullptr;
+             *gm_start = nullptr;
     uint32_t* gidx = nullptr;
     SpaceP* sp_dev = nullptr;
     uint32_t sp_cap = 0;

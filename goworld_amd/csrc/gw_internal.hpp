@@ -101,7 +101,6 @@ constexpr int SH_AOLD = 1;    // a_old | a_new << 32 (per-shard sums stay below 
 struct DevStats {
     unsigned long long n_present;     // entities in the grid
     unsigned long long n_movers;      // unused (movers are counted in shard[][SH_MOVERS])
-    unsigned long long n_bigcell;     // dirty cells too large for one wave
     unsigned long long cand_total;    // sum of candidate bounds over movers
     unsigned long long n_gm;          // mover-grid entries
     unsigned long long ev_pk;         // sum of (enters | leaves<<32) over watchers
@@ -186,7 +185,6 @@ struct TickBufs {
     uint32_t* dep;            // [ncells] departures (| CELL_DIRTY), zero between ticks
     uint32_t* arr;            // [ncells] arrivals, zero between ticks
     uint32_t* cnt_new;        // [ncells+1] entries per cell after the tick
-    uint32_t* bigcell;        // [ncells] dirty cells for the block path
     // mover grid (counting sort by cell; gm_cnt is zero between ticks)
     uint32_t* gm_cnt;         // [ncells+1]
     uint32_t* gm_start;       // [ncells+1]

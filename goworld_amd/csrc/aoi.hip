@@ -517,7 +517,7 @@ struct GlobalSrc {
 // per wave.
 template <int DIFF_U, uint32_t SCAP, class Src>
 __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_t* lds, const Src& S) {
-    const MEnt me = b.gm[m];
+    const MEnt me = S.gm(m);
     const int ln = lane_id();
     if (!(me.tags & TAG_PRIMARY)) {
         if (ln == 0) {
@@ -685,11 +685,14 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
 // lane 31's prefix for the upper half; a lane finds its range by a 5-step
 // search over its half's prefixes; ballots are masked per half; own events
 // (<= 32) are sorted inside the half in registers, more go to the block sort.
-// Returns false (nothing done) when either entry needs more rows: the caller
-// then runs both through mover_one.
+// GM: the mover-grid entries (LDS when the block staged them); L: this wave's
+// 64 LDS words, the first 32 own events of each half (sorted from there, no
+// read-back of HBM).  Returns false (nothing done) when either entry needs
+// more rows: the caller then runs both through mover_one.
 template <int HU>
 __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint64_t m_end, const SpaceP& P,
-                                           const GEnt* GN, const uint32_t* GS, const uint32_t* MS) {
+                                           const GEnt* GN, const uint32_t* GS, const uint32_t* MS,
+                                           const MEnt* GM, uint32_t* L) {
     const int ln = lane_id();
     const uint32_t half = (uint32_t)ln >> 5, hl = (uint32_t)ln & 31u, hb = half << 5;
     const uint64_t hmask = half ? 0xffffffff00000000ull : 0x00000000ffffffffull;
@@ -700,15 +703,16 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     me.tags = 0;
     me.x = me.z = me.ox = me.oz = qnan();
     me.slot = 0; me.client = 0; me.space = 0;
-    if (valid) me = b.gm[m];
+    if (valid) me = GM[m];
     const bool prim = valid && (me.tags & TAG_PRIMARY);
     const bool pn = me.x == me.x, po = me.ox == me.ox;
     Rects R;
     R.n = 0;
     if (prim) R = mover_rects(P, po, me.ox, me.oz, pn, me.x, me.z);
-    int rows = 0;
-    for (int q = 0; q < R.n; ++q) rows += R.r[q].z1 - R.r[q].z0 + 1;
-    if (wave_ballot(rows > 16)) return false;              // wave-uniform
+    // (no loop over R.r[q]: a dynamically indexed Rects lives in scratch)
+    const int nr0 = R.n > 0 ? R.r[0].z1 - R.r[0].z0 + 1 : 0;
+    const int nr1 = R.n > 1 ? R.r[1].z1 - R.r[1].z0 + 1 : 0;
+    if (wave_ballot(nr0 + nr1 > 16)) return false;         // wave-uniform
     const World& w = b.w;
     uint64_t reg = 0, cap = 0;
     bool go = prim;
@@ -730,8 +734,6 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     uint32_t rs = 0, rl = 0;
     if (go) {
         const int row = (int)(hl >> 1), kind = (int)(hl & 1u);
-        const int nr0 = R.n > 0 ? R.r[0].z1 - R.r[0].z0 + 1 : 0;
-        const int nr1 = R.n > 1 ? R.r[1].z1 - R.r[1].z0 + 1 : 0;
         if (row < nr0 + nr1) {
             const bool first = row < nr0;
             const int x0 = first ? R.r[0].x0 : R.r[1].x0;
@@ -780,7 +782,7 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
                     cc[u].slot = (e.meta & MOVER_BIT) ? A : e.slot;
                     cc[u].info = TAG_OLD | TAG_NEW | (e.meta & CLIENT_BIT ? CAND_CLIENT : 0u) | CAND_NONMOVER;
                 } else {
-                    const MEnt e = b.gm[idx];
+                    const MEnt e = GM[idx];
                     cc[u].x = e.x; cc[u].z = e.z; cc[u].ox = e.ox; cc[u].oz = e.oz;
                     cc[u].slot = e.slot;
                     cc[u].info = e.tags | (e.client ? CAND_CLIENT : 0u);
@@ -824,7 +826,10 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
             const uint64_t be = wave_ballot(ev) & hmask, bl = wave_ballot(ev && lv) & hmask;
             const uint64_t bm = wave_ballot(mev) & hmask;
             const uint32_t at = n + (uint32_t)popc64(be & lt);
-            if (ev && at < cap) out[at] = key;
+            if (ev && at < cap) {
+                if (at < 32u) L[hb + at] = key;
+                else out[at] = key;
+            }
             const uint32_t atm = nm_ + (uint32_t)popc64(bm & lt);
             if (mev && atm < cap) mir[atm] = ((uint64_t)e.slot << 32) | (A << 1) | (lv ? 1u : 0u);
             n += (uint32_t)popc64(be);
@@ -833,11 +838,14 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
             nml += (uint32_t)popc64(wave_ballot(mev && lv) & hmask);
         }
     }
-    // own events by (leave, target): <= 32 in registers inside the half, more by the block sort
-    const bool reg_sort = go && n > 1 && n <= 32;
+    // own events by (leave, target): <= 32 in registers inside the half, more
+    // by the block sort (the first 32 written out of L unsorted)
+    wave_sync();
+    const uint32_t nw = go ? (uint32_t)min((uint64_t)n, cap) : 0u;    // keys written (n <= cap but for a bug)
+    const bool reg_sort = nw > 1 && n <= 32;
+    uint32_t v = hl < nw ? L[hb + hl] : 0xffffffffu;
+    if (hl < nw && !reg_sort) out[hl] = v;
     if (wave_ballot(reg_sort)) {
-        wave_sync();
-        uint32_t v = (reg_sort && hl < n) ? out[hl] : 0xffffffffu;
         const uint32_t n2 = reg_sort ? n : 0u;
         const uint32_t nmax = max((uint32_t)__builtin_amdgcn_readlane((int)n2, 0),
                                   (uint32_t)__builtin_amdgcn_readlane((int)n2, 32));
@@ -848,7 +856,6 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
                 const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)v, 32 + (int)j);
                 r += (half ? hi : lo) < v ? 1u : 0u;
             }
-            wave_sync();
             if (reg_sort && hl < n) out[r] = v;
         } else {
             v = half_sort32(v);
@@ -881,6 +888,29 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
 // entries with every grid candidate and row start read from LDS (mover-grid
 // candidates, ~10 % of them, stay global).
 constexpr uint32_t SMALL_SORT = 256;    // own events sorted in LDS up to this many (more: block sort)
+constexpr uint32_t SMALL_GM = 256;      // mover-grid entries of a space staged in LDS (more: read from HBM)
+
+template <int DIFF_U>
+__device__ __forceinline__ void small_walk(const TickBufs& b, uint32_t m0, uint32_t m1, const SpaceP& P,
+                                           const GlobalSrc& src, uint32_t* lds) {
+    if (b.small_halves) {
+        uint32_t* L = lds + (threadIdx.x >> 6) * SMALL_SORT;
+        for (uint32_t m = m0 + (threadIdx.x >> 6) * 2; m < m1; m += NWAVE * 2) {
+            if (!mover_half<3>(b, m, m1, P, src.GN, src.GS, src.MS, src.GM, L)) {
+                mover_one<DIFF_U, SMALL_SORT>(b, m, lds, src);
+                wave_sync();
+                if (m + 1 < m1) mover_one<DIFF_U, SMALL_SORT>(b, m + 1, lds, src);
+            }
+            wave_sync();
+        }
+        return;
+    }
+    for (uint32_t m = m0 + (threadIdx.x >> 6); m < m1; m += NWAVE) {
+        mover_one<DIFF_U, SMALL_SORT>(b, m, lds, src);
+        wave_sync();
+    }
+}
+
 template <int DIFF_U>
 __global__ void __launch_bounds__(NT) k_mover_small(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * SMALL_SORT];
@@ -894,29 +924,20 @@ __global__ void __launch_bounds__(NT) k_mover_small(TickBufs b) {
     GEnt* G = (GEnt*)dyn_lds;
     uint32_t* S = (uint32_t*)(G + b.small_ents);
     uint32_t* MS = S + nc + 1;
+    MEnt* GL = (MEnt*)(dyn_lds + (b.small_ents + (2 * ((size_t)b.small_cells + 1) + 3) / 4));
     const uint32_t ng = min(g1 - g0, b.small_ents);        // (host guarantee: g1 - g0 <= small_ents)
+    const bool stage = m1 - m0 <= SMALL_GM;                 // block-uniform
     for (uint32_t i = threadIdx.x; i < ng; i += NT) G[i] = b.w.gn[g0 + i];
     for (uint32_t i = threadIdx.x; i <= nc; i += NT) {
         S[i] = b.w.gn_start[cb + i];
         MS[i] = b.gm_start[cb + i];
     }
+    if (stage)
+        for (uint32_t i = threadIdx.x; i < m1 - m0; i += NT) GL[i] = b.gm[m0 + i];
     __syncthreads();
-    if (b.small_halves) {
-        for (uint32_t m = m0 + (threadIdx.x >> 6) * 2; m < m1; m += NWAVE * 2) {
-            if (!mover_half<3>(b, m, m1, P, G - g0, S - cb, MS - cb)) {
-                const GlobalSrc src{G - g0, S - cb, MS - cb, b.gm};
-                mover_one<DIFF_U, SMALL_SORT>(b, m, lds, src);
-                wave_sync();
-                if (m + 1 < m1) mover_one<DIFF_U, SMALL_SORT>(b, m + 1, lds, src);
-            }
-            wave_sync();
-        }
-        return;
-    }
-    for (uint32_t m = m0 + (threadIdx.x >> 6); m < m1; m += NWAVE) {
-        mover_one<DIFF_U, SMALL_SORT>(b, m, lds, GlobalSrc{G - g0, S - cb, MS - cb, b.gm});
-        wave_sync();
-    }
+    // every mover's own entry and its mover-grid candidates from LDS when staged
+    if (stage) small_walk<DIFF_U>(b, m0, m1, P, GlobalSrc{G - g0, S - cb, MS - cb, GL - m0}, lds);
+    else small_walk<DIFF_U>(b, m0, m1, P, GlobalSrc{G - g0, S - cb, MS - cb, b.gm}, lds);
 }
 
 // A_old | A_new << 32 of every mover-grid entry, one shard per
@@ -1635,7 +1656,8 @@ void launch_bk_split_init(uint32_t* sp, int wbits, hipStream_t s) {
 void tick_diff(const TickBufs& b, hipStream_t s) {
     const uint64_t nmax = 2ull * b.m;
     if (b.small_ents) {                    // small-space mode: a block per space
-        const size_t lds = (size_t)b.small_ents * sizeof(GEnt) + 2 * ((size_t)b.small_cells + 1) * 4;
+        const size_t lds = ((size_t)b.small_ents + (2 * ((size_t)b.small_cells + 1) + 3) / 4) * 16 +
+                           (size_t)SMALL_GM * sizeof(MEnt);
         hipLaunchKernelGGL((k_mover_small<2>), dim3(b.n_spaces), dim3(NT), lds, s, b);
         return;
     }

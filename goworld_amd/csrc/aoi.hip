@@ -714,21 +714,21 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     const int nr1 = R.n > 1 ? R.r[1].z1 - R.r[1].z0 + 1 : 0;
     if (wave_ballot(nr0 + nr1 > 16)) return false;         // wave-uniform
     const World& w = b.w;
+    // the HBM reads of this pair (region, stamps) are first needed at the
+    // first write / boundary tie: the row ranges and candidates (LDS) go first
     uint64_t reg = 0, cap = 0;
-    bool go = prim;
+    const bool go = prim;
+    const uint32_t A = me.slot;
+    unsigned long long sA = 0, soA = 0;
     if (prim) {
         reg = b.reg[m];
         cap = b.cand[m];
-        if (reg + cap > b.own_cap) {                        // region past the buffers: the host redoes the diff
-            if (hl == 0) atomicOr(&b.st->overflow, 1ull);
-            go = false;
-        }
+        sA = w.stamp[A];
+        soA = w.prev[A].ostamp;
     }
-    const uint32_t A = me.slot;
+    const uint64_t own_cap = b.own_cap;
     const float d = P.d;
     const bool ownA = owned_x(P, pn ? me.x : me.ox);
-    unsigned long long sA = 0, soA = 0;
-    if (go) { sA = w.stamp[A]; soA = w.prev[A].ostamp; }
     const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
     // this half's row ranges: lane hl = row hl/2 of the rects, grid hl%2
     uint32_t rs = 0, rl = 0;
@@ -826,12 +826,10 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
             const uint64_t be = wave_ballot(ev) & hmask, bl = wave_ballot(ev && lv) & hmask;
             const uint64_t bm = wave_ballot(mev) & hmask;
             const uint32_t at = n + (uint32_t)popc64(be & lt);
-            if (ev && at < cap) {
-                if (at < 32u) L[hb + at] = key;
-                else out[at] = key;
-            }
+            if (ev && at < 32u) L[hb + at] = key;
+            else if (ev && at < cap && reg + cap <= own_cap) out[at] = key;
             const uint32_t atm = nm_ + (uint32_t)popc64(bm & lt);
-            if (mev && atm < cap) mir[atm] = ((uint64_t)e.slot << 32) | (A << 1) | (lv ? 1u : 0u);
+            if (mev && atm < cap && reg + cap <= own_cap) mir[atm] = ((uint64_t)e.slot << 32) | (A << 1) | (lv ? 1u : 0u);
             n += (uint32_t)popc64(be);
             nl += (uint32_t)popc64(bl);
             nm_ += (uint32_t)popc64(bm);
@@ -841,7 +839,10 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     // own events by (leave, target): <= 32 in registers inside the half, more
     // by the block sort (the first 32 written out of L unsorted)
     wave_sync();
-    const uint32_t nw = go ? (uint32_t)min((uint64_t)n, cap) : 0u;    // keys written (n <= cap but for a bug)
+    const bool ovf = prim && reg + cap > own_cap;           // region past the buffers: the host redoes the diff
+    if (ovf && hl == 0) atomicOr(&b.st->overflow, 1ull);
+    const bool fin = prim && !ovf;
+    const uint32_t nw = fin ? (uint32_t)min((uint64_t)n, cap) : 0u;   // keys to place (n <= cap but for a bug)
     const bool reg_sort = nw > 1 && n <= 32;
     uint32_t v = hl < nw ? L[hb + hl] : 0xffffffffu;
     if (hl < nw && !reg_sort) out[hl] = v;
@@ -862,9 +863,9 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
             if (reg_sort && hl < n) out[hl] = v;
         }
     }
-    if (go && n > 32 && hl == 0) b.big[atomicAdd(&b.st->n_big, 1ull)] = (uint32_t)m;
+    if (fin && n > 32 && hl == 0) b.big[atomicAdd(&b.st->n_big, 1ull)] = (uint32_t)m;
     if (valid && hl == 0) {
-        if (!go) {
+        if (!fin) {
             b.mstat[m] = 0;
             b.ownc[m] = 0;
             b.mirc[m] = 0;

@@ -928,7 +928,7 @@ __global__ void __launch_bounds__(NT) k_mover_small(TickBufs b) {
     MEnt* GL = (MEnt*)(dyn_lds + (b.small_ents + (2 * ((size_t)b.small_cells + 1) + 3) / 4));
     const uint32_t ng = min(g1 - g0, b.small_ents);        // (host guarantee: g1 - g0 <= small_ents)
     const bool stage = m1 - m0 <= SMALL_GM;                 // block-uniform
-    for (uint32_t i = threadIdx.x; i < ng; i += NT) G[i] = b.w.gn[g0 + i];
+    lds_fill16<NT>((uint4*)G, (const uint4*)(b.w.gn + g0), ng);
     for (uint32_t i = threadIdx.x; i <= nc; i += NT) {
         S[i] = b.w.gn_start[cb + i];
         MS[i] = b.gm_start[cb + i];

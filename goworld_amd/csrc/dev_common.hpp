@@ -189,6 +189,23 @@ __device__ __forceinline__ uint32_t next_pow2(uint32_t v) {
     return 1u << (32 - __clz(v - 1));
 }
 
+// Block copy of n 16-B items from HBM into LDS with 4 loads in flight per
+// thread (a plain strided loop waits out one HBM round trip per item it copies)
+template <int NTH>
+__device__ __forceinline__ void lds_fill16(uint4* dst, const uint4* __restrict__ src, uint32_t n) {
+    for (uint32_t i = threadIdx.x; i < n; i += 4 * NTH) {
+        const uint32_t left = n - i;
+        const uint4 r0 = src[i];
+        const uint4 r1 = left > NTH ? src[i + NTH] : r0;
+        const uint4 r2 = left > 2 * NTH ? src[i + 2 * NTH] : r0;
+        const uint4 r3 = left > 3 * NTH ? src[i + 3 * NTH] : r0;
+        dst[i] = r0;
+        if (left > NTH) dst[i + NTH] = r1;
+        if (left > 2 * NTH) dst[i + 2 * NTH] = r2;
+        if (left > 3 * NTH) dst[i + 3 * NTH] = r3;
+    }
+}
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

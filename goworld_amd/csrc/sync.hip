@@ -351,7 +351,7 @@ __global__ void __launch_bounds__(NT) k_sync_write_small(World w, const uint32_t
     GEnt* G = (GEnt*)dyn_lds;
     uint32_t* S = (uint32_t*)(G + max_ents);
     const uint32_t ng = min(g1 - g0, max_ents);             // (host guarantee: g1 - g0 <= max_ents)
-    for (uint32_t i = threadIdx.x; i < ng; i += NT) G[i] = w.gn[g0 + i];
+    lds_fill16<NT>((uint4*)G, (const uint4*)(w.gn + g0), ng);
     for (uint32_t i = threadIdx.x; i <= nc; i += NT) S[i] = w.gn_start[cb + i];
     __syncthreads();
     const int ln = lane_id();
@@ -405,7 +405,7 @@ __global__ void __launch_bounds__(NT) k_sync_write_small2(World w, const uint32_
     GEnt* G = (GEnt*)dyn_lds;
     uint32_t* S = (uint32_t*)(G + max_ents);
     const uint32_t ng = min(g1 - g0, max_ents);
-    for (uint32_t i = threadIdx.x; i < ng; i += NT) G[i] = w.gn[g0 + i];
+    lds_fill16<NT>((uint4*)G, (const uint4*)(w.gn + g0), ng);
     for (uint32_t i = threadIdx.x; i <= nc; i += NT) S[i] = w.gn_start[cb + i];
     __syncthreads();
     const int ln = lane_id();

@@ -51,7 +51,12 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t v, uint32_t* lis
 }
 
 // ---------------------------------------------------------------------------
-// ops: last-op dedupe per slot (seq = index in the tick's op stream)
+// ops: last-op dedupe per slot (seq = index in the tick's op stream).  Every
+// op stores its tagged index into its slot's words with plain stores (one of
+// the racing values lands); k_ops2 then raises each word to the largest index
+// with an atomicMax from the ops that find a smaller one, i.e. only where a
+// slot has several ops.  (An atomicMax per word and op runs memory-side on a
+// multi-XCD part: 2M of them took 90 us at config #4's 1M ops.)
 __global__ void __launch_bounds__(NT) k_ops1(TickBufs b) {
     const uint32_t i = b.op0 + blockIdx.x * NT + threadIdx.x;
     if (i >= b.m) return;
@@ -62,12 +67,30 @@ __global__ void __launch_bounds__(NT) k_ops1(TickBufs b) {
         return;
     }
     const unsigned long long v = ol_put(b.ol_tag, i);
-    if (op.kind != GW_OP_LEAVE) atomicMax(&b.ol[op.slot].pos, v);
-    if (op.kind != GW_OP_SYNC) atomicMax(&b.ol[op.slot].aoi, v);
+    OpLast& o = b.ol[op.slot];
+    if (op.kind != GW_OP_LEAVE) o.pos = v;
+    if (op.kind != GW_OP_SYNC) o.aoi = v;
     if (op.kind == GW_OP_LEAVE) {
-        atomicMax(&b.ol[op.slot].leave, v);
+        o.leave = v;
         for (int c = 0; c < 2; ++c)                     // the last Leave that clears bit c
-            if (!((op.sync_flags >> c) & 1)) atomicMax(&b.ol[op.slot].clr[c], v);
+            if (!((op.sync_flags >> c) & 1)) o.clr[c] = v;
+    }
+}
+__global__ void __launch_bounds__(NT) k_ops2(TickBufs b) {
+    const uint32_t i = b.op0 + blockIdx.x * NT + threadIdx.x;
+    if (i >= b.m) return;
+    gw_op op = b.ops[i];
+    if (op.kind == GW_OP_NOP || op.slot >= b.w.cap || op.kind > GW_OP_SYNC) return;
+    const unsigned long long v = ol_put(b.ol_tag, i);
+    OpLast& w = b.ol[op.slot];
+    const OpLast o = w;
+    const int32_t me = (int32_t)i;
+    if (op.kind != GW_OP_LEAVE && ol_get(o.pos, b.ol_tag) < me) atomicMax(&w.pos, v);
+    if (op.kind != GW_OP_SYNC && ol_get(o.aoi, b.ol_tag) < me) atomicMax(&w.aoi, v);
+    if (op.kind == GW_OP_LEAVE) {
+        if (ol_get(o.leave, b.ol_tag) < me) atomicMax(&w.leave, v);
+        for (int c = 0; c < 2; ++c)
+            if (!((op.sync_flags >> c) & 1) && ol_get(o.clr[c], b.ol_tag) < me) atomicMax(&w.clr[c], v);
     }
 }
 
@@ -166,7 +189,10 @@ void launch_restore(const World& w, const uint32_t* slots, const float4* xyzw, u
 }
 
 void tick_ops(const TickBufs& b, hipStream_t s) {
-    if (b.m > b.op0) hipLaunchKernelGGL(k_ops1, dim3(nblk(b.m - b.op0, NT)), dim3(NT), 0, s, b);
+    if (b.m > b.op0) {
+        hipLaunchKernelGGL(k_ops1, dim3(nblk(b.m - b.op0, NT)), dim3(NT), 0, s, b);
+        hipLaunchKernelGGL(k_ops2, dim3(nblk(b.m - b.op0, NT)), dim3(NT), 0, s, b);
+    }
     hipLaunchKernelGGL(k_ops3, dim3(nblk(b.m, NT)), dim3(NT), 0, s, b);
 }
 

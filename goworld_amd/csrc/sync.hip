@@ -290,10 +290,16 @@ __global__ void __launch_bounds__(NT) k_space_ranges(World w, const uint32_t* __
                                                      uint32_t* __restrict__ sfirst, uint32_t* __restrict__ slast) {
     const uint64_t nf = load_n(nf_max, nf_dev);
     const uint64_t k = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    // one state gather per entry: the neighbours' spaces come from the
+    // adjacent lanes, only the wave's edge lanes gather a second one
+    const auto space_at = [&](uint64_t j) { return j < nf ? (w.aoi[flagged[j]].meta & SPACE_MASK) : 0xffffffffu; };
+    const uint32_t s = space_at(k);
+    const int ln = lane_id();
+    uint32_t sp = (uint32_t)__shfl_up((int)s, 1, 64);
+    uint32_t sn = (uint32_t)__shfl_down((int)s, 1, 64);
+    if (ln == 0) sp = k ? space_at(k - 1) : 0xffffffffu;
+    if (ln == 63) sn = space_at(k + 1);
     if (k >= nf) return;
-    const uint32_t s = w.aoi[flagged[k]].meta & SPACE_MASK;
-    const uint32_t sp = k ? (w.aoi[flagged[k - 1]].meta & SPACE_MASK) : 0xffffffffu;
-    const uint32_t sn = k + 1 < nf ? (w.aoi[flagged[k + 1]].meta & SPACE_MASK) : 0xffffffffu;
     if (sp != s) sfirst[s] = (uint32_t)k;
     if (sn != s) slast[s] = (uint32_t)(k + 1);
 }

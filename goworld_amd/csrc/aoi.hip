@@ -286,7 +286,7 @@ __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, u
     if (co != NO_CELL && co == cn) {
         GEnt e;
         e.x = a.x; e.z = a.z; e.slot = A;
-        e.meta = cn | (cl ? CLIENT_BIT : 0u) | MOVER_BIT;
+        e.meta = cn | (cl ? CLIENT_BIT : 0u) | b.mbit;
         b.w.gn[b.w.gn_start[co] + b.w.gidx[A]] = e;
     } else {
         if (co != NO_CELL) {
@@ -336,7 +336,7 @@ __global__ void __launch_bounds__(NT) k_place(TickBufs b) {
         const uint32_t at = b.start_nxt[cn] + kept + atomicSub(&b.arr[cn], 1u) - 1u;
         GEnt g;
         g.x = e.x; g.z = e.z; g.slot = e.slot;
-        g.meta = cn | (cl ? CLIENT_BIT : 0u) | MOVER_BIT;
+        g.meta = cn | (cl ? CLIENT_BIT : 0u) | b.mbit;
         b.gn_nxt[at] = g;
     }
 }
@@ -347,10 +347,11 @@ __global__ void __launch_bounds__(NT) k_place(TickBufs b) {
 __global__ void __launch_bounds__(NT) k_grid_copy(TickBufs b) {
     const uint32_t n = b.w.gn_start[b.w.ncells];
     for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < n; i += gridDim.x * NT) {
-        const GEnt e = b.w.gn[i];
+        GEnt e = b.w.gn[i];
         if (e.slot == DEPARTED) continue;
         const uint32_t c = e.meta & CELL_MASK;
         if (b.dep[c] & CELL_DIRTY) continue;
+        e.meta &= ~b.mstale;                                      // the last tick's mover bit
         b.gn_nxt[b.start_nxt[c] + (i - b.w.gn_start[c])] = e;   // gidx (offset in the cell) unchanged
     }
 }
@@ -383,6 +384,7 @@ __global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) {
                 GEnt e;
                 e.slot = DEPARTED;
                 if (i < old) e = b.w.gn[so + i];
+                e.meta &= ~b.mstale;                  // the last tick's mover bit
                 const bool keep = i < old && e.slot != DEPARTED;
                 const uint64_t bm = wave_ballot(keep);
                 if (keep) b.gn_nxt[sn + run + (uint32_t)popc64(bm & lt)] = e;   // arrivals sit behind `kept`
@@ -409,6 +411,7 @@ __global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) {
             GEnt e;
             e.slot = DEPARTED;
             if (i < old) e = b.w.gn[so + i];
+            e.meta &= ~b.mstale;                  // the last tick's mover bit
             const bool keep = i < old && e.slot != DEPARTED;
             const uint64_t bm = wave_ballot(keep);
             uint32_t below = 0;                   // arrivals below this kept entry
@@ -597,7 +600,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
                     const GEnt e = S.gn(idx[u]);
                     cc[u].x = cc[u].ox = e.x;
                     cc[u].z = cc[u].oz = e.z;
-                    cc[u].slot = (e.meta & MOVER_BIT) ? A : e.slot;   // movers come from gm
+                    cc[u].slot = (e.meta & b.mbit) ? A : e.slot;      // movers come from gm
                     cc[u].info = TAG_OLD | TAG_NEW | (e.meta & CLIENT_BIT ? CAND_CLIENT : 0u) | CAND_NONMOVER;
                 } else {
                     const MEnt e = S.gm(idx[u]);
@@ -805,7 +808,7 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
                     const GEnt e = GN[idx];
                     cc[u].x = cc[u].ox = e.x;
                     cc[u].z = cc[u].oz = e.z;
-                    cc[u].slot = (e.meta & MOVER_BIT) ? A : e.slot;
+                    cc[u].slot = (e.meta & b.mbit) ? A : e.slot;
                     cc[u].info = TAG_OLD | TAG_NEW | (e.meta & CLIENT_BIT ? CAND_CLIENT : 0u) | CAND_NONMOVER;
                 } else {
                     const MEnt e = GM[idx];
@@ -1735,29 +1738,19 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// after the tick: per-op dedupe state of every op's slot back to -1 (thread
-// i: op i); MOVER bits cleared at the movers' new grid entries (thread i:
-// mover-grid entry i)
-// The tick's counters come by value (read by the host already), so block 0
-// can zero the device statistics for the next tick (no reset copy at its
-// start).
+// after the tick: the next tick's bucket bounds, and block 0 zeroes the device
+// statistics (the tick's counters come by value, read by the host already), so
+// no reset copy runs at its start.  Nothing per op or per mover: the dedupe
+// words age out with their session tag, the mover bits with the rebuild parity.
 __global__ void __launch_bounds__(NT) k_tick_reset(TickBufs b, ResetArgs r) {
-    const uint32_t i = blockIdx.x * NT + threadIdx.x;
-    bk_split_next(b, r);                     // the next tick's bucket bounds (its own launch cost 5-8 us)
+    bk_split_next(b, r);                     // (its own launch cost 5-8 us)
     if (blockIdx.x == 0) {
         unsigned long long* z = (unsigned long long*)b.st;
         for (uint32_t k = threadIdx.x; k < sizeof(DevStats) / 8; k += NT) z[k] = 0;
     }
-    if (i < r.n_gm) {
-        const MEnt e = b.gm[i];
-        if (e.tags & TAG_NEW) {                 // the new grid (b.w after the tick)
-            const uint32_t c = cell_of(b.w.sp[e.space], e.x, e.z);
-            b.w.gn[b.w.gn_start[c] + b.w.gidx[e.slot]].meta &= ~MOVER_BIT;
-        }
-    }
 }
 void tick_reset(const TickBufs& b, const ResetArgs& r, hipStream_t s) {
-    hipLaunchKernelGGL(k_tick_reset, dim3(nblk1(2ull * b.m, NT)), dim3(NT), 0, s, b, r);
+    hipLaunchKernelGGL(k_tick_reset, dim3(nblk1(BK_NSPLIT, NT)), dim3(NT), 0, s, b, r);
 }
 
 }  // namespace gw

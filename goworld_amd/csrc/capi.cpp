@@ -528,7 +528,7 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
     s.p.own_lo = -INFINITY;
     s.p.own_hi = INFINITY;
     uint64_t ncells = (uint64_t)s.p.W * (uint64_t)s.p.H;
-    if ((uint64_t)c->total_cells + ncells + 1 >= (1ull << 31)) return set_err(c, GW_ERANGE, "too many grid cells");
+    if ((uint64_t)c->total_cells + ncells + 1 > CELL_MASK) return set_err(c, GW_ERANGE, "too many grid cells");
     int rc;
     if ((rc = grow_slots(c, c->total_slots + capacity))) return rc;
     uint32_t sid = (uint32_t)c->spaces.size();
@@ -1008,6 +1008,8 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     TickBufs b{};
     b.w = world(c);
     b.ops = ops; b.m = M; b.stamp_base = c->stamp_base;
+    b.mbit = c->mpar ? MOVER_B : MOVER_A;
+    b.mstale = c->mpar ? MOVER_A : MOVER_B;
     b.ol_tag = 0;
     if (c->wd.ol_pre) {                               // the world's routing deduped its ops already
         const uint32_t k = c->wd.ol_pre;
@@ -1054,6 +1056,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     prof_end(c, (uint64_t)M * 24);
     prof_begin(c, "grid");
     tick_grid(b, c->sc, c->st);
+    c->mpar ^= 1u;                                   // the next rebuild drops this tick's mover bits
     c->cells_zero = true;
     size_t s_grid = prof_end(c, 0);
     c->gcur ^= 1;                                    // the new grid is current from here on

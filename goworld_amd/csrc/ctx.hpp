@@ -102,6 +102,7 @@ struct gw_ctx {
 
     std::vector<SpaceHost> spaces;
     uint32_t total_slots = 0, slot_cap = 0, total_cells = 0;
+    uint32_t mpar = 0;                 // parity of the incremental grid rebuilds (TickBufs::mbit)
     uint16_t max_gate = 0;
     unsigned long long stamp_base = 1;   // global op counter (stamp 0 = never)
     uint32_t epoch = 1;                  // bumped by every tick and client change (World.nbc)

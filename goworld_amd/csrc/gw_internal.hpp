@@ -58,11 +58,15 @@ __device__ __forceinline__ int32_t ol_get(unsigned long long v, uint32_t tag) {
 struct alignas(16) GEnt {
     float x, z;
     uint32_t slot;     // DEPARTED: the entity left this cell during the tick being built
-    uint32_t meta;     // cell | CLIENT_BIT | MOVER_BIT
+    uint32_t meta;     // cell | CLIENT_BIT | MOVER_A / MOVER_B
 };
-constexpr uint32_t MOVER_BIT = 0x80000000u;    // moved this tick (its pairs come from the mover grid)
+// moved this tick (its pairs come from the mover grid): the tick's bit
+// alternates between ticks (TickBufs::mbit), and the grid rebuild of the next
+// tick drops the other one while it copies the entries (no clearing pass)
+constexpr uint32_t MOVER_A = 0x80000000u;
+constexpr uint32_t MOVER_B = 0x20000000u;
 constexpr uint32_t CLIENT_BIT = 0x40000000u;   // has a client (GameClient != nil)
-constexpr uint32_t CELL_MASK = 0x3fffffffu;
+constexpr uint32_t CELL_MASK = 0x1fffffffu;
 constexpr uint32_t DEPARTED = 0xffffffffu;
 constexpr uint32_t CELL_DIRTY = 0x80000000u;   // flag in dep[c]: the cell is re-sorted this tick
 
@@ -178,6 +182,7 @@ struct TickBufs {
     unsigned long long stamp_base;
     OpLast* ol;               // [cap] per-slot op dedupe state (words of this tick's session ol_tag)
     uint32_t ol_tag;          // the tick's dedupe session
+    uint32_t mbit, mstale;    // this tick's mover bit (MOVER_A / MOVER_B) and the last tick's
     DevStats* st;
     // incremental grid: gn -> gn_nxt
     GEnt* gn_nxt;             // [cap]

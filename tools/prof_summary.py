@@ -18,7 +18,7 @@ def short(name):
 def main(path, last=5):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if short(r["Kernel_Name"]) == "k_ops1"]
+    starts = [i for i, r in enumerate(rows) if short(r["Kernel_Name"]).split("<")[0] == "k_ops1"]
     if not starts:
         print("no ticks found")
         return

@@ -1174,22 +1174,7 @@ __global__ void __launch_bounds__(NT) k_flatten(TickBufs b) {
 // their events at output time.
 constexpr int BK_RUN_BIT = BK_KEY_BITS;               // just above the (leave, watcher, target) bits
 constexpr uint64_t BK_RUN = 1ull << BK_RUN_BIT;
-__global__ void __launch_bounds__(NT) k_flat_items(TickBufs b) {
-    const uint64_t E = lo32(b.st->ev_pk) + hi32(b.st->ev_pk);
-    const uint64_t NI = b.st->n_items;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (E > b.ev_cap) atomicOr(&b.st->overflow, 1ull);
-        const uint64_t n = E > b.ev_cap ? 0 : NI;
-        b.st->n_sort = n;
-        const uint64_t T = (n + BK_TILE - 1) / BK_TILE;      // tiles in use: the count table's stride
-        b.st->bk_tiles = T;
-        b.st->bk_cells = T << b.bk_bits;
-    }
-    if (E > b.ev_cap) return;
-    const uint64_t c = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
-    if ((c << 6) >= NI) return;
-    const int ln = lane_id();
-    const uint64_t nl_ = b.st->n_mlist;
+__device__ __forceinline__ void flat_chunk(const TickBufs& b, uint64_t c, uint64_t NI, uint64_t nl_, int ln) {
     const uint32_t q0 = b.chunk_first[c];
     const uint64_t k = (uint64_t)q0 + ln;
     uint32_t at = 0xffffffffu, end = 0xffffffffu;
@@ -1217,7 +1202,7 @@ __global__ void __launch_bounds__(NT) k_flat_items(TickBufs b) {
                           (uint32_t)__shfl((int)(uint32_t)reg, q, 64);
     const uint32_t qA = (uint32_t)__shfl((int)mi.x, q, 64);
     const uint32_t qe = (uint32_t)__shfl((int)mi.y, q, 64), ql = (uint32_t)__shfl((int)mi.z, q, 64);
-    if (p >= NI) return;
+    if (p >= NI) return;                                       // (lane-local: the caller's loop is wave-uniform)
     const uint32_t W = (uint32_t)b.wbits;
     const uint32_t lvb = 1u << W;
     const uint32_t j = p - qat;
@@ -1231,6 +1216,28 @@ __global__ void __launch_bounds__(NT) k_flat_items(TickBufs b) {
         item = ((uint64_t)(((e & 1u) ? lvb : 0u) | (uint32_t)hi32(e)) << W) | (uint32_t)(lo32(e) >> 1);
     }
     b.bk_a[p] = item;
+}
+
+__global__ void __launch_bounds__(NT) k_flat_items(TickBufs b) {
+    const uint64_t E = lo32(b.st->ev_pk) + hi32(b.st->ev_pk);
+    const uint64_t NI = b.st->n_items;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (E > b.ev_cap) atomicOr(&b.st->overflow, 1ull);
+        const uint64_t n = E > b.ev_cap ? 0 : NI;
+        b.st->n_sort = n;
+        const uint64_t T = (n + BK_TILE - 1) / BK_TILE;      // tiles in use: the count table's stride
+        b.st->bk_tiles = T;
+        b.st->bk_cells = T << b.bk_bits;
+    }
+    if (E > b.ev_cap) return;
+    const int ln = lane_id();
+    const uint64_t nl_ = b.st->n_mlist;
+    // grid-stride over the 64-position chunks: the grid is sized by the last
+    // tick's item count, not by the event capacity (750k mostly idle waves
+    // cost 60 us of dispatch at config #4)
+    for (uint64_t c = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); (c << 6) < NI;
+         c += (uint64_t)gridDim.x * NWAVE)
+        flat_chunk(b, c, NI, nl_, ln);
 }
 
 // (4) bucket path.  Events are keyed by the full (leave, watcher, target) —
@@ -1718,7 +1725,9 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
         const uint32_t NB = 1u << b.bk_bits;
         scan_exclusive<uint32_t, uint32_t>(b.icnt, b.ioff, b.m, nml, sc, (uint32_t*)&b.st->n_items, s);
         hipLaunchKernelGGL(k_chunk_first_items, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
-        hipLaunchKernelGGL(k_flat_items, dim3(nblk1((b.ev_cap + 63) / 64, NWAVE)), dim3(NT), 0, s, b);
+        const uint64_t fw = std::min<uint64_t>((b.ev_cap + 63) / 64,
+                                               std::max<uint64_t>(8192, (2 * b.it_hint + 63) / 64));
+        hipLaunchKernelGGL(k_flat_items, dim3(nblk1(fw, NWAVE)), dim3(NT), 0, s, b);
         hipLaunchKernelGGL(k_bk_count, dim3(b.bk_tiles), dim3(BK_NT), 0, s, b);
         scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.bk_cnt, (uint64_t*)b.bk_cnt,
                                            (uint64_t)NB * b.bk_tiles, (const uint64_t*)&b.st->bk_cells, sc,

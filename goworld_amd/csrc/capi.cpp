@@ -726,6 +726,7 @@ static int ensure_events(gw_ctx* c) {
 static void choose_buckets(gw_ctx* c, TickBufs& b, bool full = false) {
     // items (own runs + mirror events) of the last tick, else about half the events
     const uint64_t est = std::max<uint64_t>(c->it_est ? c->it_est : c->ev_est / 2, 1);
+    b.it_hint = est;
     int bits = 1;
     while (bits < BK_MAXBITS && (est >> bits) > BK_MEAN) ++bits;
     bits = std::min(bits, b.wbits + 1);

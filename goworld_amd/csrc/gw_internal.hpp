@@ -226,6 +226,7 @@ struct TickBufs {
     uint32_t bk_tiles;        // tiles of BK_TILE flat positions covering ev_cap
     uint32_t* bk_split;       // [BK_NSPLIT] bucket bounds: quantiles of the last tick's keys
     int bk_bits;              // log2 of the bucket count (<= BK_MAXBITS, <= wbits + 1)
+    uint64_t it_hint;         // bucket-path items of the last tick (sizes the flatten's grid)
     int ev_full;              // 1: general stable radix sort instead of the bucket path
     gw_event* ev;             // [ev_cap] canonical events, enters then leaves
     uint64_t ev_cap;

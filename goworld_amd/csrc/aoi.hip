@@ -1309,14 +1309,18 @@ __global__ void __launch_bounds__(BK_NT) k_bk_count(TickBufs b) {
     __shared__ BkLut lut;
     const int t = threadIdx.x;
     const uint32_t NB = 1u << b.bk_bits;
-    for (uint32_t i = t; i < NB; i += BK_NT) h[i] = hw[i] = 0;
     const uint64_t n = b.st->n_sort;
     const uint64_t T = b.st->bk_tiles;
     if (blockIdx.x >= T) return;                            // block-uniform
-    const uint64_t base = (uint64_t)blockIdx.x * BK_TILE;
+    int lsh;
+    bk_lut_build(b, lut, NB, lsh);                          // (syncs)
+    // grid-stride over the tiles: the grid is sized by the last tick's items,
+    // not the event capacity (idle 57-KB-LDS blocks queued behind each other)
+    for (uint64_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
+    for (uint32_t i = t; i < NB; i += BK_NT) h[i] = hw[i] = 0;
+    __syncthreads();
+    const uint64_t base = tile * BK_TILE;
     {
-        int lsh;
-        bk_lut_build(b, lut, NB, lsh);                      // (syncs)
         const int W = b.wbits;
         const uint64_t km = (1ull << (2 * W + 1)) - 1;
         constexpr int IPT = BK_TILE / BK_NT;
@@ -1345,7 +1349,9 @@ __global__ void __launch_bounds__(BK_NT) k_bk_count(TickBufs b) {
     }
     __syncthreads();
     for (uint32_t i = t; i < NB; i += BK_NT)
-        b.bk_cnt[(uint64_t)i * T + blockIdx.x] = (unsigned long long)h[i] | ((unsigned long long)hw[i] << 32);
+        b.bk_cnt[(uint64_t)i * T + tile] = (unsigned long long)h[i] | ((unsigned long long)hw[i] << 32);
+    __syncthreads();                                        // before the next tile zeroes h / hw
+    }
 }
 
 // exclusive scan of one value per thread over a block of NTH threads
@@ -1367,9 +1373,9 @@ __global__ void __launch_bounds__(BK_NT) k_bucket_scatter(TickBufs b) {
     __shared__ uint32_t red[BK_NT / 64];
     const int t = threadIdx.x;
     const uint64_t n = b.st->n_sort;
-    const uint64_t base = (uint64_t)blockIdx.x * BK_TILE;
-    if (base >= n) return;                                  // block-uniform
     const uint32_t NB = 1u << b.bk_bits;
+    for (uint64_t tile = blockIdx.x; tile * BK_TILE < n; tile += gridDim.x) {   // grid-stride (k_bk_count)
+    const uint64_t base = tile * BK_TILE;
     for (uint32_t i = t; i < NB; i += BK_NT) h[i] = 0;
     __syncthreads();
     constexpr int IPT = BK_TILE / BK_NT;
@@ -1404,7 +1410,7 @@ __global__ void __launch_bounds__(BK_NT) k_bucket_scatter(TickBufs b) {
         const uint32_t i = (uint32_t)t * BPT + u;
         if (i < NB) {
             h[i] = toff;
-            go[i] = (uint32_t)b.bk_cnt[(uint64_t)i * T + blockIdx.x] - toff;   // mod 2^32: dst = go + staged index
+            go[i] = (uint32_t)b.bk_cnt[(uint64_t)i * T + tile] - toff;   // mod 2^32: dst = go + staged index
         }
         toff += cb[u];
     }
@@ -1421,6 +1427,8 @@ __global__ void __launch_bounds__(BK_NT) k_bucket_scatter(TickBufs b) {
         const uint32_t dst = go[(uint32_t)(v >> BK_KEY_SHIFT)] + i;
         if (dst < n) b.bk_b[dst] = v & ((1ull << BK_KEY_SHIFT) - 1);
         else atomicOr(&b.st->overflow, 2ull);              // (inconsistent counts: never by construction)
+    }
+    __syncthreads();                                        // before the next tile reuses h / go / stg
     }
 }
 
@@ -1728,11 +1736,14 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
         const uint64_t fw = std::min<uint64_t>((b.ev_cap + 63) / 64,
                                                std::max<uint64_t>(8192, (2 * b.it_hint + 63) / 64));
         hipLaunchKernelGGL(k_flat_items, dim3(nblk1(fw, NWAVE)), dim3(NT), 0, s, b);
-        hipLaunchKernelGGL(k_bk_count, dim3(b.bk_tiles), dim3(BK_NT), 0, s, b);
+        // tile passes: grid-stride over a grid sized by the last tick's items
+        const uint32_t bt = (uint32_t)std::min<uint64_t>(
+            b.bk_tiles, std::max<uint64_t>(256, (2 * b.it_hint + BK_TILE - 1) / BK_TILE));
+        hipLaunchKernelGGL(k_bk_count, dim3(bt), dim3(BK_NT), 0, s, b);
         scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.bk_cnt, (uint64_t*)b.bk_cnt,
                                            (uint64_t)NB * b.bk_tiles, (const uint64_t*)&b.st->bk_cells, sc,
                                            (uint64_t*)nullptr, s);
-        hipLaunchKernelGGL(k_bucket_scatter, dim3(b.bk_tiles), dim3(BK_NT), 0, s, b);
+        hipLaunchKernelGGL(k_bucket_scatter, dim3(bt), dim3(BK_NT), 0, s, b);
         hipLaunchKernelGGL(k_bucket_sort, dim3(NB), dim3(BK_SNT), 0, s, b);
     } else {
         scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.mcnt, (uint64_t*)b.moff, b.m, nml, sc,

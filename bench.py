@@ -9,14 +9,18 @@ position/yaw records).
 
 N=1 (default): BASELINE config #3, the 1M-entity clustered-hotspot space the
 metric is quoted on, on one GPU.
-N>1 (default --mode world): the SAME 1M-entity space decomposed into N X-strips,
-one per GPU (strong scaling; goworld_amd/dworld.py over the library's
-gw_world_* path): each tick every rank routes its owned ops, exchanges halo rows
-with both neighbours over RCCL inside the library (xGMI) and ticks its strip;
-walkers cross strip borders (migration is part of the measured tick).
-Every run also measures config #5, the north star's 16M-entity world
-decomposed over the same N GPUs, under the "config5" key (--no-config5 skips).
---mode spaces: an independent 1M space per GPU, no comm (weak scaling).
+N>1 (default --mode spaces): an independent 1M-entity config #3 space per GPU
+(seed 3 + rank), no data-path collective (weak scaling).  A space never spans
+processes in the reference (engine/entity/SpaceManager.go:11-31): the path
+partitions by space, so it shards with no exchange.
+Two strong-scaling legs ride along in every N>1 line:
+  "c3world": the SAME 1M-entity space decomposed into N X-strips, one per GPU
+  (goworld_amd/dworld.py over the library's gw_world_* path): each tick every
+  rank routes its owned ops, exchanges halo rows with both neighbours over RCCL
+  inside the library (xGMI) and ticks its strip; walkers cross strip borders;
+  "config5": the north star's 16M-entity world decomposed over the same N GPUs
+  (also measured at N=1).  --no-config5 / --no-c3world skip them.
+--mode world: the decomposed 1M space as the headline (strong scaling).
 --config 4 / 5: BASELINE config #4 (10k spaces x 1k) / #5 as the headline.
 
 Inputs (ops of every tick) are resident in HBM before the timed region;
@@ -24,8 +28,11 @@ outputs stay in HBM (device-resident boundary); t_e2e reports the host-in /
 host-out tick separately.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
+      (N>1 without torchrun: this process spawns the N rank processes itself,
+      one per GPU, and never touches a GPU; rank 0 prints the line)
 N>1:  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+      (WORLD_SIZE must equal --gpus)
 """
 from __future__ import annotations
 
@@ -61,9 +68,14 @@ def parse():
     ap.add_argument("--profile-stages", type=int, default=1,
                     help="1: HIP events around the dominant kernel's stage in the timed region (roofline) and "
                          "a per-stage breakdown over extra untimed steps; 0: none")
-    ap.add_argument("--mode", choices=["world", "spaces"], default="world",
-                    help="N>1 with config 3: world = the 1M space decomposed over the N GPUs (strong); spaces = an "
-                         "independent 1M space per GPU, no comm (weak)")
+    ap.add_argument("--mode", choices=["world", "spaces"], default="spaces",
+                    help="N>1 with config 3: spaces = an independent 1M space per GPU, no comm (weak; default); "
+                         "world = the 1M space decomposed over the N GPUs (strong)")
+    ap.add_argument("--no-c3world", dest="c3world", action="store_false",
+                    help="N>1, --mode spaces: skip the extra strong-scaling leg of the 1M space decomposed over N GPUs")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / control-plane rehearsal: ranks, barriers and the max-over-ranks timing with no "
+                         "GPU work (CPU tests)")
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=3,
                     help="3: the metric's 1M clustered space (N=1: one GPU; N>1: decomposed over the N GPUs); "
                          "4: config #4, 10k independent 1k-entity spaces, space s on GPU s mod N (strong); "
@@ -125,7 +137,82 @@ class Ctl:
         return bytes(t.tolist())
 
 
+def launch(a):
+    """--gpus N is the number of rank processes, one per GPU.  Under torchrun
+    (WORLD_SIZE set) this process is one of them and WORLD_SIZE must equal N.
+    Otherwise, for N > 1, this process is only the launcher: it never touches
+    a GPU, starts N copies of this script with RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set (rank r on GPU r, or on --device for one-GPU rehearsals),
+    lets rank 0 print the line, stops the others when one fails and returns
+    the exit code.  Returns None when this process should run as a rank."""
+    env_ws = os.environ.get("WORLD_SIZE")
+    if a.gpus < 1:
+        print(f"bench.py: --gpus {a.gpus} must be >= 1", file=sys.stderr)
+        return 2
+    if env_ws is not None:
+        if int(env_ws) != a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={env_ws} (launch N ranks for --gpus N)",
+                  file=sys.stderr)
+            return 2
+        return None
+    if a.gpus == 1:
+        return None
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc, live = 0, set(range(a.gpus))
+    try:
+        while live:
+            for r in sorted(live):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                live.discard(r)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    print(f"bench.py: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr)
+                    for q in live:
+                        procs[q].send_signal(signal.SIGTERM)
+            time.sleep(0.1)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
+def dry_run(a, ctl):
+    """Control-plane rehearsal (no GPU): W + K empty steps between barriers,
+    the max-over-ranks time and the sum of the ranks' unit counts, as measure()."""
+    for _ in range(a.warmup):
+        ctl.barrier()
+    ctl.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ctl.barrier()
+    el = time.perf_counter() - t0
+    ctl.barrier()
+    mx = ctl.reduce([el], "MAX")[0]
+    ranks = ctl.reduce([1.0], "SUM")[0]
+    if ctl.rank == 0:
+        print(json.dumps({"metric": "entity AOI updates/sec + enter/leave events/sec, 1M-entity space, 1/2/4/8 GPU",
+                          "value": None, "unit": "updates/s", "n_gpus": ctl.ws, "steps": a.steps,
+                          "warmup": a.warmup, "ms_per_step": mx / max(a.steps, 1) * 1e3, "dry_run": True,
+                          "ranks_reporting": int(ranks), "higher_is_better": True}), flush=True)
+
+
 STAGE_KERNEL = {"diff": "k_mover<2, 1>"}
+# the stage's kernel differs in small-space mode (config #4: many spaces whose grids fit LDS)
+STAGE_KERNEL_C4 = {"diff": "k_mover_small<2>", "sync_write": "k_sync_write_small2"}
 PMC_DIR = os.path.join(ROOT, "profiles")
 
 
@@ -525,7 +612,9 @@ def roofline_fields(res, K, config, ws):
 
         def traffic(k):
             return (kern or {}).get(k, {}).get("hbm_bytes") if kern else None
-        mv = STAGE_KERNEL["diff"]
+        names = STAGE_KERNEL_C4 if config == 4 else STAGE_KERNEL
+        mv = names["diff"]
+        sw = names.get("sync_write", "k_sync_write<4>")
         out["roofline"] = {"bound": "hbm", "kernel": mv, "achieved": ach, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic(mv),
                            "traffic_unit": "bytes/launch", "traffic_source": psrc, "traffic_src_hash": pstamp,
@@ -537,7 +626,7 @@ def roofline_fields(res, K, config, ws):
                            "timing": "HIP events around the kernel on its stream, every timed step"}
         kt = {}
         for k, alg in ((mv, mover_alg), ("k_bucket_sort", tot["events_alg"] / K),
-                       ("k_sync_write<4>", tot["sync_write_alg"] / K)):
+                       (sw, tot["sync_write_alg"] / K)):
             tr_ = traffic(k)
             kt[k] = {"bytes_alg": alg, "traffic": tr_, "traffic_over_alg": (tr_ / alg) if (tr_ and alg) else None}
         out["kernels"] = kt
@@ -552,7 +641,13 @@ def roofline_fields(res, K, config, ws):
 
 def main():
     a = parse()
+    rc = launch(a)
+    if rc is not None:                              # the launcher of N ranks (or a bad --gpus)
+        sys.exit(rc)
     ctl = Ctl(a)
+    if a.dry_run:
+        dry_run(a, ctl)
+        return
     ws, rank = ctl.ws, ctl.rank
     extra = 5 if a.profile_stages else 0         # untimed steps for the per-stage breakdown
     if a.config == 2:
@@ -565,7 +660,8 @@ def main():
         kind = "c3world"                            # the metric's 1M space decomposed over the N GPUs
     else:
         kind = "c3"                                 # N=1: the 1M space on one GPU (a one-strip world)
-    if kind in ("c5", "c3world") or (a.config5 and kind in ("c3", "c3world")):
+    c3world_leg = a.c3world and ws > 1 and kind == "c3"   # the 1M space decomposed, beside the weak line
+    if kind in ("c5", "c3world") or (a.config5 and kind in ("c3", "c3world")) or c3world_leg:
         # torch (decomposed-world runs) brings its own HIP runtime: it must
         # initialise before the library's runtime does, in this process
         import torch
@@ -608,21 +704,32 @@ def main():
                        "wall clock, untimed by the headline"}
     parallelism, n_world, m_rank = run.parallelism, run.n_world, run.m
     run.close()
+    def world_leg(which, warmup, steps, workload):
+        runw = WorldRun(a, ctl, warmup + steps + (extra if a.profile_stages else 0), which)
+        rw = measure(runw, a, ctl, warmup, steps, a.profile_stages, extra)
+        leg = {"workload": workload, "value": rw["sum_ops"] / rw["max_elapsed"], "unit": "updates/s",
+               "events_per_sec": rw["sum_events"] / rw["max_elapsed"],
+               "records_per_sec": rw["sum_records"] / rw["max_elapsed"],
+               "ms_per_step": rw["max_elapsed"] / steps * 1e3, "steps": steps, "warmup": warmup,
+               "scaling": "strong", "n_gpus": ws, "parallelism": runw.parallelism,
+               "roofline_frac": (roofline_fields(rw, steps, 5 if which == "c5" else 3, ws).get("roofline")
+                                 or {}).get("frac")}
+        runw.close()
+        return leg
+    # the metric's 1M space decomposed over the same N GPUs (strong), beside the weak headline
+    c3w = None
+    if c3world_leg:
+        c3w = world_leg("c3", W, K, (
+            f"config #3 as one world: the 1M-entity clustered space decomposed into {ws} X-strips of "
+            f"{a.side / ws:g}, one per GPU (walkers cross strip borders); step = route + RCCL halo exchange + "
+            f"gw_tick + gw_sync_collect on every rank"))
     # the north star's 16M decomposed world (config #5) at the same N, strong scaling
     c5 = None
     if a.config5 and kind in ("c3", "c3world"):
-        run5 = WorldRun(a, ctl, a.warmup5 + a.steps5 + (extra if a.profile_stages else 0), "c5")
-        r5 = measure(run5, a, ctl, a.warmup5, a.steps5, a.profile_stages, extra)
-        c5 = {"workload": "config #5: one 16M-entity uniform world space, L = 131072, AOI distance 100, 10% movers "
-                          f"per tick (+-4; walkers cross strip borders), decomposed into {ws} X-strip(s); step = "
-                          "route + RCCL halo exchange + gw_tick + gw_sync_collect on every rank",
-              "value": r5["sum_ops"] / r5["max_elapsed"], "unit": "updates/s",
-              "events_per_sec": r5["sum_events"] / r5["max_elapsed"],
-              "records_per_sec": r5["sum_records"] / r5["max_elapsed"],
-              "ms_per_step": r5["max_elapsed"] / a.steps5 * 1e3, "steps": a.steps5, "warmup": a.warmup5,
-              "scaling": "strong", "n_gpus": ws, "parallelism": run5.parallelism,
-              "roofline_frac": (roofline_fields(r5, a.steps5, 5, ws).get("roofline") or {}).get("frac")}
-        run5.close()
+        c5 = world_leg("c5", a.warmup5, a.steps5, (
+            "config #5: one 16M-entity uniform world space, L = 131072, AOI distance 100, 10% movers "
+            f"per tick (+-4; walkers cross strip borders), decomposed into {ws} X-strip(s); step = "
+            "route + RCCL halo exchange + gw_tick + gw_sync_collect on every rank"))
     if rank != 0:
         return
     mx = res["max_elapsed"]
@@ -646,7 +753,8 @@ def main():
     else:
         workload = ("config #3: single AOI space per GPU, 1M entities, 70% uniform + 30% in 64 "
                     "Gaussian hotspots (sigma 200), 10% movers per tick (+-4 / hotspot +-16), "
-                    "AOI distance 100, world 32768^2; step = gw_tick + gw_sync_collect")
+                    "AOI distance 100, world 32768^2; step = gw_tick + gw_sync_collect"
+                    + (f"; {ws} independent spaces (seed 3 + rank), one per GPU, no collective" if ws > 1 else ""))
     cfg_no = {"c2": 2, "c3": 3, "c3world": 3, "c4": 4, "c5": 5}[kind]
     line = {
         "metric": "entity AOI updates/sec + enter/leave events/sec, 1M-entity space, 1/2/4/8 GPU",
@@ -678,6 +786,8 @@ def main():
         line["t_device_ms_per_step"] = mx / K * 1e3
     if client:
         line["client_msgs"] = client
+    if c3w:
+        line["c3world"] = c3w
     if c5:
         line["config5"] = c5
     if not a.no_cpu_baseline and ws == 1 and kind == "c3":

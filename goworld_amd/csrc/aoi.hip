@@ -1735,10 +1735,13 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
         hipLaunchKernelGGL(k_chunk_first_items, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
         const uint64_t fw = std::min<uint64_t>((b.ev_cap + 63) / 64,
                                                std::max<uint64_t>(8192, (2 * b.it_hint + 63) / 64));
-        hipLaunchKernelGGL(k_flat_items, dim3(nblk1(fw, NWAVE)), dim3(NT), 0, s, b);
+        uint32_t fb = nblk1(fw, NWAVE);
+        if (b.grid_cap) fb = std::min(fb, b.grid_cap);
+        hipLaunchKernelGGL(k_flat_items, dim3(fb), dim3(NT), 0, s, b);
         // tile passes: grid-stride over a grid sized by the last tick's items
-        const uint32_t bt = (uint32_t)std::min<uint64_t>(
+        uint32_t bt = (uint32_t)std::min<uint64_t>(
             b.bk_tiles, std::max<uint64_t>(256, (2 * b.it_hint + BK_TILE - 1) / BK_TILE));
+        if (b.grid_cap) bt = std::min(bt, b.grid_cap);
         hipLaunchKernelGGL(k_bk_count, dim3(bt), dim3(BK_NT), 0, s, b);
         scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.bk_cnt, (uint64_t*)b.bk_cnt,
                                            (uint64_t)NB * b.bk_tiles, (const uint64_t*)&b.st->bk_cells, sc,

@@ -34,6 +34,41 @@ int gw_set_entity_ids(gw_ctx* c, const uint32_t* slots, const void* ids, uint32_
     if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
     const uint8_t* b = (const uint8_t*)ids;
+    // a batch names each slot and each (non-zero) id at most once
+    std::unordered_map<uint32_t, uint32_t> slot_at;
+    std::unordered_map<Id16, uint32_t, Id16Hash> id_at;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!slot_at.emplace(slots[i], i).second)
+            return set_err(c, GW_EINVAL, "slot %u named twice in one batch", slots[i]);
+        const Id16 k = id16(b + (size_t)i * GW_ID_BYTES);
+        if ((k.a | k.b) && !id_at.emplace(k, i).second)
+            return set_err(c, GW_EINVAL, "entity id of record %u repeated in one batch", i);
+    }
+    // an id that moves to a new slot is cleared at its old slot (on the device
+    // too: the wire encode must never emit one id for two entities)
+    std::vector<uint32_t> moved_from;
+    for (uint32_t i = 0; i < n; ++i) {
+        const Id16 k = id16(b + (size_t)i * GW_ID_BYTES);
+        if (!(k.a | k.b)) continue;
+        auto it = c->id_slot.find(k);
+        if (it != c->id_slot.end() && it->second != slots[i] && !slot_at.count(it->second))
+            moved_from.push_back(it->second);
+    }
+    // device first: a failure leaves host and device as they were
+    const uint32_t nt = n + (uint32_t)moved_from.size();
+    int rc;
+    const size_t off = ((size_t)nt * 4 + 15) & ~(size_t)15;
+    if ((rc = ensure(c, c->id_up, off + (size_t)nt * 16))) return rc;
+    std::vector<uint32_t> all_slots(slots, slots + n);
+    all_slots.insert(all_slots.end(), moved_from.begin(), moved_from.end());
+    std::vector<uint8_t> all_ids((size_t)nt * 16, 0);
+    memcpy(all_ids.data(), ids, (size_t)n * 16);
+    HIPCHK(hipMemcpyAsync(c->id_up.p, all_slots.data(), (size_t)nt * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(P<uint8_t>(c->id_up) + off, all_ids.data(), (size_t)nt * 16, hipMemcpyHostToDevice, c->st));
+    launch_put16(c->eid_dev, P<uint32_t>(c->id_up), (const uint4*)(P<uint8_t>(c->id_up) + off), nt, c->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->st));            // the host arrays are the caller's
+    for (uint32_t s : moved_from) c->eid_h[s] = Id16{0, 0};
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t s = slots[i];
         const Id16 old = c->eid_h[s];
@@ -41,20 +76,12 @@ int gw_set_entity_ids(gw_ctx* c, const uint32_t* slots, const void* ids, uint32_
             auto it = c->id_slot.find(old);
             if (it != c->id_slot.end() && it->second == s) c->id_slot.erase(it);
         }
-        const Id16 k = id16(b + (size_t)i * GW_ID_BYTES);
-        auto it = c->id_slot.find(k);                  // an id moves to its new slot
-        if (it != c->id_slot.end() && it->second != s) c->eid_h[it->second] = Id16{0, 0};
-        c->id_slot[k] = s;
-        c->eid_h[s] = k;
     }
-    int rc;
-    const size_t off = ((size_t)n * 4 + 15) & ~(size_t)15;
-    if ((rc = ensure(c, c->id_up, off + (size_t)n * 16))) return rc;
-    HIPCHK(hipMemcpyAsync(c->id_up.p, slots, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipMemcpyAsync(P<uint8_t>(c->id_up) + off, ids, (size_t)n * 16, hipMemcpyHostToDevice, c->st));
-    launch_put16(c->eid_dev, P<uint32_t>(c->id_up), (const uint4*)(P<uint8_t>(c->id_up) + off), n, c->st);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(c->st));            // the host arrays are the caller's
+    for (uint32_t i = 0; i < n; ++i) {
+        const Id16 k = id16(b + (size_t)i * GW_ID_BYTES);
+        c->eid_h[slots[i]] = k;
+        if (k.a | k.b) c->id_slot[k] = slots[i];
+    }
     return 0;
 }
 

@@ -197,20 +197,31 @@ int gw_world_submit(gw_ctx* c, const gw_halo_row* const recv[2], const uint32_t 
     if (!c) return GW_EINVAL;
     WorldHost& W = c->wd;
     if (!W.routed) return set_err(c, GW_ESTATE, "gw_world_route first");
+    // everything is checked before anything is queued: a failed submit leaves
+    // the routed tick in place (the caller may retry with the right rows)
+    for (int side = 0; side < 2; ++side) {
+        const uint32_t nr = recv_rows ? recv_rows[side] : 0;
+        if (nr && (!recv || !recv[side])) return set_err(c, GW_EINVAL, "rows from side %d missing", side);
+        if (nr && W.nb[side] < 0) return set_err(c, GW_EINVAL, "rows from side %d, which has no neighbour", side);
+        if (nr % ROWS) return set_err(c, GW_EINVAL, "side %d: %u rows, not whole entities", side, nr);
+    }
+    if (!c->segs.empty()) return set_err(c, GW_ESTATE, "ops queued outside the world tick: gw_tick first");
     W.routed = false;
     ++W.tick;
-    if (int rc = gw_submit_device_stamped(c, W.ops, (const uint64_t*)W.stamps.p, W.n_ops)) {
+    const size_t nseg = c->segs.size();
+    int rc = gw_submit_device_stamped(c, W.ops, (const uint64_t*)W.stamps.p, W.n_ops);
+    for (int side = 0; side < 2 && !rc; ++side) {
+        const uint32_t nr = recv_rows ? recv_rows[side] : 0;
+        if (nr) rc = gw_submit_device_rows(c, recv[side], nr);
+    }
+    if (rc) {                                         // nothing of this tick stays queued
+        c->segs.resize(nseg);
         W.kept = 0;                                   // (the session's words age out)
+        W.ol_pre = 0;
         return rc;
     }
     W.ol_pre = W.kept;                   // the tick's stream starts with the routed ops (gw_tick checks)
     W.kept = 0;
-    for (int side = 0; side < 2; ++side) {
-        const uint32_t nr = recv_rows ? recv_rows[side] : 0;
-        if (!nr) continue;
-        if (!recv || !recv[side]) return set_err(c, GW_EINVAL, "rows from side %d missing", side);
-        if (int rc = gw_submit_device_rows(c, recv[side], nr)) return rc;
-    }
     return 0;
 }
 
@@ -219,6 +230,7 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
     WorldHost& W = c->wd;
     if (!W.on) return set_err(c, GW_ESTATE, "no world strip (gw_world_create)");
     if (W.ol_pre) return set_err(c, GW_ESTATE, "the last routed world tick was not ticked (gw_tick first)");
+    if (W.routed) return set_err(c, GW_ESTATE, "tick already routed: gw_world_submit first");
     const bool any_nb = W.nb[0] >= 0 || W.nb[1] >= 0;
     if (any_nb && (!c->comm || c->c_nranks != (int)W.g.ranks || c->c_rank != (int)W.g.rank))
         return set_err(c, GW_ESTATE, "world of %u ranks needs a matching communicator (gw_comm_init)", W.g.ranks);

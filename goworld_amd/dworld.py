@@ -287,3 +287,96 @@ class StripRank:
             raise RuntimeError(f"{bad} owned entities moved more than max_step in one tick")
         if bad_ops:
             raise RuntimeError(f"{bad_ops} ops with an invalid slot or kind")
+
+
+class LocalWorld:
+    """R strip contexts of one decomposed world in ONE process on one device
+    (gw_world_create each), the halo rows handed from rank to rank by pointer:
+    rank r+1's send buffer is rank r's receive buffer (gw_world_route ->
+    gw_world_submit, no copy).  Used to rehearse the N-GPU world on the one
+    MI355X (tools/sim_ranks.py) and to check config #5 at its full size
+    against a single context (tests/test_gpu_golden.py).  x0/z0/yaw0: the
+    world's initial population; each rank enters the entities it owns, routed
+    to its neighbours as ghosts, in the same number of chunks everywhere."""
+
+    def __init__(self, R, n, side, max_step, x0, z0, yaw0, device=0, gates=None, d=100.0):
+        from . import gpuaoi, traces
+        self.R = R
+        self.geom = geom = Strips(-side / 2, side / R, R, d, max_step)
+        self.g = []
+        gates = np.ones(n, np.uint16) if gates is None else gates
+        for r in range(R):
+            g = gpuaoi.GpuAOI(device)
+            lo, hi = geom.ext(r)
+            bounds = (max(lo, -side / 2), -side / 2, min(hi, side / 2), side / 2)
+            g.world_create(geom.x0, geom.w, geom.d, geom.max_step, R, r, n, bounds)
+            g.set_clients(np.arange(n, dtype=np.uint32), gates)
+            self.g.append(g)
+        self.bufs = []
+        owner0 = geom.owner(x0)
+        chunk = 1 << 21
+        n_chunks = max(1, -(-int(np.bincount(owner0, minlength=R).max()) // chunk))
+        enters = []
+        for r in range(R):
+            mine = np.nonzero(owner0 == r)[0].astype(np.uint32)
+            enters.append(traces.enter_ops(mine, x0[mine], np.zeros(len(mine), np.float32), z0[mine], yaw0[mine]))
+        for k in range(n_chunks):
+            parts = [e[k * chunk:(k + 1) * chunk] for e in enters]
+            ptrs = [self.upload(r, p) for r, p in enumerate(parts)]
+            self.route_submit(ptrs, [len(p) for p in parts])
+            for g in self.g:
+                g.tick(copy=False, no_events=True)
+        for g in self.g:
+            g.sync_collect(copy=False)
+
+    def upload(self, r, ops):
+        """ops of rank r into device memory (kept until close)."""
+        ops = np.ascontiguousarray(ops)
+        p = self.g[r].dev_alloc(max(ops.nbytes, 64))
+        if ops.nbytes:
+            self.g[r].h2d(p, ops)
+        self.bufs.append((r, p))
+        return p
+
+    def split(self, ops, x_before):
+        """A tick's world ops -> per-rank owned ops (the strip of x before the tick), in call order."""
+        own = self.geom.owner(x_before)
+        return [ops[own == r] for r in range(self.R)]
+
+    def route_submit(self, ptrs, ms, times=None):
+        """Route every rank's owned ops and queue them with its neighbours' rows;
+        returns the halo rows moved.  times[r] += rank r's routing wall time."""
+        import time
+        if self.R == 1:                           # one strip: gw_world_step stamps and queues, no routing
+            t0 = time.perf_counter()
+            self.g[0].world_step(ptrs[0], ms[0])
+            if times is not None:
+                times[0] += time.perf_counter() - t0
+            return 0
+        sends = []
+        for r, g in enumerate(self.g):
+            g.synchronize()
+            t0 = time.perf_counter()
+            sends.append(g.world_route(ptrs[r], ms[r]))
+            if times is not None:
+                times[r] += time.perf_counter() - t0
+        rows = 0
+        for r, g in enumerate(self.g):
+            left = sends[r - 1][1] if r > 0 else (0, 0)           # left neighbour's rows to its right
+            right = sends[r + 1][0] if r + 1 < self.R else (0, 0)
+            rows += left[1] + right[1]
+            g.world_submit([left, right])
+        return rows
+
+    def check(self):
+        for r, g in enumerate(self.g):
+            ov, bad, bad_ops = g.world_status()
+            if ov or bad or bad_ops:
+                raise RuntimeError(f"rank {r}: contract counters {ov} {bad} {bad_ops}")
+
+    def close(self):
+        for r, p in self.bufs:
+            self.g[r].dev_free(p)
+        self.bufs = []
+        for g in self.g:
+            g.close()

@@ -167,3 +167,42 @@ def _encode(recs, gates):
             out += struct.pack("<4f", r["x"], r["y"], r["z"], r["yaw"])
         i = j
     return bytes(out)
+
+
+def test_entity_id_moves_and_batch_checks():
+    """An id re-registered at another slot leaves its old slot (host table and
+    the device copy the wire encode reads); a batch naming an id or a slot
+    twice is rejected with nothing changed."""
+    tr = T.dyadic_walk_trace(44, 300, 512.0, 100.0, 1, move_frac=0.2, gate_count=1, client_frac=1.0)
+    g, o, base = _setup(tr)
+    try:
+        with pytest.raises(gpuaoi.GwError):
+            g.set_entity_ids(np.array([1, 2], np.uint32) + base, _ids(1, 0x20000000) * 2)
+        with pytest.raises(gpuaoi.GwError):
+            g.set_entity_ids(np.array([3, 3], np.uint32) + base, _ids(2, 0x20000000))
+        # entity 4's id moves to slot 10 (10's own id is dropped)
+        g.set_entity_ids(np.array([10], np.uint32) + base, pyorc.fixed_uuid(4))
+        pay = pyorc.fixed_uuid(4) + struct.pack("<4f", float(tr.init_x[10]) + 1, 0, float(tr.init_z[10]), 0)
+        g.set_client_syncing(np.arange(tr.capacity, dtype=np.uint32) + base, np.ones(tr.capacity, np.uint8))
+        assert g.submit_client_sync(pay) == (1, 0)                 # decoded to slot 10
+        assert g.submit_client_sync(pyorc.fixed_uuid(10) + struct.pack("<4f", 0, 0, 0, 0)) == (0, 0)
+        mv = T.make_ops(1)
+        mv["kind"], mv["slot"], mv["sync_flags"] = T.OP_MOVED, 4 + base, 3
+        mv["x"], mv["z"] = tr.init_x[4], tr.init_z[4]
+        g.submit(mv)
+        g.tick()
+        recs = g.sync_collect().records
+        data, pk, nb, _ = g.encode_wire()
+        eids = [data[q + 16:q + 32] for _, off, ln in pk for q in range(off + 4, off + ln, 48)]
+        assert len(eids) == len(recs)
+        seen = set()
+        for r, e in zip(recs, eids):
+            if r["entity"] == 10 + base:
+                assert e == pyorc.fixed_uuid(4)
+            elif r["entity"] == 4 + base:
+                assert e == bytes(16)                              # cleared on the device too
+            seen.add(int(r["entity"]) - base)
+        assert {4, 10} <= seen
+    finally:
+        g.close()
+        o.close()

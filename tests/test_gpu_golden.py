@@ -129,3 +129,30 @@ def test_many_spaces_config4_digests(gpu, name):
         del recs
     assert g.total_neighbors() == d["nbr_total"]
     g.close()
+
+
+@pytest.mark.parametrize("cap", [1, 3])
+def test_grid_stride_passes_capped(gpu, cap, monkeypatch):
+    """The flatten and bucket tile passes loop grid-stride when a tick has more
+    items than their grid (sized by the last tick's items).  GW_GRID_CAP caps
+    those grids to `cap` blocks, so every block runs many chunk / tile
+    iterations (reusing its LDS histograms and staging): the config #2 digests
+    (100k entities, ~10^5 items per tick = dozens of 8192-item tiles) must
+    still match."""
+    monkeypatch.setenv("GW_GRID_CAP", str(cap))
+    name = "config2_100k"
+    d = G.digests()[name]
+    tr = G.DIGEST_TRACES[name]()
+    g = gpu()                                   # gw_init reads GW_GRID_CAP
+    monkeypatch.delenv("GW_GRID_CAP")
+    gpuaoi.load_space(g, tr)
+    for t, ops in enumerate(tr.ticks):
+        exp = d["ticks"][t]
+        g.submit(ops)
+        res = g.tick()
+        assert (res.n_enter, res.n_leave) == (exp["n_enter"], exp["n_leave"])
+        assert G.sha(res.enter) == exp["enter_sha"] and G.sha(res.leave) == exp["leave_sha"], f"tick {t}"
+        assert res.n_enter + res.n_leave > 4 * 8192                # several tiles per block
+        r = g.sync_collect()
+        assert G.sha(canonical(r.records, tr.gates)) == exp["rec_sha"], f"tick {t}: records"
+    g.close()

@@ -58,74 +58,21 @@ def world_ticks(which, ticks, n):
     return side, max_step, x0, z0, yaw0, tk
 
 
-class SimWorld:
+class SimWorld(dworld.LocalWorld):
+    """dworld.LocalWorld with per-rank step timing."""
+
     def __init__(self, R, n, side, max_step, x0, z0, yaw0, tk, device=0):
-        self.R = R
-        self.geom = geom = dworld.Strips(-side / 2, side / R, R, 100.0, max_step)
-        self.g = []
-        for r in range(R):
-            g = gpuaoi.GpuAOI(device)
-            lo, hi = geom.ext(r)
-            bounds = (max(lo, -side / 2), -side / 2, min(hi, side / 2), side / 2)
-            g.world_create(geom.x0, geom.w, geom.d, geom.max_step, R, r, n, bounds)
-            g.set_clients(np.arange(n, dtype=np.uint32), np.ones(n, np.uint16))
-            self.g.append(g)
-        self.bufs = []
-        owner0 = geom.owner(x0)
-        chunk = 1 << 21
-        n_chunks = max(1, -(-int(np.bincount(owner0, minlength=R).max()) // chunk))
-        enters = []
-        for r in range(R):
-            mine = np.nonzero(owner0 == r)[0].astype(np.uint32)
-            enters.append(traces.enter_ops(mine, x0[mine], np.zeros(len(mine), np.float32), z0[mine], yaw0[mine]))
-        for k in range(n_chunks):                 # load: owned Enters, routed to the neighbours as ghosts
-            parts = [e[k * chunk:(k + 1) * chunk] for e in enters]
-            self._route_submit([self._upload(r, p) for r, p in enumerate(parts)], [len(p) for p in parts])
-            for g in self.g:
-                g.tick(copy=False, no_events=True)
-        for g in self.g:
-            g.sync_collect(copy=False)
+        super().__init__(R, n, side, max_step, x0, z0, yaw0, device=device)
         self.ticks = []                           # per tick: [(dev_ptr, m)] per rank, resident in HBM
         for ops, xb in tk:
-            own = geom.owner(xb)
-            self.ticks.append([(self._upload(r, ops[own == r]), int((own == r).sum())) for r in range(R)])
-
-    def _upload(self, r, ops):
-        ops = np.ascontiguousarray(ops)
-        p = self.g[r].dev_alloc(max(ops.nbytes, 64))
-        if ops.nbytes:
-            self.g[r].h2d(p, ops)
-        self.bufs.append((r, p))
-        return p
-
-    def _route_submit(self, ptrs, ms, times=None):
-        if self.R == 1:                           # one strip: gw_world_step stamps and queues, no routing
-            t0 = time.perf_counter()
-            self.g[0].world_step(ptrs[0], ms[0])
-            if times is not None:
-                times[0] += time.perf_counter() - t0
-            return 0
-        sends = []
-        for r, g in enumerate(self.g):
-            g.synchronize()
-            t0 = time.perf_counter()
-            sends.append(g.world_route(ptrs[r], ms[r]))
-            if times is not None:
-                times[r] += time.perf_counter() - t0
-        rows = 0
-        for r, g in enumerate(self.g):
-            left = sends[r - 1][1] if r > 0 else (0, 0)           # left neighbour's rows to its right
-            right = sends[r + 1][0] if r + 1 < self.R else (0, 0)
-            rows += left[1] + right[1]
-            g.world_submit([left, right])
-        return rows
+            self.ticks.append([(self.upload(r, o), len(o)) for r, o in enumerate(self.split(ops, xb))])
 
     def step(self, t):
         """One tick of every rank; returns (per-rank seconds, updates, events, records, halo rows)."""
         times = [0.0] * self.R
         ptrs = [p for p, _ in self.ticks[t]]
         ms = [m for _, m in self.ticks[t]]
-        rows = self._route_submit(ptrs, ms, times)
+        rows = self.route_submit(ptrs, ms, times)
         upd = ev = rec = 0
         for r, g in enumerate(self.g):
             g.synchronize()
@@ -140,14 +87,8 @@ class SimWorld:
         return times, upd, ev, rec, rows
 
     def close(self):
-        for r, g in enumerate(self.g):
-            ov, bad, bad_ops = g.world_status()
-            if ov or bad or bad_ops:
-                raise RuntimeError(f"rank {r}: contract counters {ov} {bad} {bad_ops}")
-        for r, p in self.bufs:
-            self.g[r].dev_free(p)
-        for g in self.g:
-            g.close()
+        self.check()
+        super().close()
 
 
 def main():

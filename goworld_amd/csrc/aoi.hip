@@ -540,6 +540,10 @@ struct GlobalSrc {
     __device__ __forceinline__ Flat flat(const SpaceP& P, const Rects& R) const { return flat_build<2>(P, R, GS, MS); }
     __device__ __forceinline__ GEnt gn(uint32_t i) const { return GN[i]; }
     __device__ __forceinline__ MEnt gm(uint32_t i) const { return GM[i]; }
+    // entry i of the grid (kind 0) or the mover grid (kind 1) as 16-B words
+    __device__ __forceinline__ const uint4* ptr(uint32_t kind, uint32_t i) const {
+        return kind ? (const uint4*)(GM + i) : (const uint4*)(GN + i);
+    }
 };
 
 // One mover-grid entry m by one wave, candidates from S; lds: SCAP sort slots
@@ -590,25 +594,37 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
         uint32_t idx[DIFF_U], kd[DIFF_U];
         if (walk) flat_map_walk<DIFF_U, 2>(f, base, idx, kd);
         else flat_map<DIFF_U, 2>(f, base, idx, kd);
+        // branch-free candidate loads: every lane reads two 16-B words from its
+        // grid's entry (a gn entry twice), lanes past the end read lane 0's, so
+        // the loads of all DIFF_U chunks are in flight before the first is used
+        // (a divergent gn / gm branch made each chunk wait out its own loads)
+        uint4 q0[DIFF_U], q1[DIFF_U];
+#pragma unroll
+        for (int u = 0; u < DIFF_U; ++u) {
+            if (base + 64u * u >= f.total) break;              // wave-uniform
+            const uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx[u]);
+            const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)kd[u]);
+            const bool valid = idx[u] != ~0u;
+            const uint4* p = S.ptr(valid ? kd[u] : k0, valid ? idx[u] : i0);
+            q0[u] = p[0];
+            q1[u] = p[(valid ? kd[u] : k0) ? 1 : 0];
+        }
         Cand cc[DIFF_U];
 #pragma unroll
         for (int u = 0; u < DIFF_U; ++u) {
-            cc[u].info = 0;
-            cc[u].slot = A;                                    // invalid unless loaded below
-            if (idx[u] != ~0u) {
-                if (kd[u] == 0) {
-                    const GEnt e = S.gn(idx[u]);
-                    cc[u].x = cc[u].ox = e.x;
-                    cc[u].z = cc[u].oz = e.z;
-                    cc[u].slot = (e.meta & b.mbit) ? A : e.slot;      // movers come from gm
-                    cc[u].info = TAG_OLD | TAG_NEW | (e.meta & CLIENT_BIT ? CAND_CLIENT : 0u) | CAND_NONMOVER;
-                } else {
-                    const MEnt e = S.gm(idx[u]);
-                    cc[u].x = e.x; cc[u].z = e.z; cc[u].ox = e.ox; cc[u].oz = e.oz;
-                    cc[u].slot = e.slot;
-                    cc[u].info = e.tags | (e.client ? CAND_CLIENT : 0u);
-                }
-            }
+            if (base + 64u * u >= f.total) break;              // wave-uniform
+            const bool gm = kd[u] != 0;
+            const uint32_t meta = q0[u].w;                     // gn: x z slot meta; gm: x z ox oz | slot tags client space
+            cc[u].x = __uint_as_float(q0[u].x);
+            cc[u].z = __uint_as_float(q0[u].y);
+            cc[u].ox = gm ? __uint_as_float(q0[u].z) : cc[u].x;
+            cc[u].oz = gm ? __uint_as_float(q0[u].w) : cc[u].z;
+            const uint32_t slot = gm ? q1[u].x : ((meta & b.mbit) ? A : q0[u].z);   // movers come from gm
+            const uint32_t info = gm ? (q1[u].y | (q1[u].z ? CAND_CLIENT : 0u))
+                                     : (TAG_OLD | TAG_NEW | (meta & CLIENT_BIT ? CAND_CLIENT : 0u) | CAND_NONMOVER);
+            const bool valid = idx[u] != ~0u;
+            cc[u].slot = valid ? slot : A;                     // invalid: skipped below
+            cc[u].info = valid ? info : 0u;
         }
 #pragma unroll
         for (int u = 0; u < DIFF_U; ++u) {

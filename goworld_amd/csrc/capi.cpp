@@ -242,13 +242,66 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     return 0;
 }
 
-// write seq=-1 and space id for a new space's slots (AoiEnt.meta)
-int init_space_slots(gw_ctx* c, uint32_t base, uint32_t cap, uint32_t sid) {
-    std::vector<AoiEnt> h(cap);
-    for (uint32_t i = 0; i < cap; ++i) { h[i].x = 0; h[i].z = 0; h[i].seq = -1; h[i].meta = sid; }
-    HIPCHK(hipMemcpyAsync(c->aoi + base, h.data(), cap * sizeof(AoiEnt), hipMemcpyHostToDevice, c->st));
+World world(gw_ctx* c);
+
+// slots [base, base + n): absent, in space `sid`, every other per-slot array
+// cleared (a reused range, or fresh zeros from grow_slots)
+int init_space_slots(gw_ctx* c, uint32_t base, uint32_t n, uint32_t sid) {
+    launch_slots_clear(world(c), c->ol, c->eid_dev, c->cid_dev, base, n, sid, c->st);
+    HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
+}
+
+// ---- free ranges of the space lifecycle ------------------------------------
+// first fit among the released ranges, else at the end (total grows); the
+// caller checks the limit on the returned end before committing (commit=false
+// only looks)
+uint32_t take_range(std::map<uint32_t, uint32_t>& fr, uint32_t total, uint32_t n, bool commit, uint32_t* new_total) {
+    for (auto it = fr.begin(); it != fr.end(); ++it)
+        if (it->second >= n) {
+            const uint32_t base = it->first, len = it->second;
+            if (commit) {
+                fr.erase(it);
+                if (len > n) fr[base + n] = len - n;
+            }
+            *new_total = total;
+            return base;
+        }
+    *new_total = total + n;
+    return total;
+}
+
+// release [base, base + n): merged with its neighbours; a range that reaches
+// the end shrinks the total instead
+void give_range(std::map<uint32_t, uint32_t>& fr, uint32_t& total, uint32_t base, uint32_t n) {
+    if (!n) return;
+    auto nx = fr.lower_bound(base);
+    if (nx != fr.end() && nx->first == base + n) {
+        n += nx->second;
+        nx = fr.erase(nx);
+    }
+    if (nx != fr.begin()) {
+        auto pv = std::prev(nx);
+        if (pv->first + pv->second == base) {
+            base = pv->first;
+            n += pv->second;
+            fr.erase(pv);
+        }
+    }
+    if (base + n == total) {
+        total = base;
+        // a free range may now end at the new total
+        if (!fr.empty()) {
+            auto last = std::prev(fr.end());
+            if (last->first + last->second == total) {
+                total = last->first;
+                fr.erase(last);
+            }
+        }
+    } else {
+        fr[base] = n;
+    }
 }
 
 int upload_spaces(gw_ctx* c) {
@@ -497,7 +550,7 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
     if (!(aoi_dist > 0) || !std::isfinite(aoi_dist))
         return set_err(c, GW_EINVAL, "defaultAOIDistance <= 0");          // Space.go:92-94
     if (capacity == 0) return set_err(c, GW_EINVAL, "capacity must be > 0");
-    if ((uint64_t)c->total_slots + capacity >= (1ull << 31)) return set_err(c, GW_ERANGE, "too many slots");
+    if (!c->segs.empty()) return set_err(c, GW_ESTATE, "space create with ops pending: tick first");
     float b[4] = {-1000.f, -1000.f, 1000.f, 1000.f};                       // Space.GetSpaceRange, Space.go:52-54
     if (bounds) for (int i = 0; i < 4; ++i) b[i] = bounds[i];
     if (!(b[2] > b[0]) || !(b[3] > b[1]) || !std::isfinite(b[0]) || !std::isfinite(b[1]) || !std::isfinite(b[2]) ||
@@ -516,7 +569,6 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
     SpaceHost s{};
     s.d = aoi_dist;
     s.cap = capacity;
-    s.base = c->total_slots;
     s.alive = true;
     s.p.d = aoi_dist;
     s.p.x0 = b[0];
@@ -524,24 +576,41 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
     s.p.inv_cs = (float)(1.0 / cs);
     s.p.W = std::max(1, (int)std::ceil(ex / cs));
     s.p.H = std::max(1, (int)std::ceil(ez / cs));
-    s.p.cell_base = c->total_cells;
     s.p.alive = 1;
     s.p.own_lo = -INFINITY;
     s.p.own_hi = INFINITY;
     uint64_t ncells = (uint64_t)s.p.W * (uint64_t)s.p.H;
-    if ((uint64_t)c->total_cells + ncells + 1 > CELL_MASK) return set_err(c, GW_ERANGE, "too many grid cells");
+    if (ncells >= CELL_MASK) return set_err(c, GW_ERANGE, "too many grid cells");
+    // slot and cell ranges: a released range first (first fit), else at the end
+    uint32_t nt_slots = 0, nt_cells = 0;
+    const uint32_t base = take_range(c->free_slots, c->total_slots, capacity, false, &nt_slots);
+    const uint32_t cbase = take_range(c->free_cells, c->total_cells, (uint32_t)ncells, false, &nt_cells);
+    if ((uint64_t)base + capacity >= (1ull << 31) || (uint64_t)nt_slots >= (1ull << 31))
+        return set_err(c, GW_ERANGE, "too many slots");
+    if ((uint64_t)cbase + ncells + 1 > CELL_MASK || (uint64_t)nt_cells + 1 > CELL_MASK)
+        return set_err(c, GW_ERANGE, "too many grid cells");
     int rc;
-    if ((rc = grow_slots(c, c->total_slots + capacity))) return rc;
-    uint32_t sid = (uint32_t)c->spaces.size();
-    if ((rc = init_space_slots(c, s.base, capacity, sid))) return rc;
-    c->spaces.push_back(s);
-    c->total_slots += capacity;
-    c->total_cells += (uint32_t)ncells;
+    if ((rc = grow_slots(c, nt_slots))) return rc;
+    // a destroyed space's id is handed out again (lowest first)
+    uint32_t sid = 0;
+    while (sid < c->spaces.size() && c->spaces[sid].alive) ++sid;
+    if ((rc = init_space_slots(c, base, capacity, sid))) return rc;
+    (void)take_range(c->free_slots, c->total_slots, capacity, true, &nt_slots);
+    (void)take_range(c->free_cells, c->total_cells, (uint32_t)ncells, true, &nt_cells);
+    c->total_slots = nt_slots;
+    c->total_cells = nt_cells;
+    s.base = base;
+    s.p.cell_base = cbase;
+    if (sid == c->spaces.size()) c->spaces.push_back(s);
+    else c->spaces[sid] = s;
     c->grid_dirty = true;
-    for (uint32_t i = 0; i < capacity; ++i) c->space_of_h[s.base + i] = (int32_t)sid;
+    for (uint32_t i = 0; i < capacity; ++i) {
+        c->space_of_h[base + i] = (int32_t)sid;
+        c->present_h[base + i] = 0;
+    }
     if ((rc = upload_spaces(c))) return rc;
     if (space_id) *space_id = sid;
-    if (slot_base) *slot_base = s.base;
+    if (slot_base) *slot_base = base;
     return 0;
 }
 
@@ -585,18 +654,148 @@ int gw_space_restore(gw_ctx* c, uint32_t sid, const uint32_t* slots, const float
     return 0;
 }
 
+// entities present in a space's slot range, counted on the device (after
+// device-resident submits the host mirror is not exact)
+static int count_present(gw_ctx* c, uint32_t base, uint32_t n, uint64_t* out) {
+    HIPCHK(hipMemsetAsync(c->scal32, 0, 8, c->st));
+    launch_count_present(c->aoi, base, n, (unsigned long long*)c->scal32, c->st);
+    HIPCHK(hipGetLastError());
+    unsigned long long v = 0;
+    HIPCHK(hipMemcpyAsync(&v, c->scal32, 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    *out = v;
+    return 0;
+}
+
+// host mirrors of slots [base, base + n) -> nothing (released) or -> [to, to + n) (moved)
+static void move_host_slots(gw_ctx* c, uint32_t base, uint32_t n, int64_t to) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t s = base + i;
+        const gw::host::Id16 id = c->eid_h[s];
+        if (to >= 0) {
+            const uint32_t d = (uint32_t)to + i;
+            c->present_h[d] = c->present_h[s];
+            c->eid_h[d] = id;
+            c->syncing_h[d] = c->syncing_h[s];
+            if (id.a | id.b) c->id_slot[id] = d;
+        } else if (id.a | id.b) {
+            auto it = c->id_slot.find(id);
+            if (it != c->id_slot.end() && it->second == s) c->id_slot.erase(it);
+        }
+        c->present_h[s] = 0;
+        c->eid_h[s] = gw::host::Id16{0, 0};
+        c->syncing_h[s] = 0;
+        c->space_of_h[s] = -1;
+    }
+}
+
+// Space.OnDestroy destroys every entity first (Space.go:143-151: each
+// Destroy is a Space.leave -> aoiMgr.Leave, ticked before this call), then
+// SpaceManager.delSpace (SpaceManager.go:25-27).  Always checked on the
+// device: destroying a space that still holds an entity is an error.  Its
+// slot and cell ranges are cleared (pending sync flags of entities that left
+// it into the nil space go with them: collect first) and reused.
 int gw_space_destroy(gw_ctx* c, uint32_t sid) {
     if (!c) return GW_EINVAL;
     if (int rs = settle(c)) return rs;
+    (void)hipSetDevice(c->dev);
     if (sid >= c->spaces.size() || !c->spaces[sid].alive) return set_err(c, GW_ERANGE, "no space %u", sid);
+    if (!c->segs.empty()) return set_err(c, GW_ESTATE, "space destroy with ops pending: tick first");
     SpaceHost& s = c->spaces[sid];
-    if (c->validate) {
-        for (uint32_t i = 0; i < s.cap; ++i)
-            if (c->present_h[s.base + i]) return set_err(c, GW_ESTATE, "space %u not empty", sid);
-    }
+    if (c->wd.on && sid == c->wd.sid) return set_err(c, GW_ESTATE, "space %u is the context's world strip", sid);
+    uint64_t np = 0;
+    int rc;
+    if ((rc = count_present(c, s.base, s.cap, &np))) return rc;
+    if (np) return set_err(c, GW_ESTATE, "space %u not empty (%llu entities)", sid, (unsigned long long)np);
+    launch_slots_clear(world(c), c->ol, c->eid_dev, c->cid_dev, s.base, s.cap, sid, c->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->st));
+    move_host_slots(c, s.base, s.cap, -1);
+    give_range(c->free_slots, c->total_slots, s.base, s.cap);
+    give_range(c->free_cells, c->total_cells, s.p.cell_base, (uint32_t)(s.p.W * s.p.H));
     s.alive = false;
     s.p.alive = 0;
+    c->grid_dirty = true;
+    ++c->epoch;
     return upload_spaces(c);
+}
+
+// Space.enter adds entities without bound (Space.go:179-217): capacity grows
+// in place when the slots behind the space are free, else the space's state
+// moves to a new range (its slots change: new_base; events and records of
+// later calls carry the new slots).  No ops may be pending.
+int gw_space_grow(gw_ctx* c, uint32_t sid, uint32_t new_capacity, uint32_t* new_base) {
+    if (!c) return GW_EINVAL;
+    if (int rs = settle(c)) return rs;
+    (void)hipSetDevice(c->dev);
+    if (sid >= c->spaces.size() || !c->spaces[sid].alive) return set_err(c, GW_ERANGE, "no space %u", sid);
+    if (!c->segs.empty()) return set_err(c, GW_ESTATE, "space grow with ops pending: tick first");
+    SpaceHost& s = c->spaces[sid];
+    if (new_capacity < s.cap) return set_err(c, GW_EINVAL, "capacity %u below the current %u", new_capacity, s.cap);
+    if (new_base) *new_base = s.base;
+    if (new_capacity == s.cap) return 0;
+    const uint32_t delta = new_capacity - s.cap, end = s.base + s.cap;
+    int rc;
+    // in place: the space is last, or a released range starts right behind it
+    auto nx = c->free_slots.find(end);
+    const bool at_end = end == c->total_slots;
+    if (at_end || (nx != c->free_slots.end() && nx->second >= delta)) {
+        if ((uint64_t)end + delta >= (1ull << 31)) return set_err(c, GW_ERANGE, "too many slots");
+        if (at_end) {
+            if ((rc = grow_slots(c, end + delta))) return rc;
+        }
+        if ((rc = init_space_slots(c, end, delta, sid))) return rc;
+        if (at_end) {
+            c->total_slots = end + delta;
+        } else {
+            const uint32_t len = nx->second;
+            c->free_slots.erase(nx);
+            if (len > delta) c->free_slots[end + delta] = len - delta;
+        }
+        for (uint32_t i = 0; i < delta; ++i) c->space_of_h[end + i] = (int32_t)sid;
+        s.cap = new_capacity;
+        c->grid_dirty = true;
+        return 0;
+    }
+    if (c->wd.on && sid == c->wd.sid)
+        return set_err(c, GW_ESTATE, "a world strip keeps slot = entity id: it cannot move (grow it in place)");
+    uint32_t nt = 0;
+    const uint32_t nb = take_range(c->free_slots, c->total_slots, new_capacity, false, &nt);
+    if ((uint64_t)nb + new_capacity >= (1ull << 31) || (uint64_t)nt >= (1ull << 31))
+        return set_err(c, GW_ERANGE, "too many slots");
+    if ((rc = grow_slots(c, nt))) return rc;
+    (void)take_range(c->free_slots, c->total_slots, new_capacity, true, &nt);
+    c->total_slots = nt;
+    const World w = world(c);
+    launch_slots_clear(w, c->ol, c->eid_dev, c->cid_dev, nb + s.cap, delta, sid, c->st);
+    launch_slots_move(w, c->ol, c->eid_dev, c->cid_dev, s.base, nb, s.cap, c->st);
+    launch_slots_clear(w, c->ol, c->eid_dev, c->cid_dev, s.base, s.cap, sid, c->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->st));
+    const uint32_t ob = s.base, oc = s.cap;
+    move_host_slots(c, ob, oc, nb);
+    for (uint32_t i = 0; i < new_capacity; ++i) c->space_of_h[nb + i] = (int32_t)sid;
+    give_range(c->free_slots, c->total_slots, ob, oc);
+    s.base = nb;
+    s.cap = new_capacity;
+    c->grid_dirty = true;
+    ++c->epoch;
+    if (new_base) *new_base = nb;
+    return 0;
+}
+
+int gw_context_info(gw_ctx* c, gw_ctx_info* out) {
+    if (!c || !out) return GW_EINVAL;
+    memset(out, 0, sizeof *out);
+    out->total_slots = c->total_slots;
+    out->total_cells = c->total_cells;
+    for (auto& sp : c->spaces)
+        if (sp.alive) {
+            ++out->live_spaces;
+            out->live_slots += sp.cap;
+            out->live_cells += (uint32_t)(sp.p.W * sp.p.H);
+        }
+    return 0;
 }
 
 int gw_submit(gw_ctx* c, const gw_op* ops, uint32_t n) {

@@ -6,6 +6,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <map>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -102,6 +103,9 @@ struct gw_ctx {
 
     std::vector<SpaceHost> spaces;
     uint32_t total_slots = 0, slot_cap = 0, total_cells = 0;
+    // slot / cell ranges of destroyed (or moved) spaces, base -> length, all
+    // below total_slots / total_cells and cleared: handed out first-fit
+    std::map<uint32_t, uint32_t> free_slots, free_cells;
     uint32_t mpar = 0;                 // parity of the incremental grid rebuilds (TickBufs::mbit)
     uint16_t max_gate = 0;
     unsigned long long stamp_base = 1;   // global op counter (stamp 0 = never)

@@ -361,5 +361,11 @@ struct WirePacket {              // one gate's packet of the wire encode
 void launch_wire_encode(const gw_sync_record* rec, uint64_t R, const WirePacket* pk, uint32_t npk,
                         const uint4* eid, const uint4* cid, uint32_t* out, hipStream_t s);
 void launch_fill_i32(int32_t* p, int32_t v, uint64_t n, hipStream_t s);
+// space lifecycle (space.hip): move a slot range's state, clear a range, count present entities
+void launch_slots_move(const World& w, OpLast* ol, uint4* eid, uint4* cid, uint32_t src, uint32_t dst, uint32_t n,
+                       hipStream_t s);
+void launch_slots_clear(const World& w, OpLast* ol, uint4* eid, uint4* cid, uint32_t base, uint32_t n,
+                        uint32_t meta, hipStream_t s);
+void launch_count_present(const AoiEnt* aoi, uint32_t base, uint32_t n, unsigned long long* out, hipStream_t s);
 
 }  // namespace gw

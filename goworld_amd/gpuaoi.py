@@ -80,6 +80,11 @@ class WorldGeom(C.Structure):
                 ("ranks", _u32), ("rank", _u32)]
 
 
+class CtxInfo(C.Structure):
+    _fields_ = [("total_slots", _u32), ("live_slots", _u32), ("total_cells", _u32), ("live_cells", _u32),
+                ("live_spaces", _u32), ("reserved", _u32)]
+
+
 COMM_ID_BYTES = 128
 RED_SUM, RED_MAX = 0, 1
 
@@ -115,6 +120,8 @@ def lib():
         L.gw_last_error.restype = C.c_char_p
         L.gw_space_create.argtypes = [vp, C.c_float, _u32, vp, C.POINTER(_u32), C.POINTER(_u32)]
         L.gw_space_destroy.argtypes = [vp, _u32]
+        L.gw_space_grow.argtypes = [vp, _u32, _u32, C.POINTER(_u32)]
+        L.gw_context_info.argtypes = [vp, C.POINTER(CtxInfo)]
         L.gw_submit.argtypes = [vp, vp, _u32]
         L.gw_submit_device.argtypes = [vp, vp, _u32]
         L.gw_set_clients.argtypes = [vp, vp, vp, _u32]
@@ -168,7 +175,8 @@ EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_spa
             "gw_client_events", "gw_fanout", "gw_comm_unique_id", "gw_comm_init", "gw_comm_info",
             "gw_comm_exchange", "gw_comm_allreduce_u64", "gw_world_create", "gw_world_step", "gw_world_route",
             "gw_world_submit", "gw_world_status", "gw_set_entity_ids", "gw_clear_entity_ids", "gw_set_client_ids",
-            "gw_set_client_syncing", "gw_submit_client_sync", "gw_sync_encode_wire"]
+            "gw_set_client_syncing", "gw_submit_client_sync", "gw_sync_encode_wire", "gw_space_grow",
+            "gw_context_info"]
 
 
 def comm_unique_id() -> bytes:
@@ -274,7 +282,21 @@ class GpuAOI:
         return sid.value, base.value
 
     def destroy_space(self, sid: int):
+        """SpaceManager.delSpace after Space.OnDestroy (the space must be empty)."""
         self._chk(lib().gw_space_destroy(self._h, sid))
+        self.spaces = [t for t in self.spaces if t[0] != sid]
+
+    def grow_space(self, sid: int, capacity: int) -> int:
+        """Grow space sid to `capacity` slots; returns its (possibly new) first slot."""
+        nb = _u32()
+        self._chk(lib().gw_space_grow(self._h, sid, int(capacity), C.byref(nb)))
+        self.spaces = [(i, nb.value, capacity) if i == sid else (i, b, cp) for i, b, cp in self.spaces]
+        return nb.value
+
+    def context_info(self) -> dict:
+        o = CtxInfo()
+        self._chk(lib().gw_context_info(self._h, C.byref(o)))
+        return {k: getattr(o, k) for k, _ in CtxInfo._fields_ if k != "reserved"}
 
     def restore(self, sid: int, slots, x, y, z, yaw, flags: int = 3):
         """Bulk Enter in index order without events (restore path, Space.go:209-214)."""

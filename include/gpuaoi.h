@@ -32,10 +32,11 @@
  *     ABI.  The Go shim turns errors into gwlog.Panicf, as the reference panics
  *     on misuse (Space.go:92-102, 184-186, 220-222).
  *   - Slots are GLOBAL per context: a space owns slots
- *     [slot_base, slot_base + capacity) returned by gw_space_create.  Events
- *     and sync records carry global slots.  Canonical order over global slots
- *     equals (space, local slot) order because slot ranges are allocated in
- *     space-id order.
+ *     [slot_base, slot_base + capacity) returned by gw_space_create (or
+ *     gw_space_grow, which may move them).  Events and sync records carry
+ *     global slots, in canonical order over global slots.  Ranges are handed
+ *     out first-fit (a destroyed space's range is reused), so without destroys
+ *     or moves this is (space, local slot) order.
  *   - One host thread per context; not re-entrant (the reference calls AOI only
  *     from the single game goroutine, GameService.go:89-189).
  *   - Output pointers in gw_tick_out / gw_sync_out are owned by the library and
@@ -181,7 +182,30 @@ const char* gw_last_error(const gw_ctx* ctx);
  * outside the bounds are still exact (clamped cells), only slower. */
 int  gw_space_create(gw_ctx* ctx, float aoi_dist, uint32_t capacity,
                      const float* bounds, uint32_t* space_id, uint32_t* slot_base);
-int  gw_space_destroy(gw_ctx* ctx, uint32_t space_id);   /* space must be empty */
+/* Space.OnDestroy -> SpaceManager.delSpace (Space.go:143-151,
+ * SpaceManager.go:25-27; goworld.go:52-60 creates spaces at run time): the
+ * space must hold no entity (checked on the device; its entities Leave and
+ * are ticked first, as Space.OnDestroy destroys them); its slot and cell
+ * ranges are cleared and reused by later creates, its id too. */
+int  gw_space_destroy(gw_ctx* ctx, uint32_t space_id);
+/* Space.enter has no capacity bound (Space.go:179-217): grow a space to
+ * new_capacity slots.  In place when the slots behind it are free (its slots
+ * stay), else its state moves to a new range and *new_base receives the new
+ * first slot (slot base + i -> new_base + i; the tick / collect outputs of
+ * later calls carry the new slots).  No ops may be pending; a world strip
+ * grows in place only. */
+int  gw_space_grow(gw_ctx* ctx, uint32_t space_id, uint32_t new_capacity, uint32_t* new_base);
+
+/* Slot / cell accounting of the context (capacity-proportional passes run
+ * over total_slots and total_cells). */
+typedef struct gw_ctx_info {
+    uint32_t total_slots;   /* slot range in use: every live space ends below it */
+    uint32_t live_slots;    /* capacity of the live spaces                        */
+    uint32_t total_cells, live_cells;
+    uint32_t live_spaces;
+    uint32_t reserved;
+} gw_ctx_info;
+int  gw_context_info(gw_ctx* ctx, gw_ctx_info* out);
 
 /* Buffer ops (host memory, validated against the entity state; copied). */
 int  gw_submit(gw_ctx* ctx, const gw_op* ops, uint32_t n);
@@ -464,7 +488,7 @@ int  gw_world_submit(gw_ctx* ctx, const gw_halo_row* const recv[2], const uint32
 int  gw_world_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops);
 
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 10
+#define GW_ABI_VERSION 11
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

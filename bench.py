@@ -65,6 +65,9 @@ def parse():
                     help="guard on the single-thread baseline (it replays one full tick)")
     ap.add_argument("--e2e-steps", type=int, default=4, help="untimed end-to-end steps (host in/out; the first is "
                                                                  "a warm-up)")
+    ap.add_argument("--e2e-wire", type=int, default=1,
+                    help="1: the end-to-end steps also encode and copy the 48-B game->gate wire records "
+                         "(gw_sync_encode_wire, what the Go shim's Collect hands to the gates)")
     ap.add_argument("--profile-stages", type=int, default=1,
                     help="1: HIP events around the dominant kernel's stage in the timed region (roofline) and "
                          "a per-stage breakdown over extra untimed steps; 0: none")
@@ -369,9 +372,20 @@ class SpaceRun:
         records out to pinned host buffers (GW_TICK_COPY_TO_HOST /
         GW_SYNC_COPY_TO_HOST), i.e. PCIe both ways."""
         g = self.g
+        c0 = time.perf_counter()
         g.submit(self.host_ticks[t])
+        c1 = time.perf_counter()
         r = g.tick(copy=True, view=True)
+        c2 = time.perf_counter()
         s = g.sync_collect(copy=True, by_client=self.by_client, view=True)
+        c3 = time.perf_counter()
+        self.e2e_parts = {"submit": c1 - c0, "tick": c2 - c1, "collect": c3 - c2,
+                          "tick_device_us": r.device_us, "collect_device_us": s.device_us,
+                          "ops_bytes": len(self.host_ticks[t]) * traces.OP_DTYPE.itemsize,
+                          "event_bytes": 8 * (r.n_enter + r.n_leave), "record_bytes": 24 * s.n_rec}
+        if getattr(self, "e2e_wire", False):               # the Go shim's Collect: 48-B wire records to the host
+            data, pk, nb, dev_us = g.encode_wire(copy=True)
+            self.e2e_parts.update(wire=time.perf_counter() - c3, wire_bytes=nb, wire_device_us=dev_us)
         return r.movers, r, s
 
     def close(self):
@@ -691,17 +705,34 @@ def main():
         # allocates the pinned host buffers, untimed)
         t_e, e_ops = 0.0, 0
         t_first = W + K + extra + cm
+        run.e2e_wire = a.e2e_wire
         run.step_e2e(t_first)
+        parts = {}
         for t in range(t_first + 1, t_first + n_e2e):
             g.synchronize()
             c0 = time.perf_counter()
             upd, r, s_ = run.step_e2e(t)
             t_e += time.perf_counter() - c0
             e_ops += upd
-        e2e = {"ms_per_step": t_e / (n_e2e - 1) * 1e3, "updates_per_sec": e_ops / t_e, "steps": n_e2e - 1,
-               "what": "gw_submit(host ops) + gw_tick(COPY_TO_HOST) + gw_sync_collect(COPY_TO_HOST): the Go "
-                       "caller's tick, events and compact records copied to pinned host memory (PCIe); "
-                       "wall clock, untimed by the headline"}
+            for k, v in run.e2e_parts.items():
+                parts[k] = parts.get(k, 0.0) + v
+        n2 = n_e2e - 1
+        pa = {k: v / n2 for k, v in parts.items()}
+        e2e = {"ms_per_step": t_e / n2 * 1e3, "updates_per_sec": e_ops / t_e, "steps": n2,
+               "breakdown_ms": {k: round(pa[k] * 1e3, 3) for k in ("submit", "tick", "collect", "wire") if k in pa},
+               "device_ms": {"tick": round(pa["tick_device_us"] / 1e3, 3),
+                             "collect": round(pa["collect_device_us"] / 1e3, 3)},
+               "bytes_per_step": {"ops_h2d": pa["ops_bytes"], "events_d2h": pa["event_bytes"],
+                                  "records_d2h": pa["record_bytes"], **({"wire_d2h": pa["wire_bytes"]}
+                                                                         if "wire_bytes" in pa else {})},
+               "pcie_GBps": {"collect": round(pa["record_bytes"] / pa["collect"] / 1e9, 2),
+                             "tick": round(pa["event_bytes"] / pa["tick"] / 1e9, 2),
+                             **({"wire": round(pa["wire_bytes"] / pa["wire"] / 1e9, 2)} if "wire" in pa else {})},
+               "what": "gw_submit(host ops) + gw_tick(COPY_TO_HOST) + gw_sync_collect(COPY_TO_HOST)"
+                       + (" + gw_sync_encode_wire(COPY_TO_HOST)" if a.e2e_wire else "")
+                       + ": the Go caller's tick, events and records to pinned host memory (PCIe); wall clock "
+                         "per call (device_ms: HIP events of the same calls, copies included); untimed by the "
+                         "headline"}
     parallelism, n_world, m_rank = run.parallelism, run.n_world, run.m
     run.close()
     def world_leg(which, warmup, steps, workload):

@@ -801,12 +801,21 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     uint64_t* mir = b.mir + reg;
     uint32_t n = 0, nl = 0, nm_ = 0, nml = 0;
     uint32_t c_old = 0, c_new = 0, c_cli = 0;
+    // the half's first candidate (its first non-empty range): what a lane past
+    // the half's end reads
+    const uint32_t f_lane = (uint32_t)__builtin_ctzll((wave_ballot(rl != 0) & hmask) | (1ull << 63));
+    const uint32_t f_idx = (uint32_t)__shfl((int)rs, (int)f_lane, 64);
+    const uint32_t f_kind = f_lane & 1u;
     for (uint32_t base = 0; base < tmax; base += 32u * HU) {   // wave-uniform
-        Cand cc[HU];
+        // candidate loads without a divergent gn / gm branch (see mover_one):
+        // a lane past its half's end reads its half's first candidate
+        uint4 q0[HU], q1[HU];
+        uint32_t kind[HU];
+        bool in[HU];
 #pragma unroll
         for (int u = 0; u < HU; ++u) {
-            cc[u].info = 0;
-            cc[u].slot = A;
+            in[u] = false;
+            kind[u] = 0;
             if (base + 32u * u >= tmax) continue;            // wave-uniform
             const uint32_t kk = base + 32u * u + hl;
             uint32_t l2 = 0;
@@ -818,21 +827,32 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
             }
             const uint32_t ss = (uint32_t)__shfl((int)rs, (int)(hb + l2), 64);
             const uint32_t sp = (uint32_t)__shfl((int)pre, (int)(hb + l2), 64);
-            if (kk < total) {
-                const uint32_t idx = ss + (kk - sp);
-                if ((l2 & 1u) == 0) {
-                    const GEnt e = GN[idx];
-                    cc[u].x = cc[u].ox = e.x;
-                    cc[u].z = cc[u].oz = e.z;
-                    cc[u].slot = (e.meta & b.mbit) ? A : e.slot;
-                    cc[u].info = TAG_OLD | TAG_NEW | (e.meta & CLIENT_BIT ? CAND_CLIENT : 0u) | CAND_NONMOVER;
-                } else {
-                    const MEnt e = GM[idx];
-                    cc[u].x = e.x; cc[u].z = e.z; cc[u].ox = e.ox; cc[u].oz = e.oz;
-                    cc[u].slot = e.slot;
-                    cc[u].info = e.tags | (e.client ? CAND_CLIENT : 0u);
-                }
-            }
+            in[u] = kk < total;
+            const bool use = in[u];
+            kind[u] = use ? (l2 & 1u) : f_kind;
+            const uint32_t idx = use ? ss + (kk - sp) : f_idx;
+            const uint4* p = kind[u] ? (const uint4*)(GM + idx) : (const uint4*)(GN + idx);
+            const bool any = total != 0;                       // a half with no candidates reads nothing
+            q0[u] = any ? p[0] : make_uint4(0u, 0u, 0u, 0u);
+            q1[u] = any ? p[kind[u]] : make_uint4(0u, 0u, 0u, 0u);
+        }
+        Cand cc[HU];
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+            cc[u].info = 0;
+            cc[u].slot = A;
+            if (base + 32u * u >= tmax) continue;            // wave-uniform
+            const bool gmk = kind[u] != 0;
+            const uint32_t meta = q0[u].w;
+            cc[u].x = __uint_as_float(q0[u].x);
+            cc[u].z = __uint_as_float(q0[u].y);
+            cc[u].ox = gmk ? __uint_as_float(q0[u].z) : cc[u].x;
+            cc[u].oz = gmk ? __uint_as_float(q0[u].w) : cc[u].z;
+            const uint32_t slot = gmk ? q1[u].x : ((meta & b.mbit) ? A : q0[u].z);
+            const uint32_t info = gmk ? (q1[u].y | (q1[u].z ? CAND_CLIENT : 0u))
+                                      : (TAG_OLD | TAG_NEW | (meta & CLIENT_BIT ? CAND_CLIENT : 0u) | CAND_NONMOVER);
+            cc[u].slot = in[u] ? slot : A;
+            cc[u].info = in[u] ? info : 0u;
         }
 #pragma unroll
         for (int u = 0; u < HU; ++u) {
@@ -926,6 +946,30 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
         }
     }
     return true;
+}
+
+// General mode, two mover-grid entries per wave: a short candidate list
+// (config #3's uniform background, config #5: ~50 candidates) pays the
+// per-mover setup (rects, row ranges, scan, sort, writes) for half a wave;
+// a pair with a longer list (hotspots: own events sorted in LDS, not by the
+// half-wave register sort) or more rows than a half holds, or two spaces, runs
+// both entries through mover_one, one after the other.
+template <int DIFF_U>
+__global__ void __launch_bounds__(64) k_mover_pair(TickBufs b) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[SORT_LDS];
+    const uint64_t m0 = (uint64_t)blockIdx.x * 2;
+    const uint64_t ngm = b.st->n_gm;
+    if (m0 >= ngm) return;
+    const uint64_t m1 = min(m0 + 2, ngm);
+    const GlobalSrc src{b.w.gn, b.w.gn_start, b.gm_start, b.gm};
+    const uint64_t c0 = b.cand[m0], c1 = m0 + 1 < m1 ? b.cand[m0 + 1] : 0;
+    const uint32_t s0 = b.gm[m0].space, s1 = m0 + 1 < m1 ? b.gm[m0 + 1].space : s0;
+    if (max(c0, c1) <= b.pair_max && s0 == s1) {            // wave-uniform
+        if (mover_half<2>(b, m0, m1, b.w.sp[s0], src.GN, src.GS, src.MS, src.GM, lds)) return;
+    }
+    mover_one<DIFF_U, SORT_LDS>(b, m0, lds, src);
+    wave_sync();
+    if (m0 + 1 < m1) mover_one<DIFF_U, SORT_LDS>(b, m0 + 1, lds, src);
 }
 
 // Small-space mode (every space's grid fits in LDS: config #4's 10k spaces of
@@ -1720,6 +1764,10 @@ void tick_diff(const TickBufs& b, hipStream_t s) {
         const size_t lds = ((size_t)b.small_ents + (2 * ((size_t)b.small_cells + 1) + 3) / 4) * 16 +
                            (size_t)SMALL_GM * sizeof(MEnt);
         hipLaunchKernelGGL((k_mover_small<2>), dim3(b.n_spaces), dim3(NT), lds, s, b);
+        return;
+    }
+    if (b.pair_max) {                      // two short-list movers per wave (GW_PAIR_MAX, 0 = off)
+        hipLaunchKernelGGL((k_mover_pair<2>), dim3(nblk1(nmax, 2)), dim3(64), 0, s, b);
         return;
     }
     switch (b.diff_u) {                    // GW_MOVER_WPB: waves per k_mover block

@@ -495,6 +495,7 @@ int gw_init(int device_id, gw_ctx** out) {
         if (const char* e = getenv("GW_WALK_MIN")) c->walk_min = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_RANK_SORT")) c->rank_sort = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_GRID_CAP")) c->grid_cap = (uint32_t)std::max(0, atoi(e));
+        if (const char* e = getenv("GW_PAIR_MAX")) c->pair_max = (uint32_t)std::max(0, atoi(e));
     } while (0);
     if (rc) {
         (void)hipGetLastError();
@@ -1227,6 +1228,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.walk_min = c->walk_min;
     b.rank_sort = c->rank_sort;
     b.grid_cap = c->grid_cap;
+    b.pair_max = c->pair_max;
     b.ol = c->ol;
     b.st = st;
     b.gn_nxt = c->gnb[c->gcur ^ 1]; b.start_nxt = c->gsb[c->gcur ^ 1];

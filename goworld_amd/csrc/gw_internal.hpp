@@ -227,6 +227,8 @@ struct TickBufs {
     uint32_t* bk_split;       // [BK_NSPLIT] bucket bounds: quantiles of the last tick's keys
     int bk_bits;              // log2 of the bucket count (<= BK_MAXBITS, <= wbits + 1)
     uint64_t it_hint;         // bucket-path items of the last tick (sizes the flatten's grid)
+    uint32_t pair_max;        // GW_PAIR_MAX: k_mover_pair runs two movers per wave when both have at
+                              // most this many candidates (0 = one mover per wave, k_mover)
     uint32_t grid_cap;        // GW_GRID_CAP (tests): at most this many blocks for the grid-stride
                               // flatten / bucket tile passes (0 = no cap)
     int ev_full;              // 1: general stable radix sort instead of the bucket path

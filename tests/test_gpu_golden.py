@@ -156,3 +156,26 @@ def test_grid_stride_passes_capped(gpu, cap, monkeypatch):
         r = g.sync_collect()
         assert G.sha(canonical(r.records, tr.gates)) == exp["rec_sha"], f"tick {t}: records"
     g.close()
+
+
+@pytest.mark.parametrize("pair_max", [0, 1 << 20])
+def test_mover_pairing_modes(gpu, pair_max, monkeypatch):
+    """The diff runs two short-list movers per wave (k_mover_pair, default
+    GW_PAIR_MAX = 96 candidates) and longer ones one per wave (mover_one):
+    forcing either path for every mover gives the same config #2 digests."""
+    monkeypatch.setenv("GW_PAIR_MAX", str(pair_max))
+    name = "config2_100k"
+    d = G.digests()[name]
+    tr = G.DIGEST_TRACES[name]()
+    g = gpu()                                   # gw_init reads GW_PAIR_MAX
+    monkeypatch.delenv("GW_PAIR_MAX")
+    gpuaoi.load_space(g, tr)
+    for t, ops in enumerate(tr.ticks):
+        exp = d["ticks"][t]
+        g.submit(ops)
+        res = g.tick()
+        assert (res.n_enter, res.n_leave) == (exp["n_enter"], exp["n_leave"])
+        assert G.sha(res.enter) == exp["enter_sha"] and G.sha(res.leave) == exp["leave_sha"], f"tick {t}"
+        r = g.sync_collect()
+        assert G.sha(canonical(r.records, tr.gates)) == exp["rec_sha"], f"tick {t}: records"
+    g.close()

@@ -67,19 +67,27 @@ class SimWorld(dworld.LocalWorld):
         for ops, xb in tk:
             self.ticks.append([(self.upload(r, o), len(o)) for r, o in enumerate(self.split(ops, xb))])
 
-    def step(self, t):
-        """One tick of every rank; returns (per-rank seconds, updates, events, records, halo rows)."""
+    def step(self, t, phases=None):
+        """One tick of every rank; returns (per-rank seconds, updates, events, records, halo rows).
+        phases: dict accumulating host seconds per phase (route / tick call / collect call) over ranks."""
         times = [0.0] * self.R
         ptrs = [p for p, _ in self.ticks[t]]
         ms = [m for _, m in self.ticks[t]]
         rows = self.route_submit(ptrs, ms, times)
+        if phases is not None:
+            phases["route"] += sum(times)
         upd = ev = rec = 0
         for r, g in enumerate(self.g):
             g.synchronize()
             t0 = time.perf_counter()
             g.tick(copy=False, defer=True)
+            t1 = time.perf_counter()
             s = g.sync_collect(copy=False)
-            times[r] += time.perf_counter() - t0
+            t2 = time.perf_counter()
+            times[r] += t2 - t0
+            if phases is not None:
+                phases["tick_call"] += t1 - t0
+                phases["collect_call"] += t2 - t1
             res = g.tick_result()
             upd += ms[r]
             ev += res.n_enter + res.n_leave
@@ -111,13 +119,25 @@ def main():
         t0 = time.perf_counter()
         w = SimWorld(R, n, side, max_step, x0, z0, yaw0, tk)
         load = time.perf_counter() - t0
+        stages = None
         for t in range(a.warmup):
+            if t == a.warmup - 3:                  # the last 3 warm-up steps: device time per stage of rank 0
+                w.g[0].set_profiling(1)
             w.step(t)
+        if a.warmup >= 3:
+            acc = {}
+            for name, us, _, calls in w.g[0].stage_times():
+                v = acc.setdefault(name, [0.0, 0])
+                v[0] += us
+                v[1] += calls
+            w.g[0].set_profiling(0)
+            stages = {k: round(v[0] / 3, 1) for k, v in acc.items()}
         per = np.zeros(R)
         smax = 0.0
         upd = ev = rec = rows = 0
+        phases = {"route": 0.0, "tick_call": 0.0, "collect_call": 0.0}
         for t in range(a.warmup, ticks):
-            ts, u, e, rc, rw = w.step(t)
+            ts, u, e, rc, rw = w.step(t, phases)
             per += np.array(ts)
             smax += max(ts)                        # ranks meet at every exchange: a step costs its slowest rank
             upd += u; ev += e; rec += rc; rows += rw
@@ -132,7 +152,10 @@ def main():
                 "records_per_step": rec / a.steps, "halo_bytes_per_step_all_ranks": row_bytes,
                 "projected_updates_per_sec_excl_exchange": upd / a.steps / (step_ms * 1e-3),
                 "projected_events_per_sec_excl_exchange": ev / a.steps / (step_ms * 1e-3),
-                "load_s": round(load, 1)}
+                "load_s": round(load, 1),
+                "host_us_per_rank_step": {k: round(v / a.steps / R * 1e6, 1) for k, v in phases.items()}}
+        if stages:
+            line["rank0_device_us_per_stage"] = stages
         if base is None and R == 1:
             base = line
         if base is not None:

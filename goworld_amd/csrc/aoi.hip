@@ -103,7 +103,7 @@ __global__ void __launch_bounds__(NT) k_ops2(TickBufs b) {
 // last Leave that cleared c.  The slot's last Leave clears in k_ops3, every
 // op's bits after it are OR'd in by k_place (a later launch: clear, then OR).
 __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, uint32_t A, const AoiEnt& a,
-                                                const PrevEnt& p);
+                                                const PrevEnt& p, bool lng);
 
 // Per op: the syncInfoFlag bits, the sync payload of the slot's last
 // non-Leave op; the slot's last AOI op saves the pre-tick position and stamp
@@ -112,7 +112,7 @@ __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, u
 // op, the dedupe record and the slot state)
 __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
-    bool mv = false;
+    bool mv = false, lng = false;
     uint32_t s = 0, fbits = 0;
     AoiEnt a;
     PrevEnt p;
@@ -152,6 +152,10 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
                 else { a.x = op.x; a.z = op.z; a.meta |= PRESENT_BIT; }
                 b.w.aoi[s] = a;
                 mv = true;
+                // decomposed world: a long mover (a halo row says so, or an
+                // owned op moved it further than max_step)
+                lng = (op.reserved & RES_LONG) != 0 ||
+                      (was && (a.meta & PRESENT_BIT) && fabsf(a.x - p.ox) > b.long_step);
             }
         }
     }
@@ -160,7 +164,7 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
     const uint32_t nw = (uint32_t)popc64(wave_ballot(mv));
     if (lane_id() == 0 && nw) shard_add(b.st, blockIdx.x * NWAVE + (threadIdx.x >> 6), SH_MOVERS, nw);
     uint2 cc = make_uint2(NO_CELL, NO_CELL);
-    if (mv) cc = classify_mover(b, i, s, a, p);
+    if (mv) cc = classify_mover(b, i, s, a, p, lng);
     if (i < b.m) b.mcell[i] = make_uint4(cc.x, cc.y, s, fbits);   // k_place reads them back coalesced
 }
 
@@ -267,7 +271,7 @@ void grid_rebuild(const World& w, DevStats* st, uint32_t* k0, uint32_t* v0, uint
 // mover's mover-grid entry (tags aside) goes to mtmp[i] and its cells are
 // returned for mcell[i], so k_place reads them coalesced.
 __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, uint32_t A, const AoiEnt& a,
-                                                const PrevEnt& p) {
+                                                const PrevEnt& p, bool lng) {
     const SpaceP P = b.w.sp[a.meta & SPACE_MASK];
     uint32_t co = NO_CELL, cn = NO_CELL;
     if (p.ox == p.ox) co = cell_of(P, p.ox, p.oz);
@@ -278,7 +282,7 @@ __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, u
         MEnt m;
         m.x = pn ? a.x : qnan(); m.z = pn ? a.z : qnan();
         m.ox = p.ox; m.oz = p.oz;
-        m.slot = A; m.tags = 0; m.client = cl ? 1u : 0u; m.space = a.meta & SPACE_MASK;
+        m.slot = A; m.tags = lng ? TAG_LONG : 0u; m.client = cl ? 1u : 0u; m.space = a.meta & SPACE_MASK;
         b.mtmp[i] = m;
     }
     if (co != NO_CELL) atomicAdd(&b.gm_cnt[co], 1u);
@@ -326,11 +330,11 @@ __global__ void __launch_bounds__(NT) k_place(TickBufs b) {
     const bool cl = e.client != 0;
     const bool pn = cn != NO_CELL;
     if (co != NO_CELL) {
-        e.tags = TAG_OLD | (cn == co ? TAG_NEW | TAG_PRIMARY : 0u) | (pn ? 0u : TAG_PRIMARY);
+        e.tags = (e.tags & TAG_LONG) | TAG_OLD | (cn == co ? TAG_NEW | TAG_PRIMARY : 0u) | (pn ? 0u : TAG_PRIMARY);
         b.gm[b.gm_start[co] + atomicSub(&b.gm_cnt[co], 1u) - 1u] = e;
     }
     if (pn && cn != co) {
-        e.tags = TAG_NEW | TAG_PRIMARY;
+        e.tags = (e.tags & TAG_LONG) | TAG_NEW | TAG_PRIMARY;
         b.gm[b.gm_start[cn] + atomicSub(&b.gm_cnt[cn], 1u) - 1u] = e;
         const uint32_t kept = (b.w.gn_start[cn + 1] - b.w.gn_start[cn]) - (b.dep[cn] & ~CELL_DIRTY);
         const uint32_t at = b.start_nxt[cn] + kept + atomicSub(&b.arr[cn], 1u) - 1u;
@@ -579,6 +583,9 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     // decomposed world: A's own events only where A is owned (after the tick,
     // before it for a leaver); an op-less B's events only where B is owned
     const bool ownA = owned_x(P, pn ? me.x : me.ox);
+    // a long mover's pairs are emitted by the owners of the other members
+    // (they hold both ends of every pair that changes)
+    const bool longA = (me.tags & TAG_LONG) != 0;
     const unsigned long long sA = w.stamp[A], soA = w.prev[A].ostamp;
     const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
     const Rects R = mover_rects(P, po, me.ox, me.oz, pn, me.x, me.z);
@@ -662,7 +669,12 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             // B has no op: (B,A) is B's event too (kept in A's region; the
             // events stage places it)
             const bool mev = ev && nmv && owned_x(P, e.x);
-            ev = ev && ownA;
+            const bool longB = (e.info & TAG_LONG) != 0;
+            ev = ev && (longA ? !longB && owned_x(P, e.x == e.x ? e.x : e.ox) : ownA);
+            if (longA && b.conflicts) {                  // two related long movers: not supported
+                const uint64_t bc = wave_ballot(longB && (t_ro || t_rn));
+                if (bc && ln == 0) atomicAdd(b.conflicts, (unsigned long long)popc64(bc));
+            }
             const uint64_t be = wave_ballot(ev), bl = wave_ballot(ev && lv), bm = wave_ballot(mev);
             const uint32_t at = n + (uint32_t)popc64(be & lt);
             if (ev && at < cap) out[at] = key;
@@ -774,6 +786,7 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     const uint64_t own_cap = b.own_cap;
     const float d = P.d;
     const bool ownA = owned_x(P, pn ? me.x : me.ox);
+    const bool longA = (me.tags & TAG_LONG) != 0;           // (see mover_one)
     const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
     // this half's row ranges: lane hl = row hl/2 of the rects, grid hl%2
     uint32_t rs = 0, rl = 0;
@@ -887,7 +900,12 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
             c_new += (uint32_t)popc64(wave_ballot(t_rn) & hmask);
             c_cli += (uint32_t)popc64(wave_ballot(t_cli) & hmask);
             const bool mev = ev && nmv && owned_x(P, e.x);
-            ev = ev && ownA;
+            const bool longB = (e.info & TAG_LONG) != 0;
+            ev = ev && (longA ? !longB && owned_x(P, e.x == e.x ? e.x : e.ox) : ownA);
+            if (b.conflicts) {
+                const uint64_t bc = wave_ballot(longA && longB && (t_ro || t_rn));
+                if (bc && ln == 0) atomicAdd(b.conflicts, (unsigned long long)popc64(bc));
+            }
             const uint64_t be = wave_ballot(ev) & hmask, bl = wave_ballot(ev && lv) & hmask;
             const uint64_t bm = wave_ballot(mev) & hmask;
             const uint32_t at = n + (uint32_t)popc64(be & lt);

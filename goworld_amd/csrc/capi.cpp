@@ -860,7 +860,7 @@ int gw_route_halo(gw_ctx* c, const gw_op* dev_ops, const uint64_t* dev_stamps, u
     return 0;
 }
 
-int gw_halo_status(gw_ctx* c, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops) {
+int gw_halo_status(gw_ctx* c, uint64_t* overflow, uint64_t* long_moves, uint64_t* bad_ops) {
     if (!c) return GW_EINVAL;
     if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
@@ -869,7 +869,7 @@ int gw_halo_status(gw_ctx* c, uint64_t* overflow, uint64_t* bad_moves, uint64_t*
     HIPCHK(hipMemsetAsync(c->halo, 0, sizeof h, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     if (overflow) *overflow = h.overflow;
-    if (bad_moves) *bad_moves = h.bad_moves;
+    if (long_moves) *long_moves = h.long_moves;
     if (bad_ops) *bad_ops = h.bad_ops;
     return 0;
 }
@@ -1124,6 +1124,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     memset(out, 0, sizeof *out);
     int rc0 = settle(c);                             // a deferred tick before this one
     if (rc0) return rc0;
+    c->wd.submitted = false;
     bool host_ops = false;                           // pageable host ops: no deferral
     for (auto& sg : c->segs) host_ops |= sg.host;
     uint64_t M64 = 0;
@@ -1229,6 +1230,8 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.rank_sort = c->rank_sort;
     b.grid_cap = c->grid_cap;
     b.pair_max = c->pair_max;
+    b.long_step = c->wd.on ? c->wd.g.max_step : INFINITY;   // decomposed world: long movers
+    b.conflicts = c->wd.on ? &c->halo->conflicts : nullptr;
     b.ol = c->ol;
     b.st = st;
     b.gn_nxt = c->gnb[c->gcur ^ 1]; b.start_nxt = c->gsb[c->gcur ^ 1];

@@ -58,9 +58,17 @@ struct WorldHost {
     const gw_op* ops = nullptr;     // this tick's owned ops (caller's device memory)
     uint32_t n_ops = 0;
     bool routed = false;
+    bool submitted = false;         // gw_world_submit queued a tick that gw_tick has not run yet
     uint32_t kept = 0;              // routed ops whose dedupe session (k_route1 = k_ops1) the tick ...
     uint32_t ol_pre = 0;            // ... reuses once submitted: the next tick's first ol_pre ops (gw_tick)
     uint32_t kept_tag = 0;          // that session
+    // long moves (teleports): far triples, partitioned by destination rank
+    DevBuf ext, far_rows, far_dest, far_cnt, far_sorted, far_off, far_cursor, far_recv, far_mat;
+    uint32_t far_cap = 0;                        // triples the far buffer holds
+    std::vector<uint32_t> far_cnt_h;             // [ranks] triples this rank sends to each rank (incl. itself)
+    std::vector<uint32_t> far_off_h;             // [ranks] their offsets in far_sorted (triples)
+    std::vector<uint32_t> far_mat_h;             // [ranks * ranks] triples rank p sends to rank q (step path)
+    std::vector<float> ext_h;                    // [2 * ranks] held x-range of every rank
 };
 
 // a 16-byte EntityID as a hash-map key

@@ -80,6 +80,7 @@ struct alignas(16) MEnt {
     uint32_t slot, tags, client, space;
 };
 constexpr uint32_t TAG_OLD = 1u, TAG_NEW = 2u, TAG_PRIMARY = 4u;
+constexpr uint32_t TAG_LONG = 8u;   // decomposed world: the mover jumped further than max_step this tick
 
 // Per-space parameters (32 B).  Cells are squares of side cs = 1/inv_cs >=
 // d / cells_per_d; a window spans at most 10 rows (capi.cpp).  The cell
@@ -227,6 +228,9 @@ struct TickBufs {
     uint32_t* bk_split;       // [BK_NSPLIT] bucket bounds: quantiles of the last tick's keys
     int bk_bits;              // log2 of the bucket count (<= BK_MAXBITS, <= wbits + 1)
     uint64_t it_hint;         // bucket-path items of the last tick (sizes the flatten's grid)
+    float long_step;          // decomposed world: an owned mover whose x moves further is a long
+                              // mover (its pairs are attributed to the targets' owners); +inf otherwise
+    unsigned long long* conflicts;   // decomposed world: long-mover pairs related before or after (or null)
     uint32_t pair_max;        // GW_PAIR_MAX: k_mover_pair runs two movers per wave when both have at
                               // most this many candidates (0 = one mover per wave, k_mover)
     uint32_t grid_cap;        // GW_GRID_CAP (tests): at most this many blocks for the grid-stride
@@ -311,10 +315,27 @@ void launch_neighbors(const World& w, uint32_t slot, uint32_t* out, uint32_t* n_
 void launch_count_all(const World& w, uint64_t n_present, unsigned long long* total, hipStream_t s);
 // ---- decomposed world: owner-side halo routing (halo.hip) -----------------
 constexpr uint8_t SIF_ROUTED = GW_SIF_OWN_CLIENT | GW_SIF_NEIGHBOR_CLIENTS;   // flag bits rows carry
+// the first three words are summed over ranks by gw_world_status
 struct HaloStats {
-    unsigned long long overflow, bad_moves, bad_ops;
-    uint32_t cnt[2];           // entities placed per destination (this call)
+    unsigned long long overflow;    // routed entities past a fixed-size buffer (0 by construction)
+    unsigned long long conflicts;   // pairs of long movers related before or after a tick (the diff)
+    unsigned long long bad_ops;     // ops with an invalid slot or kind
+    unsigned long long long_moves;  // owned entities that moved more than max_step (routed far)
+    uint32_t cnt[2];                // entities placed per neighbour destination (this call)
+    uint32_t far_n, pad;            // far triples placed (this call; may exceed the buffer)
 };
+// halo rows of long moves (teleports): to every rank holding the old or the
+// new position that is not a neighbour, and a LEAVE for the owner's own copy
+// when the entity left its held range.  Triples in placement order with
+// their destination rank (partitioned by destination afterwards).
+struct HaloFar {
+    gw_halo_row* rows;          // cap triples (3 rows each)
+    uint32_t* dest;             // destination rank of each triple
+    uint32_t* cnt;              // [nranks] triples per destination (zeroed by the first pass)
+    const float* ext;           // [2 * nranks] held x-range [lo, hi) of every rank, float32
+    uint32_t cap, nranks, self, pad;
+};
+constexpr uint16_t RES_LONG = 1;   // gw_op.reserved of a halo row: the entity moved more than max_step
 struct HaloDst {
     float x_lo, x_hi;
     gw_halo_row* rows;
@@ -329,7 +350,12 @@ struct HaloDsts {
 // (then `stamps` may be stamps_out); pad: NOP rows up to each buffer's capacity
 void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
                        float max_step, const HaloDsts& D, OpLast* ol, uint32_t ol_tag, HaloStats* hs, hipStream_t s,
-                       bool pad = true, unsigned long long* stamps_out = nullptr, unsigned long long stamp_base = 0);
+                       bool pad = true, unsigned long long* stamps_out = nullptr, unsigned long long stamp_base = 0,
+                       const HaloFar* far = nullptr);
+// far triples -> out, grouped by destination: triple t goes to off[dest[t]] + (its rank among them);
+// cursor: [nranks] scratch, overwritten
+void launch_far_partition(const gw_halo_row* rows, const uint32_t* dest, uint32_t n, const uint32_t* off,
+                          uint32_t* cursor, uint32_t nranks, gw_halo_row* out, hipStream_t s);
 void launch_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n, hipStream_t s);
 void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,
                        hipStream_t s);

@@ -31,9 +31,11 @@ __device__ __forceinline__ bool op_valid(const gw_op& op, uint32_t cap) {
 
 __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
                                                 OpLast* ol, uint32_t tag, HaloStats* hs,
-                                                unsigned long long* stamps_out, unsigned long long stamp_base) {
+                                                unsigned long long* stamps_out, unsigned long long stamp_base,
+                                                HaloFar F) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
-    if (i == 0) hs->cnt[0] = hs->cnt[1] = 0;         // placement counters of this call
+    if (i == 0) hs->cnt[0] = hs->cnt[1] = hs->far_n = 0;   // placement counters of this call
+    if (F.cnt && i < F.nranks) F.cnt[i] = 0;
     if (i >= n) return;
     if (stamps_out) stamps_out[i] = stamp_base + i;
     const gw_op op = ops[i];
@@ -63,11 +65,12 @@ __global__ void __launch_bounds__(NT) k_route2(const gw_op* __restrict__ ops, ui
             ol[op.slot].rb[c] = ol_put(tag, 1);
 }
 
-__device__ __forceinline__ gw_op mk_op(uint8_t kind, uint8_t flags, uint32_t slot, const gw_op* payload) {
+__device__ __forceinline__ gw_op mk_op(uint8_t kind, uint8_t flags, uint32_t slot, const gw_op* payload,
+                                       uint16_t res = 0) {
     gw_op o;
     o.kind = kind;
     o.sync_flags = flags;
-    o.reserved = 0;
+    o.reserved = res;
     o.slot = slot;
     if (payload) {
         o.x = payload->x; o.y = payload->y; o.z = payload->z; o.yaw = payload->yaw;
@@ -82,9 +85,46 @@ __device__ __forceinline__ void put_row(gw_halo_row* r, const gw_op& o, unsigned
     r->stamp = stamp;
 }
 
+// the three rows of an entity for a destination holding [lo, hi): LEAVE
+// (left and re-entered inside the tick) / the net AOI change / SYNC
+struct RowKinds {
+    uint8_t k0, k1, k2;
+};
+__device__ __forceinline__ RowKinds row_kinds(bool was, bool now, int32_t la, int32_t ll, int32_t lp, uint32_t f) {
+    RowKinds k{GW_OP_NOP, GW_OP_NOP, GW_OP_NOP};
+    if (la >= 0) {
+        if (ll >= 0 && was && now) k.k0 = GW_OP_LEAVE;
+        if (now && (!was || ll >= 0)) k.k1 = GW_OP_ENTER;
+        else if (was && now) k.k1 = GW_OP_MOVED;
+        else if (was) k.k1 = GW_OP_LEAVE;
+    }
+    if (now && (f != 0 || lp > la)) k.k2 = GW_OP_SYNC;
+    return k;
+}
+
+__device__ __forceinline__ void put_triple(gw_halo_row* r, const RowKinds& k, uint32_t s, const gw_op& oa,
+                                           const gw_op& op_pos, uint32_t f, uint16_t res,
+                                           const unsigned long long* stamps, int32_t ll, int32_t la, uint32_t i) {
+    const gw_op nop = mk_op(GW_OP_NOP, 0, 0, nullptr);
+    put_row(r + 0, k.k0 ? mk_op(k.k0, 0, s, nullptr, res) : nop, k.k0 ? stamps[ll] : 0ull);
+    put_row(r + 1, k.k1 ? mk_op(k.k1, 0, s, &oa, res) : nop, k.k1 ? stamps[la] : 0ull);
+    put_row(r + 2, k.k2 ? mk_op(k.k2, (uint8_t)f, s, &op_pos) : nop, k.k2 ? stamps[i] : 0ull);
+}
+
+// a far triple (long moves only: rare, one atomic each)
+__device__ __forceinline__ void put_far(const HaloFar& F, HaloStats* hs, uint32_t q, const RowKinds& k, uint32_t s,
+                                        const gw_op& oa, const gw_op& op_pos, uint32_t f,
+                                        const unsigned long long* stamps, int32_t ll, int32_t la, uint32_t i) {
+    atomicAdd(&F.cnt[q], 1u);                        // counted even past the buffer: the exchange sizes
+    const uint32_t t = atomicAdd(&hs->far_n, 1u);
+    if (t >= F.cap) return;                          // the host grows the buffer and routes again
+    put_triple(F.rows + (size_t)t * ROWS, k, s, oa, op_pos, f, RES_LONG, stamps, ll, la, i);
+    F.dest[t] = q;
+}
+
 __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, const unsigned long long* __restrict__ stamps,
                                                 uint32_t n, World w, const OpLast* __restrict__ ol, uint32_t tag,
-                                                float max_step, HaloDsts D, HaloStats* hs) {
+                                                float max_step, HaloDsts D, HaloStats* hs, HaloFar F) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     // every lane reaches the wave-aggregated appends below
     bool rep = false;
@@ -100,7 +140,7 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
             rep = (int32_t)i == max(lp, ll);          // the entity's last op
         }
     }
-    bool old_p = false, new_p = false;
+    bool old_p = false, new_p = false, lng = false;
     float old_x = 0.f, new_x = 0.f;
     uint32_t f = 0;
     gw_op oa{}, op_pos{};
@@ -114,7 +154,10 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
             oa = ops[la];
             new_p = oa.kind != GW_OP_LEAVE;
             if (new_p) new_x = oa.x;
-            if (old_p && new_p && fabsf(new_x - old_x) > max_step) atomicAdd(&hs->bad_moves, 1ull);
+            // a long move (a teleport: Entity.SetPosition has no step bound,
+            // Entity.go:1185-1187): routed to every rank holding either end
+            lng = old_p && new_p && fabsf(new_x - old_x) > max_step;
+            if (lng) atomicAdd(&hs->long_moves, 1ull);
         }
         if (lp >= 0) op_pos = ops[lp];
         // syncInfoFlag after the tick's ops (k_ops3 / k_place): old bits a Leave
@@ -126,21 +169,14 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
         }
         f = ((flag_get(w.flags, s) & keep) | rbits) & SIF_ROUTED;
     }
+    const uint16_t res = lng ? RES_LONG : 0;
     for (uint32_t d = 0; d < D.n; ++d) {
         const HaloDst& dst = D.d[d];
         const bool was = old_p && old_x >= dst.x_lo && old_x < dst.x_hi;
         const bool now = new_p && new_x >= dst.x_lo && new_x < dst.x_hi;
-        uint8_t k0 = GW_OP_NOP, k1 = GW_OP_NOP, k2 = GW_OP_NOP;
-        if (rep) {
-            if (la >= 0) {
-                if (ll >= 0 && was && now) k0 = GW_OP_LEAVE;
-                if (now && (!was || ll >= 0)) k1 = GW_OP_ENTER;
-                else if (was && now) k1 = GW_OP_MOVED;
-                else if (was) k1 = GW_OP_LEAVE;
-            }
-            if (now && (f != 0 || lp > la)) k2 = GW_OP_SYNC;
-        }
-        const bool emit = rep && (k0 | k1 | k2);
+        RowKinds k{GW_OP_NOP, GW_OP_NOP, GW_OP_NOP};
+        if (rep) k = row_kinds(was, now, la, ll, lp, f);
+        const bool emit = rep && (k.k0 | k.k1 | k.k2);
         const uint64_t bm = wave_ballot(emit);
         if (!bm) continue;
         const int leader = __builtin_ctzll(bm);
@@ -153,11 +189,24 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
             atomicAdd(&hs->overflow, 1ull);
             continue;
         }
-        gw_halo_row* r = dst.rows + (size_t)e * ROWS;
-        const gw_op nop = mk_op(GW_OP_NOP, 0, 0, nullptr);
-        put_row(r + 0, k0 ? mk_op(k0, 0, s, nullptr) : nop, k0 ? stamps[ll] : 0ull);
-        put_row(r + 1, k1 ? mk_op(k1, 0, s, &oa) : nop, k1 ? stamps[la] : 0ull);
-        put_row(r + 2, k2 ? mk_op(k2, (uint8_t)f, s, &op_pos) : nop, k2 ? stamps[i] : 0ull);
+        put_triple(dst.rows + (size_t)e * ROWS, k, s, oa, op_pos, f, res, stamps, ll, la, i);
+    }
+    if (lng && F.rows) {
+        // every other rank (not this one, not a neighbour) holding either end
+        for (uint32_t q = 0; q < F.nranks; ++q) {
+            if (q + 1 >= F.self && q <= F.self + 1) continue;   // self and the neighbours
+            const float lo = F.ext[2 * q], hi = F.ext[2 * q + 1];
+            const bool was = old_x >= lo && old_x < hi, now = new_x >= lo && new_x < hi;
+            if (!(was || now)) continue;
+            put_far(F, hs, q, row_kinds(was, now, la, ll, lp, f), s, oa, op_pos, f, stamps, ll, la, i);
+        }
+        // this rank's own copy, if the entity left its held range: a LEAVE
+        // (keep-mask 0) after the tick's own ops, so no copy stays outside
+        const float lo = F.ext[2 * F.self], hi = F.ext[2 * F.self + 1];
+        if (!(new_x >= lo && new_x < hi)) {
+            RowKinds k{GW_OP_NOP, GW_OP_LEAVE, GW_OP_NOP};
+            put_far(F, hs, F.self, k, s, oa, op_pos, 0, stamps, ll, la, i);
+        }
     }
 }
 
@@ -183,15 +232,38 @@ __global__ void __launch_bounds__(NT) k_split_rows(const gw_halo_row* __restrict
 
 void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
                        float max_step, const HaloDsts& D, OpLast* ol, uint32_t ol_tag, HaloStats* hs, hipStream_t s,
-                       bool pad, unsigned long long* stamps_out, unsigned long long stamp_base) {
-    const uint32_t nb = nblk1(n, NT);
+                       bool pad, unsigned long long* stamps_out, unsigned long long stamp_base, const HaloFar* far) {
+    HaloFar F{};
+    if (far) F = *far;
+    const uint32_t nb = nblk1(std::max<uint32_t>(n, F.nranks), NT);
     uint64_t rows = 0;                                   // NOP padding up to the capacity (fixed-size exchanges)
     if (pad)
         for (uint32_t d = 0; d < D.n; ++d) rows = std::max<uint64_t>(rows, (uint64_t)D.d[d].cap * ROWS);
-    hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, ol_tag, hs, stamps_out, stamp_base);
+    hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, ol_tag, hs, stamps_out, stamp_base, F);
     hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, ol_tag);
-    hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, ol, ol_tag, max_step, D, hs);
+    hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, ol, ol_tag, max_step, D, hs, F);
     if (rows) hipLaunchKernelGGL(k_route4, dim3(nblk1(rows, NT)), dim3(NT), 0, s, D, hs);
+}
+
+__global__ void __launch_bounds__(NT) k_far_partition(const gw_halo_row* __restrict__ rows,
+                                                       const uint32_t* __restrict__ dest, uint32_t n,
+                                                       const uint32_t* __restrict__ off, uint32_t* cursor,
+                                                       uint32_t nranks, gw_halo_row* __restrict__ out) {
+    const uint32_t t = blockIdx.x * NT + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t q = dest[t];
+    if (q >= nranks) return;
+    const uint32_t at = off[q] + atomicAdd(&cursor[q], 1u);
+    for (uint32_t j = 0; j < ROWS; ++j) out[(size_t)at * ROWS + j] = rows[(size_t)t * ROWS + j];
+}
+__global__ void k_zero_u32(uint32_t* p, uint32_t n) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i < n) p[i] = 0;
+}
+void launch_far_partition(const gw_halo_row* rows, const uint32_t* dest, uint32_t n, const uint32_t* off,
+                          uint32_t* cursor, uint32_t nranks, gw_halo_row* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_zero_u32, dim3(nblk1(nranks, NT)), dim3(NT), 0, s, cursor, nranks);
+    if (n) hipLaunchKernelGGL(k_far_partition, dim3(nblk(n, NT)), dim3(NT), 0, s, rows, dest, n, off, cursor, nranks, out);
 }
 
 __global__ void __launch_bounds__(NT) k_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n) {

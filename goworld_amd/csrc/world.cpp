@@ -50,6 +50,70 @@ float f32_ceil(double v, int side) {
     return f;
 }
 
+// the routing launch of one world tick (both paths): neighbour rows into the
+// send buffers, far triples (long moves) into the far buffer
+int route_launch(gw_ctx* c, const gw_op* ops, uint32_t n, const HaloDsts& D, uint32_t tag, unsigned long long base) {
+    WorldHost& W = c->wd;
+    HaloFar F{};
+    if (W.far_cap) {
+        F.rows = P<gw_halo_row>(W.far_rows);
+        F.dest = P<uint32_t>(W.far_dest);
+        F.cap = W.far_cap;
+    }
+    F.cnt = P<uint32_t>(W.far_cnt);
+    F.ext = P<float>(W.ext);
+    F.nranks = W.g.ranks;
+    F.self = W.g.rank;
+    // without a far buffer the long moves are still counted (F.rows null:
+    // nothing placed); a rank of 1 or 2 strips has no far destination, but the
+    // owner's own copy may still need its LEAVE row
+    if (!F.rows) {
+        if (int rc = ensure(c, W.far_rows, 1024 * ROWS * sizeof(gw_halo_row))) return rc;
+        if (int rc = ensure(c, W.far_dest, 1024 * 4)) return rc;
+        W.far_cap = 1024;
+        F.rows = P<gw_halo_row>(W.far_rows);
+        F.dest = P<uint32_t>(W.far_dest);
+        F.cap = W.far_cap;
+    }
+    launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->ol, tag, c->halo,
+                      c->st, /*pad=*/false, P<unsigned long long>(W.stamps), base, &F);   // stamps by r1
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// after the routing's host sync (hs, cnt read back): a far buffer too small
+// is grown and the routing rerun (idempotent: same session, same stamps,
+// same counts); then the far triples are grouped by destination
+int far_settle(gw_ctx* c, const gw_op* ops, uint32_t n, const HaloDsts& D, uint32_t tag, unsigned long long base,
+               HaloStats& hs) {
+    WorldHost& W = c->wd;
+    int rc;
+    if (hs.far_n > W.far_cap) {
+        const uint32_t cap = hs.far_n + hs.far_n / 2 + 64;
+        if ((rc = ensure(c, W.far_rows, (size_t)cap * ROWS * sizeof(gw_halo_row))) ||
+            (rc = ensure(c, W.far_dest, (size_t)cap * 4)))
+            return rc;
+        W.far_cap = cap;
+        if ((rc = route_launch(c, ops, n, D, tag, base))) return rc;
+        HIPCHK(hipMemcpyAsync(&hs, c->halo, sizeof hs, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        if (hs.far_n > W.far_cap) return set_err(c, GW_ENOMEM, "far halo rows overflowed twice");
+    }
+    uint32_t acc = 0;
+    for (uint32_t q = 0; q < W.g.ranks; ++q) {
+        W.far_off_h[q] = acc;
+        acc += W.far_cnt_h[q];
+    }
+    if (acc != hs.far_n) return set_err(c, GW_EDEVICE, "far halo counts disagree (%u vs %u)", acc, hs.far_n);
+    if (!acc) return 0;
+    if ((rc = ensure(c, W.far_sorted, (size_t)acc * ROWS * sizeof(gw_halo_row)))) return rc;
+    HIPCHK(hipMemcpyAsync(W.far_off.p, W.far_off_h.data(), (size_t)W.g.ranks * 4, hipMemcpyHostToDevice, c->st));
+    launch_far_partition(P<gw_halo_row>(W.far_rows), P<uint32_t>(W.far_dest), acc, P<uint32_t>(W.far_off),
+                         P<uint32_t>(W.far_cursor), W.g.ranks, P<gw_halo_row>(W.far_sorted), c->st);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -141,6 +205,22 @@ int gw_world_create(gw_ctx* c, const gw_world_geom* g, uint32_t capacity, const 
             W.ext_hi[side] = (float)(strip_hi(*g, nb) + W.h);
         }
     }
+    W.ext_h.assign(2 * (size_t)g->ranks, 0.f);
+    for (uint32_t q = 0; q < g->ranks; ++q) {
+        W.ext_h[2 * q] = (float)(strip_lo(*g, (int)q) - W.h);
+        W.ext_h[2 * q + 1] = (float)(strip_hi(*g, (int)q) + W.h);
+    }
+    int rc2;
+    if ((rc2 = ensure(c, W.ext, W.ext_h.size() * 4)) || (rc2 = ensure(c, W.far_cnt, (size_t)g->ranks * 4)) ||
+        (rc2 = ensure(c, W.far_off, (size_t)g->ranks * 4)) || (rc2 = ensure(c, W.far_cursor, (size_t)g->ranks * 4)) ||
+        (rc2 = ensure(c, W.far_mat, (size_t)g->ranks * g->ranks * 4)))
+        return rc2;
+    HIPCHK(hipMemcpyAsync(W.ext.p, W.ext_h.data(), W.ext_h.size() * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    W.far_cnt_h.assign(g->ranks, 0);
+    W.far_off_h.assign(g->ranks, 0);
+    W.far_mat_h.assign((size_t)g->ranks * g->ranks, 0);
+    W.far_cap = 0;
     W.sid = sid;
     W.tick = 0;
     W.on = true;
@@ -169,14 +249,14 @@ int gw_world_route(gw_ctx* c, const gw_op* ops, uint32_t n, const gw_halo_row* s
     const unsigned long long base = 1 + (W.tick * W.g.ranks + W.g.rank) * STAMP_STRIDE;
     uint32_t tag = 0;
     if ((rc = next_ol_tag(c, &tag))) return rc;      // the tick reuses this session (gw_world_submit)
-    launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->ol, tag,
-                      c->halo, c->st, /*pad=*/false, P<unsigned long long>(W.stamps), base);   // stamps by r1
-    HIPCHK(hipGetLastError());
+    if ((rc = route_launch(c, ops, n, D, tag, base))) return rc;
     W.kept = n;
     W.kept_tag = tag;
     HaloStats hs{};
     HIPCHK(hipMemcpyAsync(&hs, c->halo, sizeof hs, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(W.far_cnt_h.data(), W.far_cnt.p, (size_t)W.g.ranks * 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    if ((rc = far_settle(c, ops, n, D, tag, base, hs))) return rc;
     uint32_t k = 0;
     for (int side = 0; side < 2; ++side) {
         W.send_cnt[side] = 0;
@@ -222,6 +302,7 @@ int gw_world_submit(gw_ctx* c, const gw_halo_row* const recv[2], const uint32_t 
     }
     W.ol_pre = W.kept;                   // the tick's stream starts with the routed ops (gw_tick checks)
     W.kept = 0;
+    W.submitted = true;                  // far rows may join until gw_tick
     return 0;
 }
 
@@ -248,16 +329,18 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
     }
     const unsigned long long base = 1 + (W.tick * W.g.ranks + W.g.rank) * STAMP_STRIDE;
     if (!D.n) launch_iota_u64(P<unsigned long long>(W.stamps), base, n, c->st);
+    uint32_t tag = 0;
     if (D.n) {                                        // a one-strip world has nobody to route to
-        uint32_t tag = 0;
         if ((rc = next_ol_tag(c, &tag))) return rc;  // the tick reuses this session (gw_world_submit)
-        launch_route_halo(world_of(c), ops, P<unsigned long long>(W.stamps), n, W.g.max_step, D, c->ol, tag,
-                          c->halo, c->st, /*pad=*/false, P<unsigned long long>(W.stamps), base);   // stamps by r1
+        if ((rc = route_launch(c, ops, n, D, tag, base))) return rc;
         W.kept = n;
         W.kept_tag = tag;
     }
     HIPCHK(hipGetLastError());
+    const uint32_t R = W.g.ranks, me = W.g.rank;
+    const bool far_round = R >= 3;                    // ranks that are not neighbours exist
     uint32_t rcnt[2] = {0, 0};
+    uint32_t far_in = 0;                              // triples received from far ranks
     if (any_nb) {
         // round 1: the entity counts (u32) both ways; HaloStats.cnt[k] is the
         // k-th destination of D, i.e. left first when both exist
@@ -271,20 +354,33 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
             if (r1 != ncclSuccess || r2 != ncclSuccess) { (void)ncclGroupEnd(); NCCLCHK(r1 != ncclSuccess ? r1 : r2); }
         }
         NCCLCHK(ncclGroupEnd());
+        // the far triples every rank sends every rank (long moves; R u32 each)
+        if (far_round)
+            NCCLCHK(ncclAllGather(W.far_cnt.p, W.far_mat.p, R, ncclUint32, c->comm, c->st));
         uint32_t h[4] = {0, 0, 0, 0};
+        HaloStats hs{};
         HIPCHK(hipMemcpyAsync(h, dcnt, 8, hipMemcpyDeviceToHost, c->st));
-        HIPCHK(hipMemcpyAsync(h + 2, c->halo->cnt, 8, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipMemcpyAsync(&hs, c->halo, sizeof hs, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipMemcpyAsync(W.far_cnt_h.data(), W.far_cnt.p, (size_t)R * 4, hipMemcpyDeviceToHost, c->st));
+        if (far_round)
+            HIPCHK(hipMemcpyAsync(W.far_mat_h.data(), W.far_mat.p, (size_t)R * R * 4, hipMemcpyDeviceToHost, c->st));
         HIPCHK(hipStreamSynchronize(c->st));
+        if ((rc = far_settle(c, ops, n, D, tag, base, hs))) return rc;
         k = 0;
         for (int side = 0; side < 2; ++side) {
             W.send_cnt[side] = 0;
             if (W.nb[side] < 0) continue;
-            W.send_cnt[side] = std::min<uint32_t>(h[2 + k++], (uint32_t)cap_ent);
+            W.send_cnt[side] = std::min<uint32_t>(hs.cnt[k++], (uint32_t)cap_ent);
             rcnt[side] = h[side];
             if ((rc = ensure(c, W.recv[side], (size_t)std::max<uint32_t>(rcnt[side], 1) * ROWS * sizeof(gw_halo_row))))
                 return rc;
         }
-        // round 2: exactly the used rows
+        if (far_round) {
+            for (uint32_t p = 0; p < R; ++p)
+                if (p != me) far_in += W.far_mat_h[(size_t)p * R + me];
+            if (far_in && (rc = ensure(c, W.far_recv, (size_t)far_in * ROWS * sizeof(gw_halo_row)))) return rc;
+        }
+        // round 2: exactly the used rows (neighbours), and the far triples
         NCCLCHK(ncclGroupStart());
         for (int side = 0; side < 2; ++side) {
             if (W.nb[side] < 0) continue;
@@ -297,6 +393,22 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
                               c->comm, c->st);
             if (r1 != ncclSuccess || r2 != ncclSuccess) { (void)ncclGroupEnd(); NCCLCHK(r1 != ncclSuccess ? r1 : r2); }
         }
+        if (far_round) {
+            size_t roff = 0;
+            for (uint32_t p = 0; p < R; ++p) {
+                if (p == me) continue;
+                ncclResult_t r1 = ncclSuccess, r2 = ncclSuccess;
+                const uint32_t out = W.far_cnt_h[p], in = W.far_mat_h[(size_t)p * R + me];
+                if (out)
+                    r1 = ncclSend(P<gw_halo_row>(W.far_sorted) + (size_t)W.far_off_h[p] * ROWS,
+                                  (size_t)out * ROWS * sizeof(gw_halo_row), ncclUint8, (int)p, c->comm, c->st);
+                if (in)
+                    r2 = ncclRecv(P<gw_halo_row>(W.far_recv) + roff * ROWS, (size_t)in * ROWS * sizeof(gw_halo_row),
+                                  ncclUint8, (int)p, c->comm, c->st);
+                roff += in;
+                if (r1 != ncclSuccess || r2 != ncclSuccess) { (void)ncclGroupEnd(); NCCLCHK(r1 != ncclSuccess ? r1 : r2); }
+            }
+        }
         NCCLCHK(ncclGroupEnd());
     }
     W.ops = ops;
@@ -304,10 +416,35 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
     W.routed = true;
     const gw_halo_row* recv[2] = {P<gw_halo_row>(W.recv[0]), P<gw_halo_row>(W.recv[1])};
     const uint32_t rrows[2] = {rcnt[0] * ROWS, rcnt[1] * ROWS};
-    return gw_world_submit(c, recv, rrows);
+    if ((rc = gw_world_submit(c, recv, rrows))) return rc;
+    // this rank's own LEAVE rows (long movers that left its range), then the far rows received
+    const uint32_t self_n = any_nb ? W.far_cnt_h[me] : 0;
+    if (self_n && (rc = gw_submit_device_rows(c, P<gw_halo_row>(W.far_sorted) + (size_t)W.far_off_h[me] * ROWS,
+                                              self_n * ROWS)))
+        return rc;
+    if (far_in && (rc = gw_submit_device_rows(c, P<gw_halo_row>(W.far_recv), far_in * ROWS))) return rc;
+    return 0;
 }
 
-int gw_world_status(gw_ctx* c, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops) {
+int gw_world_far(gw_ctx* c, const gw_halo_row** rows, const uint32_t** counts) {
+    if (!c) return GW_EINVAL;
+    WorldHost& W = c->wd;
+    if (!W.on) return set_err(c, GW_ESTATE, "no world strip (gw_world_create)");
+    if (rows) *rows = W.far_sorted.p ? P<gw_halo_row>(W.far_sorted) : nullptr;
+    if (counts) *counts = W.far_cnt_h.data();
+    return 0;
+}
+
+int gw_world_submit_far(gw_ctx* c, const gw_halo_row* rows, uint32_t n_rows) {
+    if (!c || (n_rows && !rows)) return GW_EINVAL;
+    WorldHost& W = c->wd;
+    if (!W.on) return set_err(c, GW_ESTATE, "no world strip (gw_world_create)");
+    if (W.routed || !W.submitted) return set_err(c, GW_ESTATE, "gw_world_submit first (far rows join its tick)");
+    if (n_rows % ROWS) return set_err(c, GW_EINVAL, "%u rows: not whole entities", n_rows);
+    return gw_submit_device_rows(c, rows, n_rows);
+}
+
+int gw_world_status(gw_ctx* c, uint64_t* overflow, uint64_t* conflicts, uint64_t* bad_ops) {
     if (!c) return GW_EINVAL;
     if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
@@ -315,7 +452,14 @@ int gw_world_status(gw_ctx* c, uint64_t* overflow, uint64_t* bad_moves, uint64_t
         // the three counters are the first three u64 of HaloStats
         NCCLCHK(ncclAllReduce(c->halo, c->halo, 3, ncclUint64, ncclSum, c->comm, c->st));
     }
-    return gw_halo_status(c, overflow, bad_moves, bad_ops);
+    HaloStats h{};
+    HIPCHK(hipMemcpyAsync(&h, c->halo, sizeof h, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemsetAsync(c->halo, 0, sizeof h, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (overflow) *overflow = h.overflow;
+    if (conflicts) *conflicts = h.conflicts;
+    if (bad_ops) *bad_ops = h.bad_ops;
+    return 0;
 }
 
 }  // extern "C"

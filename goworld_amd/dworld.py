@@ -59,6 +59,7 @@ OP_WORDS = 6            # gw_op as 6 int32 words: kind | flags<<8, slot, x, y, z
 ROW_WORDS = 8           # + the u64 stamp
 ROWS_PER_ENTITY = 3
 STAMP_STRIDE = 1 << 26  # stamp = 1 + (tick * ranks + rank) * STAMP_STRIDE + op index
+RES_LONG = 1            # gw_op.reserved bit of a halo row: the entity moved more than max_step this tick
 
 
 @dataclasses.dataclass
@@ -160,6 +161,39 @@ def exchange_rows(pg, rank: int, ranks: int, sends, device, comm_device):
     return [None if r is None else back(r) for r in recv]
 
 
+def exchange_far(pg, rank: int, ranks: int, far: dict, device, comm_device):
+    """Host-transport exchange of the rows of long moves (teleports) with every
+    rank (gloo for the CPU tests and one-GPU rehearsals): the (ranks x ranks)
+    matrix of row counts first (all_gather), then exactly the used rows.
+    far: {dest rank: (rows, 8) int32} (dest == rank: rows for this rank
+    itself).  Returns the received row tensors on `device`, by source rank."""
+    import torch.distributed as dist
+    cnt = torch.zeros(ranks, dtype=torch.int64)
+    for q, rows in far.items():
+        cnt[q] = int(rows.shape[0])
+    allc = [torch.zeros(ranks, dtype=torch.int64) for _ in range(ranks)]
+    dist.all_gather(allc, cnt, group=pg)
+    mv = (lambda t: t) if comm_device == device else (lambda t: t.to(comm_device))
+    back = (lambda t: t) if comm_device == device else (lambda t: t.to(device))
+    out, ops = [], []
+    for p in range(ranks):
+        n_in = int(allc[p][rank].item())
+        if p == rank:
+            if n_in:
+                out.append(far[rank])
+            continue
+        if int(cnt[p].item()):
+            ops.append(dist.P2POp(dist.isend, mv(far[p]).contiguous(), p, group=pg))
+        if n_in:
+            buf = torch.empty((n_in, ROW_WORDS), dtype=torch.int32, device=comm_device)
+            ops.append(dist.P2POp(dist.irecv, buf, p, group=pg))
+            out.append(buf)
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return [back(t) for t in out]
+
+
 class HipStrip:
     """Engine adapter over the library's decomposed world (gw_world_*): a
     gpuaoi.GpuAOI context sharing one stream with torch (made torch's current
@@ -201,16 +235,33 @@ class HipStrip:
             out.append(torch.from_numpy(buf))
         return out
 
-    def submit(self, words: torch.Tensor, stamps, recvd):
+    def far(self) -> dict:
+        """Rows of the last route for ranks that are not neighbours (long
+        moves), {rank: (rows, 8) int32 host tensor}."""
+        out = {}
+        for q, (ptr, rows) in self.g.world_far().items():
+            buf = np.zeros((rows, ROW_WORDS), np.int32)
+            self.g.d2h(buf, ptr)
+            out[q] = torch.from_numpy(buf)
+        return out
+
+    def submit(self, words: torch.Tensor, stamps, recvd, far_in=()):
         rows = []
+        dev = torch.device("cuda", torch.cuda.current_device())
         for r in recvd:
             if r is None or r.shape[0] == 0:
                 rows.append((0, 0))
                 continue
-            r = r.to(device=torch.device("cuda", torch.cuda.current_device()), dtype=torch.int32).contiguous()
+            r = r.to(device=dev, dtype=torch.int32).contiguous()
             self._keep.append(r)
             rows.append((r.data_ptr(), r.shape[0]))
         self.g.world_submit(rows)
+        for r in far_in:
+            if r is None or r.shape[0] == 0:
+                continue
+            r = r.to(device=dev, dtype=torch.int32).contiguous()
+            self._keep.append(r)
+            self.g.world_submit_far(r.data_ptr(), r.shape[0])
 
     def tick(self, copy=True, no_events=False, defer=False):
         res = self.g.tick(copy=copy, no_events=no_events, defer=defer)
@@ -259,11 +310,14 @@ class StripRank:
         else:
             st = stamps_for(self.tick_no, self.r, self.g.ranks, m, self.dev)
             sends = self.e.route(words, st)
+            far = self.e.far()
             if self.g.ranks > 1:
                 recvd = exchange_rows(self.pg, self.r, self.g.ranks, sends, self.dev, self.cdev)
+                far_in = exchange_far(self.pg, self.r, self.g.ranks, far, self.dev, self.cdev)
             else:
                 recvd = [None, None]
-            self.e.submit(words, st, recvd)
+                far_in = [far[self.r]] if self.r in far else []
+            self.e.submit(words, st, recvd, far_in)
         self.tick_no += 1
 
     def tick(self, copy=True, **kw):
@@ -360,12 +414,18 @@ class LocalWorld:
             sends.append(g.world_route(ptrs[r], ms[r]))
             if times is not None:
                 times[r] += time.perf_counter() - t0
+        fars = [g.world_far() for g in self.g]                   # long moves: {dest: (ptr, rows)}
         rows = 0
         for r, g in enumerate(self.g):
             left = sends[r - 1][1] if r > 0 else (0, 0)           # left neighbour's rows to its right
             right = sends[r + 1][0] if r + 1 < self.R else (0, 0)
             rows += left[1] + right[1]
             g.world_submit([left, right])
+            for p in range(self.R):
+                if r in fars[p]:
+                    ptr, n = fars[p][r]
+                    g.world_submit_far(ptr, n)
+                    rows += n
         return rows
 
     def check(self):

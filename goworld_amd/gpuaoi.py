@@ -156,6 +156,8 @@ def lib():
         L.gw_world_route.argtypes = [vp, vp, _u32, C.POINTER(vp * 2), C.POINTER(_u32 * 2)]
         L.gw_world_submit.argtypes = [vp, C.POINTER(vp * 2), C.POINTER(_u32 * 2)]
         L.gw_world_status.argtypes = [vp, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64)]
+        L.gw_world_far.argtypes = [vp, C.POINTER(vp), C.POINTER(C.POINTER(_u32))]
+        L.gw_world_submit_far.argtypes = [vp, vp, _u32]
         L.gw_set_entity_ids.argtypes = [vp, vp, vp, _u32]
         L.gw_clear_entity_ids.argtypes = [vp, vp, _u32]
         L.gw_set_client_ids.argtypes = [vp, vp, vp, _u32]
@@ -176,7 +178,7 @@ EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_spa
             "gw_comm_exchange", "gw_comm_allreduce_u64", "gw_world_create", "gw_world_step", "gw_world_route",
             "gw_world_submit", "gw_world_status", "gw_set_entity_ids", "gw_clear_entity_ids", "gw_set_client_ids",
             "gw_set_client_syncing", "gw_submit_client_sync", "gw_sync_encode_wire", "gw_space_grow",
-            "gw_context_info"]
+            "gw_context_info", "gw_world_far", "gw_world_submit_far"]
 
 
 def comm_unique_id() -> bytes:
@@ -528,6 +530,7 @@ class GpuAOI:
         barr = (C.c_float * 4)(*[float(v) for v in bounds])
         sid = _u32()
         self._chk(lib().gw_world_create(self._h, C.byref(geom), capacity, C.cast(barr, C.c_void_p), C.byref(sid)))
+        self._ranks = int(ranks)
         self.spaces.append((sid.value, 0, capacity))
         return sid.value
 
@@ -547,7 +550,26 @@ class GpuAOI:
         rows = (_u32 * 2)(*[n for _, n in recv])
         self._chk(lib().gw_world_submit(self._h, C.byref(ptrs), C.byref(rows)))
 
+    def world_far(self) -> dict:
+        """After world_route: {dest rank: (device ptr, rows)} of the long moves' rows
+        (this rank's own LEAVE rows under its own rank)."""
+        rows, cnt = C.c_void_p(), C.POINTER(_u32)()
+        self._chk(lib().gw_world_far(self._h, C.byref(rows), C.byref(cnt)))
+        out, off = {}, 0
+        nranks = self._ranks
+        for q in range(nranks):
+            k = cnt[q]
+            if k:
+                out[q] = (rows.value + off * 3 * 32, k * 3)
+            off += k
+        return out
+
+    def world_submit_far(self, dev_rows: int, n_rows: int):
+        """Queue far rows received for this tick (after world_submit)."""
+        self._chk(lib().gw_world_submit_far(self._h, C.c_void_p(dev_rows), n_rows))
+
     def world_status(self) -> tuple[int, int, int]:
+        """(halo overflows, long-move conflicts, bad ops), summed over ranks."""
         v = [_u64() for _ in range(3)]
         self._chk(lib().gw_world_status(self._h, *[C.byref(x) for x in v]))
         return tuple(x.value for x in v)

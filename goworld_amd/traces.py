@@ -420,12 +420,17 @@ class StripTrace:
 
 def strip_world_trace(seed: int, n: int, ranks: int, strip_w: float, height: float, d: float,
                       ticks: int, max_step: float, move_frac: float = 0.5,
-                      churn: bool = True, edge_frac: float = 0.2) -> StripTrace:
+                      churn: bool = True, edge_frac: float = 0.2, teleports: int = 0) -> StripTrace:
     """Random walk across strips (entities migrate between ranks) with churn:
     Leave, re-Enter anywhere, Leave + re-Enter nearby inside one tick, two
     moves of one entity in one tick, Sync ops.  Positions are dyadic except
     an `edge_frac` share placed on strip borders and on the window edge of a
-    border entity (x = border +- d, +-1 ulp)."""
+    border entity (x = border +- d, +-1 ulp).  `teleports` > 0: up to that
+    many present entities per tick jump anywhere in the world (a Moved op far
+    beyond max_step: Entity.SetPosition has no step bound, Entity.go:1185-1187),
+    chosen so that no two of them are related before or after the tick (a
+    pair of related entities that both jump is not supported by the strip
+    decomposition)."""
     W = ranks * strip_w
     step_q = int(max_step * Q) // 2          # half a step per move, <= 2 moves per tick
     lo_q, hi_q = 0, int(W * Q)
@@ -494,6 +499,31 @@ def strip_world_trace(seed: int, n: int, ranks: int, strip_w: float, height: flo
         sy = ids[pres & (u >= move_frac) & (u < move_frac + 0.1)]
         yaw[sy] = (v[sy] * 6.25).astype(np.float32)
         emit(rows1, OP_SYNC, np.where(v[sy] < 0.3, SIF_OWN, SIF_NEIGHBOR | SIF_OWN), sy, x[sy], z[sy], yaw[sy])
+        if teleports:
+            # candidates: present, no other op this tick; far jumps; no two
+            # jumpers within 2d + 2 max_step of each other (old or new position)
+            cand = ids[pres & (u >= move_frac + 0.1) & (u < 0.97)]
+            cand = cand[np.argsort(rand_u64(stream_key(seed, 109, t), len(cand)), kind="stable")]
+            tx = (rand_int(stream_key(seed, 110, t), len(cand), lo_q, hi_q) / Q).astype(np.float32)
+            tz = (rand_int(stream_key(seed, 111, t), len(cand), zlo_q, zhi_q) / Q).astype(np.float32)
+            sep = 2 * d + 2 * max_step + 1
+            taken_x, taken_z, jumps = [], [], []
+            for j, i in enumerate(cand.tolist()):
+                if len(jumps) == teleports:
+                    break
+                if abs(float(tx[j]) - float(x[i])) <= 2 * d + 4 * max_step:
+                    continue                                   # a short jump: not a teleport
+                pts = [(float(x[i]), float(z[i])), (float(tx[j]), float(tz[j]))]
+                if any(abs(px - qx) <= sep and abs(pz - qz) <= sep
+                       for px, pz in pts for qx, qz in zip(taken_x, taken_z)):
+                    continue
+                taken_x += [p[0] for p in pts]
+                taken_z += [p[1] for p in pts]
+                jumps.append(j)
+            jumps = np.array(jumps, np.int64)
+            tp = cand[jumps]
+            x[tp], z[tp] = tx[jumps], tz[jumps]
+            emit(rows1, OP_MOVED, SIF_NEIGHBOR | SIF_OWN, tp, x[tp], z[tp], yaw[tp])
         enter_owner = {}
         if churn:
             lv = ids[pres & (u >= 0.97) & (u < 0.985)]            # leave for a while

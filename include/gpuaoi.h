@@ -231,7 +231,11 @@ int  gw_space_set_ownership(gw_ctx* ctx, uint32_t space_id, float x_lo, float x_
 /* ---- decomposed world (one space split into X-strips over processes) ----
  * A halo row (32 B) is an op with its global stamp.  A destination is a
  * neighbour process: the x-range its local space holds (its strip widened by
- * the halo) and a device buffer of cap_entities * 3 rows. */
+ * the halo) and a device buffer of cap_entities * 3 rows.  In halo rows
+ * op.reserved bit 0 (GW_ROW_LONG) marks the AOI rows of an entity that moved
+ * more than max_step in the tick (a teleport); the ops a caller submits keep
+ * reserved = 0. */
+#define GW_ROW_LONG 1u
 typedef struct gw_halo_row {
     gw_op    op;
     uint64_t stamp;
@@ -265,8 +269,9 @@ int  gw_route_halo(gw_ctx* ctx, const gw_op* dev_ops, const uint64_t* dev_stamps
 int  gw_submit_device_rows(gw_ctx* ctx, const gw_halo_row* dev_rows, uint32_t n);
 
 /* Counters accumulated by gw_route_halo since the last call (synchronises,
- * then resets them). */
-int  gw_halo_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops);
+ * then resets them): overflows, owned entities that moved more than
+ * max_step (long moves), ops with an invalid slot or kind. */
+int  gw_halo_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* long_moves, uint64_t* bad_ops);
 
 /* (GW_OP_LEAVE: sync_flags is the mask of the entity's pending syncInfoFlag
  * bits it keeps.  Space.leave leaves the flag alone (Space.go:219-242), so an
@@ -482,13 +487,31 @@ int  gw_world_step(gw_ctx* ctx, const gw_op* dev_ops, uint32_t n);
 int  gw_world_route(gw_ctx* ctx, const gw_op* dev_ops, uint32_t n, const gw_halo_row* send[2],
                     uint32_t send_rows[2]);
 int  gw_world_submit(gw_ctx* ctx, const gw_halo_row* const recv[2], const uint32_t recv_rows[2]);
+/* Long moves (an owned entity moving more than max_step in x in one tick, e.g.
+ * SetPosition far away, Entity.go:1185-1187): besides its
+ * neighbours, every rank whose held range contains the entity's old or new
+ * position gets its rows, and the owner gets a LEAVE row for its own copy
+ * when the entity left the owner's held range.  gw_world_step exchanges them
+ * itself (an all-gather of the per-rank counts when there are >= 3 ranks,
+ * then the rows with the neighbours' in one grouped round).  On the caller's
+ * transport: after gw_world_route, gw_world_far gives these rows grouped by
+ * destination rank (counts[q] entities = 3 rows each, rank q's at the sum of
+ * the counts before q; counts has `ranks` entries, this rank's own LEAVE rows
+ * under its own rank); the caller delivers them and every rank queues what it
+ * received (its own included) with gw_world_submit_far after gw_world_submit
+ * (device memory, valid until the tick).  Events of a long mover's pairs are
+ * emitted by the owner of the other member; two entities that both move more
+ * than max_step in one tick and are related before or after it (a group
+ * teleport) are not supported: counted as conflicts by gw_world_status. */
+int  gw_world_far(gw_ctx* ctx, const gw_halo_row** rows, const uint32_t** counts);
+int  gw_world_submit_far(gw_ctx* ctx, const gw_halo_row* rows, uint32_t n_rows);
 /* Contract counters since the last call, summed over ranks when a
- * communicator exists: halo overflows (0 by construction), owned entities
- * that moved more than max_step, ops with an invalid slot or kind. */
-int  gw_world_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* bad_moves, uint64_t* bad_ops);
+ * communicator exists: halo overflows (0 by construction), long-move
+ * conflicts (see gw_world_far), ops with an invalid slot or kind. */
+int  gw_world_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* conflicts, uint64_t* bad_ops);
 
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 11
+#define GW_ABI_VERSION 12
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

@@ -32,6 +32,7 @@ class OracleStrip:
         self.words, self.stamps = [], []
 
     def create_world(self, geom, rank, n_global, bounds):
+        self.max_step = np.float32(geom.max_step)
         self.router = torch_router.Router(geom, rank, n_global, torch.device("cpu"), n_global)
         self.o = self.pyorc.OracleSpace(n_global, geom.d, self.pyorc.SEQRULE)
         self.x = np.zeros(n_global, np.float32)
@@ -42,10 +43,13 @@ class OracleStrip:
     def route(self, words, stamps):
         return self.router.route_exact(words, stamps)
 
-    def submit(self, words, stamps, recvd=()):
+    def far(self):
+        return self.router.far_exact()
+
+    def submit(self, words, stamps, recvd=(), far_in=()):
         self.words.append(words.cpu().numpy())
         self.stamps.append(stamps.cpu().numpy())
-        for rows in recvd:
+        for rows in list(recvd) + list(far_in):
             if rows is None:
                 continue
             self.router.receive(rows)
@@ -73,6 +77,10 @@ class OracleStrip:
         self.words, self.stamps = [], []
         keep = (w[:, 0] & 0xFF) != 0
         w, s = w[keep], s[keep]
+        # long movers: a row says so (RES_LONG), or an owned op moved one
+        # further than max_step; their pairs are emitted by the other member's owner
+        lng = np.zeros(len(self.x), bool)
+        lng[w[((w[:, 0] >> 16) & dworld.RES_LONG) != 0][:, 1]] = True
         ops = dworld.words_to_ops(w[np.argsort(s, kind="stable")])
         x0, p0 = self.x.copy(), self.present.copy()
         for op in ops:
@@ -83,9 +91,14 @@ class OracleStrip:
                 self.present[sl] = False
         assert self.o.tick(ops) == 0
         e, l = self.o.events()
+        lng |= p0 & self.present & (np.abs(self.x - x0) > self.max_step)
         xr = np.where(self.present, self.x, x0)
         own = self._owned(xr)
-        return _Res(enter=e[own[e["watcher"]]].copy(), leave=l[own[l["watcher"]]].copy())
+
+        def mine(ev):
+            wt, tg = ev["watcher"], ev["target"]
+            return ev[(own[wt] & ~lng[wt]) | (lng[wt] & own[tg] & ~lng[tg])].copy()
+        return _Res(enter=mine(e), leave=mine(l))
 
     def collect(self, copy=True):
         r = self.o.collect()
@@ -118,13 +131,15 @@ def main():
     ap.add_argument("--collect-every", type=int, default=3)
     ap.add_argument("--trace", choices=["strip", "walk"], default="strip")
     ap.add_argument("--side", type=float, default=36864.0, help="walk: world side")
+    ap.add_argument("--teleports", type=int, default=0, help="strip: jumps anywhere per tick")
     a = ap.parse_args()
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{a.port}", rank=a.rank,
                             world_size=a.world)
     if a.trace == "walk":
         tr = T.walk_strip_trace(a.seed, a.n, a.side, a.world, a.ticks)
     else:
-        tr = T.strip_world_trace(a.seed, a.n, a.world, a.strip_w, a.height, a.d, a.ticks, a.max_step)
+        tr = T.strip_world_trace(a.seed, a.n, a.world, a.strip_w, a.height, a.d, a.ticks, a.max_step,
+                                 teleports=a.teleports)
     geom = dworld.Strips(0.0, tr.strip_w, a.world, tr.d, tr.max_step)
     if a.engine == "oracle":
         eng, dev = OracleStrip(), torch.device("cpu")

@@ -53,9 +53,8 @@ def test_world_size_must_match_gpus():
 
 
 def test_torchrun_ranks():
-    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(_port()), BENCH, "--gpus", "2",
-                        "--dry-run", "--steps", "3", "--warmup", "1"],
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+                        "--nproc-per-node", "2", BENCH, "--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1"],
                        cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=180)
     assert p.returncode == 0, p.stderr[-2000:]
     line = _line(p.stdout)

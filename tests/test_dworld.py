@@ -69,9 +69,12 @@ def _sort_rec(r):
     return r[np.lexsort((r["watcher"], r["entity"]))]
 
 
-def _check(world, results):
-    tr = T.strip_world_trace(TRACE["seed"], TRACE["n"], world, TRACE["strip_w"], TRACE["height"],
-                             TRACE["d"], TRACE["ticks"], TRACE["max_step"])
+TELEPORT = dict(TRACE, teleports=3)
+
+
+def _check(world, results, trace=TRACE):
+    tr = T.strip_world_trace(trace["seed"], trace["n"], world, trace["strip_w"], trace["height"],
+                             trace["d"], trace["ticks"], trace["max_step"], teleports=trace.get("teleports", 0))
     o = pyorc.OracleSpace(tr.n, tr.d, pyorc.SEQRULE)
     o.set_clients(tr.gates)
     n_ev = n_rec = 0
@@ -129,6 +132,35 @@ def test_dworld_gloo_oracle_ranks(world, tmp_path):
 def test_dworld_gpu_ranks(world, tmp_path):
     """The HIP engine per rank (HipRouter + gw_route_halo), ranks sharing the GPU."""
     _check(world, _run_ranks(world, "hip", tmp_path, timeout=100))
+
+
+def _teleports_cross_two_strips(world):
+    tr = T.strip_world_trace(TELEPORT["seed"], TELEPORT["n"], world, TELEPORT["strip_w"], TELEPORT["height"],
+                             TELEPORT["d"], TELEPORT["ticks"], TELEPORT["max_step"], teleports=TELEPORT["teleports"])
+    far = 0
+    for t in range(1, len(tr.ticks)):
+        ops, own = tr.ticks[t]
+        dst = np.clip(np.floor(ops["x"] / tr.strip_w).astype(np.int64), 0, world - 1)
+        far += int(np.sum((ops["kind"] == T.OP_MOVED) & (np.abs(dst - own) >= 2)))
+    return far
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_dworld_gloo_oracle_teleports(world, tmp_path):
+    """Long moves (Entity.SetPosition has no step bound, Entity.go:1185-1187):
+    entities jump anywhere, across two or more strips, every tick; their rows
+    reach every rank holding either end, their pairs are emitted by the other
+    member's owner, and the union still equals one global oracle space."""
+    assert world == 2 or _teleports_cross_two_strips(world) >= 5
+    _check(world, _run_ranks(world, "oracle", tmp_path, args=TELEPORT), trace=TELEPORT)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_dworld_gpu_teleports(world, tmp_path):
+    """The same with the HIP engine per rank (gw_world_route / gw_world_far /
+    gw_world_submit_far over gloo), ranks sharing the GPU."""
+    _check(world, _run_ranks(world, "hip", tmp_path, timeout=100, args=TELEPORT), trace=TELEPORT)
 
 
 WALK_SMALL = dict(trace="walk", seed=9, n=20000, side=6144.0, ticks=5)
@@ -286,9 +318,10 @@ def test_hip_router_rows_match_torch_router():
                 eng.collect(copy=False)
                 ref.collected()
         assert n_rows > 300
-        # no overflow; the same move-bound violations (entities that come back
-        # after ticks owned elsewhere, whose ghost rows this lone rank never got)
-        assert eng.status() == ref.status()
+        # no overflow; the same long moves (entities that come back after ticks
+        # owned elsewhere, whose ghost rows this lone rank never got)
+        ov, n_long, bad = eng.g.halo_status()
+        assert ov == 0 and bad == 0 and n_long == ref.long_count() > 0
         # invalid slots are counted, never followed
         bad = w.clone()
         bad[:, 1] = tr.n + 5

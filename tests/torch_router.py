@@ -11,8 +11,8 @@ from __future__ import annotations
 
 import torch
 
-from goworld_amd.dworld import (OP_ENTER, OP_LEAVE, OP_MOVED, OP_SYNC, OP_WORDS, ROW_WORDS, ROWS_PER_ENTITY,
-                                SIF_MASK, Strips)
+from goworld_amd.dworld import (OP_ENTER, OP_LEAVE, OP_MOVED, OP_SYNC, OP_WORDS, RES_LONG, ROW_WORDS,
+                                ROWS_PER_ENTITY, SIF_MASK, Strips)
 
 
 def _f32(words_col: torch.Tensor) -> torch.Tensor:
@@ -34,7 +34,8 @@ class Router:
         self.pflags = torch.zeros(n1, dtype=torch.int32, device=device)
         self.scratch = torch.full((n1,), -1, dtype=torch.int64, device=device)
         self.overflow = torch.zeros((), dtype=torch.int64, device=device)
-        self.bad_moves = torch.zeros((), dtype=torch.int64, device=device)
+        self.long_moves = torch.zeros((), dtype=torch.int64, device=device)
+        self.last_far = {}
         self.ext_lo, self.ext_hi = geom.ext(rank)
         self.lo, self.hi = geom.lo(rank), geom.hi(rank)
 
@@ -93,12 +94,20 @@ class Router:
             set_after = self._any(slot, bit, valid & ~lv & (idx > clr))
             keep = torch.where(clr < 0, (old_f >> c) & 1, torch.zeros_like(old_f))
             new_f |= (keep | set_after) << c
-        # the strip contract: an owned entity stays inside this rank's range + max_step
+        # a long move (present before and after, |dx| > max_step, e.g. a
+        # teleport): its AOI rows carry RES_LONG, and every rank whose held
+        # range has the old or the new position gets rows, not only the
+        # neighbours
         moved = rep & has_aoi & old_p & new_p
-        self.bad_moves += (moved & ((new_x - old_x).abs() > g.max_step)).sum()
+        lng = moved & ((new_x - old_x).abs() > g.max_step)
+        self.long_moves += lng.sum()
         sends = []
         self.last_used = []
-        for nb in (r - 1, r + 1):
+        self.last_far = {}
+        dests = [(r - 1, True), (r + 1, True)]
+        if bool(lng.any()):
+            dests += [(q, False) for q in range(g.ranks) if abs(q - r) > 1]
+        for nb, is_nb in dests:
             if nb < 0 or nb >= g.ranks:
                 sends.append(None)
                 continue
@@ -113,8 +122,29 @@ class Router:
             k1 = torch.where(has_aoi, k1, nop)
             k2 = torch.where(now & ((new_f != 0) | (lp > la)), torch.full_like(kind, OP_SYNC), nop)
             sel = rep & ((k0 | k1 | k2) != 0)
-            sends.append(self._pack(words, stamps, slot, sel, k0, ll.clamp(min=0), k1, la_c,
-                                    k2, lp_c, new_f, lany, cap))
+            if not is_nb:
+                sel = sel & lng                         # far ranks hear only of long moves
+            fl = torch.where(lng, torch.full_like(kind, RES_LONG << 16), nop)
+            k0 = torch.where(k0 != 0, k0 | fl, k0)
+            k1 = torch.where(k1 != 0, k1 | fl, k1)
+            buf = self._pack(words, stamps, slot, sel, k0, ll.clamp(min=0), k1, la_c, k2, lp_c, new_f, lany, cap)
+            if is_nb:
+                sends.append(buf)
+            else:
+                used = self.last_used.pop()
+                if used:
+                    self.last_far[nb] = buf[:used * ROWS_PER_ENTITY]
+        if bool(lng.any()):
+            # this rank's own copy of a long mover that left its held range:
+            # a LEAVE row for itself (keep-mask 0) after the tick's own ops,
+            # so no rank keeps a copy outside its range
+            away = lng & ~((new_x >= self.ext_lo) & (new_x < self.ext_hi))
+            if bool(away.any()):
+                nop = torch.zeros_like(kind)
+                k1 = torch.where(away, torch.full_like(kind, OP_LEAVE | (RES_LONG << 16)), nop)
+                buf = self._pack(words, stamps, slot, away, nop, la_c, k1, la_c, nop, lp_c,
+                                 torch.zeros_like(new_f), lany, cap)
+                self.last_far[r] = buf[:self.last_used.pop() * ROWS_PER_ENTITY]
         # routing state of the rows this rank owns (dummy row n absorbs the rest)
         s = torch.where(rep, slot, torch.full_like(slot, self.n))
         self.x[s] = new_x
@@ -179,11 +209,21 @@ class Router:
         """Sync flags are cleared everywhere by a collect (Entity.go:1221-1267)."""
         self.pflags.zero_()
 
+    def far_exact(self) -> dict:
+        """Rows of the last route() for ranks that are not neighbours (long
+        moves only), exact size: {rank: (rows, 8) int32}."""
+        return dict(self.last_far)
+
     def status(self):
-        ov, bad = int(self.overflow.item()), int(self.bad_moves.item())
+        """(overflow, long-move conflicts (not detected here: 0), bad ops)."""
+        ov = int(self.overflow.item())
         self.overflow.zero_()
-        self.bad_moves.zero_()
-        return max(ov, 0), bad, 0
+        return max(ov, 0), 0, 0
+
+    def long_count(self):
+        v = int(self.long_moves.item())
+        self.long_moves.zero_()
+        return v
 
 
 def split_rows(buf: torch.Tensor):

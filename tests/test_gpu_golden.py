@@ -152,7 +152,7 @@ def test_grid_stride_passes_capped(gpu, cap, monkeypatch):
         res = g.tick()
         assert (res.n_enter, res.n_leave) == (exp["n_enter"], exp["n_leave"])
         assert G.sha(res.enter) == exp["enter_sha"] and G.sha(res.leave) == exp["leave_sha"], f"tick {t}"
-        assert res.n_enter + res.n_leave > 4 * 8192                # several tiles per block
+        assert res.n_enter + res.n_leave > 2 * 8192                # many chunks per wave, >= 2 tiles
         r = g.sync_collect()
         assert G.sha(canonical(r.records, tr.gates)) == exp["rec_sha"], f"tick {t}: records"
     g.close()

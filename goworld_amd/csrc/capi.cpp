@@ -521,8 +521,12 @@ void gw_shutdown(gw_ctx* c) {
                       &c->m_fanout.b, &c->m_flag, &c->m_at, &c->m_items, &c->m_cnt, &c->m_off};
     for (DevBuf* b : bufs) if (b->p) (void)hipFree(b->p);
     DevBuf* wb[] = {&c->wd.stamps, &c->wd.send[0], &c->wd.send[1], &c->wd.recv[0], &c->wd.recv[1], &c->wd.cnt,
-                    &c->wire_d, &c->wire_tab, &c->id_up};
+                    &c->wire_d, &c->wire_tab, &c->id_up, &c->wd.ext, &c->wd.far_rows, &c->wd.far_dest,
+                    &c->wd.far_cnt, &c->wd.far_sorted, &c->wd.far_off, &c->wd.far_cursor, &c->wd.far_recv,
+                    &c->wd.far_mat, &c->wd.dstage};
     if (c->wire_h.p) (void)hipHostFree(c->wire_h.p);
+    if (c->wd.hstage.p) (void)hipHostFree(c->wd.hstage.p);
+    if (c->wd.staged) (void)hipEventDestroy(c->wd.staged);
     if (c->eid_dev) (void)hipFree(c->eid_dev);
     if (c->cid_dev) (void)hipFree(c->cid_dev);
     for (DevBuf* b : wb) if (b->p) (void)hipFree(b->p);

@@ -69,6 +69,10 @@ struct WorldHost {
     std::vector<uint32_t> far_off_h;             // [ranks] their offsets in far_sorted (triples)
     std::vector<uint32_t> far_mat_h;             // [ranks * ranks] triples rank p sends to rank q (step path)
     std::vector<float> ext_h;                    // [2 * ranks] held x-range of every rank
+    // host ops of a tick (gw_world_stage_ops): pinned staging, device copy, and
+    // the event after the upload (the pinned buffer is reused once it fired)
+    DevBuf hstage, dstage;
+    hipEvent_t staged = nullptr;
 };
 
 // a 16-byte EntityID as a hash-map key

@@ -426,6 +426,46 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
     return 0;
 }
 
+int gw_world_stage_ops(gw_ctx* c, const gw_op* ops, uint32_t n, const gw_op** dev_ops) {
+    if (!c || !dev_ops || (n && !ops)) return GW_EINVAL;
+    *dev_ops = nullptr;
+    WorldHost& W = c->wd;
+    if (!W.on) return set_err(c, GW_ESTATE, "no world strip (gw_world_create)");
+    if (W.routed || W.ol_pre || W.submitted)      // the staged ops of a queued tick are still to be read
+        return set_err(c, GW_ESTATE, "a world tick is pending (gw_world_submit / gw_tick first)");
+    if ((uint64_t)n >= STAMP_STRIDE) return set_err(c, GW_ERANGE, "too many ops in one tick for the stamp layout");
+    // what the host can check without the entity state (the owner's presence
+    // is on the device): kind, slot inside the world's id range, finite x/z
+    const uint32_t cap = c->spaces[W.sid].cap;
+    for (uint32_t i = 0; i < n; ++i) {
+        const gw_op& o = ops[i];
+        if (o.kind < GW_OP_ENTER || o.kind > GW_OP_SYNC || o.reserved)
+            return set_err(c, GW_EINVAL, "op %u: bad kind %u / reserved %u", i, o.kind, o.reserved);
+        if (o.slot >= cap) return set_err(c, GW_ERANGE, "op %u: entity %u outside the world (%u ids)", i, o.slot, cap);
+        if ((o.kind == GW_OP_ENTER || o.kind == GW_OP_MOVED) && !(std::isfinite(o.x) && std::isfinite(o.z)))
+            return set_err(c, GW_EINVAL, "op %u: non-finite coordinates", i);
+    }
+    (void)hipSetDevice(c->dev);
+    if (!W.staged) HIPCHK(hipEventCreateWithFlags(&W.staged, hipEventDisableTiming));
+    HIPCHK(hipEventSynchronize(W.staged));           // the last upload has left the pinned buffer
+    const size_t bytes = (size_t)std::max<uint32_t>(n, 1) * sizeof(gw_op);
+    int rc;
+    if ((rc = ensure_host(c, W.hstage, bytes)) || (rc = ensure(c, W.dstage, bytes))) return rc;
+    if (n) {
+        memcpy(W.hstage.p, ops, (size_t)n * sizeof(gw_op));
+        HIPCHK(hipMemcpyAsync(W.dstage.p, W.hstage.p, (size_t)n * sizeof(gw_op), hipMemcpyHostToDevice, c->st));
+    }
+    HIPCHK(hipEventRecord(W.staged, c->st));
+    *dev_ops = P<gw_op>(W.dstage);
+    return 0;
+}
+
+int gw_world_step_host(gw_ctx* c, const gw_op* ops, uint32_t n) {
+    const gw_op* dev = nullptr;
+    if (int rc = gw_world_stage_ops(c, ops, n, &dev)) return rc;
+    return gw_world_step(c, dev, n);
+}
+
 int gw_world_far(gw_ctx* c, const gw_halo_row** rows, const uint32_t** counts) {
     if (!c) return GW_EINVAL;
     WorldHost& W = c->wd;

@@ -158,6 +158,8 @@ def lib():
         L.gw_world_status.argtypes = [vp, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64)]
         L.gw_world_far.argtypes = [vp, C.POINTER(vp), C.POINTER(C.POINTER(_u32))]
         L.gw_world_submit_far.argtypes = [vp, vp, _u32]
+        L.gw_world_stage_ops.argtypes = [vp, vp, _u32, C.POINTER(vp)]
+        L.gw_world_step_host.argtypes = [vp, vp, _u32]
         L.gw_set_entity_ids.argtypes = [vp, vp, vp, _u32]
         L.gw_clear_entity_ids.argtypes = [vp, vp, _u32]
         L.gw_set_client_ids.argtypes = [vp, vp, vp, _u32]
@@ -178,7 +180,8 @@ EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_spa
             "gw_comm_exchange", "gw_comm_allreduce_u64", "gw_world_create", "gw_world_step", "gw_world_route",
             "gw_world_submit", "gw_world_status", "gw_set_entity_ids", "gw_clear_entity_ids", "gw_set_client_ids",
             "gw_set_client_syncing", "gw_submit_client_sync", "gw_sync_encode_wire", "gw_space_grow",
-            "gw_context_info", "gw_world_far", "gw_world_submit_far"]
+            "gw_context_info", "gw_world_far", "gw_world_submit_far", "gw_world_stage_ops",
+            "gw_world_step_host"]
 
 
 def comm_unique_id() -> bytes:
@@ -537,6 +540,18 @@ class GpuAOI:
     def world_step(self, dev_ops: int, n: int):
         """Route + RCCL exchange + queue this rank's tick (then tick / sync_collect)."""
         self._chk(lib().gw_world_step(self._h, C.c_void_p(dev_ops), n))
+
+    def world_step_host(self, ops: np.ndarray):
+        """gw_world_step_host: this rank's owned ops from host memory (staged by the library)."""
+        ops = np.ascontiguousarray(ops, dtype=OP_DTYPE)
+        self._chk(lib().gw_world_step_host(self._h, _p(ops), len(ops)))
+
+    def world_stage_ops(self, ops: np.ndarray) -> int:
+        """gw_world_stage_ops: host ops -> a library-owned device copy (valid until the tick)."""
+        ops = np.ascontiguousarray(ops, dtype=OP_DTYPE)
+        p = C.c_void_p()
+        self._chk(lib().gw_world_stage_ops(self._h, _p(ops), len(ops), C.byref(p)))
+        return p.value or 0
 
     def world_route(self, dev_ops: int, n: int):
         """-> ((left_ptr, left_rows), (right_ptr, right_rows)) device rows to send (ptr 0 = no neighbour)."""

@@ -487,6 +487,16 @@ int  gw_world_step(gw_ctx* ctx, const gw_op* dev_ops, uint32_t n);
 int  gw_world_route(gw_ctx* ctx, const gw_op* dev_ops, uint32_t n, const gw_halo_row* send[2],
                     uint32_t send_rows[2]);
 int  gw_world_submit(gw_ctx* ctx, const gw_halo_row* const recv[2], const uint32_t recv_rows[2]);
+/* Host ops (the Go caller's Space.enter / leave / move calls of the tick on
+ * the entities this rank owns, host memory, call order; Space.go:179-252,
+ * Entity.go:1185-1205): checked for what needs no entity state (kind,
+ * reserved = 0, entity id inside the world's id range, finite x/z for
+ * Enter/Moved; presence is the owner's device state), copied through a
+ * pinned buffer into a device buffer the library owns; *dev_ops stays valid
+ * until the tick that consumes it.  Then gw_world_step or gw_world_route as
+ * with device ops.  gw_world_step_host = stage + gw_world_step. */
+int  gw_world_stage_ops(gw_ctx* ctx, const gw_op* ops, uint32_t n, const gw_op** dev_ops);
+int  gw_world_step_host(gw_ctx* ctx, const gw_op* ops, uint32_t n);
 /* Long moves (an owned entity moving more than max_step in x in one tick, e.g.
  * SetPosition far away, Entity.go:1185-1187): besides its
  * neighbours, every rank whose held range contains the entity's old or new
@@ -511,7 +521,7 @@ int  gw_world_submit_far(gw_ctx* ctx, const gw_halo_row* rows, uint32_t n_rows);
 int  gw_world_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* conflicts, uint64_t* bad_ops);
 
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 12
+#define GW_ABI_VERSION 13
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

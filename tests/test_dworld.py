@@ -279,6 +279,89 @@ def test_rccl_self_exchange_and_allreduce():
     assert outs[0] == outs[1]
 
 
+@pytest.mark.gpu
+def test_world_step_host_ops():
+    """gw_world_step_host (the Go caller's host ops, staged by the library):
+    a one-strip world fed host ops equals the plain space, tick by tick; the
+    host checks reject a bad kind / an id outside the world / non-finite
+    coordinates before anything is queued, and a second stage before the tick
+    is refused.  Then a 2-strip world on the one GPU (two contexts, rows handed
+    over by pointer) driven by gw_world_stage_ops + gw_world_route equals the
+    plain space's events and records."""
+    from goworld_amd import gpuaoi
+    tr = T.walk_strip_trace(17, 20000, 8192.0, 1, 4)
+    outs = []
+    for path in ("world", "plain"):
+        with gpuaoi.GpuAOI(0) as g:
+            if path == "world":
+                g.world_create(0.0, 8192.0, tr.d, tr.max_step, 1, 0, tr.n, tr.bounds)
+            else:
+                g.create_space(tr.d, tr.n, tr.bounds)
+            g.set_clients(np.arange(tr.n, dtype=np.uint32), tr.gates)
+            seq = []
+            for t in range(len(tr.ticks)):
+                ops = tr.global_ops(t)
+                if path == "world":
+                    bad = ops[:4].copy()
+                    bad["slot"][2] = tr.n
+                    with pytest.raises(gpuaoi.GwError):
+                        g.world_step_host(bad)
+                    bad = ops[:4].copy()
+                    bad["kind"][1] = 9
+                    with pytest.raises(gpuaoi.GwError):
+                        g.world_step_host(bad)
+                    if len(ops) and ops["kind"][0] in (T.OP_ENTER, T.OP_MOVED):
+                        bad = ops[:1].copy()
+                        bad["x"][0] = np.inf
+                        with pytest.raises(gpuaoi.GwError):
+                            g.world_step_host(bad)
+                    g.world_step_host(ops)
+                    with pytest.raises(gpuaoi.GwError):
+                        g.world_stage_ops(ops[:1])             # the queued tick still reads the staged ops
+                else:
+                    g.submit(ops)
+                r = g.tick()
+                seq.append((r.enter.tobytes(), r.leave.tobytes(), g.sync_collect().records.tobytes()))
+            outs.append(seq)
+    assert outs[0] == outs[1]
+    # two strips on the one GPU, host ops staged per rank
+    tr2 = T.walk_strip_trace(19, 20000, 8192.0, 2, 4)
+    geom = dworld.Strips(0.0, tr2.strip_w, 2, tr2.d, tr2.max_step)
+    gs = [gpuaoi.GpuAOI(0) for _ in range(2)]
+    try:
+        for r, g in enumerate(gs):
+            lo, hi = geom.ext(r)
+            g.world_create(geom.x0, geom.w, geom.d, geom.max_step, 2, r, tr2.n,
+                           (max(lo, tr2.bounds[0]), tr2.bounds[1], min(hi, tr2.bounds[2]), tr2.bounds[3]))
+            g.set_clients(np.arange(tr2.n, dtype=np.uint32), tr2.gates)
+        with gpuaoi.GpuAOI(0) as ref:
+            ref.create_space(tr2.d, tr2.n, tr2.bounds)
+            ref.set_clients(np.arange(tr2.n, dtype=np.uint32), tr2.gates)
+            for t in range(len(tr2.ticks)):
+                sends = []
+                for r, g in enumerate(gs):
+                    dev = g.world_stage_ops(tr2.rank_ops(t, r))
+                    sends.append(g.world_route(dev, len(tr2.rank_ops(t, r))))
+                gs[0].world_submit([(0, 0), sends[1][0]])
+                gs[1].world_submit([sends[0][1], (0, 0)])
+                res = [g.tick() for g in gs]
+                ref.submit(tr2.global_ops(t))
+                e = ref.tick()
+                if t == 0:
+                    for g in gs:
+                        g.sync_collect()
+                    ref.sync_collect()
+                    continue
+                for name, exp in (("enter", e.enter), ("leave", e.leave)):
+                    got = np.concatenate([getattr(x, name) for x in res])
+                    assert _sort_ev(got).tobytes() == _sort_ev(exp).tobytes(), f"tick {t}: {name} events differ"
+                got = np.concatenate([g.sync_collect().records for g in gs])
+                assert _sort_rec(got).tobytes() == _sort_rec(ref.sync_collect().records).tobytes()
+    finally:
+        for g in gs:
+            g.close()
+
+
 def _canon_rows(buf):
     rows = buf.reshape(-1, 3, 8).cpu().numpy()
     used = rows[np.any(rows[:, :, 0] & 0xFF, axis=1)]

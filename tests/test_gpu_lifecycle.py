@@ -104,10 +104,11 @@ def test_grow_moves_space_mid_trace_bit_exact():
             g.submit(np.concatenate([gb, ga]) if t % 2 else np.concatenate([ga, gb]))
             r = g.tick()
             assert oa.tick(ops) == 0 and ob.tick(tb.ticks[t]) == 0
-            _check_tick(r, oa, base, base, base + n, f"A tick {t}")
+            hi_a = base + (n if t >= t_grow else n0)      # A's slot range (B sits right behind it before the grow)
+            _check_tick(r, oa, base, base, hi_a, f"A tick {t}")
             _check_tick(r, ob, base_b, base_b, base_b + tb.capacity, f"B tick {t}")
             recs = g.sync_collect().records
-            _check_records(recs, oa, base, base, base + n, tr.gates, f"A tick {t}")
+            _check_records(recs, oa, base, base, hi_a, tr.gates, f"A tick {t}")
             _check_records(recs, ob, base_b, base_b, base_b + tb.capacity, tb.gates, f"B tick {t}")
         for s in range(0, n, 7):
             assert np.array_equal(g.neighbors(base + s) - base, oa.neighbors(s)), s

@@ -49,6 +49,7 @@ sys.path.insert(0, ROOT)
 
 from goworld_amd import gpuaoi, traces  # noqa: E402
 
+PCIE_GBS = 57.1          # device->host copy rate into pinned memory on the box (tools/micro/pcie.hip, profiles/r03f_pcie.txt)
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s spec)
 
 
@@ -63,11 +64,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="multi-threaded CPU baseline time budget")
     ap.add_argument("--cpu-st-max-seconds", type=float, default=240.0,
                     help="guard on the single-thread baseline (it replays one full tick)")
-    ap.add_argument("--e2e-steps", type=int, default=4, help="untimed end-to-end steps (host in/out; the first is "
-                                                                 "a warm-up)")
+    ap.add_argument("--e2e-steps", type=int, default=8, help="untimed end-to-end steps (host in/out), split over "
+                                                                 "the two caller paths; the first of each is a warm-up")
     ap.add_argument("--e2e-wire", type=int, default=1,
-                    help="1: the end-to-end steps also encode and copy the 48-B game->gate wire records "
-                         "(gw_sync_encode_wire, what the Go shim's Collect hands to the gates)")
+                    help="1: half the end-to-end steps take the Go shim's path instead: the 48-B game->gate wire "
+                         "records (gw_sync_encode_wire) to the host, the compact records left on the device")
     ap.add_argument("--profile-stages", type=int, default=1,
                     help="1: HIP events around the dominant kernel's stage in the timed region (roofline) and "
                          "a per-stage breakdown over extra untimed steps; 0: none")
@@ -213,7 +214,8 @@ def dry_run(a, ctl):
                           "ranks_reporting": int(ranks), "higher_is_better": True}), flush=True)
 
 
-STAGE_KERNEL = {"diff": "k_mover<2, 1>"}
+# the diff stage's kernel: k_mover (one mover per wave), or k_mover_pair when GW_PAIR_MAX > 0
+STAGE_KERNEL = {"diff": "k_mover_pair<2>" if int(os.environ.get("GW_PAIR_MAX", "0") or 0) > 0 else "k_mover<2, 1>"}
 # the stage's kernel differs in small-space mode (config #4: many spaces whose grids fit LDS)
 STAGE_KERNEL_C4 = {"diff": "k_mover_small<2>", "sync_write": "k_sync_write_small2"}
 PMC_DIR = os.path.join(ROOT, "profiles")
@@ -366,25 +368,27 @@ class SpaceRun:
         r = g.tick_result()
         return r.movers, r, s
 
-    def step_e2e(self, t):
+    def step_e2e(self, t, wire=False):
         """The Go caller's game tick: host ops in (gw_submit: pageable host
-        memory, copied to the device), the canonical events and the sync
-        records out to pinned host buffers (GW_TICK_COPY_TO_HOST /
-        GW_SYNC_COPY_TO_HOST), i.e. PCIe both ways."""
+        memory, copied to the device), the canonical events out to pinned host
+        buffers (GW_TICK_COPY_TO_HOST), then either the compact 24-B sync
+        records (GW_SYNC_COPY_TO_HOST; wire=False) or, as the Go shim's Collect
+        does, the 48-B game->gate wire packets (gw_sync_encode_wire with
+        COPY_TO_HOST; the compact records stay on the device; wire=True)."""
         g = self.g
         c0 = time.perf_counter()
         g.submit(self.host_ticks[t])
         c1 = time.perf_counter()
         r = g.tick(copy=True, view=True)
         c2 = time.perf_counter()
-        s = g.sync_collect(copy=True, by_client=self.by_client, view=True)
+        s = g.sync_collect(copy=not wire, by_client=self.by_client, view=True)
         c3 = time.perf_counter()
         self.e2e_parts = {"submit": c1 - c0, "tick": c2 - c1, "collect": c3 - c2,
                           "tick_device_us": r.device_us, "collect_device_us": s.device_us,
                           "ops_bytes": len(self.host_ticks[t]) * traces.OP_DTYPE.itemsize,
-                          "event_bytes": 8 * (r.n_enter + r.n_leave), "record_bytes": 24 * s.n_rec}
-        if getattr(self, "e2e_wire", False):               # the Go shim's Collect: 48-B wire records to the host
-            data, pk, nb, dev_us = g.encode_wire(copy=True)
+                          "event_bytes": 8 * (r.n_enter + r.n_leave), "record_bytes": 0 if wire else 24 * s.n_rec}
+        if wire:
+            data, pk, nb, dev_us = g.encode_wire(copy=True, view=True)
             self.e2e_parts.update(wire=time.perf_counter() - c3, wire_bytes=nb, wire_device_us=dev_us)
         return r.movers, r, s
 
@@ -698,41 +702,57 @@ def main():
     g = run.g
     res = measure(run, a, ctl, W, K, a.profile_stages, extra)
     client = client_msgs(run, W + K + extra, cm) if cm else None
-    e2e = None
+    e2e = {}
     if n_e2e >= 2:
-        # end-to-end game ticks (host ops in, events + records out over PCIe),
-        # after the timed region; wall clock per step (the first one, which
-        # allocates the pinned host buffers, untimed)
-        t_e, e_ops = 0.0, 0
-        t_first = W + K + extra + cm
-        run.e2e_wire = a.e2e_wire
-        run.step_e2e(t_first)
-        parts = {}
-        for t in range(t_first + 1, t_first + n_e2e):
-            g.synchronize()
-            c0 = time.perf_counter()
-            upd, r, s_ = run.step_e2e(t)
-            t_e += time.perf_counter() - c0
-            e_ops += upd
-            for k, v in run.e2e_parts.items():
-                parts[k] = parts.get(k, 0.0) + v
-        n2 = n_e2e - 1
-        pa = {k: v / n2 for k, v in parts.items()}
-        e2e = {"ms_per_step": t_e / n2 * 1e3, "updates_per_sec": e_ops / t_e, "steps": n2,
-               "breakdown_ms": {k: round(pa[k] * 1e3, 3) for k in ("submit", "tick", "collect", "wire") if k in pa},
-               "device_ms": {"tick": round(pa["tick_device_us"] / 1e3, 3),
-                             "collect": round(pa["collect_device_us"] / 1e3, 3)},
-               "bytes_per_step": {"ops_h2d": pa["ops_bytes"], "events_d2h": pa["event_bytes"],
-                                  "records_d2h": pa["record_bytes"], **({"wire_d2h": pa["wire_bytes"]}
-                                                                         if "wire_bytes" in pa else {})},
-               "pcie_GBps": {"collect": round(pa["record_bytes"] / pa["collect"] / 1e9, 2),
-                             "tick": round(pa["event_bytes"] / pa["tick"] / 1e9, 2),
-                             **({"wire": round(pa["wire_bytes"] / pa["wire"] / 1e9, 2)} if "wire" in pa else {})},
-               "what": "gw_submit(host ops) + gw_tick(COPY_TO_HOST) + gw_sync_collect(COPY_TO_HOST)"
-                       + (" + gw_sync_encode_wire(COPY_TO_HOST)" if a.e2e_wire else "")
-                       + ": the Go caller's tick, events and records to pinned host memory (PCIe); wall clock "
-                         "per call (device_ms: HIP events of the same calls, copies included); untimed by the "
-                         "headline"}
+        # end-to-end game ticks (host ops in, events + records / wire packets out
+        # over PCIe), after the timed region; wall clock per step, the first of
+        # each path (which allocates the pinned host buffers) untimed
+        t_next = W + K + extra + cm
+        for key, wire in (("t_e2e", False), ("t_e2e_wire", True)):
+            if wire and not a.e2e_wire:
+                continue
+            t_e, e_ops, parts = 0.0, 0, {}
+            n2 = n_e2e // 2 - 1 if a.e2e_wire else n_e2e - 1
+            if n2 < 1:
+                continue
+            run.step_e2e(t_next, wire)
+            t_next += 1
+            for _ in range(n2):
+                g.synchronize()
+                c0 = time.perf_counter()
+                upd, r, s_ = run.step_e2e(t_next, wire)
+                t_e += time.perf_counter() - c0
+                t_next += 1
+                e_ops += upd
+                for k, v in run.e2e_parts.items():
+                    parts[k] = parts.get(k, 0.0) + v
+            pa = {k: v / n2 for k, v in parts.items()}
+            h2d = pa["ops_bytes"]
+            d2h = pa["event_bytes"] + pa["record_bytes"] + pa.get("wire_bytes", 0)
+            ms = t_e / n2 * 1e3
+            # PCIe roofline of the step: its host<->device bytes at the copy rate
+            # tools/micro/pcie.hip measures on the box (pinned, one stream)
+            floor_ms = (h2d + d2h) / (PCIE_GBS * 1e9) * 1e3
+            e2e[key] = {
+                "ms_per_step": ms, "updates_per_sec": e_ops / t_e, "steps": n2,
+                "breakdown_ms": {k: round(pa[k] * 1e3, 3) for k in ("submit", "tick", "collect", "wire") if k in pa},
+                "device_ms": {"tick": round(pa["tick_device_us"] / 1e3, 3),
+                              "collect": round(pa["collect_device_us"] / 1e3, 3),
+                              **({"wire": round(pa["wire_device_us"] / 1e3, 3)} if wire else {})},
+                "bytes_per_step": {"ops_h2d": h2d, "events_d2h": pa["event_bytes"],
+                                   **({"wire_d2h": pa["wire_bytes"]} if wire else {"records_d2h": pa["record_bytes"]})},
+                "pcie_GBps": {"tick": round(pa["event_bytes"] / pa["tick"] / 1e9, 2),
+                              **({"wire": round(pa["wire_bytes"] / pa["wire"] / 1e9, 2)} if wire else
+                                 {"collect": round(pa["record_bytes"] / pa["collect"] / 1e9, 2)})},
+                "pcie_roofline": {"bound": "pcie", "peak_GBps": PCIE_GBS, "floor_ms": round(floor_ms, 3),
+                                  "frac": round(floor_ms / ms, 3)},
+                "what": ("gw_submit(host ops) + gw_tick(COPY_TO_HOST) + gw_sync_collect() + "
+                         "gw_sync_encode_wire(COPY_TO_HOST): the Go shim's tick (INTEGRATION.md), events and "
+                         "48-B wire packets to pinned host memory" if wire else
+                         "gw_submit(host ops) + gw_tick(COPY_TO_HOST) + gw_sync_collect(COPY_TO_HOST): events "
+                         "and compact 24-B records to pinned host memory") +
+                        "; wall clock per call (device_ms: HIP events of the same calls, copies included); "
+                        "untimed by the headline"}
     parallelism, n_world, m_rank = run.parallelism, run.n_world, run.m
     run.close()
     def world_leg(which, warmup, steps, workload):
@@ -812,8 +832,8 @@ def main():
         "load_s": t_load,
     }
     line.update(roofline_fields(res, K, cfg_no, ws))
+    line.update(e2e)
     if e2e:
-        line["t_e2e"] = e2e
         line["t_device_ms_per_step"] = mx / K * 1e3
     if client:
         line["client_msgs"] = client

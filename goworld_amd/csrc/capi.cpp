@@ -67,7 +67,10 @@ int ensure(gw_ctx* c, DevBuf& b, size_t bytes) {
 int ensure_host(gw_ctx* c, DevBuf& b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return 0;
-    size_t nb = std::max(bytes, b.cap + b.cap / 2);
+    // pinned allocations cost ~0.16 ms per MB (hipHostMalloc 700 MB: 111 ms on
+    // the box, tools/micro/pcie.hip): a quarter of headroom, so the per-tick
+    // output sizes (which vary by a few %) do not reallocate every other tick
+    size_t nb = std::max(bytes + bytes / 4, b.cap + b.cap / 2);
     if (b.p) HIPCHK(hipHostFree(b.p));
     b.p = nullptr;
     b.cap = 0;

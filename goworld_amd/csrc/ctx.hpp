@@ -174,7 +174,7 @@ struct gw_ctx {
     DevBuf scan_status, rs_hist;
     uint32_t walk_min = 32;              // GW_WALK_MIN: TickBufs.walk_min (0: always walk)
     uint32_t rank_sort = 12;             // GW_RANK_SORT: TickBufs.rank_sort
-    uint32_t pair_max = 96;              // GW_PAIR_MAX: TickBufs.pair_max
+    uint32_t pair_max = 0;               // GW_PAIR_MAX: TickBufs.pair_max (0: off; 96 measured +47 us at config #3)
     uint32_t grid_cap = 0;               // GW_GRID_CAP: TickBufs.grid_cap (tests of the grid-stride loops)
     uint64_t ev_cap = 0;                 // events the flatten/sort buffers hold (grows on overflow)
     uint64_t ev_est = 0;                 // events expected this tick (last tick's count): sizes the buckets

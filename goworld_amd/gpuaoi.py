@@ -500,11 +500,15 @@ class GpuAOI:
         self._chk(lib().gw_submit_client_sync(self._h, _p(b), len(b) // 32, C.byref(ap), C.byref(tc)))
         return ap.value, tc.value
 
-    def encode_wire(self, copy: bool = True):
-        """-> (bytes or None, [(gate, offset, length)], n_bytes, device_us) of the last collect's packets."""
+    def encode_wire(self, copy: bool = True, view: bool = False):
+        """-> (bytes or None, [(gate, offset, length)], n_bytes, device_us) of the last collect's packets.
+        view (with copy): the packets are a u8 view of the library's pinned host buffer (valid until
+        the next encode), as a Go caller would read them in place."""
         o = WireOut()
         self._chk(lib().gw_sync_encode_wire(self._h, 1 if copy else 0, C.byref(o)))
         pk = [(o.gate[k], o.off[k], o.off[k + 1] - o.off[k]) for k in range(o.n_packets)]
+        if copy and view:
+            return _host_view(o.bytes, o.n_bytes, np.dtype(np.uint8)), pk, o.n_bytes, o.device_us
         data = C.string_at(o.bytes, o.n_bytes) if (copy and o.n_bytes) else (b"" if copy else None)
         return data, pk, o.n_bytes, o.device_us
 

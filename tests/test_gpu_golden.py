@@ -158,11 +158,12 @@ def test_grid_stride_passes_capped(gpu, cap, monkeypatch):
     g.close()
 
 
-@pytest.mark.parametrize("pair_max", [0, 1 << 20])
+@pytest.mark.parametrize("pair_max", [96, 1 << 20])
 def test_mover_pairing_modes(gpu, pair_max, monkeypatch):
-    """The diff runs two short-list movers per wave (k_mover_pair, default
-    GW_PAIR_MAX = 96 candidates) and longer ones one per wave (mover_one):
-    forcing either path for every mover gives the same config #2 digests."""
+    """With GW_PAIR_MAX > 0 the diff runs two short-list movers per wave
+    (k_mover_pair; off by default since it measured slower at config #3) and
+    longer ones one per wave (mover_one): the mixed path (96) and pairing every
+    mover give the same config #2 digests as the default one-wave path."""
     monkeypatch.setenv("GW_PAIR_MAX", str(pair_max))
     name = "config2_100k"
     d = G.digests()[name]

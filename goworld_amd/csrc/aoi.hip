@@ -483,7 +483,9 @@ __device__ __forceinline__ Rects mover_rects(const SpaceP& P, bool po, float ox,
 }
 
 // candidate bound of each primary mover-grid entry (entries of gn and gm in
-// its cells) -> the size of its own-event region
+// its cells) -> the size of its own-event region.  The index ranges of its
+// rows (<= RR_ROWS) go to rowrec for k_mover, whose wave then starts its walk
+// one load after its entry instead of three (entry -> space -> row starts).
 __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
     const uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x;
     if (m >= b.st->n_gm) return;
@@ -492,15 +494,23 @@ __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
     if (e.tags & TAG_PRIMARY) {
         const SpaceP P = b.w.sp[e.space];
         const Rects R = mover_rects(P, e.ox == e.ox, e.ox, e.oz, e.x == e.x, e.x, e.z);
+        uint4* rec = b.rowrec ? b.rowrec + m * RR_ROWS : nullptr;
+        uint32_t nr = 0;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             if (q >= R.n) break;
             const Rect rr = q == 0 ? R.r[0] : R.r[1];
-            for (int cz = rr.z0; cz <= rr.z1; ++cz) {
+            for (int cz = rr.z0; cz <= rr.z1; ++cz, ++nr) {
                 const uint32_t row = P.cell_base + (uint32_t)cz * (uint32_t)P.W;
-                c += b.w.gn_start[row + rr.x1 + 1] - b.w.gn_start[row + rr.x0];
-                c += b.gm_start[row + rr.x1 + 1] - b.gm_start[row + rr.x0];
+                const uint32_t g0 = b.w.gn_start[row + rr.x0], g1 = b.w.gn_start[row + rr.x1 + 1];
+                const uint32_t m0 = b.gm_start[row + rr.x0], m1 = b.gm_start[row + rr.x1 + 1];
+                c += (g1 - g0) + (m1 - m0);
+                if (rec && nr < RR_ROWS) rec[nr] = make_uint4(g0, g1, m0, m1);
             }
+        }
+        if (rec) {
+            if (nr > RR_ROWS) rec[0] = make_uint4(1u, 0u, 0u, 0u);   // too many rows: k_mover builds its own
+            for (uint32_t r = nr; r < RR_ROWS; ++r) rec[r] = make_uint4(0u, 0u, 0u, 0u);
         }
     }
     b.cand[m] = c;
@@ -552,10 +562,14 @@ struct GlobalSrc {
 
 // One mover-grid entry m by one wave, candidates from S; lds: SCAP sort slots
 // per wave.
-template <int DIFF_U, uint32_t SCAP, class Src>
+// RR (k_mover): the row ranges k_bounds gathered, loaded with the entry
+// itself (the walk then starts one round trip after the wave does).
+template <int DIFF_U, uint32_t SCAP, class Src, bool RR = false>
 __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_t* lds, const Src& S) {
-    const MEnt me = S.gm(m);
     const int ln = lane_id();
+    const uint2 rr = (RR && ln < (int)(2 * RR_ROWS)) ? ((const uint2*)b.rowrec)[m * 2 * RR_ROWS + ln]
+                                                    : make_uint2(0u, 0u);
+    const MEnt me = S.gm(m);
     if (!(me.tags & TAG_PRIMARY)) {
         if (ln == 0) {
             b.mstat[m] = 0;
@@ -588,12 +602,15 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     const bool longA = (me.tags & TAG_LONG) != 0;
     const unsigned long long sA = w.stamp[A], soA = w.prev[A].ostamp;
     const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
-    const Rects R = mover_rects(P, po, me.ox, me.oz, pn, me.x, me.z);
     uint32_t* out = b.own + reg;
     uint64_t* mir = b.mir + reg;
     uint32_t n = 0, nl = 0, nm_ = 0, nml = 0;
     uint32_t c_old = 0, c_new = 0, c_cli = 0;
-    Flat f = S.flat(P, R);
+    Flat f;
+    if (RR && (uint32_t)__builtin_amdgcn_readfirstlane((int)rr.x) <= (uint32_t)__builtin_amdgcn_readfirstlane((int)rr.y))
+        f = flat_from(rr.x, rr.y - rr.x);
+    else
+        f = S.flat(P, mover_rects(P, po, me.ox, me.oz, pn, me.x, me.z));
     // long ranges (crowded rows): walk the live ranges with readlanes, a chunk
     // overlaps one or two of them; short ones: the shuffle binary search
     const bool walk = f.total >= (uint32_t)popc64(f.live) * b.walk_min;
@@ -733,7 +750,7 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[WPB * SORT_LDS];
     const uint64_t m = (uint64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
     if (m >= b.st->n_gm) return;
-    mover_one<DIFF_U, SORT_LDS>(b, m, lds, GlobalSrc{b.w.gn, b.w.gn_start, b.gm_start, b.gm});
+    mover_one<DIFF_U, SORT_LDS, GlobalSrc, true>(b, m, lds, GlobalSrc{b.w.gn, b.w.gn_start, b.gm_start, b.gm});
 }
 
 // Two mover-grid entries per wave (a half-wave each), small-space mode: with

@@ -515,7 +515,7 @@ void gw_shutdown(gw_ctx* c) {
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
     DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1,
-                      &c->gm, &c->cand, &c->reg, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
+                      &c->gm, &c->cand, &c->reg, &c->rowrec, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
                       &c->mcnt, &c->moff, &c->minfo, &c->icnt, &c->ioff, &c->mreg, &c->chunk_first, &c->srange, &c->bk_a, &c->bk_b, &c->bk_id, &c->bk_cnt, &c->bk_split, &c->ev_d, &c->rtable,
                       &c->scan_status, &c->rs_hist,
                       &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
@@ -1200,6 +1200,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     if ((rc = ensure(c, c->gm, M2 * sizeof(MEnt))) || (rc = ensure(c, c->mtmp, (size_t)M * sizeof(MEnt))) ||
         (rc = ensure(c, c->mcell, (size_t)M * 16)) ||
         (rc = ensure(c, c->cand, M2 * 8)) || (rc = ensure(c, c->reg, M2 * 8)) ||
+        (rc = ensure(c, c->rowrec, M2 * RR_ROWS * 16)) ||
         (rc = ensure(c, c->ownc, M2 * 8)) || (rc = ensure(c, c->mirc, M2 * 8)) || (rc = ensure(c, c->big, M2 * 4)) ||
         (rc = ensure(c, c->mstat, M2 * 8)) ||
         (rc = ensure(c, c->mlist, (size_t)M * 4)) || (rc = ensure(c, c->mcnt, (size_t)M * 8)) ||
@@ -1246,6 +1247,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.gm_cnt = c->gm_cnt; b.gm_start = c->gm_start; b.gm = P<MEnt>(c->gm);
     b.mtmp = P<MEnt>(c->mtmp); b.mcell = P<uint4>(c->mcell);
     b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg);
+    b.rowrec = P<uint4>(c->rowrec);
     b.ownc = P<unsigned long long>(c->ownc); b.mirc = P<unsigned long long>(c->mirc);
     b.big = P<uint32_t>(c->big);
     b.mstat = P<unsigned long long>(c->mstat);
@@ -1256,6 +1258,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.icnt = P<uint32_t>(c->icnt); b.ioff = P<uint32_t>(c->ioff);
     b.wbits = ceil_log2(C);
     small_mode(c, b);
+    if (b.small_ents || b.pair_max) b.rowrec = nullptr;   // only k_mover reads the row ranges
     bind_events(c, b);
     if (!c->ev_est) c->ev_est = 16ull * M;
     choose_buckets(c, b);

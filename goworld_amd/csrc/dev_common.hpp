@@ -106,6 +106,18 @@ __device__ __forceinline__ Flat flat_build(const SpaceP& P, const Rects& R, cons
     return f;
 }
 
+// The same from ranges already gathered (lane j: range j = [s, s + l))
+__device__ __forceinline__ Flat flat_from(uint32_t s, uint32_t l) {
+    Flat f;
+    const uint32_t inc = wave_incl_scan<uint32_t>(l);
+    f.start = s;
+    f.len = l;
+    f.pre = inc - l;
+    f.total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    f.live = wave_ballot(l != 0);
+    return f;
+}
+
 // Maps the lane's candidates k = B + 64u + lane (u < U) to (grid, index);
 // idx = ~0 past the end.  Each lane finds its range by a binary search over
 // the ranges' exclusive prefixes (the largest range j with pre[j] <= k; empty

@@ -173,6 +173,9 @@ struct World {
     int nb_u;                  // candidate chunks of 64 in flight in the sync walks
 };
 
+// rows of a mover's rectangles whose index ranges k_bounds hands to k_mover
+constexpr uint32_t RR_ROWS = 8;
+
 // ---- tick buffers handed to the launchers ----------------------------------
 struct TickBufs {
     World w;                  // gn / gn_start: the grid before the tick (the new one from tick_movers on)
@@ -200,6 +203,8 @@ struct TickBufs {
     // diff (indexed by mover-grid entry)
     uint64_t* cand;           // [2m] candidate bound (0 unless TAG_PRIMARY)
     uint64_t* reg;            // [2m] exclusive scan of cand
+    uint4* rowrec;            // [2m * RR_ROWS] per primary entry: its rows' grid / mover-grid index ranges
+                              // (start, end, start, end) from k_bounds; row 0 = (1, 0, ..) when > RR_ROWS rows
     uint64_t own_cap;         // capacity of own / mir
     uint32_t* own;            // own events (target<<1 | leave), sorted by target per mover
     uint64_t* mir;            // mirror events of op-less neighbours: watcher<<32 | mover<<1 | leave

@@ -364,16 +364,16 @@ __global__ void __launch_bounds__(NT) k_grid_copy(TickBufs b) {
 // arrivals (few, in arrival order at the cell's tail) by rank: a kept entry
 // moves up by the arrivals with a smaller slot, an arrival lands after the
 // kept entries and arrivals with a smaller slot.  A wave scans the flags of
-// DIRTY_SPAN cells and merges its dirty ones; cells with more than 64
+// dirty_span cells and merges its dirty ones; cells with more than 64
 // arrivals are compacted and sorted by the wave (bitonic, in place).
-constexpr uint32_t DIRTY_SPAN = 16;
 __global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
-    const uint32_t c0 = (blockIdx.x * NWAVE + (threadIdx.x >> 6)) * DIRTY_SPAN;
+    const uint32_t span = b.dirty_span;
+    const uint32_t c0 = (blockIdx.x * NWAVE + (threadIdx.x >> 6)) * span;
     if (c0 >= b.w.ncells) return;
     const uint32_t cl = c0 + ln;
-    uint64_t dm = wave_ballot(ln < (int)DIRTY_SPAN && cl < b.w.ncells && (b.dep[cl] & CELL_DIRTY));
+    uint64_t dm = wave_ballot(ln < (int)span && cl < b.w.ncells && (b.dep[cl] & CELL_DIRTY));
     while (dm) {
         const uint32_t c = c0 + (uint32_t)__builtin_ctzll(dm);
         dm &= dm - 1;
@@ -450,7 +450,7 @@ void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
                 (uint32_t*)&b.st->n_gm, s);
     hipLaunchKernelGGL(k_place, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
     hipLaunchKernelGGL(k_grid_copy, dim3(std::min<uint32_t>(nblk1(b.w.cap, NT), 16384)), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_grid_dirty, dim3(nblk1((uint64_t)NC, DIRTY_SPAN * NWAVE)), dim3(NT), 0, s, b);
+    hipLaunchKernelGGL(k_grid_dirty, dim3(nblk1((uint64_t)NC, b.dirty_span * NWAVE)), dim3(NT), 0, s, b);
 }
 
 // ---------------------------------------------------------------------------

@@ -329,9 +329,14 @@ int read_stats(gw_ctx* c) {
     return 0;
 }
 
+// the collect's statistics; with a deferred tick pending, the tick's too (one
+// copy of both: the tick's are final once the collect's launches are queued)
 int read_cstats(gw_ctx* c) {
-    HIPCHK(hipMemcpyAsync(c->hcstats, c->cstats, sizeof(DevStats), hipMemcpyDeviceToHost, c->st));
+    const bool both = c->pt.on && !c->pt.copied;
+    HIPCHK(hipMemcpyAsync(both ? c->hstats : c->hcstats, both ? c->stats : c->cstats,
+                          (both ? 2 : 1) * sizeof(DevStats), hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    if (both) c->pt.copied = true;
     return 0;
 }
 
@@ -478,18 +483,19 @@ int gw_init(int device_id, gw_ctx** out) {
         if (hipSetDevice(device_id) != hipSuccess) { rc = set_err(c, GW_EDEVICE, "hipSetDevice(%d) failed", device_id); break; }
         if (hipStreamCreateWithFlags(&c->own_st, hipStreamNonBlocking) != hipSuccess) { rc = set_err(c, GW_EDEVICE, "stream"); break; }
         c->st = c->own_st;
-        if (hipMalloc(&c->stats, sizeof(DevStats)) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "stats"); break; }
-        if (hipHostMalloc((void**)&c->hstats, sizeof(DevStats), hipHostMallocDefault) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "hstats"); break; }
-        if (hipMalloc(&c->cstats, sizeof(DevStats)) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "cstats"); break; }
-        if (hipHostMalloc((void**)&c->hcstats, sizeof(DevStats), hipHostMallocDefault) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "hcstats"); break; }
+        // the tick's and the collect's statistics side by side, so a collect
+        // that settles a deferred tick reads both with one copy
+        if (hipMalloc(&c->stats, 2 * sizeof(DevStats)) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "stats"); break; }
+        if (hipHostMalloc((void**)&c->hstats, 2 * sizeof(DevStats), hipHostMallocDefault) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "hstats"); break; }
+        c->cstats = c->stats + 1;
+        c->hcstats = c->hstats + 1;
         if (hipMalloc(&c->scal32, 64) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "scal"); break; }
         if (hipMalloc(&c->halo, sizeof(HaloStats)) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "halo"); break; }
         (void)hipMemset(c->halo, 0, sizeof(HaloStats));
         if (hipMalloc(&c->sc.ticket, 8) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "ticket"); break; }
         (void)hipMemset(c->sc.ticket, 0, 8);
-        memset(c->hstats, 0, sizeof(DevStats));
-        (void)hipMemset(c->stats, 0, sizeof(DevStats));
-        (void)hipMemset(c->cstats, 0, sizeof(DevStats));
+        memset(c->hstats, 0, 2 * sizeof(DevStats));
+        (void)hipMemset(c->stats, 0, 2 * sizeof(DevStats));
         (void)hipEventCreate(&c->ev_t0);
         (void)hipEventCreate(&c->ev_t1);
         if (const char* e = getenv("GW_CELLS_PER_D")) c->cells_per_d = std::min(4, std::max(1, atoi(e)));
@@ -499,6 +505,7 @@ int gw_init(int device_id, gw_ctx** out) {
         if (const char* e = getenv("GW_RANK_SORT")) c->rank_sort = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_GRID_CAP")) c->grid_cap = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_PAIR_MAX")) c->pair_max = (uint32_t)std::max(0, atoi(e));
+        if (const char* e = getenv("GW_DIRTY_SPAN")) c->dirty_span = (uint32_t)std::min(64, std::max(1, atoi(e)));
     } while (0);
     if (rc) {
         (void)hipGetLastError();
@@ -538,11 +545,10 @@ void gw_shutdown(gw_ctx* c) {
                     &c->m_destroy.h, &c->m_fanout.h};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
     void* ps[] = {c->halo, c->sc.ticket, c->movbit, c->gmi, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->nbc, c->ol,
-                  c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->cstats, c->scal32, c->gsb[0],
+                  c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->scal32, c->gsb[0],
                   c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->gm_start};
     for (void* p : ps) if (p) (void)hipFree(p);
-    if (c->hstats) (void)hipHostFree(c->hstats);
-    if (c->hcstats) (void)hipHostFree(c->hcstats);
+    if (c->hstats) (void)hipHostFree(c->hstats);   // hcstats lives behind it
     for (auto& s : c->stages) { (void)hipEventDestroy(s.a); (void)hipEventDestroy(s.b); }
     if (c->ev_t0) (void)hipEventDestroy(c->ev_t0);
     if (c->ev_t1) (void)hipEventDestroy(c->ev_t1);
@@ -1168,7 +1174,21 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         if ((rc = ensure(c, c->ops_buf, (size_t)M * sizeof(gw_op)))) return rc;
         if (any_stamped && (rc = ensure(c, c->stamp_buf, (size_t)M * 8))) return rc;
         size_t off = 0;
+        bool all_dev = c->segs.size() <= (size_t)SEG_MAX;
+        for (auto& s : c->segs) all_dev &= !s.host && (!any_stamped || s.rows || s.stamps);
+        if (all_dev) {                               // one launch for every segment
+            SegTable t{};
+            for (auto& s : c->segs) {
+                t.seg[t.n] = SegTable::Seg{s.dev, (const unsigned long long*)s.stamps, s.rows, (uint32_t)off};
+                ++t.n;
+                off += s.n;
+            }
+            t.total = (uint32_t)off;
+            launch_gather_segs(t, P<gw_op>(c->ops_buf), any_stamped ? P<unsigned long long>(c->stamp_buf) : nullptr,
+                               c->st);
+        }
         for (auto& s : c->segs) {
+            if (all_dev) break;
             if (s.rows)
                 launch_split_rows(s.rows, s.n, P<gw_op>(c->ops_buf) + off, P<unsigned long long>(c->stamp_buf) + off,
                                   c->st);
@@ -1238,6 +1258,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.rank_sort = c->rank_sort;
     b.grid_cap = c->grid_cap;
     b.pair_max = c->pair_max;
+    b.dirty_span = c->dirty_span;
     b.long_step = c->wd.on ? c->wd.g.max_step : INFINITY;   // decomposed world: long movers
     b.conflicts = c->wd.on ? &c->halo->conflicts : nullptr;
     b.ol = c->ol;
@@ -1299,8 +1320,8 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     p.b = b;
     if ((flags & GW_TICK_DEFER) && !(flags & GW_TICK_COPY_TO_HOST) && !host_ops) {
         // no host sync now: the next call that needs the results settles it
-        HIPCHK(hipMemcpyAsync(c->hstats, c->stats, sizeof(DevStats), hipMemcpyDeviceToHost, c->st));
-        p.copied = true;
+        // (a collect reads the statistics with its own; anything else copies them)
+        p.copied = false;
         out->ops = M;
         return 0;
     }

@@ -174,6 +174,7 @@ struct gw_ctx {
     DevBuf scan_status, rs_hist;
     uint32_t walk_min = 32;              // GW_WALK_MIN: TickBufs.walk_min (0: always walk)
     uint32_t rank_sort = 12;             // GW_RANK_SORT: TickBufs.rank_sort
+    uint32_t dirty_span = 16;            // GW_DIRTY_SPAN: TickBufs.dirty_span
     uint32_t pair_max = 0;               // GW_PAIR_MAX: TickBufs.pair_max (0: off; 96 measured +47 us at config #3)
     uint32_t grid_cap = 0;               // GW_GRID_CAP: TickBufs.grid_cap (tests of the grid-stride loops)
     uint64_t ev_cap = 0;                 // events the flatten/sort buffers hold (grows on overflow)

@@ -236,6 +236,7 @@ struct TickBufs {
     float long_step;          // decomposed world: an owned mover whose x moves further is a long
                               // mover (its pairs are attributed to the targets' owners); +inf otherwise
     unsigned long long* conflicts;   // decomposed world: long-mover pairs related before or after (or null)
+    uint32_t dirty_span;      // GW_DIRTY_SPAN: cells whose dirty flags one k_grid_dirty wave scans (1..64)
     uint32_t pair_max;        // GW_PAIR_MAX: k_mover_pair runs two movers per wave when both have at
                               // most this many candidates (0 = one mover per wave, k_mover)
     uint32_t grid_cap;        // GW_GRID_CAP (tests): at most this many blocks for the grid-stride
@@ -362,6 +363,19 @@ void launch_route_halo(const World& w, const gw_op* ops, const unsigned long lon
 void launch_far_partition(const gw_halo_row* rows, const uint32_t* dest, uint32_t n, const uint32_t* off,
                           uint32_t* cursor, uint32_t nranks, gw_halo_row* out, hipStream_t s);
 void launch_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n, hipStream_t s);
+// up to SEG_MAX device segments of a tick's op stream (halo rows, or ops with
+// stamps when the tick is stamped) gathered by one launch
+constexpr int SEG_MAX = 8;
+struct SegTable {
+    struct Seg {
+        const gw_op* ops;
+        const unsigned long long* stamps;
+        const gw_halo_row* rows;
+        uint32_t off;
+    } seg[SEG_MAX];
+    uint32_t n, total;
+};
+void launch_gather_segs(const SegTable& t, gw_op* ops, unsigned long long* stamps, hipStream_t s);
 void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,
                        hipStream_t s);
 void launch_watcher_keys(const gw_sync_record* rec, uint64_t n, uint32_t* keys, uint32_t* vals, hipStream_t s);

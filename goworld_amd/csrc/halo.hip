@@ -228,7 +228,32 @@ __global__ void __launch_bounds__(NT) k_split_rows(const gw_halo_row* __restrict
     stamps[i] = rows[i].stamp;
 }
 
+// the tick's device segments (ops with or without stamps, halo rows) into
+// one op stream by one launch (a copy per segment was a blit launch each:
+// ~3.5 us apiece per world tick)
+__global__ void __launch_bounds__(NT) k_gather_segs(SegTable t, gw_op* __restrict__ ops,
+                                                    unsigned long long* __restrict__ stamps) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i >= t.total) return;
+    uint32_t k = 0;
+    while (k + 1 < t.n && i >= t.seg[k + 1].off) ++k;
+    const SegTable::Seg& g = t.seg[k];
+    const uint32_t j = i - g.off;
+    if (g.rows) {
+        const gw_halo_row r = g.rows[j];
+        ops[i] = r.op;
+        if (stamps) stamps[i] = r.stamp;
+    } else {
+        ops[i] = g.ops[j];
+        if (stamps) stamps[i] = g.stamps[j];
+    }
+}
+
 }  // namespace
+
+void launch_gather_segs(const SegTable& t, gw_op* ops, unsigned long long* stamps, hipStream_t s) {
+    if (t.total) hipLaunchKernelGGL(k_gather_segs, dim3(nblk1(t.total, NT)), dim3(NT), 0, s, t, ops, stamps);
+}
 
 void launch_route_halo(const World& w, const gw_op* ops, const unsigned long long* stamps, uint32_t n,
                        float max_step, const HaloDsts& D, OpLast* ol, uint32_t ol_tag, HaloStats* hs, hipStream_t s,

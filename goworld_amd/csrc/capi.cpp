@@ -43,11 +43,15 @@ int set_err(gw_ctx* c, int code, const char* fmt, ...) {
 
 
 // (re)allocate scratch without preserving contents; callers only grow buffers
-// at points where the stream is idle (after a host sync)
+// at points where the stream is idle (after a host sync).  An eighth of
+// headroom: buffers sized by the tick's op count (which drifts by a few per
+// mille between ticks in a world strip) otherwise reallocated whenever it
+// reached a new high, each time a device sync plus hipFree / hipMalloc of up to
+// hundreds of MB (0.3-1.2 ms on a 16M world strip)
 int ensure(gw_ctx* c, DevBuf& b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return 0;
-    size_t nb = std::max(bytes, b.cap + b.cap / 2);
+    size_t nb = std::max(bytes + bytes / 8, b.cap + b.cap / 2);
     nb = (nb + 255) & ~(size_t)255;
     if (b.p) {
         HIPCHK(hipStreamSynchronize(c->st));

@@ -76,6 +76,8 @@ class SimWorld(dworld.LocalWorld):
         rows = self.route_submit(ptrs, ms, times)
         if phases is not None:
             phases["route"] += sum(times)
+            for r in range(self.R):
+                phases["per_rank"][r][0] += times[r]
         upd = ev = rec = 0
         for r, g in enumerate(self.g):
             g.synchronize()
@@ -88,6 +90,8 @@ class SimWorld(dworld.LocalWorld):
             if phases is not None:
                 phases["tick_call"] += t1 - t0
                 phases["collect_call"] += t2 - t1
+                phases["per_rank"][r][1] += t1 - t0
+                phases["per_rank"][r][2] += t2 - t1
             res = g.tick_result()
             upd += ms[r]
             ev += res.n_enter + res.n_leave
@@ -135,7 +139,7 @@ def main():
         per = np.zeros(R)
         smax = 0.0
         upd = ev = rec = rows = 0
-        phases = {"route": 0.0, "tick_call": 0.0, "collect_call": 0.0}
+        phases = {"route": 0.0, "tick_call": 0.0, "collect_call": 0.0, "per_rank": [[0.0, 0.0, 0.0] for _ in range(R)]}
         for t in range(a.warmup, ticks):
             ts, u, e, rc, rw = w.step(t, phases)
             per += np.array(ts)
@@ -153,7 +157,10 @@ def main():
                 "projected_updates_per_sec_excl_exchange": upd / a.steps / (step_ms * 1e-3),
                 "projected_events_per_sec_excl_exchange": ev / a.steps / (step_ms * 1e-3),
                 "load_s": round(load, 1),
-                "host_us_per_rank_step": {k: round(v / a.steps / R * 1e6, 1) for k, v in phases.items()}}
+                "host_us_per_rank_step": {k: round(v / a.steps / R * 1e6, 1) for k, v in phases.items()
+                                          if k != "per_rank"},
+                "route_tick_collect_us_by_rank": [[round(v / a.steps * 1e6, 1) for v in pr]
+                                                  for pr in phases["per_rank"]]}
         if stages:
             line["rank0_device_us_per_stage"] = stages
         if base is None and R == 1:

@@ -508,7 +508,10 @@ int gw_init(int device_id, gw_ctx** out) {
         if (const char* e = getenv("GW_WALK_MIN")) c->walk_min = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_RANK_SORT")) c->rank_sort = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_GRID_CAP")) c->grid_cap = (uint32_t)std::max(0, atoi(e));
-        if (const char* e = getenv("GW_PAIR_MAX")) c->pair_max = (uint32_t)std::max(0, atoi(e));
+        if (const char* e = getenv("GW_PAIR_MAX")) {
+            c->pair_max = (uint32_t)std::max(0, atoi(e));
+            c->pair_auto = false;
+        }
         if (const char* e = getenv("GW_DIRTY_SPAN")) c->dirty_span = (uint32_t)std::min(64, std::max(1, atoi(e)));
     } while (0);
     if (rc) {
@@ -1081,6 +1084,7 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     o.ops = M;
     o.movers = n_mov;
     o.pairs_tested = pairs;
+    if (!(flags & GW_TICK_NO_EVENTS) && n_mov) c->cand_mean = n_mov >= gw_ctx::PAIR_MOVERS ? pairs / n_mov : ~0ull;
     o.nbr_old = a_old;
     o.nbr_new = a_new;
     o.enter_dev = (flags & GW_TICK_NO_EVENTS) ? nullptr : P<gw_event>(c->ev_d);
@@ -1261,7 +1265,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.walk_min = c->walk_min;
     b.rank_sort = c->rank_sort;
     b.grid_cap = c->grid_cap;
-    b.pair_max = c->pair_max;
+    b.pair_max = c->pair_auto ? (c->cand_mean <= gw_ctx::PAIR_MEAN ? gw_ctx::PAIR_AUTO : 0u) : c->pair_max;
     b.dirty_span = c->dirty_span;
     b.long_step = c->wd.on ? c->wd.g.max_step : INFINITY;   // decomposed world: long movers
     b.conflicts = c->wd.on ? &c->halo->conflicts : nullptr;

@@ -122,6 +122,7 @@ struct gw_ctx {
     uint16_t max_gate = 0;
     unsigned long long stamp_base = 1;   // global op counter (stamp 0 = never)
     uint32_t epoch = 1;                  // bumped by every tick and client change (World.nbc)
+    static constexpr uint32_t PAIR_AUTO = 96, PAIR_MEAN = 128, PAIR_MOVERS = 131072;
     int cells_per_d = 2;                 // grid cells per AOI distance (GW_CELLS_PER_D)
     int diff_u = 1, nb_u = 4;            // k_mover waves per block (GW_MOVER_WPB), sync chunks in flight (GW_NB_U)
     bool grid_dirty = true;              // gn/gn_start must be rebuilt before queries
@@ -175,7 +176,14 @@ struct gw_ctx {
     uint32_t walk_min = 32;              // GW_WALK_MIN: TickBufs.walk_min (0: always walk)
     uint32_t rank_sort = 12;             // GW_RANK_SORT: TickBufs.rank_sort
     uint32_t dirty_span = 16;            // GW_DIRTY_SPAN: TickBufs.dirty_span
-    uint32_t pair_max = 0;               // GW_PAIR_MAX: TickBufs.pair_max (0: off; 96 measured +47 us at config #3)
+    // GW_PAIR_MAX: TickBufs.pair_max.  Unset: automatic, PAIR_AUTO when the last
+    // tick had >= PAIR_MOVERS movers averaging <= PAIR_MEAN candidates (many
+    // uniform short lists: config #5 diff 1677 -> 1573 us), else 0 (hotspots:
+    // two long movers in one wave made config #3's diff 192 -> 239 us; few
+    // movers: half the waves, config #2's 10k movers 15 -> 18 us)
+    uint32_t pair_max = 0;
+    bool pair_auto = true;
+    uint64_t cand_mean = ~0ull;          // candidates per mover of the last tick
     uint32_t grid_cap = 0;               // GW_GRID_CAP: TickBufs.grid_cap (tests of the grid-stride loops)
     uint64_t ev_cap = 0;                 // events the flatten/sort buffers hold (grows on overflow)
     uint64_t ev_est = 0;                 // events expected this tick (last tick's count): sizes the buckets

@@ -1228,7 +1228,6 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     if ((rc = ensure(c, c->gm, M2 * sizeof(MEnt))) || (rc = ensure(c, c->mtmp, (size_t)M * sizeof(MEnt))) ||
         (rc = ensure(c, c->mcell, (size_t)M * 16)) ||
         (rc = ensure(c, c->cand, M2 * 8)) || (rc = ensure(c, c->reg, M2 * 8)) ||
-        (rc = ensure(c, c->rowrec, M2 * RR_ROWS * 16)) ||
         (rc = ensure(c, c->ownc, M2 * 8)) || (rc = ensure(c, c->mirc, M2 * 8)) || (rc = ensure(c, c->big, M2 * 4)) ||
         (rc = ensure(c, c->mstat, M2 * 8)) ||
         (rc = ensure(c, c->mlist, (size_t)M * 4)) || (rc = ensure(c, c->mcnt, (size_t)M * 8)) ||
@@ -1276,7 +1275,6 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.gm_cnt = c->gm_cnt; b.gm_start = c->gm_start; b.gm = P<MEnt>(c->gm);
     b.mtmp = P<MEnt>(c->mtmp); b.mcell = P<uint4>(c->mcell);
     b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg);
-    b.rowrec = P<uint4>(c->rowrec);
     b.ownc = P<unsigned long long>(c->ownc); b.mirc = P<unsigned long long>(c->mirc);
     b.big = P<uint32_t>(c->big);
     b.mstat = P<unsigned long long>(c->mstat);
@@ -1287,7 +1285,12 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.icnt = P<uint32_t>(c->icnt); b.ioff = P<uint32_t>(c->ioff);
     b.wbits = ceil_log2(C);
     small_mode(c, b);
-    if (b.small_ents || b.pair_max) b.rowrec = nullptr;   // only k_mover reads the row ranges
+    if (b.small_ents || b.pair_max || !ev_on) {
+        b.rowrec = nullptr;                          // only k_mover reads the row ranges
+    } else {
+        if ((rc = ensure(c, c->rowrec, M2 * RR_ROWS * 16))) return rc;
+        b.rowrec = P<uint4>(c->rowrec);
+    }
     bind_events(c, b);
     if (!c->ev_est) c->ev_est = 16ull * M;
     choose_buckets(c, b);

@@ -154,13 +154,14 @@ __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __re
             e = flagged[k];
             f = fbits[k];
             const AoiEnt a = w.aoi[e];
+            const uint32_t gt = w.gate[e];                  // loaded with the state, not behind the test
+            const unsigned long long c = w.nbc[e];
             // an entity that left the space (into the nil space, keeping its
             // flag) still syncs its own client (Entity.go:1221-1239); only a
             // present one has neighbours
             if (owned_x(w.sp[a.meta & SPACE_MASK], a.x)) {
-                if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) r = 1;
+                if ((f & GW_SIF_OWN_CLIENT) && gt) r = 1;
                 if ((f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
-                    const unsigned long long c = w.nbc[e];
                     if ((uint32_t)(c >> 32) == w.epoch) r += (uint32_t)c;   // counted by this tick's diff
                     else walk = true;
                 }
@@ -239,9 +240,10 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
             continue;
         }
         const AoiEnt a = w.aoi[e];
+        const float4 p = w.pos[e];                          // loaded with the state, not behind the test
+        const uint32_t gt = w.gate[e];
         if (!owned_x(w.sp[a.meta & SPACE_MASK], a.x)) continue;
-        const float4 p = w.pos[e];
-        if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
+        if ((f & GW_SIF_OWN_CLIENT) && gt) {
             if (ln == 0) st_record_nt(rec + at, e, e, p);
             ++at;
         }
@@ -419,30 +421,40 @@ __global__ void __launch_bounds__(NT) k_sync_write_small2(World w, const uint32_
     const uint64_t hmask = half ? 0xffffffff00000000ull : 0x00000000ffffffffull;
     const uint64_t lt = lanemask_lt();
     const float d = P.d;
+    // the entity's list entry, then its state: position and gate are loaded
+    // with the AOI state (not behind the ownership test), and the next
+    // entity's list entry is in flight during this one's walk
+    const auto entry = [&](uint32_t k, uint32_t& e, uint32_t& f, uint64_t& at, uint32_t& c) {
+        e = f = c = 0;
+        at = 0;
+        if (k < hi) { e = flagged[k]; f = fbits[k]; at = rec_off[k]; c = cnt[k]; }
+    };
+    uint32_t ne, nf, nc_;
+    uint64_t nat;
+    entry(lo + (threadIdx.x >> 6) * 2 + half, ne, nf, nat, nc_);
     for (uint32_t k0 = lo + (threadIdx.x >> 6) * 2; k0 < hi; k0 += NWAVE * 2) {
         const uint32_t k = k0 + half;
         const bool valid = k < hi;
-        uint32_t e = 0, f = 0, c = 0;
-        uint64_t at = 0;
-        if (valid) {
-            e = flagged[k];
-            f = fbits[k];
-            at = rec_off[k];
-            c = cnt[k];
-        }
+        const uint32_t e = ne, f = nf, c = nc_;
+        uint64_t at = nat;
+        entry(k0 + NWAVE * 2 + half, ne, nf, nat, nc_);
         bool walk = false;
         AoiEnt a;
         a.x = a.z = 0.0f;
         a.meta = 0;
         float4 p = make_float4(0, 0, 0, 0);
+        uint32_t gt = 0;
+        if (valid) {
+            a = w.aoi[e];
+            p = w.pos[e];
+            gt = w.gate[e];
+        }
         if (valid) {
             if (at + c > rec_cap) {
                 if (hl == 0) atomicOr(&st->overflow, 1ull);
             } else {
-                a = w.aoi[e];
                 if (owned_x(P, a.x)) {
-                    p = w.pos[e];
-                    if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
+                    if ((f & GW_SIF_OWN_CLIENT) && gt) {
                         if (hl == 0) st_record_nt(rec + at, e, e, p);
                         ++at;
                     }

@@ -259,12 +259,12 @@ struct TickBufs {
 constexpr int BK_NT = 1024;           // threads of the tile kernels
 constexpr int BK_TILE = 8192;         // flat positions per tile
 constexpr int BK_MAXBITS = 12;        // at most 4096 buckets
-constexpr int BK_LCAP = 7168;         // items a bucket may hold (LDS sort)
+constexpr int BK_LCAP = 3584;         // items a bucket may hold (LDS sort; 3.5x the mean: 44 KB of LDS, 3 blocks per CU)
 constexpr int BK_SNT = 512;           // threads of the bucket sort
 constexpr int BK_HBINS = 2048;        // bins of the counting sort inside a bucket
 constexpr int BK_SHORT = 16;          // longer bins are sorted by a wave
 constexpr int BK_RUNS = 512;          // own runs a bucket copies block-wide (more: by their lane); == BK_SNT
-constexpr uint64_t BK_MEAN = 2048;    // target mean bucket size when choosing bk_bits
+constexpr uint64_t BK_MEAN = 1024;    // target mean bucket size when choosing bk_bits (2048 with 7168: +6 us at config #3)
 constexpr uint32_t BK_NSPLIT = 1u << BK_MAXBITS;   // quantile table size
 // item bits: (leave, watcher, target) = 2*wbits + 1 <= BK_KEY_BITS, then the
 // run flag, then (staged only) the bucket in the top BK_MAXBITS bits

@@ -361,12 +361,15 @@ class SpaceRun:
         self.n_world = self.tr.n * (ctl.ws if ctl.ws > 1 else 1)
 
     def step(self, t):
-        g = self.g
-        g.submit_device(self.dev_ops + t * self.nbytes_tick, self.m)
-        g.tick(copy=False, defer=True)       # no host sync: the collect's sync settles it
-        s = g.sync_collect(copy=False, by_client=self.by_client)
-        r = g.tick_result()
+        # gw_step: submit + deferred tick + collect in one call (the collect's
+        # sync settles the tick); the library's output structs are read back
+        r, s = self.g.step_device(self.dev_ops + t * self.nbytes_tick, self.m, by_client=self.by_client)
         return r.movers, r, s
+
+    def replay(self, t0, k):
+        """gw_replay: steps t0 .. t0+k-1 (each one gw_step) in one call, the
+        tick loop in C as the Go caller runs it (no per-step Python)."""
+        return self.g.replay_device(self.dev_ops + t0 * self.nbytes_tick, self.m, self.m, k, by_client=self.by_client)
 
     def step_e2e(self, t, wire=False):
         """The Go caller's game tick: host ops in (gw_submit: pageable host
@@ -579,7 +582,13 @@ def measure(run, a, ctl, warmup, steps, profile, extra):
     ctl.barrier()
     g.synchronize()
     t0 = time.perf_counter()
-    for t in range(warmup, warmup + steps):
+    if hasattr(run, "replay"):                  # the K steps as one gw_replay call
+        sm = run.replay(warmup, steps)
+        ev = sm["n_enter"] + sm["n_leave"]
+        tot.update(ops=sm["movers"], events=ev, records=sm["n_rec"], bytes_alg=sm["bytes_alg"],
+                   mover_alg=4 * (sm["nbr_old"] + sm["nbr_new"]) + 8 * ev, events_alg=8 * ev,
+                   sync_write_alg=24 * sm["n_rec"], cand=sm["pairs_tested"])
+    for t in range(warmup, warmup + steps) if not hasattr(run, "replay") else ():
         upd, r, s = run.step(t)
         ev = r.n_enter + r.n_leave
         tot["ops"] += upd

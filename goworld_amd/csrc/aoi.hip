@@ -1775,11 +1775,14 @@ __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
 // quantiles of this tick's sorted (leave, watcher) keys: the next tick's
 // bucket bounds (BK_NSPLIT of them; a tick with fewer buckets takes every
 // (BK_NSPLIT / NB)-th).  Kept when the tick overflowed or had no events.
-__device__ __forceinline__ void bk_split_next(const TickBufs& b, const ResetArgs& r) {
-    const uint64_t E = lo32(r.ev_pk) + hi32(r.ev_pk), ne = lo32(r.ev_pk);
-    if (E == 0 || E > b.ev_cap || r.overflow) return;
+__device__ __forceinline__ void bk_split_next(const TickBufs& b, unsigned long long ev_pk, unsigned long long overflow) {
+    const uint64_t E = lo32(ev_pk) + hi32(ev_pk), ne = lo32(ev_pk);
+    if (E == 0 || E > b.ev_cap || overflow) return;
     const uint32_t lvb = 1u << b.wbits;
-    for (uint32_t j = 1 + blockIdx.x * NT + threadIdx.x; j < BK_NSPLIT; j += gridDim.x * NT) {   // 1 per thread
+#pragma unroll
+    for (uint32_t q = 0; q < BK_NSPLIT / RESET_NT; ++q) {   // the loads of every split in flight together
+        const uint32_t j = q * RESET_NT + threadIdx.x;
+        if (j == 0) continue;
         const uint64_t p = (uint64_t)j * E / BK_NSPLIT;
         b.bk_split[j] = (p >= ne ? lvb : 0u) | b.ev[p].watcher;
     }
@@ -1860,19 +1863,44 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// after the tick: the next tick's bucket bounds, and block 0 zeroes the device
-// statistics (the tick's counters come by value, read by the host already), so
-// no reset copy runs at its start.  Nothing per op or per mover: the dedupe
-// words age out with their session tag, the mover bits with the rebuild parity.
-__global__ void __launch_bounds__(NT) k_tick_reset(TickBufs b, ResetArgs r) {
-    bk_split_next(b, r);                     // (its own launch cost 5-8 us)
-    if (blockIdx.x == 0) {
-        unsigned long long* z = (unsigned long long*)b.st;
-        for (uint32_t k = threadIdx.x; k < sizeof(DevStats) / 8; k += NT) z[k] = 0;
+// after the tick: the next tick's bucket bounds, and the device statistics
+// zeroed, so no reset copy runs at the next tick's start.  Nothing per op or
+// per mover: the dedupe words age out with their session tag, the mover bits
+// with the rebuild parity.  One block: the tick's event totals and overflow
+// flag are read from the device statistics before the block zeroes them, so
+// the pass needs nothing from the host and a collect queues it behind its
+// statistics copy, before its host sync (off the path between the collect and
+// the next tick)
+__global__ void __launch_bounds__(RESET_NT) k_tick_reset(TickBufs b, const unsigned long long* __restrict__ pub_src,
+                                                        unsigned long long* pub_dst, uint32_t pub_words) {
+    __shared__ unsigned long long s_ev, s_ov;
+    // the statistics the host reads after its sync, written straight into its
+    // (coherent, pinned) buffer: no blit copy between the collect and the reset
+    for (uint32_t k = threadIdx.x; k < pub_words; k += RESET_NT) pub_dst[k] = pub_src[k];
+    __syncthreads();
+    if (!b.st) {
+        __threadfence_system();
+        return;
     }
+    if (threadIdx.x == 0) {
+        s_ev = b.st->ev_pk;
+        s_ov = b.st->overflow;
+    }
+    __syncthreads();
+    bk_split_next(b, s_ev, s_ov);
+    unsigned long long* z = (unsigned long long*)b.st;
+    for (uint32_t k = threadIdx.x; k < sizeof(DevStats) / 8; k += RESET_NT) z[k] = 0;
+    __threadfence_system();
 }
-void tick_reset(const TickBufs& b, const ResetArgs& r, hipStream_t s) {
-    hipLaunchKernelGGL(k_tick_reset, dim3(nblk1(BK_NSPLIT, NT)), dim3(NT), 0, s, b, r);
+
+void tick_reset(const TickBufs& b, hipStream_t s) {
+    hipLaunchKernelGGL(k_tick_reset, dim3(1), dim3(RESET_NT), 0, s, b, nullptr, nullptr, 0u);
+}
+void publish_stats(const TickBufs* b, const void* src, void* host_dst, size_t bytes, hipStream_t s) {
+    TickBufs t{};
+    if (b) t = *b;                                   // with the tick's reset, else the copy alone (t.st null)
+    hipLaunchKernelGGL(k_tick_reset, dim3(1), dim3(RESET_NT), 0, s, t, (const unsigned long long*)src,
+                       (unsigned long long*)host_dst, (uint32_t)(bytes / 8));
 }
 
 }  // namespace gw

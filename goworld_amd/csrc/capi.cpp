@@ -337,8 +337,12 @@ int read_stats(gw_ctx* c) {
 // copy of both: the tick's are final once the collect's launches are queued)
 int read_cstats(gw_ctx* c) {
     const bool both = c->pt.on && !c->pt.copied;
-    HIPCHK(hipMemcpyAsync(both ? c->hstats : c->hcstats, both ? c->stats : c->cstats,
-                          (both ? 2 : 1) * sizeof(DevStats), hipMemcpyDeviceToHost, c->st));
+    // one kernel writes the statistics into the pinned host buffers (coherent,
+    // device-visible) and, for a deferred tick, runs its reset (which reads the
+    // device statistics itself): no blit copy and no launch after the sync
+    publish_stats(both ? &c->pt.b : nullptr, both ? (const void*)c->stats : (const void*)c->cstats,
+                  both ? c->hstats_dev : c->hstats_dev + 1, (both ? 2 : 1) * sizeof(DevStats), c->st);
+    if (both) c->pt.reset_queued = true;
     HIPCHK(hipStreamSynchronize(c->st));
     if (both) c->pt.copied = true;
     return 0;
@@ -490,7 +494,9 @@ int gw_init(int device_id, gw_ctx** out) {
         // the tick's and the collect's statistics side by side, so a collect
         // that settles a deferred tick reads both with one copy
         if (hipMalloc(&c->stats, 2 * sizeof(DevStats)) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "stats"); break; }
-        if (hipHostMalloc((void**)&c->hstats, 2 * sizeof(DevStats), hipHostMallocDefault) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "hstats"); break; }
+        // coherent: the publishing kernel writes them over PCIe (read_cstats)
+        if (hipHostMalloc((void**)&c->hstats, 2 * sizeof(DevStats), hipHostMallocCoherent) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "hstats"); break; }
+        if (hipHostGetDevicePointer((void**)&c->hstats_dev, c->hstats, 0) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "hstats map"); break; }
         c->cstats = c->stats + 1;
         c->hcstats = c->hstats + 1;
         if (hipMalloc(&c->scal32, 64) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "scal"); break; }
@@ -1011,7 +1017,9 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     // bitmap was cleared by the list pass).  A region overflow hides the events
     // of the movers it stopped, so the event count is only exact on the next
     // attempt: up to three.
+    bool redone = false;
     for (int attempt = 0; c->hstats->overflow; ++attempt) {
+        redone = true;
         if (attempt == 3) return set_err(c, GW_ENOMEM, "event buffers overflowed three times");
         const uint64_t E = (c->hstats->ev_pk & 0xffffffffull) + (c->hstats->ev_pk >> 32);
         if (c->hstats->cand_total > c->own_cap) c->own_cap = c->hstats->cand_total + c->hstats->cand_total / 4 + 4096;
@@ -1040,13 +1048,13 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         HIPCHK(hipGetLastError());
         if ((rc = read_stats(c))) return rc;
     }
-    prof_begin(c, "reset");
-    {                                                // asynchronous: the next call orders behind it
-        const DevStats& h = *c->hstats;
-        tick_reset(b, ResetArgs{h.n_gm, h.ev_pk, h.overflow}, c->st);
-        c->stats_zero = true;                        // the reset zeroed the device statistics
+    if (!p.reset_queued || redone) {                 // (a collect queued it behind its statistics copy)
+        prof_begin(c, "reset");
+        tick_reset(b, c->st);                        // asynchronous: the next call orders behind it
+        prof_end(c, (uint64_t)M * 24);
     }
-    prof_end(c, (uint64_t)M * 24);
+    p.reset_queued = false;
+    c->stats_zero = true;                            // the reset zeroed the device statistics
     HIPCHK(hipEventRecord(c->ev_t1, c->st));
     HIPCHK(hipGetLastError());
     DevStats& hs = *c->hstats;
@@ -1753,6 +1761,38 @@ int gw_memcpy_d2h(gw_ctx* c, void* dst, const void* src, size_t bytes) {
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
 }
+int gw_step(gw_ctx* c, const gw_op* ops, uint32_t n, int ops_on_device, uint32_t tick_flags, uint32_t sync_flags,
+            gw_tick_out* tick_out, gw_sync_out* sync_out) {
+    if (!c || !tick_out || !sync_out) return GW_EINVAL;
+    int rc;
+    if (n && (rc = ops_on_device ? gw_submit_device(c, ops, n) : gw_submit(c, ops, n))) return rc;
+    const uint32_t tf = tick_flags | ((ops_on_device && !(tick_flags & GW_TICK_COPY_TO_HOST)) ? GW_TICK_DEFER : 0u);
+    if ((rc = gw_tick(c, tf, tick_out))) return rc;
+    if ((rc = gw_sync_collect(c, sync_flags, sync_out))) return rc;
+    return (tf & GW_TICK_DEFER) ? gw_tick_result(c, tick_out) : 0;
+}
+
+int gw_replay(gw_ctx* c, const gw_op* dev_ops, uint32_t n, uint64_t stride_ops, uint32_t ticks, uint32_t sync_flags,
+              gw_replay_sum* sum) {
+    if (!c || !sum || (n && !dev_ops)) return GW_EINVAL;
+    memset(sum, 0, sizeof *sum);
+    for (uint32_t t = 0; t < ticks; ++t) {
+        gw_tick_out to;
+        gw_sync_out so;
+        if (int rc = gw_step(c, dev_ops + (size_t)t * stride_ops, n, 1, 0, sync_flags, &to, &so)) return rc;
+        sum->ops += to.ops;
+        sum->movers += to.movers;
+        sum->n_enter += to.n_enter;
+        sum->n_leave += to.n_leave;
+        sum->n_rec += so.n_rec;
+        sum->pairs_tested += to.pairs_tested;
+        sum->nbr_old += to.nbr_old;
+        sum->nbr_new += to.nbr_new;
+        sum->bytes_alg += to.bytes_alg + so.bytes_alg;
+    }
+    return 0;
+}
+
 int gw_tick_result(gw_ctx* c, gw_tick_out* out) {
     if (!c || !out) return GW_EINVAL;
     (void)hipSetDevice(c->dev);

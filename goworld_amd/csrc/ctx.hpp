@@ -155,14 +155,15 @@ struct gw_ctx {
 
     DevStats* stats = nullptr;     // device (grid rebuild, tick)
     bool stats_zero = true;        // stats is all zero (the last tick's reset pass, or init)
-    DevStats* hstats = nullptr;    // pinned host
+    DevStats* hstats = nullptr;    // pinned host (coherent): the tick's statistics, then the collect's (hcstats)
+    DevStats* hstats_dev = nullptr;  // the same buffer as the device sees it
     DevStats* cstats = nullptr;    // device (collect: a deferred tick's stats stay intact)
     DevStats* hcstats = nullptr;   // pinned host
 
     // a tick launched but not read back yet (GW_TICK_DEFER): settled by the
     // next call that needs its results (the collect's one sync covers it)
     struct Pending {
-        bool on = false, copied = false;
+        bool on = false, copied = false, reset_queued = false;
         uint32_t M = 0, C = 0, NC = 0, flags = 0;
         size_t s_grid = 0, s_movers = 0, s_diff = 0, s_events = 0;
         TickBufs b{};

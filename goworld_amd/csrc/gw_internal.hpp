@@ -285,10 +285,12 @@ void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s);   // b.w: the n
 void tick_diff(const TickBufs& b, hipStream_t s);                  // own + mirror events per mover
 void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s);   // canonical event arrays
 // after the host read the counts (given by value); zeroes the tick's DevStats
-struct ResetArgs {
-    unsigned long long n_gm, ev_pk, overflow;
-};
-void tick_reset(const TickBufs& b, const ResetArgs& r, hipStream_t s);
+// the per-tick reset (next tick's bucket bounds, zeroed statistics): one block
+constexpr int RESET_NT = 1024;
+void tick_reset(const TickBufs& b, hipStream_t s);
+// bytes (multiple of 8) from device src to a device-visible pinned host buffer
+// by one kernel, then the reset of tick *b unless b is null
+void publish_stats(const TickBufs* b, const void* src, void* host_dst, size_t bytes, hipStream_t s);
 
 void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n, bool grid_ok,
                         hipStream_t s);

@@ -40,6 +40,11 @@ MAX_STAGES = 32
 _u64, _u32, _f64 = C.c_uint64, C.c_uint32, C.c_double
 
 
+class ReplaySum(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("ops", "movers", "n_enter", "n_leave", "n_rec", "pairs_tested",
+                                          "nbr_old", "nbr_new", "bytes_alg")]
+
+
 class TickOut(C.Structure):
     _fields_ = [("enter", C.c_void_p), ("leave", C.c_void_p), ("enter_dev", C.c_void_p),
                 ("leave_dev", C.c_void_p), ("n_enter", _u64), ("n_leave", _u64), ("ops", _u64),
@@ -129,6 +134,8 @@ def lib():
         L.gw_tick_result.argtypes = [vp, C.POINTER(TickOut)]
         L.gw_space_restore.argtypes = [vp, _u32, vp, vp, vp, vp, vp, _u32, C.c_uint8]
         L.gw_sync_collect.argtypes = [vp, _u32, C.POINTER(SyncOut)]
+        L.gw_step.argtypes = [vp, vp, _u32, C.c_int, _u32, _u32, C.POINTER(TickOut), C.POINTER(SyncOut)]
+        L.gw_replay.argtypes = [vp, vp, _u32, C.c_uint64, _u32, _u32, C.POINTER(ReplaySum)]
         L.gw_neighbors.argtypes = [vp, _u32, vp, _u32, C.POINTER(_u32)]
         L.gw_set_profiling.argtypes = [vp, C.c_int]
         L.gw_get_stage_times.argtypes = [vp, C.POINTER(StageTimes)]
@@ -172,7 +179,7 @@ def lib():
 
 EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_space_create",
             "gw_space_destroy", "gw_submit", "gw_submit_device", "gw_set_clients", "gw_tick",
-            "gw_sync_collect", "gw_neighbors", "gw_set_profiling", "gw_get_stage_times",
+            "gw_sync_collect", "gw_step", "gw_replay", "gw_neighbors", "gw_set_profiling", "gw_get_stage_times",
             "gw_total_neighbors", "gw_device_alloc", "gw_device_free", "gw_memcpy_h2d",
             "gw_memcpy_d2h", "gw_synchronize", "gw_submit_device_stamped", "gw_space_set_ownership",
             "gw_set_stream", "gw_route_halo", "gw_submit_device_rows", "gw_halo_status", "gw_tick_result", "gw_space_restore",
@@ -361,6 +368,26 @@ class GpuAOI:
                               o.n_enter, o.n_leave, o.ops, o.movers, o.pairs_tested, o.nbr_old, o.nbr_new,
                               o.bytes_alg, o.device_us, o.enter_dev or 0, o.leave_dev or 0)
         return self._tick_result(o, copy, no_events)
+
+    def step_device(self, dev_ptr: int, n: int, by_client: bool = False):
+        """gw_step with device-resident ops: submit + deferred tick + collect in
+        one call, outputs left on the device.  Returns the library's TickOut and
+        SyncOut structures (reused between calls: read them before the next
+        step) -- the bench's hot loop, with no per-step Python objects."""
+        if not hasattr(self, "_step_outs"):
+            self._step_outs = (TickOut(), SyncOut())
+        to, so = self._step_outs
+        self._chk(lib().gw_step(self._h, C.c_void_p(dev_ptr), n, 1, 0, SYNC_BY_CLIENT if by_client else 0,
+                                C.byref(to), C.byref(so)))
+        return to, so
+
+    def replay_device(self, dev_ptr: int, n: int, stride_ops: int, ticks: int, by_client: bool = False) -> dict:
+        """gw_replay: `ticks` gw_step calls over a device-resident op log (tick t
+        at dev_ptr + t * stride_ops ops); returns the summed counters."""
+        r = ReplaySum()
+        self._chk(lib().gw_replay(self._h, C.c_void_p(dev_ptr), n, stride_ops, ticks,
+                                  SYNC_BY_CLIENT if by_client else 0, C.byref(r)))
+        return {f: getattr(r, f) for f, _ in ReplaySum._fields_}
 
     def tick_result(self) -> TickResult:
         """Outputs of the last tick (settles a deferred tick)."""

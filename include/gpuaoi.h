@@ -303,6 +303,29 @@ int  gw_tick_result(gw_ctx* ctx, gw_tick_out* out);
 /* CollectEntitySyncInfos for all spaces of the context; clears the flags. */
 int  gw_sync_collect(gw_ctx* ctx, uint32_t flags, gw_sync_out* out);
 
+/* One game tick in one call: the position/yaw updates that reach the spaces
+ * during a GameService tick (Entity.SetPosition -> Space.move,
+ * GameService.go:183-187 / Entity.go:1185-1187) are submitted, flushed
+ * (gw_tick) and followed by the tick's CollectEntitySyncInfos (Entity.go:
+ * 1221-1267).  ops_on_device != 0: ops is device memory (gw_submit_device);
+ * the tick is then deferred and settled by the collect's single host sync
+ * (tick_flags may add GW_TICK_COPY_TO_HOST, which forgoes the deferral).  The
+ * same as gw_submit + gw_tick + gw_sync_collect + gw_tick_result, with the
+ * device never waiting on the host between the tick and the collect. */
+int  gw_step(gw_ctx* ctx, const gw_op* ops, uint32_t n, int ops_on_device, uint32_t tick_flags,
+             uint32_t sync_flags, gw_tick_out* tick_out, gw_sync_out* sync_out);
+
+/* gw_step over `ticks` consecutive ticks of a device-resident op log (tick t:
+ * n ops at dev_ops + t * stride_ops), outputs left on the device: GameService's
+ * tick loop (GameService.go:77-190) replayed from a recorded log, e.g. to catch
+ * a server up or to measure the path without a per-tick host-language round
+ * trip.  Counters of all ticks are summed into *sum (zeroed first). */
+typedef struct gw_replay_sum {
+    uint64_t ops, movers, n_enter, n_leave, n_rec, pairs_tested, nbr_old, nbr_new, bytes_alg;
+} gw_replay_sum;
+int  gw_replay(gw_ctx* ctx, const gw_op* dev_ops, uint32_t n, uint64_t stride_ops, uint32_t ticks,
+               uint32_t sync_flags, gw_replay_sum* sum);
+
 /* InterestedIn(slot) == InterestedBy(slot), ascending slots. *n receives the
  * full count even when it exceeds cap. */
 int  gw_neighbors(gw_ctx* ctx, uint32_t slot, uint32_t* buf, uint32_t cap, uint32_t* n);

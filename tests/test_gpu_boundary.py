@@ -206,3 +206,78 @@ def test_entity_id_moves_and_batch_checks():
     finally:
         g.close()
         o.close()
+
+
+def test_step_equals_separate_calls():
+    """gw_step (submit + deferred tick + collect in one call, device-resident
+    ops, outputs left on the device) produces byte-identical events and records
+    to gw_submit_device + gw_tick(DEFER) + gw_sync_collect + gw_tick_result."""
+    tr = T.config1(ticks=6, seed=7, n=600)
+    outs = []
+    for one_call in (False, True):
+        g = gpuaoi.GpuAOI(0)
+        gpuaoi.load_space(g, tr)
+        g.sync_collect()
+        dev = g.dev_alloc(max(len(o) for o in tr.ticks) * T.OP_DTYPE.itemsize)
+        got = []
+        for ops in tr.ticks:
+            g.h2d(dev, np.ascontiguousarray(ops))
+            if one_call:
+                r, s = g.step_device(dev, len(ops))
+                n_enter, n_leave, n_rec = r.n_enter, r.n_leave, s.n_rec
+                enter_dev, leave_dev, rec_dev = r.enter_dev, r.leave_dev, s.rec_dev
+            else:
+                g.submit_device(dev, len(ops))
+                g.tick(copy=False, defer=True)
+                s = g.sync_collect(copy=False)
+                r = g.tick_result()
+                n_enter, n_leave, n_rec = r.n_enter, r.n_leave, s.n_rec
+                enter_dev, leave_dev, rec_dev = r.enter_dev, r.leave_dev, s.rec_dev
+            e = np.zeros(n_enter, gpuaoi.EVENT_DTYPE)
+            l = np.zeros(n_leave, gpuaoi.EVENT_DTYPE)
+            rec = np.zeros(n_rec, gpuaoi.REC_DTYPE)
+            for arr, p in ((e, enter_dev), (l, leave_dev), (rec, rec_dev)):
+                if len(arr):
+                    g.d2h(arr, p)
+            got.append((e.tobytes(), l.tobytes(), rec.tobytes()))
+        g.dev_free(dev)
+        g.close()
+        outs.append(got)
+    assert sum(len(t[0]) + len(t[1]) for t in outs[0]) > 0
+    assert outs[0] == outs[1]
+
+
+def test_replay_equals_steps():
+    """gw_replay over a device-resident op log equals one gw_step per tick: the
+    same summed counters and the same last tick's events and records."""
+    tr = T.config1(ticks=5, seed=11, n=500)
+    m = max(len(o) for o in tr.ticks)
+    log = np.zeros(m * len(tr.ticks), T.OP_DTYPE)          # NOP padding up to m ops per tick
+    for t, ops in enumerate(tr.ticks):
+        log[t * m:t * m + len(ops)] = ops
+    res = []
+    for use_replay in (False, True):
+        g = gpuaoi.GpuAOI(0)
+        gpuaoi.load_space(g, tr)
+        g.sync_collect()
+        dev = g.dev_alloc(log.nbytes)
+        g.h2d(dev, log)
+        if use_replay:
+            sm = g.replay_device(dev, m, m, len(tr.ticks))
+        else:
+            sm = dict.fromkeys(("ops", "movers", "n_enter", "n_leave", "n_rec"), 0)
+            for t in range(len(tr.ticks)):
+                r, s = g.step_device(dev + t * m * T.OP_DTYPE.itemsize, m)
+                for k in ("ops", "movers", "n_enter", "n_leave"):
+                    sm[k] += getattr(r, k)
+                sm["n_rec"] += s.n_rec
+        r = g.tick_result()
+        e = np.zeros(r.n_enter, gpuaoi.EVENT_DTYPE)
+        if len(e):
+            g.d2h(e, r.enter_dev)
+        res.append(({k: sm[k] for k in ("ops", "movers", "n_enter", "n_leave", "n_rec")}, e.tobytes(),
+                    g.total_neighbors()))
+        g.dev_free(dev)
+        g.close()
+    assert res[0][0]["n_enter"] > 0
+    assert res[0] == res[1]

@@ -1896,6 +1896,20 @@ __global__ void __launch_bounds__(RESET_NT) k_tick_reset(TickBufs b, const unsig
 void tick_reset(const TickBufs& b, hipStream_t s) {
     hipLaunchKernelGGL(k_tick_reset, dim3(1), dim3(RESET_NT), 0, s, b, nullptr, nullptr, 0u);
 }
+struct PubTab {
+    PubSeg s[4];
+    int n;
+};
+__global__ void __launch_bounds__(RESET_NT) k_publish_words(PubTab t) {
+    for (int q = 0; q < t.n; ++q)
+        for (uint32_t k = threadIdx.x; k < t.s[q].words; k += RESET_NT) t.s[q].dst[k] = t.s[q].src[k];
+    __threadfence_system();
+}
+void publish_words(const PubSeg* segs, int n, hipStream_t s) {
+    PubTab t{};
+    for (int q = 0; q < n && q < 4; ++q) t.s[t.n++] = segs[q];
+    hipLaunchKernelGGL(k_publish_words, dim3(1), dim3(RESET_NT), 0, s, t);
+}
 void publish_stats(const TickBufs* b, const void* src, void* host_dst, size_t bytes, hipStream_t s) {
     TickBufs t{};
     if (b) t = *b;                                   // with the tick's reset, else the copy alone (t.st null)

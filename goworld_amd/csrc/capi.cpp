@@ -549,6 +549,7 @@ void gw_shutdown(gw_ctx* c) {
                     &c->wd.far_mat, &c->wd.dstage};
     if (c->wire_h.p) (void)hipHostFree(c->wire_h.p);
     if (c->wd.hstage.p) (void)hipHostFree(c->wd.hstage.p);
+    if (c->wd.pub_h) (void)hipHostFree(c->wd.pub_h);
     if (c->wd.staged) (void)hipEventDestroy(c->wd.staged);
     if (c->eid_dev) (void)hipFree(c->eid_dev);
     if (c->cid_dev) (void)hipFree(c->cid_dev);

@@ -73,6 +73,10 @@ struct WorldHost {
     // the event after the upload (the pinned buffer is reused once it fired)
     DevBuf hstage, dstage;
     hipEvent_t staged = nullptr;
+    // the routing's counts after each route, written by one kernel into pinned
+    // coherent host memory: [HaloStats | received counts (2) | far_cnt (R) | far_mat (R*R)]
+    uint32_t* pub_h = nullptr;
+    uint32_t* pub_d = nullptr;      // the same buffer as the device sees it
 };
 
 // a 16-byte EntityID as a hash-map key

@@ -291,6 +291,14 @@ void tick_reset(const TickBufs& b, hipStream_t s);
 // bytes (multiple of 8) from device src to a device-visible pinned host buffer
 // by one kernel, then the reset of tick *b unless b is null
 void publish_stats(const TickBufs* b, const void* src, void* host_dst, size_t bytes, hipStream_t s);
+// up to 4 device ranges of u32 words into device-visible pinned host memory by
+// one kernel (instead of a blit copy each): the world's routing counts
+struct PubSeg {
+    const uint32_t* src;
+    uint32_t* dst;
+    uint32_t words;
+};
+void publish_words(const PubSeg* segs, int n, hipStream_t s);
 
 void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n, bool grid_ok,
                         hipStream_t s);

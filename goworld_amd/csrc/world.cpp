@@ -81,6 +81,30 @@ int route_launch(gw_ctx* c, const gw_op* ops, uint32_t n, const HaloDsts& D, uin
     return 0;
 }
 
+// words of the routing's counts in WorldHost::pub_h: HaloStats first
+constexpr size_t pub_off_cnt() { return (sizeof(HaloStats) + 3) / 4; }
+
+// the routing's counts (HaloStats, and with rcnt the received counts and the
+// far matrix) into pub_h by one kernel, the host sync, then into hs / the vectors
+int read_route_counts(gw_ctx* c, HaloStats& hs, uint32_t* rcnt, bool far_mat) {
+    WorldHost& W = c->wd;
+    const uint32_t R = W.g.ranks;
+    const size_t o_cnt = pub_off_cnt(), o_far = o_cnt + 2, o_mat = o_far + R;
+    PubSeg segs[4];
+    int n = 0;
+    segs[n++] = PubSeg{(const uint32_t*)c->halo, W.pub_d, (uint32_t)o_cnt};
+    segs[n++] = PubSeg{P<uint32_t>(W.far_cnt), W.pub_d + o_far, R};
+    if (rcnt) segs[n++] = PubSeg{P<uint32_t>(W.cnt), W.pub_d + o_cnt, 2};
+    if (far_mat) segs[n++] = PubSeg{P<uint32_t>(W.far_mat), W.pub_d + o_mat, R * R};
+    publish_words(segs, n, c->st);
+    HIPCHK(hipStreamSynchronize(c->st));
+    memcpy(&hs, W.pub_h, sizeof hs);
+    memcpy(W.far_cnt_h.data(), W.pub_h + o_far, (size_t)R * 4);
+    if (rcnt) memcpy(rcnt, W.pub_h + o_cnt, 8);
+    if (far_mat) memcpy(W.far_mat_h.data(), W.pub_h + o_mat, (size_t)R * R * 4);
+    return 0;
+}
+
 // after the routing's host sync (hs, cnt read back): a far buffer too small
 // is grown and the routing rerun (idempotent: same session, same stamps,
 // same counts); then the far triples are grouped by destination
@@ -217,6 +241,10 @@ int gw_world_create(gw_ctx* c, const gw_world_geom* g, uint32_t capacity, const 
         return rc2;
     HIPCHK(hipMemcpyAsync(W.ext.p, W.ext_h.data(), W.ext_h.size() * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    const size_t pub_words = pub_off_cnt() + 2 + g->ranks + (size_t)g->ranks * g->ranks;
+    if (hipHostMalloc((void**)&W.pub_h, pub_words * 4, hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&W.pub_d, W.pub_h, 0) != hipSuccess)
+        return set_err(c, GW_ENOMEM, "world count buffer");
     W.far_cnt_h.assign(g->ranks, 0);
     W.far_off_h.assign(g->ranks, 0);
     W.far_mat_h.assign((size_t)g->ranks * g->ranks, 0);
@@ -253,9 +281,7 @@ int gw_world_route(gw_ctx* c, const gw_op* ops, uint32_t n, const gw_halo_row* s
     W.kept = n;
     W.kept_tag = tag;
     HaloStats hs{};
-    HIPCHK(hipMemcpyAsync(&hs, c->halo, sizeof hs, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipMemcpyAsync(W.far_cnt_h.data(), W.far_cnt.p, (size_t)W.g.ranks * 4, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    if ((rc = read_route_counts(c, hs, nullptr, false))) return rc;
     if ((rc = far_settle(c, ops, n, D, tag, base, hs))) return rc;
     uint32_t k = 0;
     for (int side = 0; side < 2; ++side) {
@@ -359,12 +385,7 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
             NCCLCHK(ncclAllGather(W.far_cnt.p, W.far_mat.p, R, ncclUint32, c->comm, c->st));
         uint32_t h[4] = {0, 0, 0, 0};
         HaloStats hs{};
-        HIPCHK(hipMemcpyAsync(h, dcnt, 8, hipMemcpyDeviceToHost, c->st));
-        HIPCHK(hipMemcpyAsync(&hs, c->halo, sizeof hs, hipMemcpyDeviceToHost, c->st));
-        HIPCHK(hipMemcpyAsync(W.far_cnt_h.data(), W.far_cnt.p, (size_t)R * 4, hipMemcpyDeviceToHost, c->st));
-        if (far_round)
-            HIPCHK(hipMemcpyAsync(W.far_mat_h.data(), W.far_mat.p, (size_t)R * R * 4, hipMemcpyDeviceToHost, c->st));
-        HIPCHK(hipStreamSynchronize(c->st));
+        if ((rc = read_route_counts(c, hs, h, far_round))) return rc;
         if ((rc = far_settle(c, ops, n, D, tag, base, hs))) return rc;
         k = 0;
         for (int side = 0; side < 2; ++side) {

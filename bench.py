@@ -525,6 +525,7 @@ class WorldRun:
             self.m_ticks.append(len(own))
             self.slots.append(own["slot"])
         self.m = int(np.mean(self.m_ticks))
+        self.one_call = comm == "rccl" or ws == 1        # the exchange runs inside the library
         torch.cuda.synchronize()
         self.parallelism = (f"decomposed world, {ws} X-strips of {side / ws:g} x {side:g}, halo rows over "
                             f"{'RCCL (gw_world_step)' if comm == 'rccl' else 'gloo'}" if ws > 1
@@ -532,6 +533,10 @@ class WorldRun:
         self.tr = None
 
     def step(self, t):
+        if self.one_call:                    # gw_step: gw_world_step + tick + collect in one call
+            w = self.words[t]
+            r, s = self.g.step_device(w.data_ptr(), w.shape[0])
+            return self.m_ticks[t], r, s
         self.sr.step(self.words[t], copy=False, defer=True)
         s = self.sr.collect(copy=False)
         return self.m_ticks[t], self.sr.e.tick_result(), s

@@ -1766,7 +1766,11 @@ int gw_step(gw_ctx* c, const gw_op* ops, uint32_t n, int ops_on_device, uint32_t
             gw_tick_out* tick_out, gw_sync_out* sync_out) {
     if (!c || !tick_out || !sync_out) return GW_EINVAL;
     int rc;
-    if (n && (rc = ops_on_device ? gw_submit_device(c, ops, n) : gw_submit(c, ops, n))) return rc;
+    if (c->wd.on)                                    // a world strip: route + exchange + queue (even with no ops)
+        rc = ops_on_device ? gw_world_step(c, ops, n) : gw_world_step_host(c, ops, n);
+    else
+        rc = n ? (ops_on_device ? gw_submit_device(c, ops, n) : gw_submit(c, ops, n)) : 0;
+    if (rc) return rc;
     const uint32_t tf = tick_flags | ((ops_on_device && !(tick_flags & GW_TICK_COPY_TO_HOST)) ? GW_TICK_DEFER : 0u);
     if ((rc = gw_tick(c, tf, tick_out))) return rc;
     if ((rc = gw_sync_collect(c, sync_flags, sync_out))) return rc;

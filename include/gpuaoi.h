@@ -311,7 +311,10 @@ int  gw_sync_collect(gw_ctx* ctx, uint32_t flags, gw_sync_out* out);
  * the tick is then deferred and settled by the collect's single host sync
  * (tick_flags may add GW_TICK_COPY_TO_HOST, which forgoes the deferral).  The
  * same as gw_submit + gw_tick + gw_sync_collect + gw_tick_result, with the
- * device never waiting on the host between the tick and the collect. */
+ * device never waiting on the host between the tick and the collect.  On a
+ * world strip (gw_world_create) the ops are this rank's owned ops and go
+ * through gw_world_step / gw_world_step_host (routing + RCCL exchange) instead
+ * of gw_submit, every tick, with or without ops. */
 int  gw_step(gw_ctx* ctx, const gw_op* ops, uint32_t n, int ops_on_device, uint32_t tick_flags,
              uint32_t sync_flags, gw_tick_out* tick_out, gw_sync_out* sync_out);
 

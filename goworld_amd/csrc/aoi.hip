@@ -139,18 +139,18 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
                     if (ol.clr[c] >= 0) clear |= 1u << c;
                 if (clear) atomicAnd(&b.w.flags[flag_word(s)], ~(clear << flag_sh(s)));
             }
-            if (ol.pos == (int32_t)i) b.w.pos[s] = make_float4(op.x, op.y, op.z, op.yaw);
+            if (ol.pos == (int32_t)i) b.w.rec[s].p = make_float4(op.x, op.y, op.z, op.yaw);
             if (ol.aoi == (int32_t)i) {                 // the slot's mover entry (never a SYNC op)
-                a = b.w.aoi[s];
+                a = b.w.rec[s].a;
                 const bool was = (a.meta & PRESENT_BIT) != 0;
                 p.ox = was ? a.x : qnan();
                 p.oz = was ? a.z : qnan();
-                p.ostamp = b.w.stamp[s];
-                b.w.prev[s] = p;
-                b.w.stamp[s] = b.stamps ? b.stamps[i] : b.stamp_base + i;
+                p.ostamp = b.w.rec[s].stamp;
+                b.w.rec[s].pv = p;
+                b.w.rec[s].stamp = b.stamps ? b.stamps[i] : b.stamp_base + i;
                 if (op.kind == GW_OP_LEAVE) a.meta &= ~PRESENT_BIT;
                 else { a.x = op.x; a.z = op.z; a.meta |= PRESENT_BIT; }
-                b.w.aoi[s] = a;
+                b.w.rec[s].a = a;
                 mv = true;
                 // decomposed world: a long mover (a halo row says so, or an
                 // owned op moved it further than max_step)
@@ -178,13 +178,13 @@ __global__ void __launch_bounds__(NT) k_restore(World w, const uint32_t* __restr
     if (i >= n) return;
     const uint32_t s = slots[i];
     const float4 p = xyzw[i];
-    AoiEnt a = w.aoi[s];
+    AoiEnt a = w.rec[s].a;
     a.x = p.x;
     a.z = p.z;
     a.meta |= PRESENT_BIT;
-    w.aoi[s] = a;
-    w.pos[s] = p;
-    w.stamp[s] = stamp_base + i;
+    w.rec[s].a = a;
+    w.rec[s].p = p;
+    w.rec[s].stamp = stamp_base + i;
     if (flags & 3u) atomicOr(&w.flags[flag_word(s)], (flags & 3u) << flag_sh(s));
 }
 void launch_restore(const World& w, const uint32_t* slots, const float4* xyzw, uint32_t n,
@@ -206,7 +206,7 @@ void tick_ops(const TickBufs& b, hipStream_t s) {
 __global__ void __launch_bounds__(NT) k_grid_keys(World w, uint32_t* k0, uint32_t* v0) {
     uint32_t s = blockIdx.x * NT + threadIdx.x;
     if (s >= w.cap) return;
-    const AoiEnt a = w.aoi[s];
+    const AoiEnt a = w.rec[s].a;
     uint32_t key = w.ncells;
     if (a.meta & PRESENT_BIT) key = cell_of(w.sp[a.meta & SPACE_MASK], a.x, a.z);
     k0[s] = key;
@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(NT) k_grid_fill(World w, const uint32_t* __res
     const uint32_t key = keys[i];
     if (key < w.ncells) {
         const uint32_t s = slots[i];
-        const AoiEnt a = w.aoi[s];
+        const AoiEnt a = w.rec[s].a;
         GEnt e;
         e.x = a.x; e.z = a.z; e.slot = s;
         e.meta = key | (w.gate[s] ? CLIENT_BIT : 0u);
@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(NT) k_grid_rel(World w) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i >= w.gn_start[w.ncells]) return;
     const GEnt e = w.gn[i];
-    w.gidx[e.slot] = i - w.gn_start[e.meta & CELL_MASK];
+    w.rec[e.slot].gidx = i - w.gn_start[e.meta & CELL_MASK];
 }
 // gn_start[c] = first index with key >= c (binary search over the sorted keys)
 __global__ void __launch_bounds__(NT) k_grid_starts(World w, const uint32_t* __restrict__ keys, DevStats* st) {
@@ -291,11 +291,11 @@ __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, u
         GEnt e;
         e.x = a.x; e.z = a.z; e.slot = A;
         e.meta = cn | (cl ? CLIENT_BIT : 0u) | b.mbit;
-        b.w.gn[b.w.gn_start[co] + b.w.gidx[A]] = e;
+        b.w.gn[b.w.gn_start[co] + b.w.rec[A].gidx] = e;
     } else {
         if (co != NO_CELL) {
             atomicAdd(&b.dep[co], 1u);
-            b.w.gn[b.w.gn_start[co] + b.w.gidx[A]].slot = DEPARTED;
+            b.w.gn[b.w.gn_start[co] + b.w.rec[A].gidx].slot = DEPARTED;
         }
         if (cn != NO_CELL) atomicAdd(&b.arr[cn], 1u);
     }
@@ -396,7 +396,7 @@ __global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) {
             }
             wave_sync();
             bitonic_inplace<64>(b.gn_nxt + sn, nn, ln, [](const GEnt& e) { return e.slot; }, [] { wave_sync(); });
-            for (uint32_t j = (uint32_t)ln; j < nn; j += 64) b.w.gidx[b.gn_nxt[sn + j].slot] = j;
+            for (uint32_t j = (uint32_t)ln; j < nn; j += 64) b.w.rec[b.gn_nxt[sn + j].slot].gidx = j;
             if (ln == 0) b.dep[c] = 0;
             continue;
         }
@@ -428,13 +428,13 @@ __global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) {
             if (keep) {
                 const uint32_t at = sn + k0 + (uint32_t)popc64(bm & lt) + below;
                 b.gn_nxt[at] = e;
-                b.w.gidx[e.slot] = at - sn;
+                b.w.rec[e.slot].gidx = at - sn;
             }
             k0 += (uint32_t)popc64(bm);
         }
         if (ln < (int)narr) {
             b.gn_nxt[sn + arank] = ar;
-            b.w.gidx[ar.slot] = arank;
+            b.w.rec[ar.slot].gidx = arank;
         }
         if (ln == 0) b.dep[c] = 0;
     }
@@ -600,7 +600,8 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     // a long mover's pairs are emitted by the owners of the other members
     // (they hold both ends of every pair that changes)
     const bool longA = (me.tags & TAG_LONG) != 0;
-    const unsigned long long sA = w.stamp[A], soA = w.prev[A].ostamp;
+    // A's stamps are read only at a boundary tie (rare): loaded up front, the
+    // in-order memory counter made every first chunk wait for them too
     const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
     uint32_t* out = b.own + reg;
     uint64_t* mir = b.mir + reg;
@@ -665,8 +666,9 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
                 b_o = iao != ibo;
                 b_n = ian != ibn;
                 if (b_o || b_n) {
-                    const unsigned long long sb = w.stamp[e.slot];
-                    const unsigned long long sbo = nmv ? sb : w.prev[e.slot].ostamp;
+                    const unsigned long long sA = w.rec[A].stamp, soA = w.rec[A].pv.ostamp;
+                    const unsigned long long sb = w.rec[e.slot].stamp;
+                    const unsigned long long sbo = nmv ? sb : w.rec[e.slot].pv.ostamp;
                     if (b_o) ro = resolve(iao, ibo, soA, sbo);
                     if (b_n) rn = resolve(ian, ibn, sA, sb);
                 }
@@ -788,17 +790,15 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     const int nr1 = R.n > 1 ? R.r[1].z1 - R.r[1].z0 + 1 : 0;
     if (wave_ballot(nr0 + nr1 > 16)) return false;         // wave-uniform
     const World& w = b.w;
-    // the HBM reads of this pair (region, stamps) are first needed at the
-    // first write / boundary tie: the row ranges and candidates (LDS) go first
+    // the HBM reads of this pair (region) are first needed at the first
+    // write: the row ranges and candidates (LDS) go first; stamps only at a
+    // boundary tie
     uint64_t reg = 0, cap = 0;
     const bool go = prim;
     const uint32_t A = me.slot;
-    unsigned long long sA = 0, soA = 0;
     if (prim) {
         reg = b.reg[m];
         cap = b.cand[m];
-        sA = w.stamp[A];
-        soA = w.prev[A].ostamp;
     }
     const uint64_t own_cap = b.own_cap;
     const float d = P.d;
@@ -899,8 +899,9 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
                 b_o = iao != ibo;
                 b_n = ian != ibn;
                 if (b_o || b_n) {
-                    const unsigned long long sb = w.stamp[e.slot];
-                    const unsigned long long sbo = nmv ? sb : w.prev[e.slot].ostamp;
+                    const unsigned long long sA = w.rec[A].stamp, soA = w.rec[A].pv.ostamp;
+                    const unsigned long long sb = w.rec[e.slot].stamp;
+                    const unsigned long long sbo = nmv ? sb : w.rec[e.slot].pv.ostamp;
                     if (b_o) ro = resolve(iao, ibo, soA, sbo);
                     if (b_n) rn = resolve(ian, ibn, sA, sb);
                 }

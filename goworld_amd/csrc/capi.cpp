@@ -212,10 +212,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     uint32_t nc = std::max<uint32_t>(new_total, c->slot_cap + c->slot_cap / 2);
     uint32_t oc = c->slot_cap;
     int rc;
-    if ((rc = grow_preserve(c, c->aoi, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->prev, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->stamp, oc, nc))) return rc;
-    if ((rc = grow_preserve(c, c->pos, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->rec, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->flags, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->gate, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->nbc, oc, nc))) return rc;
@@ -226,12 +223,8 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->ol, oc, nc))) return rc;     // new records: zero (session 0 is never used)
     if ((rc = grow_preserve(c, c->gnb[0], 0, nc))) return rc;    // rebuilt (grid_dirty)
     if ((rc = grow_preserve(c, c->gnb[1], 0, nc))) return rc;
-    if ((rc = grow_preserve(c, c->gidx, 0, nc))) return rc;
     size_t n = nc - oc;
-    HIPCHK(hipMemsetAsync(c->aoi + oc, 0, n * sizeof(AoiEnt), c->st));
-    HIPCHK(hipMemsetAsync(c->prev + oc, 0, n * sizeof(PrevEnt), c->st));
-    HIPCHK(hipMemsetAsync(c->stamp + oc, 0, n * 8, c->st));
-    HIPCHK(hipMemsetAsync(c->pos + oc, 0, n * sizeof(float4), c->st));
+    HIPCHK(hipMemsetAsync(c->rec + oc, 0, n * sizeof(SlotRec), c->st));
     HIPCHK(hipMemsetAsync(c->flags + oc, 0, n * 4, c->st));
     HIPCHK(hipMemsetAsync(c->gate + oc, 0, n * 2, c->st));
     HIPCHK(hipMemsetAsync(c->nbc + oc, 0, n * 8, c->st));
@@ -361,8 +354,8 @@ World world(gw_ctx* c) {
     w.cap = c->total_slots;
     w.ncells = c->total_cells;
     w.sp = c->sp_dev;
-    w.aoi = c->aoi; w.prev = c->prev; w.stamp = c->stamp; w.pos = c->pos; w.flags = c->flags; w.gate = c->gate;
-    w.gn = c->gnb[c->gcur]; w.gn_start = c->gsb[c->gcur]; w.gidx = c->gidx;
+    w.rec = c->rec; w.flags = c->flags; w.gate = c->gate;
+    w.gn = c->gnb[c->gcur]; w.gn_start = c->gsb[c->gcur];
     w.nbc = c->nbc;
     w.epoch = c->epoch;
     w.nb_u = c->nb_u;
@@ -558,8 +551,8 @@ void gw_shutdown(gw_ctx* c) {
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off, &c->m_create.h,
                     &c->m_destroy.h, &c->m_fanout.h};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
-    void* ps[] = {c->halo, c->sc.ticket, c->movbit, c->gmi, c->aoi, c->prev, c->stamp, c->pos, c->flags, c->gate, c->nbc, c->ol,
-                  c->gnb[0], c->gnb[1], c->gidx, c->sp_dev, c->stats, c->scal32, c->gsb[0],
+    void* ps[] = {c->halo, c->sc.ticket, c->movbit, c->gmi, c->rec, c->flags, c->gate, c->nbc, c->ol,
+                  c->gnb[0], c->gnb[1], c->sp_dev, c->stats, c->scal32, c->gsb[0],
                   c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->gm_start};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);   // hcstats lives behind it
@@ -686,7 +679,7 @@ int gw_space_restore(gw_ctx* c, uint32_t sid, const uint32_t* slots, const float
 // device-resident submits the host mirror is not exact)
 static int count_present(gw_ctx* c, uint32_t base, uint32_t n, uint64_t* out) {
     HIPCHK(hipMemsetAsync(c->scal32, 0, 8, c->st));
-    launch_count_present(c->aoi, base, n, (unsigned long long*)c->scal32, c->st);
+    launch_count_present(c->rec, base, n, (unsigned long long*)c->scal32, c->st);
     HIPCHK(hipGetLastError());
     unsigned long long v = 0;
     HIPCHK(hipMemcpyAsync(&v, c->scal32, 8, hipMemcpyDeviceToHost, c->st));
@@ -1625,7 +1618,7 @@ int gw_client_events(gw_ctx* c, uint32_t flags, gw_msg_out* create, gw_msg_out* 
                 return rc;
             launch_event_client_flags(evs[k], n, c->gate, P<uint32_t>(c->m_flag), c->st);
             scan_u32_u32(P<uint32_t>(c->m_flag), P<uint32_t>(c->m_at), n, nullptr, c->sc, c->scal32 + 2, c->st);
-            launch_event_client_write(evs[k], n, P<uint32_t>(c->m_flag), P<uint32_t>(c->m_at), c->pos,
+            launch_event_client_write(evs[k], n, P<uint32_t>(c->m_flag), P<uint32_t>(c->m_at), c->rec,
                                       P<uint32_t>(m.a), k == 0, c->st);
             HIPCHK(hipGetLastError());
             HIPCHK(hipMemcpyAsync(&R, c->scal32 + 2, 4, hipMemcpyDeviceToHost, c->st));

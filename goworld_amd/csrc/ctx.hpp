@@ -135,10 +135,7 @@ struct gw_ctx {
     bool cells_zero = false;             // dep / arr / gm_cnt hold zeros
 
     // persistent device state (slot-indexed)
-    AoiEnt* aoi = nullptr;
-    PrevEnt* prev = nullptr;
-    unsigned long long* stamp = nullptr;
-    float4* pos = nullptr;
+    gw::SlotRec* rec = nullptr;              // [slot_cap] AOI state, payload, pre-tick state, stamp, grid offset
     uint32_t* flags = nullptr;
     uint16_t* gate = nullptr;
     unsigned long long* nbc = nullptr;       // [slot_cap] epoch<<32 | neighbours with a client
@@ -153,7 +150,6 @@ struct gw_ctx {
     uint32_t cells_cap = 0;              // words in each per-cell array
     uint32_t *dep = nullptr, *arr = nullptr, *gm_cnt = nullptr, *cnt_new = nullptr, *dirty = nullptr,
              *gm_start = nullptr;
-    uint32_t* gidx = nullptr;
     SpaceP* sp_dev = nullptr;
     uint32_t sp_cap = 0;
 

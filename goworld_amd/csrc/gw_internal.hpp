@@ -35,6 +35,19 @@ struct alignas(16) PrevEnt {
     unsigned long long ostamp;
 };
 
+// A slot's state in one 64-B record: an op, a collect or a resolve touches one
+// line for all of it instead of one per array (AOI state, sync payload,
+// pre-tick state, stamp, grid offset).
+struct alignas(64) SlotRec {
+    AoiEnt a;                  // AOI state
+    float4 p;                  // x, y, z, yaw (sync payload)
+    PrevEnt pv;                // pre-tick position and stamp (this tick's movers)
+    unsigned long long stamp;  // global stamp of the slot's last AOI op
+    uint32_t gidx;             // offset of the slot's entry inside its cell's range of gn
+    uint32_t pad;
+};
+static_assert(sizeof(SlotRec) == 64, "SlotRec is one 64-B line");
+
 // Per-slot op dedupe state, one 64-B record (a tick's op touches one line for
 // all of it): the index of the slot's last op that sets the sync payload
 // (non-Leave), its last AOI op, its last Leave, and per sync bit the last
@@ -156,15 +169,11 @@ struct World {
     uint32_t cap;              // total slots
     uint32_t ncells;
     const SpaceP* sp;
-    AoiEnt* aoi;
-    PrevEnt* prev;
-    unsigned long long* stamp; // global stamp of the slot's last AOI op
-    float4* pos;               // x, y, z, yaw (sync payload)
+    SlotRec* rec;              // [cap] per-slot state
     uint32_t* flags;           // syncInfoFlag, packed: 2 bits per slot, 16 slots per word (flag_word / flag_sh)
     uint16_t* gate;            // client gate, 0 = no client
     GEnt* gn;                  // [cap] current grid, n_present entries
     uint32_t* gn_start;        // [ncells+1] first entry of each cell
-    uint32_t* gidx;            // [cap] offset of the slot's entry inside its cell's range of gn
     // |{w related to e : w has a client}| as of the end of tick `epoch`
     // (epoch<<32 | count), written for every present mover by the diff; a
     // collect right after that tick takes it instead of walking e's window
@@ -397,7 +406,7 @@ void launch_restore(const World& w, const uint32_t* slots, const float4* xyzw, u
 // client messages (sync.hip)
 void launch_event_client_flags(const gw_event* ev, uint64_t n, const uint16_t* gate, uint32_t* f, hipStream_t s);
 void launch_event_client_write(const gw_event* ev, uint64_t n, const uint32_t* f, const uint32_t* at,
-                               const float4* pos, uint32_t* out, bool create, hipStream_t s);
+                               const SlotRec* rec, uint32_t* out, bool create, hipStream_t s);
 // out == nullptr: counts per item into cnt; else deliveries at off[k]
 void launch_fanout(const World& w, const uint32_t* items, uint32_t n, uint32_t* cnt, const uint64_t* off,
                    gw_fanout_rec* out, hipStream_t s);
@@ -423,6 +432,6 @@ void launch_slots_move(const World& w, OpLast* ol, uint4* eid, uint4* cid, uint3
                        hipStream_t s);
 void launch_slots_clear(const World& w, OpLast* ol, uint4* eid, uint4* cid, uint32_t base, uint32_t n,
                         uint32_t meta, hipStream_t s);
-void launch_count_present(const AoiEnt* aoi, uint32_t base, uint32_t n, unsigned long long* out, hipStream_t s);
+void launch_count_present(const SlotRec* rec, uint32_t base, uint32_t n, unsigned long long* out, hipStream_t s);
 
 }  // namespace gw

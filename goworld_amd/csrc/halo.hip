@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
     uint32_t f = 0;
     gw_op oa{}, op_pos{};
     if (rep) {
-        const AoiEnt a = w.aoi[s];
+        const AoiEnt a = w.rec[s].a;
         old_p = (a.meta & PRESENT_BIT) != 0;
         old_x = a.x;
         new_p = old_p;

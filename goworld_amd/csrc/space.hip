@@ -24,10 +24,7 @@ __global__ void __launch_bounds__(NT) k_slots_move(World w, OpLast* __restrict__
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = src + i, d = dst + i;
-    w.aoi[d] = w.aoi[s];
-    w.prev[d] = w.prev[s];
-    w.stamp[d] = w.stamp[s];
-    w.pos[d] = w.pos[s];
+    w.rec[d] = w.rec[s];               // (its grid offset is rebuilt with the grid)
     w.gate[d] = w.gate[s];
     w.nbc[d] = 0;                      // cached neighbour counts are recomputed (the epoch moves on)
     ol[d] = ol[s];
@@ -49,14 +46,14 @@ __global__ void __launch_bounds__(NT) k_slots_clear(World w, OpLast* __restrict_
     a.z = 0.f;
     a.seq = -1;
     a.meta = meta;
-    w.aoi[s] = a;
+    w.rec[s].a = a;
     PrevEnt p;
     p.ox = 0.f;
     p.oz = 0.f;
     p.ostamp = 0ull;
-    w.prev[s] = p;
-    w.stamp[s] = 0ull;
-    w.pos[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+    w.rec[s].pv = p;
+    w.rec[s].stamp = 0ull;
+    w.rec[s].p = make_float4(0.f, 0.f, 0.f, 0.f);
     w.gate[s] = 0;
     w.nbc[s] = 0ull;
     OpLast z{};
@@ -67,10 +64,10 @@ __global__ void __launch_bounds__(NT) k_slots_clear(World w, OpLast* __restrict_
 }
 
 // entities present in [base, base + n): one add per wave
-__global__ void __launch_bounds__(NT) k_count_present(const AoiEnt* __restrict__ aoi, uint32_t base, uint32_t n,
+__global__ void __launch_bounds__(NT) k_count_present(const SlotRec* __restrict__ rec, uint32_t base, uint32_t n,
                                                        unsigned long long* out) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
-    const bool p = i < n && (aoi[base + i].meta & PRESENT_BIT) != 0;
+    const bool p = i < n && (rec[base + i].a.meta & PRESENT_BIT) != 0;
     const uint64_t bm = wave_ballot(p);
     if (lane_id() == 0 && bm) atomicAdd(out, (unsigned long long)popc64(bm));
 }
@@ -87,8 +84,8 @@ void launch_slots_clear(const World& w, OpLast* ol, uint4* eid, uint4* cid, uint
     if (n) hipLaunchKernelGGL(k_slots_clear, dim3(nblk(n, NT)), dim3(NT), 0, s, w, ol, eid, cid, base, n, meta);
 }
 
-void launch_count_present(const AoiEnt* aoi, uint32_t base, uint32_t n, unsigned long long* out, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(k_count_present, dim3(nblk(n, NT)), dim3(NT), 0, s, aoi, base, n, out);
+void launch_count_present(const SlotRec* rec, uint32_t base, uint32_t n, unsigned long long* out, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_count_present, dim3(nblk(n, NT)), dim3(NT), 0, s, rec, base, n, out);
 }
 
 }  // namespace gw

@@ -19,7 +19,7 @@ namespace gw {
 // The window's row ranges are walked flattened, NB_U chunks of 64 in flight.
 template <int NB_U = 4, typename F>
 __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) {
-    const AoiEnt a = w.aoi[e];
+    const AoiEnt a = w.rec[e].a;
     if (!(a.meta & PRESENT_BIT)) return;
     const SpaceP P = w.sp[a.meta & SPACE_MASK];
     const float d = P.d;
@@ -48,8 +48,8 @@ __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) 
                 const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
                 rel = ia;
                 if (ia != ib) {
-                    if (!have_se) { se = w.stamp[e]; have_se = true; }
-                    rel = resolve(ia, ib, se, w.stamp[g.slot]);
+                    if (!have_se) { se = w.rec[e].stamp; have_se = true; }
+                    rel = resolve(ia, ib, se, w.rec[g.slot].stamp);
                 }
             }
             f(rel, g.slot, (g.meta & CLIENT_BIT) ? 1u : 0u);
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __re
         if (valid) {
             e = flagged[k];
             f = fbits[k];
-            const AoiEnt a = w.aoi[e];
+            const AoiEnt a = w.rec[e].a;
             const uint32_t gt = w.gate[e];                  // loaded with the state, not behind the test
             const unsigned long long c = w.nbc[e];
             // an entity that left the space (into the nil space, keeping its
@@ -239,8 +239,8 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
             if (ln == 0) atomicOr(&st->overflow, 1ull);
             continue;
         }
-        const AoiEnt a = w.aoi[e];
-        const float4 p = w.pos[e];                          // loaded with the state, not behind the test
+        const AoiEnt a = w.rec[e].a;
+        const float4 p = w.rec[e].p;                          // loaded with the state, not behind the test
         const uint32_t gt = w.gate[e];
         if (!owned_x(w.sp[a.meta & SPACE_MASK], a.x)) continue;
         if ((f & GW_SIF_OWN_CLIENT) && gt) {
@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(NT) k_space_ranges(World w, const uint32_t* __
     const uint64_t k = (uint64_t)blockIdx.x * NT + threadIdx.x;
     // one state gather per entry: the neighbours' spaces come from the
     // adjacent lanes, only the wave's edge lanes gather a second one
-    const auto space_at = [&](uint64_t j) { return j < nf ? (w.aoi[flagged[j]].meta & SPACE_MASK) : 0xffffffffu; };
+    const auto space_at = [&](uint64_t j) { return j < nf ? (w.rec[flagged[j]].a.meta & SPACE_MASK) : 0xffffffffu; };
     const uint32_t s = space_at(k);
     const int ln = lane_id();
     uint32_t sp = (uint32_t)__shfl_up((int)s, 1, 64);
@@ -332,8 +332,8 @@ __device__ __forceinline__ void wave_neighbors_lds(const World& w, uint32_t e, c
                 const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
                 rel = ia;
                 if (ia != ib) {
-                    if (!have_se) { se = w.stamp[e]; have_se = true; }
-                    rel = resolve(ia, ib, se, w.stamp[g.slot]);
+                    if (!have_se) { se = w.rec[e].stamp; have_se = true; }
+                    rel = resolve(ia, ib, se, w.rec[g.slot].stamp);
                 }
             }
             f(rel, g.slot, (g.meta & CLIENT_BIT) ? 1u : 0u);
@@ -372,9 +372,9 @@ __global__ void __launch_bounds__(NT) k_sync_write_small(World w, const uint32_t
             if (ln == 0) atomicOr(&st->overflow, 1ull);
             continue;
         }
-        const AoiEnt a = w.aoi[e];
+        const AoiEnt a = w.rec[e].a;
         if (!owned_x(P, a.x)) continue;
-        const float4 p = w.pos[e];
+        const float4 p = w.rec[e].p;
         if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
             if (ln == 0) st_record_nt(rec + at, e, e, p);
             ++at;
@@ -445,8 +445,8 @@ __global__ void __launch_bounds__(NT) k_sync_write_small2(World w, const uint32_
         float4 p = make_float4(0, 0, 0, 0);
         uint32_t gt = 0;
         if (valid) {
-            a = w.aoi[e];
-            p = w.pos[e];
+            a = w.rec[e].a;
+            p = w.rec[e].p;
             gt = w.gate[e];
         }
         if (valid) {
@@ -505,8 +505,8 @@ __global__ void __launch_bounds__(NT) k_sync_write_small2(World w, const uint32_
                 const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
                 bool rel = ia;
                 if (ia != ib) {
-                    if (!have_se) { se = w.stamp[e]; have_se = true; }
-                    rel = resolve(ia, ib, se, w.stamp[g.slot]);
+                    if (!have_se) { se = w.rec[e].stamp; have_se = true; }
+                    rel = resolve(ia, ib, se, w.rec[g.slot].stamp);
                 }
                 take = rel;
             }
@@ -669,9 +669,9 @@ __global__ void __launch_bounds__(NT) k_set_clients(World w, const uint32_t* slo
     if (i >= n || slots[i] >= w.cap) return;
     const uint32_t s = slots[i];
     w.gate[s] = gates[i];
-    const AoiEnt a = w.aoi[s];
+    const AoiEnt a = w.rec[s].a;
     if (grid_ok && (a.meta & PRESENT_BIT)) {
-        const uint32_t k = w.gn_start[cell_of(w.sp[a.meta & SPACE_MASK], a.x, a.z)] + w.gidx[s];
+        const uint32_t k = w.gn_start[cell_of(w.sp[a.meta & SPACE_MASK], a.x, a.z)] + w.rec[s].gidx;
         if (k < w.cap) {
             GEnt* g = w.gn + k;
             if (g->slot == s) g->meta = (g->meta & ~CLIENT_BIT) | (gates[i] ? CLIENT_BIT : 0u);
@@ -745,13 +745,13 @@ __global__ void __launch_bounds__(NT) k_event_client_flags(const gw_event* __res
 __global__ void __launch_bounds__(NT) k_event_client_write(const gw_event* __restrict__ ev, uint64_t n,
                                                            const uint32_t* __restrict__ f,
                                                            const uint32_t* __restrict__ at,
-                                                           const float4* __restrict__ pos, uint32_t* out,
+                                                           const SlotRec* __restrict__ srec, uint32_t* out,
                                                            int create) {
     const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
     if (r >= n || !f[r]) return;
     const gw_event e = ev[r];
     if (create) {
-        const float4 p = pos[e.target];
+        const float4 p = srec[e.target].p;
         gw_sync_record m;
         m.watcher = e.watcher; m.entity = e.target; m.x = p.x; m.y = p.y; m.z = p.z; m.yaw = p.w;
         ((gw_sync_record*)out)[at[r]] = m;
@@ -763,9 +763,9 @@ void launch_event_client_flags(const gw_event* ev, uint64_t n, const uint16_t* g
     if (n) hipLaunchKernelGGL(k_event_client_flags, dim3(nblk(n, NT)), dim3(NT), 0, s, ev, n, gate, f);
 }
 void launch_event_client_write(const gw_event* ev, uint64_t n, const uint32_t* f, const uint32_t* at,
-                               const float4* pos, uint32_t* out, bool create, hipStream_t s) {
+                               const SlotRec* rec, uint32_t* out, bool create, hipStream_t s) {
     if (n)
-        hipLaunchKernelGGL(k_event_client_write, dim3(nblk(n, NT)), dim3(NT), 0, s, ev, n, f, at, pos, out,
+        hipLaunchKernelGGL(k_event_client_write, dim3(nblk(n, NT)), dim3(NT), 0, s, ev, n, f, at, rec, out,
                            create ? 1 : 0);
 }
 

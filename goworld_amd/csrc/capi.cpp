@@ -1267,7 +1267,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.rank_sort = c->rank_sort;
     b.grid_cap = c->grid_cap;
     b.pair_max = c->pair_auto ? (c->cand_mean <= gw_ctx::PAIR_MEAN ? gw_ctx::PAIR_AUTO : 0u) : c->pair_max;
-    b.dirty_span = c->dirty_span;
+    b.dirty_span = c->dirty_span ? c->dirty_span : (NC > (1u << 20) ? 16u : 8u);
     b.long_step = c->wd.on ? c->wd.g.max_step : INFINITY;   // decomposed world: long movers
     b.conflicts = c->wd.on ? &c->halo->conflicts : nullptr;
     b.ol = c->ol;

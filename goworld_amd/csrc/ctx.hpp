@@ -176,7 +176,10 @@ struct gw_ctx {
     DevBuf scan_status, rs_hist;
     uint32_t walk_min = 32;              // GW_WALK_MIN: TickBufs.walk_min (0: always walk)
     uint32_t rank_sort = 12;             // GW_RANK_SORT: TickBufs.rank_sort
-    uint32_t dirty_span = 16;            // GW_DIRTY_SPAN: TickBufs.dirty_span
+    // GW_DIRTY_SPAN: TickBufs.dirty_span; 0 = by the cell count: 8 up to 1M cells (a hotspot wave
+    // merges fewer dirty cells in a row: config #3 grid 63 -> 58 us), 16 above (fewer idle waves:
+    // config #4's 4.4M cells at 4 per wave cost +50 us)
+    uint32_t dirty_span = 0;
     // GW_PAIR_MAX: TickBufs.pair_max.  Unset: automatic, PAIR_AUTO when the last
     // tick had >= PAIR_MOVERS movers averaging <= PAIR_MEAN candidates (many
     // uniform short lists: config #5 diff 1677 -> 1573 us), else 0 (hotspots:

@@ -1776,16 +1776,27 @@ __global__ void __launch_bounds__(BK_SNT) k_bucket_sort(TickBufs b) {
 // quantiles of this tick's sorted (leave, watcher) keys: the next tick's
 // bucket bounds (BK_NSPLIT of them; a tick with fewer buckets takes every
 // (BK_NSPLIT / NB)-th).  Kept when the tick overflowed or had no events.
-__device__ __forceinline__ void bk_split_next(const TickBufs& b, unsigned long long ev_pk, unsigned long long overflow) {
+constexpr uint32_t SPLIT_PT = BK_NSPLIT / RESET_NT;      // splits per reset thread
+// the loads: every split's event in flight together (registers), stored by
+// bk_split_store after the statistics copy has been issued
+__device__ __forceinline__ bool bk_split_load(const TickBufs& b, unsigned long long ev_pk, unsigned long long overflow,
+                                              uint32_t (&v)[SPLIT_PT]) {
     const uint64_t E = lo32(ev_pk) + hi32(ev_pk), ne = lo32(ev_pk);
-    if (E == 0 || E > b.ev_cap || overflow) return;
+    if (E == 0 || E > b.ev_cap || overflow) return false;
     const uint32_t lvb = 1u << b.wbits;
 #pragma unroll
-    for (uint32_t q = 0; q < BK_NSPLIT / RESET_NT; ++q) {   // the loads of every split in flight together
+    for (uint32_t q = 0; q < SPLIT_PT; ++q) {
         const uint32_t j = q * RESET_NT + threadIdx.x;
-        if (j == 0) continue;
         const uint64_t p = (uint64_t)j * E / BK_NSPLIT;
-        b.bk_split[j] = (p >= ne ? lvb : 0u) | b.ev[p].watcher;
+        v[q] = (p >= ne ? lvb : 0u) | b.ev[p].watcher;
+    }
+    return true;
+}
+__device__ __forceinline__ void bk_split_store(const TickBufs& b, const uint32_t (&v)[SPLIT_PT]) {
+#pragma unroll
+    for (uint32_t q = 0; q < SPLIT_PT; ++q) {
+        const uint32_t j = q * RESET_NT + threadIdx.x;
+        if (j) b.bk_split[j] = v[q];
     }
 }
 // uniform bounds over the key range [0, 2^(wbits+1))
@@ -1874,21 +1885,19 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
 // the next tick)
 __global__ void __launch_bounds__(RESET_NT) k_tick_reset(TickBufs b, const unsigned long long* __restrict__ pub_src,
                                                         unsigned long long* pub_dst, uint32_t pub_words) {
-    __shared__ unsigned long long s_ev, s_ov;
+    // the next tick's bucket bounds: their event loads go out first, the
+    // statistics copy below overlaps them
+    uint32_t v[SPLIT_PT];
+    const bool split = b.st && bk_split_load(b, b.st->ev_pk, b.st->overflow, v);
     // the statistics the host reads after its sync, written straight into its
     // (coherent, pinned) buffer: no blit copy between the collect and the reset
     for (uint32_t k = threadIdx.x; k < pub_words; k += RESET_NT) pub_dst[k] = pub_src[k];
-    __syncthreads();
     if (!b.st) {
         __threadfence_system();
         return;
     }
-    if (threadIdx.x == 0) {
-        s_ev = b.st->ev_pk;
-        s_ov = b.st->overflow;
-    }
-    __syncthreads();
-    bk_split_next(b, s_ev, s_ov);
+    if (split) bk_split_store(b, v);
+    __syncthreads();                                        // every read of the statistics done
     unsigned long long* z = (unsigned long long*)b.st;
     for (uint32_t k = threadIdx.x; k < sizeof(DevStats) / 8; k += RESET_NT) z[k] = 0;
     __threadfence_system();

@@ -103,7 +103,7 @@ __global__ void __launch_bounds__(NT) k_ops2(TickBufs b) {
 // last Leave that cleared c.  The slot's last Leave clears in k_ops3, every
 // op's bits after it are OR'd in by k_place (a later launch: clear, then OR).
 __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, uint32_t A, const AoiEnt& a,
-                                                const PrevEnt& p, bool lng);
+                                                const PrevEnt& p, bool lng, bool cl, uint32_t gidx);
 
 // Per op: the syncInfoFlag bits, the sync payload of the slot's last
 // non-Leave op; the slot's last AOI op saves the pre-tick position and stamp
@@ -116,11 +116,19 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
     uint32_t s = 0, fbits = 0;
     AoiEnt a;
     PrevEnt p;
+    bool cl = false;
+    uint32_t gidx = 0;
     if (i < b.m) {
         const gw_op op = b.ops[i];
         s = op.slot;
         if (s < b.w.cap && op.kind >= GW_OP_ENTER && op.kind <= GW_OP_SYNC) {
             const OpLast o = b.ol[s];
+            // the slot's state, loaded with its dedupe record (used when op i
+            // is the slot's last AOI op, nearly always): one round trip less
+            const AoiEnt a0 = b.w.rec[s].a;
+            const unsigned long long st0 = b.w.rec[s].stamp;
+            gidx = b.w.rec[s].gidx;
+            cl = b.w.gate[s] != 0;
             struct { int32_t pos, aoi, leave, clr[2]; } ol;
             ol.pos = ol_get(o.pos, b.ol_tag);
             ol.aoi = ol_get(o.aoi, b.ol_tag);
@@ -141,11 +149,11 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
             }
             if (ol.pos == (int32_t)i) b.w.rec[s].p = make_float4(op.x, op.y, op.z, op.yaw);
             if (ol.aoi == (int32_t)i) {                 // the slot's mover entry (never a SYNC op)
-                a = b.w.rec[s].a;
+                a = a0;
                 const bool was = (a.meta & PRESENT_BIT) != 0;
                 p.ox = was ? a.x : qnan();
                 p.oz = was ? a.z : qnan();
-                p.ostamp = b.w.rec[s].stamp;
+                p.ostamp = st0;
                 b.w.rec[s].pv = p;
                 b.w.rec[s].stamp = b.stamps ? b.stamps[i] : b.stamp_base + i;
                 if (op.kind == GW_OP_LEAVE) a.meta &= ~PRESENT_BIT;
@@ -164,7 +172,7 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
     const uint32_t nw = (uint32_t)popc64(wave_ballot(mv));
     if (lane_id() == 0 && nw) shard_add(b.st, blockIdx.x * NWAVE + (threadIdx.x >> 6), SH_MOVERS, nw);
     uint2 cc = make_uint2(NO_CELL, NO_CELL);
-    if (mv) cc = classify_mover(b, i, s, a, p, lng);
+    if (mv) cc = classify_mover(b, i, s, a, p, lng, cl, gidx);
     if (i < b.m) b.mcell[i] = make_uint4(cc.x, cc.y, s, fbits);   // k_place reads them back coalesced
 }
 
@@ -271,12 +279,11 @@ void grid_rebuild(const World& w, DevStats* st, uint32_t* k0, uint32_t* v0, uint
 // mover's mover-grid entry (tags aside) goes to mtmp[i] and its cells are
 // returned for mcell[i], so k_place reads them coalesced.
 __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, uint32_t A, const AoiEnt& a,
-                                                const PrevEnt& p, bool lng) {
+                                                const PrevEnt& p, bool lng, bool cl, uint32_t gidx) {
     const SpaceP P = b.w.sp[a.meta & SPACE_MASK];
     uint32_t co = NO_CELL, cn = NO_CELL;
     if (p.ox == p.ox) co = cell_of(P, p.ox, p.oz);
     if (a.meta & PRESENT_BIT) cn = cell_of(P, a.x, a.z);
-    const bool cl = b.w.gate[A] != 0;
     if (co != NO_CELL || cn != NO_CELL) {
         const bool pn = cn != NO_CELL;
         MEnt m;
@@ -291,11 +298,11 @@ __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, u
         GEnt e;
         e.x = a.x; e.z = a.z; e.slot = A;
         e.meta = cn | (cl ? CLIENT_BIT : 0u) | b.mbit;
-        b.w.gn[b.w.gn_start[co] + b.w.rec[A].gidx] = e;
+        b.w.gn[b.w.gn_start[co] + gidx] = e;
     } else {
         if (co != NO_CELL) {
             atomicAdd(&b.dep[co], 1u);
-            b.w.gn[b.w.gn_start[co] + b.w.rec[A].gidx].slot = DEPARTED;
+            b.w.gn[b.w.gn_start[co] + gidx].slot = DEPARTED;
         }
         if (cn != NO_CELL) atomicAdd(&b.arr[cn], 1u);
     }
@@ -445,7 +452,9 @@ void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint32_t NC = b.w.ncells;
     hipLaunchKernelGGL(k_cellcnt, dim3(nblk1((uint64_t)NC + 1, NT)), dim3(NT), 0, s, b);
     // both cell scans in one launch; totals land in the low words of the
-    // (zeroed, little-endian) 64-bit counters
+    // (zeroed, little-endian) 64-bit counters.  (Computing the cell counts in
+    // the scan's loads instead of k_cellcnt: grid stage +10 us at config #3,
+    // +23 us at config #4 -- the tiles post their aggregates later.)
     scan_pair32(b.cnt_new, b.gm_cnt, b.start_nxt, b.gm_start, (uint64_t)NC + 1, sc, (uint32_t*)&b.st->n_present,
                 (uint32_t*)&b.st->n_gm, s);
     hipLaunchKernelGGL(k_place, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
@@ -1186,14 +1195,21 @@ __global__ void __launch_bounds__(NT) k_chunk_first(TickBufs b) {
     const uint64_t end = at + mi.y + mi.z + mi.w;
     for (uint64_t c = (at + 63) >> 6; (c << 6) < end; ++c) b.chunk_first[c] = (uint32_t)k;
 }
-__global__ void __launch_bounds__(NT) k_chunk_first_items(TickBufs b) {
-    const uint64_t k = (uint64_t)blockIdx.x * NT + threadIdx.x;
-    if (k >= b.st->n_mlist) return;
-    if (lo32(b.st->ev_pk) + hi32(b.st->ev_pk) > b.ev_cap) return;   // overflow: nothing is flattened (redo)
-    const uint64_t at = b.ioff[k];
-    const uint64_t end = at + b.icnt[k];
-    for (uint64_t c = (at + 63) >> 6; (c << 6) < end; ++c) b.chunk_first[c] = (uint32_t)k;
-}
+// bucket path: chunk_first from the items scan's store phase (its offsets
+// are at hand there), nothing when the tick overflowed (the host redoes it)
+struct ItemsPost {
+    uint32_t* chunk_first;
+    const unsigned long long* ev_pk;
+    uint64_t ev_cap;
+    __device__ bool active() const {
+        const unsigned long long e = *ev_pk;
+        return lo32(e) + hi32(e) <= ev_cap;
+    }
+    __device__ void operator()(uint64_t k, uint32_t at, uint32_t cnt) const {
+        const uint64_t end = (uint64_t)at + cnt;
+        for (uint64_t c = ((uint64_t)at + 63) >> 6; (c << 6) < end; ++c) chunk_first[c] = (uint32_t)k;
+    }
+};
 // element p = 64c + lane of the flat list (wave-uniform c; every lane runs
 // the shuffles); false past E
 __device__ __forceinline__ bool flat_elem(const TickBufs& b, uint64_t c, uint64_t E, uint32_t& key, uint32_t& val) {
@@ -1845,8 +1861,8 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     hipLaunchKernelGGL(k_mover_counts, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
     if (!b.ev_full) {
         const uint32_t NB = 1u << b.bk_bits;
-        scan_exclusive<uint32_t, uint32_t>(b.icnt, b.ioff, b.m, nml, sc, (uint32_t*)&b.st->n_items, s);
-        hipLaunchKernelGGL(k_chunk_first_items, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
+        scan_exclusive<uint32_t, uint32_t>(b.icnt, b.ioff, b.m, nml, sc, (uint32_t*)&b.st->n_items, s,
+                                           ItemsPost{b.chunk_first, &b.st->ev_pk, b.ev_cap});
         const uint64_t fw = std::min<uint64_t>((b.ev_cap + 63) / 64,
                                                std::max<uint64_t>(8192, (2 * b.it_hint + 63) / 64));
         uint32_t fb = nblk1(fw, NWAVE);

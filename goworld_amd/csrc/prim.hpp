@@ -227,11 +227,20 @@ __device__ __forceinline__ TO scan_lookback(unsigned long long* __restrict__ sta
     return excl;
 }
 
-template <typename TI, typename TO, int IPT>
+// Output hook of a scan (element index, exclusive prefix, element): work that
+// needs the scanned offsets rides in the scan's store phase instead of a
+// launch of its own.  active() is read once per thread.
+struct ScanNoPost {
+    __device__ bool active() const { return false; }
+    template <typename T>
+    __device__ void operator()(uint64_t, T, T) const {}
+};
+
+template <typename TI, typename TO, int IPT, class Post = ScanNoPost>
 __global__ void __launch_bounds__(NT) k_scan1(const TI* in, TO* out, uint64_t n_max, const uint64_t* n_dev,
                                               unsigned long long* __restrict__ status,
                                               unsigned long long* __restrict__ ticket, unsigned long long tbase,
-                                              uint32_t tag, TO* total) {
+                                              uint32_t tag, TO* total, Post post) {
     __shared__ TO lds[IPT * NWAVE];
     __shared__ uint32_t s_tile;
     __shared__ TO s_prefix;
@@ -248,6 +257,10 @@ __global__ void __launch_bounds__(NT) k_scan1(const TI* in, TO* out, uint64_t n_
         const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
         v[j] = i < n ? (TO)in[i] : (TO)0;
     }
+    const bool pa = post.active();
+    TO x[IPT];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) x[j] = v[j];
     TO tot;
     tile_excl_scan_striped<TO, IPT>(v, lds, tot);
     if (threadIdx.x < 64) {
@@ -261,6 +274,13 @@ __global__ void __launch_bounds__(NT) k_scan1(const TI* in, TO* out, uint64_t n_
         for (int j = 0; j < IPT; ++j) {
             const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
             if (i < n) out[i] = pre + v[j];
+        }
+    }
+    if (pa) {
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
+            if (i < n) post(i, (TO)(pre + v[j]), x[j]);
         }
     }
     // the last tile holding data (tile 0 when n == 0) writes the total
@@ -328,9 +348,9 @@ inline void scan_pair32(const uint32_t* a, const uint32_t* b, uint32_t* oa, uint
     sc.tbase += nb;
 }
 
-template <typename TI, typename TO>
+template <typename TI, typename TO, class Post = ScanNoPost>
 inline void scan_exclusive(const TI* in, TO* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
-                           TO* total_dev, hipStream_t st) {
+                           TO* total_dev, hipStream_t st, Post post = Post{}) {
     // big scans take 8192-element tiles: half the tickets and look-back windows
     const bool big = n_max > SCAN_BIG;
     const uint64_t tile = big ? 2 * SCAN_TILE : SCAN_TILE;
@@ -342,11 +362,11 @@ inline void scan_exclusive(const TI* in, TO* out, uint64_t n_max, const uint64_t
     }
     ++sc.tag;
     if (big)
-        hipLaunchKernelGGL((k_scan1<TI, TO, 2 * SCAN_IPT>), dim3(nb), dim3(NT), 0, st, in, out, n_max, n_dev,
-                           sc.status, sc.ticket, sc.tbase, sc.tag, total_dev);
+        hipLaunchKernelGGL((k_scan1<TI, TO, 2 * SCAN_IPT, Post>), dim3(nb), dim3(NT), 0, st, in, out, n_max, n_dev,
+                           sc.status, sc.ticket, sc.tbase, sc.tag, total_dev, post);
     else
-        hipLaunchKernelGGL((k_scan1<TI, TO, SCAN_IPT>), dim3(nb), dim3(NT), 0, st, in, out, n_max, n_dev,
-                           sc.status, sc.ticket, sc.tbase, sc.tag, total_dev);
+        hipLaunchKernelGGL((k_scan1<TI, TO, SCAN_IPT, Post>), dim3(nb), dim3(NT), 0, st, in, out, n_max, n_dev,
+                           sc.status, sc.ticket, sc.tbase, sc.tag, total_dev, post);
     sc.tbase += nb;
 }
 inline uint64_t scan_tiles(uint64_t n_max) { return (n_max + SCAN_TILE - 1) / SCAN_TILE + 1; }

@@ -292,17 +292,18 @@ __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, u
         m.slot = A; m.tags = lng ? TAG_LONG : 0u; m.client = cl ? 1u : 0u; m.space = a.meta & SPACE_MASK;
         b.mtmp[i] = m;
     }
+    const uint32_t at = co != NO_CELL ? b.w.gn_start[co] + gidx : 0u;   // (loaded before the atomics)
     if (co != NO_CELL) atomicAdd(&b.gm_cnt[co], 1u);
     if (cn != NO_CELL && cn != co) atomicAdd(&b.gm_cnt[cn], 1u);
     if (co != NO_CELL && co == cn) {
         GEnt e;
         e.x = a.x; e.z = a.z; e.slot = A;
         e.meta = cn | (cl ? CLIENT_BIT : 0u) | b.mbit;
-        b.w.gn[b.w.gn_start[co] + gidx] = e;
+        b.w.gn[at] = e;
     } else {
         if (co != NO_CELL) {
             atomicAdd(&b.dep[co], 1u);
-            b.w.gn[b.w.gn_start[co] + gidx].slot = DEPARTED;
+            b.w.gn[at].slot = DEPARTED;
         }
         if (cn != NO_CELL) atomicAdd(&b.arr[cn], 1u);
     }
@@ -333,22 +334,39 @@ __global__ void __launch_bounds__(NT) k_place(TickBufs b) {
     if (cc.w) atomicOr(&b.w.flags[flag_word(cc.z)], cc.w << flag_sh(cc.z));   // op i's syncInfoFlag bits
     const uint32_t co = cc.x, cn = cc.y;
     if (co == NO_CELL && cn == NO_CELL) return;             // not a mover, or absent before and after
-    MEnt e = b.mtmp[i];
-    const bool cl = e.client != 0;
     const bool pn = cn != NO_CELL;
+    const bool arrive = pn && cn != co;
+    // every load, then every cursor atomic, all in flight together (an atomic
+    // with a return made the loads after it wait for it)
+    MEnt e = b.mtmp[i];
+    uint32_t so = 0, sn = 0, g0 = 0, g1 = 0, dp = 0, nx = 0;
+    if (co != NO_CELL) so = b.gm_start[co];
+    if (arrive) {
+        sn = b.gm_start[cn];
+        g0 = b.w.gn_start[cn];
+        g1 = b.w.gn_start[cn + 1];
+        dp = b.dep[cn];
+        nx = b.start_nxt[cn];
+    }
+    uint32_t ro = 0, rn = 0, ra = 0;
+    if (co != NO_CELL) ro = atomicSub(&b.gm_cnt[co], 1u);
+    if (arrive) {
+        rn = atomicSub(&b.gm_cnt[cn], 1u);
+        ra = atomicSub(&b.arr[cn], 1u);
+    }
+    const bool cl = e.client != 0;
     if (co != NO_CELL) {
         e.tags = (e.tags & TAG_LONG) | TAG_OLD | (cn == co ? TAG_NEW | TAG_PRIMARY : 0u) | (pn ? 0u : TAG_PRIMARY);
-        b.gm[b.gm_start[co] + atomicSub(&b.gm_cnt[co], 1u) - 1u] = e;
+        b.gm[so + ro - 1u] = e;
     }
-    if (pn && cn != co) {
+    if (arrive) {
         e.tags = (e.tags & TAG_LONG) | TAG_NEW | TAG_PRIMARY;
-        b.gm[b.gm_start[cn] + atomicSub(&b.gm_cnt[cn], 1u) - 1u] = e;
-        const uint32_t kept = (b.w.gn_start[cn + 1] - b.w.gn_start[cn]) - (b.dep[cn] & ~CELL_DIRTY);
-        const uint32_t at = b.start_nxt[cn] + kept + atomicSub(&b.arr[cn], 1u) - 1u;
+        b.gm[sn + rn - 1u] = e;
+        const uint32_t kept = (g1 - g0) - (dp & ~CELL_DIRTY);
         GEnt g;
         g.x = e.x; g.z = e.z; g.slot = e.slot;
         g.meta = cn | (cl ? CLIENT_BIT : 0u) | b.mbit;
-        b.gn_nxt[at] = g;
+        b.gn_nxt[nx + kept + ra - 1u] = g;
     }
 }
 

@@ -1371,17 +1371,6 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     // the passes over the flagged list are sized by that bound, not the slots
     const uint32_t NFM = (uint32_t)std::min<uint64_t>(C, std::max<uint64_t>(c->flag_bound, 1));
     c->flag_bound = 0;
-    prof_begin(c, "sync_flagged");
-    launch_flag_compact(c->flags, C, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), c->sc, &st->flagged,
-                        &st->overflow, c->st);
-    prof_end(c, (uint64_t)C * 4 * 2);
-    const uint64_t* nf = (const uint64_t*)&st->flagged;
-    prof_begin(c, "sync_count");
-    launch_sync_count(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint32_t>(c->rec_cnt), c->st);
-    scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), NFM, nf, c->sc,
-                 (uint64_t*)&st->rec_total, c->st);
-    size_t s_count = prof_end(c, 0);
-    prof_begin(c, "sync_write");
     // small-space mode: every space's grid fits in LDS (config #4's many small spaces)
     uint32_t max_ents = 0, max_cells = 0;
     for (auto& sp : c->spaces)
@@ -1393,21 +1382,31 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     static const bool small_on = !getenv("GW_SMALL") || atoi(getenv("GW_SMALL")) != 0;
     const bool small = small_on && n_sp >= 2 &&
                        (size_t)max_ents * sizeof(GEnt) + ((size_t)max_cells + 1) * 4 <= SMALL_LDS_MAX;
+    // the spaces' runs of the flagged list: zeroed by the compaction, set by the count pass
+    if (small && (rc = ensure(c, c->srange, (size_t)n_sp * 8))) return rc;
+    uint32_t* sfirst = small ? P<uint32_t>(c->srange) : nullptr;
+    uint32_t* slast = small ? sfirst + n_sp : nullptr;
+    prof_begin(c, "sync_flagged");
+    launch_flag_compact(c->flags, C, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), c->sc, &st->flagged,
+                        &st->overflow, sfirst, small ? 2 * n_sp : 0u, c->st);
+    prof_end(c, (uint64_t)C * 4 * 2);
+    const uint64_t* nf = (const uint64_t*)&st->flagged;
+    prof_begin(c, "sync_count");
+    launch_sync_count(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint32_t>(c->rec_cnt), sfirst,
+                      slast, c->st);
+    scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), NFM, nf, c->sc,
+                 (uint64_t*)&st->rec_total, c->st);
+    size_t s_count = prof_end(c, 0);
+    prof_begin(c, "sync_write");
     auto write_pass = [&]() {
         if (small)
             launch_sync_write_small(w, n_sp, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), P<uint64_t>(c->rec_off),
                                     P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st,
-                                    P<uint32_t>(c->srange), P<uint32_t>(c->srange) + n_sp, max_ents, max_cells, c->st);
+                                    sfirst, slast, max_ents, max_cells, c->st);
         else
             launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint64_t>(c->rec_off),
                               P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
     };
-    if (small) {
-        if ((rc = ensure(c, c->srange, (size_t)n_sp * 8))) return rc;
-        HIPCHK(hipMemsetAsync(c->srange.p, 0, (size_t)n_sp * 8, c->st));
-        launch_space_ranges(w, P<uint32_t>(c->flagged), nf, NFM, P<uint32_t>(c->srange), P<uint32_t>(c->srange) + n_sp,
-                            c->st);
-    }
     write_pass();
     size_t s_write = prof_end(c, 0);
     HIPCHK(hipGetLastError());

@@ -312,8 +312,6 @@ void publish_words(const PubSeg* segs, int n, hipStream_t s);
 void launch_set_clients(const World& w, const uint32_t* slots, const uint16_t* gates, uint32_t n, bool grid_ok,
                         hipStream_t s);
 // sync collect
-void launch_space_ranges(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
-                         uint32_t* sfirst, uint32_t* slast, hipStream_t s);
 void launch_sync_write_small(const World& w, uint32_t n_spaces, const uint32_t* flagged, const uint32_t* fbits,
                              const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec, uint64_t rec_cap,
                              DevStats* st, const uint32_t* sfirst, const uint32_t* slast, uint32_t max_ents,
@@ -321,11 +319,13 @@ void launch_sync_write_small(const World& w, uint32_t n_spaces, const uint32_t* 
 // small-space mode: every space's grid (entries + row starts) in this many LDS bytes at most
 constexpr size_t SMALL_LDS_MAX = 48 * 1024;
 // also zeroes *ovf, the write passes' overflow flag (the collect's only
-// accumulated counter: no reset copy of the collect's DevStats)
+// accumulated counter: no reset copy of the collect's DevStats), and zero[0, nzero)
 void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint32_t* fbits, ScanCtx& sc,
-                         unsigned long long* total, unsigned long long* ovf, hipStream_t s);
+                         unsigned long long* total, unsigned long long* ovf, uint32_t* zero, uint32_t nzero,
+                         hipStream_t s);
+// sfirst / slast (small-space mode, else null): each space's run of the flagged list
 void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
-                       uint32_t nf_max, uint32_t* cnt, hipStream_t s);
+                       uint32_t nf_max, uint32_t* cnt, uint32_t* sfirst, uint32_t* slast, hipStream_t s);
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
                        uint64_t rec_cap, DevStats* st, hipStream_t s);

@@ -68,7 +68,8 @@ __global__ void __launch_bounds__(NT) k_flag_compact1(uint32_t* __restrict__ fla
                                                       unsigned long long* __restrict__ status,
                                                       unsigned long long* __restrict__ ticket,
                                                       unsigned long long tbase, uint32_t tag,
-                                                      unsigned long long* total, unsigned long long* ovf) {
+                                                      unsigned long long* total, unsigned long long* ovf,
+                                                      uint32_t* __restrict__ zero, uint32_t nzero) {
     __shared__ uint32_t lds[IPT * NWAVE];
     __shared__ uint32_t s_tile, s_prefix;
     if (blockIdx.x == 0 && threadIdx.x == 0) *ovf = 0;
@@ -107,10 +108,13 @@ __global__ void __launch_bounds__(NT) k_flag_compact1(uint32_t* __restrict__ fla
         }
     }
     if (tile == gridDim.x - 1 && threadIdx.x == 0) *total = pre + tot;   // all 64 bits (no reset copy)
+    // the next pass's per-space ranges start empty (no fill launch of their own)
+    for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < nzero; i += gridDim.x * NT) zero[i] = 0;
 }
 
 void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint32_t* fbits, ScanCtx& sc,
-                         unsigned long long* total, unsigned long long* ovf, hipStream_t s) {
+                         unsigned long long* total, unsigned long long* ovf, uint32_t* zero, uint32_t nzero,
+                         hipStream_t s) {
     const uint32_t nwords = (cap + 15) / 16;
     const bool big = nwords > SCAN_BIG;
     const uint64_t tile = big ? 2 * SCAN_TILE : SCAN_TILE;
@@ -123,10 +127,10 @@ void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint3
     ++sc.tag;
     if (big)
         hipLaunchKernelGGL(k_flag_compact1<2 * SCAN_IPT>, dim3(nb), dim3(NT), 0, s, flags, nwords, flagged, fbits,
-                           sc.status, sc.ticket, sc.tbase, sc.tag, total, ovf);
+                           sc.status, sc.ticket, sc.tbase, sc.tag, total, ovf, zero, nzero);
     else
         hipLaunchKernelGGL(k_flag_compact1<SCAN_IPT>, dim3(nb), dim3(NT), 0, s, flags, nwords, flagged, fbits,
-                           sc.status, sc.ticket, sc.tbase, sc.tag, total, ovf);
+                           sc.status, sc.ticket, sc.tbase, sc.tag, total, ovf, zero, nzero);
     sc.tbase += nb;
 }
 
@@ -138,24 +142,50 @@ constexpr uint32_t SYNC_MAX_BLOCKS = 8192;
 // record count per flagged entity: a lane per entity (the diff's cached count
 // of neighbours with a client when it is from this epoch); the entities that
 // need a window walk are then walked one at a time by the whole wave
+// Small-space mode (sfirst non-null): each space's run [sfirst, slast) of the
+// flagged list (slot order) for the write pass, from the spaces this pass
+// reads anyway; the neighbours' spaces come from the adjacent lanes, only a
+// wave's edge lanes gather one more.
 template <int U>
 __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __restrict__ flagged,
                                                    const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
-                                                   uint32_t nf_max, uint32_t* cnt) {
+                                                   uint32_t nf_max, uint32_t* cnt, uint32_t* __restrict__ sfirst,
+                                                   uint32_t* __restrict__ slast) {
     const uint64_t nf = load_n(nf_max, nf_dev);
     const int ln = lane_id();
     const uint64_t stride = (uint64_t)gridDim.x * NT;
     for (uint64_t base = (uint64_t)blockIdx.x * NT + (threadIdx.x & ~63u); base < nf; base += stride) {
         const uint64_t k = base + ln;
         const bool valid = k < nf;
-        uint32_t e = 0, f = 0, r = 0;
-        bool walk = false;
+        uint32_t e = 0, f = 0, r = 0, gt = 0;
+        AoiEnt a{};
+        unsigned long long c = 0;
+        uint32_t eo = 0xffffffffu;                          // small-space mode: an edge lane's outer neighbour
         if (valid) {
             e = flagged[k];
             f = fbits[k];
-            const AoiEnt a = w.rec[e].a;
-            const uint32_t gt = w.gate[e];                  // loaded with the state, not behind the test
-            const unsigned long long c = w.nbc[e];
+        }
+        if (sfirst) {                                       // kernel-uniform
+            if (ln == 0 && valid && k) eo = flagged[k - 1];
+            if (ln == 63 && k + 1 < nf) eo = flagged[k + 1];
+        }
+        if (valid) {
+            a = w.rec[e].a;
+            gt = w.gate[e];                                 // loaded with the state, not behind the test
+            c = w.nbc[e];
+        }
+        if (sfirst) {
+            const uint32_t so = eo != 0xffffffffu ? (w.rec[eo].a.meta & SPACE_MASK) : 0xffffffffu;
+            const uint32_t sq = valid ? (a.meta & SPACE_MASK) : 0xffffffffu;
+            uint32_t sp = (uint32_t)__shfl_up((int)sq, 1, 64);
+            uint32_t sn = (uint32_t)__shfl_down((int)sq, 1, 64);
+            if (ln == 0) sp = so;
+            if (ln == 63) sn = so;
+            if (valid && sp != sq) sfirst[sq] = (uint32_t)k;
+            if (valid && sn != sq) slast[sq] = (uint32_t)(k + 1);
+        }
+        bool walk = false;
+        if (valid) {
             // an entity that left the space (into the nil space, keeping its
             // flag) still syncs its own client (Entity.go:1221-1239); only a
             // present one has neighbours
@@ -182,12 +212,15 @@ __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __re
     }
 }
 void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
-                       uint32_t nf_max, uint32_t* cnt, hipStream_t s) {
+                       uint32_t nf_max, uint32_t* cnt, uint32_t* sfirst, uint32_t* slast, hipStream_t s) {
     if (!nf_max) return;
     const dim3 g(std::min(nblk(nf_max, NT), SYNC_MAX_BLOCKS));
-    if (w.nb_u >= 8) hipLaunchKernelGGL(k_sync_count<8>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, cnt);
-    else if (w.nb_u <= 2) hipLaunchKernelGGL(k_sync_count<2>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, cnt);
-    else hipLaunchKernelGGL(k_sync_count<4>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, cnt);
+    if (w.nb_u >= 8)
+        hipLaunchKernelGGL(k_sync_count<8>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, cnt, sfirst, slast);
+    else if (w.nb_u <= 2)
+        hipLaunchKernelGGL(k_sync_count<2>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, cnt, sfirst, slast);
+    else
+        hipLaunchKernelGGL(k_sync_count<4>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, cnt, sfirst, slast);
 }
 
 // A record as three 8-B non-temporal stores: the collect never reads its
@@ -287,25 +320,6 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
 // flagged entities (a contiguous range of the slot-ordered flagged list) with
 // every candidate read from LDS: the per-entity chain of dependent global
 // loads shrinks to the entity's own state.
-__global__ void __launch_bounds__(NT) k_space_ranges(World w, const uint32_t* __restrict__ flagged,
-                                                     const uint64_t* nf_dev, uint32_t nf_max,
-                                                     uint32_t* __restrict__ sfirst, uint32_t* __restrict__ slast) {
-    const uint64_t nf = load_n(nf_max, nf_dev);
-    const uint64_t k = (uint64_t)blockIdx.x * NT + threadIdx.x;
-    // one state gather per entry: the neighbours' spaces come from the
-    // adjacent lanes, only the wave's edge lanes gather a second one
-    const auto space_at = [&](uint64_t j) { return j < nf ? (w.rec[flagged[j]].a.meta & SPACE_MASK) : 0xffffffffu; };
-    const uint32_t s = space_at(k);
-    const int ln = lane_id();
-    uint32_t sp = (uint32_t)__shfl_up((int)s, 1, 64);
-    uint32_t sn = (uint32_t)__shfl_down((int)s, 1, 64);
-    if (ln == 0) sp = k ? space_at(k - 1) : 0xffffffffu;
-    if (ln == 63) sn = space_at(k + 1);
-    if (k >= nf) return;
-    if (sp != s) sfirst[s] = (uint32_t)k;
-    if (sn != s) slast[s] = (uint32_t)(k + 1);
-}
-
 template <int NB_U, typename F>
 __device__ __forceinline__ void wave_neighbors_lds(const World& w, uint32_t e, const AoiEnt& a, const SpaceP& P,
                                                    const GEnt* G, uint32_t g0, const uint32_t* S, F f) {
@@ -522,11 +536,6 @@ __global__ void __launch_bounds__(NT) k_sync_write_small2(World w, const uint32_
     }
 }
 
-void launch_space_ranges(const World& w, const uint32_t* flagged, const uint64_t* nf_dev, uint32_t nf_max,
-                         uint32_t* sfirst, uint32_t* slast, hipStream_t s) {
-    if (nf_max) hipLaunchKernelGGL(k_space_ranges, dim3(nblk1(nf_max, NT)), dim3(NT), 0, s, w, flagged, nf_dev, nf_max,
-                                   sfirst, slast);
-}
 void launch_sync_write_small(const World& w, uint32_t n_spaces, const uint32_t* flagged, const uint32_t* fbits,
                              const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec, uint64_t rec_cap,
                              DevStats* st, const uint32_t* sfirst, const uint32_t* slast, uint32_t max_ents,

@@ -6,7 +6,7 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-f
 LIBDIR   := goworld_amd/lib
 CSRC     := goworld_amd/csrc
 HDR      := $(CSRC)/prim.hpp $(CSRC)/gw_internal.hpp $(CSRC)/dev_common.hpp $(CSRC)/ctx.hpp include/gpuaoi.h
-OBJ      := $(LIBDIR)/aoi.o $(LIBDIR)/sync.o $(LIBDIR)/halo.o $(LIBDIR)/capi.o $(LIBDIR)/world.o $(LIBDIR)/wire.o $(LIBDIR)/space.o
+OBJ      := $(LIBDIR)/aoi.o $(LIBDIR)/sync.o $(LIBDIR)/halo.o $(LIBDIR)/capi.o $(LIBDIR)/world.o $(LIBDIR)/wire.o $(LIBDIR)/space.o $(LIBDIR)/xport.o
 ROCM     ?= /opt/rocm
 
 all: $(LIBDIR)/libgpuaoi.so $(LIBDIR)/c_harness oracle

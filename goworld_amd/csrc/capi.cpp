@@ -547,7 +547,7 @@ void gw_shutdown(gw_ctx* c) {
     if (c->eid_dev) (void)hipFree(c->eid_dev);
     if (c->cid_dev) (void)hipFree(c->cid_dev);
     for (DevBuf* b : wb) if (b->p) (void)hipFree(b->p);
-    if (c->comm) (void)ncclCommDestroy(c->comm);
+    xp_release(c);
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off, &c->m_create.h,
                     &c->m_destroy.h, &c->m_fanout.h};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);

@@ -79,6 +79,16 @@ struct WorldHost {
     uint32_t* pub_d = nullptr;      // the same buffer as the device sees it
 };
 
+// transport (xport.cpp): one point-to-point transfer of an open group, and the
+// loopback group of contexts driven by threads of one process
+struct P2P {
+    bool send;
+    void* p;
+    size_t bytes;
+    int peer;
+};
+struct LocalGroup;
+
 // a 16-byte EntityID as a hash-map key
 struct Id16 {
     uint64_t a, b;
@@ -242,9 +252,14 @@ struct gw_ctx {
     std::vector<uint16_t> wire_gate;
     std::vector<uint64_t> wire_off;
 
-    // RCCL communicator and decomposed world (world.cpp)
+    // communicator (xport.cpp: RCCL, or a loopback group of contexts of this
+    // process) and decomposed world (world.cpp)
     ncclComm_t comm = nullptr;
+    gw::host::LocalGroup* lgrp = nullptr;
     int c_nranks = 0, c_rank = 0;
+    bool xp_open = false;                       // a transport group is being issued
+    std::vector<gw::host::P2P> xp_pend;         // its transfers
+    DevBuf xp_tmp;                              // loopback all-reduce scratch
     gw::host::WorldHost wd;
 };
 
@@ -258,6 +273,16 @@ int next_ol_tag(gw_ctx* c, uint32_t* tag);
 World world_of(gw_ctx* c);
 template <typename T>
 T* P(DevBuf& b) { return (T*)b.p; }
+// transport (xport.cpp): NCCL semantics on the context's stream, RCCL or loopback
+bool xp_on(const gw_ctx* c);
+int xp_group_start(gw_ctx* c);
+int xp_send(gw_ctx* c, const void* p, size_t bytes, int peer);
+int xp_recv(gw_ctx* c, void* p, size_t bytes, int peer);
+int xp_group_end(gw_ctx* c);
+void xp_abort(gw_ctx* c);                                   // drop an open group (error path)
+int xp_allgather(gw_ctx* c, const void* send, void* recv, size_t bytes);   // `bytes` from every rank, rank order
+int xp_allreduce_u64(gw_ctx* c, unsigned long long* dev, uint32_t n, int op);   // in place, GW_RED_*
+void xp_release(gw_ctx* c);                                 // gw_shutdown
 }  // namespace host
 }  // namespace gw
 

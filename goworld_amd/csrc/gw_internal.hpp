@@ -382,6 +382,9 @@ void launch_route_halo(const World& w, const gw_op* ops, const unsigned long lon
 void launch_far_partition(const gw_halo_row* rows, const uint32_t* dest, uint32_t n, const uint32_t* off,
                           uint32_t* cursor, uint32_t nranks, gw_halo_row* out, hipStream_t s);
 void launch_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n, hipStream_t s);
+// out[i] = sum (mx: max) over r < R of in[r * n + i]
+void launch_reduce_u64(const unsigned long long* in, unsigned long long* out, uint32_t n, uint32_t R, bool mx,
+                       hipStream_t s);
 // up to SEG_MAX device segments of a tick's op stream (halo rows, or ops with
 // stamps when the tick is stamped) gathered by one launch
 constexpr int SEG_MAX = 8;

@@ -299,6 +299,24 @@ void launch_iota_u64(unsigned long long* p, unsigned long long base, uint32_t n,
     if (n) hipLaunchKernelGGL(k_iota_u64, dim3(nblk(n, NT)), dim3(NT), 0, s, p, base, n);
 }
 
+// loopback all-reduce (xport.cpp): out[i] = sum / max over the R gathered copies in[r * n + i]
+__global__ void __launch_bounds__(NT) k_reduce_u64(const unsigned long long* __restrict__ in,
+                                                    unsigned long long* __restrict__ out, uint32_t n, uint32_t R,
+                                                    bool mx) {
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    unsigned long long v = in[i];
+    for (uint32_t r = 1; r < R; ++r) {
+        const unsigned long long x = in[(size_t)r * n + i];
+        v = mx ? (x > v ? x : v) : v + x;
+    }
+    out[i] = v;
+}
+void launch_reduce_u64(const unsigned long long* in, unsigned long long* out, uint32_t n, uint32_t R, bool mx,
+                       hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_reduce_u64, dim3(nblk(n, NT)), dim3(NT), 0, s, in, out, n, R, mx);
+}
+
 void launch_split_rows(const gw_halo_row* rows, uint32_t n, gw_op* ops, unsigned long long* stamps,
                        hipStream_t s) {
     hipLaunchKernelGGL(k_split_rows, dim3(nblk1(n, NT)), dim3(NT), 0, s, rows, n, ops, stamps);

@@ -118,7 +118,11 @@ int far_settle(gw_ctx* c, const gw_op* ops, uint32_t n, const HaloDsts& D, uint3
             (rc = ensure(c, W.far_dest, (size_t)cap * 4)))
             return rc;
         W.far_cap = cap;
+        // the rerun places the same rows again; the accumulating counters
+        // (overflow, conflicts, bad ops, long moves) must not count them twice
+        unsigned long long keep[4] = {hs.overflow, hs.conflicts, hs.bad_ops, hs.long_moves};
         if ((rc = route_launch(c, ops, n, D, tag, base))) return rc;
+        HIPCHK(hipMemcpyAsync(c->halo, keep, sizeof keep, hipMemcpyHostToDevice, c->st));
         HIPCHK(hipMemcpyAsync(&hs, c->halo, sizeof hs, hipMemcpyDeviceToHost, c->st));
         HIPCHK(hipStreamSynchronize(c->st));
         if (hs.far_n > W.far_cap) return set_err(c, GW_ENOMEM, "far halo rows overflowed twice");
@@ -152,7 +156,7 @@ int gw_comm_unique_id(void* id) {
 
 int gw_comm_init(gw_ctx* c, const void* id, int nranks, int rank) {
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return GW_EINVAL;
-    if (c->comm) return set_err(c, GW_ESTATE, "communicator already initialised");
+    if (xp_on(c)) return set_err(c, GW_ESTATE, "communicator already initialised");
     if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
     ncclUniqueId u;
@@ -165,41 +169,31 @@ int gw_comm_init(gw_ctx* c, const void* id, int nranks, int rank) {
 
 int gw_comm_info(gw_ctx* c, int* nranks, int* rank) {
     if (!c) return GW_EINVAL;
-    if (nranks) *nranks = c->comm ? c->c_nranks : 0;
-    if (rank) *rank = c->comm ? c->c_rank : 0;
+    if (nranks) *nranks = xp_on(c) ? c->c_nranks : 0;
+    if (rank) *rank = xp_on(c) ? c->c_rank : 0;
     return 0;
 }
 
 int gw_comm_exchange(gw_ctx* c, const gw_xfer* x, uint32_t n) {
     if (!c || (n && !x)) return GW_EINVAL;
-    if (!c->comm) return set_err(c, GW_ESTATE, "no communicator (gw_comm_init)");
+    if (!xp_on(c)) return set_err(c, GW_ESTATE, "no communicator (gw_comm_init)");
     for (uint32_t i = 0; i < n; ++i)
         if (x[i].peer < 0 || x[i].peer >= c->c_nranks || (x[i].send_bytes && !x[i].send) ||
             (x[i].recv_bytes && !x[i].recv))
             return set_err(c, GW_EINVAL, "bad transfer %u", i);
-    (void)hipSetDevice(c->dev);
-    NCCLCHK(ncclGroupStart());
+    int rc;
+    if ((rc = xp_group_start(c))) return rc;
     for (uint32_t i = 0; i < n; ++i) {
-        if (x[i].send_bytes) {
-            ncclResult_t r = ncclSend(x[i].send, x[i].send_bytes, ncclUint8, x[i].peer, c->comm, c->st);
-            if (r != ncclSuccess) { (void)ncclGroupEnd(); NCCLCHK(r); }
-        }
-        if (x[i].recv_bytes) {
-            ncclResult_t r = ncclRecv(x[i].recv, x[i].recv_bytes, ncclUint8, x[i].peer, c->comm, c->st);
-            if (r != ncclSuccess) { (void)ncclGroupEnd(); NCCLCHK(r); }
-        }
+        if (x[i].send_bytes) (void)xp_send(c, x[i].send, x[i].send_bytes, x[i].peer);
+        if (x[i].recv_bytes) (void)xp_recv(c, x[i].recv, x[i].recv_bytes, x[i].peer);
     }
-    NCCLCHK(ncclGroupEnd());
-    return 0;
+    return xp_group_end(c);
 }
 
 int gw_comm_allreduce_u64(gw_ctx* c, uint64_t* dev, uint32_t n, int op) {
     if (!c || (n && !dev) || (op != GW_RED_SUM && op != GW_RED_MAX)) return GW_EINVAL;
-    if (!c->comm) return set_err(c, GW_ESTATE, "no communicator (gw_comm_init)");
-    if (!n) return 0;
-    (void)hipSetDevice(c->dev);
-    NCCLCHK(ncclAllReduce(dev, dev, n, ncclUint64, op == GW_RED_SUM ? ncclSum : ncclMax, c->comm, c->st));
-    return 0;
+    if (!xp_on(c)) return set_err(c, GW_ESTATE, "no communicator (gw_comm_init)");
+    return xp_allreduce_u64(c, (unsigned long long*)dev, n, op);
 }
 
 int gw_world_create(gw_ctx* c, const gw_world_geom* g, uint32_t capacity, const float* bounds, uint32_t* space_id) {
@@ -215,12 +209,7 @@ int gw_world_create(gw_ctx* c, const gw_world_geom* g, uint32_t capacity, const 
     if (g->ranks > 2 && !(g->strip_w > W.h + g->max_step))
         return set_err(c, GW_EINVAL, "strip width %g must exceed halo %g + max_step %g", g->strip_w, W.h,
                        g->max_step);
-    uint32_t sid = 0, base = 0;
-    if (int rc = gw_space_create(c, g->aoi_dist, capacity, bounds, &sid, &base)) return rc;
-    if (base != 0) return set_err(c, GW_ESTATE, "a world strip must be the context's first space (slot = id)");
     const int r = (int)g->rank;
-    if (int rc = gw_space_set_ownership(c, sid, f32_ceil(strip_lo(*g, r), -1), f32_ceil(strip_hi(*g, r), 1)))
-        return rc;
     for (int side = 0; side < 2; ++side) {
         const int nb = side == 0 ? r - 1 : r + 1;
         W.nb[side] = (nb >= 0 && nb < (int)g->ranks) ? nb : -1;
@@ -234,6 +223,8 @@ int gw_world_create(gw_ctx* c, const gw_world_geom* g, uint32_t capacity, const 
         W.ext_h[2 * q] = (float)(strip_lo(*g, (int)q) - W.h);
         W.ext_h[2 * q + 1] = (float)(strip_hi(*g, (int)q) + W.h);
     }
+    // the world's buffers first: a failure leaves no space behind (a retry
+    // must find the context empty, the strip's space at slot base 0)
     int rc2;
     if ((rc2 = ensure(c, W.ext, W.ext_h.size() * 4)) || (rc2 = ensure(c, W.far_cnt, (size_t)g->ranks * 4)) ||
         (rc2 = ensure(c, W.far_off, (size_t)g->ranks * 4)) || (rc2 = ensure(c, W.far_cursor, (size_t)g->ranks * 4)) ||
@@ -241,10 +232,24 @@ int gw_world_create(gw_ctx* c, const gw_world_geom* g, uint32_t capacity, const 
         return rc2;
     HIPCHK(hipMemcpyAsync(W.ext.p, W.ext_h.data(), W.ext_h.size() * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    if (W.pub_h) (void)hipHostFree(W.pub_h);
+    W.pub_h = W.pub_d = nullptr;
     const size_t pub_words = pub_off_cnt() + 2 + g->ranks + (size_t)g->ranks * g->ranks;
     if (hipHostMalloc((void**)&W.pub_h, pub_words * 4, hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&W.pub_d, W.pub_h, 0) != hipSuccess)
         return set_err(c, GW_ENOMEM, "world count buffer");
+    uint32_t sid = 0, base = 0;
+    if (int rc = gw_space_create(c, g->aoi_dist, capacity, bounds, &sid, &base)) return rc;
+    if (base != 0) {
+        (void)gw_space_destroy(c, sid);
+        return set_err(c, GW_ESTATE, "a world strip must be the context's first space (slot = id)");
+    }
+    if (int rc = gw_space_set_ownership(c, sid, f32_ceil(strip_lo(*g, r), -1), f32_ceil(strip_hi(*g, r), 1))) {
+        std::string keep = c->err;
+        (void)gw_space_destroy(c, sid);
+        c->err = keep;
+        return rc;
+    }
     W.far_cnt_h.assign(g->ranks, 0);
     W.far_off_h.assign(g->ranks, 0);
     W.far_mat_h.assign((size_t)g->ranks * g->ranks, 0);
@@ -339,7 +344,7 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
     if (W.ol_pre) return set_err(c, GW_ESTATE, "the last routed world tick was not ticked (gw_tick first)");
     if (W.routed) return set_err(c, GW_ESTATE, "tick already routed: gw_world_submit first");
     const bool any_nb = W.nb[0] >= 0 || W.nb[1] >= 0;
-    if (any_nb && (!c->comm || c->c_nranks != (int)W.g.ranks || c->c_rank != (int)W.g.rank))
+    if (any_nb && (!xp_on(c) || c->c_nranks != (int)W.g.ranks || c->c_rank != (int)W.g.rank))
         return set_err(c, GW_ESTATE, "world of %u ranks needs a matching communicator (gw_comm_init)", W.g.ranks);
     if ((uint64_t)n >= STAMP_STRIDE) return set_err(c, GW_ERANGE, "too many ops in one tick for the stamp layout");
     if (int rs = settle(c)) return rs;
@@ -371,18 +376,16 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
         // round 1: the entity counts (u32) both ways; HaloStats.cnt[k] is the
         // k-th destination of D, i.e. left first when both exist
         uint32_t* dcnt = P<uint32_t>(W.cnt);         // [0..1] received from left / right
-        NCCLCHK(ncclGroupStart());
+        if ((rc = xp_group_start(c))) return rc;
         uint32_t k = 0;
         for (int side = 0; side < 2; ++side) {
             if (W.nb[side] < 0) continue;
-            ncclResult_t r1 = ncclSend(&c->halo->cnt[k++], 1, ncclUint32, W.nb[side], c->comm, c->st);
-            ncclResult_t r2 = ncclRecv(dcnt + side, 1, ncclUint32, W.nb[side], c->comm, c->st);
-            if (r1 != ncclSuccess || r2 != ncclSuccess) { (void)ncclGroupEnd(); NCCLCHK(r1 != ncclSuccess ? r1 : r2); }
+            (void)xp_send(c, &c->halo->cnt[k++], 4, W.nb[side]);
+            (void)xp_recv(c, dcnt + side, 4, W.nb[side]);
         }
-        NCCLCHK(ncclGroupEnd());
+        if ((rc = xp_group_end(c))) return rc;
         // the far triples every rank sends every rank (long moves; R u32 each)
-        if (far_round)
-            NCCLCHK(ncclAllGather(W.far_cnt.p, W.far_mat.p, R, ncclUint32, c->comm, c->st));
+        if (far_round && (rc = xp_allgather(c, W.far_cnt.p, W.far_mat.p, (size_t)R * 4))) return rc;
         uint32_t h[4] = {0, 0, 0, 0};
         HaloStats hs{};
         if ((rc = read_route_counts(c, hs, h, far_round))) return rc;
@@ -402,35 +405,29 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
             if (far_in && (rc = ensure(c, W.far_recv, (size_t)far_in * ROWS * sizeof(gw_halo_row)))) return rc;
         }
         // round 2: exactly the used rows (neighbours), and the far triples
-        NCCLCHK(ncclGroupStart());
+        if ((rc = xp_group_start(c))) return rc;
         for (int side = 0; side < 2; ++side) {
             if (W.nb[side] < 0) continue;
-            ncclResult_t r1 = ncclSuccess, r2 = ncclSuccess;
             if (W.send_cnt[side])
-                r1 = ncclSend(W.send[side].p, (size_t)W.send_cnt[side] * ROWS * sizeof(gw_halo_row), ncclUint8,
-                              W.nb[side], c->comm, c->st);
+                (void)xp_send(c, W.send[side].p, (size_t)W.send_cnt[side] * ROWS * sizeof(gw_halo_row), W.nb[side]);
             if (rcnt[side])
-                r2 = ncclRecv(W.recv[side].p, (size_t)rcnt[side] * ROWS * sizeof(gw_halo_row), ncclUint8, W.nb[side],
-                              c->comm, c->st);
-            if (r1 != ncclSuccess || r2 != ncclSuccess) { (void)ncclGroupEnd(); NCCLCHK(r1 != ncclSuccess ? r1 : r2); }
+                (void)xp_recv(c, W.recv[side].p, (size_t)rcnt[side] * ROWS * sizeof(gw_halo_row), W.nb[side]);
         }
         if (far_round) {
             size_t roff = 0;
             for (uint32_t p = 0; p < R; ++p) {
                 if (p == me) continue;
-                ncclResult_t r1 = ncclSuccess, r2 = ncclSuccess;
                 const uint32_t out = W.far_cnt_h[p], in = W.far_mat_h[(size_t)p * R + me];
                 if (out)
-                    r1 = ncclSend(P<gw_halo_row>(W.far_sorted) + (size_t)W.far_off_h[p] * ROWS,
-                                  (size_t)out * ROWS * sizeof(gw_halo_row), ncclUint8, (int)p, c->comm, c->st);
+                    (void)xp_send(c, P<gw_halo_row>(W.far_sorted) + (size_t)W.far_off_h[p] * ROWS,
+                                  (size_t)out * ROWS * sizeof(gw_halo_row), (int)p);
                 if (in)
-                    r2 = ncclRecv(P<gw_halo_row>(W.far_recv) + roff * ROWS, (size_t)in * ROWS * sizeof(gw_halo_row),
-                                  ncclUint8, (int)p, c->comm, c->st);
+                    (void)xp_recv(c, P<gw_halo_row>(W.far_recv) + roff * ROWS, (size_t)in * ROWS * sizeof(gw_halo_row),
+                                  (int)p);
                 roff += in;
-                if (r1 != ncclSuccess || r2 != ncclSuccess) { (void)ncclGroupEnd(); NCCLCHK(r1 != ncclSuccess ? r1 : r2); }
             }
         }
-        NCCLCHK(ncclGroupEnd());
+        if ((rc = xp_group_end(c))) return rc;
     }
     W.ops = ops;
     W.n_ops = n;
@@ -509,9 +506,8 @@ int gw_world_status(gw_ctx* c, uint64_t* overflow, uint64_t* conflicts, uint64_t
     if (!c) return GW_EINVAL;
     if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
-    if (c->comm && c->c_nranks > 1) {
-        // the three counters are the first three u64 of HaloStats
-        NCCLCHK(ncclAllReduce(c->halo, c->halo, 3, ncclUint64, ncclSum, c->comm, c->st));
+    if (xp_on(c) && c->c_nranks > 1) {                // the three counters are the first three u64 of HaloStats
+        if (int rc = xp_allreduce_u64(c, (unsigned long long*)c->halo, 3, GW_RED_SUM)) return rc;
     }
     HaloStats h{};
     HIPCHK(hipMemcpyAsync(&h, c->halo, sizeof h, hipMemcpyDeviceToHost, c->st));

@@ -440,3 +440,121 @@ class LocalWorld:
         self.bufs = []
         for g in self.g:
             g.close()
+
+
+class _RankThread:
+    """A persistent host thread driving one rank's context (a rank process
+    drives its context from one thread; the library's calls on it are
+    blocking and release the GIL, so the R threads run their calls
+    concurrently)."""
+
+    def __init__(self, r):
+        import queue
+        import threading
+        self.q_in, self.q_out = queue.Queue(), queue.Queue()
+        self.t = threading.Thread(target=self._loop, name=f"gw-rank-{r}", daemon=True)
+        self.t.start()
+
+    def _loop(self):
+        while True:
+            job = self.q_in.get()
+            if job is None:
+                return
+            fn, args = job
+            try:
+                self.q_out.put((True, fn(*args)))
+            except BaseException as e:            # handed to the caller of run()
+                self.q_out.put((False, e))
+
+    def stop(self):
+        self.q_in.put(None)
+        self.t.join(timeout=30)
+
+
+class LoopbackWorld:
+    """R strip contexts of one decomposed world in ONE process, each driven by
+    its own host thread through gw_world_step over the library's loopback
+    transport (gw_comm_init_local): the exact call sequence R rank processes
+    run over RCCL (route, count round, host read of the counts, far-count
+    all-gather at R >= 3, exact-size rows and far rows, queue), with the bytes
+    moved by copies between the contexts on the one device.  run(fn) calls
+    fn(r, g) on every rank's thread at once and returns the R results."""
+
+    def __init__(self, geom: Strips, n_global: int, bounds, device: int = 0, gates=None):
+        from . import gpuaoi
+        self.R, self.geom, self.n = geom.ranks, geom, n_global
+        self.g = [gpuaoi.GpuAOI(device) for _ in range(self.R)]
+        self.th = []
+        try:
+            for r, g in enumerate(self.g):
+                lo, hi = geom.ext(r)
+                b = (max(lo, bounds[0]), bounds[1], min(hi, bounds[2]), bounds[3])
+                g.world_create(geom.x0, geom.w, geom.d, geom.max_step, self.R, r, n_global, b)
+                g.set_clients(np.arange(n_global, dtype=np.uint32),
+                              np.ones(n_global, np.uint16) if gates is None else gates)
+            gpuaoi.comm_init_local(self.g)
+            self.th = [_RankThread(r) for r in range(self.R)]
+        except BaseException:
+            self.close()
+            raise
+        self.bufs = []
+
+    def run(self, fn, *args):
+        for r, th in enumerate(self.th):
+            th.q_in.put((fn, (r, self.g[r]) + args))
+        out, err = [], None
+        for th in self.th:                          # every rank's result, then the first error
+            ok, v = th.q_out.get()
+            out.append(v if ok else None)
+            if not ok and err is None:
+                err = v
+        if err is not None:
+            raise err
+        return out
+
+    def upload(self, r, ops) -> int:
+        """ops (gw_op array) of rank r into device memory (kept until close); returns the pointer."""
+        ops = np.ascontiguousarray(ops)
+        p = self.g[r].dev_alloc(max(ops.nbytes, 64))
+        if ops.nbytes:
+            self.g[r].h2d(p, ops)
+        self.bufs.append((r, p))
+        return p
+
+    def load(self, x0, z0, yaw0, chunk: int = 1 << 21):
+        """Every rank enters the entities it owns (routed to its neighbours as
+        ghosts) through gw_world_step, no events, in the same number of chunks."""
+        from . import traces
+        owner0 = self.geom.owner(x0)
+        n_chunks = max(1, -(-int(np.bincount(owner0, minlength=self.R).max()) // chunk))
+        ptrs = []
+        for r in range(self.R):
+            mine = np.nonzero(owner0 == r)[0].astype(np.uint32)
+            ops = traces.enter_ops(mine, x0[mine], np.zeros(len(mine), np.float32), z0[mine], yaw0[mine])
+            ptrs.append([(self.upload(r, ops[k * chunk:(k + 1) * chunk]), len(ops[k * chunk:(k + 1) * chunk]))
+                         for k in range(n_chunks)])
+
+        def one(r, g):
+            for p, m in ptrs[r]:
+                g.world_step(p, m)
+                g.tick(copy=False, no_events=True)
+            g.sync_collect(copy=False)
+        self.run(one)
+
+    def check(self):
+        """Contract counters summed over the ranks (gw_world_status is a collective)."""
+        st = self.run(lambda r, g: g.world_status())
+        ov, conflicts, bad_ops = st[0]
+        if ov or conflicts or bad_ops:
+            raise RuntimeError(f"world contract counters: overflow {ov}, conflicts {conflicts}, bad ops {bad_ops}")
+
+    def close(self):
+        for th in self.th:
+            th.stop()
+        self.th = []
+        for r, p in getattr(self, "bufs", []):
+            self.g[r].dev_free(p)
+        self.bufs = []
+        for g in self.g:
+            g.close()
+        self.g = []

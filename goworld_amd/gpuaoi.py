@@ -156,6 +156,7 @@ def lib():
         L.gw_comm_unique_id.argtypes = [vp]
         L.gw_comm_init.argtypes = [vp, vp, C.c_int, C.c_int]
         L.gw_comm_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.gw_comm_init_local.argtypes = [C.POINTER(vp), C.c_int]
         L.gw_comm_exchange.argtypes = [vp, C.POINTER(Xfer), _u32]
         L.gw_comm_allreduce_u64.argtypes = [vp, vp, _u32, C.c_int]
         L.gw_world_create.argtypes = [vp, C.POINTER(WorldGeom), _u32, vp, C.POINTER(_u32)]
@@ -188,7 +189,16 @@ EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_spa
             "gw_world_submit", "gw_world_status", "gw_set_entity_ids", "gw_clear_entity_ids", "gw_set_client_ids",
             "gw_set_client_syncing", "gw_submit_client_sync", "gw_sync_encode_wire", "gw_space_grow",
             "gw_context_info", "gw_world_far", "gw_world_submit_far", "gw_world_stage_ops",
-            "gw_world_step_host"]
+            "gw_world_step_host", "gw_comm_init_local"]
+
+
+def comm_init_local(ctxs) -> None:
+    """gw_comm_init_local: the GpuAOI contexts of this process become ranks 0..n-1
+    of a loopback group (each then driven by its own thread, as a rank process)."""
+    arr = (C.c_void_p * len(ctxs))(*[g._h.value for g in ctxs])
+    rc = lib().gw_comm_init_local(arr, len(ctxs))
+    if rc:
+        raise GwError(rc, lib().gw_last_error(ctxs[0]._h).decode(errors="replace") if ctxs else "")
 
 
 def comm_unique_id() -> bytes:

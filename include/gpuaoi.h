@@ -464,6 +464,16 @@ int  gw_sync_encode_wire(gw_ctx* ctx, uint32_t flags, gw_wire_out* out);
 int  gw_comm_unique_id(void* id /* GW_COMM_ID_BYTES */);
 int  gw_comm_init(gw_ctx* ctx, const void* id, int nranks, int rank);
 int  gw_comm_info(gw_ctx* ctx, int* nranks, int* rank);      /* 0 ranks: no communicator */
+/* Loopback communicator: the nranks contexts of ONE process become ranks
+ * 0..nranks-1 of a group whose collectives copy between their buffers
+ * (hipMemcpyAsync on the contexts' streams) with the semantics of the RCCL
+ * path - same calls, same matching, same ordering.  Each context is then
+ * driven by its own host thread exactly as a rank process drives its own
+ * (gw_world_step / gw_comm_exchange block until the peers' matching calls
+ * are issued; a peer that never issues them fails the call after
+ * GW_LOOPBACK_TIMEOUT_S seconds, default 120).  For running the multi-rank
+ * world sequence on one device; the contexts may share it. */
+int  gw_comm_init_local(gw_ctx* const* ctxs, int nranks);
 
 /* One transfer of a grouped point-to-point exchange (bytes, device memory). */
 typedef struct gw_xfer {
@@ -547,7 +557,7 @@ int  gw_world_submit_far(gw_ctx* ctx, const gw_halo_row* rows, uint32_t n_rows);
 int  gw_world_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* conflicts, uint64_t* bad_ops);
 
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 13
+#define GW_ABI_VERSION 14
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version_and_layouts():
-    assert gpuaoi.lib().gw_abi_version() == 13
+    assert gpuaoi.lib().gw_abi_version() == 14
     assert ctypes.sizeof(gpuaoi.CtxInfo) == 24
     assert ctypes.sizeof(gpuaoi.WireOut) == 7 * 8
     assert ctypes.sizeof(gpuaoi.Xfer) == 40 and ctypes.sizeof(gpuaoi.WorldGeom) == 24

@@ -9,19 +9,22 @@ position/yaw records).
 
 N=1 (default): BASELINE config #3, the 1M-entity clustered-hotspot space the
 metric is quoted on, on one GPU.
-N>1 (default --mode spaces): an independent 1M-entity config #3 space per GPU
-(seed 3 + rank), no data-path collective (weak scaling).  A space never spans
-processes in the reference (engine/entity/SpaceManager.go:11-31): the path
-partitions by space, so it shards with no exchange.
-Two strong-scaling legs ride along in every N>1 line:
-  "c3world": the SAME 1M-entity space decomposed into N X-strips, one per GPU
-  (goworld_amd/dworld.py over the library's gw_world_* path): each tick every
-  rank routes its owned ops, exchanges halo rows with both neighbours over RCCL
-  inside the library (xGMI) and ticks its strip; walkers cross strip borders;
+N>1 (default --mode world): the SAME 1M-entity space decomposed into N
+X-strips, one per GPU (strong scaling; goworld_amd/dworld.py over the
+library's gw_world_* path): each tick every rank routes its owned ops,
+exchanges halo rows with both neighbours (and far rows of long moves) over
+RCCL inside the library (xGMI) and ticks its strip; walkers cross borders.
+Two legs ride along in every N>1 line:
+  "spaces": an independent 1M-entity config #3 space per GPU (seed 3 + rank),
+  no data-path collective (weak scaling: a space never spans processes in the
+  reference, engine/entity/SpaceManager.go:11-31, so that is how it shards);
   "config5": the north star's 16M-entity world decomposed over the same N GPUs
-  (also measured at N=1).  --no-config5 / --no-c3world skip them.
---mode world: the decomposed 1M space as the headline (strong scaling).
+  (also measured at N=1).  --no-spaces-leg / --no-config5 skip them.
+--mode spaces: the weak line as the headline ("c3world" rides along).
 --config 4 / 5: BASELINE config #4 (10k spaces x 1k) / #5 as the headline.
+--comm loopback --gpus N: the world's N ranks as N threads of ONE process on
+one device (the library's loopback transport, the RCCL path's exact call
+sequence): a rehearsal of the multi-rank path, not a scaling number.
 
 Inputs (ops of every tick) are resident in HBM before the timed region;
 outputs stay in HBM (device-resident boundary); t_e2e reports the host-in /
@@ -72,11 +75,13 @@ def parse():
     ap.add_argument("--profile-stages", type=int, default=1,
                     help="1: HIP events around the dominant kernel's stage in the timed region (roofline) and "
                          "a per-stage breakdown over extra untimed steps; 0: none")
-    ap.add_argument("--mode", choices=["world", "spaces"], default="spaces",
-                    help="N>1 with config 3: spaces = an independent 1M space per GPU, no comm (weak; default); "
-                         "world = the 1M space decomposed over the N GPUs (strong)")
+    ap.add_argument("--mode", choices=["world", "spaces"], default="world",
+                    help="N>1 with config 3: world = the metric's 1M space decomposed over the N GPUs (strong; "
+                         "default); spaces = an independent 1M space per GPU, no comm (weak)")
     ap.add_argument("--no-c3world", dest="c3world", action="store_false",
                     help="N>1, --mode spaces: skip the extra strong-scaling leg of the 1M space decomposed over N GPUs")
+    ap.add_argument("--no-spaces-leg", dest="spaces_leg", action="store_false",
+                    help="N>1, --mode world: skip the weak-scaling leg (an independent 1M space per GPU)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / control-plane rehearsal: ranks, barriers and the max-over-ranks timing with no "
                          "GPU work (CPU tests)")
@@ -85,9 +90,11 @@ def parse():
                          "4: config #4, 10k independent 1k-entity spaces, space s on GPU s mod N (strong); "
                          "5: the 16M uniform world of config #5 over N strips (strong)")
     ap.add_argument("--spaces", type=int, default=10_000, help="config #4: number of spaces")
-    ap.add_argument("--comm", choices=["rccl", "gloo"], default="rccl",
-                    help="halo exchange: RCCL inside the library (gw_world_step) or gloo (rehearsal of several "
-                         "ranks on one GPU)")
+    ap.add_argument("--comm", choices=["rccl", "gloo", "loopback"], default="rccl",
+                    help="halo exchange: RCCL inside the library (gw_world_step, one process per GPU); gloo "
+                         "(rank processes sharing one GPU, rows through the host); loopback (ONE process, --gpus N "
+                         "rank threads on --device, gw_world_step over the library's loopback transport: the "
+                         "multi-rank call sequence on one GPU, not a scaling number)")
     ap.add_argument("--world-entities", type=int, default=16_000_000, help="config #5 world population")
     ap.add_argument("--no-config5", dest="config5", action="store_false",
                     help="skip the extra config #5 (16M decomposed world) measurement")
@@ -159,7 +166,7 @@ def launch(a):
                   file=sys.stderr)
             return 2
         return None
-    if a.gpus == 1:
+    if a.gpus == 1 or a.comm == "loopback":        # loopback: the N ranks are threads of this process
         return None
     import signal
     import socket
@@ -460,14 +467,36 @@ class ManySpacesRun(SpaceRun):
         self.tr = None
 
 
+def world_workload(a, ticks, which):
+    """The world legs' population and walk: which = "c3", the metric's 1M
+    clustered space as one world (steps +-4, hotspots +-16); "c5", config #5's
+    16M uniform world (L = 131072, +-4).  Returns (n, side, max_step, x0, z0,
+    yaw0, ticks) with ticks a generator of (ops, x before the tick): every rank
+    regenerates the same walk and keeps the ops of the entities it owns at the
+    start of each tick."""
+    if which == "c5":
+        n, side, max_step = a.world_entities, 131072.0, 4.0
+        walk = traces.WorldWalk(seed=5, n=n, side=side)
+        return n, side, max_step, walk.x(), walk.z(), walk.yaw.copy(), (walk.next_tick() for _ in range(ticks))
+    n, side, max_step = a.entities, a.side, 16.0
+    tr = traces.config3(ticks=ticks, seed=3, n=n, side=side)
+    xcur = tr.init_x.copy()
+
+    def gen3():
+        for ops in tr.ticks:
+            xb = xcur[ops["slot"]].copy()
+            xcur[ops["slot"]] = ops["x"]
+            yield ops, xb
+    return n, side, max_step, tr.init_x, tr.init_z, tr.init_yaw, gen3()
+
+
 class WorldRun:
     """One world decomposed into N X-strips, one per GPU (dworld.StripRank over
     the library's gw_world_* path; halo rows over RCCL inside the library).
     which = "c3": the metric's 1M-entity clustered space (config #3) as one
     world over N strips; "c5": config #5, the 16M uniform world (L = 131072).
     Both walks are global: entities cross strip borders and migrate between
-    ranks; every rank regenerates the same walk and keeps the ops of the
-    entities it owns at the start of each tick."""
+    ranks (world_workload)."""
 
     def __init__(self, a, ctl, ticks, which):
         import torch
@@ -476,23 +505,7 @@ class WorldRun:
         dev = torch.device("cuda", ctl.local)
         torch.cuda.set_device(dev)
         ws, r = ctl.ws, ctl.rank
-        if which == "c5":
-            n, side, max_step = a.world_entities, 131072.0, 4.0
-            walk = traces.WorldWalk(seed=5, n=n, side=side)
-            x0_all, z0_all, yaw0 = walk.x(), walk.z(), walk.yaw.copy()
-            gen = (walk.next_tick() for _ in range(ticks))
-        else:
-            n, side, max_step = a.entities, a.side, 16.0         # config #3 steps: +-4, hotspots +-16
-            tr = traces.config3(ticks=ticks, seed=3, n=n, side=side)
-            x0_all, z0_all, yaw0 = tr.init_x, tr.init_z, tr.init_yaw
-            xcur = tr.init_x.copy()
-
-            def gen3():
-                for ops in tr.ticks:
-                    xb = xcur[ops["slot"]].copy()
-                    xcur[ops["slot"]] = ops["x"]
-                    yield ops, xb
-            gen = gen3()
+        n, side, max_step, x0_all, z0_all, yaw0, gen = world_workload(a, ticks, which)
         geom = dworld.Strips(-side / 2, side / ws, ws, 100.0, max_step)
         lo, hi = geom.ext(r)
         bounds = (max(lo, -side / 2), -side / 2, min(hi, side / 2), side / 2)
@@ -530,6 +543,7 @@ class WorldRun:
         self.parallelism = (f"decomposed world, {ws} X-strips of {side / ws:g} x {side:g}, halo rows over "
                             f"{'RCCL (gw_world_step)' if comm == 'rccl' else 'gloo'}" if ws > 1
                             else "single GPU, one-strip world")
+        self.ranks = ws
         self.tr = None
 
     def step(self, t):
@@ -544,6 +558,85 @@ class WorldRun:
     def close(self):
         self.sr.check()
         self.g.close()
+
+
+class _Sum:
+    """Counters of one step summed over the loopback ranks (TickOut / SyncOut fields measure() reads)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+class _RanksG:
+    """measure()'s view of the loopback ranks' contexts: every call on all of
+    them (stage times: per stage the slowest rank)."""
+
+    def __init__(self, lw):
+        self.lw = lw
+
+    def synchronize(self):
+        for g in self.lw.g:
+            g.synchronize()
+
+    def set_profiling(self, mode):
+        for g in self.lw.g:
+            g.set_profiling(mode)
+
+    def stage_times(self):
+        best = {}
+        for g in self.lw.g:
+            for name, us, b, calls in g.stage_times():
+                if name not in best or us / max(calls, 1) > best[name][0] / max(best[name][2], 1):
+                    best[name] = (us, b, calls)
+        return [(k, *v) for k, v in best.items()]
+
+
+class LoopbackWorldRun:
+    """--comm loopback: the world of world_workload decomposed into --gpus R
+    X-strips whose R contexts live in THIS process on one device, each rank
+    driven by its own thread through gw_step (gw_world_step over the library's
+    loopback transport: the count round, host read, far all-gather and exact
+    rows of the RCCL path, bytes copied between the contexts; dworld.
+    LoopbackWorld).  The R ranks share one GPU, so the time is not a scaling
+    number; the line shows the multi-rank path running end to end."""
+
+    def __init__(self, a, ticks, which):
+        from goworld_amd import dworld
+        R = a.gpus
+        n, side, max_step, x0_all, z0_all, yaw0, gen = world_workload(a, ticks, which)
+        geom = dworld.Strips(-side / 2, side / R, R, 100.0, max_step)
+        dev = a.device if a.device is not None else 0
+        self.lw = lw = dworld.LoopbackWorld(geom, n, (-side / 2, -side / 2, side / 2, side / 2), device=dev)
+        lw.load(x0_all, z0_all, yaw0)
+        self.ptrs, self.m_ticks = [], []
+        for ops, xb in gen:
+            own = geom.owner(xb)
+            mine = [ops[own == r] for r in range(R)]
+            self.ptrs.append([(lw.upload(r, mine[r]), len(mine[r])) for r in range(R)])
+            self.m_ticks.append(sum(len(x) for x in mine))
+        self.g = _RanksG(lw)
+        self.n_world, self.ranks = n, R
+        self.m = int(np.mean(self.m_ticks) / R)          # per rank
+        self.parallelism = (f"decomposed world, {R} X-strips of {side / R:g} x {side:g}, {R} rank threads on "
+                            f"device {dev}, halo rows over the loopback transport (gw_world_step); the ranks share "
+                            f"one GPU: not a scaling number")
+        self.tr = None
+
+    def step(self, t):
+        ptrs = self.ptrs[t]
+
+        def one(r, g):
+            to, so = g.step_device(*ptrs[r])
+            return (to.n_enter, to.n_leave, to.bytes_alg, to.nbr_old, to.nbr_new, to.pairs_tested, so.n_rec,
+                    so.bytes_alg)
+        v = np.array(self.lw.run(one), np.float64).sum(axis=0)
+        r = _Sum(n_enter=int(v[0]), n_leave=int(v[1]), bytes_alg=int(v[2]), nbr_old=int(v[3]), nbr_new=int(v[4]),
+                 pairs_tested=int(v[5]))
+        return self.m_ticks[t], r, _Sum(n_rec=int(v[6]), bytes_alg=int(v[7]))
+
+    def close(self):
+        self.lw.check()
+        self.lw.close()
 
 
 def client_msgs(run, t0, n):
@@ -681,6 +774,8 @@ def main():
         dry_run(a, ctl)
         return
     ws, rank = ctl.ws, ctl.rank
+    loop = a.comm == "loopback" and a.gpus > 1   # the N ranks are threads of this process on one device
+    R = a.gpus if loop else ws                    # ranks of the run
     extra = 5 if a.profile_stages else 0         # untimed steps for the per-stage breakdown
     if a.config == 2:
         kind = "c2"                                 # config #2 (100k uniform), one space per GPU
@@ -688,12 +783,18 @@ def main():
         kind = "c4"
     elif a.config == 5:
         kind = "c5"
-    elif ws > 1 and a.mode == "world":
-        kind = "c3world"                            # the metric's 1M space decomposed over the N GPUs
+    elif R > 1 and (a.mode == "world" or loop):
+        kind = "c3world"                            # the metric's 1M space decomposed over the N GPUs (default)
     else:
-        kind = "c3"                                 # N=1: the 1M space on one GPU (a one-strip world)
-    c3world_leg = a.c3world and ws > 1 and kind == "c3"   # the 1M space decomposed, beside the weak line
-    if kind in ("c5", "c3world") or (a.config5 and kind in ("c3", "c3world")) or c3world_leg:
+        kind = "c3"                                 # N=1: the 1M space on one GPU
+    if loop and kind not in ("c3world", "c5"):
+        print("bench.py: --comm loopback runs a decomposed world (config 3 --mode world, or --config 5)",
+              file=sys.stderr)
+        sys.exit(2)
+    c3world_leg = a.c3world and R > 1 and kind == "c3"   # --mode spaces: the 1M space decomposed, beside it
+    spaces_leg = a.spaces_leg and R > 1 and kind == "c3world" and not loop   # the weak line, beside the world
+    c5_leg = a.config5 and kind in ("c3", "c3world") and not loop
+    if not loop and (kind in ("c5", "c3world") or c5_leg or c3world_leg):
         # torch (decomposed-world runs) brings its own HIP runtime: it must
         # initialise before the library's runtime does, in this process
         import torch
@@ -706,10 +807,9 @@ def main():
     t_load = time.perf_counter()
     if kind == "c4":
         run = ManySpacesRun(a, ctl, ticks)
-    elif kind == "c5":
-        run = WorldRun(a, ctl, ticks, "c5")
-    elif kind == "c3world":
-        run = WorldRun(a, ctl, ticks, "c3")
+    elif kind in ("c5", "c3world"):
+        which = "c5" if kind == "c5" else "c3"
+        run = LoopbackWorldRun(a, ticks, which) if loop else WorldRun(a, ctl, ticks, which)
     else:
         run = SpaceRun(a, ctl, ticks)
     t_load = time.perf_counter() - t_load
@@ -781,16 +881,29 @@ def main():
                                  or {}).get("frac")}
         runw.close()
         return leg
-    # the metric's 1M space decomposed over the same N GPUs (strong), beside the weak headline
+    # --mode spaces: the metric's 1M space decomposed over the same N GPUs (strong), beside the weak headline
     c3w = None
     if c3world_leg:
         c3w = world_leg("c3", W, K, (
             f"config #3 as one world: the 1M-entity clustered space decomposed into {ws} X-strips of "
             f"{a.side / ws:g}, one per GPU (walkers cross strip borders); step = route + RCCL halo exchange + "
             f"gw_tick + gw_sync_collect on every rank"))
+    # --mode world (default): an independent 1M config #3 space per GPU (weak, no collective), beside it
+    spc = None
+    if spaces_leg:
+        runs = SpaceRun(a, ctl, W + K)
+        rs = measure(runs, a, ctl, W, K, False, 0)
+        spc = {"workload": (f"config #3: an independent 1M-entity space per GPU (seed 3 + rank), {ws} GPUs, no "
+                            f"collective; step = gw_tick + gw_sync_collect"),
+               "value": rs["sum_ops"] / rs["max_elapsed"], "unit": "updates/s",
+               "events_per_sec": rs["sum_events"] / rs["max_elapsed"],
+               "records_per_sec": rs["sum_records"] / rs["max_elapsed"],
+               "ms_per_step": rs["max_elapsed"] / K * 1e3, "steps": K, "warmup": W, "scaling": "weak",
+               "n_gpus": ws, "parallelism": runs.parallelism}
+        runs.close()
     # the north star's 16M decomposed world (config #5) at the same N, strong scaling
     c5 = None
-    if a.config5 and kind in ("c3", "c3world"):
+    if c5_leg:
         c5 = world_leg("c5", a.warmup5, a.steps5, (
             "config #5: one 16M-entity uniform world space, L = 131072, AOI distance 100, 10% movers "
             f"per tick (+-4; walkers cross strip borders), decomposed into {ws} X-strip(s); step = "
@@ -813,8 +926,10 @@ def main():
     elif kind == "c3world":
         workload = (f"config #3 as one world: the 1M-entity clustered space (70% uniform + 30% in 64 Gaussian "
                     f"hotspots, sigma 200; 10% movers per tick, +-4 / hotspot +-16; AOI distance 100; world "
-                    f"32768^2) decomposed into {ws} X-strips of {a.side / ws:g}, one per GPU (walkers cross "
-                    f"strip borders); step = route + RCCL halo exchange + gw_tick + gw_sync_collect")
+                    f"32768^2) decomposed into {R} X-strips of {a.side / R:g}, "
+                    + (f"{R} rank threads on one GPU (loopback transport)" if loop else "one per GPU")
+                    + " (walkers cross strip borders); step = route + "
+                    + ("loopback" if loop else "RCCL") + " halo exchange + gw_tick + gw_sync_collect on every rank")
     else:
         workload = ("config #3: single AOI space per GPU, 1M entities, 70% uniform + 30% in 64 "
                     "Gaussian hotspots (sigma 200), 10% movers per tick (+-4 / hotspot +-16), "
@@ -826,6 +941,7 @@ def main():
         "value": res["sum_ops"] / mx,
         "unit": "updates/s",
         "n_gpus": ws,
+        "ranks": R,
         "steps": K,
         "warmup": W,
         "ms_per_step": mx / K * 1e3,
@@ -834,7 +950,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #{cfg_no})",
-        "config": {"workload": workload, "world_entities": n_world, "entities_per_gpu": n_world // ws,
+        "config": {"workload": workload, "world_entities": n_world, "entities_per_gpu": n_world // R,
                    "movers_per_tick_per_gpu": m_rank, "aoi_dist": 100.0,
                    "world_side": {2: 10240.0, 4: 1024.0, 5: 131072.0}.get(cfg_no, a.side), "gates": 1,
                    "parallelism": parallelism},
@@ -851,8 +967,12 @@ def main():
         line["t_device_ms_per_step"] = mx / K * 1e3
     if client:
         line["client_msgs"] = client
+    if loop:
+        line["comm"] = "loopback"
     if c3w:
         line["c3world"] = c3w
+    if spc:
+        line["spaces"] = spc
     if c5:
         line["config5"] = c5
     if not a.no_cpu_baseline and ws == 1 and kind == "c3":

@@ -467,6 +467,19 @@ int validate_ops(gw_ctx* c, const gw_op* ops, uint32_t n) {
 
 }  // namespace
 
+namespace gw {
+namespace host {
+int space_idx(gw_ctx* c, uint32_t h, uint32_t* idx) {
+    const uint32_t i = h & SID_MASK;
+    if (i >= c->spaces.size() || !c->spaces[i].alive) return set_err(c, GW_ERANGE, "no space %u", h);
+    if ((h >> SID_BITS) != (c->spaces[i].gen & SID_GEN_MASK))
+        return set_err(c, GW_ERANGE, "space id %u is stale (that space was destroyed)", h);
+    *idx = i;
+    return 0;
+}
+}  // namespace host
+}  // namespace gw
+
 // =========================================================================
 extern "C" {
 
@@ -615,6 +628,8 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
     // a destroyed space's id is handed out again (lowest first)
     uint32_t sid = 0;
     while (sid < c->spaces.size() && c->spaces[sid].alive) ++sid;
+    if (sid > SID_MASK) return set_err(c, GW_ERANGE, "too many spaces");
+    if (sid < c->spaces.size()) s.gen = c->spaces[sid].gen;   // the destroyed space's next generation
     if ((rc = init_space_slots(c, base, capacity, sid))) return rc;
     (void)take_range(c->free_slots, c->total_slots, capacity, true, &nt_slots);
     (void)take_range(c->free_cells, c->total_cells, (uint32_t)ncells, true, &nt_cells);
@@ -630,17 +645,18 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
         c->present_h[base + i] = 0;
     }
     if ((rc = upload_spaces(c))) return rc;
-    if (space_id) *space_id = sid;
+    if (space_id) *space_id = sid_handle(c->spaces[sid], sid);
     if (slot_base) *slot_base = base;
     return 0;
 }
 
-int gw_space_restore(gw_ctx* c, uint32_t sid, const uint32_t* slots, const float* x, const float* y,
+int gw_space_restore(gw_ctx* c, uint32_t sid_h, const uint32_t* slots, const float* x, const float* y,
                      const float* z, const float* yaw, uint32_t n, uint8_t sync_flags) {
     if (!c || (n && (!slots || !x || !y || !z || !yaw))) return GW_EINVAL;
     if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
-    if (sid >= c->spaces.size() || !c->spaces[sid].alive) return set_err(c, GW_ERANGE, "no space %u", sid);
+    uint32_t sid = 0;
+    if (int rs = space_idx(c, sid_h, &sid)) return rs;
     if (!c->segs.empty()) return set_err(c, GW_ESTATE, "restore with ops pending: tick first");
     if (!n) return 0;
     const SpaceHost& sp = c->spaces[sid];
@@ -716,11 +732,12 @@ static void move_host_slots(gw_ctx* c, uint32_t base, uint32_t n, int64_t to) {
 // device: destroying a space that still holds an entity is an error.  Its
 // slot and cell ranges are cleared (pending sync flags of entities that left
 // it into the nil space go with them: collect first) and reused.
-int gw_space_destroy(gw_ctx* c, uint32_t sid) {
+int gw_space_destroy(gw_ctx* c, uint32_t sid_h) {
     if (!c) return GW_EINVAL;
     if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
-    if (sid >= c->spaces.size() || !c->spaces[sid].alive) return set_err(c, GW_ERANGE, "no space %u", sid);
+    uint32_t sid = 0;
+    if (int rs = space_idx(c, sid_h, &sid)) return rs;
     if (!c->segs.empty()) return set_err(c, GW_ESTATE, "space destroy with ops pending: tick first");
     SpaceHost& s = c->spaces[sid];
     if (c->wd.on && sid == c->wd.sid) return set_err(c, GW_ESTATE, "space %u is the context's world strip", sid);
@@ -736,6 +753,7 @@ int gw_space_destroy(gw_ctx* c, uint32_t sid) {
     give_range(c->free_cells, c->total_cells, s.p.cell_base, (uint32_t)(s.p.W * s.p.H));
     s.alive = false;
     s.p.alive = 0;
+    ++s.gen;
     c->grid_dirty = true;
     ++c->epoch;
     return upload_spaces(c);
@@ -745,11 +763,12 @@ int gw_space_destroy(gw_ctx* c, uint32_t sid) {
 // in place when the slots behind the space are free, else the space's state
 // moves to a new range (its slots change: new_base; events and records of
 // later calls carry the new slots).  No ops may be pending.
-int gw_space_grow(gw_ctx* c, uint32_t sid, uint32_t new_capacity, uint32_t* new_base) {
+int gw_space_grow(gw_ctx* c, uint32_t sid_h, uint32_t new_capacity, uint32_t* new_base) {
     if (!c) return GW_EINVAL;
     if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
-    if (sid >= c->spaces.size() || !c->spaces[sid].alive) return set_err(c, GW_ERANGE, "no space %u", sid);
+    uint32_t sid = 0;
+    if (int rs = space_idx(c, sid_h, &sid)) return rs;
     if (!c->segs.empty()) return set_err(c, GW_ESTATE, "space grow with ops pending: tick first");
     SpaceHost& s = c->spaces[sid];
     if (new_capacity < s.cap) return set_err(c, GW_EINVAL, "capacity %u below the current %u", new_capacity, s.cap);
@@ -894,10 +913,11 @@ int gw_halo_status(gw_ctx* c, uint64_t* overflow, uint64_t* long_moves, uint64_t
     return 0;
 }
 
-int gw_space_set_ownership(gw_ctx* c, uint32_t sid, float x_lo, float x_hi) {
+int gw_space_set_ownership(gw_ctx* c, uint32_t sid_h, float x_lo, float x_hi) {
     if (!c) return GW_EINVAL;
     if (int rs = settle(c)) return rs;
-    if (sid >= c->spaces.size() || !c->spaces[sid].alive) return set_err(c, GW_ERANGE, "no space %u", sid);
+    uint32_t sid = 0;
+    if (int rs = space_idx(c, sid_h, &sid)) return rs;
     if (!(x_lo < x_hi)) return set_err(c, GW_EINVAL, "empty ownership range");
     c->spaces[sid].p.own_lo = x_lo;
     c->spaces[sid].p.own_hi = x_hi;

@@ -26,7 +26,15 @@ struct SpaceHost {
     uint32_t cap, base;
     SpaceP p;
     bool alive;
+    uint32_t gen = 0;     // bumped by each destroy: a handle of the destroyed space no longer matches
 };
+// A space id handed to the caller: index | generation << SID_BITS.  A
+// destroyed space's index is reused with the next generation, so a stale id
+// (late destroy / grow / restore / set_ownership) is refused, never applied to
+// the space that took its index (upstream spaces are keyed by unique EntityIDs,
+// SpaceManager.go:21-27).
+constexpr uint32_t SID_BITS = 20, SID_MASK = (1u << SID_BITS) - 1, SID_GEN_MASK = (1u << (32 - SID_BITS)) - 1;
+inline uint32_t sid_handle(const SpaceHost& s, uint32_t idx) { return idx | ((s.gen & SID_GEN_MASK) << SID_BITS); }
 
 struct OpSeg {            // submission order of a tick: host or device segment
     bool host;
@@ -270,6 +278,7 @@ int ensure(gw_ctx* c, DevBuf& b, size_t bytes);
 int ensure_host(gw_ctx* c, DevBuf& b, size_t bytes);
 int settle(gw_ctx* c);
 int next_ol_tag(gw_ctx* c, uint32_t* tag);
+int space_idx(gw_ctx* c, uint32_t handle, uint32_t* idx);   // a live space's index from its id (GW_ERANGE if stale)
 World world_of(gw_ctx* c);
 template <typename T>
 T* P(DevBuf& b) { return (T*)b.p; }

@@ -254,7 +254,7 @@ int gw_world_create(gw_ctx* c, const gw_world_geom* g, uint32_t capacity, const 
     W.far_off_h.assign(g->ranks, 0);
     W.far_mat_h.assign((size_t)g->ranks * g->ranks, 0);
     W.far_cap = 0;
-    W.sid = sid;
+    W.sid = sid & SID_MASK;
     W.tick = 0;
     W.on = true;
     if (space_id) *space_id = sid;

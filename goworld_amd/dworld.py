@@ -334,11 +334,12 @@ class StripRank:
 
     def check(self):
         """Host check of the contract counters (one sync; call outside timed loops)."""
-        ov, bad, bad_ops = self.e.status()
+        ov, conflicts, bad_ops = self.e.status()
         if ov > 0:
             raise RuntimeError(f"halo buffers overflowed by {ov} entities")
-        if bad:
-            raise RuntimeError(f"{bad} owned entities moved more than max_step in one tick")
+        if conflicts:
+            raise RuntimeError(f"{conflicts} long-move conflicts (pairs of related entities that both moved more "
+                               f"than max_step in one tick)")
         if bad_ops:
             raise RuntimeError(f"{bad_ops} ops with an invalid slot or kind")
 

@@ -61,15 +61,39 @@ def test_torchrun_ranks():
     assert line["n_gpus"] == 2 and line["ranks_reporting"] == 2
 
 
+_SMALL = ["--entities", "100000", "--steps", "3", "--warmup", "2", "--no-config5", "--no-cpu-baseline",
+          "--profile-stages", "0", "--client-msgs", "0", "--e2e-steps", "0"]
+
+
 @pytest.mark.gpu
 def test_launcher_two_ranks_on_one_gpu():
     """Two real ranks (independent spaces, weak) plus the decomposed-world leg
     over gloo, both on device 0 (RCCL needs one GPU per rank)."""
-    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--device", "0", "--comm", "gloo",
-                        "--entities", "100000", "--steps", "3", "--warmup", "2", "--no-config5",
-                        "--no-cpu-baseline", "--profile-stages", "0", "--client-msgs", "0", "--e2e-steps", "0"],
-                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=110)
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--device", "0", "--comm", "gloo", "--mode", "spaces"]
+                       + _SMALL, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-3000:]
     line = _line(p.stdout)
     assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["value"] > 0
     assert line["c3world"]["n_gpus"] == 2 and line["c3world"]["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_loopback_world_line():
+    """--comm loopback: the default N > 1 headline (the 1M space decomposed
+    into N strips, strong) with its N ranks as threads of one process on the
+    one GPU, every step through gw_step -> gw_world_step over the loopback
+    transport (the RCCL path's call sequence); also the world headline of two
+    gloo rank processes with the weak spaces leg beside it."""
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "3", "--device", "0", "--comm", "loopback"] + _SMALL
+                       + ["--profile-stages", "1"],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = _line(p.stdout)
+    assert line["ranks"] == 3 and line["comm"] == "loopback" and line["scaling"] == "strong"
+    assert line["value"] > 0 and line["events_per_sec"] > 0 and line["roofline"]["frac"] > 0
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--device", "0", "--comm", "gloo"] + _SMALL,
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = _line(p.stdout)
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["value"] > 0
+    assert line["spaces"]["scaling"] == "weak" and line["spaces"]["value"] > 0

@@ -158,7 +158,8 @@ def test_create_destroy_cycles_reuse_ranges():
             peak = max(peak, info["total_slots"])
             assert info["live_spaces"] == 1 and info["live_slots"] == keep.capacity
         assert peak <= keep.capacity + 1500            # one space's range at a time, reused
-        assert len(sids) == 1                          # the id is reused too
+        assert len({v & 0xFFFFF for v in sids}) == 1   # the space index is reused,
+        assert len(sids) == 1000                       # each time under a new generation
         info = g.context_info()
         assert info["total_slots"] == keep.capacity and info["total_cells"] == info["live_cells"]
         _check_records(g.sync_collect().records, o, bk, bk, bk + keep.capacity, keep.gates, "after the cycles")
@@ -188,6 +189,19 @@ def test_destroy_refuses_a_non_empty_space_after_device_submits():
         g.destroy_space(sid)
         with pytest.raises(gpuaoi.GwError):
             g.destroy_space(sid)                     # gone
+        # the index is reused by the next space; the old id stays refused for
+        # every call that takes a space id and leaves the new space alone
+        sid2, base2 = g.create_space(100.0, 64)
+        assert sid2 & 0xFFFFF == sid & 0xFFFFF and sid2 != sid
+        for call in (lambda: g.destroy_space(sid), lambda: g.grow_space(sid, 128),
+                     lambda: g.set_ownership(sid, 0.0, 1.0),
+                     lambda: g.restore(sid, np.array([base2], np.uint32), np.ones(1, np.float32),
+                                       np.zeros(1, np.float32), np.ones(1, np.float32), np.zeros(1, np.float32))):
+            with pytest.raises(gpuaoi.GwError) as e:
+                call()
+            assert e.value.code == -5 and "stale" in str(e.value)
+        assert g.context_info()["live_spaces"] == 1 and g.grow_space(sid2, 64) == base2
+        g.destroy_space(sid2)
         g.dev_free(dev)
     finally:
         g.close()

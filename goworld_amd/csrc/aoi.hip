@@ -539,15 +539,31 @@ __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
             if (nr > RR_ROWS) rec[0] = make_uint4(1u, 0u, 0u, 0u);   // too many rows: k_mover builds its own
             for (uint32_t r = nr; r < RR_ROWS; ++r) rec[r] = make_uint4(0u, 0u, 0u, 0u);
         }
+        c |= PRIM_ONE;
+    } else {                      // a secondary entry has no events or statistics (coalesced here)
+        b.mstat[m] = 0;
+        b.ownc[m] = 0;
+        b.mirc[m] = 0;
     }
     b.cand[m] = c;
 }
+
+// the scan of the tagged bounds lists the primary entries in mover-grid
+// (cell) order: pidx[k] = the k-th, k_mover's wave k
+struct PrimPost {
+    uint32_t* pidx;
+    __device__ bool active() const { return pidx != nullptr; }
+    __device__ void operator()(uint64_t i, uint64_t excl, uint64_t x) const {
+        if (x >> PRIM_SHIFT) pidx[excl >> PRIM_SHIFT] = (uint32_t)i;
+    }
+};
 
 void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint64_t nmax = 2ull * b.m;
     const uint64_t* ngm = (const uint64_t*)&b.st->n_gm;
     hipLaunchKernelGGL(k_bounds, dim3(nblk1(nmax, NT)), dim3(NT), 0, s, b);
-    scan_exclusive<uint64_t, uint64_t>(b.cand, b.reg, nmax, ngm, sc, (uint64_t*)&b.st->cand_total, s);
+    scan_exclusive<uint64_t, uint64_t>(b.cand, b.reg, nmax, ngm, sc, (uint64_t*)&b.st->cand_total, s,
+                                       PrimPost{b.compact && !b.small_ents && !b.pair_max ? b.pidx : nullptr});
 }
 
 // ---------------------------------------------------------------------------
@@ -607,7 +623,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     }
     const uint64_t lt = lanemask_lt();
     const World& w = b.w;
-    const uint64_t reg = b.reg[m], cap = b.cand[m];
+    const uint64_t reg = b.reg[m] & CAND_MASK, cap = b.cand[m] & CAND_MASK;
     if (reg + cap > b.own_cap) {                      // region past the buffers: the host redoes the diff
         if (ln == 0) {
             atomicOr(&b.st->overflow, 1ull);
@@ -632,8 +648,10 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
     uint32_t* out = b.own + reg;
     uint64_t* mir = b.mir + reg;
-    uint32_t n = 0, nl = 0, nm_ = 0, nml = 0;
-    uint32_t c_old = 0, c_new = 0, c_cli = 0;
+    uint32_t n = 0, nm_ = 0;
+    // per-lane counts, summed once after the walk (a ballot + popcount per
+    // count and chunk was ~10 scalar instructions of every chunk's chain)
+    uint32_t l_old = 0, l_new = 0, l_cli = 0, l_nl = 0, l_nml = 0;
     Flat f;
     if (RR && (uint32_t)__builtin_amdgcn_readfirstlane((int)rr.x) <= (uint32_t)__builtin_amdgcn_readfirstlane((int)rr.y))
         f = flat_from(rr.x, rr.y - rr.x);
@@ -708,10 +726,9 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
                     key = (lv ? 0x80000000u : 0u) | e.slot;      // own events sort as (leave, target)
                 }
             }
-            // statistics as wave-uniform ballot counts (no cross-lane sums at the end)
-            c_old += (uint32_t)popc64(wave_ballot(t_ro));
-            c_new += (uint32_t)popc64(wave_ballot(t_rn));
-            c_cli += (uint32_t)popc64(wave_ballot(t_cli));
+            l_old += t_ro ? 1u : 0u;
+            l_new += t_rn ? 1u : 0u;
+            l_cli += t_cli ? 1u : 0u;
             // B has no op: (B,A) is B's event too (kept in A's region; the
             // events stage places it)
             const bool mev = ev && nmv && owned_x(P, e.x);
@@ -721,17 +738,26 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
                 const uint64_t bc = wave_ballot(longB && (t_ro || t_rn));
                 if (bc && ln == 0) atomicAdd(b.conflicts, (unsigned long long)popc64(bc));
             }
-            const uint64_t be = wave_ballot(ev), bl = wave_ballot(ev && lv), bm = wave_ballot(mev);
+            const uint64_t be = wave_ballot(ev), bm = wave_ballot(mev);
             const uint32_t at = n + (uint32_t)popc64(be & lt);
             if (ev && at < cap) out[at] = key;
             const uint32_t atm = nm_ + (uint32_t)popc64(bm & lt);
             if (mev && atm < cap) mir[atm] = ((uint64_t)e.slot << 32) | (A << 1) | (lv ? 1u : 0u);
             n += (uint32_t)popc64(be);
-            nl += (uint32_t)popc64(bl);
             nm_ += (uint32_t)popc64(bm);
-            nml += (uint32_t)popc64(wave_ballot(mev && lv));
+            l_nl += (ev && lv) ? 1u : 0u;
+            l_nml += (mev && lv) ? 1u : 0u;
         }
     }
+    // the wave's sums (DPP scans, lane 63): old | new, client | own leaves, mirror leaves
+    const unsigned long long s_on = wave_incl_scan<unsigned long long>(l_old | ((unsigned long long)l_new << 32));
+    const unsigned long long s_cl = wave_incl_scan<unsigned long long>(l_cli | ((unsigned long long)l_nl << 32));
+    const uint32_t s_ml = wave_incl_scan<uint32_t>(l_nml);
+    const uint32_t c_old = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s_on, 63);
+    const uint32_t c_new = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(s_on >> 32), 63);
+    const uint32_t c_cli = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s_cl, 63);
+    const uint32_t nl = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(s_cl >> 32), 63);
+    const uint32_t nml = (uint32_t)__builtin_amdgcn_readlane((int)s_ml, 63);
     // sort the own events by (target, kind)
     if (n > 1) {
         if (n <= b.rank_sort) {                    // a few events: place each by its rank
@@ -774,6 +800,18 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
 
 // WPB waves per block: a block keeps its LDS until its slowest wave ends, so
 // small blocks keep more waves resident when hotspot movers run long
+// one wave per primary entry (pidx, cell order): no wave is dispatched for
+// the secondary entries (half the mover grid), whose zeros k_bounds wrote
+template <int DIFF_U>
+__global__ void __launch_bounds__(64) k_mover_c(TickBufs b) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[SORT_LDS];
+    const uint64_t k = blockIdx.x;
+    const uint64_t np = b.st->cand_total >> PRIM_SHIFT;
+    const uint32_t m = b.pidx[k];                 // in bounds (k < ops), read with the count
+    if (k >= np) return;
+    mover_one<DIFF_U, SORT_LDS, GlobalSrc, true>(b, m, lds, GlobalSrc{b.w.gn, b.w.gn_start, b.gm_start, b.gm});
+}
+
 template <int DIFF_U, int WPB>
 __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[WPB * SORT_LDS];
@@ -824,8 +862,8 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     const bool go = prim;
     const uint32_t A = me.slot;
     if (prim) {
-        reg = b.reg[m];
-        cap = b.cand[m];
+        reg = b.reg[m] & CAND_MASK;
+        cap = b.cand[m] & CAND_MASK;
     }
     const uint64_t own_cap = b.own_cap;
     const float d = P.d;
@@ -1025,7 +1063,7 @@ __global__ void __launch_bounds__(64) k_mover_pair(TickBufs b) {
     if (m0 >= ngm) return;
     const uint64_t m1 = min(m0 + 2, ngm);
     const GlobalSrc src{b.w.gn, b.w.gn_start, b.gm_start, b.gm};
-    const uint64_t c0 = b.cand[m0], c1 = m0 + 1 < m1 ? b.cand[m0 + 1] : 0;
+    const uint64_t c0 = b.cand[m0] & CAND_MASK, c1 = m0 + 1 < m1 ? b.cand[m0 + 1] & CAND_MASK : 0;
     const uint32_t s0 = b.gm[m0].space, s1 = m0 + 1 < m1 ? b.gm[m0 + 1].space : s0;
     if (max(c0, c1) <= b.pair_max && s0 == s1) {            // wave-uniform
         if (mover_half<2>(b, m0, m1, b.w.sp[s0], src.GN, src.GS, src.MS, src.GM, lds)) return;
@@ -1105,7 +1143,7 @@ __global__ void __launch_bounds__(NT) k_mover_post(TickBufs b) {
             const uint32_t m = b.big[k];
             const uint64_t c = b.ownc[m];
             const uint32_t n = (uint32_t)(lo32(c) + hi32(c));
-            bitonic_inplace<NT>(b.own + b.reg[m], n, (int)threadIdx.x, [](uint32_t v) { return v; },
+            bitonic_inplace<NT>(b.own + (b.reg[m] & CAND_MASK), n, (int)threadIdx.x, [](uint32_t v) { return v; },
                                 [] { __syncthreads(); });
             __syncthreads();
         }
@@ -1189,7 +1227,7 @@ __global__ void __launch_bounds__(NT) k_mover_counts(TickBufs b) {
     b.mcnt[k] = oc + mc;
     const uint32_t nm = (uint32_t)(lo32(mc) + hi32(mc));
     b.minfo[k] = make_uint4(A, (uint32_t)lo32(oc), (uint32_t)hi32(oc), nm);
-    b.mreg[k] = b.reg[m];
+    b.mreg[k] = b.reg[m] & CAND_MASK;
     // bucket path: items = one per nonempty own run (enters, leaves) + one per mirror event
     b.icnt[k] = (lo32(oc) ? 1u : 0u) + (hi32(oc) ? 1u : 0u) + nm;
 }
@@ -1852,6 +1890,10 @@ void tick_diff(const TickBufs& b, hipStream_t s) {
     }
     if (b.pair_max) {                      // two short-list movers per wave (GW_PAIR_MAX, 0 = off)
         hipLaunchKernelGGL((k_mover_pair<2>), dim3(nblk1(nmax, 2)), dim3(64), 0, s, b);
+        return;
+    }
+    if (b.compact) {                       // one wave per primary entry (<= one per op)
+        hipLaunchKernelGGL((k_mover_c<2>), dim3(nblk1(b.m, 1)), dim3(64), 0, s, b);
         return;
     }
     switch (b.diff_u) {                    // GW_MOVER_WPB: waves per k_mover block

@@ -524,6 +524,7 @@ int gw_init(int device_id, gw_ctx** out) {
             c->pair_max = (uint32_t)std::max(0, atoi(e));
             c->pair_auto = false;
         }
+        if (const char* e = getenv("GW_MOVER_COMPACT")) c->mover_compact = atoi(e) != 0;
         if (const char* e = getenv("GW_DIRTY_SPAN")) c->dirty_span = (uint32_t)std::min(64, std::max(1, atoi(e)));
     } while (0);
     if (rc) {
@@ -541,7 +542,7 @@ void gw_shutdown(gw_ctx* c) {
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
     DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1,
-                      &c->gm, &c->cand, &c->reg, &c->rowrec, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
+                      &c->gm, &c->cand, &c->reg, &c->pidx, &c->rowrec, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
                       &c->mcnt, &c->moff, &c->minfo, &c->icnt, &c->ioff, &c->mreg, &c->chunk_first, &c->srange, &c->bk_a, &c->bk_b, &c->bk_id, &c->bk_cnt, &c->bk_split, &c->ev_d, &c->rtable,
                       &c->scan_status, &c->rs_hist,
                       &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
@@ -1036,7 +1037,8 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         redone = true;
         if (attempt == 3) return set_err(c, GW_ENOMEM, "event buffers overflowed three times");
         const uint64_t E = (c->hstats->ev_pk & 0xffffffffull) + (c->hstats->ev_pk >> 32);
-        if (c->hstats->cand_total > c->own_cap) c->own_cap = c->hstats->cand_total + c->hstats->cand_total / 4 + 4096;
+        const uint64_t ct = c->hstats->cand_total & CAND_MASK;
+        if (ct > c->own_cap) c->own_cap = ct + ct / 4 + 4096;
         if (E > c->ev_cap) c->ev_cap = E + E / 4 + 4096;
         // a bucket outgrew the LDS sort: this attempt on the general sort (its
         // output gives the next tick quantile bounds); twice running, the
@@ -1089,7 +1091,7 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     uint64_t n_mov = 0;
     for (int i = 0; i < STAT_SHARDS; ++i) n_mov += hs.shard[i][SH_MOVERS];
     // candidates tested == the candidate bounds; a_old | a_new << 32 per shard
-    const uint64_t pairs = hs.cand_total;
+    const uint64_t pairs = hs.cand_total & CAND_MASK;
     uint64_t a_old = 0, a_new = 0;
     for (int i = 0; i < STAT_SHARDS; ++i) {
         a_old += hs.shard[i][SH_AOLD] & 0xffffffffull;
@@ -1100,7 +1102,7 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         for (int i = 0; i < STAT_SHARDS; ++i) { f0 += hs.shard[i][0]; f2 += hs.shard[i][2]; }
         fprintf(stderr, "gw_tick: movers %llu gm %llu cand %llu ev %llu+%llu big %llu mlist %llu "
                 "f0 %llu f2 %llu bits %d full %d items %llu\n",
-                (unsigned long long)n_mov, hs.n_gm, hs.cand_total, hs.ev_pk & 0xffffffffull,
+                (unsigned long long)n_mov, hs.n_gm, hs.cand_total & CAND_MASK, hs.ev_pk & 0xffffffffull,
                 hs.ev_pk >> 32, hs.n_big, hs.n_mlist, f0, f2, b.bk_bits, b.ev_full, hs.n_items);
     }
     o.ops = M;
@@ -1251,7 +1253,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         (rc = ensure(c, c->mcell, (size_t)M * 16)) ||
         (rc = ensure(c, c->cand, M2 * 8)) || (rc = ensure(c, c->reg, M2 * 8)) ||
         (rc = ensure(c, c->ownc, M2 * 8)) || (rc = ensure(c, c->mirc, M2 * 8)) || (rc = ensure(c, c->big, M2 * 4)) ||
-        (rc = ensure(c, c->mstat, M2 * 8)) ||
+        (rc = ensure(c, c->mstat, M2 * 8)) || (rc = ensure(c, c->pidx, (size_t)M * 4)) ||
         (rc = ensure(c, c->mlist, (size_t)M * 4)) || (rc = ensure(c, c->mcnt, (size_t)M * 8)) ||
         (rc = ensure(c, c->moff, (size_t)M * 8)) || (rc = ensure(c, c->minfo, (size_t)M * 16)) ||
         (rc = ensure(c, c->mreg, (size_t)M * 8)) || (rc = ensure(c, c->icnt, (size_t)M * 4)) ||
@@ -1283,6 +1285,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     if (!b.ol_tag && (rc = next_ol_tag(c, &b.ol_tag))) return rc;
     b.stamps = stamps;
     b.diff_u = c->diff_u;
+    b.compact = c->mover_compact;
     b.walk_min = c->walk_min;
     b.rank_sort = c->rank_sort;
     b.grid_cap = c->grid_cap;
@@ -1296,7 +1299,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.dep = c->dep; b.arr = c->arr; b.cnt_new = c->cnt_new;
     b.gm_cnt = c->gm_cnt; b.gm_start = c->gm_start; b.gm = P<MEnt>(c->gm);
     b.mtmp = P<MEnt>(c->mtmp); b.mcell = P<uint4>(c->mcell);
-    b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg);
+    b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg); b.pidx = P<uint32_t>(c->pidx);
     b.ownc = P<unsigned long long>(c->ownc); b.mirc = P<unsigned long long>(c->mirc);
     b.big = P<uint32_t>(c->big);
     b.mstat = P<unsigned long long>(c->mstat);

@@ -186,6 +186,13 @@ struct World {
 constexpr uint32_t RR_ROWS = 8;
 
 // ---- tick buffers handed to the launchers ----------------------------------
+// k_bounds tags each primary mover-grid entry's candidate bound with PRIM_ONE,
+// so the scan of the bounds also counts the primaries before each entry (its
+// index among them) and their total; readers of cand / reg mask with CAND_MASK
+constexpr int PRIM_SHIFT = 36;
+constexpr uint64_t PRIM_ONE = 1ull << PRIM_SHIFT;
+constexpr uint64_t CAND_MASK = PRIM_ONE - 1;
+
 struct TickBufs {
     World w;                  // gn / gn_start: the grid before the tick (the new one from tick_movers on)
     const gw_op* ops;
@@ -210,8 +217,9 @@ struct TickBufs {
     MEnt* mtmp;               // [m] op i's mover-grid entry (tags aside) when op i is a mover (k_ops3 -> k_place)
     uint4* mcell;             // [m] op i: old / new cell of its mover (NO_CELL: none), slot, syncInfoFlag bits to OR
     // diff (indexed by mover-grid entry)
-    uint64_t* cand;           // [2m] candidate bound (0 unless TAG_PRIMARY)
-    uint64_t* reg;            // [2m] exclusive scan of cand
+    uint64_t* cand;           // [2m] candidate bound (0 unless TAG_PRIMARY) | PRIM_ONE if primary
+    uint64_t* reg;            // [2m] exclusive scan of cand: region offset | primaries before << PRIM_SHIFT
+    uint32_t* pidx;           // [m] k-th primary entry (written by the scan of cand; k_mover's waves)
     uint4* rowrec;            // [2m * RR_ROWS] per primary entry: its rows' grid / mover-grid index ranges
                               // (start, end, start, end) from k_bounds; row 0 = (1, 0, ..) when > RR_ROWS rows
     uint64_t own_cap;         // capacity of own / mir
@@ -246,6 +254,8 @@ struct TickBufs {
                               // mover (its pairs are attributed to the targets' owners); +inf otherwise
     unsigned long long* conflicts;   // decomposed world: long-mover pairs related before or after (or null)
     uint32_t dirty_span;      // GW_DIRTY_SPAN: cells whose dirty flags one k_grid_dirty wave scans (1..64)
+    uint32_t compact;         // GW_MOVER_COMPACT (default 1): k_mover runs one wave per primary entry
+                              // (pidx), else one per mover-grid entry, the others exiting
     uint32_t pair_max;        // GW_PAIR_MAX: k_mover_pair runs two movers per wave when both have at
                               // most this many candidates (0 = one mover per wave, k_mover)
     uint32_t grid_cap;        // GW_GRID_CAP (tests): at most this many blocks for the grid-stride

@@ -515,8 +515,11 @@ __device__ __forceinline__ Rects mover_rects(const SpaceP& P, bool po, float ox,
 // one load after its entry instead of three (entry -> space -> row starts).
 __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
     const uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x;
-    if (m >= b.st->n_gm) return;
-    const MEnt e = b.gm[m];
+    const uint64_t ngm = b.st->n_gm;
+    if (m >= ngm && !(b.heavy_min && m - lane_id() < ngm)) return;   // heavy mode: whole waves reach the ballot
+    MEnt e;
+    e.tags = 0;
+    if (m < ngm) e = b.gm[m];
     uint64_t c = 0;
     if (e.tags & TAG_PRIMARY) {
         const SpaceP P = b.w.sp[e.space];
@@ -539,13 +542,22 @@ __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
             if (nr > RR_ROWS) rec[0] = make_uint4(1u, 0u, 0u, 0u);   // too many rows: k_mover builds its own
             for (uint32_t r = nr; r < RR_ROWS; ++r) rec[r] = make_uint4(0u, 0u, 0u, 0u);
         }
-        c |= PRIM_ONE;
-    } else {                      // a secondary entry has no events or statistics (coalesced here)
+    } else if (m < ngm) {         // a secondary entry has no events or statistics (coalesced here)
         b.mstat[m] = 0;
         b.ownc[m] = 0;
         b.mirc[m] = 0;
     }
-    b.cand[m] = c;
+    // heavy-first mode: the longest walks are listed apart and dispatched first
+    const bool hv = (e.tags & TAG_PRIMARY) && b.heavy_min && c >= b.heavy_min;
+    const uint64_t hm = wave_ballot(hv);
+    if (hm) {
+        const int leader = __builtin_ctzll(hm);
+        uint32_t base = 0;
+        if (lane_id() == leader) base = (uint32_t)atomicAdd(&b.st->n_heavy, (unsigned long long)popc64(hm));
+        base = __shfl(base, leader, 64);
+        if (hv) b.heavy[base + (uint32_t)popc64(hm & lanemask_lt())] = (uint32_t)m;
+    }
+    if (m < ngm) b.cand[m] = c | ((e.tags & TAG_PRIMARY) && !hv ? PRIM_ONE : 0ull);
 }
 
 // the scan of the tagged bounds lists the primary entries in mover-grid
@@ -807,8 +819,15 @@ __global__ void __launch_bounds__(64) k_mover_c(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[SORT_LDS];
     const uint64_t k = blockIdx.x;
     const uint64_t np = b.st->cand_total >> PRIM_SHIFT;
-    const uint32_t m = b.pidx[k];                 // in bounds (k < ops), read with the count
-    if (k >= np) return;
+    uint32_t m;
+    if (b.heavy_min) {                            // heavy entries first, then the others in cell order
+        const uint64_t nh = b.st->n_heavy;
+        if (k >= nh + np) return;
+        m = k < nh ? b.heavy[k] : b.pidx[k - nh];
+    } else {
+        m = b.pidx[k];                            // in bounds (k < ops), read with the count
+        if (k >= np) return;
+    }
     mover_one<DIFF_U, SORT_LDS, GlobalSrc, true>(b, m, lds, GlobalSrc{b.w.gn, b.w.gn_start, b.gm_start, b.gm});
 }
 
@@ -1966,8 +1985,26 @@ __global__ void __launch_bounds__(RESET_NT) k_tick_reset(TickBufs b, const unsig
     uint32_t v[SPLIT_PT];
     const bool split = b.st && bk_split_load(b, b.st->ev_pk, b.st->overflow, v);
     // the statistics the host reads after its sync, written straight into its
-    // (coherent, pinned) buffer: no blit copy between the collect and the reset
-    for (uint32_t k = threadIdx.x; k < pub_words; k += RESET_NT) pub_dst[k] = pub_src[k];
+    // (coherent, pinned) buffer: no blit copy between the collect and the reset.
+    // Each DevStats goes over as its header words and, per field, the sum of
+    // its shards in shard[0] (20 PCIe stores instead of 1040: the host reads
+    // shard[0] only; config #3 world strips spent ~10 us here)
+    constexpr uint32_t HDR = (uint32_t)(offsetof(DevStats, shard) / 8), DSW = (uint32_t)(sizeof(DevStats) / 8);
+    static_assert(STAT_SHARDS * SH_FIELDS == RESET_NT, "one shard word per thread");
+    __shared__ unsigned long long red[RESET_NT];
+    for (uint32_t q = 0; q * DSW < pub_words; ++q) {
+        const unsigned long long* src = pub_src + (size_t)q * DSW;
+        unsigned long long* dst = pub_dst + (size_t)q * DSW;
+        if (threadIdx.x < HDR) dst[threadIdx.x] = src[threadIdx.x];
+        red[threadIdx.x] = src[HDR + threadIdx.x];         // shard t / SH_FIELDS, field t % SH_FIELDS
+        __syncthreads();
+        for (uint32_t h = RESET_NT / 2; h >= SH_FIELDS; h >>= 1) {
+            if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+            __syncthreads();
+        }
+        if (threadIdx.x < SH_FIELDS) dst[HDR + threadIdx.x] = red[threadIdx.x];
+        __syncthreads();
+    }
     if (!b.st) {
         __threadfence_system();
         return;

@@ -320,9 +320,21 @@ int upload_spaces(gw_ctx* c) {
     return 0;
 }
 
+// the per-field sums of the statistics shards into shard[0] (the form the
+// publishing kernel writes; readers only look at shard[0])
+static void fold_shards(DevStats& s) {
+    for (int f = 0; f < SH_FIELDS; ++f) {
+        unsigned long long t = 0;
+        for (int i = 0; i < STAT_SHARDS; ++i) t += s.shard[i][f];
+        s.shard[0][f] = t;
+        for (int i = 1; i < STAT_SHARDS; ++i) s.shard[i][f] = 0;
+    }
+}
+
 int read_stats(gw_ctx* c) {
     HIPCHK(hipMemcpyAsync(c->hstats, c->stats, sizeof(DevStats), hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    fold_shards(*c->hstats);
     return 0;
 }
 
@@ -341,11 +353,6 @@ int read_cstats(gw_ctx* c) {
     return 0;
 }
 
-unsigned long long shard_sum(const DevStats& s, int f) {
-    unsigned long long t = 0;
-    for (int i = 0; i < STAT_SHARDS; ++i) t += s.shard[i][f];
-    return t;
-}
 
 void reset_stats_host(gw_ctx* c) { memset(c->hstats, 0, sizeof(DevStats)); }
 
@@ -525,6 +532,8 @@ int gw_init(int device_id, gw_ctx** out) {
             c->pair_auto = false;
         }
         if (const char* e = getenv("GW_MOVER_COMPACT")) c->mover_compact = atoi(e) != 0;
+        if (const char* e = getenv("GW_HEAVY_MIN")) c->heavy_min = (uint32_t)std::max(0, atoi(e));
+        if (const char* e = getenv("GW_HEAVY_MAXM")) c->heavy_maxm = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_DIRTY_SPAN")) c->dirty_span = (uint32_t)std::min(64, std::max(1, atoi(e)));
     } while (0);
     if (rc) {
@@ -542,7 +551,7 @@ void gw_shutdown(gw_ctx* c) {
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
     DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1,
-                      &c->gm, &c->cand, &c->reg, &c->pidx, &c->rowrec, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
+                      &c->gm, &c->cand, &c->reg, &c->pidx, &c->heavy, &c->rowrec, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
                       &c->mcnt, &c->moff, &c->minfo, &c->icnt, &c->ioff, &c->mreg, &c->chunk_first, &c->srange, &c->bk_a, &c->bk_b, &c->bk_id, &c->bk_cnt, &c->bk_split, &c->ev_d, &c->rtable,
                       &c->scan_status, &c->rs_hist,
                       &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
@@ -1051,9 +1060,9 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         choose_buckets(c, b, bk_over || b.ev_full);
         DevStats* h = c->hstats;
         h->overflow = 0; h->n_big = 0; h->ev_pk = 0; h->n_mlist = 0; h->n_sort = 0; h->bk_max = 0; h->n_items = 0; h->bk_tiles = 0; h->bk_cells = 0;
-        for (int i = 0; i < STAT_SHARDS; ++i)      // the diff's shards restart; the mover count stays
-            for (int f = 0; f < SH_FIELDS; ++f)
-                if (f != SH_MOVERS) h->shard[i][f] = 0;
+        for (int i = 0; i < STAT_SHARDS; ++i)      // the diff's shards restart; the mover count (its
+            for (int f = 0; f < SH_FIELDS; ++f)      // total in shard[0]) stays
+                if (f != SH_MOVERS || i) h->shard[i][f] = 0;
         HIPCHK(hipMemcpyAsync(c->stats, c->hstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
         prof_begin(c, "diff");
         tick_diff(b, c->st);
@@ -1089,17 +1098,16 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     if (c->ev_full_ticks > 0) --c->ev_full_ticks;
     if (!b.ev_full) c->bk_overflows = 0;
     uint64_t n_mov = 0;
-    for (int i = 0; i < STAT_SHARDS; ++i) n_mov += hs.shard[i][SH_MOVERS];
+    n_mov = hs.shard[0][SH_MOVERS];                  // shard[0] holds the totals (fold_shards / the publish)
     // candidates tested == the candidate bounds; a_old | a_new << 32 per shard
     const uint64_t pairs = hs.cand_total & CAND_MASK;
     uint64_t a_old = 0, a_new = 0;
-    for (int i = 0; i < STAT_SHARDS; ++i) {
-        a_old += hs.shard[i][SH_AOLD] & 0xffffffffull;
-        a_new += hs.shard[i][SH_AOLD] >> 32;
-    }
+    a_old = hs.shard[0][SH_AOLD] & 0xffffffffull;
+    a_new = hs.shard[0][SH_AOLD] >> 32;
     if (getenv("GW_DEBUG_STATS")) {
         unsigned long long f0 = 0, f2 = 0;
-        for (int i = 0; i < STAT_SHARDS; ++i) { f0 += hs.shard[i][0]; f2 += hs.shard[i][2]; }
+        f0 = hs.shard[0][0];
+        f2 = hs.shard[0][2];
         fprintf(stderr, "gw_tick: movers %llu gm %llu cand %llu ev %llu+%llu big %llu mlist %llu "
                 "f0 %llu f2 %llu bits %d full %d items %llu\n",
                 (unsigned long long)n_mov, hs.n_gm, hs.cand_total & CAND_MASK, hs.ev_pk & 0xffffffffull,
@@ -1254,6 +1262,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         (rc = ensure(c, c->cand, M2 * 8)) || (rc = ensure(c, c->reg, M2 * 8)) ||
         (rc = ensure(c, c->ownc, M2 * 8)) || (rc = ensure(c, c->mirc, M2 * 8)) || (rc = ensure(c, c->big, M2 * 4)) ||
         (rc = ensure(c, c->mstat, M2 * 8)) || (rc = ensure(c, c->pidx, (size_t)M * 4)) ||
+        (rc = ensure(c, c->heavy, (size_t)M * 4)) ||
         (rc = ensure(c, c->mlist, (size_t)M * 4)) || (rc = ensure(c, c->mcnt, (size_t)M * 8)) ||
         (rc = ensure(c, c->moff, (size_t)M * 8)) || (rc = ensure(c, c->minfo, (size_t)M * 16)) ||
         (rc = ensure(c, c->mreg, (size_t)M * 8)) || (rc = ensure(c, c->icnt, (size_t)M * 4)) ||
@@ -1286,11 +1295,17 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.stamps = stamps;
     b.diff_u = c->diff_u;
     b.compact = c->mover_compact;
+    b.heavy = P<uint32_t>(c->heavy);
+    // heavy-first only for few movers (a world strip): the tick's tail is then
+    // the longest walk; with many movers the one-wave-per-mover dispatch balances
+    b.heavy_min = (b.compact && M <= c->heavy_maxm) ? c->heavy_min : 0u;
     b.walk_min = c->walk_min;
     b.rank_sort = c->rank_sort;
     b.grid_cap = c->grid_cap;
     b.pair_max = c->pair_auto ? (c->cand_mean <= gw_ctx::PAIR_MEAN ? gw_ctx::PAIR_AUTO : 0u) : c->pair_max;
-    b.dirty_span = c->dirty_span ? c->dirty_span : (NC > (1u << 20) ? 16u : 8u);
+    // dirty-cell span by cell count: a world strip's few cells spread over
+    // more waves (1M world at 8 strips, 57k cells: grid 37 -> 30 us at 2)
+    b.dirty_span = c->dirty_span ? c->dirty_span : (NC > (1u << 20) ? 16u : NC > (1u << 17) ? 8u : 2u);
     b.long_step = c->wd.on ? c->wd.g.max_step : INFINITY;   // decomposed world: long movers
     b.conflicts = c->wd.on ? &c->halo->conflicts : nullptr;
     b.ol = c->ol;

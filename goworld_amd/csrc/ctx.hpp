@@ -189,13 +189,17 @@ struct gw_ctx {
     gw_tick_out last_out{};
 
     // grid + tick scratch
-    DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, mtmp, mcell, cand, reg, pidx, rowrec, own, big, mstat;
+    DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, mtmp, mcell, cand, reg, pidx, heavy, rowrec, own, big, mstat;
     DevBuf mir, ownc, mirc, mlist, mcnt, moff, minfo, icnt, ioff, mreg, chunk_first, srange, bk_a, bk_b, bk_id, bk_cnt, bk_split, ev_d, rtable;
     DevBuf scan_status, rs_hist;
     uint32_t walk_min = 32;              // GW_WALK_MIN: TickBufs.walk_min (0: always walk)
     bool mover_compact = true;           // GW_MOVER_COMPACT: TickBufs.compact
+    uint32_t heavy_min = 512;            // GW_HEAVY_MIN: TickBufs.heavy_min (0: off; 1M world at 8 strips:
+                                         // diff 58 -> 47 us; at 100k movers one wave per mover in cell order
+                                         // balances better) ...
+    uint32_t heavy_maxm = 65536;         // ... for ticks of at most GW_HEAVY_MAXM ops
     uint32_t rank_sort = 12;             // GW_RANK_SORT: TickBufs.rank_sort
-    // GW_DIRTY_SPAN: TickBufs.dirty_span; 0 = by the cell count: 8 up to 1M cells (a hotspot wave
+    // GW_DIRTY_SPAN: TickBufs.dirty_span; 0 = by the cell count: 2 up to 128k cells, 8 up to 1M cells (a hotspot wave
     // merges fewer dirty cells in a row: config #3 grid 63 -> 58 us), 16 above (fewer idle waves:
     // config #4's 4.4M cells at 4 per wave cost +50 us)
     uint32_t dirty_span = 0;

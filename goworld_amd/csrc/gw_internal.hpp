@@ -133,7 +133,9 @@ struct DevStats {
     unsigned long long bad_ops;
     unsigned long long flagged;       // sync: flagged entities
     unsigned long long rec_total;     // sync: records
-    unsigned long long shard[STAT_SHARDS][SH_FIELDS];   // summed on the host
+    unsigned long long n_heavy;       // heavy-first k_mover: primaries with >= heavy_min candidates (heavy[])
+    unsigned long long pad_;
+    unsigned long long shard[STAT_SHARDS][SH_FIELDS];   // per-field sums in shard[0] on the host
 };
 
 // ---- primitives (prim.hpp; host wrappers in sync.hip) -----------------------
@@ -220,6 +222,8 @@ struct TickBufs {
     uint64_t* cand;           // [2m] candidate bound (0 unless TAG_PRIMARY) | PRIM_ONE if primary
     uint64_t* reg;            // [2m] exclusive scan of cand: region offset | primaries before << PRIM_SHIFT
     uint32_t* pidx;           // [m] k-th primary entry (written by the scan of cand; k_mover's waves)
+    uint32_t* heavy;          // [m] heavy-first mode: primaries with >= heavy_min candidates, walked first
+    uint32_t heavy_min;       // GW_HEAVY_MIN (0: off): longest walks first when few movers (shorter tail)
     uint4* rowrec;            // [2m * RR_ROWS] per primary entry: its rows' grid / mover-grid index ranges
                               // (start, end, start, end) from k_bounds; row 0 = (1, 0, ..) when > RR_ROWS rows
     uint64_t own_cap;         // capacity of own / mir

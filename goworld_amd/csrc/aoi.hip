@@ -542,6 +542,7 @@ __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
             if (nr > RR_ROWS) rec[0] = make_uint4(1u, 0u, 0u, 0u);   // too many rows: k_mover builds its own
             for (uint32_t r = nr; r < RR_ROWS; ++r) rec[r] = make_uint4(0u, 0u, 0u, 0u);
         }
+        if (e.tags & TAG_LONG) c += b.n_long;   // its pairs with the other long movers (long_pairs)
     } else if (m < ngm) {         // a secondary entry has no events or statistics (coalesced here)
         b.mstat[m] = 0;
         b.ownc[m] = 0;
@@ -614,6 +615,48 @@ struct GlobalSrc {
         return kind ? (const uint4*)(GM + i) : (const uint4*)(GN + i);
     }
 };
+
+// The relation of a pair from the two entities' positions and last-AOI-op
+// stamps alone: the window of the member with the later op.
+__device__ __forceinline__ bool pair_rel(float ax, float az, unsigned long long as, float bx, float bz,
+                                         unsigned long long bs, float d) {
+    return as > bs ? in_win(ax, az, d, bx, bz) : in_win(bx, bz, d, ax, az);
+}
+
+// A long mover's own events with the other long movers (group teleports): the
+// lists hold every long mover's state before and after the tick, so the old
+// and the new relation of each pair are evaluated here even when no rank holds
+// both ends.  Events are appended to A's region before its sort.
+__device__ __noinline__ void long_pairs(const TickBufs& b, uint32_t A, float d, uint32_t* out, uint64_t cap,
+                                        uint32_t& n, uint32_t& l_nl) {
+    const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint32_t nl = b.n_long;
+    int32_t ia = -1;                                   // A's own entry
+    for (uint32_t base = 0; base < nl && ia < 0; base += 64) {
+        const uint32_t j = base + (uint32_t)ln;
+        const uint64_t hit = wave_ballot(j < nl && b.longs[j].slot == A);
+        if (hit) ia = (int32_t)(base + (uint32_t)__builtin_ctzll(hit));
+    }
+    if (ia < 0) return;                                // not listed (a rank's list was not queued)
+    const gw_long_move LA = b.longs[ia];
+    for (uint32_t base = 0; base < nl; base += 64) {
+        const uint32_t j = base + (uint32_t)ln;
+        gw_long_move L;
+        L.slot = A;
+        if (j < nl) L = b.longs[j];
+        bool ev = false, lv = false;
+        if (L.slot != A) {
+            lv = pair_rel(LA.old_x, LA.old_z, LA.old_stamp, L.old_x, L.old_z, L.old_stamp, d);
+            ev = lv != pair_rel(LA.new_x, LA.new_z, LA.new_stamp, L.new_x, L.new_z, L.new_stamp, d);
+        }
+        const uint64_t be = wave_ballot(ev);
+        const uint32_t at = n + (uint32_t)popc64(be & lt);
+        if (ev && at < cap) out[at] = (lv ? 0x80000000u : 0u) | L.slot;
+        n += (uint32_t)popc64(be);
+        l_nl += (ev && lv) ? 1u : 0u;
+    }
+}
 
 // One mover-grid entry m by one wave, candidates from S; lds: SCAP sort slots
 // per wave.
@@ -744,12 +787,10 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             // B has no op: (B,A) is B's event too (kept in A's region; the
             // events stage places it)
             const bool mev = ev && nmv && owned_x(P, e.x);
+            // a long mover's pairs: with a short mover B by B's owner (it holds
+            // both ends); with another long mover from the long lists (below)
             const bool longB = (e.info & TAG_LONG) != 0;
             ev = ev && (longA ? !longB && owned_x(P, e.x == e.x ? e.x : e.ox) : ownA);
-            if (longA && b.conflicts) {                  // two related long movers: not supported
-                const uint64_t bc = wave_ballot(longB && (t_ro || t_rn));
-                if (bc && ln == 0) atomicAdd(b.conflicts, (unsigned long long)popc64(bc));
-            }
             const uint64_t be = wave_ballot(ev), bm = wave_ballot(mev);
             const uint32_t at = n + (uint32_t)popc64(be & lt);
             if (ev && at < cap) out[at] = key;
@@ -761,6 +802,9 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             l_nml += (mev && lv) ? 1u : 0u;
         }
     }
+    // group teleports: A is a long mover owned here after the tick; its pairs
+    // with the other long movers come from the lists of every rank
+    if (longA && ownA && b.n_long) long_pairs(b, A, d, out, cap, n, l_nl);
     // the wave's sums (DPP scans, lane 63): old | new, client | own leaves, mirror leaves
     const unsigned long long s_on = wave_incl_scan<unsigned long long>(l_old | ((unsigned long long)l_new << 32));
     const unsigned long long s_cl = wave_incl_scan<unsigned long long>(l_cli | ((unsigned long long)l_nl << 32));
@@ -1003,11 +1047,8 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
             c_cli += (uint32_t)popc64(wave_ballot(t_cli) & hmask);
             const bool mev = ev && nmv && owned_x(P, e.x);
             const bool longB = (e.info & TAG_LONG) != 0;
+            // (long movers never come here: k_mover_pair runs them through mover_one)
             ev = ev && (longA ? !longB && owned_x(P, e.x == e.x ? e.x : e.ox) : ownA);
-            if (b.conflicts) {
-                const uint64_t bc = wave_ballot(longA && longB && (t_ro || t_rn));
-                if (bc && ln == 0) atomicAdd(b.conflicts, (unsigned long long)popc64(bc));
-            }
             const uint64_t be = wave_ballot(ev) & hmask, bl = wave_ballot(ev && lv) & hmask;
             const uint64_t bm = wave_ballot(mev) & hmask;
             const uint32_t at = n + (uint32_t)popc64(be & lt);
@@ -1084,7 +1125,8 @@ __global__ void __launch_bounds__(64) k_mover_pair(TickBufs b) {
     const GlobalSrc src{b.w.gn, b.w.gn_start, b.gm_start, b.gm};
     const uint64_t c0 = b.cand[m0] & CAND_MASK, c1 = m0 + 1 < m1 ? b.cand[m0 + 1] & CAND_MASK : 0;
     const uint32_t s0 = b.gm[m0].space, s1 = m0 + 1 < m1 ? b.gm[m0 + 1].space : s0;
-    if (max(c0, c1) <= b.pair_max && s0 == s1) {            // wave-uniform
+    const uint32_t tg = b.gm[m0].tags | (m0 + 1 < m1 ? b.gm[m0 + 1].tags : 0u);
+    if (max(c0, c1) <= b.pair_max && s0 == s1 && !(tg & TAG_LONG)) {   // wave-uniform; long movers: mover_one
         if (mover_half<2>(b, m0, m1, b.w.sp[s0], src.GN, src.GS, src.MS, src.GM, lds)) return;
     }
     mover_one<DIFF_U, SORT_LDS>(b, m0, lds, src);

@@ -1306,8 +1306,12 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     // dirty-cell span by cell count: a world strip's few cells spread over
     // more waves (1M world at 8 strips, 57k cells: grid 37 -> 30 us at 2)
     b.dirty_span = c->dirty_span ? c->dirty_span : (NC > (1u << 20) ? 16u : NC > (1u << 17) ? 8u : 2u);
-    b.long_step = c->wd.on ? c->wd.g.max_step : INFINITY;   // decomposed world: long movers
-    b.conflicts = c->wd.on ? &c->halo->conflicts : nullptr;
+    // decomposed world of >= 2 strips: long movers (a one-strip world holds every pair)
+    b.long_step = (c->wd.on && c->wd.g.ranks > 1) ? c->wd.g.max_step : INFINITY;
+    b.longs = c->wd.tick_longs;                      // the long lists queued for this tick (world.cpp)
+    b.n_long = c->wd.tick_nlong;
+    c->wd.tick_longs = nullptr;
+    c->wd.tick_nlong = 0;
     b.ol = c->ol;
     b.st = st;
     b.gn_nxt = c->gnb[c->gcur ^ 1]; b.start_nxt = c->gsb[c->gcur ^ 1];

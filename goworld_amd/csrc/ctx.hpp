@@ -73,9 +73,16 @@ struct WorldHost {
     // long moves (teleports): far triples, partitioned by destination rank
     DevBuf ext, far_rows, far_dest, far_cnt, far_sorted, far_off, far_cursor, far_recv, far_mat;
     uint32_t far_cap = 0;                        // triples the far buffer holds
-    std::vector<uint32_t> far_cnt_h;             // [ranks] triples this rank sends to each rank (incl. itself)
+    std::vector<uint32_t> far_cnt_h;             // [ranks + 1] triples this rank sends to each rank (incl.
+                                                 // itself), then its long movers listed
     std::vector<uint32_t> far_off_h;             // [ranks] their offsets in far_sorted (triples)
-    std::vector<uint32_t> far_mat_h;             // [ranks * ranks] triples rank p sends to rank q (step path)
+    std::vector<uint32_t> far_mat_h;             // [ranks * (ranks + 1)] rank p's far_cnt vector (step path)
+    // long-mover lists (group teleports): this rank's (longs, long_cap entries;
+    // own_nlong after the last route), all ranks' (long_all) for the tick
+    DevBuf longs, long_all;
+    uint32_t long_cap = 0, own_nlong = 0;
+    const gw_long_move* tick_longs = nullptr;    // queued for the next gw_tick (then cleared)
+    uint32_t tick_nlong = 0;
     std::vector<float> ext_h;                    // [2 * ranks] held x-range of every rank
     // host ops of a tick (gw_world_stage_ops): pinned staging, device copy, and
     // the event after the upload (the pinned buffer is reused once it fired)

@@ -256,7 +256,8 @@ struct TickBufs {
     uint64_t it_hint;         // bucket-path items of the last tick (sizes the flatten's grid)
     float long_step;          // decomposed world: an owned mover whose x moves further is a long
                               // mover (its pairs are attributed to the targets' owners); +inf otherwise
-    unsigned long long* conflicts;   // decomposed world: long-mover pairs related before or after (or null)
+    const gw_long_move* longs;   // decomposed world: every rank's long movers of the tick (group teleports:
+    uint32_t n_long;             // their pairs are evaluated from these by the owner of the watcher)
     uint32_t dirty_span;      // GW_DIRTY_SPAN: cells whose dirty flags one k_grid_dirty wave scans (1..64)
     uint32_t compact;         // GW_MOVER_COMPACT (default 1): k_mover runs one wave per primary entry
                               // (pidx), else one per mover-grid entry, the others exiting
@@ -361,7 +362,8 @@ struct HaloStats {
     unsigned long long bad_ops;     // ops with an invalid slot or kind
     unsigned long long long_moves;  // owned entities that moved more than max_step (routed far)
     uint32_t cnt[2];                // entities placed per neighbour destination (this call)
-    uint32_t far_n, pad;            // far triples placed (this call; may exceed the buffer)
+    uint32_t far_n;                 // far triples placed (this call; may exceed the buffer)
+    uint32_t long_n;                // long movers listed (this call; may exceed the list buffer)
 };
 // halo rows of long moves (teleports): to every rank holding the old or the
 // new position that is not a neighbour, and a LEAVE for the owner's own copy
@@ -370,9 +372,12 @@ struct HaloStats {
 struct HaloFar {
     gw_halo_row* rows;          // cap triples (3 rows each)
     uint32_t* dest;             // destination rank of each triple
-    uint32_t* cnt;              // [nranks] triples per destination (zeroed by the first pass)
+    uint32_t* cnt;              // [nranks + 1] triples per destination, then the long movers listed
+                                // (zeroed by the first pass; all-gathered as one vector)
     const float* ext;           // [2 * nranks] held x-range [lo, hi) of every rank, float32
     uint32_t cap, nranks, self, pad;
+    gw_long_move* longs;        // [long_cap] this rank's long movers (group teleports), or null
+    uint32_t long_cap, pad2;
 };
 constexpr uint16_t RES_LONG = 1;   // gw_op.reserved of a halo row: the entity moved more than max_step
 struct HaloDst {

@@ -34,8 +34,8 @@ __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, ui
                                                 unsigned long long* stamps_out, unsigned long long stamp_base,
                                                 HaloFar F) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
-    if (i == 0) hs->cnt[0] = hs->cnt[1] = hs->far_n = 0;   // placement counters of this call
-    if (F.cnt && i < F.nranks) F.cnt[i] = 0;
+    if (i == 0) hs->cnt[0] = hs->cnt[1] = hs->far_n = hs->long_n = 0;   // placement counters of this call
+    if (F.cnt && i <= F.nranks) F.cnt[i] = 0;
     if (i >= n) return;
     if (stamps_out) stamps_out[i] = stamp_base + i;
     const gw_op op = ops[i];
@@ -191,6 +191,24 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
         }
         put_triple(dst.rows + (size_t)e * ROWS, k, s, oa, op_pos, f, res, stamps, ll, la, i);
     }
+    if (lng && F.longs) {
+        // the long-mover list (group teleports): state before and after the
+        // tick, for the owner of every other long mover's new position
+        atomicAdd(&F.cnt[F.nranks], 1u);
+        const uint32_t t = atomicAdd(&hs->long_n, 1u);
+        if (t < F.long_cap) {                         // else the host grows the list and routes again
+            gw_long_move L;
+            L.slot = s;
+            L.reserved[0] = L.reserved[1] = L.reserved[2] = 0;
+            L.old_x = old_x;
+            L.old_z = w.rec[s].a.z;
+            L.new_x = oa.x;
+            L.new_z = oa.z;
+            L.old_stamp = w.rec[s].stamp;             // the pre-tick state: the tick has not run
+            L.new_stamp = stamps[la];
+            F.longs[t] = L;
+        }
+    }
     if (lng && F.rows) {
         // every other rank (not this one, not a neighbour) holding either end
         for (uint32_t q = 0; q < F.nranks; ++q) {
@@ -260,7 +278,7 @@ void launch_route_halo(const World& w, const gw_op* ops, const unsigned long lon
                        bool pad, unsigned long long* stamps_out, unsigned long long stamp_base, const HaloFar* far) {
     HaloFar F{};
     if (far) F = *far;
-    const uint32_t nb = nblk1(std::max<uint32_t>(n, F.nranks), NT);
+    const uint32_t nb = nblk1(std::max<uint32_t>(n, F.nranks + 1), NT);
     uint64_t rows = 0;                                   // NOP padding up to the capacity (fixed-size exchanges)
     if (pad)
         for (uint32_t d = 0; d < D.n; ++d) rows = std::max<uint64_t>(rows, (uint64_t)D.d[d].cap * ROWS);

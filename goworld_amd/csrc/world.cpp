@@ -64,6 +64,12 @@ int route_launch(gw_ctx* c, const gw_op* ops, uint32_t n, const HaloDsts& D, uin
     F.ext = P<float>(W.ext);
     F.nranks = W.g.ranks;
     F.self = W.g.rank;
+    if (!W.long_cap) {                                // the long-mover list (group teleports)
+        if (int rc = ensure(c, W.longs, 256 * sizeof(gw_long_move))) return rc;
+        W.long_cap = 256;
+    }
+    F.longs = P<gw_long_move>(W.longs);
+    F.long_cap = W.long_cap;
     // without a far buffer the long moves are still counted (F.rows null:
     // nothing placed); a rank of 1 or 2 strips has no far destination, but the
     // owner's own copy may still need its LEAVE row
@@ -81,27 +87,30 @@ int route_launch(gw_ctx* c, const gw_op* ops, uint32_t n, const HaloDsts& D, uin
     return 0;
 }
 
-// words of the routing's counts in WorldHost::pub_h: HaloStats first
+// words of the routing's counts in WorldHost::pub_h: HaloStats first, then
+// the 4 received counts (rows from left / right, long movers from left / right)
 constexpr size_t pub_off_cnt() { return (sizeof(HaloStats) + 3) / 4; }
+constexpr size_t RCNT = 4;
 
-// the routing's counts (HaloStats, and with rcnt the received counts and the
-// far matrix) into pub_h by one kernel, the host sync, then into hs / the vectors
+// the routing's counts (HaloStats, the far / long counts, and with rcnt the
+// received counts, with far_mat the all-gathered count vectors) into pub_h by
+// one kernel, the host sync, then into hs / the vectors
 int read_route_counts(gw_ctx* c, HaloStats& hs, uint32_t* rcnt, bool far_mat) {
     WorldHost& W = c->wd;
-    const uint32_t R = W.g.ranks;
-    const size_t o_cnt = pub_off_cnt(), o_far = o_cnt + 2, o_mat = o_far + R;
+    const uint32_t R = W.g.ranks, R1 = R + 1;
+    const size_t o_cnt = pub_off_cnt(), o_far = o_cnt + RCNT, o_mat = o_far + R1;
     PubSeg segs[4];
     int n = 0;
     segs[n++] = PubSeg{(const uint32_t*)c->halo, W.pub_d, (uint32_t)o_cnt};
-    segs[n++] = PubSeg{P<uint32_t>(W.far_cnt), W.pub_d + o_far, R};
-    if (rcnt) segs[n++] = PubSeg{P<uint32_t>(W.cnt), W.pub_d + o_cnt, 2};
-    if (far_mat) segs[n++] = PubSeg{P<uint32_t>(W.far_mat), W.pub_d + o_mat, R * R};
+    segs[n++] = PubSeg{P<uint32_t>(W.far_cnt), W.pub_d + o_far, R1};
+    if (rcnt) segs[n++] = PubSeg{P<uint32_t>(W.cnt), W.pub_d + o_cnt, (uint32_t)RCNT};
+    if (far_mat) segs[n++] = PubSeg{P<uint32_t>(W.far_mat), W.pub_d + o_mat, R * R1};
     publish_words(segs, n, c->st);
     HIPCHK(hipStreamSynchronize(c->st));
     memcpy(&hs, W.pub_h, sizeof hs);
-    memcpy(W.far_cnt_h.data(), W.pub_h + o_far, (size_t)R * 4);
-    if (rcnt) memcpy(rcnt, W.pub_h + o_cnt, 8);
-    if (far_mat) memcpy(W.far_mat_h.data(), W.pub_h + o_mat, (size_t)R * R * 4);
+    memcpy(W.far_cnt_h.data(), W.pub_h + o_far, (size_t)R1 * 4);
+    if (rcnt) memcpy(rcnt, W.pub_h + o_cnt, RCNT * 4);
+    if (far_mat) memcpy(W.far_mat_h.data(), W.pub_h + o_mat, (size_t)R * R1 * 4);
     return 0;
 }
 
@@ -112,12 +121,19 @@ int far_settle(gw_ctx* c, const gw_op* ops, uint32_t n, const HaloDsts& D, uint3
                HaloStats& hs) {
     WorldHost& W = c->wd;
     int rc;
-    if (hs.far_n > W.far_cap) {
-        const uint32_t cap = hs.far_n + hs.far_n / 2 + 64;
-        if ((rc = ensure(c, W.far_rows, (size_t)cap * ROWS * sizeof(gw_halo_row))) ||
-            (rc = ensure(c, W.far_dest, (size_t)cap * 4)))
-            return rc;
-        W.far_cap = cap;
+    if (hs.far_n > W.far_cap || hs.long_n > W.long_cap) {
+        if (hs.far_n > W.far_cap) {
+            const uint32_t cap = hs.far_n + hs.far_n / 2 + 64;
+            if ((rc = ensure(c, W.far_rows, (size_t)cap * ROWS * sizeof(gw_halo_row))) ||
+                (rc = ensure(c, W.far_dest, (size_t)cap * 4)))
+                return rc;
+            W.far_cap = cap;
+        }
+        if (hs.long_n > W.long_cap) {
+            const uint32_t cap = hs.long_n + hs.long_n / 2 + 64;
+            if ((rc = ensure(c, W.longs, (size_t)cap * sizeof(gw_long_move)))) return rc;
+            W.long_cap = cap;
+        }
         // the rerun places the same rows again; the accumulating counters
         // (overflow, conflicts, bad ops, long moves) must not count them twice
         unsigned long long keep[4] = {hs.overflow, hs.conflicts, hs.bad_ops, hs.long_moves};
@@ -125,8 +141,10 @@ int far_settle(gw_ctx* c, const gw_op* ops, uint32_t n, const HaloDsts& D, uint3
         HIPCHK(hipMemcpyAsync(c->halo, keep, sizeof keep, hipMemcpyHostToDevice, c->st));
         HIPCHK(hipMemcpyAsync(&hs, c->halo, sizeof hs, hipMemcpyDeviceToHost, c->st));
         HIPCHK(hipStreamSynchronize(c->st));
-        if (hs.far_n > W.far_cap) return set_err(c, GW_ENOMEM, "far halo rows overflowed twice");
+        if (hs.far_n > W.far_cap || hs.long_n > W.long_cap)
+            return set_err(c, GW_ENOMEM, "far halo rows / long-mover list overflowed twice");
     }
+    W.own_nlong = hs.long_n;
     uint32_t acc = 0;
     for (uint32_t q = 0; q < W.g.ranks; ++q) {
         W.far_off_h[q] = acc;
@@ -226,15 +244,15 @@ int gw_world_create(gw_ctx* c, const gw_world_geom* g, uint32_t capacity, const 
     // the world's buffers first: a failure leaves no space behind (a retry
     // must find the context empty, the strip's space at slot base 0)
     int rc2;
-    if ((rc2 = ensure(c, W.ext, W.ext_h.size() * 4)) || (rc2 = ensure(c, W.far_cnt, (size_t)g->ranks * 4)) ||
+    if ((rc2 = ensure(c, W.ext, W.ext_h.size() * 4)) || (rc2 = ensure(c, W.far_cnt, ((size_t)g->ranks + 1) * 4)) ||
         (rc2 = ensure(c, W.far_off, (size_t)g->ranks * 4)) || (rc2 = ensure(c, W.far_cursor, (size_t)g->ranks * 4)) ||
-        (rc2 = ensure(c, W.far_mat, (size_t)g->ranks * g->ranks * 4)))
+        (rc2 = ensure(c, W.far_mat, (size_t)g->ranks * (g->ranks + 1) * 4)))
         return rc2;
     HIPCHK(hipMemcpyAsync(W.ext.p, W.ext_h.data(), W.ext_h.size() * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     if (W.pub_h) (void)hipHostFree(W.pub_h);
     W.pub_h = W.pub_d = nullptr;
-    const size_t pub_words = pub_off_cnt() + 2 + g->ranks + (size_t)g->ranks * g->ranks;
+    const size_t pub_words = pub_off_cnt() + RCNT + (g->ranks + 1) + (size_t)g->ranks * (g->ranks + 1);
     if (hipHostMalloc((void**)&W.pub_h, pub_words * 4, hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&W.pub_d, W.pub_h, 0) != hipSuccess)
         return set_err(c, GW_ENOMEM, "world count buffer");
@@ -250,9 +268,12 @@ int gw_world_create(gw_ctx* c, const gw_world_geom* g, uint32_t capacity, const 
         c->err = keep;
         return rc;
     }
-    W.far_cnt_h.assign(g->ranks, 0);
+    W.far_cnt_h.assign(g->ranks + 1, 0);
     W.far_off_h.assign(g->ranks, 0);
-    W.far_mat_h.assign((size_t)g->ranks * g->ranks, 0);
+    W.far_mat_h.assign((size_t)g->ranks * (g->ranks + 1), 0);
+    W.own_nlong = 0;
+    W.tick_longs = nullptr;
+    W.tick_nlong = 0;
     W.far_cap = 0;
     W.sid = sid & SID_MASK;
     W.tick = 0;
@@ -368,25 +389,32 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
         W.kept_tag = tag;
     }
     HIPCHK(hipGetLastError());
-    const uint32_t R = W.g.ranks, me = W.g.rank;
+    const uint32_t R = W.g.ranks, me = W.g.rank, R1 = R + 1;
     const bool far_round = R >= 3;                    // ranks that are not neighbours exist
     uint32_t rcnt[2] = {0, 0};
     uint32_t far_in = 0;                              // triples received from far ranks
+    uint32_t n_long = 0;                              // long movers of all ranks (group teleports)
     if (any_nb) {
         // round 1: the entity counts (u32) both ways; HaloStats.cnt[k] is the
-        // k-th destination of D, i.e. left first when both exist
-        uint32_t* dcnt = P<uint32_t>(W.cnt);         // [0..1] received from left / right
+        // k-th destination of D, i.e. left first when both exist.  With two
+        // ranks the long-mover counts go along (with more, the all-gather)
+        uint32_t* dcnt = P<uint32_t>(W.cnt);         // [0..1] rows from left / right, [2..3] long movers
         if ((rc = xp_group_start(c))) return rc;
         uint32_t k = 0;
         for (int side = 0; side < 2; ++side) {
             if (W.nb[side] < 0) continue;
             (void)xp_send(c, &c->halo->cnt[k++], 4, W.nb[side]);
             (void)xp_recv(c, dcnt + side, 4, W.nb[side]);
+            if (!far_round) {
+                (void)xp_send(c, P<uint32_t>(W.far_cnt) + R, 4, W.nb[side]);
+                (void)xp_recv(c, dcnt + 2 + side, 4, W.nb[side]);
+            }
         }
         if ((rc = xp_group_end(c))) return rc;
-        // the far triples every rank sends every rank (long moves; R u32 each)
-        if (far_round && (rc = xp_allgather(c, W.far_cnt.p, W.far_mat.p, (size_t)R * 4))) return rc;
-        uint32_t h[4] = {0, 0, 0, 0};
+        // the far triples every rank sends every rank and its long-mover count
+        // (long moves; R + 1 u32 each)
+        if (far_round && (rc = xp_allgather(c, W.far_cnt.p, W.far_mat.p, (size_t)R1 * 4))) return rc;
+        uint32_t h[RCNT] = {0, 0, 0, 0};
         HaloStats hs{};
         if ((rc = read_route_counts(c, hs, h, far_round))) return rc;
         if ((rc = far_settle(c, ops, n, D, tag, base, hs))) return rc;
@@ -401,8 +429,23 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
         }
         if (far_round) {
             for (uint32_t p = 0; p < R; ++p)
-                if (p != me) far_in += W.far_mat_h[(size_t)p * R + me];
+                if (p != me) far_in += W.far_mat_h[(size_t)p * R1 + me];
             if (far_in && (rc = ensure(c, W.far_recv, (size_t)far_in * ROWS * sizeof(gw_halo_row)))) return rc;
+        }
+        // every rank's long-mover list into long_all, in rank order
+        auto nlong = [&](uint32_t p) -> uint32_t {
+            if (p == me) return W.own_nlong;
+            if (far_round) return W.far_mat_h[(size_t)p * R1 + R];
+            return h[2 + (p < me ? 0 : 1)];
+        };
+        for (uint32_t p = 0; p < R; ++p) n_long += nlong(p);
+        if (n_long) {
+            if ((rc = ensure(c, W.long_all, (size_t)n_long * sizeof(gw_long_move)))) return rc;
+            size_t off = 0;
+            for (uint32_t p = 0; p < me; ++p) off += nlong(p);
+            if (W.own_nlong)
+                HIPCHK(hipMemcpyAsync(P<gw_long_move>(W.long_all) + off, W.longs.p, (size_t)W.own_nlong *
+                                      sizeof(gw_long_move), hipMemcpyDeviceToDevice, c->st));
         }
         // round 2: exactly the used rows (neighbours), and the far triples
         if ((rc = xp_group_start(c))) return rc;
@@ -413,11 +456,23 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
             if (rcnt[side])
                 (void)xp_recv(c, W.recv[side].p, (size_t)rcnt[side] * ROWS * sizeof(gw_halo_row), W.nb[side]);
         }
+        if (n_long) {                                 // the long lists: everyone's to everyone
+            size_t off = 0;
+            for (uint32_t p = 0; p < R; ++p) {
+                const uint32_t np_ = nlong(p);
+                if (p != me && (far_round || p + 1 == me || p == me + 1)) {
+                    if (W.own_nlong) (void)xp_send(c, W.longs.p, (size_t)W.own_nlong * sizeof(gw_long_move), (int)p);
+                    if (np_)
+                        (void)xp_recv(c, P<gw_long_move>(W.long_all) + off, (size_t)np_ * sizeof(gw_long_move), (int)p);
+                }
+                off += np_;
+            }
+        }
         if (far_round) {
             size_t roff = 0;
             for (uint32_t p = 0; p < R; ++p) {
                 if (p == me) continue;
-                const uint32_t out = W.far_cnt_h[p], in = W.far_mat_h[(size_t)p * R + me];
+                const uint32_t out = W.far_cnt_h[p], in = W.far_mat_h[(size_t)p * R1 + me];
                 if (out)
                     (void)xp_send(c, P<gw_halo_row>(W.far_sorted) + (size_t)W.far_off_h[p] * ROWS,
                                   (size_t)out * ROWS * sizeof(gw_halo_row), (int)p);
@@ -441,6 +496,8 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
                                               self_n * ROWS)))
         return rc;
     if (far_in && (rc = gw_submit_device_rows(c, P<gw_halo_row>(W.far_recv), far_in * ROWS))) return rc;
+    W.tick_longs = n_long ? P<gw_long_move>(W.long_all) : nullptr;
+    W.tick_nlong = n_long;
     return 0;
 }
 
@@ -500,6 +557,25 @@ int gw_world_submit_far(gw_ctx* c, const gw_halo_row* rows, uint32_t n_rows) {
     if (W.routed || !W.submitted) return set_err(c, GW_ESTATE, "gw_world_submit first (far rows join its tick)");
     if (n_rows % ROWS) return set_err(c, GW_EINVAL, "%u rows: not whole entities", n_rows);
     return gw_submit_device_rows(c, rows, n_rows);
+}
+
+int gw_world_longs(gw_ctx* c, const gw_long_move** rows, uint32_t* n) {
+    if (!c) return GW_EINVAL;
+    WorldHost& W = c->wd;
+    if (!W.on) return set_err(c, GW_ESTATE, "no world strip (gw_world_create)");
+    if (rows) *rows = W.own_nlong ? P<gw_long_move>(W.longs) : nullptr;
+    if (n) *n = W.own_nlong;
+    return 0;
+}
+
+int gw_world_submit_longs(gw_ctx* c, const gw_long_move* rows, uint32_t n) {
+    if (!c || (n && !rows)) return GW_EINVAL;
+    WorldHost& W = c->wd;
+    if (!W.on) return set_err(c, GW_ESTATE, "no world strip (gw_world_create)");
+    if (W.routed || !W.submitted) return set_err(c, GW_ESTATE, "gw_world_submit first (the lists join its tick)");
+    W.tick_longs = n ? rows : nullptr;
+    W.tick_nlong = n;
+    return 0;
 }
 
 int gw_world_status(gw_ctx* c, uint64_t* overflow, uint64_t* conflicts, uint64_t* bad_ops) {

@@ -194,6 +194,26 @@ def exchange_far(pg, rank: int, ranks: int, far: dict, device, comm_device):
     return [back(t) for t in out]
 
 
+def exchange_longs(pg, rank: int, ranks: int, mine: np.ndarray) -> np.ndarray:
+    """Host-transport all-gather of the long-mover lists (gw_long_move rows,
+    group teleports; gloo for the CPU tests and one-GPU rehearsals): every
+    rank's list, concatenated in rank order."""
+    import torch.distributed as dist
+    from .traces import LONG_DTYPE
+    raw = torch.from_numpy(np.ascontiguousarray(mine, LONG_DTYPE).view(np.uint8).copy())
+    cnt = torch.tensor([raw.numel()], dtype=torch.int64)
+    allc = [torch.zeros(1, dtype=torch.int64) for _ in range(ranks)]
+    dist.all_gather(allc, cnt, group=pg)
+    mx = max(int(c.item()) for c in allc)
+    if mx == 0:
+        return np.zeros(0, LONG_DTYPE)
+    pad = torch.zeros(mx, dtype=torch.uint8)
+    pad[:raw.numel()] = raw
+    bufs = [torch.zeros(mx, dtype=torch.uint8) for _ in range(ranks)]
+    dist.all_gather(bufs, pad, group=pg)
+    return np.concatenate([b[:int(c.item())].numpy() for b, c in zip(bufs, allc)]).view(LONG_DTYPE)
+
+
 class HipStrip:
     """Engine adapter over the library's decomposed world (gw_world_*): a
     gpuaoi.GpuAOI context sharing one stream with torch (made torch's current
@@ -245,7 +265,16 @@ class HipStrip:
             out[q] = torch.from_numpy(buf)
         return out
 
-    def submit(self, words: torch.Tensor, stamps, recvd, far_in=()):
+    def longs(self) -> np.ndarray:
+        """This rank's long-mover list of the last route (gw_long_move rows, host copy)."""
+        from .traces import LONG_DTYPE
+        ptr, n = self.g.world_longs()
+        out = np.zeros(n, LONG_DTYPE)
+        if n:
+            self.g.d2h(out, ptr)
+        return out
+
+    def submit(self, words: torch.Tensor, stamps, recvd, far_in=(), longs=None):
         rows = []
         dev = torch.device("cuda", torch.cuda.current_device())
         for r in recvd:
@@ -262,6 +291,10 @@ class HipStrip:
             r = r.to(device=dev, dtype=torch.int32).contiguous()
             self._keep.append(r)
             self.g.world_submit_far(r.data_ptr(), r.shape[0])
+        if longs is not None and len(longs):           # every rank's long-mover list for the tick
+            t = torch.from_numpy(np.ascontiguousarray(longs).view(np.uint8).copy()).to(dev)
+            self._keep.append(t)
+            self.g.world_submit_longs(t.data_ptr(), len(longs))
 
     def tick(self, copy=True, no_events=False, defer=False):
         res = self.g.tick(copy=copy, no_events=no_events, defer=defer)
@@ -311,13 +344,15 @@ class StripRank:
             st = stamps_for(self.tick_no, self.r, self.g.ranks, m, self.dev)
             sends = self.e.route(words, st)
             far = self.e.far()
+            lg = self.e.longs()
             if self.g.ranks > 1:
                 recvd = exchange_rows(self.pg, self.r, self.g.ranks, sends, self.dev, self.cdev)
                 far_in = exchange_far(self.pg, self.r, self.g.ranks, far, self.dev, self.cdev)
+                lg = exchange_longs(self.pg, self.r, self.g.ranks, lg)
             else:
                 recvd = [None, None]
                 far_in = [far[self.r]] if self.r in far else []
-            self.e.submit(words, st, recvd, far_in)
+            self.e.submit(words, st, recvd, far_in, longs=lg)
         self.tick_no += 1
 
     def tick(self, copy=True, **kw):
@@ -416,6 +451,7 @@ class LocalWorld:
             if times is not None:
                 times[r] += time.perf_counter() - t0
         fars = [g.world_far() for g in self.g]                   # long moves: {dest: (ptr, rows)}
+        lptr = self._longs_all()                                   # every rank's long-mover list
         rows = 0
         for r, g in enumerate(self.g):
             left = sends[r - 1][1] if r > 0 else (0, 0)           # left neighbour's rows to its right
@@ -427,7 +463,33 @@ class LocalWorld:
                     ptr, n = fars[p][r]
                     g.world_submit_far(ptr, n)
                     rows += n
+            if lptr[1]:
+                g.world_submit_longs(*lptr)
         return rows
+
+    def _longs_all(self):
+        """The ranks' long-mover lists of the last route concatenated into one
+        device buffer (all contexts share the device): (ptr, n)."""
+        from .traces import LONG_DTYPE
+        parts = []
+        for g in self.g:
+            ptr, n = g.world_longs()
+            if n:
+                a = np.zeros(n, LONG_DTYPE)
+                g.d2h(a, ptr)
+                parts.append(a)
+        if not parts:
+            return 0, 0
+        allv = np.concatenate(parts)
+        cap, ptr = getattr(self, "_lbuf", (0, 0))
+        if allv.nbytes > cap:
+            if ptr:
+                self.g[0].dev_free(ptr)
+            cap = 2 * allv.nbytes
+            ptr = self.g[0].dev_alloc(cap)
+            self._lbuf = (cap, ptr)
+        self.g[0].h2d(ptr, allv)
+        return ptr, len(allv)
 
     def check(self):
         for r, g in enumerate(self.g):
@@ -439,6 +501,9 @@ class LocalWorld:
         for r, p in self.bufs:
             self.g[r].dev_free(p)
         self.bufs = []
+        if getattr(self, "_lbuf", (0, 0))[1]:
+            self.g[0].dev_free(self._lbuf[1])
+            self._lbuf = (0, 0)
         for g in self.g:
             g.close()
 

@@ -20,7 +20,7 @@ import os
 
 import numpy as np
 
-from .traces import OP_DTYPE
+from .traces import LONG_DTYPE, OP_DTYPE
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # GW_LIB_PATH selects another build of the same library (A/B experiments)
@@ -166,6 +166,8 @@ def lib():
         L.gw_world_status.argtypes = [vp, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64)]
         L.gw_world_far.argtypes = [vp, C.POINTER(vp), C.POINTER(C.POINTER(_u32))]
         L.gw_world_submit_far.argtypes = [vp, vp, _u32]
+        L.gw_world_longs.argtypes = [vp, C.POINTER(vp), C.POINTER(_u32)]
+        L.gw_world_submit_longs.argtypes = [vp, vp, _u32]
         L.gw_world_stage_ops.argtypes = [vp, vp, _u32, C.POINTER(vp)]
         L.gw_world_step_host.argtypes = [vp, vp, _u32]
         L.gw_set_entity_ids.argtypes = [vp, vp, vp, _u32]
@@ -189,7 +191,7 @@ EXPORTED = ["gw_abi_version", "gw_init", "gw_shutdown", "gw_last_error", "gw_spa
             "gw_world_submit", "gw_world_status", "gw_set_entity_ids", "gw_clear_entity_ids", "gw_set_client_ids",
             "gw_set_client_syncing", "gw_submit_client_sync", "gw_sync_encode_wire", "gw_space_grow",
             "gw_context_info", "gw_world_far", "gw_world_submit_far", "gw_world_stage_ops",
-            "gw_world_step_host", "gw_comm_init_local"]
+            "gw_world_step_host", "gw_comm_init_local", "gw_world_longs", "gw_world_submit_longs"]
 
 
 def comm_init_local(ctxs) -> None:
@@ -623,6 +625,16 @@ class GpuAOI:
     def world_submit_far(self, dev_rows: int, n_rows: int):
         """Queue far rows received for this tick (after world_submit)."""
         self._chk(lib().gw_world_submit_far(self._h, C.c_void_p(dev_rows), n_rows))
+
+    def world_longs(self) -> tuple[int, int]:
+        """After world_route: (device ptr, n) of this rank's long-mover list (gw_long_move)."""
+        p, n = C.c_void_p(), _u32()
+        self._chk(lib().gw_world_longs(self._h, C.byref(p), C.byref(n)))
+        return p.value or 0, n.value
+
+    def world_submit_longs(self, dev_ptr: int, n: int):
+        """Queue every rank's long-mover lists for this tick (after world_submit; device memory)."""
+        self._chk(lib().gw_world_submit_longs(self._h, C.c_void_p(dev_ptr or None), n))
 
     def world_status(self) -> tuple[int, int, int]:
         """(halo overflows, long-move conflicts, bad ops), summed over ranks."""

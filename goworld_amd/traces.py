@@ -32,6 +32,9 @@ OP_DTYPE = np.dtype([("kind", "u1"), ("sync_flags", "u1"), ("reserved", "<u2"),
                      ("slot", "<u4"), ("x", "<f4"), ("y", "<f4"), ("z", "<f4"),
                      ("yaw", "<f4")])
 assert OP_DTYPE.itemsize == 24
+# gw_long_move (include/gpuaoi.h): a long mover's state before and after a tick
+LONG_DTYPE = np.dtype([("slot", "<u4"), ("reserved", "<u4", (3,)), ("old_x", "<f4"), ("old_z", "<f4"),
+                       ("new_x", "<f4"), ("new_z", "<f4"), ("old_stamp", "<u8"), ("new_stamp", "<u8")])
 
 OP_ENTER, OP_MOVED, OP_LEAVE, OP_SYNC = 1, 2, 3, 4
 SIF_OWN, SIF_NEIGHBOR = 1, 2
@@ -420,7 +423,8 @@ class StripTrace:
 
 def strip_world_trace(seed: int, n: int, ranks: int, strip_w: float, height: float, d: float,
                       ticks: int, max_step: float, move_frac: float = 0.5,
-                      churn: bool = True, edge_frac: float = 0.2, teleports: int = 0) -> StripTrace:
+                      churn: bool = True, edge_frac: float = 0.2, teleports: int = 0,
+                      groups: int = 0) -> StripTrace:
     """Random walk across strips (entities migrate between ranks) with churn:
     Leave, re-Enter anywhere, Leave + re-Enter nearby inside one tick, two
     moves of one entity in one tick, Sync ops.  Positions are dyadic except
@@ -428,9 +432,13 @@ def strip_world_trace(seed: int, n: int, ranks: int, strip_w: float, height: flo
     border entity (x = border +- d, +-1 ulp).  `teleports` > 0: up to that
     many present entities per tick jump anywhere in the world (a Moved op far
     beyond max_step: Entity.SetPosition has no step bound, Entity.go:1185-1187),
-    chosen so that no two of them are related before or after the tick (a
-    pair of related entities that both jump is not supported by the strip
-    decomposition)."""
+    chosen so that no two of them are related before or after the tick.
+    `groups` > 0: that many group teleports per tick besides (Entity.SetPosition
+    of several related entities in one tick; enterLocalSpace moves entities
+    together, Entity.go:975-998), by turns: an entity and up to two neighbours
+    within d jump by the same far offset (related before and after), jump to
+    separate far places (related before only), or two entities far apart jump
+    next to each other (related after only)."""
     W = ranks * strip_w
     step_q = int(max_step * Q) // 2          # half a step per move, <= 2 moves per tick
     lo_q, hi_q = 0, int(W * Q)
@@ -524,6 +532,63 @@ def strip_world_trace(seed: int, n: int, ranks: int, strip_w: float, height: flo
             tp = cand[jumps]
             x[tp], z[tp] = tx[jumps], tz[jumps]
             emit(rows1, OP_MOVED, SIF_NEIGHBOR | SIF_OWN, tp, x[tp], z[tp], yaw[tp])
+        if groups:
+            taken = set(tp.tolist()) if teleports else set()
+            cand = [i for i in ids[pres & (u >= move_frac + 0.1) & (u < 0.97)].tolist() if i not in taken]
+            perm = np.argsort(rand_u64(stream_key(seed, 112, t), len(cand)), kind="stable")
+            cand = [cand[k] for k in perm.tolist()]
+            far = 2 * d + 4 * max_step
+            rx = rand_int(stream_key(seed, 113, t), 64 * groups, lo_q, hi_q) / Q
+            rz = rand_int(stream_key(seed, 114, t), 64 * groups, zlo_q, zhi_q) / Q
+            ro = (rand_int(stream_key(seed, 115, t), 64 * groups, -int(d / 2 * Q), int(d / 2 * Q) + 1) / Q)
+            draw = iter(range(64 * groups))
+            used, gids, gx, gz = set(), [], [], []
+
+            def far_spot(i):                       # a random place a teleport away from entity i
+                for k in draw:
+                    if abs(rx[k] - float(x[i])) > far:
+                        return float(rx[k]), float(rz[k]), k
+                return None
+            for gi in range(groups):
+                s0 = next((i for i in cand if i not in used), None)
+                if s0 is None:
+                    break
+                mode = gi % 3
+                if mode < 2:
+                    mem = [s0] + [i for i in cand if i not in used and i != s0 and abs(float(x[i] - x[s0])) <= d
+                                  and abs(float(z[i] - z[s0])) <= d][:2]
+                else:
+                    mem = [s0] + [i for i in cand if i not in used and i != s0 and
+                                  abs(float(x[i] - x[s0])) > far + d][:1]
+                spot = far_spot(s0)
+                if spot is None or len(mem) < 2:
+                    used.add(s0)
+                    continue
+                tx0, tz0, k0 = spot
+                for j, i in enumerate(mem):
+                    if mode == 0:                      # together: the same offset
+                        nx_, nz_ = float(x[i]) + tx0 - float(x[s0]), float(z[i]) + tz0 - float(z[s0])
+                    elif mode == 1 and j:              # split: a separate far place each
+                        sp = far_spot(i)
+                        if sp is None:
+                            continue
+                        nx_, nz_ = sp[0], sp[1]
+                    elif mode == 2 and j:              # merge: next to the first one's destination
+                        nx_, nz_ = tx0 + float(ro[k0]), tz0 + float(ro[(k0 + 1) % len(ro)])
+                    else:
+                        nx_, nz_ = tx0, tz0
+                    nx_ = float(np.float32(min(max(nx_, 0.0), W - 1.0)))
+                    nz_ = float(np.float32(min(max(nz_, 0.0), height - 1.0)))
+                    if abs(nx_ - float(x[i])) <= far:     # clipped back near: not a teleport
+                        continue
+                    used.add(i)
+                    gids.append(i); gx.append(nx_); gz.append(nz_)
+                used.add(s0)
+            if gids:
+                gi_ = np.array(gids, np.int64)
+                x[gi_] = np.array(gx, np.float32)
+                z[gi_] = np.array(gz, np.float32)
+                emit(rows1, OP_MOVED, SIF_NEIGHBOR | SIF_OWN, gi_, x[gi_], z[gi_], yaw[gi_])
         enter_owner = {}
         if churn:
             lv = ids[pres & (u >= 0.97) & (u < 0.985)]            # leave for a while

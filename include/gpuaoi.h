@@ -545,19 +545,42 @@ int  gw_world_step_host(gw_ctx* ctx, const gw_op* ops, uint32_t n);
  * the counts before q; counts has `ranks` entries, this rank's own LEAVE rows
  * under its own rank); the caller delivers them and every rank queues what it
  * received (its own included) with gw_world_submit_far after gw_world_submit
- * (device memory, valid until the tick).  Events of a long mover's pairs are
- * emitted by the owner of the other member; two entities that both move more
- * than max_step in one tick and are related before or after it (a group
- * teleport) are not supported: counted as conflicts by gw_world_status. */
+ * (device memory, valid until the tick).  Events of a long mover's pairs with
+ * entities that are not long movers are emitted by the owner of the other
+ * member; pairs of two long movers (a group teleport) by the owner of the
+ * watcher's new position, from the long lists (gw_world_longs below). */
 int  gw_world_far(gw_ctx* ctx, const gw_halo_row** rows, const uint32_t** counts);
 int  gw_world_submit_far(gw_ctx* ctx, const gw_halo_row* rows, uint32_t n_rows);
+/* Group teleports (Entity.SetPosition of several related entities in one
+ * tick, Entity.go:1185; enterLocalSpace moves entities together, Entity.go:
+ * 975-998): a pair of long movers may be related before the tick on one rank
+ * and after it on another, so no rank holds both ends of the pair.  Every long
+ * mover is therefore also listed once, by its owner, with its state before
+ * and after the tick (position and the stamp of its last AOI op); all ranks
+ * receive every rank's list, and the owner of each long mover's new position
+ * evaluates its pairs with the other long movers from the lists (the seq rule
+ * of DESIGN.md §2 needs only those positions and stamps) and emits its events.
+ * gw_world_step exchanges the lists itself.  On the caller's transport: after
+ * gw_world_route, gw_world_longs gives this rank's list (device memory,
+ * *n entries); the caller all-gathers the lists and queues the concatenation
+ * of all ranks' lists (its own included, any order) with gw_world_submit_longs
+ * after gw_world_submit (device memory, valid until the tick). */
+typedef struct gw_long_move {
+    uint32_t slot;                    /* global entity id                       */
+    uint32_t reserved[3];
+    float    old_x, old_z, new_x, new_z;
+    uint64_t old_stamp, new_stamp;    /* stamps of its last AOI op before / after */
+} gw_long_move;
+int  gw_world_longs(gw_ctx* ctx, const gw_long_move** rows, uint32_t* n);
+int  gw_world_submit_longs(gw_ctx* ctx, const gw_long_move* rows, uint32_t n);
 /* Contract counters since the last call, summed over ranks when a
  * communicator exists: halo overflows (0 by construction), long-move
- * conflicts (see gw_world_far), ops with an invalid slot or kind. */
+ * conflicts (pairs of long movers the lists did not cover: 0 unless a rank's
+ * long list was not queued for its tick), ops with an invalid slot or kind. */
 int  gw_world_status(gw_ctx* ctx, uint64_t* overflow, uint64_t* conflicts, uint64_t* bad_ops);
 
 /* ABI version (bumped on layout changes). */
-#define GW_ABI_VERSION 14
+#define GW_ABI_VERSION 15
 int  gw_abi_version(void);
 
 #ifdef __cplusplus

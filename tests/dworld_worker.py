@@ -35,6 +35,7 @@ class OracleStrip:
         self.max_step = np.float32(geom.max_step)
         self.router = torch_router.Router(geom, rank, n_global, torch.device("cpu"), n_global)
         self.o = self.pyorc.OracleSpace(n_global, geom.d, self.pyorc.SEQRULE)
+        self.o_d = geom.d
         self.x = np.zeros(n_global, np.float32)
         self.present = np.zeros(n_global, bool)
         self.lo, self.hi = (np.float32(v) for v in geom.own_range_f32(rank))
@@ -46,7 +47,11 @@ class OracleStrip:
     def far(self):
         return self.router.far_exact()
 
-    def submit(self, words, stamps, recvd=(), far_in=()):
+    def longs(self):
+        return self.router.longs_exact()
+
+    def submit(self, words, stamps, recvd=(), far_in=(), longs=None):
+        self.tick_longs = longs
         self.words.append(words.cpu().numpy())
         self.stamps.append(stamps.cpu().numpy())
         for rows in list(recvd) + list(far_in):
@@ -98,7 +103,33 @@ class OracleStrip:
         def mine(ev):
             wt, tg = ev["watcher"], ev["target"]
             return ev[(own[wt] & ~lng[wt]) | (lng[wt] & own[tg] & ~lng[tg])].copy()
-        return _Res(enter=mine(e), leave=mine(l))
+        enter, leave = mine(e), mine(l)
+        # pairs of two long movers (group teleports): from every rank's long
+        # list, by the owner of the watcher's new position (the engine's rule)
+        L = getattr(self, "tick_longs", None)
+        self.tick_longs = None
+        if L is not None and len(L):
+            d = np.float32(self.o_d)
+
+            def rel(ax, az, as_, bx, bz, bs):
+                cx, cz, ox, oz = (ax, az, bx, bz) if as_ > bs else (bx, bz, ax, az)
+                return (ox >= np.float32(cx - d)) and (ox <= np.float32(cx + d)) and \
+                       (oz >= np.float32(cz - d)) and (oz <= np.float32(cz + d))
+            ee, ll = [], []
+            for a in L:
+                if not self._owned(np.float32(a["new_x"])):
+                    continue
+                for b in L:
+                    if b["slot"] == a["slot"]:
+                        continue
+                    ro = rel(a["old_x"], a["old_z"], int(a["old_stamp"]), b["old_x"], b["old_z"], int(b["old_stamp"]))
+                    rn = rel(a["new_x"], a["new_z"], int(a["new_stamp"]), b["new_x"], b["new_z"], int(b["new_stamp"]))
+                    if ro != rn:
+                        (ll if ro else ee).append((int(a["slot"]), int(b["slot"])))
+            ev_t = enter.dtype
+            enter = np.concatenate([enter, np.array(ee, dtype=np.uint32).reshape(-1, 2).view(ev_t).reshape(-1)])
+            leave = np.concatenate([leave, np.array(ll, dtype=np.uint32).reshape(-1, 2).view(ev_t).reshape(-1)])
+        return _Res(enter=enter, leave=leave)
 
     def collect(self, copy=True):
         r = self.o.collect()
@@ -132,6 +163,7 @@ def main():
     ap.add_argument("--trace", choices=["strip", "walk"], default="strip")
     ap.add_argument("--side", type=float, default=36864.0, help="walk: world side")
     ap.add_argument("--teleports", type=int, default=0, help="strip: jumps anywhere per tick")
+    ap.add_argument("--groups", type=int, default=0, help="strip: group teleports per tick")
     a = ap.parse_args()
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{a.port}", rank=a.rank,
                             world_size=a.world)
@@ -139,7 +171,7 @@ def main():
         tr = T.walk_strip_trace(a.seed, a.n, a.side, a.world, a.ticks)
     else:
         tr = T.strip_world_trace(a.seed, a.n, a.world, a.strip_w, a.height, a.d, a.ticks, a.max_step,
-                                 teleports=a.teleports)
+                                 teleports=a.teleports, groups=a.groups)
     geom = dworld.Strips(0.0, tr.strip_w, a.world, tr.d, tr.max_step)
     if a.engine == "oracle":
         eng, dev = OracleStrip(), torch.device("cpu")

@@ -31,13 +31,14 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version_and_layouts():
-    assert gpuaoi.lib().gw_abi_version() == 14
+    assert gpuaoi.lib().gw_abi_version() == 15
     assert ctypes.sizeof(gpuaoi.CtxInfo) == 24
     assert ctypes.sizeof(gpuaoi.WireOut) == 7 * 8
     assert ctypes.sizeof(gpuaoi.Xfer) == 40 and ctypes.sizeof(gpuaoi.WorldGeom) == 24
     assert gpuaoi.FANOUT_DTYPE.itemsize == 12
     assert ctypes.sizeof(gpuaoi.MsgOut) == 7 * 8
     assert ctypes.sizeof(gpuaoi.HaloDst) == 24
+    assert traces.LONG_DTYPE.itemsize == 48            # gw_long_move
     assert traces.OP_DTYPE.itemsize == 24
     assert gpuaoi.EVENT_DTYPE.itemsize == 8
     assert gpuaoi.REC_DTYPE.itemsize == 24

@@ -74,7 +74,8 @@ TELEPORT = dict(TRACE, teleports=3)
 
 def _check(world, results, trace=TRACE):
     tr = T.strip_world_trace(trace["seed"], trace["n"], world, trace["strip_w"], trace["height"],
-                             trace["d"], trace["ticks"], trace["max_step"], teleports=trace.get("teleports", 0))
+                             trace["d"], trace["ticks"], trace["max_step"], teleports=trace.get("teleports", 0),
+                             groups=trace.get("groups", 0))
     o = pyorc.OracleSpace(tr.n, tr.d, pyorc.SEQRULE)
     o.set_clients(tr.gates)
     n_ev = n_rec = 0
@@ -161,6 +162,55 @@ def test_dworld_gpu_teleports(world, tmp_path):
     """The same with the HIP engine per rank (gw_world_route / gw_world_far /
     gw_world_submit_far over gloo), ranks sharing the GPU."""
     _check(world, _run_ranks(world, "hip", tmp_path, timeout=100, args=TELEPORT), trace=TELEPORT)
+
+
+GROUPS = dict(TRACE, teleports=2, groups=6)
+
+
+def _long_pairs(world, trace):
+    """Pairs of entities that both jump (long moves) in one tick and are related
+    before or after it (by the oracle's relation), over the trace."""
+    tr = T.strip_world_trace(trace["seed"], trace["n"], world, trace["strip_w"], trace["height"], trace["d"],
+                             trace["ticks"], trace["max_step"], teleports=trace["teleports"], groups=trace["groups"])
+    o = pyorc.OracleSpace(tr.n, tr.d, pyorc.SEQRULE)
+    x = np.zeros(tr.n, np.float32)
+    pres = np.zeros(tr.n, bool)
+    both = 0
+    for t in range(len(tr.ticks)):
+        ops = tr.global_ops(t)
+        before = {s: set(o.neighbors(s).tolist()) for s in range(tr.n) if pres[s]}
+        mv = ops[(ops["kind"] == T.OP_MOVED)]
+        far = set(int(op["slot"]) for op in mv if pres[op["slot"]] and abs(float(op["x"]) - float(x[op["slot"]])) >
+                  tr.max_step)
+        assert o.tick(ops) == 0
+        for op in ops:
+            if op["kind"] in (T.OP_ENTER, T.OP_MOVED):
+                x[op["slot"]], pres[op["slot"]] = op["x"], True
+            elif op["kind"] == T.OP_LEAVE:
+                pres[op["slot"]] = False
+        for a in far:
+            after = set(o.neighbors(a).tolist())
+            both += len((before.get(a, set()) | after) & far)
+    o.close()
+    return both // 2
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_dworld_gloo_oracle_group_teleports(world, tmp_path):
+    """Group teleports (related entities jumping in one tick: together,
+    apart, or next to each other) across strips: the long-mover lists carry
+    every long mover's state before and after the tick to every rank, and
+    the union of the ranks' outputs still equals one global oracle space."""
+    assert _long_pairs(world, GROUPS) >= 20            # the trace has related long-mover pairs
+    _check(world, _run_ranks(world, "oracle", tmp_path, args=GROUPS), trace=GROUPS)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_dworld_gpu_group_teleports(world, tmp_path):
+    """The same with the HIP engine per rank (gw_world_route / gw_world_far /
+    gw_world_longs / gw_world_submit_longs over gloo), ranks sharing the GPU."""
+    _check(world, _run_ranks(world, "hip", tmp_path, timeout=100, args=GROUPS), trace=GROUPS)
 
 
 WALK_SMALL = dict(trace="walk", seed=9, n=20000, side=6144.0, ticks=5)
@@ -386,7 +436,7 @@ def test_hip_router_rows_match_torch_router():
         eng = dworld.HipStrip(g)
         eng.create_world(geom, 1, tr.n, tr.bounds)
         ref = torch_router.Router(geom, 1, tr.n, dev, tr.n)
-        n_rows = 0
+        n_rows = n_long = 0
         for t in range(len(tr.ticks)):
             w = torch.from_numpy(dworld.ops_to_words(tr.rank_ops(t, 1)).copy()).to(dev)
             st = dworld.stamps_for(t, 1, 3, w.shape[0], dev)
@@ -395,6 +445,10 @@ def test_hip_router_rows_match_torch_router():
                 assert ca.shape == cb.shape, (t, side, ca.shape, cb.shape)
                 assert ca.tobytes() == cb.tobytes(), f"tick {t} side {side}: halo rows differ"
                 n_rows += len(ca)
+            # the long-mover list (group teleports) equals the torch statement's
+            la, lb = eng.longs(), ref.longs_exact()
+            assert np.array_equal(np.sort(la, order="slot"), np.sort(lb, order="slot")), f"tick {t}: long lists"
+            n_long += len(la)
             eng.submit(w, st, [None, None])
             eng.tick(copy=False)
             if t % 3 == 2:
@@ -403,8 +457,8 @@ def test_hip_router_rows_match_torch_router():
         assert n_rows > 300
         # no overflow; the same long moves (entities that come back after ticks
         # owned elsewhere, whose ghost rows this lone rank never got)
-        ov, n_long, bad = eng.g.halo_status()
-        assert ov == 0 and bad == 0 and n_long == ref.long_count() > 0
+        ov, n_long_moves, bad = eng.g.halo_status()
+        assert ov == 0 and bad == 0 and n_long_moves == ref.long_count() > 0 and n_long > 0
         # invalid slots are counted, never followed
         bad = w.clone()
         bad[:, 1] = tr.n + 5

@@ -30,12 +30,15 @@ class Router:
         self.g, self.r, self.n, self.dev, self.K = geom, rank, n_global, device, halo_cap
         n1 = n_global + 1
         self.x = torch.zeros(n1, dtype=torch.float32, device=device)
+        self.z = torch.zeros(n1, dtype=torch.float32, device=device)
+        self.stamp = torch.zeros(n1, dtype=torch.int64, device=device)    # of the last AOI op
         self.present = torch.zeros(n1, dtype=torch.bool, device=device)
         self.pflags = torch.zeros(n1, dtype=torch.int32, device=device)
         self.scratch = torch.full((n1,), -1, dtype=torch.int64, device=device)
         self.overflow = torch.zeros((), dtype=torch.int64, device=device)
         self.long_moves = torch.zeros((), dtype=torch.int64, device=device)
         self.last_far = {}
+        self.last_longs = None
         self.ext_lo, self.ext_hi = geom.ext(rank)
         self.lo, self.hi = geom.lo(rank), geom.hi(rank)
 
@@ -84,9 +87,13 @@ class Router:
         la_c, lp_c = la.clamp(min=0), lp.clamp(min=0)
         ka = kind[la_c]
         xa = _f32(words[:, 2])[la_c]
+        za = _f32(words[:, 4])[la_c]
         old_x, old_p, old_f = self.x[slot], self.present[slot], self.pflags[slot]
+        old_z, old_s = self.z[slot], self.stamp[slot]
         new_p = torch.where(has_aoi, ka != OP_LEAVE, old_p)
         new_x = torch.where(has_aoi & new_p, xa, old_x)
+        new_z = torch.where(has_aoi & new_p, za, old_z)
+        new_s = torch.where(has_aoi, stamps[la_c], old_s)
         new_f = torch.zeros_like(old_f)
         for c in range(2):
             bit = (flags >> c) & 1
@@ -101,6 +108,17 @@ class Router:
         moved = rep & has_aoi & old_p & new_p
         lng = moved & ((new_x - old_x).abs() > g.max_step)
         self.long_moves += lng.sum()
+        # the long-mover list (group teleports): state before and after the tick
+        from goworld_amd.traces import LONG_DTYPE
+        import numpy as np
+        li = torch.nonzero(lng).flatten()
+        lst = np.zeros(int(li.numel()), LONG_DTYPE)
+        if li.numel():
+            lst["slot"] = slot[li].cpu().numpy()
+            lst["old_x"], lst["old_z"] = old_x[li].cpu().numpy(), old_z[li].cpu().numpy()
+            lst["new_x"], lst["new_z"] = new_x[li].cpu().numpy(), new_z[li].cpu().numpy()
+            lst["old_stamp"], lst["new_stamp"] = old_s[li].cpu().numpy(), new_s[li].cpu().numpy()
+        self.last_longs = lst
         sends = []
         self.last_used = []
         self.last_far = {}
@@ -148,6 +166,8 @@ class Router:
         # routing state of the rows this rank owns (dummy row n absorbs the rest)
         s = torch.where(rep, slot, torch.full_like(slot, self.n))
         self.x[s] = new_x
+        self.z[s] = new_z
+        self.stamp[s] = new_s
         self.present[s] = new_p
         self.pflags[s] = new_f
         return sends[0], sends[1]
@@ -197,17 +217,25 @@ class Router:
         kany = (rows[:, 0, 0] | rows[:, 1, 0] | rows[:, 2, 0]) & 0xFF
         slot = torch.maximum(torch.maximum(rows[:, 0, 1], rows[:, 1, 1]), rows[:, 2, 1]).to(torch.int64)
         slot = torch.where(kany != 0, slot, torch.full_like(slot, self.n))
-        cur_x, cur_p = self.x[slot], self.present[slot]
+        cur_x, cur_p, cur_z, cur_s = self.x[slot], self.present[slot], self.z[slot], self.stamp[slot]
         p = torch.where(k1 != 0, k1 != OP_LEAVE, cur_p)
         x = torch.where((k1 != 0) & p, _f32(rows[:, 1, 2]), cur_x)
+        zz = torch.where((k1 != 0) & p, _f32(rows[:, 1, 4]), cur_z)
+        st = torch.where(k1 != 0, rows[:, 1, 6:8].contiguous().view(torch.int64).view(-1), cur_s)
         f = torch.where(k2 != 0, f2, torch.zeros_like(f2))
         self.x[slot] = x
+        self.z[slot] = zz
+        self.stamp[slot] = st
         self.present[slot] = p
         self.pflags[slot] = f
 
     def collected(self):
         """Sync flags are cleared everywhere by a collect (Entity.go:1221-1267)."""
         self.pflags.zero_()
+
+    def longs_exact(self):
+        """This rank's long-mover list of the last route() (gw_long_move rows)."""
+        return self.last_longs
 
     def far_exact(self) -> dict:
         """Rows of the last route() for ranks that are not neighbours (long

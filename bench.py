@@ -308,14 +308,24 @@ def cpu_baseline(tr, max_seconds):
             **cpu_info()}
 
 
-def cpu_baseline_mt(seconds, entities, side):
+def cpu_quota():
+    """CPU cores the cgroup grants this job (cpu.max quota / period), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline_mt(seconds, entities, side, threads=None):
     """Fairness point: oracle/gridmt.c, a multi-threaded (OpenMP)
-    uniform-grid CPU implementation of the same batched tick + collect, on the
-    host cores this job may use (OMP_NUM_THREADS; 16 per GPU on the box), over
-    config #3 ticks until the time budget is spent."""
+    uniform-grid CPU implementation of the same batched tick + collect, over
+    config #3 ticks until the time budget is spent.  threads: by default the
+    job's share (OMP_NUM_THREADS, 16 per GPU on the box); main() also runs it
+    on every core the process may use (sched_getaffinity)."""
     from oracle import pyorc
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = min(threads, 16)
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     tr = traces.config3(ticks=8, seed=3, n=entities, side=side)
     m = pyorc.GridMT(tr.capacity, tr.d, tr.bounds, threads=threads)
     m.load(tr)
@@ -979,6 +989,12 @@ def main():
         cb = cpu_baseline(traces.config3(ticks=1, seed=3, n=a.entities, side=a.side), a.cpu_st_max_seconds)
         line["cpu_baseline"] = cb
         line["cpu_baseline_mt"] = cpu_baseline_mt(a.cpu_seconds, a.entities, a.side)
+        allowed = cpu_info()["cpus_allowed"] or 1
+        if allowed != line["cpu_baseline_mt"]["cores"]:
+            # every core the process may use (the cgroup quota, if any, is stated: it may throttle them)
+            mt = cpu_baseline_mt(a.cpu_seconds, a.entities, a.side, threads=allowed)
+            mt["cgroup_cpu_quota_cores"] = cpu_quota()
+            line["cpu_baseline_mt_all_cores"] = mt
     print(json.dumps(line), flush=True)
 
 

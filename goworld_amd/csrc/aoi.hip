@@ -802,9 +802,10 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             l_nml += (mev && lv) ? 1u : 0u;
         }
     }
-    // group teleports: A is a long mover owned here after the tick; its pairs
-    // with the other long movers come from the lists of every rank
-    if (longA && ownA && b.n_long) long_pairs(b, A, d, out, cap, n, l_nl);
+    // group teleports: A is a long mover whose new position is owned here (not
+    // its old owner, where it left); its pairs with the other long movers come
+    // from the lists of every rank
+    if (longA && pn && owned_x(P, me.x) && b.n_long) long_pairs(b, A, d, out, cap, n, l_nl);
     // the wave's sums (DPP scans, lane 63): old | new, client | own leaves, mirror leaves
     const unsigned long long s_on = wave_incl_scan<unsigned long long>(l_old | ((unsigned long long)l_new << 32));
     const unsigned long long s_cl = wave_incl_scan<unsigned long long>(l_cli | ((unsigned long long)l_nl << 32));

@@ -627,7 +627,7 @@ __device__ __forceinline__ bool pair_rel(float ax, float az, unsigned long long 
 // lists hold every long mover's state before and after the tick, so the old
 // and the new relation of each pair are evaluated here even when no rank holds
 // both ends.  Events are appended to A's region before its sort.
-__device__ __noinline__ void long_pairs(const TickBufs& b, uint32_t A, float d, uint32_t* out, uint64_t cap,
+__device__ __forceinline__ void long_pairs(const TickBufs& b, uint32_t A, float d, uint32_t* out, uint64_t cap,
                                         uint32_t& n, uint32_t& l_nl) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
@@ -857,10 +857,20 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
 
 // WPB waves per block: a block keeps its LDS until its slowest wave ends, so
 // small blocks keep more waves resident when hotspot movers run long
+// SGPRs decide k_mover's residency: a SIMD holds floor(800 / (ceil(sgpr/16)*16 + 16))
+// waves (MI355X_MICROARCH.md): 106 SGPRs -> 6 waves, <= 80 -> 8
+#ifndef GW_KMOVER_SGPR
+#define GW_KMOVER_SGPR 0
+#endif
+#if GW_KMOVER_SGPR
+#define KMOVER_SGPR __attribute__((amdgpu_num_sgpr(GW_KMOVER_SGPR)))
+#else
+#define KMOVER_SGPR
+#endif
 // one wave per primary entry (pidx, cell order): no wave is dispatched for
 // the secondary entries (half the mover grid), whose zeros k_bounds wrote
 template <int DIFF_U>
-__global__ void __launch_bounds__(64) k_mover_c(TickBufs b) {
+__global__ void __launch_bounds__(64) KMOVER_SGPR k_mover_c(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[SORT_LDS];
     const uint64_t k = blockIdx.x;
     const uint64_t np = b.st->cand_total >> PRIM_SHIFT;

@@ -1439,6 +1439,12 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), NFM, nf, c->sc,
                  (uint64_t*)&st->rec_total, c->st);
     size_t s_count = prof_end(c, 0);
+    // per-client grouping (GW_SYNC_BY_CLIENT): the write pass leaves (watcher,
+    // entity) pairs, the sort's keys and values; the records are built once
+    // after the sort (not written, keyed, sorted and gathered at 24 B)
+    const bool by_client = (flags & GW_SYNC_BY_CLIENT) != 0;
+    const bool pairs = by_client && !small;
+    if (pairs && ((rc = ensure(c, c->gk0, c->rec_cap * 4)) || (rc = ensure(c, c->gv0, c->rec_cap * 4)))) return rc;
     prof_begin(c, "sync_write");
     auto write_pass = [&]() {
         if (small)
@@ -1447,7 +1453,8 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
                                     sfirst, slast, max_ents, max_cells, c->st);
         else
             launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint64_t>(c->rec_off),
-                              P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st);
+                              P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st,
+                              pairs ? P<uint32_t>(c->gk0) : nullptr, pairs ? P<uint32_t>(c->gv0) : nullptr);
     };
     write_pass();
     size_t s_write = prof_end(c, 0);
@@ -1459,6 +1466,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     if (c->hcstats->overflow) {
         c->rec_cap = R + R / 4 + 1024;
         if ((rc = ensure(c, c->rec0, c->rec_cap * sizeof(gw_sync_record)))) return rc;
+        if (pairs && ((rc = ensure(c, c->gk0, c->rec_cap * 4)) || (rc = ensure(c, c->gv0, c->rec_cap * 4)))) return rc;
         c->hcstats->overflow = 0;
         HIPCHK(hipMemcpyAsync(c->cstats, c->hcstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
         write_pass();
@@ -1467,10 +1475,57 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         if (c->hcstats->overflow) return set_err(c, GW_ENOMEM, "sync record buffer overflowed twice");
     }
     gw_sync_record* recs = P<gw_sync_record>(c->rec0);
-    const bool by_client = (flags & GW_SYNC_BY_CLIENT) != 0;
+    bool gates_done = false;
+    if (pairs) {
+        // (watcher, entity) pairs in entity order -> stable sort by watcher ->
+        // with several gates in use a stable sort of the pairs' gates -> records:
+        // order (gate, watcher, entity)
+        prof_begin(c, "sync_clients");
+        gates_done = true;
+        const uint32_t* idx = nullptr;
+        uint32_t *wk = P<uint32_t>(c->gk0), *wv = P<uint32_t>(c->gv0);
+        for (uint32_t g = 0; g <= G; ++g) c->gate_off[g] = (g == G) ? R : 0;   // one gate id in use
+        if (R) {
+            if ((rc = ensure(c, c->gk1, R * 4)) || (rc = ensure(c, c->gv1, R * 4))) return rc;
+            RadixTmp rt;
+            if ((rc = radix_tmp(c, R, rt))) return rc;
+            if (R > 1) {
+                const int wsel = sort_u32_u32(P<uint32_t>(c->gk0), P<uint32_t>(c->gv0), P<uint32_t>(c->gk1),
+                                              P<uint32_t>(c->gv1), R, nullptr, 0, ceil_log2(C), rt, c->st);
+                if (wsel) {
+                    wk = P<uint32_t>(c->gk1);
+                    wv = P<uint32_t>(c->gv1);
+                }
+            }
+            if (G > 2) {
+                uint32_t* ka = wk == P<uint32_t>(c->gk0) ? P<uint32_t>(c->gk1) : P<uint32_t>(c->gk0);
+                uint32_t* va = wv == P<uint32_t>(c->gv0) ? P<uint32_t>(c->gv1) : P<uint32_t>(c->gv0);
+                if ((rc = ensure(c, c->m_flag, R * 4)) || (rc = ensure(c, c->m_at, R * 4)) ||
+                    (rc = ensure(c, c->gate_hist, (size_t)65536 * 4)))
+                    return rc;
+                HIPCHK(hipMemsetAsync(c->gate_hist.p, 0, (size_t)G * 4, c->st));
+                launch_gate_keys(wk, c->gate, R, ka, va, P<uint32_t>(c->gate_hist), c->st);
+                std::vector<uint32_t> h(G);
+                HIPCHK(hipMemcpyAsync(h.data(), c->gate_hist.p, (size_t)G * 4, hipMemcpyDeviceToHost, c->st));
+                HIPCHK(hipStreamSynchronize(c->st));
+                uint32_t nonzero = 0;
+                uint64_t acc = 0;
+                for (uint32_t g = 0; g < G; ++g) { nonzero += h[g] != 0; c->gate_off[g] = acc; acc += h[g]; }
+                c->gate_off[G] = acc;
+                if (nonzero > 1) {
+                    const int gs = sort_u32_u32(ka, va, P<uint32_t>(c->m_flag), P<uint32_t>(c->m_at), R, nullptr, 0,
+                                                ceil_log2(G), rt, c->st);
+                    idx = gs ? P<uint32_t>(c->m_at) : va;
+                }
+            }
+            launch_records_from_pairs(w, wk, wv, idx, R, recs, c->st);
+            HIPCHK(hipGetLastError());
+        }
+        prof_end(c, R * (8 * 2 * 3 + 24));
+    }
     // ---- per-client grouping: stable sort by watcher (the gate grouping below
     // is stable too, so the order becomes (gate, watcher, entity)) ---------
-    if (by_client && R > 1) {
+    if (by_client && !pairs && R > 1) {
         prof_begin(c, "sync_clients");
         if ((rc = ensure(c, c->gk0, R * 4)) || (rc = ensure(c, c->gv0, R * 4)) || (rc = ensure(c, c->gk1, R * 4)) ||
             (rc = ensure(c, c->gv1, R * 4)) || (rc = ensure(c, c->rec1, R * sizeof(gw_sync_record))))
@@ -1487,7 +1542,8 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         prof_end(c, R * (24 * 2 + 8 * 4));
     }
     // ---- per-gate grouping (stable, keeps the entity order) -------------
-    if (R && G > 2) {
+    if (gates_done) {
+    } else if (R && G > 2) {
         prof_begin(c, "sync_gates");
         if ((rc = ensure(c, c->gate_hist, (size_t)65536 * 4))) return rc;
         HIPCHK(hipMemsetAsync(c->gate_hist.p, 0, (size_t)G * 4, c->st));
@@ -1686,6 +1742,8 @@ int gw_fanout(gw_ctx* c, const uint32_t* slots, uint32_t n, uint32_t flags, gw_m
         if (slots[k] >= c->total_slots) return set_err(c, GW_ERANGE, "fanout: slot %u out of range", slots[k]);
     HIPCHK(hipEventRecord(c->ev_t0, c->st));
     gw_ctx::MsgBufs& m = c->m_fanout;
+    const uint32_t G = (uint32_t)c->max_gate + 1;
+    m.goff.assign((size_t)G + 1, 0);
     uint64_t R = 0;
     if (n) {
         if ((rc = rebuild_grid(c))) return rc;
@@ -1694,17 +1752,57 @@ int gw_fanout(gw_ctx* c, const uint32_t* slots, uint32_t n, uint32_t flags, gw_m
             return rc;
         HIPCHK(hipMemcpyAsync(c->m_items.p, slots, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
         const World w = world(c);
-        launch_fanout(w, P<uint32_t>(c->m_items), n, P<uint32_t>(c->m_cnt), nullptr, nullptr, c->st);
+        launch_fanout(w, P<uint32_t>(c->m_items), n, P<uint32_t>(c->m_cnt), nullptr, nullptr, nullptr, c->st);
         uint64_t* tot = P<uint64_t>(c->m_off) + n;   // the total lands after the offsets
         scan_u32_u64(P<uint32_t>(c->m_cnt), P<uint64_t>(c->m_off), n, nullptr, c->sc, tot, c->st);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(&R, tot, 8, hipMemcpyDeviceToHost, c->st));
         HIPCHK(hipStreamSynchronize(c->st));
-        if ((rc = ensure(c, m.a, std::max<uint64_t>(R, 1) * sizeof(gw_fanout_rec)))) return rc;
-        launch_fanout(w, P<uint32_t>(c->m_items), n, nullptr, P<uint64_t>(c->m_off), P<gw_fanout_rec>(m.a), c->st);
+    }
+    if (R) {
+        // deliveries as (watcher, item) pairs, a stable radix sort by watcher
+        // (item order inside each watcher), then, with several gates in use, a
+        // stable sort of the pairs' gates; the 12-B records are written once
+        if ((rc = ensure(c, c->gk0, R * 4)) || (rc = ensure(c, c->gv0, R * 4)) || (rc = ensure(c, c->gk1, R * 4)) ||
+            (rc = ensure(c, c->gv1, R * 4)) || (rc = ensure(c, m.a, R * sizeof(gw_fanout_rec))))
+            return rc;
+        RadixTmp rt;
+        if ((rc = radix_tmp(c, R, rt))) return rc;
+        const World w = world(c);
+        launch_fanout(w, P<uint32_t>(c->m_items), n, nullptr, P<uint64_t>(c->m_off), P<uint32_t>(c->gk0),
+                      P<uint32_t>(c->gv0), c->st);
+        const int sel = sort_u32_u32(P<uint32_t>(c->gk0), P<uint32_t>(c->gv0), P<uint32_t>(c->gk1),
+                                     P<uint32_t>(c->gv1), R, nullptr, 0, ceil_log2(c->total_slots), rt, c->st);
+        uint32_t* wk = sel ? P<uint32_t>(c->gk1) : P<uint32_t>(c->gk0);
+        uint32_t* wv = sel ? P<uint32_t>(c->gv1) : P<uint32_t>(c->gv0);
+        const uint32_t* idx = nullptr;
+        if (G > 2) {
+            uint32_t* ka = sel ? P<uint32_t>(c->gk0) : P<uint32_t>(c->gk1);   // the free pair + two more words
+            uint32_t* va = sel ? P<uint32_t>(c->gv0) : P<uint32_t>(c->gv1);
+            if ((rc = ensure(c, c->m_flag, R * 4)) || (rc = ensure(c, c->m_at, R * 4)) ||
+                (rc = ensure(c, c->gate_hist, (size_t)65536 * 4)))
+                return rc;
+            HIPCHK(hipMemsetAsync(c->gate_hist.p, 0, (size_t)G * 4, c->st));
+            launch_gate_keys(wk, c->gate, R, ka, va, P<uint32_t>(c->gate_hist), c->st);
+            std::vector<uint32_t> h(G);
+            HIPCHK(hipMemcpyAsync(h.data(), c->gate_hist.p, (size_t)G * 4, hipMemcpyDeviceToHost, c->st));
+            HIPCHK(hipStreamSynchronize(c->st));
+            uint32_t nonzero = 0;
+            uint64_t acc = 0;
+            for (uint32_t g = 0; g < G; ++g) { nonzero += h[g] != 0; m.goff[g] = acc; acc += h[g]; }
+            m.goff[G] = acc;
+            if (nonzero > 1) {
+                const int gs = sort_u32_u32(ka, va, P<uint32_t>(c->m_flag), P<uint32_t>(c->m_at), R, nullptr, 0,
+                                            ceil_log2(G), rt, c->st);
+                idx = gs ? P<uint32_t>(c->m_at) : va;
+            }
+        } else {
+            for (uint32_t g = 0; g <= G; ++g) m.goff[g] = (g == G) ? R : 0;   // one gate id in use
+        }
+        launch_fanout_final(wk, wv, idx, P<uint32_t>(c->m_items), R, P<gw_fanout_rec>(m.a), c->st);
         HIPCHK(hipGetLastError());
     }
-    if ((rc = group_msgs(c, m, R, 3, true)) || (rc = msg_out(c, m, R, 3, flags, out))) return rc;
+    if ((rc = msg_out(c, m, R, 3, flags, out))) return rc;
     out->bytes_alg += (uint64_t)n * 4;
     HIPCHK(hipEventRecord(c->ev_t1, c->st));
     HIPCHK(hipStreamSynchronize(c->st));

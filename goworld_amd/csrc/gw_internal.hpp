@@ -343,7 +343,10 @@ void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* 
                        uint32_t nf_max, uint32_t* cnt, uint32_t* sfirst, uint32_t* slast, hipStream_t s);
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
-                       uint64_t rec_cap, DevStats* st, hipStream_t s);
+                       uint64_t rec_cap, DevStats* st, hipStream_t s,
+                       uint32_t* pk = nullptr, uint32_t* pv = nullptr);
+void launch_records_from_pairs(const World& w, const uint32_t* pk, const uint32_t* pv, const uint32_t* idx,
+                               uint64_t n, gw_sync_record* out, hipStream_t s);
 void launch_gate_hist(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,
                       uint32_t* hist /*65536*/, hipStream_t s);
 void launch_gate_keys(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,
@@ -431,7 +434,12 @@ void launch_event_client_write(const gw_event* ev, uint64_t n, const uint32_t* f
                                const SlotRec* rec, uint32_t* out, bool create, hipStream_t s);
 // out == nullptr: counts per item into cnt; else deliveries at off[k]
 void launch_fanout(const World& w, const uint32_t* items, uint32_t n, uint32_t* cnt, const uint64_t* off,
-                   gw_fanout_rec* out, hipStream_t s);
+                   uint32_t* keys, uint32_t* vals, hipStream_t s);
+void launch_fanout_final(const uint32_t* keys, const uint32_t* vals, const uint32_t* idx, const uint32_t* items,
+                         uint64_t n, gw_fanout_rec* out, hipStream_t s);
+// keys[i] = gate[w[i]], vals[i] = i, hist[gate] += 1 (hist zeroed by the caller)
+void launch_gate_keys(const uint32_t* w, const uint16_t* gate, uint64_t n, uint32_t* keys, uint32_t* vals,
+                      uint32_t* hist, hipStream_t s);
 void launch_msg_keys(const uint32_t* rec, int words, uint64_t n, const uint16_t* gate, uint32_t* keys, uint32_t* vals,
                      hipStream_t s);   // gate == nullptr: key = watcher
 void launch_msg_gate_hist(const uint32_t* rec, int words, uint64_t n, const uint16_t* gate, uint32_t* hist,

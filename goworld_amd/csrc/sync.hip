@@ -251,13 +251,16 @@ __device__ __forceinline__ void sw_flush64(unsigned long long* buf, unsigned lon
 }
 
 // writes e's records at rec_off[k] (nothing if the buffer is too small: the
-// host grows it and reruns this pass)
-template <int U>
+// host grows it and reruns this pass).  PAIRS (the per-client grouping): only
+// (watcher, entity) as two u32 arrays, the sort's keys and values (pk, pv),
+// whose 24-B records are built once after the sort (k_records_from_pairs)
+template <int U, bool PAIRS = false>
 __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __restrict__ flagged,
                                                    const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
                                                    uint32_t nf_max, const uint64_t* __restrict__ rec_off,
                                                    const uint32_t* __restrict__ cnt, gw_sync_record* rec,
-                                                   uint64_t rec_cap, DevStats* st) {
+                                                   uint64_t rec_cap, DevStats* st, uint32_t* __restrict__ pk,
+                                                   uint32_t* __restrict__ pv) {
     __shared__ unsigned long long sbuf[NWAVE][3 * SW_BUF];
     unsigned long long* buf = sbuf[threadIdx.x >> 6];
     const uint64_t nf = load_n(nf_max, nf_dev);
@@ -277,10 +280,28 @@ __global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __re
         const uint32_t gt = w.gate[e];
         if (!owned_x(w.sp[a.meta & SPACE_MASK], a.x)) continue;
         if ((f & GW_SIF_OWN_CLIENT) && gt) {
-            if (ln == 0) st_record_nt(rec + at, e, e, p);
+            if (ln == 0) {
+                if (PAIRS) {
+                    pk[at] = e;
+                    pv[at] = e;
+                } else {
+                    st_record_nt(rec + at, e, e, p);
+                }
+            }
             ++at;
         }
-        if ((f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
+        if (PAIRS && (f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
+            wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
+                const bool take = rel && g != 0;
+                const uint64_t bt = wave_ballot(take);
+                if (take) {
+                    const uint64_t j = at + (uint64_t)popc64(bt & lt);
+                    pk[j] = ws;
+                    pv[j] = e;
+                }
+                at += (uint64_t)popc64(bt);
+            });
+        } else if ((f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
             const unsigned long long pxy = ((unsigned long long)__float_as_uint(p.y) << 32) | __float_as_uint(p.x);
             const unsigned long long pzw = ((unsigned long long)__float_as_uint(p.w) << 32) | __float_as_uint(p.z);
             uint32_t nb = 0;                                   // staged records (wave-uniform)
@@ -561,18 +582,38 @@ void launch_sync_write_small(const World& w, uint32_t n_spaces, const uint32_t* 
 
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
-                       uint64_t rec_cap, DevStats* st, hipStream_t s) {
+                       uint64_t rec_cap, DevStats* st, hipStream_t s, uint32_t* pk, uint32_t* pv) {
     if (!nf_max) return;
     const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
-    if (w.nb_u >= 8)
+    if (pk)
+        hipLaunchKernelGGL((k_sync_write<4, true>), g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt,
+                           rec, rec_cap, st, pk, pv);
+    else if (w.nb_u >= 8)
         hipLaunchKernelGGL(k_sync_write<8>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st);
+                           rec_cap, st, pk, pv);
     else if (w.nb_u <= 2)
         hipLaunchKernelGGL(k_sync_write<2>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st);
+                           rec_cap, st, pk, pv);
     else
         hipLaunchKernelGGL(k_sync_write<4>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st);
+                           rec_cap, st, pk, pv);
+}
+
+// 24-B records from sorted (watcher, entity) pairs (through idx, the gate
+// grouping's permutation, when given): the entity's payload from its slot
+__global__ void __launch_bounds__(NT) k_records_from_pairs(World w, const uint32_t* __restrict__ pk,
+                                                           const uint32_t* __restrict__ pv,
+                                                           const uint32_t* __restrict__ idx, uint64_t n,
+                                                           gw_sync_record* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t j = idx ? idx[i] : (uint32_t)i;
+    const uint32_t e = pv[j];
+    st_record_nt(out + i, pk[j], e, w.rec[e].p);
+}
+void launch_records_from_pairs(const World& w, const uint32_t* pk, const uint32_t* pv, const uint32_t* idx,
+                               uint64_t n, gw_sync_record* out, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_records_from_pairs, dim3(nblk(n, NT)), dim3(NT), 0, s, w, pk, pv, idx, n, out);
 }
 
 // per-gate record histogram: LDS buckets for gates < 256, global atomics above
@@ -781,24 +822,52 @@ void launch_event_client_write(const gw_event* ev, uint64_t n, const uint32_t* f
 // (b) AllClients fan-out: CallAllClients and every AllClients attribute
 // notification send to e.client, then to n.client for n in e.InterestedBy
 // (Entity.go:743-749, 814-917).  Item k (entity items[k]) -> deliveries
-// {watcher, entity, k}: the own one first, then the related entities with a
-// client, from the current grid (one wave per item, like the collect).
+// (watcher, k): the own one first, then the related entities with a client,
+// from the current grid (one wave per item, like the collect).  A delivery is
+// two u32 words, the sort key and its value: the entity is items[k], so the
+// 12-B record is built once, after the sort (k_fanout_final).
+// Counts: a lane per item takes the diff's cached count of neighbours with a
+// client when this epoch's tick made it (a call on a mover of the last tick),
+// the rest are walked one at a time by the wave (as k_sync_count).
 template <int U>
 __global__ void __launch_bounds__(NT) k_fanout_count(World w, const uint32_t* __restrict__ items, uint32_t n,
                                                      uint32_t* cnt) {
-    const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
-    for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < n; k += stride) {
-        const uint32_t e = items[k];
-        uint32_t r = w.gate[e] ? 1u : 0u;
-        wave_neighbors<U>(w, e, [&](bool rel, uint32_t, uint32_t g) {
-            r += (uint32_t)popc64(wave_ballot(rel && g != 0));
-        });
-        if (lane_id() == 0) cnt[k] = r;
+    const int ln = lane_id();
+    const uint64_t stride = (uint64_t)gridDim.x * NT;
+    for (uint64_t base = (uint64_t)blockIdx.x * NT + (threadIdx.x & ~63u); base < n; base += stride) {
+        const uint64_t k = base + ln;
+        const bool valid = k < n;
+        uint32_t e = 0, r = 0;
+        bool walk = false;
+        if (valid) {
+            e = items[k];
+            const AoiEnt a = w.rec[e].a;
+            const uint32_t g = w.gate[e];
+            const unsigned long long c = w.nbc[e];
+            r = g ? 1u : 0u;
+            if (a.meta & PRESENT_BIT) {
+                if ((uint32_t)(c >> 32) == w.epoch) r += (uint32_t)c;
+                else walk = true;
+            }
+        }
+        uint64_t todo = wave_ballot(walk);
+        while (todo) {
+            const int q = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t eq = (uint32_t)__builtin_amdgcn_readlane((int)e, q);
+            uint32_t m = 0;
+            wave_neighbors<U>(w, eq, [&](bool rel, uint32_t, uint32_t g) {
+                m += (uint32_t)popc64(wave_ballot(rel && g != 0));
+            });
+            if (ln == q) r += m;
+        }
+        if (valid) cnt[k] = r;
     }
 }
 template <int U>
 __global__ void __launch_bounds__(NT) k_fanout_write(World w, const uint32_t* __restrict__ items, uint32_t n,
-                                                     const uint64_t* __restrict__ off, gw_fanout_rec* out) {
+                                                     const uint64_t* __restrict__ off, uint32_t* __restrict__ keys,
+                                                     uint32_t* __restrict__ vals) {
     const uint64_t lt = lanemask_lt();
     const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
     for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < n; k += stride) {
@@ -806,9 +875,8 @@ __global__ void __launch_bounds__(NT) k_fanout_write(World w, const uint32_t* __
         uint64_t at = off[k];
         if (w.gate[e]) {
             if (lane_id() == 0) {
-                gw_fanout_rec m;
-                m.watcher = e; m.entity = e; m.item = (uint32_t)k;
-                out[at] = m;
+                keys[at] = e;
+                vals[at] = (uint32_t)k;
             }
             ++at;
         }
@@ -816,20 +884,61 @@ __global__ void __launch_bounds__(NT) k_fanout_write(World w, const uint32_t* __
             const bool take = rel && g != 0;
             const uint64_t bt = wave_ballot(take);
             if (take) {
-                gw_fanout_rec m;
-                m.watcher = ws; m.entity = e; m.item = (uint32_t)k;
-                out[at + (uint64_t)popc64(bt & lt)] = m;
+                const uint64_t j = at + (uint64_t)popc64(bt & lt);
+                keys[j] = ws;
+                vals[j] = (uint32_t)k;
             }
             at += (uint64_t)popc64(bt);
         });
     }
 }
 void launch_fanout(const World& w, const uint32_t* items, uint32_t n, uint32_t* cnt, const uint64_t* off,
-                   gw_fanout_rec* out, hipStream_t s) {
+                   uint32_t* keys, uint32_t* vals, hipStream_t s) {
     if (!n) return;
-    const dim3 g(std::min(nblk(n, NWAVE), SYNC_MAX_BLOCKS));
-    if (!out) hipLaunchKernelGGL(k_fanout_count<4>, g, dim3(NT), 0, s, w, items, n, cnt);
-    else hipLaunchKernelGGL(k_fanout_write<4>, g, dim3(NT), 0, s, w, items, n, off, out);
+    if (cnt)
+        hipLaunchKernelGGL(k_fanout_count<4>, dim3(std::min(nblk(n, NT), SYNC_MAX_BLOCKS)), dim3(NT), 0, s, w, items,
+                           n, cnt);
+    else
+        hipLaunchKernelGGL(k_fanout_write<4>, dim3(std::min(nblk(n, NWAVE), SYNC_MAX_BLOCKS)), dim3(NT), 0, s, w,
+                           items, n, off, keys, vals);
+}
+// the records from the sorted (watcher, item) pairs, through idx (the gate
+// grouping's permutation) when given; gate keys of the pairs for that grouping
+__global__ void __launch_bounds__(NT) k_fanout_final(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                     const uint32_t* __restrict__ idx,
+                                                     const uint32_t* __restrict__ items, uint64_t n,
+                                                     gw_fanout_rec* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t j = idx ? idx[i] : (uint32_t)i;
+    gw_fanout_rec r;
+    r.watcher = keys[j];
+    r.item = vals[j];
+    r.entity = items[r.item];
+    out[i] = r;
+}
+__global__ void __launch_bounds__(NT) k_gate_keys(const uint32_t* __restrict__ w, const uint16_t* __restrict__ gate,
+                                                  uint64_t n, uint32_t* keys, uint32_t* vals, uint32_t* hist) {
+    __shared__ uint32_t h[NT];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * NT) {
+        const uint32_t g = gate[w[i]];
+        keys[i] = g;
+        vals[i] = (uint32_t)i;
+        if (g < NT) atomicAdd(&h[g], 1u); else atomicAdd(&hist[g], 1u);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+void launch_fanout_final(const uint32_t* keys, const uint32_t* vals, const uint32_t* idx, const uint32_t* items,
+                         uint64_t n, gw_fanout_rec* out, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_fanout_final, dim3(nblk(n, NT)), dim3(NT), 0, s, keys, vals, idx, items, n, out);
+}
+void launch_gate_keys(const uint32_t* w, const uint16_t* gate, uint64_t n, uint32_t* keys, uint32_t* vals,
+                      uint32_t* hist, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_gate_keys, dim3(std::min<uint32_t>(nblk(n, NT), 2048)), dim3(NT), 0, s, w, gate, n,
+                              keys, vals, hist);
 }
 
 // (c) stable grouping of a message stream: keys (watcher, or gate(watcher)),

@@ -375,13 +375,15 @@ struct HaloStats {
 struct HaloFar {
     gw_halo_row* rows;          // cap triples (3 rows each)
     uint32_t* dest;             // destination rank of each triple
-    uint32_t* cnt;              // [nranks + 1] triples per destination, then the long movers listed
-                                // (zeroed by the first pass; all-gathered as one vector)
+    uint32_t* cnt;              // [nranks + FAR_EXTRA] triples per destination, the long movers listed,
+                                // a pad word, the entities routed to the left / right neighbour
+                                // (zeroed by the first pass; all-gathered as one vector at >= 3 ranks)
     const float* ext;           // [2 * nranks] held x-range [lo, hi) of every rank, float32
     uint32_t cap, nranks, self, pad;
     gw_long_move* longs;        // [long_cap] this rank's long movers (group teleports), or null
     uint32_t long_cap, pad2;
 };
+constexpr uint32_t FAR_EXTRA = 4;  // HaloFar::cnt words after the per-rank triples
 constexpr uint16_t RES_LONG = 1;   // gw_op.reserved of a halo row: the entity moved more than max_step
 struct HaloDst {
     float x_lo, x_hi;

@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, ui
                                                 HaloFar F) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i == 0) hs->cnt[0] = hs->cnt[1] = hs->far_n = hs->long_n = 0;   // placement counters of this call
-    if (F.cnt && i <= F.nranks) F.cnt[i] = 0;
+    if (F.cnt && i < F.nranks + FAR_EXTRA) F.cnt[i] = 0;
     if (i >= n) return;
     if (stamps_out) stamps_out[i] = stamp_base + i;
     const gw_op op = ops[i];
@@ -181,7 +181,13 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
         if (!bm) continue;
         const int leader = __builtin_ctzll(bm);
         uint32_t base = 0;
-        if (lane_id() == leader) base = atomicAdd(&hs->cnt[d], (uint32_t)popc64(bm));
+        if (lane_id() == leader) {
+            base = atomicAdd(&hs->cnt[d], (uint32_t)popc64(bm));
+            // the same count by side in the all-gathered vector (>= 3 ranks: it
+            // replaces the neighbours' count round); one destination = the
+            // outer rank's only neighbour
+            if (F.cnt) atomicAdd(&F.cnt[F.nranks + 2 + (D.n == 2 ? d : (F.self == 0 ? 1u : 0u))], (uint32_t)popc64(bm));
+        }
         base = __shfl(base, leader, 64);
         if (!emit) continue;
         const uint32_t e = base + (uint32_t)popc64(bm & lanemask_lt());
@@ -278,7 +284,7 @@ void launch_route_halo(const World& w, const gw_op* ops, const unsigned long lon
                        bool pad, unsigned long long* stamps_out, unsigned long long stamp_base, const HaloFar* far) {
     HaloFar F{};
     if (far) F = *far;
-    const uint32_t nb = nblk1(std::max<uint32_t>(n, F.nranks + 1), NT);
+    const uint32_t nb = nblk1(std::max<uint32_t>(n, F.nranks + FAR_EXTRA), NT);
     uint64_t rows = 0;                                   // NOP padding up to the capacity (fixed-size exchanges)
     if (pad)
         for (uint32_t d = 0; d < D.n; ++d) rows = std::max<uint64_t>(rows, (uint64_t)D.d[d].cap * ROWS);

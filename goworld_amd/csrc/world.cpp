@@ -97,7 +97,7 @@ constexpr size_t RCNT = 4;
 // one kernel, the host sync, then into hs / the vectors
 int read_route_counts(gw_ctx* c, HaloStats& hs, uint32_t* rcnt, bool far_mat) {
     WorldHost& W = c->wd;
-    const uint32_t R = W.g.ranks, R1 = R + 1;
+    const uint32_t R = W.g.ranks, R1 = R + FAR_EXTRA;
     const size_t o_cnt = pub_off_cnt(), o_far = o_cnt + RCNT, o_mat = o_far + R1;
     PubSeg segs[4];
     int n = 0;
@@ -244,15 +244,16 @@ int gw_world_create(gw_ctx* c, const gw_world_geom* g, uint32_t capacity, const 
     // the world's buffers first: a failure leaves no space behind (a retry
     // must find the context empty, the strip's space at slot base 0)
     int rc2;
-    if ((rc2 = ensure(c, W.ext, W.ext_h.size() * 4)) || (rc2 = ensure(c, W.far_cnt, ((size_t)g->ranks + 1) * 4)) ||
+    if ((rc2 = ensure(c, W.ext, W.ext_h.size() * 4)) ||
+        (rc2 = ensure(c, W.far_cnt, ((size_t)g->ranks + FAR_EXTRA) * 4)) ||
         (rc2 = ensure(c, W.far_off, (size_t)g->ranks * 4)) || (rc2 = ensure(c, W.far_cursor, (size_t)g->ranks * 4)) ||
-        (rc2 = ensure(c, W.far_mat, (size_t)g->ranks * (g->ranks + 1) * 4)))
+        (rc2 = ensure(c, W.far_mat, (size_t)g->ranks * (g->ranks + FAR_EXTRA) * 4)))
         return rc2;
     HIPCHK(hipMemcpyAsync(W.ext.p, W.ext_h.data(), W.ext_h.size() * 4, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     if (W.pub_h) (void)hipHostFree(W.pub_h);
     W.pub_h = W.pub_d = nullptr;
-    const size_t pub_words = pub_off_cnt() + RCNT + (g->ranks + 1) + (size_t)g->ranks * (g->ranks + 1);
+    const size_t pub_words = pub_off_cnt() + RCNT + (g->ranks + FAR_EXTRA) + (size_t)g->ranks * (g->ranks + FAR_EXTRA);
     if (hipHostMalloc((void**)&W.pub_h, pub_words * 4, hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&W.pub_d, W.pub_h, 0) != hipSuccess)
         return set_err(c, GW_ENOMEM, "world count buffer");
@@ -268,9 +269,9 @@ int gw_world_create(gw_ctx* c, const gw_world_geom* g, uint32_t capacity, const 
         c->err = keep;
         return rc;
     }
-    W.far_cnt_h.assign(g->ranks + 1, 0);
+    W.far_cnt_h.assign(g->ranks + FAR_EXTRA, 0);
     W.far_off_h.assign(g->ranks, 0);
-    W.far_mat_h.assign((size_t)g->ranks * (g->ranks + 1), 0);
+    W.far_mat_h.assign((size_t)g->ranks * (g->ranks + FAR_EXTRA), 0);
     W.own_nlong = 0;
     W.tick_longs = nullptr;
     W.tick_nlong = 0;
@@ -389,34 +390,40 @@ int gw_world_step(gw_ctx* c, const gw_op* ops, uint32_t n) {
         W.kept_tag = tag;
     }
     HIPCHK(hipGetLastError());
-    const uint32_t R = W.g.ranks, me = W.g.rank, R1 = R + 1;
+    const uint32_t R = W.g.ranks, me = W.g.rank, R1 = R + FAR_EXTRA;
     const bool far_round = R >= 3;                    // ranks that are not neighbours exist
     uint32_t rcnt[2] = {0, 0};
     uint32_t far_in = 0;                              // triples received from far ranks
     uint32_t n_long = 0;                              // long movers of all ranks (group teleports)
     if (any_nb) {
-        // round 1: the entity counts (u32) both ways; HaloStats.cnt[k] is the
-        // k-th destination of D, i.e. left first when both exist.  With two
-        // ranks the long-mover counts go along (with more, the all-gather)
-        uint32_t* dcnt = P<uint32_t>(W.cnt);         // [0..1] rows from left / right, [2..3] long movers
-        if ((rc = xp_group_start(c))) return rc;
+        // round 1, the counts.  Two ranks: the entity count (u32) and the
+        // long-mover count both ways (HaloStats.cnt[k] is the k-th destination
+        // of D, i.e. left first when both exist).  More: ONE all-gather of every
+        // rank's count vector (far triples per rank, long movers, entities to
+        // its left / right neighbour) instead of a neighbour round and an
+        // all-gather
         uint32_t k = 0;
-        for (int side = 0; side < 2; ++side) {
-            if (W.nb[side] < 0) continue;
-            (void)xp_send(c, &c->halo->cnt[k++], 4, W.nb[side]);
-            (void)xp_recv(c, dcnt + side, 4, W.nb[side]);
-            if (!far_round) {
+        if (!far_round) {
+            uint32_t* dcnt = P<uint32_t>(W.cnt);     // [0..1] rows from left / right, [2..3] long movers
+            if ((rc = xp_group_start(c))) return rc;
+            for (int side = 0; side < 2; ++side) {
+                if (W.nb[side] < 0) continue;
+                (void)xp_send(c, &c->halo->cnt[k++], 4, W.nb[side]);
+                (void)xp_recv(c, dcnt + side, 4, W.nb[side]);
                 (void)xp_send(c, P<uint32_t>(W.far_cnt) + R, 4, W.nb[side]);
                 (void)xp_recv(c, dcnt + 2 + side, 4, W.nb[side]);
             }
+            if ((rc = xp_group_end(c))) return rc;
+        } else if ((rc = xp_allgather(c, W.far_cnt.p, W.far_mat.p, (size_t)R1 * 4))) {
+            return rc;
         }
-        if ((rc = xp_group_end(c))) return rc;
-        // the far triples every rank sends every rank and its long-mover count
-        // (long moves; R + 1 u32 each)
-        if (far_round && (rc = xp_allgather(c, W.far_cnt.p, W.far_mat.p, (size_t)R1 * 4))) return rc;
         uint32_t h[RCNT] = {0, 0, 0, 0};
         HaloStats hs{};
-        if ((rc = read_route_counts(c, hs, h, far_round))) return rc;
+        if ((rc = read_route_counts(c, hs, far_round ? nullptr : h, far_round))) return rc;
+        if (far_round) {                             // the neighbours' entity counts towards this rank
+            if (me > 0) h[0] = W.far_mat_h[(size_t)(me - 1) * R1 + R + 3];    // left neighbour's "to the right"
+            if (me + 1 < R) h[1] = W.far_mat_h[(size_t)(me + 1) * R1 + R + 2];   // right neighbour's "to the left"
+        }
         if ((rc = far_settle(c, ops, n, D, tag, base, hs))) return rc;
         k = 0;
         for (int side = 0; side < 2; ++side) {

@@ -1175,7 +1175,12 @@ __device__ __forceinline__ void small_walk(const TickBufs& b, uint32_t m0, uint3
 }
 
 template <int DIFF_U>
-__global__ void __launch_bounds__(NT) k_mover_small(TickBufs b) {
+// (GW_MS_MINB: blocks per CU the register allocation must allow; 4 caps the
+// VGPRs at 128: 4 waves per SIMD instead of 3 at 129, as LDS allows 5 blocks)
+#ifndef GW_MS_MINB
+#define GW_MS_MINB 1
+#endif
+__global__ void __launch_bounds__(NT, GW_MS_MINB) k_mover_small(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * SMALL_SORT];
     extern __shared__ uint4 dyn_lds[];
     const uint32_t s = blockIdx.x;

@@ -254,8 +254,13 @@ __device__ __forceinline__ void sw_flush64(unsigned long long* buf, unsigned lon
 // host grows it and reruns this pass).  PAIRS (the per-client grouping): only
 // (watcher, entity) as two u32 arrays, the sort's keys and values (pk, pv),
 // whose 24-B records are built once after the sort (k_records_from_pairs)
+// (GW_SW_MINB: blocks per CU the register allocation must allow; 8 caps the
+// VGPRs at 64, i.e. 8 waves per SIMD instead of 7 at 66)
+#ifndef GW_SW_MINB
+#define GW_SW_MINB 1
+#endif
 template <int U, bool PAIRS = false>
-__global__ void __launch_bounds__(NT) k_sync_write(World w, const uint32_t* __restrict__ flagged,
+__global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const uint32_t* __restrict__ flagged,
                                                    const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
                                                    uint32_t nf_max, const uint64_t* __restrict__ rec_off,
                                                    const uint32_t* __restrict__ cnt, gw_sync_record* rec,

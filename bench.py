@@ -127,6 +127,16 @@ class Ctl:
             self.group = dist.group.WORLD
             self.dist = dist
 
+    def close(self, ok=True):
+        """Leave the group together (a rank process that exits while its
+        peers' gloo threads still talk to it can abort them)."""
+        if self.group is None:
+            return
+        if ok:
+            self.dist.barrier(group=self.group)
+        self.dist.destroy_process_group()
+        self.group = None
+
     def barrier(self):
         if self.group is not None:
             self.dist.barrier(group=self.group)
@@ -221,8 +231,10 @@ def dry_run(a, ctl):
                           "ranks_reporting": int(ranks), "higher_is_better": True}), flush=True)
 
 
-# the diff stage's kernel: k_mover (one mover per wave), or k_mover_pair when GW_PAIR_MAX > 0
-STAGE_KERNEL = {"diff": "k_mover_pair<2>" if int(os.environ.get("GW_PAIR_MAX", "0") or 0) > 0 else "k_mover<2, 1>"}
+# the diff stage's kernel: k_mover_c (one wave per primary mover entry), k_mover (one wave per
+# mover-grid entry, GW_MOVER_COMPACT=0), or k_mover_pair when GW_PAIR_MAX > 0
+STAGE_KERNEL = {"diff": "k_mover_pair<2>" if int(os.environ.get("GW_PAIR_MAX", "0") or 0) > 0
+                else "k_mover<2, 1>" if os.environ.get("GW_MOVER_COMPACT", "1") == "0" else "k_mover_c<2>"}
 # the stage's kernel differs in small-space mode (config #4: many spaces whose grids fit LDS)
 STAGE_KERNEL_C4 = {"diff": "k_mover_small<2>", "sync_write": "k_sync_write_small2"}
 PMC_DIR = os.path.join(ROOT, "profiles")
@@ -780,9 +792,18 @@ def main():
     if rc is not None:                              # the launcher of N ranks (or a bad --gpus)
         sys.exit(rc)
     ctl = Ctl(a)
-    if a.dry_run:
-        dry_run(a, ctl)
-        return
+    ok = False
+    try:
+        if a.dry_run:
+            dry_run(a, ctl)
+        else:
+            run(a, ctl)
+        ok = True
+    finally:
+        ctl.close(ok)
+
+
+def run(a, ctl):
     ws, rank = ctl.ws, ctl.rank
     loop = a.comm == "loopback" and a.gpus > 1   # the N ranks are threads of this process on one device
     R = a.gpus if loop else ws                    # ranks of the run

@@ -343,13 +343,20 @@ int read_stats(gw_ctx* c) {
 int read_cstats(gw_ctx* c) {
     const bool both = c->pt.on && !c->pt.copied;
     // one kernel writes the statistics into the pinned host buffers (coherent,
-    // device-visible) and, for a deferred tick, runs its reset (which reads the
-    // device statistics itself): no blit copy and no launch after the sync
-    publish_stats(both ? &c->pt.b : nullptr, both ? (const void*)c->stats : (const void*)c->cstats,
+    // device-visible): no blit copy.  A deferred tick's reset (the next tick's
+    // bucket bounds, the device statistics zeroed) reads the device statistics
+    // itself, so it can go after the sync: it then runs while the host returns
+    // to its caller and issues the next step (GW_RESET_LATE=0: in the same
+    // kernel as the copy, before the sync)
+    const bool late = both && c->reset_late;
+    publish_stats(both && !late ? &c->pt.b : nullptr, both ? (const void*)c->stats : (const void*)c->cstats,
                   both ? c->hstats_dev : c->hstats_dev + 1, (both ? 2 : 1) * sizeof(DevStats), c->st);
-    if (both) c->pt.reset_queued = true;
     HIPCHK(hipStreamSynchronize(c->st));
-    if (both) c->pt.copied = true;
+    if (late) tick_reset(c->pt.b, c->st);
+    if (both) {
+        c->pt.reset_queued = true;
+        c->pt.copied = true;
+    }
     return 0;
 }
 
@@ -534,6 +541,7 @@ int gw_init(int device_id, gw_ctx** out) {
         if (const char* e = getenv("GW_MOVER_COMPACT")) c->mover_compact = atoi(e) != 0;
         if (const char* e = getenv("GW_HEAVY_MIN")) c->heavy_min = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_HEAVY_MAXM")) c->heavy_maxm = (uint32_t)std::max(0, atoi(e));
+        if (const char* e = getenv("GW_RESET_LATE")) c->reset_late = atoi(e) != 0;
         if (const char* e = getenv("GW_DIRTY_SPAN")) c->dirty_span = (uint32_t)std::min(64, std::max(1, atoi(e)));
     } while (0);
     if (rc) {

@@ -205,6 +205,7 @@ struct gw_ctx {
                                          // diff 58 -> 47 us; at 100k movers one wave per mover in cell order
                                          // balances better) ...
     uint32_t heavy_maxm = 65536;         // ... for ticks of at most GW_HEAVY_MAXM ops
+    bool reset_late = true;              // GW_RESET_LATE: a collect queues the tick's reset after its host sync
     uint32_t rank_sort = 12;             // GW_RANK_SORT: TickBufs.rank_sort
     // GW_DIRTY_SPAN: TickBufs.dirty_span; 0 = by the cell count: 2 up to 128k cells, 8 up to 1M cells (a hotspot wave
     // merges fewer dirty cells in a row: config #3 grid 63 -> 58 us), 16 above (fewer idle waves:

@@ -858,9 +858,10 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
 // WPB waves per block: a block keeps its LDS until its slowest wave ends, so
 // small blocks keep more waves resident when hotspot movers run long
 // SGPRs decide k_mover's residency: a SIMD holds floor(800 / (ceil(sgpr/16)*16 + 16))
-// waves (MI355X_MICROARCH.md): 106 SGPRs -> 6 waves, <= 80 -> 8
+// waves (MI355X_MICROARCH.md): 106 SGPRs -> 6 waves, <= 80 -> 8 (34 spilled to
+// VGPR lanes; config #3 diff 180 -> 172 us).  GW_KMOVER_SGPR=0: no cap
 #ifndef GW_KMOVER_SGPR
-#define GW_KMOVER_SGPR 0
+#define GW_KMOVER_SGPR 80
 #endif
 #if GW_KMOVER_SGPR
 #define KMOVER_SGPR __attribute__((amdgpu_num_sgpr(GW_KMOVER_SGPR)))
@@ -1176,9 +1177,10 @@ __device__ __forceinline__ void small_walk(const TickBufs& b, uint32_t m0, uint3
 
 template <int DIFF_U>
 // (GW_MS_MINB: blocks per CU the register allocation must allow; 4 caps the
-// VGPRs at 128: 4 waves per SIMD instead of 3 at 129, as LDS allows 5 blocks)
+// VGPRs at 128: 4 waves per SIMD instead of 3 at 129, as LDS allows 5 blocks;
+// config #4 diff 854 -> 711 us)
 #ifndef GW_MS_MINB
-#define GW_MS_MINB 1
+#define GW_MS_MINB 4
 #endif
 __global__ void __launch_bounds__(NT, GW_MS_MINB) k_mover_small(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * SMALL_SORT];

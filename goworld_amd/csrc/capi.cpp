@@ -200,8 +200,10 @@ int radix_tmp(gw_ctx* c, uint64_t n_max, RadixTmp& rt) {
     uint64_t hn = 256 * nb;
     int rc;
     if ((rc = ensure(c, c->rs_hist, hn * 4))) return rc;
+    if ((rc = ensure(c, c->rs_os, radix2_scratch(n_max) * 4 + 64))) return rc;
     if ((rc = ensure_scan(c, hn))) return rc;
     rt.hist = P<uint32_t>(c->rs_hist);
+    rt.os = P<uint32_t>(c->rs_os);
     rt.sc = &c->sc;
     return 0;
 }
@@ -343,20 +345,15 @@ int read_stats(gw_ctx* c) {
 int read_cstats(gw_ctx* c) {
     const bool both = c->pt.on && !c->pt.copied;
     // one kernel writes the statistics into the pinned host buffers (coherent,
-    // device-visible): no blit copy.  A deferred tick's reset (the next tick's
-    // bucket bounds, the device statistics zeroed) reads the device statistics
-    // itself, so it can go after the sync: it then runs while the host returns
-    // to its caller and issues the next step (GW_RESET_LATE=0: in the same
-    // kernel as the copy, before the sync)
-    const bool late = both && c->reset_late;
-    publish_stats(both && !late ? &c->pt.b : nullptr, both ? (const void*)c->stats : (const void*)c->cstats,
+    // device-visible) and, for a deferred tick, runs its reset (which reads the
+    // device statistics itself): no blit copy and no launch after the sync
+    // (the reset launched after the sync instead, to overlap the host's return:
+    // config #3 step +25 us)
+    publish_stats(both ? &c->pt.b : nullptr, both ? (const void*)c->stats : (const void*)c->cstats,
                   both ? c->hstats_dev : c->hstats_dev + 1, (both ? 2 : 1) * sizeof(DevStats), c->st);
+    if (both) c->pt.reset_queued = true;
     HIPCHK(hipStreamSynchronize(c->st));
-    if (late) tick_reset(c->pt.b, c->st);
-    if (both) {
-        c->pt.reset_queued = true;
-        c->pt.copied = true;
-    }
+    if (both) c->pt.copied = true;
     return 0;
 }
 
@@ -541,7 +538,6 @@ int gw_init(int device_id, gw_ctx** out) {
         if (const char* e = getenv("GW_MOVER_COMPACT")) c->mover_compact = atoi(e) != 0;
         if (const char* e = getenv("GW_HEAVY_MIN")) c->heavy_min = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_HEAVY_MAXM")) c->heavy_maxm = (uint32_t)std::max(0, atoi(e));
-        if (const char* e = getenv("GW_RESET_LATE")) c->reset_late = atoi(e) != 0;
         if (const char* e = getenv("GW_DIRTY_SPAN")) c->dirty_span = (uint32_t)std::min(64, std::max(1, atoi(e)));
     } while (0);
     if (rc) {
@@ -561,7 +557,7 @@ void gw_shutdown(gw_ctx* c) {
     DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1,
                       &c->gm, &c->cand, &c->reg, &c->pidx, &c->heavy, &c->rowrec, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
                       &c->mcnt, &c->moff, &c->minfo, &c->icnt, &c->ioff, &c->mreg, &c->chunk_first, &c->srange, &c->bk_a, &c->bk_b, &c->bk_id, &c->bk_cnt, &c->bk_split, &c->ev_d, &c->rtable,
-                      &c->scan_status, &c->rs_hist,
+                      &c->scan_status, &c->rs_hist, &c->rs_os,
                       &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
                       &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf, &c->cl_slot, &c->cl_off,
                       &c->m_create.a, &c->m_create.b, &c->m_destroy.a, &c->m_destroy.b, &c->m_fanout.a,

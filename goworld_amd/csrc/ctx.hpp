@@ -198,14 +198,13 @@ struct gw_ctx {
     // grid + tick scratch
     DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, mtmp, mcell, cand, reg, pidx, heavy, rowrec, own, big, mstat;
     DevBuf mir, ownc, mirc, mlist, mcnt, moff, minfo, icnt, ioff, mreg, chunk_first, srange, bk_a, bk_b, bk_id, bk_cnt, bk_split, ev_d, rtable;
-    DevBuf scan_status, rs_hist;
+    DevBuf scan_status, rs_hist, rs_os;   // rs_os: the one-kernel-per-pass sort's scratch (sort_u32_u32)
     uint32_t walk_min = 32;              // GW_WALK_MIN: TickBufs.walk_min (0: always walk)
     bool mover_compact = true;           // GW_MOVER_COMPACT: TickBufs.compact
     uint32_t heavy_min = 512;            // GW_HEAVY_MIN: TickBufs.heavy_min (0: off; 1M world at 8 strips:
                                          // diff 58 -> 47 us; at 100k movers one wave per mover in cell order
                                          // balances better) ...
     uint32_t heavy_maxm = 65536;         // ... for ticks of at most GW_HEAVY_MAXM ops
-    bool reset_late = true;              // GW_RESET_LATE: a collect queues the tick's reset after its host sync
     uint32_t rank_sort = 12;             // GW_RANK_SORT: TickBufs.rank_sort
     // GW_DIRTY_SPAN: TickBufs.dirty_span; 0 = by the cell count: 2 up to 128k cells, 8 up to 1M cells (a hotspot wave
     // merges fewer dirty cells in a row: config #3 grid 63 -> 58 us), 16 above (fewer idle waves:

@@ -151,6 +151,7 @@ struct ScanCtx {
 struct RadixTmp {
     uint32_t* hist;      // 256 * radix_blocks(n_max)
     ScanCtx* sc;
+    uint32_t* os = nullptr;   // radix2_scratch(n_max) words: sort_u32_u32 runs radix_sort2 (one kernel per pass)
 };
 uint64_t radix_tile();            // keys per radix block
 uint64_t radix2_tile();           // keys per tile of radix_sort2

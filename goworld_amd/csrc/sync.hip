@@ -1074,6 +1074,11 @@ void scan_u64_u64(const uint64_t* in, uint64_t* out, uint64_t n_max, const uint6
 }
 int sort_u32_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
                  int lo_bit, int hi_bit, RadixTmp& tmp, hipStream_t s) {
+    // the pairs of the client paths (fanout, per-client grouping, gate groups):
+    // one kernel per 8-bit pass, each tile's digit runs written contiguously
+    // from LDS (the three-kernel sort's direct scatter: 173 us per pass over
+    // config #3's 14.7M fanout pairs)
+    if (tmp.os && hi_bit - lo_bit <= 32) return radix_sort2(k0, v0, k1, v1, n_max, n_dev, lo_bit, hi_bit, tmp.os, s);
     return radix_sort<uint32_t>(k0, v0, k1, v1, n_max, n_dev, lo_bit, hi_bit, tmp, s);
 }
 

@@ -473,74 +473,88 @@ inline int radix_sort(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n_max, 
 }
 
 // ---------------------------------------------------------------------------
-// Stable LSD radix sort of (u32 key, u32 value) pairs, 8-bit digits, ONE kernel
-// per pass ("onesweep"): the digit counts of every pass are order-independent,
-// so one upfront pass over the keys gives each pass's global digit bases; a
-// pass then ranks its 4096-pair tile in LDS, publishes the tile's per-digit
-// counts and gets the counts of all earlier tiles by a decoupled look-back per
-// digit (thread d follows digit d back through the tiles' status words until
-// an inclusive prefix; tiles take tickets in dispatch order, so every tile it
-// waits on is running), and writes each digit's run of the tile contiguously
-// from LDS.  Ranking is wave-private (no barrier inside the loop): wave w owns
-// the tile's w-th quarter in input order and ranks each 64-key chunk by
-// match-any over the 8 digit bits (8 ballots) against a wave-private LDS
-// histogram; the waves' counts are then prefix-summed per digit, so the order
-// within a digit is the input order (stable).  The last pass may write
-// gw_event {key & mask, value} instead of the two arrays.
+// Stable LSD radix sort of (u32 key, u32 value) pairs, ONE kernel per pass
+// ("onesweep"), DB-bit digits (8, 10 or 11: keys of 17-22 bits sort in two
+// passes instead of three): the digit counts of every pass are
+// order-independent, so one upfront pass over the keys gives each pass's
+// global digit bases; a pass then ranks its 4096-pair tile in LDS, publishes
+// the tile's per-digit counts and gets the counts of all earlier tiles by a
+// decoupled look-back per digit (a thread follows its digits back through the
+// tiles' status words until an inclusive prefix; tiles take tickets in
+// dispatch order, so every tile it waits on is running), and writes each
+// digit's run of the tile contiguously from LDS.  Ranking is wave-private (no
+// barrier inside the loop): wave w owns the tile's w-th eighth in input order
+// and ranks each 64-key chunk by match-any over the DB digit bits (DB ballots)
+// against a wave-private LDS histogram; the waves' counts are then
+// prefix-summed per digit, so the order within a digit is the input order
+// (stable).  The last pass may write gw_event {key & mask, value} instead of
+// the two arrays.
 constexpr int RS2_NT = 512;                          // 8 waves per tile: short serial ranking loops
 constexpr int RS2_NW = RS2_NT / 64;
 constexpr int RS2_TILE = 4096;
 constexpr int RS2_WAVE_KEYS = RS2_TILE / RS2_NW;     // 512 per wave
 constexpr int RS2_CHUNKS = RS2_WAVE_KEYS / 64;      // 8
 constexpr int RS2_MAX_PASSES = 4;
+constexpr int RS2_MAX_RADIX = 2048;                 // DB <= 11
+constexpr int RS2_STATUS_PER_TILE = 4096;           // max over the digit widths of passes * radix
 constexpr int RS2_GBLOCKS = 256;                    // blocks of the upfront histogram
 constexpr uint32_t OS_AGG = 1u << 30, OS_INC = 2u << 30, OS_VAL = (1u << 30) - 1;
 
-// per-block digit counts of every pass (wave-private LDS copies: the top
-// digit of a key has few distinct values, so one shared copy would serialise
-// its bins' atomics; grid-stride)
-template <int TILE_ = RS2_TILE>   // templates: the header is included by several translation units
+template <int DB>
+struct OsCfg {
+    static constexpr int RD = 1 << DB;                                  // digits
+    static constexpr int MAXP = DB == 8 ? RS2_MAX_PASSES : 2;
+    static constexpr int DPT = RD > RS2_NT ? RD / RS2_NT : 1;           // digits per pass thread
+    static constexpr int DT = RD / DPT;                                 // pass threads owning digits
+    static_assert(MAXP * RD <= RS2_STATUS_PER_TILE, "status words per tile");
+};
+
+// digit totals of every pass (wave-private LDS copies: the top digit of a key
+// has few distinct values, so one shared copy would serialise its bins'
+// atomics; grid-stride), added into the zeroed totals[p][d]
+template <int DB>
 __global__ void __launch_bounds__(NT) k_os_hist(const uint32_t* __restrict__ keys, const uint64_t* n_dev,
-                                                uint64_t n_max, int lo_bit, int passes, uint32_t* __restrict__ part) {
-    __shared__ uint32_t h[NWAVE][RS2_MAX_PASSES][RS_RADIX];
+                                                uint64_t n_max, int lo_bit, int passes, uint32_t* __restrict__ totals) {
+    using C = OsCfg<DB>;
+    __shared__ uint32_t h[NWAVE][C::MAXP][C::RD];
     const int w = threadIdx.x >> 6;
-#pragma unroll
-    for (int q = 0; q < NWAVE; ++q)
-#pragma unroll
-        for (int p = 0; p < RS2_MAX_PASSES; ++p) h[q][p][threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < NWAVE * C::MAXP * C::RD; i += NT) (&h[0][0][0])[i] = 0;
     __syncthreads();
     const uint64_t n = load_n(n_max, n_dev);
     for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * NT) {
         const uint32_t k = keys[i];
-        for (int p = 0; p < passes; ++p) atomicAdd(&h[w][p][(k >> (lo_bit + 8 * p)) & 255u], 1u);
+        for (int p = 0; p < passes; ++p) atomicAdd(&h[w][p][(k >> (lo_bit + DB * p)) & (C::RD - 1)], 1u);
     }
     __syncthreads();
-    for (int p = 0; p < passes; ++p) {
-        uint32_t v = 0;
+    for (int p = 0; p < passes; ++p)
+        for (int d = threadIdx.x; d < C::RD; d += NT) {
+            uint32_t v = 0;
 #pragma unroll
-        for (int q = 0; q < NWAVE; ++q) v += h[q][p][threadIdx.x];
-        part[((uint64_t)p * RS_RADIX + threadIdx.x) * gridDim.x + blockIdx.x] = v;
-    }
+            for (int q = 0; q < NWAVE; ++q) v += h[q][p][d];
+            if (v) atomicAdd(&totals[p * RS2_MAX_RADIX + d], v);
+        }
 }
-// global digit bases per pass: block p, thread d sums digit d over the
-// partial histograms (independent loads, batched), then an exclusive scan
-// over the digits
-template <int TILE_ = RS2_TILE>
-__global__ void __launch_bounds__(NT) k_os_bases(const uint32_t* __restrict__ part, uint32_t nblocks,
-                                                 uint32_t* __restrict__ gbase) {
+// global digit bases per pass (block p): an exclusive scan over the digits,
+// thread t owning digits [t*DPB, (t+1)*DPB)
+template <int DB>
+__global__ void __launch_bounds__(NT) k_os_bases(const uint32_t* __restrict__ totals, uint32_t* __restrict__ gbase) {
+    using C = OsCfg<DB>;
+    constexpr int DPB = C::RD / NT;
     __shared__ uint32_t red[NWAVE];
-    const uint32_t p = blockIdx.x, d = threadIdx.x;
-    const uint32_t* q = part + ((uint64_t)p * RS_RADIX + d) * nblocks;
-    uint32_t acc[16] = {};
-    for (uint32_t b = 0; b < nblocks; b += 16) {
+    const uint32_t p = blockIdx.x;
+    uint32_t v[DPB], s = 0;
 #pragma unroll
-        for (int u = 0; u < 16; ++u) acc[u] += (b + u < nblocks) ? q[b + u] : 0u;
+    for (int u = 0; u < DPB; ++u) {
+        v[u] = totals[p * RS2_MAX_RADIX + threadIdx.x * DPB + u];
+        s += v[u];
     }
-    uint32_t tot = 0;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) tot += acc[u];
     uint32_t all;
-    gbase[p * RS_RADIX + d] = block_excl_scan<uint32_t>(tot, red, all);
+    uint32_t pre = block_excl_scan<uint32_t>(s, red, all);
+#pragma unroll
+    for (int u = 0; u < DPB; ++u) {
+        gbase[p * RS2_MAX_RADIX + threadIdx.x * DPB + u] = pre;
+        pre += v[u];
+    }
 }
 
 __device__ __forceinline__ uint32_t os_ld(const uint32_t* p) {
@@ -550,20 +564,22 @@ __device__ __forceinline__ void os_st(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int TILE_ = RS2_TILE>
+template <int DB>
 __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                     gw_event* __restrict__ aos, uint32_t aos_mask,
                                                     const uint64_t* n_dev, uint64_t n_max, int shift,
                                                     const uint32_t* __restrict__ gbase, uint32_t* __restrict__ status,
                                                     unsigned long long* __restrict__ ticket) {
-    __shared__ uint32_t whist[RS2_NW][RS_RADIX];
-    __shared__ uint32_t tstart[RS_RADIX], gofs[RS_RADIX], red[RS_RADIX / 64];
+    using C = OsCfg<DB>;
+    constexpr uint32_t DM = C::RD - 1;
+    __shared__ uint32_t whist[RS2_NW][C::RD];
+    __shared__ uint32_t tstart[C::RD], gofs[C::RD], red[RS2_NW];
     __shared__ uint32_t sk[RS2_TILE], sv[RS2_TILE];
     __shared__ uint32_t s_tile;
     const int t = threadIdx.x, w = t >> 6, ln = lane_id();
     if (t == 0) s_tile = (uint32_t)atomicAdd(ticket, 1ull);
-    for (int i = t; i < RS2_NW * RS_RADIX; i += RS2_NT) (&whist[0][0])[i] = 0;
+    for (int i = t; i < RS2_NW * C::RD; i += RS2_NT) (&whist[0][0])[i] = 0;
     __syncthreads();
     const uint32_t tile = s_tile;
     const uint64_t n = load_n(n_max, n_dev);
@@ -583,10 +599,10 @@ __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__
     for (int c = 0; c < RS2_CHUNKS; ++c) {
         const uint64_t i = wbase + (uint64_t)c * 64 + ln;
         const bool valid = i < n;
-        const uint32_t d = (key[c] >> shift) & 255u;
+        const uint32_t d = (key[c] >> shift) & DM;
         uint64_t peers = wave_ballot(valid);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
+        for (int b = 0; b < DB; ++b) {
             const bool bit = (d >> b) & 1u;
             const uint64_t bb = wave_ballot(bit);
             peers &= bit ? bb : ~bb;
@@ -601,38 +617,54 @@ __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__
         rk[c] = valid ? old + r : 0xffffffffu;
     }
     __syncthreads();
-    uint32_t run = 0, inc = 0;
-    if (t < RS_RADIX) {
-        // thread t = digit t: prefix over the waves, then the tile's global
-        // offset for the digit by a look-back over earlier tiles
+    // thread t < DT owns digits [t*DPT, (t+1)*DPT): prefix over the waves, the
+    // tile's global offset per digit by a look-back over earlier tiles, then
+    // the tile's digit starts by a scan over the digits
+    uint32_t run[C::DPT], tsum = 0;
+    if (t < C::DT) {
 #pragma unroll
-        for (int k = 0; k < RS2_NW; ++k) { const uint32_t v = whist[k][t]; whist[k][t] = run; run += v; }
-        uint32_t* my = status + (uint64_t)tile * RS_RADIX + t;
-        os_st(my, (tile == 0 ? OS_INC : OS_AGG) | run);
-        uint32_t excl = 0;
-        for (int64_t j = (int64_t)tile - 1; j >= 0; --j) {
-            uint32_t v;
-            do { v = os_ld(status + (uint64_t)j * RS_RADIX + t); } while (!(v & (OS_AGG | OS_INC)));
-            excl += v & OS_VAL;
-            if (v & OS_INC) break;
+        for (int u = 0; u < C::DPT; ++u) {
+            const uint32_t d = (uint32_t)t * C::DPT + u;
+            uint32_t r = 0;
+#pragma unroll
+            for (int k = 0; k < RS2_NW; ++k) { const uint32_t v = whist[k][d]; whist[k][d] = r; r += v; }
+            run[u] = r;
+            tsum += r;
+            os_st(status + (uint64_t)tile * C::RD + d, (tile == 0 ? OS_INC : OS_AGG) | r);
         }
-        if (tile) os_st(my, OS_INC | (excl + run));
-        gofs[t] = gbase[t] + excl;
-        inc = wave_incl_scan<uint32_t>(run);                 // the tile's digit starts: a scan over 256 digits
-        if (ln == 63) red[w] = inc;
+#pragma unroll
+        for (int u = 0; u < C::DPT; ++u) {
+            const uint32_t d = (uint32_t)t * C::DPT + u;
+            uint32_t excl = 0;
+            for (int64_t j = (int64_t)tile - 1; j >= 0; --j) {
+                uint32_t v;
+                do { v = os_ld(status + (uint64_t)j * C::RD + d); } while (!(v & (OS_AGG | OS_INC)));
+                excl += v & OS_VAL;
+                if (v & OS_INC) break;
+            }
+            if (tile) os_st(status + (uint64_t)tile * C::RD + d, OS_INC | (excl + run[u]));
+            gofs[d] = gbase[d] + excl;
+        }
     }
+    const uint32_t inc = wave_incl_scan<uint32_t>(t < C::DT ? tsum : 0u);
+    if (ln == 63) red[w] = inc;
     __syncthreads();
-    if (t < RS_RADIX) {
+    if (t < C::DT) {
         uint32_t pre = 0;
 #pragma unroll
-        for (int k = 0; k < RS_RADIX / 64; ++k) pre += (k < w) ? red[k] : 0u;
-        tstart[t] = pre + inc - run;
+        for (int k = 0; k < RS2_NW; ++k) pre += (k < w) ? red[k] : 0u;
+        pre += inc - tsum;
+#pragma unroll
+        for (int u = 0; u < C::DPT; ++u) {
+            tstart[t * C::DPT + u] = pre;
+            pre += run[u];
+        }
     }
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < RS2_CHUNKS; ++c) {
         if (rk[c] == 0xffffffffu) continue;
-        const uint32_t d = (key[c] >> shift) & 255u;
+        const uint32_t d = (key[c] >> shift) & DM;
         const uint32_t pos = tstart[d] + hw[d] + rk[c];
         sk[pos] = key[c];
         sv[pos] = val[c];
@@ -641,7 +673,7 @@ __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__
     const uint32_t tn = (uint32_t)min<uint64_t>((uint64_t)RS2_TILE, n - base);
     for (uint32_t i = t; i < tn; i += RS2_NT) {              // each digit's run of the tile is contiguous
         const uint32_t k = sk[i], v = sv[i];
-        const uint32_t d = (k >> shift) & 255u;
+        const uint32_t d = (k >> shift) & DM;
         const uint32_t dst = gofs[d] + (i - tstart[d]);
         if (aos) {
             gw_event e;
@@ -656,41 +688,57 @@ __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__
 }
 
 inline uint64_t radix2_tiles(uint64_t n_max) { return (n_max + RS2_TILE - 1) / RS2_TILE; }
-// scratch words radix_sort2 needs for n_max pairs
+// scratch words radix_sort2 needs for n_max pairs: tickets (8 words), digit
+// totals and bases ([MAX_PASSES][MAX_RADIX] each), status ([tiles][<= 4096])
 inline uint64_t radix2_scratch_words(uint64_t n_max) {
-    return (uint64_t)RS2_MAX_PASSES * RS_RADIX * (RS2_GBLOCKS + 1 + radix2_tiles(n_max)) + 2 * RS2_MAX_PASSES;
+    return 8 + 2ull * RS2_MAX_PASSES * RS2_MAX_RADIX + (uint64_t)RS2_STATUS_PER_TILE * radix2_tiles(n_max);
 }
 
-// Sorts (k0,v0) by bits [lo_bit, hi_bit) (at most 32 bits) with (k1,v1) as
-// ping-pong; scratch holds radix2_scratch_words(n_max) u32 (no clearing
-// needed by the caller).  With aos, the last pass writes gw_event
-// {key & aos_mask, value} there (and the return value is meaningless).
-// Returns 0 if the result is in (k0,v0), 1 if in (k1,v1).
-inline int radix_sort2(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
-                       int lo_bit, int hi_bit, uint32_t* scratch, hipStream_t st,
-                       gw_event* aos = nullptr, uint32_t aos_mask = 0xffffffffu) {
+template <int DB>
+inline int radix_sort2_db(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max,
+                          const uint64_t* n_dev, int lo_bit, int passes, uint32_t* scratch, hipStream_t st,
+                          gw_event* aos, uint32_t aos_mask) {
+    using C = OsCfg<DB>;
     const uint64_t nt = radix2_tiles(n_max);
-    if (nt == 0 || hi_bit <= lo_bit) return 0;
-    const int passes = (hi_bit - lo_bit + 7) / 8;
-    uint32_t* part = scratch;                                             // [P][256][GBLOCKS]
-    uint32_t* gbase = part + (uint64_t)RS2_MAX_PASSES * RS_RADIX * RS2_GBLOCKS;   // [P][256]
-    unsigned long long* tickets = (unsigned long long*)(gbase + RS2_MAX_PASSES * RS_RADIX);   // [P]
-    uint32_t* status = (uint32_t*)(tickets + RS2_MAX_PASSES);            // [P][tiles][256]
-    // tickets and the status words of the passes used start at zero
-    (void)hipMemsetAsync(tickets, 0, RS2_MAX_PASSES * 8 + (uint64_t)passes * RS_RADIX * nt * 4, st);
-    hipLaunchKernelGGL(k_os_hist<>, dim3(RS2_GBLOCKS), dim3(NT), 0, st, k0, n_dev, n_max, lo_bit, passes, part);
-    hipLaunchKernelGGL(k_os_bases<>, dim3(passes), dim3(NT), 0, st, part, (uint32_t)RS2_GBLOCKS, gbase);
+    unsigned long long* tickets = (unsigned long long*)scratch;                 // [MAX_PASSES]
+    uint32_t* totals = scratch + 8;                                             // [MAX_PASSES][MAX_RADIX]
+    uint32_t* status = totals + RS2_MAX_PASSES * RS2_MAX_RADIX;                 // [passes][tiles][RD]
+    uint32_t* gbase = status + (uint64_t)RS2_STATUS_PER_TILE * nt;              // [MAX_PASSES][MAX_RADIX]
+    // tickets, totals and the status words of the passes used start at zero
+    (void)hipMemsetAsync(scratch, 0, 32 + (uint64_t)RS2_MAX_PASSES * RS2_MAX_RADIX * 4 +
+                                         (uint64_t)passes * C::RD * nt * 4, st);
+    hipLaunchKernelGGL(k_os_hist<DB>, dim3(RS2_GBLOCKS), dim3(NT), 0, st, k0, n_dev, n_max, lo_bit, passes, totals);
+    hipLaunchKernelGGL(k_os_bases<DB>, dim3(passes), dim3(NT), 0, st, totals, gbase);
     int cur = 0;
     for (int p = 0; p < passes; ++p) {
         const bool last = p == passes - 1;
         uint32_t* ki = cur ? k1 : k0; uint32_t* ko = cur ? k0 : k1;
         uint32_t* vi = cur ? v1 : v0; uint32_t* vo = cur ? v0 : v1;
-        hipLaunchKernelGGL(k_os_pass<>, dim3((uint32_t)nt), dim3(RS2_NT), 0, st, ki, vi, ko, vo, last ? aos : nullptr,
-                           aos_mask, n_dev, n_max, lo_bit + 8 * p, gbase + p * RS_RADIX,
-                           status + (uint64_t)p * RS_RADIX * nt, tickets + p);
+        hipLaunchKernelGGL(k_os_pass<DB>, dim3((uint32_t)nt), dim3(RS2_NT), 0, st, ki, vi, ko, vo,
+                           last ? aos : nullptr, aos_mask, n_dev, n_max, lo_bit + DB * p,
+                           gbase + p * RS2_MAX_RADIX, status + (uint64_t)p * C::RD * nt, tickets + p);
         cur ^= 1;
     }
     return cur;
+}
+
+// Sorts (k0,v0) by bits [lo_bit, hi_bit) (at most 32 bits) with (k1,v1) as
+// ping-pong; scratch holds radix2_scratch_words(n_max) u32 (no clearing
+// needed by the caller).  Digit width: 17-20 key bits in two 10-bit passes,
+// 21-22 in two 11-bit passes, else 8-bit passes.  With aos, the last pass
+// writes gw_event {key & aos_mask, value} there (and the return value is
+// meaningless).  Returns 0 if the result is in (k0,v0), 1 if in (k1,v1).
+inline int radix_sort2(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
+                       int lo_bit, int hi_bit, uint32_t* scratch, hipStream_t st,
+                       gw_event* aos = nullptr, uint32_t aos_mask = 0xffffffffu) {
+    const uint64_t nt = radix2_tiles(n_max);
+    if (nt == 0 || hi_bit <= lo_bit) return 0;
+    const int bits = hi_bit - lo_bit;
+    if (bits > 16 && bits <= 20)
+        return radix_sort2_db<10>(k0, v0, k1, v1, n_max, n_dev, lo_bit, 2, scratch, st, aos, aos_mask);
+    if (bits > 20 && bits <= 22)
+        return radix_sort2_db<11>(k0, v0, k1, v1, n_max, n_dev, lo_bit, 2, scratch, st, aos, aos_mask);
+    return radix_sort2_db<8>(k0, v0, k1, v1, n_max, n_dev, lo_bit, (bits + 7) / 8, scratch, st, aos, aos_mask);
 }
 
 }  // namespace gw

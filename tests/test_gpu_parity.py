@@ -580,3 +580,49 @@ def test_tick_statistics_match_oracle(ctx_factory):
         g.submit(ops)
         r = g.tick()
         assert (r.movers, r.nbr_old, r.nbr_new) == (len(aoi), a_old, a_new)
+
+
+@pytest.mark.parametrize("pad", [150_000, 1_600_000])
+def test_client_paths_wide_slot_keys(ctx_factory, pad):
+    """The client paths' stable sorts by watcher slot at wider keys: an empty
+    first space of `pad` slots puts the traced space's slots past 2^17 (18-bit
+    keys: two 10-bit passes) or 2^20 (21-bit keys: two 11-bit passes).  Client
+    messages, fan-out and the per-client collect equal the oracle's, slots
+    shifted by the space's base."""
+    tr = T.config2(ticks=3, n=20_000)
+    tr.gates = np.where(np.arange(tr.capacity) % 7 == 6, 0, 1 + np.arange(tr.capacity) % 3).astype(np.uint16)
+    g = ctx_factory()
+    g.create_space(100.0, pad, (-1000.0, -1000.0, 1000.0, 1000.0))
+    sid, base = gpuaoi.load_space(g, tr)
+    assert base >= pad
+    gates = np.zeros(base + tr.capacity, np.uint16)
+    gates[base:] = tr.gates
+    o = pyorc.OracleSpace(tr.capacity, tr.d, pyorc.SEQRULE)
+    pyorc.load_trace(o, tr)
+    rng = np.random.default_rng(11)
+
+    def shifted(a, fields):
+        a = a.copy()
+        for f in fields:
+            a[f] += np.uint32(base)
+        return a
+    n_fo = n_rec = 0
+    for t, ops in enumerate(tr.ticks):
+        g.submit(T.with_global_slots(ops, base))
+        g.tick(copy=False)
+        assert o.tick(ops) == 0
+        cr, de = g.client_events()
+        ocr, ode = o.client_events()
+        assert cr.records.tobytes() == shifted(ocr, ("watcher", "entity")).tobytes(), f"tick {t}: creates differ"
+        assert de.records.tobytes() == shifted(ode, ("watcher", "target")).tobytes(), f"tick {t}: destroys differ"
+        calls = rng.integers(0, tr.capacity, 3000).astype(np.uint32)
+        f = g.fanout(calls + np.uint32(base))
+        assert f.records.tobytes() == shifted(o.fanout(calls), ("watcher", "entity")).tobytes(), \
+            f"tick {t}: fan-out differs"
+        r = g.sync_collect(by_client=True)
+        exp = shifted(o.collect(), ("watcher", "entity"))
+        exp = exp[np.lexsort((exp["entity"], exp["watcher"], gates[exp["watcher"]]))]
+        assert r.records.tobytes() == exp.tobytes(), f"tick {t}: per-client records differ"
+        n_fo += len(f.records)
+        n_rec += len(r.records)
+    assert n_fo > 1000 and n_rec > 10_000

@@ -1522,7 +1522,11 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
                     idx = gs ? P<uint32_t>(c->m_at) : va;
                 }
             }
-            launch_records_from_pairs(w, wk, wv, idx, R, recs, c->st);
+            if ((rc = ensure(c, c->cl_slot, R * 4)) || (rc = ensure(c, c->cl_off, (R + 1) * 8)) ||
+                (rc = ensure_scan(c, R)))
+                return rc;
+            launch_records_seg(w, wk, wv, idx, R, recs, P<uint32_t>(c->cl_slot), P<uint64_t>(c->cl_off),
+                               c->scal32 + 1, c->sc, c->st);
             HIPCHK(hipGetLastError());
         }
         prof_end(c, R * (8 * 2 * 3 + 24));
@@ -1581,12 +1585,14 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     }
     uint32_t n_clients = 0;
     if (by_client && R) {
-        if ((rc = ensure(c, c->gk0, R * 4)) || (rc = ensure(c, c->gk1, R * 4)) ||
-            (rc = ensure(c, c->cl_slot, R * 4)) || (rc = ensure(c, c->cl_off, (R + 1) * 8)) ||
-            (rc = ensure_scan(c, R)))
-            return rc;
-        launch_client_segments(recs, R, P<uint32_t>(c->gk0), P<uint32_t>(c->gk1), c->scal32 + 1,
-                               P<uint32_t>(c->cl_slot), P<uint64_t>(c->cl_off), c->sc, c->st);
+        if (!pairs) {                                 // (the pairs path built the table with its records)
+            if ((rc = ensure(c, c->gk0, R * 4)) || (rc = ensure(c, c->gk1, R * 4)) ||
+                (rc = ensure(c, c->cl_slot, R * 4)) || (rc = ensure(c, c->cl_off, (R + 1) * 8)) ||
+                (rc = ensure_scan(c, R)))
+                return rc;
+            launch_client_segments(recs, R, P<uint32_t>(c->gk0), P<uint32_t>(c->gk1), c->scal32 + 1,
+                                   P<uint32_t>(c->cl_slot), P<uint64_t>(c->cl_off), c->sc, c->st);
+        }
         HIPCHK(hipMemcpyAsync(&n_clients, c->scal32 + 1, 4, hipMemcpyDeviceToHost, c->st));
     }
     // the stream is synced again only for host outputs (records, client

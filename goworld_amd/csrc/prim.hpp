@@ -497,7 +497,7 @@ constexpr int RS2_CHUNKS = RS2_WAVE_KEYS / 64;      // 8
 constexpr int RS2_MAX_PASSES = 4;
 constexpr int RS2_MAX_RADIX = 2048;                 // DB <= 11
 constexpr int RS2_STATUS_PER_TILE = 4096;           // max over the digit widths of passes * radix
-constexpr int RS2_GBLOCKS = 256;                    // blocks of the upfront histogram
+constexpr int RS2_GBLOCKS = 1024;                   // blocks of the upfront histogram (grid-stride)
 constexpr uint32_t OS_AGG = 1u << 30, OS_INC = 2u << 30, OS_VAL = (1u << 30) - 1;
 
 template <int DB>
@@ -573,13 +573,19 @@ __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__
                                                     unsigned long long* __restrict__ ticket) {
     using C = OsCfg<DB>;
     constexpr uint32_t DM = C::RD - 1;
-    __shared__ uint32_t whist[RS2_NW][C::RD];
+    // one 32-KB region: the waves' 16-bit digit counts while ranking, then the
+    // tile's pairs in digit order (every position is in registers by then):
+    // 40 KB of LDS at DB = 10, four tiles per CU
+    __shared__ uint32_t region[2 * RS2_TILE];
     __shared__ uint32_t tstart[C::RD], gofs[C::RD], red[RS2_NW];
-    __shared__ uint32_t sk[RS2_TILE], sv[RS2_TILE];
     __shared__ uint32_t s_tile;
+    static_assert(RS2_NW * C::RD * 2 <= (int)sizeof(region), "wave counts fit the pair region");
+    uint16_t(*whist)[C::RD] = reinterpret_cast<uint16_t(*)[C::RD]>(region);
+    uint32_t* sk = region;
+    uint32_t* sv = region + RS2_TILE;
     const int t = threadIdx.x, w = t >> 6, ln = lane_id();
     if (t == 0) s_tile = (uint32_t)atomicAdd(ticket, 1ull);
-    for (int i = t; i < RS2_NW * C::RD; i += RS2_NT) (&whist[0][0])[i] = 0;
+    for (int i = t; i < RS2_NW * C::RD / 2; i += RS2_NT) region[i] = 0;
     __syncthreads();
     const uint32_t tile = s_tile;
     const uint64_t n = load_n(n_max, n_dev);
@@ -594,7 +600,7 @@ __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__
         key[c] = i < n ? kin[i] : 0u;
         val[c] = i < n ? vin[i] : 0u;
     }
-    uint32_t* hw = whist[w];
+    uint16_t* hw = whist[w];
 #pragma unroll
     for (int c = 0; c < RS2_CHUNKS; ++c) {
         const uint64_t i = wbase + (uint64_t)c * 64 + ln;
@@ -610,7 +616,7 @@ __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__
         const uint32_t r = (uint32_t)popc64(peers & lt);
         const uint32_t old = valid ? hw[d] : 0u;             // same-digit lanes read the same count
         __builtin_amdgcn_wave_barrier();
-        if (valid && r == 0) hw[d] = old + (uint32_t)popc64(peers);
+        if (valid && r == 0) hw[d] = (uint16_t)(old + (uint32_t)popc64(peers));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -627,7 +633,7 @@ __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__
             const uint32_t d = (uint32_t)t * C::DPT + u;
             uint32_t r = 0;
 #pragma unroll
-            for (int k = 0; k < RS2_NW; ++k) { const uint32_t v = whist[k][d]; whist[k][d] = r; r += v; }
+            for (int k = 0; k < RS2_NW; ++k) { const uint32_t v = whist[k][d]; whist[k][d] = (uint16_t)r; r += v; }
             run[u] = r;
             tsum += r;
             os_st(status + (uint64_t)tile * C::RD + d, (tile == 0 ? OS_INC : OS_AGG) | r);
@@ -662,12 +668,17 @@ __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__
     }
     __syncthreads();
 #pragma unroll
+    for (int c = 0; c < RS2_CHUNKS; ++c) {                   // positions to registers: the counts' region
+        if (rk[c] == 0xffffffffu) continue;                  // becomes the pair buffer below
+        const uint32_t d = (key[c] >> shift) & DM;
+        rk[c] += tstart[d] + hw[d];
+    }
+    __syncthreads();
+#pragma unroll
     for (int c = 0; c < RS2_CHUNKS; ++c) {
         if (rk[c] == 0xffffffffu) continue;
-        const uint32_t d = (key[c] >> shift) & DM;
-        const uint32_t pos = tstart[d] + hw[d] + rk[c];
-        sk[pos] = key[c];
-        sv[pos] = val[c];
+        sk[rk[c]] = key[c];
+        sv[rk[c]] = val[c];
     }
     __syncthreads();
     const uint32_t tn = (uint32_t)min<uint64_t>((uint64_t)RS2_TILE, n - base);

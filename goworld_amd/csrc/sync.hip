@@ -605,20 +605,96 @@ void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* 
 }
 
 // 24-B records from sorted (watcher, entity) pairs (through idx, the gate
-// grouping's permutation, when given): the entity's payload from its slot
-__global__ void __launch_bounds__(NT) k_records_from_pairs(World w, const uint32_t* __restrict__ pk,
-                                                           const uint32_t* __restrict__ pv,
-                                                           const uint32_t* __restrict__ idx, uint64_t n,
-                                                           gw_sync_record* __restrict__ out) {
-    const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t j = idx ? idx[i] : (uint32_t)i;
-    const uint32_t e = pv[j];
-    st_record_nt(out + i, pk[j], e, w.rec[e].p);
+// grouping's permutation, when given; the entity's payload from its slot)
+// and, in the same pass, the client segment table of the stream (what
+// k_client_heads + scan + k_client_segments derive from written records):
+// a head per first record of a watcher, compacted by a
+// decoupled look-back (prim.hpp) into client_slot / client_off; the
+// watchers come from the sorted keys, not from a re-read of the records.
+// Tiles of SCAN_TILE pairs, striped: lane l's predecessor is lane l-1's
+// element, lane 0 loads its own.
+__global__ void __launch_bounds__(NT) k_records_seg(World w, const uint32_t* __restrict__ pk,
+                                                    const uint32_t* __restrict__ pv,
+                                                    const uint32_t* __restrict__ idx, uint64_t n,
+                                                    gw_sync_record* __restrict__ out,
+                                                    uint32_t* __restrict__ client_slot,
+                                                    uint64_t* __restrict__ client_off, uint32_t* n_clients,
+                                                    unsigned long long* __restrict__ status,
+                                                    unsigned long long* __restrict__ ticket, unsigned long long tbase,
+                                                    uint32_t tag) {
+    constexpr int IPT = SCAN_IPT;
+    constexpr int G = 4;                                 // rows whose gathers are in flight together
+    __shared__ uint32_t lds[IPT * NWAVE];
+    __shared__ uint32_t s_tile, s_prefix;
+    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tbase);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t t0 = (uint64_t)tile * (IPT * NT);
+    const int ln = lane_id();
+    uint32_t wt[IPT], c[IPT];
+#pragma unroll
+    for (int j0 = 0; j0 < IPT; j0 += G) {
+        uint32_t e[G], pw[G];
+        float4 p[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const uint64_t i = t0 + (uint64_t)(j0 + u) * NT + threadIdx.x;
+            const uint32_t q = i < n ? (idx ? idx[i] : (uint32_t)i) : 0u;
+            wt[j0 + u] = i < n ? pk[q] : 0xffffffffu;
+            e[u] = i < n ? pv[q] : 0u;
+            pw[u] = (ln == 0 && i < n && i > 0) ? pk[idx ? idx[i - 1] : (uint32_t)(i - 1)] : 0xffffffffu;
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const uint64_t i = t0 + (uint64_t)(j0 + u) * NT + threadIdx.x;
+            if (i < n) p[u] = w.rec[e[u]].p;
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const uint64_t i = t0 + (uint64_t)(j0 + u) * NT + threadIdx.x;
+            uint32_t prev = (uint32_t)__shfl_up((int)wt[j0 + u], 1, 64);
+            if (ln == 0) prev = pw[u];
+            c[j0 + u] = (i < n && (i == 0 || prev != wt[j0 + u])) ? 1u : 0u;
+            if (i < n) st_record_nt(out + i, wt[j0 + u], e[u], p[u]);
+        }
+    }
+    uint32_t head = 0;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) head |= c[j] << j;
+    uint32_t tot;
+    tile_excl_scan_striped<uint32_t, IPT>(c, lds, tot);
+    if (threadIdx.x < 64) {
+        const uint32_t excl = scan_lookback<uint32_t>(status, tile, tag, tot);
+        if (threadIdx.x == 0) s_prefix = excl;
+    }
+    __syncthreads();
+    const uint32_t pre = s_prefix;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        if ((head >> j) & 1u) {
+            const uint32_t at = pre + c[j];
+            client_slot[at] = wt[j];
+            client_off[at] = t0 + (uint64_t)j * NT + threadIdx.x;
+        }
+    }
+    if (tile == gridDim.x - 1 && threadIdx.x == 0) {
+        *n_clients = pre + tot;
+        client_off[pre + tot] = n;                       // end of the last client
+    }
 }
-void launch_records_from_pairs(const World& w, const uint32_t* pk, const uint32_t* pv, const uint32_t* idx,
-                               uint64_t n, gw_sync_record* out, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(k_records_from_pairs, dim3(nblk(n, NT)), dim3(NT), 0, s, w, pk, pv, idx, n, out);
+void launch_records_seg(const World& w, const uint32_t* pk, const uint32_t* pv, const uint32_t* idx, uint64_t n,
+                        gw_sync_record* out, uint32_t* client_slot, uint64_t* client_off, uint32_t* n_clients,
+                        ScanCtx& sc, hipStream_t s) {
+    if (!n) return;
+    const uint32_t nb = (uint32_t)((n + SCAN_TILE - 1) / SCAN_TILE);
+    if (sc.tag >= SCAN_TAG_MAX) {
+        (void)hipMemsetAsync(sc.status, 0, sc.max_tiles * SCAN_WORDS * 8, s);
+        sc.tag = 0;
+    }
+    ++sc.tag;
+    hipLaunchKernelGGL(k_records_seg, dim3(nb), dim3(NT), 0, s, w, pk, pv, idx, n, out, client_slot, client_off,
+                       n_clients, sc.status, sc.ticket, sc.tbase, sc.tag);
+    sc.tbase += nb;
 }
 
 // per-gate record histogram: LDS buckets for gates < 256, global atomics above

@@ -575,7 +575,7 @@ void gw_shutdown(gw_ctx* c) {
     if (c->cid_dev) (void)hipFree(c->cid_dev);
     for (DevBuf* b : wb) if (b->p) (void)hipFree(b->p);
     xp_release(c);
-    DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off, &c->m_create.h,
+    DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off, &c->h_items, &c->m_create.h,
                     &c->m_destroy.h, &c->m_fanout.h};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
     void* ps[] = {c->halo, c->sc.ticket, c->movbit, c->gmi, c->rec, c->flags, c->gate, c->nbc, c->ol,
@@ -1713,26 +1713,29 @@ int gw_client_events(gw_ctx* c, uint32_t flags, gw_msg_out* create, gw_msg_out* 
     const uint64_t ns[2] = {evs[0] ? t.n_enter : 0, evs[1] ? t.n_leave : 0};
     gw_ctx::MsgBufs* ms[2] = {&c->m_create, &c->m_destroy};
     gw_msg_out* outs[2] = {create, destroy};
+    // both kinds' messages (one look-back pass each), then one host sync for
+    // both counts
+    uint32_t Rk[2] = {0, 0};
     for (int k = 0; k < 2; ++k) {
         const uint64_t n = ns[k];
+        if (!n) continue;
+        if (n >= 0xffffffffull) return set_err(c, GW_ERANGE, "too many events (%llu)", (unsigned long long)n);
+        if ((rc = ensure_scan(c, n)) || (rc = ensure(c, ms[k]->a, n * (k == 0 ? 6 : 2) * 4))) return rc;
+        launch_event_client_compact(evs[k], n, c->gate, c->rec, P<uint32_t>(ms[k]->a), k == 0, c->scal32 + 2 + k,
+                                    c->sc, c->st);
+    }
+    if (ns[0] || ns[1]) {
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(Rk, c->scal32 + 2, 8, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        for (int k = 0; k < 2; ++k)
+            if (!ns[k]) Rk[k] = 0;
+    }
+    for (int k = 0; k < 2; ++k) {
         const int words = k == 0 ? 6 : 2;
-        gw_ctx::MsgBufs& m = *ms[k];
-        uint32_t R = 0;
-        if (n) {
-            if (n >= 0xffffffffull) return set_err(c, GW_ERANGE, "too many events (%llu)", (unsigned long long)n);
-            if ((rc = ensure(c, c->m_flag, n * 4)) || (rc = ensure(c, c->m_at, n * 4)) || (rc = ensure_scan(c, n)) ||
-                (rc = ensure(c, m.a, n * words * 4)))
-                return rc;
-            launch_event_client_flags(evs[k], n, c->gate, P<uint32_t>(c->m_flag), c->st);
-            scan_u32_u32(P<uint32_t>(c->m_flag), P<uint32_t>(c->m_at), n, nullptr, c->sc, c->scal32 + 2, c->st);
-            launch_event_client_write(evs[k], n, P<uint32_t>(c->m_flag), P<uint32_t>(c->m_at), c->rec,
-                                      P<uint32_t>(m.a), k == 0, c->st);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipMemcpyAsync(&R, c->scal32 + 2, 4, hipMemcpyDeviceToHost, c->st));
-            HIPCHK(hipStreamSynchronize(c->st));
-        }
-        if ((rc = group_msgs(c, m, R, words, false)) || (rc = msg_out(c, m, R, words, flags, outs[k]))) return rc;
-        outs[k]->bytes_alg += n * 8;
+        if ((rc = group_msgs(c, *ms[k], Rk[k], words, false)) || (rc = msg_out(c, *ms[k], Rk[k], words, flags, outs[k])))
+            return rc;
+        outs[k]->bytes_alg += ns[k] * 8;
     }
     HIPCHK(hipEventRecord(c->ev_t1, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
@@ -1748,8 +1751,20 @@ int gw_fanout(gw_ctx* c, const uint32_t* slots, uint32_t n, uint32_t flags, gw_m
     if ((rc = settle(c))) return rc;
     (void)hipSetDevice(c->dev);
     memset(out, 0, sizeof *out);
-    for (uint32_t k = 0; k < n; ++k)
-        if (slots[k] >= c->total_slots) return set_err(c, GW_ERANGE, "fanout: slot %u out of range", slots[k]);
+    // the calls are checked while they are staged in pinned memory (an async
+    // copy from there instead of a pageable one)
+    if (n && (rc = ensure_host(c, c->h_items, (size_t)n * 4))) return rc;
+    uint32_t* hi = (uint32_t*)c->h_items.p;
+    uint32_t bad = 0;
+    const uint32_t C = c->total_slots;
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t s = slots[k];
+        bad |= s >= C;
+        hi[k] = s;
+    }
+    if (bad)
+        for (uint32_t k = 0; k < n; ++k)
+            if (slots[k] >= C) return set_err(c, GW_ERANGE, "fanout: slot %u out of range", slots[k]);
     HIPCHK(hipEventRecord(c->ev_t0, c->st));
     gw_ctx::MsgBufs& m = c->m_fanout;
     const uint32_t G = (uint32_t)c->max_gate + 1;
@@ -1760,7 +1775,7 @@ int gw_fanout(gw_ctx* c, const uint32_t* slots, uint32_t n, uint32_t flags, gw_m
         if ((rc = ensure(c, c->m_items, (size_t)n * 4)) || (rc = ensure(c, c->m_cnt, (size_t)n * 4)) ||
             (rc = ensure(c, c->m_off, ((size_t)n + 1) * 8)) || (rc = ensure_scan(c, n)))
             return rc;
-        HIPCHK(hipMemcpyAsync(c->m_items.p, slots, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
+        HIPCHK(hipMemcpyAsync(c->m_items.p, hi, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
         const World w = world(c);
         launch_fanout(w, P<uint32_t>(c->m_items), n, P<uint32_t>(c->m_cnt), nullptr, nullptr, nullptr, c->st);
         uint64_t* tot = P<uint64_t>(c->m_off) + n;   // the total lands after the offsets

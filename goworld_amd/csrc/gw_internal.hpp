@@ -434,9 +434,9 @@ void launch_client_segments(const gw_sync_record* rec, uint64_t n, uint32_t* hea
 void launch_restore(const World& w, const uint32_t* slots, const float4* xyzw, uint32_t n,
                     unsigned long long stamp_base, uint32_t flags, hipStream_t s);
 // client messages (sync.hip)
-void launch_event_client_flags(const gw_event* ev, uint64_t n, const uint16_t* gate, uint32_t* f, hipStream_t s);
-void launch_event_client_write(const gw_event* ev, uint64_t n, const uint32_t* f, const uint32_t* at,
-                               const SlotRec* rec, uint32_t* out, bool create, hipStream_t s);
+// client messages of n events in one look-back pass; the count to *n_out
+void launch_event_client_compact(const gw_event* ev, uint64_t n, const uint16_t* gate, const SlotRec* rec,
+                                 uint32_t* out, bool create, uint32_t* n_out, ScanCtx& sc, hipStream_t s);
 // out == nullptr: counts per item into cnt; else deliveries at off[k]
 void launch_fanout(const World& w, const uint32_t* items, uint32_t n, uint32_t* cnt, const uint64_t* off,
                    uint32_t* keys, uint32_t* vals, hipStream_t s);

@@ -865,39 +865,78 @@ void launch_fill_i32(int32_t* p, int32_t v, uint64_t n, hipStream_t s) {
 //
 // (a) AOI events -> client messages: Entity.interest / uninterest call
 // e.client.sendCreateEntity(other) / sendDestroyEntity(other), a no-op when the
-// watcher has no client (Entity.go:236-246, GameClient.go:37-59).  A flag per
-// canonical event, a scan, and a write pass that keeps the (watcher, target)
-// order; creates carry the target's position and yaw (GameClient.go:49-52).
-__global__ void __launch_bounds__(NT) k_event_client_flags(const gw_event* __restrict__ ev, uint64_t n,
-                                                           const uint16_t* __restrict__ gate, uint32_t* f) {
-    const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
-    if (r < n) f[r] = gate[ev[r].watcher] != 0 ? 1u : 0u;
-}
-__global__ void __launch_bounds__(NT) k_event_client_write(const gw_event* __restrict__ ev, uint64_t n,
-                                                           const uint32_t* __restrict__ f,
-                                                           const uint32_t* __restrict__ at,
-                                                           const SlotRec* __restrict__ srec, uint32_t* out,
-                                                           int create) {
-    const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
-    if (r >= n || !f[r]) return;
-    const gw_event e = ev[r];
-    if (create) {
-        const float4 p = srec[e.target].p;
-        gw_sync_record m;
-        m.watcher = e.watcher; m.entity = e.target; m.x = p.x; m.y = p.y; m.z = p.z; m.yaw = p.w;
-        ((gw_sync_record*)out)[at[r]] = m;
-    } else {
-        ((gw_event*)out)[at[r]] = e;
+// watcher has no client (Entity.go:236-246, GameClient.go:37-59).  One pass
+// per kind: a tile of SCAN_TILE canonical events (striped) flags the events
+// whose watcher has a client, takes its offset by a decoupled look-back
+// (prim.hpp) and writes its messages in the (watcher, target) order; creates
+// carry the target's position and yaw (GameClient.go:49-52).  The last tile
+// writes the count.
+__global__ void __launch_bounds__(NT) k_event_client_compact(const gw_event* __restrict__ ev, uint64_t n,
+                                                             const uint16_t* __restrict__ gate,
+                                                             const SlotRec* __restrict__ srec, uint32_t* out,
+                                                             int create, uint32_t* n_out,
+                                                             unsigned long long* __restrict__ status,
+                                                             unsigned long long* __restrict__ ticket,
+                                                             unsigned long long tbase, uint32_t tag) {
+    constexpr int IPT = SCAN_IPT;
+    __shared__ uint32_t lds[IPT * NWAVE];
+    __shared__ uint32_t s_tile, s_prefix;
+    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tbase);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t t0 = (uint64_t)tile * (IPT * NT);
+    gw_event e[IPT];
+    uint32_t c[IPT];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
+        e[j].watcher = 0;
+        e[j].target = 0;
+        if (i < n) e[j] = ev[i];
     }
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t i = t0 + (uint64_t)j * NT + threadIdx.x;
+        c[j] = (i < n && gate[e[j].watcher] != 0) ? 1u : 0u;
+    }
+    uint32_t flag = 0;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) flag |= c[j] << j;
+    uint32_t tot;
+    tile_excl_scan_striped<uint32_t, IPT>(c, lds, tot);
+    if (threadIdx.x < 64) {
+        const uint32_t excl = scan_lookback<uint32_t>(status, tile, tag, tot);
+        if (threadIdx.x == 0) s_prefix = excl;
+    }
+    __syncthreads();
+    const uint32_t pre = s_prefix;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        if (!((flag >> j) & 1u)) continue;
+        const uint32_t at = pre + c[j];
+        if (create) {
+            const float4 p = srec[e[j].target].p;
+            gw_sync_record m;
+            m.watcher = e[j].watcher; m.entity = e[j].target; m.x = p.x; m.y = p.y; m.z = p.z; m.yaw = p.w;
+            ((gw_sync_record*)out)[at] = m;
+        } else {
+            ((gw_event*)out)[at] = e[j];
+        }
+    }
+    if (tile == gridDim.x - 1 && threadIdx.x == 0) *n_out = pre + tot;
 }
-void launch_event_client_flags(const gw_event* ev, uint64_t n, const uint16_t* gate, uint32_t* f, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(k_event_client_flags, dim3(nblk(n, NT)), dim3(NT), 0, s, ev, n, gate, f);
-}
-void launch_event_client_write(const gw_event* ev, uint64_t n, const uint32_t* f, const uint32_t* at,
-                               const SlotRec* rec, uint32_t* out, bool create, hipStream_t s) {
-    if (n)
-        hipLaunchKernelGGL(k_event_client_write, dim3(nblk(n, NT)), dim3(NT), 0, s, ev, n, f, at, rec, out,
-                           create ? 1 : 0);
+void launch_event_client_compact(const gw_event* ev, uint64_t n, const uint16_t* gate, const SlotRec* rec,
+                                 uint32_t* out, bool create, uint32_t* n_out, ScanCtx& sc, hipStream_t s) {
+    if (!n) return;
+    const uint32_t nb = (uint32_t)((n + SCAN_TILE - 1) / SCAN_TILE);
+    if (sc.tag >= SCAN_TAG_MAX) {
+        (void)hipMemsetAsync(sc.status, 0, sc.max_tiles * SCAN_WORDS * 8, s);
+        sc.tag = 0;
+    }
+    ++sc.tag;
+    hipLaunchKernelGGL(k_event_client_compact, dim3(nb), dim3(NT), 0, s, ev, n, gate, rec, out, create ? 1 : 0,
+                       n_out, sc.status, sc.ticket, sc.tbase, sc.tag);
+    sc.tbase += nb;
 }
 
 // (b) AllClients fan-out: CallAllClients and every AllClients attribute

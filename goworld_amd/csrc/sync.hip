@@ -17,11 +17,9 @@ namespace gw {
 // neighbours of a present entity e from the current grid: calls
 // f(rel, w, has_client) per lane for every candidate (rel: w != e is related to e).
 // The window's row ranges are walked flattened, NB_U chunks of 64 in flight.
+// (wave_neighbors_of: e's state a and its space P already loaded)
 template <int NB_U = 4, typename F>
-__device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) {
-    const AoiEnt a = w.rec[e].a;
-    if (!(a.meta & PRESENT_BIT)) return;
-    const SpaceP P = w.sp[a.meta & SPACE_MASK];
+__device__ __forceinline__ void wave_neighbors_of(const World& w, uint32_t e, const AoiEnt& a, const SpaceP& P, F f) {
     const float d = P.d;
     const Win we = win_of(a.x, a.z, d);
     Rects R;
@@ -55,6 +53,12 @@ __device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) 
             f(rel, g.slot, (g.meta & CLIENT_BIT) ? 1u : 0u);
         }
     }
+}
+template <int NB_U = 4, typename F>
+__device__ __forceinline__ void wave_neighbors(const World& w, uint32_t e, F f) {
+    const AoiEnt a = w.rec[e].a;
+    if (!(a.meta & PRESENT_BIT)) return;
+    wave_neighbors_of<NB_U>(w, e, a, w.sp[a.meta & SPACE_MASK], f);
 }
 
 // ---------------------------------------------------------------------------
@@ -259,6 +263,18 @@ __device__ __forceinline__ void sw_flush64(unsigned long long* buf, unsigned lon
 #ifndef GW_SW_MINB
 #define GW_SW_MINB 1
 #endif
+// An entity's header (its flagged-list entry) and state: a wave walks
+// entities k, k + stride, ... and loads the next entity's state and the one
+// after's header before it walks the current one, so those two dependent
+// loads are in flight during the walk instead of ahead of it.
+struct SwHdr {
+    uint32_t e, f, cnt;
+    uint64_t at;
+};
+struct SwEnt {
+    AoiEnt a;
+    uint32_t gt;
+};
 template <int U, bool PAIRS = false>
 __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const uint32_t* __restrict__ flagged,
                                                    const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
@@ -272,19 +288,36 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
     const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
-    for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < nf; k += stride) {
-        const uint32_t e = flagged[k];
-        const uint32_t f = fbits[k];
-        uint64_t at = rec_off[k];
-        if (at + cnt[k] > rec_cap) {
-            if (ln == 0) atomicOr(&st->overflow, 1ull);
-            continue;
+    auto hdr = [&](uint64_t q) {
+        SwHdr h{};
+        if (q < nf) {
+            h.e = flagged[q];
+            h.f = fbits[q];
+            h.at = rec_off[q];
+            h.cnt = cnt[q];
         }
-        const AoiEnt a = w.rec[e].a;
-        const float4 p = w.rec[e].p;                          // loaded with the state, not behind the test
-        const uint32_t gt = w.gate[e];
-        if (!owned_x(w.sp[a.meta & SPACE_MASK], a.x)) continue;
-        if ((f & GW_SIF_OWN_CLIENT) && gt) {
+        return h;
+    };
+    auto ent = [&](uint64_t q, const SwHdr& h) {
+        SwEnt x{};
+        if (q < nf) {
+            x.a = w.rec[h.e].a;
+            x.gt = w.gate[h.e];
+        }
+        return x;
+    };
+    auto one = [&](const SwHdr& h, const SwEnt& x) {
+        const uint32_t e = h.e, f = h.f;
+        uint64_t at = h.at;
+        if (at + h.cnt > rec_cap) {
+            if (ln == 0) atomicOr(&st->overflow, 1ull);
+            return;
+        }
+        const AoiEnt a = x.a;
+        const float4 p = w.rec[e].p;                          // used at the first record: in flight with the walk
+        const SpaceP P = w.sp[a.meta & SPACE_MASK];
+        if (!owned_x(P, a.x)) return;
+        if ((f & GW_SIF_OWN_CLIENT) && x.gt) {
             if (ln == 0) {
                 if (PAIRS) {
                     pk[at] = e;
@@ -295,8 +328,9 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
             }
             ++at;
         }
-        if (PAIRS && (f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
-            wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
+        if (!(f & GW_SIF_NEIGHBOR_CLIENTS) || !(a.meta & PRESENT_BIT)) return;
+        if (PAIRS) {
+            wave_neighbors_of<U>(w, e, a, P, [&](bool rel, uint32_t ws, uint32_t g) {
                 const bool take = rel && g != 0;
                 const uint64_t bt = wave_ballot(take);
                 if (take) {
@@ -306,37 +340,50 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
                 }
                 at += (uint64_t)popc64(bt);
             });
-        } else if ((f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
-            const unsigned long long pxy = ((unsigned long long)__float_as_uint(p.y) << 32) | __float_as_uint(p.x);
-            const unsigned long long pzw = ((unsigned long long)__float_as_uint(p.w) << 32) | __float_as_uint(p.z);
-            uint32_t nb = 0;                                   // staged records (wave-uniform)
-            wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
-                const bool take = rel && g != 0;
-                const uint64_t bt = wave_ballot(take);
-                if (take) {
-                    unsigned long long* r = buf + 3 * (nb + (uint32_t)popc64(bt & lt));
-                    r[0] = ((unsigned long long)e << 32) | ws;
-                    r[1] = pxy;
-                    r[2] = pzw;
-                }
-                nb += (uint32_t)popc64(bt);
-                if (nb >= 64) {
-                    wave_sync();
-                    sw_flush64(buf, (unsigned long long*)(rec + at), 64);
-                    at += 64;
-                    nb -= 64;
-                    wave_sync();
-                    for (uint32_t i = (uint32_t)ln; i < 3 * nb; i += 64) buf[i] = buf[192 + i];
-                    wave_sync();
-                }
-            });
-            if (nb) {
+            return;
+        }
+        const unsigned long long pxy = ((unsigned long long)__float_as_uint(p.y) << 32) | __float_as_uint(p.x);
+        const unsigned long long pzw = ((unsigned long long)__float_as_uint(p.w) << 32) | __float_as_uint(p.z);
+        uint32_t nb = 0;                                      // staged records (wave-uniform)
+        wave_neighbors_of<U>(w, e, a, P, [&](bool rel, uint32_t ws, uint32_t g) {
+            const bool take = rel && g != 0;
+            const uint64_t bt = wave_ballot(take);
+            if (take) {
+                unsigned long long* r = buf + 3 * (nb + (uint32_t)popc64(bt & lt));
+                r[0] = ((unsigned long long)e << 32) | ws;
+                r[1] = pxy;
+                r[2] = pzw;
+            }
+            nb += (uint32_t)popc64(bt);
+            if (nb >= 64) {
                 wave_sync();
-                sw_flush64(buf, (unsigned long long*)(rec + at), nb);
-                at += nb;
+                sw_flush64(buf, (unsigned long long*)(rec + at), 64);
+                at += 64;
+                nb -= 64;
+                wave_sync();
+                for (uint32_t i = (uint32_t)ln; i < 3 * nb; i += 64) buf[i] = buf[192 + i];
                 wave_sync();
             }
+        });
+        if (nb) {
+            wave_sync();
+            sw_flush64(buf, (unsigned long long*)(rec + at), nb);
+            wave_sync();
         }
+    };
+    // the wave index as a uniform value: the headers and states are scalar
+    // loads into SGPRs, not VGPRs that would cost the walk its occupancy
+    uint64_t k = (uint64_t)blockIdx.x * NWAVE + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    SwHdr h0 = hdr(k);
+    SwEnt x0 = ent(k, h0);
+    SwHdr h1 = hdr(k + stride);
+    for (; k < nf; k += stride) {
+        const SwEnt x1 = ent(k + stride, h1);
+        const SwHdr h2 = hdr(k + 2 * stride);
+        one(h0, x0);
+        h0 = h1;
+        x0 = x1;
+        h1 = h2;
     }
 }
 // ---------------------------------------------------------------------------

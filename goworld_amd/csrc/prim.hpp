@@ -499,6 +499,7 @@ constexpr int RS2_MAX_RADIX = 2048;                 // DB <= 11
 constexpr int RS2_STATUS_PER_TILE = 4096;           // max over the digit widths of passes * radix
 constexpr int RS2_GBLOCKS = 1024;                   // blocks of the upfront histogram (grid-stride)
 constexpr uint32_t OS_AGG = 1u << 30, OS_INC = 2u << 30, OS_VAL = (1u << 30) - 1;
+constexpr int OS_LB = 4;                             // predecessors a look-back step reads
 
 template <int DB>
 struct OsCfg {
@@ -640,13 +641,29 @@ __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__
         }
 #pragma unroll
         for (int u = 0; u < C::DPT; ++u) {
+            // the look-back reads OS_LB predecessors per step (their loads in
+            // flight together) and consumes them nearest first, up to the first
+            // inclusive prefix or the first word not posted yet (re-read from
+            // there): a walk over many aggregate-only tiles is OS_LB times shorter
             const uint32_t d = (uint32_t)t * C::DPT + u;
             uint32_t excl = 0;
-            for (int64_t j = (int64_t)tile - 1; j >= 0; --j) {
-                uint32_t v;
-                do { v = os_ld(status + (uint64_t)j * C::RD + d); } while (!(v & (OS_AGG | OS_INC)));
-                excl += v & OS_VAL;
-                if (v & OS_INC) break;
+            int64_t j = (int64_t)tile - 1;
+            while (j >= 0) {
+                uint32_t v[OS_LB];
+#pragma unroll
+                for (int q = 0; q < OS_LB; ++q)
+                    v[q] = j - q >= 0 ? os_ld(status + (uint64_t)(j - q) * C::RD + d) : OS_INC;
+                bool done = false;
+                int used = 0;
+#pragma unroll
+                for (int q = 0; q < OS_LB; ++q) {
+                    if (done || used < q || !(v[q] & (OS_AGG | OS_INC))) continue;
+                    excl += v[q] & OS_VAL;
+                    ++used;
+                    done = (v[q] & OS_INC) != 0;
+                }
+                if (done) break;
+                j -= used;
             }
             if (tile) os_st(status + (uint64_t)tile * C::RD + d, OS_INC | (excl + run[u]));
             gofs[d] = gbase[d] + excl;

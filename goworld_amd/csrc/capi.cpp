@@ -554,7 +554,7 @@ void gw_shutdown(gw_ctx* c) {
     (void)settle(c);
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1,
+    DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->pay, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1,
                       &c->gm, &c->cand, &c->reg, &c->pidx, &c->heavy, &c->rowrec, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
                       &c->mcnt, &c->moff, &c->minfo, &c->icnt, &c->ioff, &c->mreg, &c->chunk_first, &c->srange, &c->bk_a, &c->bk_b, &c->bk_id, &c->bk_cnt, &c->bk_split, &c->ev_d, &c->rtable,
                       &c->scan_status, &c->rs_hist, &c->rs_os,
@@ -1448,7 +1448,9 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     // after the sort (not written, keyed, sorted and gathered at 24 B)
     const bool by_client = (flags & GW_SYNC_BY_CLIENT) != 0;
     const bool pairs = by_client && !small;
-    if (pairs && ((rc = ensure(c, c->gk0, c->rec_cap * 4)) || (rc = ensure(c, c->gv0, c->rec_cap * 4)))) return rc;
+    if (pairs && ((rc = ensure(c, c->gk0, c->rec_cap * 4)) || (rc = ensure(c, c->gv0, c->rec_cap * 4)) ||
+                  (rc = ensure(c, c->pay, (size_t)NFM * 16))))
+        return rc;
     prof_begin(c, "sync_write");
     auto write_pass = [&]() {
         if (small)
@@ -1458,7 +1460,8 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         else
             launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint64_t>(c->rec_off),
                               P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st,
-                              pairs ? P<uint32_t>(c->gk0) : nullptr, pairs ? P<uint32_t>(c->gv0) : nullptr);
+                              pairs ? P<uint32_t>(c->gk0) : nullptr, pairs ? P<uint32_t>(c->gv0) : nullptr,
+                              pairs ? P<float4>(c->pay) : nullptr);
     };
     write_pass();
     size_t s_write = prof_end(c, 0);
@@ -1481,7 +1484,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     gw_sync_record* recs = P<gw_sync_record>(c->rec0);
     bool gates_done = false;
     if (pairs) {
-        // (watcher, entity) pairs in entity order -> stable sort by watcher ->
+        // (watcher, flagged index) pairs in entity order -> stable sort by watcher ->
         // with several gates in use a stable sort of the pairs' gates -> records:
         // order (gate, watcher, entity)
         prof_begin(c, "sync_clients");
@@ -1525,8 +1528,8 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
             if ((rc = ensure(c, c->cl_slot, R * 4)) || (rc = ensure(c, c->cl_off, (R + 1) * 8)) ||
                 (rc = ensure_scan(c, R)))
                 return rc;
-            launch_records_seg(w, wk, wv, idx, R, recs, P<uint32_t>(c->cl_slot), P<uint64_t>(c->cl_off),
-                               c->scal32 + 1, c->sc, c->st);
+            launch_records_seg(w, wk, wv, idx, P<uint32_t>(c->flagged), P<float4>(c->pay), R, recs,
+                               P<uint32_t>(c->cl_slot), P<uint64_t>(c->cl_off), c->scal32 + 1, c->sc, c->st);
             HIPCHK(hipGetLastError());
         }
         prof_end(c, R * (8 * 2 * 3 + 24));

@@ -230,6 +230,7 @@ struct gw_ctx {
     DevBuf fbits, flagged, rec_cnt, rec_off, rec0, rec1, gate_hist, gk0, gv0, gk1, gv1, qbuf;
     DevBuf cl_slot, cl_off, h_cl_slot, h_cl_off;   // GW_SYNC_BY_CLIENT segments (device / pinned host)
     DevBuf h_items;                               // gw_fanout's calls, staged in pinned memory
+    DevBuf pay;                                   // per-client collect: payload per flagged entity
     uint64_t rec_cap = 0;                // records the rec0 buffer holds (grows on overflow)
     uint64_t flag_bound = 0;             // ops + restored slots since the last collect (>= flagged slots)
     // client messages (gw_client_events, gw_fanout): ping-pong + pinned host + gate offsets

@@ -345,11 +345,12 @@ void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* 
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
                        uint64_t rec_cap, DevStats* st, hipStream_t s,
-                       uint32_t* pk = nullptr, uint32_t* pv = nullptr);
+                       uint32_t* pk = nullptr, uint32_t* pv = nullptr, float4* pay = nullptr);
 // the records and the client segment table in one pass (k_records_seg)
-void launch_records_seg(const World& w, const uint32_t* pk, const uint32_t* pv, const uint32_t* idx, uint64_t n,
-                        gw_sync_record* out, uint32_t* client_slot, uint64_t* client_off, uint32_t* n_clients,
-                        ScanCtx& sc, hipStream_t s);
+void launch_records_seg(const World& w, const uint32_t* pk, const uint32_t* pv, const uint32_t* idx,
+                        const uint32_t* flagged, const float4* pay, uint64_t n, gw_sync_record* out,
+                        uint32_t* client_slot, uint64_t* client_off, uint32_t* n_clients, ScanCtx& sc,
+                        hipStream_t s);
 void launch_gate_hist(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,
                       uint32_t* hist /*65536*/, hipStream_t s);
 void launch_gate_keys(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,

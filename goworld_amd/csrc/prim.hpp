@@ -7,6 +7,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "gw_internal.hpp"
 
@@ -762,6 +763,9 @@ inline int radix_sort2(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, u
     const uint64_t nt = radix2_tiles(n_max);
     if (nt == 0 || hi_bit <= lo_bit) return 0;
     const int bits = hi_bit - lo_bit;
+    static const int db_max = getenv("GW_SORT_DB") ? atoi(getenv("GW_SORT_DB")) : 11;   // A/B of digit widths
+    if (db_max <= 8)
+        return radix_sort2_db<8>(k0, v0, k1, v1, n_max, n_dev, lo_bit, (bits + 7) / 8, scratch, st, aos, aos_mask);
     if (bits > 16 && bits <= 20)
         return radix_sort2_db<10>(k0, v0, k1, v1, n_max, n_dev, lo_bit, 2, scratch, st, aos, aos_mask);
     if (bits > 20 && bits <= 22)

@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
                                                    uint32_t nf_max, const uint64_t* __restrict__ rec_off,
                                                    const uint32_t* __restrict__ cnt, gw_sync_record* rec,
                                                    uint64_t rec_cap, DevStats* st, uint32_t* __restrict__ pk,
-                                                   uint32_t* __restrict__ pv) {
+                                                   uint32_t* __restrict__ pv, float4* __restrict__ pay) {
     __shared__ unsigned long long sbuf[NWAVE][3 * SW_BUF];
     unsigned long long* buf = sbuf[threadIdx.x >> 6];
     const uint64_t nf = load_n(nf_max, nf_dev);
@@ -306,7 +306,7 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
         }
         return x;
     };
-    auto one = [&](const SwHdr& h, const SwEnt& x) {
+    auto one = [&](uint64_t k, const SwHdr& h, const SwEnt& x) {
         const uint32_t e = h.e, f = h.f;
         uint64_t at = h.at;
         if (at + h.cnt > rec_cap) {
@@ -317,11 +317,15 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
         const float4 p = w.rec[e].p;                          // used at the first record: in flight with the walk
         const SpaceP P = w.sp[a.meta & SPACE_MASK];
         if (!owned_x(P, a.x)) return;
+        // PAIRS: the value is the flagged index k, and the entity's payload goes
+        // to pay[k]: the records are built from that compact table (L2-resident)
+        // instead of a 64-B slot-state line per record
+        if (PAIRS && ln == 0) pay[k] = p;
         if ((f & GW_SIF_OWN_CLIENT) && x.gt) {
             if (ln == 0) {
                 if (PAIRS) {
                     pk[at] = e;
-                    pv[at] = e;
+                    pv[at] = (uint32_t)k;
                 } else {
                     st_record_nt(rec + at, e, e, p);
                 }
@@ -336,7 +340,7 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
                 if (take) {
                     const uint64_t j = at + (uint64_t)popc64(bt & lt);
                     pk[j] = ws;
-                    pv[j] = e;
+                    pv[j] = (uint32_t)k;
                 }
                 at += (uint64_t)popc64(bt);
             });
@@ -380,7 +384,7 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
     for (; k < nf; k += stride) {
         const SwEnt x1 = ent(k + stride, h1);
         const SwHdr h2 = hdr(k + 2 * stride);
-        one(h0, x0);
+        one(k, h0, x0);
         h0 = h1;
         x0 = x1;
         h1 = h2;
@@ -634,21 +638,21 @@ void launch_sync_write_small(const World& w, uint32_t n_spaces, const uint32_t* 
 
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
-                       uint64_t rec_cap, DevStats* st, hipStream_t s, uint32_t* pk, uint32_t* pv) {
+                       uint64_t rec_cap, DevStats* st, hipStream_t s, uint32_t* pk, uint32_t* pv, float4* pay) {
     if (!nf_max) return;
     const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
     if (pk)
         hipLaunchKernelGGL((k_sync_write<4, true>), g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt,
-                           rec, rec_cap, st, pk, pv);
+                           rec, rec_cap, st, pk, pv, pay);
     else if (w.nb_u >= 8)
         hipLaunchKernelGGL(k_sync_write<8>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st, pk, pv);
+                           rec_cap, st, pk, pv, pay);
     else if (w.nb_u <= 2)
         hipLaunchKernelGGL(k_sync_write<2>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st, pk, pv);
+                           rec_cap, st, pk, pv, pay);
     else
         hipLaunchKernelGGL(k_sync_write<4>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st, pk, pv);
+                           rec_cap, st, pk, pv, pay);
 }
 
 // 24-B records from sorted (watcher, entity) pairs (through idx, the gate
@@ -662,7 +666,9 @@ void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* 
 // element, lane 0 loads its own.
 __global__ void __launch_bounds__(NT) k_records_seg(World w, const uint32_t* __restrict__ pk,
                                                     const uint32_t* __restrict__ pv,
-                                                    const uint32_t* __restrict__ idx, uint64_t n,
+                                                    const uint32_t* __restrict__ idx,
+                                                    const uint32_t* __restrict__ flagged,
+                                                    const float4* __restrict__ pay, uint64_t n,
                                                     gw_sync_record* __restrict__ out,
                                                     uint32_t* __restrict__ client_slot,
                                                     uint64_t* __restrict__ client_off, uint32_t* n_clients,
@@ -681,20 +687,23 @@ __global__ void __launch_bounds__(NT) k_records_seg(World w, const uint32_t* __r
     uint32_t wt[IPT], c[IPT];
 #pragma unroll
     for (int j0 = 0; j0 < IPT; j0 += G) {
-        uint32_t e[G], pw[G];
+        uint32_t e[G], pw[G], f[G];
         float4 p[G];
 #pragma unroll
         for (int u = 0; u < G; ++u) {
             const uint64_t i = t0 + (uint64_t)(j0 + u) * NT + threadIdx.x;
             const uint32_t q = i < n ? (idx ? idx[i] : (uint32_t)i) : 0u;
             wt[j0 + u] = i < n ? pk[q] : 0xffffffffu;
-            e[u] = i < n ? pv[q] : 0u;
+            f[u] = i < n ? pv[q] : 0u;
             pw[u] = (ln == 0 && i < n && i > 0) ? pk[idx ? idx[i - 1] : (uint32_t)(i - 1)] : 0xffffffffu;
         }
 #pragma unroll
-        for (int u = 0; u < G; ++u) {
+        for (int u = 0; u < G; ++u) {                    // the flagged entity's slot and payload
             const uint64_t i = t0 + (uint64_t)(j0 + u) * NT + threadIdx.x;
-            if (i < n) p[u] = w.rec[e[u]].p;
+            if (i < n) {
+                e[u] = flagged[f[u]];
+                p[u] = pay[f[u]];
+            }
         }
 #pragma unroll
         for (int u = 0; u < G; ++u) {
@@ -729,9 +738,10 @@ __global__ void __launch_bounds__(NT) k_records_seg(World w, const uint32_t* __r
         client_off[pre + tot] = n;                       // end of the last client
     }
 }
-void launch_records_seg(const World& w, const uint32_t* pk, const uint32_t* pv, const uint32_t* idx, uint64_t n,
-                        gw_sync_record* out, uint32_t* client_slot, uint64_t* client_off, uint32_t* n_clients,
-                        ScanCtx& sc, hipStream_t s) {
+void launch_records_seg(const World& w, const uint32_t* pk, const uint32_t* pv, const uint32_t* idx,
+                        const uint32_t* flagged, const float4* pay, uint64_t n, gw_sync_record* out,
+                        uint32_t* client_slot, uint64_t* client_off, uint32_t* n_clients, ScanCtx& sc,
+                        hipStream_t s) {
     if (!n) return;
     const uint32_t nb = (uint32_t)((n + SCAN_TILE - 1) / SCAN_TILE);
     if (sc.tag >= SCAN_TAG_MAX) {
@@ -739,8 +749,8 @@ void launch_records_seg(const World& w, const uint32_t* pk, const uint32_t* pv, 
         sc.tag = 0;
     }
     ++sc.tag;
-    hipLaunchKernelGGL(k_records_seg, dim3(nb), dim3(NT), 0, s, w, pk, pv, idx, n, out, client_slot, client_off,
-                       n_clients, sc.status, sc.ticket, sc.tbase, sc.tag);
+    hipLaunchKernelGGL(k_records_seg, dim3(nb), dim3(NT), 0, s, w, pk, pv, idx, flagged, pay, n, out, client_slot,
+                       client_off, n_clients, sc.status, sc.ticket, sc.tbase, sc.tag);
     sc.tbase += nb;
 }
 

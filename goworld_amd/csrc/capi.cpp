@@ -1448,8 +1448,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     // after the sort (not written, keyed, sorted and gathered at 24 B)
     const bool by_client = (flags & GW_SYNC_BY_CLIENT) != 0;
     const bool pairs = by_client && !small;
-    if (pairs && ((rc = ensure(c, c->gk0, c->rec_cap * 4)) || (rc = ensure(c, c->gv0, c->rec_cap * 4)) ||
-                  (rc = ensure(c, c->pay, (size_t)NFM * 16))))
+    if (pairs && ((rc = ensure(c, c->gk0, c->rec_cap * 8)) || (rc = ensure(c, c->pay, (size_t)NFM * 16))))
         return rc;
     prof_begin(c, "sync_write");
     auto write_pass = [&]() {
@@ -1460,8 +1459,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         else
             launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint64_t>(c->rec_off),
                               P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st,
-                              pairs ? P<uint32_t>(c->gk0) : nullptr, pairs ? P<uint32_t>(c->gv0) : nullptr,
-                              pairs ? P<float4>(c->pay) : nullptr);
+                              pairs ? P<uint64_t>(c->gk0) : nullptr, pairs ? P<float4>(c->pay) : nullptr);
     };
     write_pass();
     size_t s_write = prof_end(c, 0);
@@ -1473,7 +1471,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     if (c->hcstats->overflow) {
         c->rec_cap = R + R / 4 + 1024;
         if ((rc = ensure(c, c->rec0, c->rec_cap * sizeof(gw_sync_record)))) return rc;
-        if (pairs && ((rc = ensure(c, c->gk0, c->rec_cap * 4)) || (rc = ensure(c, c->gv0, c->rec_cap * 4)))) return rc;
+        if (pairs && (rc = ensure(c, c->gk0, c->rec_cap * 8))) return rc;
         c->hcstats->overflow = 0;
         HIPCHK(hipMemcpyAsync(c->cstats, c->hcstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
         write_pass();
@@ -1484,34 +1482,28 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     gw_sync_record* recs = P<gw_sync_record>(c->rec0);
     bool gates_done = false;
     if (pairs) {
-        // (watcher, flagged index) pairs in entity order -> stable sort by watcher ->
-        // with several gates in use a stable sort of the pairs' gates -> records:
-        // order (gate, watcher, entity)
+        // (watcher, flagged index) pairs, packed u64, in entity order -> stable
+        // sort by watcher -> with several gates in use a stable sort of the
+        // pairs' gates -> records and client table: order (gate, watcher, entity)
         prof_begin(c, "sync_clients");
         gates_done = true;
         const uint32_t* idx = nullptr;
-        uint32_t *wk = P<uint32_t>(c->gk0), *wv = P<uint32_t>(c->gv0);
+        uint64_t* wp = P<uint64_t>(c->gk0);
         for (uint32_t g = 0; g <= G; ++g) c->gate_off[g] = (g == G) ? R : 0;   // one gate id in use
         if (R) {
-            if ((rc = ensure(c, c->gk1, R * 4)) || (rc = ensure(c, c->gv1, R * 4))) return rc;
+            if ((rc = ensure(c, c->gk1, R * 8))) return rc;
             RadixTmp rt;
             if ((rc = radix_tmp(c, R, rt))) return rc;
-            if (R > 1) {
-                const int wsel = sort_u32_u32(P<uint32_t>(c->gk0), P<uint32_t>(c->gv0), P<uint32_t>(c->gk1),
-                                              P<uint32_t>(c->gv1), R, nullptr, 0, ceil_log2(C), rt, c->st);
-                if (wsel) {
-                    wk = P<uint32_t>(c->gk1);
-                    wv = P<uint32_t>(c->gv1);
-                }
-            }
+            if (R > 1 && sort_pairs64(P<uint64_t>(c->gk0), P<uint64_t>(c->gk1), R, nullptr, 0, ceil_log2(C), rt, c->st))
+                wp = P<uint64_t>(c->gk1);
             if (G > 2) {
-                uint32_t* ka = wk == P<uint32_t>(c->gk0) ? P<uint32_t>(c->gk1) : P<uint32_t>(c->gk0);
-                uint32_t* va = wv == P<uint32_t>(c->gv0) ? P<uint32_t>(c->gv1) : P<uint32_t>(c->gv0);
-                if ((rc = ensure(c, c->m_flag, R * 4)) || (rc = ensure(c, c->m_at, R * 4)) ||
+                if ((rc = ensure(c, c->gv0, R * 4)) || (rc = ensure(c, c->gv1, R * 4)) ||
+                    (rc = ensure(c, c->m_flag, R * 4)) || (rc = ensure(c, c->m_at, R * 4)) ||
                     (rc = ensure(c, c->gate_hist, (size_t)65536 * 4)))
                     return rc;
+                uint32_t *ka = P<uint32_t>(c->gv0), *va = P<uint32_t>(c->gv1);
                 HIPCHK(hipMemsetAsync(c->gate_hist.p, 0, (size_t)G * 4, c->st));
-                launch_gate_keys(wk, c->gate, R, ka, va, P<uint32_t>(c->gate_hist), c->st);
+                launch_gate_keys(wp, c->gate, R, ka, va, P<uint32_t>(c->gate_hist), c->st);
                 std::vector<uint32_t> h(G);
                 HIPCHK(hipMemcpyAsync(h.data(), c->gate_hist.p, (size_t)G * 4, hipMemcpyDeviceToHost, c->st));
                 HIPCHK(hipStreamSynchronize(c->st));
@@ -1528,7 +1520,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
             if ((rc = ensure(c, c->cl_slot, R * 4)) || (rc = ensure(c, c->cl_off, (R + 1) * 8)) ||
                 (rc = ensure_scan(c, R)))
                 return rc;
-            launch_records_seg(w, wk, wv, idx, P<uint32_t>(c->flagged), P<float4>(c->pay), R, recs,
+            launch_records_seg(w, wp, idx, P<uint32_t>(c->flagged), P<float4>(c->pay), R, recs,
                                P<uint32_t>(c->cl_slot), P<uint64_t>(c->cl_off), c->scal32 + 1, c->sc, c->st);
             HIPCHK(hipGetLastError());
         }
@@ -1780,7 +1772,7 @@ int gw_fanout(gw_ctx* c, const uint32_t* slots, uint32_t n, uint32_t flags, gw_m
             return rc;
         HIPCHK(hipMemcpyAsync(c->m_items.p, hi, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
         const World w = world(c);
-        launch_fanout(w, P<uint32_t>(c->m_items), n, P<uint32_t>(c->m_cnt), nullptr, nullptr, nullptr, c->st);
+        launch_fanout(w, P<uint32_t>(c->m_items), n, P<uint32_t>(c->m_cnt), nullptr, nullptr, c->st);
         uint64_t* tot = P<uint64_t>(c->m_off) + n;   // the total lands after the offsets
         scan_u32_u64(P<uint32_t>(c->m_cnt), P<uint64_t>(c->m_off), n, nullptr, c->sc, tot, c->st);
         HIPCHK(hipGetLastError());
@@ -1788,30 +1780,29 @@ int gw_fanout(gw_ctx* c, const uint32_t* slots, uint32_t n, uint32_t flags, gw_m
         HIPCHK(hipStreamSynchronize(c->st));
     }
     if (R) {
-        // deliveries as (watcher, item) pairs, a stable radix sort by watcher
-        // (item order inside each watcher), then, with several gates in use, a
-        // stable sort of the pairs' gates; the 12-B records are written once
-        if ((rc = ensure(c, c->gk0, R * 4)) || (rc = ensure(c, c->gv0, R * 4)) || (rc = ensure(c, c->gk1, R * 4)) ||
-            (rc = ensure(c, c->gv1, R * 4)) || (rc = ensure(c, m.a, R * sizeof(gw_fanout_rec))))
+        // deliveries as packed (watcher, item) pairs, a stable radix sort by
+        // watcher (item order inside each watcher), then, with several gates in
+        // use, a stable sort of the pairs' gates; the 12-B records are written once
+        if ((rc = ensure(c, c->gk0, R * 8)) || (rc = ensure(c, c->gk1, R * 8)) ||
+            (rc = ensure(c, m.a, R * sizeof(gw_fanout_rec))))
             return rc;
         RadixTmp rt;
         if ((rc = radix_tmp(c, R, rt))) return rc;
         const World w = world(c);
-        launch_fanout(w, P<uint32_t>(c->m_items), n, nullptr, P<uint64_t>(c->m_off), P<uint32_t>(c->gk0),
-                      P<uint32_t>(c->gv0), c->st);
-        const int sel = sort_u32_u32(P<uint32_t>(c->gk0), P<uint32_t>(c->gv0), P<uint32_t>(c->gk1),
-                                     P<uint32_t>(c->gv1), R, nullptr, 0, ceil_log2(c->total_slots), rt, c->st);
-        uint32_t* wk = sel ? P<uint32_t>(c->gk1) : P<uint32_t>(c->gk0);
-        uint32_t* wv = sel ? P<uint32_t>(c->gv1) : P<uint32_t>(c->gv0);
+        launch_fanout(w, P<uint32_t>(c->m_items), n, nullptr, P<uint64_t>(c->m_off), P<uint64_t>(c->gk0), c->st);
+        uint64_t* wp = P<uint64_t>(c->gk0);
+        if (sort_pairs64(P<uint64_t>(c->gk0), P<uint64_t>(c->gk1), R, nullptr, 0, ceil_log2(c->total_slots), rt,
+                         c->st))
+            wp = P<uint64_t>(c->gk1);
         const uint32_t* idx = nullptr;
         if (G > 2) {
-            uint32_t* ka = sel ? P<uint32_t>(c->gk0) : P<uint32_t>(c->gk1);   // the free pair + two more words
-            uint32_t* va = sel ? P<uint32_t>(c->gv0) : P<uint32_t>(c->gv1);
-            if ((rc = ensure(c, c->m_flag, R * 4)) || (rc = ensure(c, c->m_at, R * 4)) ||
+            if ((rc = ensure(c, c->gv0, R * 4)) || (rc = ensure(c, c->gv1, R * 4)) ||
+                (rc = ensure(c, c->m_flag, R * 4)) || (rc = ensure(c, c->m_at, R * 4)) ||
                 (rc = ensure(c, c->gate_hist, (size_t)65536 * 4)))
                 return rc;
+            uint32_t *ka = P<uint32_t>(c->gv0), *va = P<uint32_t>(c->gv1);
             HIPCHK(hipMemsetAsync(c->gate_hist.p, 0, (size_t)G * 4, c->st));
-            launch_gate_keys(wk, c->gate, R, ka, va, P<uint32_t>(c->gate_hist), c->st);
+            launch_gate_keys(wp, c->gate, R, ka, va, P<uint32_t>(c->gate_hist), c->st);
             std::vector<uint32_t> h(G);
             HIPCHK(hipMemcpyAsync(h.data(), c->gate_hist.p, (size_t)G * 4, hipMemcpyDeviceToHost, c->st));
             HIPCHK(hipStreamSynchronize(c->st));
@@ -1827,7 +1818,7 @@ int gw_fanout(gw_ctx* c, const uint32_t* slots, uint32_t n, uint32_t flags, gw_m
         } else {
             for (uint32_t g = 0; g <= G; ++g) m.goff[g] = (g == G) ? R : 0;   // one gate id in use
         }
-        launch_fanout_final(wk, wv, idx, P<uint32_t>(c->m_items), R, P<gw_fanout_rec>(m.a), c->st);
+        launch_fanout_final(wp, idx, P<uint32_t>(c->m_items), R, P<gw_fanout_rec>(m.a), c->st);
         HIPCHK(hipGetLastError());
     }
     if ((rc = msg_out(c, m, R, 3, flags, out))) return rc;

@@ -164,6 +164,9 @@ void scan_u32_u64(const uint32_t* in, uint64_t* out, uint64_t n_max, const uint6
                   uint64_t* total, hipStream_t s);
 void scan_u64_u64(const uint64_t* in, uint64_t* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
                   uint64_t* total, hipStream_t s);
+// stable sort of packed pairs (u64: value << 32 | key) by key bits [lo_bit, hi_bit); 1 = result in p1
+int sort_pairs64(uint64_t* p0, uint64_t* p1, uint64_t n_max, const uint64_t* n_dev, int lo_bit, int hi_bit,
+                 RadixTmp& tmp, hipStream_t s);
 int sort_u32_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
                  int lo_bit, int hi_bit, RadixTmp& tmp, hipStream_t s);
 
@@ -345,10 +348,9 @@ void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* 
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
                        uint64_t rec_cap, DevStats* st, hipStream_t s,
-                       uint32_t* pk = nullptr, uint32_t* pv = nullptr, float4* pay = nullptr);
+                       uint64_t* pairs = nullptr, float4* pay = nullptr);
 // the records and the client segment table in one pass (k_records_seg)
-void launch_records_seg(const World& w, const uint32_t* pk, const uint32_t* pv, const uint32_t* idx,
-                        const uint32_t* flagged, const float4* pay, uint64_t n, gw_sync_record* out,
+void launch_records_seg(const World& w, const uint64_t* pairs, const uint32_t* idx, const uint32_t* flagged, const float4* pay, uint64_t n, gw_sync_record* out,
                         uint32_t* client_slot, uint64_t* client_off, uint32_t* n_clients, ScanCtx& sc,
                         hipStream_t s);
 void launch_gate_hist(const gw_sync_record* rec, const uint64_t* n_dev, uint64_t n_max, const uint16_t* gate,
@@ -440,11 +442,11 @@ void launch_event_client_compact(const gw_event* ev, uint64_t n, const uint16_t*
                                  uint32_t* out, bool create, uint32_t* n_out, ScanCtx& sc, hipStream_t s);
 // out == nullptr: counts per item into cnt; else deliveries at off[k]
 void launch_fanout(const World& w, const uint32_t* items, uint32_t n, uint32_t* cnt, const uint64_t* off,
-                   uint32_t* keys, uint32_t* vals, hipStream_t s);
-void launch_fanout_final(const uint32_t* keys, const uint32_t* vals, const uint32_t* idx, const uint32_t* items,
-                         uint64_t n, gw_fanout_rec* out, hipStream_t s);
+                   uint64_t* pairs, hipStream_t s);
+void launch_fanout_final(const uint64_t* pairs, const uint32_t* idx, const uint32_t* items, uint64_t n,
+                         gw_fanout_rec* out, hipStream_t s);
 // keys[i] = gate[w[i]], vals[i] = i, hist[gate] += 1 (hist zeroed by the caller)
-void launch_gate_keys(const uint32_t* w, const uint16_t* gate, uint64_t n, uint32_t* keys, uint32_t* vals,
+void launch_gate_keys(const uint64_t* pairs, const uint16_t* gate, uint64_t n, uint32_t* keys, uint32_t* vals,
                       uint32_t* hist, hipStream_t s);
 void launch_msg_keys(const uint32_t* rec, int words, uint64_t n, const uint16_t* gate, uint32_t* keys, uint32_t* vals,
                      hipStream_t s);   // gate == nullptr: key = watcher

@@ -514,7 +514,7 @@ struct OsCfg {
 // digit totals of every pass (wave-private LDS copies: the top digit of a key
 // has few distinct values, so one shared copy would serialise its bins'
 // atomics; grid-stride), added into the zeroed totals[p][d]
-template <int DB>
+template <int DB, int KS = 1>   // KS: u32 words from one key to the next (2: packed pairs, key in the low word)
 __global__ void __launch_bounds__(NT) k_os_hist(const uint32_t* __restrict__ keys, const uint64_t* n_dev,
                                                 uint64_t n_max, int lo_bit, int passes, uint32_t* __restrict__ totals) {
     using C = OsCfg<DB>;
@@ -524,7 +524,7 @@ __global__ void __launch_bounds__(NT) k_os_hist(const uint32_t* __restrict__ key
     __syncthreads();
     const uint64_t n = load_n(n_max, n_dev);
     for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * NT) {
-        const uint32_t k = keys[i];
+        const uint32_t k = keys[i * KS];
         for (int p = 0; p < passes; ++p) atomicAdd(&h[w][p][(k >> (lo_bit + DB * p)) & (C::RD - 1)], 1u);
     }
     __syncthreads();
@@ -566,7 +566,9 @@ __device__ __forceinline__ void os_st(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int DB>
+// P64: the pairs are packed u64 (value << 32 | key) in kin / kout (vin / vout unused): one
+// 8-B load and one 8-B store per pair, a digit's run of a tile one contiguous segment
+template <int DB, bool P64 = false>
 __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                     gw_event* __restrict__ aos, uint32_t aos_mask,
@@ -599,8 +601,14 @@ __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__
 #pragma unroll
     for (int c = 0; c < RS2_CHUNKS; ++c) {                   // loads first: all in flight together
         const uint64_t i = wbase + (uint64_t)c * 64 + ln;
-        key[c] = i < n ? kin[i] : 0u;
-        val[c] = i < n ? vin[i] : 0u;
+        if (P64) {
+            const uint64_t x = i < n ? reinterpret_cast<const uint64_t*>(kin)[i] : 0ull;
+            key[c] = (uint32_t)x;
+            val[c] = (uint32_t)(x >> 32);
+        } else {
+            key[c] = i < n ? kin[i] : 0u;
+            val[c] = i < n ? vin[i] : 0u;
+        }
     }
     uint16_t* hw = whist[w];
 #pragma unroll
@@ -704,7 +712,9 @@ __global__ void __launch_bounds__(RS2_NT) k_os_pass(const uint32_t* __restrict__
         const uint32_t k = sk[i], v = sv[i];
         const uint32_t d = (k >> shift) & DM;
         const uint32_t dst = gofs[d] + (i - tstart[d]);
-        if (aos) {
+        if (P64) {
+            reinterpret_cast<uint64_t*>(kout)[dst] = ((uint64_t)v << 32) | k;
+        } else if (aos) {
             gw_event e;
             e.watcher = k & aos_mask;
             e.target = v;
@@ -723,7 +733,7 @@ inline uint64_t radix2_scratch_words(uint64_t n_max) {
     return 8 + 2ull * RS2_MAX_PASSES * RS2_MAX_RADIX + (uint64_t)RS2_STATUS_PER_TILE * radix2_tiles(n_max);
 }
 
-template <int DB>
+template <int DB, bool P64 = false>
 inline int radix_sort2_db(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max,
                           const uint64_t* n_dev, int lo_bit, int passes, uint32_t* scratch, hipStream_t st,
                           gw_event* aos, uint32_t aos_mask) {
@@ -736,14 +746,15 @@ inline int radix_sort2_db(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1
     // tickets, totals and the status words of the passes used start at zero
     (void)hipMemsetAsync(scratch, 0, 32 + (uint64_t)RS2_MAX_PASSES * RS2_MAX_RADIX * 4 +
                                          (uint64_t)passes * C::RD * nt * 4, st);
-    hipLaunchKernelGGL(k_os_hist<DB>, dim3(RS2_GBLOCKS), dim3(NT), 0, st, k0, n_dev, n_max, lo_bit, passes, totals);
+    hipLaunchKernelGGL((k_os_hist<DB, P64 ? 2 : 1>), dim3(RS2_GBLOCKS), dim3(NT), 0, st, k0, n_dev, n_max, lo_bit,
+                       passes, totals);
     hipLaunchKernelGGL(k_os_bases<DB>, dim3(passes), dim3(NT), 0, st, totals, gbase);
     int cur = 0;
     for (int p = 0; p < passes; ++p) {
         const bool last = p == passes - 1;
         uint32_t* ki = cur ? k1 : k0; uint32_t* ko = cur ? k0 : k1;
         uint32_t* vi = cur ? v1 : v0; uint32_t* vo = cur ? v0 : v1;
-        hipLaunchKernelGGL(k_os_pass<DB>, dim3((uint32_t)nt), dim3(RS2_NT), 0, st, ki, vi, ko, vo,
+        hipLaunchKernelGGL((k_os_pass<DB, P64>), dim3((uint32_t)nt), dim3(RS2_NT), 0, st, ki, vi, ko, vo,
                            last ? aos : nullptr, aos_mask, n_dev, n_max, lo_bit + DB * p,
                            gbase + p * RS2_MAX_RADIX, status + (uint64_t)p * C::RD * nt, tickets + p);
         cur ^= 1;
@@ -771,6 +782,24 @@ inline int radix_sort2(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, u
     if (bits > 20 && bits <= 22)
         return radix_sort2_db<11>(k0, v0, k1, v1, n_max, n_dev, lo_bit, 2, scratch, st, aos, aos_mask);
     return radix_sort2_db<8>(k0, v0, k1, v1, n_max, n_dev, lo_bit, (bits + 7) / 8, scratch, st, aos, aos_mask);
+}
+
+// The same for packed pairs (u64: value << 32 | key) in p0 with p1 as ping-pong.
+// Returns 0 if the result is in p0, 1 if in p1.
+inline int radix_sort2_p64(uint64_t* p0, uint64_t* p1, uint64_t n_max, const uint64_t* n_dev, int lo_bit, int hi_bit,
+                           uint32_t* scratch, hipStream_t st) {
+    const uint64_t nt = radix2_tiles(n_max);
+    if (nt == 0 || hi_bit <= lo_bit) return 0;
+    const int bits = hi_bit - lo_bit;
+    uint32_t* a = reinterpret_cast<uint32_t*>(p0);
+    uint32_t* b = reinterpret_cast<uint32_t*>(p1);
+    static const int db_max = getenv("GW_SORT_DB") ? atoi(getenv("GW_SORT_DB")) : 11;
+    if (db_max > 8 && bits > 16 && bits <= 20)
+        return radix_sort2_db<10, true>(a, nullptr, b, nullptr, n_max, n_dev, lo_bit, 2, scratch, st, nullptr, 0);
+    if (db_max > 8 && bits > 20 && bits <= 22)
+        return radix_sort2_db<11, true>(a, nullptr, b, nullptr, n_max, n_dev, lo_bit, 2, scratch, st, nullptr, 0);
+    return radix_sort2_db<8, true>(a, nullptr, b, nullptr, n_max, n_dev, lo_bit, (bits + 7) / 8, scratch, st,
+                                   nullptr, 0);
 }
 
 }  // namespace gw

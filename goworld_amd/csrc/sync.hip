@@ -280,8 +280,8 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
                                                    const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
                                                    uint32_t nf_max, const uint64_t* __restrict__ rec_off,
                                                    const uint32_t* __restrict__ cnt, gw_sync_record* rec,
-                                                   uint64_t rec_cap, DevStats* st, uint32_t* __restrict__ pk,
-                                                   uint32_t* __restrict__ pv, float4* __restrict__ pay) {
+                                                   uint64_t rec_cap, DevStats* st, uint64_t* __restrict__ pr,
+                                                   float4* __restrict__ pay) {
     __shared__ unsigned long long sbuf[NWAVE][3 * SW_BUF];
     unsigned long long* buf = sbuf[threadIdx.x >> 6];
     const uint64_t nf = load_n(nf_max, nf_dev);
@@ -324,8 +324,7 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
         if ((f & GW_SIF_OWN_CLIENT) && x.gt) {
             if (ln == 0) {
                 if (PAIRS) {
-                    pk[at] = e;
-                    pv[at] = (uint32_t)k;
+                    pr[at] = (k << 32) | e;
                 } else {
                     st_record_nt(rec + at, e, e, p);
                 }
@@ -337,11 +336,7 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
             wave_neighbors_of<U>(w, e, a, P, [&](bool rel, uint32_t ws, uint32_t g) {
                 const bool take = rel && g != 0;
                 const uint64_t bt = wave_ballot(take);
-                if (take) {
-                    const uint64_t j = at + (uint64_t)popc64(bt & lt);
-                    pk[j] = ws;
-                    pv[j] = (uint32_t)k;
-                }
+                if (take) pr[at + (uint64_t)popc64(bt & lt)] = (k << 32) | ws;
                 at += (uint64_t)popc64(bt);
             });
             return;
@@ -638,21 +633,21 @@ void launch_sync_write_small(const World& w, uint32_t n_spaces, const uint32_t* 
 
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
-                       uint64_t rec_cap, DevStats* st, hipStream_t s, uint32_t* pk, uint32_t* pv, float4* pay) {
+                       uint64_t rec_cap, DevStats* st, hipStream_t s, uint64_t* pr, float4* pay) {
     if (!nf_max) return;
     const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
-    if (pk)
+    if (pr)
         hipLaunchKernelGGL((k_sync_write<4, true>), g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt,
-                           rec, rec_cap, st, pk, pv, pay);
+                           rec, rec_cap, st, pr, pay);
     else if (w.nb_u >= 8)
         hipLaunchKernelGGL(k_sync_write<8>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st, pk, pv, pay);
+                           rec_cap, st, pr, pay);
     else if (w.nb_u <= 2)
         hipLaunchKernelGGL(k_sync_write<2>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st, pk, pv, pay);
+                           rec_cap, st, pr, pay);
     else
         hipLaunchKernelGGL(k_sync_write<4>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st, pk, pv, pay);
+                           rec_cap, st, pr, pay);
 }
 
 // 24-B records from sorted (watcher, entity) pairs (through idx, the gate
@@ -664,8 +659,7 @@ void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* 
 // watchers come from the sorted keys, not from a re-read of the records.
 // Tiles of SCAN_TILE pairs, striped: lane l's predecessor is lane l-1's
 // element, lane 0 loads its own.
-__global__ void __launch_bounds__(NT) k_records_seg(World w, const uint32_t* __restrict__ pk,
-                                                    const uint32_t* __restrict__ pv,
+__global__ void __launch_bounds__(NT) k_records_seg(World w, const uint64_t* __restrict__ pr,
                                                     const uint32_t* __restrict__ idx,
                                                     const uint32_t* __restrict__ flagged,
                                                     const float4* __restrict__ pay, uint64_t n,
@@ -693,9 +687,10 @@ __global__ void __launch_bounds__(NT) k_records_seg(World w, const uint32_t* __r
         for (int u = 0; u < G; ++u) {
             const uint64_t i = t0 + (uint64_t)(j0 + u) * NT + threadIdx.x;
             const uint32_t q = i < n ? (idx ? idx[i] : (uint32_t)i) : 0u;
-            wt[j0 + u] = i < n ? pk[q] : 0xffffffffu;
-            f[u] = i < n ? pv[q] : 0u;
-            pw[u] = (ln == 0 && i < n && i > 0) ? pk[idx ? idx[i - 1] : (uint32_t)(i - 1)] : 0xffffffffu;
+            const uint64_t x = i < n ? pr[q] : ~0ull;
+            wt[j0 + u] = (uint32_t)x;
+            f[u] = (uint32_t)(x >> 32);
+            pw[u] = (ln == 0 && i < n && i > 0) ? (uint32_t)pr[idx ? idx[i - 1] : (uint32_t)(i - 1)] : 0xffffffffu;
         }
 #pragma unroll
         for (int u = 0; u < G; ++u) {                    // the flagged entity's slot and payload
@@ -738,8 +733,7 @@ __global__ void __launch_bounds__(NT) k_records_seg(World w, const uint32_t* __r
         client_off[pre + tot] = n;                       // end of the last client
     }
 }
-void launch_records_seg(const World& w, const uint32_t* pk, const uint32_t* pv, const uint32_t* idx,
-                        const uint32_t* flagged, const float4* pay, uint64_t n, gw_sync_record* out,
+void launch_records_seg(const World& w, const uint64_t* pairs, const uint32_t* idx, const uint32_t* flagged, const float4* pay, uint64_t n, gw_sync_record* out,
                         uint32_t* client_slot, uint64_t* client_off, uint32_t* n_clients, ScanCtx& sc,
                         hipStream_t s) {
     if (!n) return;
@@ -749,7 +743,7 @@ void launch_records_seg(const World& w, const uint32_t* pk, const uint32_t* pv, 
         sc.tag = 0;
     }
     ++sc.tag;
-    hipLaunchKernelGGL(k_records_seg, dim3(nb), dim3(NT), 0, s, w, pk, pv, idx, flagged, pay, n, out, client_slot,
+    hipLaunchKernelGGL(k_records_seg, dim3(nb), dim3(NT), 0, s, w, pairs, idx, flagged, pay, n, out, client_slot,
                        client_off, n_clients, sc.status, sc.ticket, sc.tbase, sc.tag);
     sc.tbase += nb;
 }
@@ -1043,64 +1037,57 @@ __global__ void __launch_bounds__(NT) k_fanout_count(World w, const uint32_t* __
 }
 template <int U>
 __global__ void __launch_bounds__(NT) k_fanout_write(World w, const uint32_t* __restrict__ items, uint32_t n,
-                                                     const uint64_t* __restrict__ off, uint32_t* __restrict__ keys,
-                                                     uint32_t* __restrict__ vals) {
+                                                     const uint64_t* __restrict__ off, uint64_t* __restrict__ pr) {
     const uint64_t lt = lanemask_lt();
     const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
     for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < n; k += stride) {
         const uint32_t e = items[k];
         uint64_t at = off[k];
         if (w.gate[e]) {
-            if (lane_id() == 0) {
-                keys[at] = e;
-                vals[at] = (uint32_t)k;
-            }
+            if (lane_id() == 0) pr[at] = (k << 32) | e;
             ++at;
         }
         wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
             const bool take = rel && g != 0;
             const uint64_t bt = wave_ballot(take);
-            if (take) {
-                const uint64_t j = at + (uint64_t)popc64(bt & lt);
-                keys[j] = ws;
-                vals[j] = (uint32_t)k;
-            }
+            if (take) pr[at + (uint64_t)popc64(bt & lt)] = (k << 32) | ws;
             at += (uint64_t)popc64(bt);
         });
     }
 }
 void launch_fanout(const World& w, const uint32_t* items, uint32_t n, uint32_t* cnt, const uint64_t* off,
-                   uint32_t* keys, uint32_t* vals, hipStream_t s) {
+                   uint64_t* pairs, hipStream_t s) {
     if (!n) return;
     if (cnt)
         hipLaunchKernelGGL(k_fanout_count<4>, dim3(std::min(nblk(n, NT), SYNC_MAX_BLOCKS)), dim3(NT), 0, s, w, items,
                            n, cnt);
     else
         hipLaunchKernelGGL(k_fanout_write<4>, dim3(std::min(nblk(n, NWAVE), SYNC_MAX_BLOCKS)), dim3(NT), 0, s, w,
-                           items, n, off, keys, vals);
+                           items, n, off, pairs);
 }
 // the records from the sorted (watcher, item) pairs, through idx (the gate
 // grouping's permutation) when given; gate keys of the pairs for that grouping
-__global__ void __launch_bounds__(NT) k_fanout_final(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+__global__ void __launch_bounds__(NT) k_fanout_final(const uint64_t* __restrict__ pr,
                                                      const uint32_t* __restrict__ idx,
                                                      const uint32_t* __restrict__ items, uint64_t n,
                                                      gw_fanout_rec* __restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
     const uint32_t j = idx ? idx[i] : (uint32_t)i;
+    const uint64_t x = pr[j];
     gw_fanout_rec r;
-    r.watcher = keys[j];
-    r.item = vals[j];
+    r.watcher = (uint32_t)x;
+    r.item = (uint32_t)(x >> 32);
     r.entity = items[r.item];
     out[i] = r;
 }
-__global__ void __launch_bounds__(NT) k_gate_keys(const uint32_t* __restrict__ w, const uint16_t* __restrict__ gate,
+__global__ void __launch_bounds__(NT) k_gate_keys(const uint64_t* __restrict__ pr, const uint16_t* __restrict__ gate,
                                                   uint64_t n, uint32_t* keys, uint32_t* vals, uint32_t* hist) {
     __shared__ uint32_t h[NT];
     h[threadIdx.x] = 0;
     __syncthreads();
     for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * NT) {
-        const uint32_t g = gate[w[i]];
+        const uint32_t g = gate[(uint32_t)pr[i]];
         keys[i] = g;
         vals[i] = (uint32_t)i;
         if (g < NT) atomicAdd(&h[g], 1u); else atomicAdd(&hist[g], 1u);
@@ -1108,14 +1095,14 @@ __global__ void __launch_bounds__(NT) k_gate_keys(const uint32_t* __restrict__ w
     __syncthreads();
     if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
 }
-void launch_fanout_final(const uint32_t* keys, const uint32_t* vals, const uint32_t* idx, const uint32_t* items,
-                         uint64_t n, gw_fanout_rec* out, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(k_fanout_final, dim3(nblk(n, NT)), dim3(NT), 0, s, keys, vals, idx, items, n, out);
+void launch_fanout_final(const uint64_t* pairs, const uint32_t* idx, const uint32_t* items, uint64_t n,
+                         gw_fanout_rec* out, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_fanout_final, dim3(nblk(n, NT)), dim3(NT), 0, s, pairs, idx, items, n, out);
 }
-void launch_gate_keys(const uint32_t* w, const uint16_t* gate, uint64_t n, uint32_t* keys, uint32_t* vals,
+void launch_gate_keys(const uint64_t* pairs, const uint16_t* gate, uint64_t n, uint32_t* keys, uint32_t* vals,
                       uint32_t* hist, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(k_gate_keys, dim3(std::min<uint32_t>(nblk(n, NT), 2048)), dim3(NT), 0, s, w, gate, n,
-                              keys, vals, hist);
+    if (n) hipLaunchKernelGGL(k_gate_keys, dim3(std::min<uint32_t>(nblk(n, NT), 2048)), dim3(NT), 0, s, pairs, gate,
+                              n, keys, vals, hist);
 }
 
 // (c) stable grouping of a message stream: keys (watcher, or gate(watcher)),
@@ -1243,6 +1230,10 @@ void scan_u32_u64(const uint32_t* in, uint64_t* out, uint64_t n_max, const uint6
 void scan_u64_u64(const uint64_t* in, uint64_t* out, uint64_t n_max, const uint64_t* n_dev, ScanCtx& sc,
                   uint64_t* total, hipStream_t s) {
     scan_exclusive<uint64_t, uint64_t>(in, out, n_max, n_dev, sc, total, s);
+}
+int sort_pairs64(uint64_t* p0, uint64_t* p1, uint64_t n_max, const uint64_t* n_dev, int lo_bit, int hi_bit,
+                 RadixTmp& tmp, hipStream_t s) {
+    return radix_sort2_p64(p0, p1, n_max, n_dev, lo_bit, hi_bit, tmp.os, s);
 }
 int sort_u32_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
                  int lo_bit, int hi_bit, RadixTmp& tmp, hipStream_t s) {

@@ -764,8 +764,8 @@ inline int radix_sort2_db(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1
 
 // Sorts (k0,v0) by bits [lo_bit, hi_bit) (at most 32 bits) with (k1,v1) as
 // ping-pong; scratch holds radix2_scratch_words(n_max) u32 (no clearing
-// needed by the caller).  Digit width: 17-20 key bits in two 10-bit passes,
-// 21-22 in two 11-bit passes, else 8-bit passes.  With aos, the last pass
+// needed by the caller).  Digit width: 8 bits; with GW_SORT_DB >= 10, 17-20
+// key bits in two 10-bit passes, 21-22 in two 11-bit passes.  With aos, the last pass
 // writes gw_event {key & aos_mask, value} there (and the return value is
 // meaningless).  Returns 0 if the result is in (k0,v0), 1 if in (k1,v1).
 inline int radix_sort2(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
@@ -774,7 +774,10 @@ inline int radix_sort2(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, u
     const uint64_t nt = radix2_tiles(n_max);
     if (nt == 0 || hi_bit <= lo_bit) return 0;
     const int bits = hi_bit - lo_bit;
-    static const int db_max = getenv("GW_SORT_DB") ? atoi(getenv("GW_SORT_DB")) : 11;   // A/B of digit widths
+    // 8-bit digits unless GW_SORT_DB asks for wider ones: two 10-bit passes
+    // over config #3's 14.7M fan-out pairs took 214 us each, three 8-bit
+    // passes 103 us each (a wider digit's runs per tile are shorter segments)
+    static const int db_max = getenv("GW_SORT_DB") ? atoi(getenv("GW_SORT_DB")) : 8;
     if (db_max <= 8)
         return radix_sort2_db<8>(k0, v0, k1, v1, n_max, n_dev, lo_bit, (bits + 7) / 8, scratch, st, aos, aos_mask);
     if (bits > 16 && bits <= 20)
@@ -793,7 +796,7 @@ inline int radix_sort2_p64(uint64_t* p0, uint64_t* p1, uint64_t n_max, const uin
     const int bits = hi_bit - lo_bit;
     uint32_t* a = reinterpret_cast<uint32_t*>(p0);
     uint32_t* b = reinterpret_cast<uint32_t*>(p1);
-    static const int db_max = getenv("GW_SORT_DB") ? atoi(getenv("GW_SORT_DB")) : 11;
+    static const int db_max = getenv("GW_SORT_DB") ? atoi(getenv("GW_SORT_DB")) : 8;   // (as radix_sort2)
     if (db_max > 8 && bits > 16 && bits <= 20)
         return radix_sort2_db<10, true>(a, nullptr, b, nullptr, n_max, n_dev, lo_bit, 2, scratch, st, nullptr, 0);
     if (db_max > 8 && bits > 20 && bits <= 22)

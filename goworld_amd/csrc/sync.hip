@@ -673,11 +673,13 @@ __global__ void __launch_bounds__(NT) k_records_seg(World w, const uint64_t* __r
     constexpr int G = 4;                                 // rows whose gathers are in flight together
     __shared__ uint32_t lds[IPT * NWAVE];
     __shared__ uint32_t s_tile, s_prefix;
+    __shared__ unsigned long long stg[NWAVE][3 * 64];     // a wave's 64 records, written out coalesced
     if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tbase);
     __syncthreads();
     const uint32_t tile = s_tile;
     const uint64_t t0 = (uint64_t)tile * (IPT * NT);
     const int ln = lane_id();
+    unsigned long long* sb = stg[threadIdx.x >> 6];
     uint32_t wt[IPT], c[IPT];
 #pragma unroll
     for (int j0 = 0; j0 < IPT; j0 += G) {
@@ -706,7 +708,26 @@ __global__ void __launch_bounds__(NT) k_records_seg(World w, const uint64_t* __r
             uint32_t prev = (uint32_t)__shfl_up((int)wt[j0 + u], 1, 64);
             if (ln == 0) prev = pw[u];
             c[j0 + u] = (i < n && (i == 0 || prev != wt[j0 + u])) ? 1u : 0u;
-            if (i < n) st_record_nt(out + i, wt[j0 + u], e[u], p[u]);
+            // the row's 64 records (1536 B) staged, then 3 x 64 contiguous 8-B
+            // stores (one 24-B record per lane as three strided stores leaves
+            // partial lines behind each instruction)
+            if (i < n) {
+                sb[3 * ln] = ((unsigned long long)e[u] << 32) | wt[j0 + u];
+                sb[3 * ln + 1] = ((unsigned long long)__float_as_uint(p[u].y) << 32) | __float_as_uint(p[u].x);
+                sb[3 * ln + 2] = ((unsigned long long)__float_as_uint(p[u].w) << 32) | __float_as_uint(p[u].z);
+            }
+            wave_sync();
+            const uint64_t ib = i - (uint64_t)ln;                 // the wave's first record of the row
+            if (ib < n) {
+                const uint32_t words = 3u * (uint32_t)min<uint64_t>(64, n - ib);
+                unsigned long long* dst = reinterpret_cast<unsigned long long*>(out + ib);
+#pragma unroll
+                for (uint32_t q = 0; q < 3; ++q) {
+                    const uint32_t x = q * 64 + (uint32_t)ln;
+                    if (x < words) __builtin_nontemporal_store(sb[x], dst + x);
+                }
+            }
+            wave_sync();
         }
     }
     uint32_t head = 0;

@@ -1450,12 +1450,8 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     const bool pairs = by_client && !small;
     if (pairs && ((rc = ensure(c, c->gk0, c->rec_cap * 8)) || (rc = ensure(c, c->pay, (size_t)NFM * 16))))
         return rc;
-    // the pairs' sort scratch before the write pass, which counts its digits
-    RadixTmp prt{};
-    if (pairs && (rc = radix_tmp(c, c->rec_cap, prt))) return rc;
     prof_begin(c, "sync_write");
     auto write_pass = [&]() {
-        if (pairs) radix_zero_totals(prt, c->st);
         if (small)
             launch_sync_write_small(w, n_sp, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), P<uint64_t>(c->rec_off),
                                     P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st,
@@ -1463,8 +1459,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         else
             launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint64_t>(c->rec_off),
                               P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st,
-                              pairs ? P<uint64_t>(c->gk0) : nullptr, pairs ? P<float4>(c->pay) : nullptr,
-                              pairs ? radix_totals(prt) : nullptr, ceil_log2(C));
+                              pairs ? P<uint64_t>(c->gk0) : nullptr, pairs ? P<float4>(c->pay) : nullptr);
     };
     write_pass();
     size_t s_write = prof_end(c, 0);
@@ -1476,7 +1471,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     if (c->hcstats->overflow) {
         c->rec_cap = R + R / 4 + 1024;
         if ((rc = ensure(c, c->rec0, c->rec_cap * sizeof(gw_sync_record)))) return rc;
-        if (pairs && ((rc = ensure(c, c->gk0, c->rec_cap * 8)) || (rc = radix_tmp(c, c->rec_cap, prt)))) return rc;
+        if (pairs && (rc = ensure(c, c->gk0, c->rec_cap * 8))) return rc;
         c->hcstats->overflow = 0;
         HIPCHK(hipMemcpyAsync(c->cstats, c->hcstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
         write_pass();
@@ -1498,9 +1493,8 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         if (R) {
             if ((rc = ensure(c, c->gk1, R * 8))) return rc;
             RadixTmp rt;
-            if ((rc = radix_tmp(c, R, rt))) return rc;       // (no growth: the write pass's, R <= rec_cap)
-            if (R > 1 && sort_pairs64(P<uint64_t>(c->gk0), P<uint64_t>(c->gk1), R, nullptr, 0, ceil_log2(C), rt, c->st,
-                                      true))
+            if ((rc = radix_tmp(c, R, rt))) return rc;
+            if (R > 1 && sort_pairs64(P<uint64_t>(c->gk0), P<uint64_t>(c->gk1), R, nullptr, 0, ceil_log2(C), rt, c->st))
                 wp = P<uint64_t>(c->gk1);
             if (G > 2) {
                 if ((rc = ensure(c, c->gv0, R * 4)) || (rc = ensure(c, c->gv1, R * 4)) ||
@@ -1778,7 +1772,7 @@ int gw_fanout(gw_ctx* c, const uint32_t* slots, uint32_t n, uint32_t flags, gw_m
             return rc;
         HIPCHK(hipMemcpyAsync(c->m_items.p, hi, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
         const World w = world(c);
-        launch_fanout(w, P<uint32_t>(c->m_items), n, P<uint32_t>(c->m_cnt), nullptr, nullptr, nullptr, 0, c->st);
+        launch_fanout(w, P<uint32_t>(c->m_items), n, P<uint32_t>(c->m_cnt), nullptr, nullptr, c->st);
         uint64_t* tot = P<uint64_t>(c->m_off) + n;   // the total lands after the offsets
         scan_u32_u64(P<uint32_t>(c->m_cnt), P<uint64_t>(c->m_off), n, nullptr, c->sc, tot, c->st);
         HIPCHK(hipGetLastError());
@@ -1795,12 +1789,10 @@ int gw_fanout(gw_ctx* c, const uint32_t* slots, uint32_t n, uint32_t flags, gw_m
         RadixTmp rt;
         if ((rc = radix_tmp(c, R, rt))) return rc;
         const World w = world(c);
-        const int kb = ceil_log2(c->total_slots);
-        radix_zero_totals(rt, c->st);                // the write pass counts the sort's digits
-        launch_fanout(w, P<uint32_t>(c->m_items), n, nullptr, P<uint64_t>(c->m_off), P<uint64_t>(c->gk0),
-                      radix_totals(rt), kb, c->st);
+        launch_fanout(w, P<uint32_t>(c->m_items), n, nullptr, P<uint64_t>(c->m_off), P<uint64_t>(c->gk0), c->st);
         uint64_t* wp = P<uint64_t>(c->gk0);
-        if (sort_pairs64(P<uint64_t>(c->gk0), P<uint64_t>(c->gk1), R, nullptr, 0, kb, rt, c->st, true))
+        if (sort_pairs64(P<uint64_t>(c->gk0), P<uint64_t>(c->gk1), R, nullptr, 0, ceil_log2(c->total_slots), rt,
+                         c->st))
             wp = P<uint64_t>(c->gk1);
         const uint32_t* idx = nullptr;
         if (G > 2) {

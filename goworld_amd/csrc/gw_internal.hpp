@@ -166,10 +166,7 @@ void scan_u64_u64(const uint64_t* in, uint64_t* out, uint64_t n_max, const uint6
                   uint64_t* total, hipStream_t s);
 // stable sort of packed pairs (u64: value << 32 | key) by key bits [lo_bit, hi_bit); 1 = result in p1
 int sort_pairs64(uint64_t* p0, uint64_t* p1, uint64_t n_max, const uint64_t* n_dev, int lo_bit, int hi_bit,
-                 RadixTmp& tmp, hipStream_t s, bool pre_hist = false);
-// the digit totals a pairs producer counts into (zeroed first: radix_zero_totals)
-uint32_t* radix_totals(const RadixTmp& tmp);
-void radix_zero_totals(const RadixTmp& tmp, hipStream_t s);
+                 RadixTmp& tmp, hipStream_t s);
 int sort_u32_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
                  int lo_bit, int hi_bit, RadixTmp& tmp, hipStream_t s);
 
@@ -351,8 +348,7 @@ void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* 
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
                        uint64_t rec_cap, DevStats* st, hipStream_t s,
-                       uint64_t* pairs = nullptr, float4* pay = nullptr, uint32_t* totals = nullptr,
-                       int key_bits = 0);
+                       uint64_t* pairs = nullptr, float4* pay = nullptr);
 // the records and the client segment table in one pass (k_records_seg)
 void launch_records_seg(const World& w, const uint64_t* pairs, const uint32_t* idx, const uint32_t* flagged, const float4* pay, uint64_t n, gw_sync_record* out,
                         uint32_t* client_slot, uint64_t* client_off, uint32_t* n_clients, ScanCtx& sc,
@@ -445,9 +441,8 @@ void launch_restore(const World& w, const uint32_t* slots, const float4* xyzw, u
 void launch_event_client_compact(const gw_event* ev, uint64_t n, const uint16_t* gate, const SlotRec* rec,
                                  uint32_t* out, bool create, uint32_t* n_out, ScanCtx& sc, hipStream_t s);
 // out == nullptr: counts per item into cnt; else deliveries at off[k]
-// (pairs: their keys' 8-bit digits counted into the sort's totals, radix2_totals)
 void launch_fanout(const World& w, const uint32_t* items, uint32_t n, uint32_t* cnt, const uint64_t* off,
-                   uint64_t* pairs, uint32_t* totals, int key_bits, hipStream_t s);
+                   uint64_t* pairs, hipStream_t s);
 void launch_fanout_final(const uint64_t* pairs, const uint32_t* idx, const uint32_t* items, uint64_t n,
                          gw_fanout_rec* out, hipStream_t s);
 // keys[i] = gate[w[i]], vals[i] = i, hist[gate] += 1 (hist zeroed by the caller)

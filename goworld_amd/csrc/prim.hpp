@@ -559,19 +559,6 @@ __global__ void __launch_bounds__(NT) k_os_bases(const uint32_t* __restrict__ to
     }
 }
 
-// a producer's 8-bit digit counts of the keys it writes, per block in LDS
-// (h[MAX_PASSES][256], zeroed by the block), added to the sort's totals at the
-// block's end (radix2_totals; passes = ceil(key bits / 8))
-__device__ __forceinline__ void os_count_key(uint32_t (*h)[256], uint32_t key, int passes) {
-    for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(key >> (8 * p)) & 255u], 1u);
-}
-__device__ __forceinline__ void os_flush_counts(uint32_t (*h)[256], int passes, uint32_t* totals) {
-    __syncthreads();
-    for (int p = 0; p < passes; ++p)
-        for (int d = threadIdx.x; d < 256; d += blockDim.x)
-            if (h[p][d]) atomicAdd(&totals[p * RS2_MAX_RADIX + d], h[p][d]);
-}
-
 __device__ __forceinline__ uint32_t os_ld(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -746,35 +733,21 @@ inline uint64_t radix2_scratch_words(uint64_t n_max) {
     return 8 + 2ull * RS2_MAX_PASSES * RS2_MAX_RADIX + (uint64_t)RS2_STATUS_PER_TILE * radix2_tiles(n_max);
 }
 
-// the digit totals of a sort's scratch ([MAX_PASSES][MAX_RADIX] u32): a
-// producer that counts the 8-bit digits of the keys it writes (pre_hist) adds
-// them here after the caller zeroed them (radix2_zero_totals)
-inline uint32_t* radix2_totals(uint32_t* scratch) { return scratch + 8; }
-inline void radix2_zero_totals(uint32_t* scratch, hipStream_t st) {
-    (void)hipMemsetAsync(radix2_totals(scratch), 0, (size_t)RS2_MAX_PASSES * RS2_MAX_RADIX * 4, st);
-}
-
 template <int DB, bool P64 = false>
 inline int radix_sort2_db(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max,
                           const uint64_t* n_dev, int lo_bit, int passes, uint32_t* scratch, hipStream_t st,
-                          gw_event* aos, uint32_t aos_mask, bool pre_hist = false) {
+                          gw_event* aos, uint32_t aos_mask) {
     using C = OsCfg<DB>;
     const uint64_t nt = radix2_tiles(n_max);
     unsigned long long* tickets = (unsigned long long*)scratch;                 // [MAX_PASSES]
     uint32_t* totals = scratch + 8;                                             // [MAX_PASSES][MAX_RADIX]
     uint32_t* status = totals + RS2_MAX_PASSES * RS2_MAX_RADIX;                 // [passes][tiles][RD]
     uint32_t* gbase = status + (uint64_t)RS2_STATUS_PER_TILE * nt;              // [MAX_PASSES][MAX_RADIX]
-    // tickets, totals (unless the producer counted them) and the status words
-    // of the passes used start at zero
-    if (pre_hist) {
-        (void)hipMemsetAsync(scratch, 0, 32, st);
-        (void)hipMemsetAsync(status, 0, (uint64_t)passes * C::RD * nt * 4, st);
-    } else {
-        (void)hipMemsetAsync(scratch, 0, 32 + (uint64_t)RS2_MAX_PASSES * RS2_MAX_RADIX * 4 +
-                                             (uint64_t)passes * C::RD * nt * 4, st);
-        hipLaunchKernelGGL((k_os_hist<DB, P64 ? 2 : 1>), dim3(RS2_GBLOCKS), dim3(NT), 0, st, k0, n_dev, n_max,
-                           lo_bit, passes, totals);
-    }
+    // tickets, totals and the status words of the passes used start at zero
+    (void)hipMemsetAsync(scratch, 0, 32 + (uint64_t)RS2_MAX_PASSES * RS2_MAX_RADIX * 4 +
+                                         (uint64_t)passes * C::RD * nt * 4, st);
+    hipLaunchKernelGGL((k_os_hist<DB, P64 ? 2 : 1>), dim3(RS2_GBLOCKS), dim3(NT), 0, st, k0, n_dev, n_max, lo_bit,
+                       passes, totals);
     hipLaunchKernelGGL(k_os_bases<DB>, dim3(passes), dim3(NT), 0, st, totals, gbase);
     int cur = 0;
     for (int p = 0; p < passes; ++p) {
@@ -814,20 +787,16 @@ inline int radix_sort2(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, u
     return radix_sort2_db<8>(k0, v0, k1, v1, n_max, n_dev, lo_bit, (bits + 7) / 8, scratch, st, aos, aos_mask);
 }
 
-// The same for packed pairs (u64: value << 32 | key) in p0 with p1 as ping-pong
-// (pre_hist: the 8-bit digit totals of keys [0, hi_bit) were counted by the
-// producer, lo_bit 0).  Returns 0 if the result is in p0, 1 if in p1.
+// The same for packed pairs (u64: value << 32 | key) in p0 with p1 as ping-pong.
+// Returns 0 if the result is in p0, 1 if in p1.
 inline int radix_sort2_p64(uint64_t* p0, uint64_t* p1, uint64_t n_max, const uint64_t* n_dev, int lo_bit, int hi_bit,
-                           uint32_t* scratch, hipStream_t st, bool pre_hist = false) {
+                           uint32_t* scratch, hipStream_t st) {
     const uint64_t nt = radix2_tiles(n_max);
     if (nt == 0 || hi_bit <= lo_bit) return 0;
     const int bits = hi_bit - lo_bit;
     uint32_t* a = reinterpret_cast<uint32_t*>(p0);
     uint32_t* b = reinterpret_cast<uint32_t*>(p1);
     static const int db_max = getenv("GW_SORT_DB") ? atoi(getenv("GW_SORT_DB")) : 8;   // (as radix_sort2)
-    if (pre_hist)
-        return radix_sort2_db<8, true>(a, nullptr, b, nullptr, n_max, n_dev, 0, (bits + 7) / 8, scratch, st,
-                                       nullptr, 0, true);
     if (db_max > 8 && bits > 16 && bits <= 20)
         return radix_sort2_db<10, true>(a, nullptr, b, nullptr, n_max, n_dev, lo_bit, 2, scratch, st, nullptr, 0);
     if (db_max > 8 && bits > 20 && bits <= 22)

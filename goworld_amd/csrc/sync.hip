@@ -281,14 +281,8 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
                                                    uint32_t nf_max, const uint64_t* __restrict__ rec_off,
                                                    const uint32_t* __restrict__ cnt, gw_sync_record* rec,
                                                    uint64_t rec_cap, DevStats* st, uint64_t* __restrict__ pr,
-                                                   float4* __restrict__ pay, uint32_t* __restrict__ totals,
-                                                   int passes) {
+                                                   float4* __restrict__ pay) {
     __shared__ unsigned long long sbuf[NWAVE][3 * SW_BUF];
-    __shared__ uint32_t oh[PAIRS ? RS2_MAX_PASSES : 1][256];    // PAIRS: the sort's digit counts of the keys
-    if (PAIRS) {
-        for (int i = threadIdx.x; i < RS2_MAX_PASSES * 256; i += NT) (&oh[0][0])[i] = 0;
-        __syncthreads();
-    }
     unsigned long long* buf = sbuf[threadIdx.x >> 6];
     const uint64_t nf = load_n(nf_max, nf_dev);
     const int ln = lane_id();
@@ -331,7 +325,6 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
             if (ln == 0) {
                 if (PAIRS) {
                     pr[at] = (k << 32) | e;
-                    os_count_key(oh, e, passes);
                 } else {
                     st_record_nt(rec + at, e, e, p);
                 }
@@ -343,10 +336,7 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
             wave_neighbors_of<U>(w, e, a, P, [&](bool rel, uint32_t ws, uint32_t g) {
                 const bool take = rel && g != 0;
                 const uint64_t bt = wave_ballot(take);
-                if (take) {
-                    pr[at + (uint64_t)popc64(bt & lt)] = (k << 32) | ws;
-                    os_count_key(oh, ws, passes);
-                }
+                if (take) pr[at + (uint64_t)popc64(bt & lt)] = (k << 32) | ws;
                 at += (uint64_t)popc64(bt);
             });
             return;
@@ -394,7 +384,6 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
         x0 = x1;
         h1 = h2;
     }
-    if (PAIRS) os_flush_counts(oh, passes, totals);
 }
 // ---------------------------------------------------------------------------
 // Small-space mode (every space's grid fits in LDS, e.g. config #4's 10k
@@ -644,22 +633,21 @@ void launch_sync_write_small(const World& w, uint32_t n_spaces, const uint32_t* 
 
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
-                       uint64_t rec_cap, DevStats* st, hipStream_t s, uint64_t* pr, float4* pay, uint32_t* totals,
-                       int key_bits) {
+                       uint64_t rec_cap, DevStats* st, hipStream_t s, uint64_t* pr, float4* pay) {
     if (!nf_max) return;
     const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
     if (pr)
         hipLaunchKernelGGL((k_sync_write<4, true>), g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt,
-                           rec, rec_cap, st, pr, pay, totals, (key_bits + 7) / 8);
+                           rec, rec_cap, st, pr, pay);
     else if (w.nb_u >= 8)
         hipLaunchKernelGGL(k_sync_write<8>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st, pr, pay, totals, (key_bits + 7) / 8);
+                           rec_cap, st, pr, pay);
     else if (w.nb_u <= 2)
         hipLaunchKernelGGL(k_sync_write<2>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st, pr, pay, totals, (key_bits + 7) / 8);
+                           rec_cap, st, pr, pay);
     else
         hipLaunchKernelGGL(k_sync_write<4>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec,
-                           rec_cap, st, pr, pay, totals, (key_bits + 7) / 8);
+                           rec_cap, st, pr, pay);
 }
 
 // 24-B records from sorted (watcher, entity) pairs (through idx, the gate
@@ -1070,44 +1058,33 @@ __global__ void __launch_bounds__(NT) k_fanout_count(World w, const uint32_t* __
 }
 template <int U>
 __global__ void __launch_bounds__(NT) k_fanout_write(World w, const uint32_t* __restrict__ items, uint32_t n,
-                                                     const uint64_t* __restrict__ off, uint64_t* __restrict__ pr,
-                                                     uint32_t* __restrict__ totals, int passes) {
-    __shared__ uint32_t oh[RS2_MAX_PASSES][256];             // the sort's digit counts of the keys written
-    for (int i = threadIdx.x; i < RS2_MAX_PASSES * 256; i += NT) (&oh[0][0])[i] = 0;
-    __syncthreads();
+                                                     const uint64_t* __restrict__ off, uint64_t* __restrict__ pr) {
     const uint64_t lt = lanemask_lt();
     const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
     for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6); k < n; k += stride) {
         const uint32_t e = items[k];
         uint64_t at = off[k];
         if (w.gate[e]) {
-            if (lane_id() == 0) {
-                pr[at] = (k << 32) | e;
-                os_count_key(oh, e, passes);
-            }
+            if (lane_id() == 0) pr[at] = (k << 32) | e;
             ++at;
         }
         wave_neighbors<U>(w, e, [&](bool rel, uint32_t ws, uint32_t g) {
             const bool take = rel && g != 0;
             const uint64_t bt = wave_ballot(take);
-            if (take) {
-                pr[at + (uint64_t)popc64(bt & lt)] = (k << 32) | ws;
-                os_count_key(oh, ws, passes);
-            }
+            if (take) pr[at + (uint64_t)popc64(bt & lt)] = (k << 32) | ws;
             at += (uint64_t)popc64(bt);
         });
     }
-    os_flush_counts(oh, passes, totals);
 }
 void launch_fanout(const World& w, const uint32_t* items, uint32_t n, uint32_t* cnt, const uint64_t* off,
-                   uint64_t* pairs, uint32_t* totals, int key_bits, hipStream_t s) {
+                   uint64_t* pairs, hipStream_t s) {
     if (!n) return;
     if (cnt)
         hipLaunchKernelGGL(k_fanout_count<4>, dim3(std::min(nblk(n, NT), SYNC_MAX_BLOCKS)), dim3(NT), 0, s, w, items,
                            n, cnt);
     else
         hipLaunchKernelGGL(k_fanout_write<4>, dim3(std::min(nblk(n, NWAVE), SYNC_MAX_BLOCKS)), dim3(NT), 0, s, w,
-                           items, n, off, pairs, totals, (key_bits + 7) / 8);
+                           items, n, off, pairs);
 }
 // the records from the sorted (watcher, item) pairs, through idx (the gate
 // grouping's permutation) when given; gate keys of the pairs for that grouping
@@ -1276,11 +1253,9 @@ void scan_u64_u64(const uint64_t* in, uint64_t* out, uint64_t n_max, const uint6
     scan_exclusive<uint64_t, uint64_t>(in, out, n_max, n_dev, sc, total, s);
 }
 int sort_pairs64(uint64_t* p0, uint64_t* p1, uint64_t n_max, const uint64_t* n_dev, int lo_bit, int hi_bit,
-                 RadixTmp& tmp, hipStream_t s, bool pre_hist) {
-    return radix_sort2_p64(p0, p1, n_max, n_dev, lo_bit, hi_bit, tmp.os, s, pre_hist);
+                 RadixTmp& tmp, hipStream_t s) {
+    return radix_sort2_p64(p0, p1, n_max, n_dev, lo_bit, hi_bit, tmp.os, s);
 }
-uint32_t* radix_totals(const RadixTmp& tmp) { return radix2_totals(tmp.os); }
-void radix_zero_totals(const RadixTmp& tmp, hipStream_t s) { radix2_zero_totals(tmp.os, s); }
 int sort_u32_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
                  int lo_bit, int hi_bit, RadixTmp& tmp, hipStream_t s) {
     // the pairs of the client paths (fanout, per-client grouping, gate groups):

@@ -18,5 +18,5 @@ rows=list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r:-float(r['TotalDurationNs']))
 for r in rows[:22]: print(f\"{r['Name'][:60]:60s} calls {int(r['Calls']):5d} total_us {float(r['TotalDurationNs'])/1e3:10.1f} avg_us {float(r['AverageNs'])/1e3:8.1f}\")
 " gpurun_out/fprof_${tag}_${w}_kernel_stats.csv
-  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(json.dumps(d.get('client_msgs'))[:600]); print('ms', d['ms_per_step'])" gpurun_out/fprof_${tag}_$w.log
+  python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(json.dumps(d.get('client_msgs'))[:600]); print('ms', d['ms_per_step'])" gpurun_out/fprof_${tag}_$w.log
 done

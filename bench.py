@@ -768,7 +768,7 @@ def roofline_fields(res, K, config, ws):
             return (kern or {}).get(k, {}).get("hbm_bytes") if kern else None
         names = STAGE_KERNEL_C4 if config == 4 else STAGE_KERNEL
         mv = names["diff"]
-        sw = names.get("sync_write", "k_sync_write<4>")
+        sw = names.get("sync_write", "k_sync_write<4, false>")
         out["roofline"] = {"bound": "hbm", "kernel": mv, "achieved": ach, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic(mv),
                            "traffic_unit": "bytes/launch", "traffic_source": psrc, "traffic_src_hash": pstamp,

@@ -2037,7 +2037,15 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
 // flag are read from the device statistics before the block zeroes them, so
 // the pass needs nothing from the host and a collect queues it behind its
 // statistics copy, before its host sync (off the path between the collect and
-// the next tick)
+// the next tick).  The host reads the published words only after a stream
+// sync, which makes a kernel's writes to pinned host memory visible: no
+// system-scope fence (an L2 write-back of the tick's dirty lines) here
+// (GW_PUB_FENCE=1 puts it back, for comparison).
+#if defined(GW_PUB_FENCE) && GW_PUB_FENCE
+#define PUB_FENCE() __threadfence_system()
+#else
+#define PUB_FENCE() ((void)0)
+#endif
 __global__ void __launch_bounds__(RESET_NT) k_tick_reset(TickBufs b, const unsigned long long* __restrict__ pub_src,
                                                         unsigned long long* pub_dst, uint32_t pub_words) {
     // the next tick's bucket bounds: their event loads go out first, the
@@ -2066,14 +2074,14 @@ __global__ void __launch_bounds__(RESET_NT) k_tick_reset(TickBufs b, const unsig
         __syncthreads();
     }
     if (!b.st) {
-        __threadfence_system();
+        PUB_FENCE();
         return;
     }
     if (split) bk_split_store(b, v);
     __syncthreads();                                        // every read of the statistics done
     unsigned long long* z = (unsigned long long*)b.st;
     for (uint32_t k = threadIdx.x; k < sizeof(DevStats) / 8; k += RESET_NT) z[k] = 0;
-    __threadfence_system();
+    PUB_FENCE();
 }
 
 void tick_reset(const TickBufs& b, hipStream_t s) {
@@ -2086,7 +2094,7 @@ struct PubTab {
 __global__ void __launch_bounds__(RESET_NT) k_publish_words(PubTab t) {
     for (int q = 0; q < t.n; ++q)
         for (uint32_t k = threadIdx.x; k < t.s[q].words; k += RESET_NT) t.s[q].dst[k] = t.s[q].src[k];
-    __threadfence_system();
+    PUB_FENCE();
 }
 void publish_words(const PubSeg* segs, int n, hipStream_t s) {
     PubTab t{};

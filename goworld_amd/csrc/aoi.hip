@@ -516,8 +516,7 @@ __device__ __forceinline__ Rects mover_rects(const SpaceP& P, bool po, float ox,
 __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
     const uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x;
     const uint64_t ngm = b.st->n_gm;
-    const bool listing = b.heavy_min || b.light_max;           // heavy[] is built: whole waves reach the ballot
-    if (m >= ngm && !(listing && m - lane_id() < ngm)) return;
+    if (m >= ngm && !(b.heavy_min && m - lane_id() < ngm)) return;   // heavy mode: whole waves reach the ballot
     MEnt e;
     e.tags = 0;
     if (m < ngm) e = b.gm[m];
@@ -549,10 +548,8 @@ __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
         b.ownc[m] = 0;
         b.mirc[m] = 0;
     }
-    // heavy-first mode: the longest walks are listed apart and dispatched first;
-    // light pairs: everything but the short lists (and long movers) is listed
-    const bool hv = (e.tags & TAG_PRIMARY) &&
-                    ((b.heavy_min && c >= b.heavy_min) || (b.light_max && (c > b.light_max || (e.tags & TAG_LONG))));
+    // heavy-first mode: the longest walks are listed apart and dispatched first
+    const bool hv = (e.tags & TAG_PRIMARY) && b.heavy_min && c >= b.heavy_min;
     const uint64_t hm = wave_ballot(hv);
     if (hm) {
         const int leader = __builtin_ctzll(hm);
@@ -871,11 +868,6 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
 #else
 #define KMOVER_SGPR
 #endif
-template <int HU>
-__device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t mA, uint64_t mB, bool validB, const SpaceP& P,
-                                           const GEnt* GN, const uint32_t* GS, const uint32_t* MS,
-                                           const MEnt* GM, uint32_t* L);
-
 // one wave per primary entry (pidx, cell order): no wave is dispatched for
 // the secondary entries (half the mover grid), whose zeros k_bounds wrote
 template <int DIFF_U>
@@ -893,40 +885,6 @@ __global__ void __launch_bounds__(64) KMOVER_SGPR k_mover_c(TickBufs b) {
         if (k >= np) return;
     }
     mover_one<DIFF_U, SORT_LDS, GlobalSrc, true>(b, m, lds, GlobalSrc{b.w.gn, b.w.gn_start, b.gm_start, b.gm});
-}
-
-// Light pairs (light_max): the listed entries (heavy[]) one per wave first,
-// then the short lists (pidx, cell order) two per wave, a half-wave each
-// (mover_half: the per-mover setup of a ~60-candidate list is most of its
-// wave's work); a pair in two spaces or with more rows than a half holds
-// runs both through mover_one.  A kernel of its own: the half-wave path's
-// registers would cost k_mover_c its residency.
-#ifndef GW_LP_MINW
-#define GW_LP_MINW 1
-#endif
-template <int DIFF_U>
-__global__ void __launch_bounds__(64, GW_LP_MINW) KMOVER_SGPR k_mover_lp(TickBufs b) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[SORT_LDS];
-    const uint64_t k = blockIdx.x;
-    const uint64_t np = b.st->cand_total >> PRIM_SHIFT;
-    const GlobalSrc src{b.w.gn, b.w.gn_start, b.gm_start, b.gm};
-    const uint64_t nh = b.st->n_heavy;
-    if (k < nh) {
-        mover_one<DIFF_U, SORT_LDS, GlobalSrc, true>(b, b.heavy[k], lds, src);
-        return;
-    }
-    const uint64_t j = 2 * (k - nh);
-    if (j >= np) return;
-    const uint32_t mA = b.pidx[j];
-    const bool hasB = j + 1 < np;
-    const uint32_t mB = hasB ? b.pidx[j + 1] : mA;
-    const uint32_t sA = b.gm[mA].space;
-    if ((!hasB || b.gm[mB].space == sA) &&
-        mover_half<2>(b, mA, mB, hasB, b.w.sp[sA], src.GN, src.GS, src.MS, src.GM, lds))
-        return;
-    mover_one<DIFF_U, SORT_LDS, GlobalSrc, true>(b, mA, lds, src);
-    wave_sync();
-    if (hasB) mover_one<DIFF_U, SORT_LDS, GlobalSrc, true>(b, mB, lds, src);
 }
 
 template <int DIFF_U, int WPB>
@@ -948,15 +906,15 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
 // read-back of HBM).  Returns false (nothing done) when either entry needs
 // more rows: the caller then runs both through mover_one.
 template <int HU>
-__device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t mA, uint64_t mB, bool validB, const SpaceP& P,
+__device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint64_t m_end, const SpaceP& P,
                                            const GEnt* GN, const uint32_t* GS, const uint32_t* MS,
                                            const MEnt* GM, uint32_t* L) {
     const int ln = lane_id();
     const uint32_t half = (uint32_t)ln >> 5, hl = (uint32_t)ln & 31u, hb = half << 5;
     const uint64_t hmask = half ? 0xffffffff00000000ull : 0x00000000ffffffffull;
     const uint64_t lt = lanemask_lt();
-    const uint64_t m = half ? mB : mA;                     // entry A in lanes 0-31, B in 32-63
-    const bool valid = half ? validB : true;
+    const uint64_t m = m0 + half;
+    const bool valid = m < m_end;
     MEnt me;
     me.tags = 0;
     me.x = me.z = me.ox = me.oz = qnan();
@@ -1181,7 +1139,7 @@ __global__ void __launch_bounds__(64) k_mover_pair(TickBufs b) {
     const uint32_t s0 = b.gm[m0].space, s1 = m0 + 1 < m1 ? b.gm[m0 + 1].space : s0;
     const uint32_t tg = b.gm[m0].tags | (m0 + 1 < m1 ? b.gm[m0 + 1].tags : 0u);
     if (max(c0, c1) <= b.pair_max && s0 == s1 && !(tg & TAG_LONG)) {   // wave-uniform; long movers: mover_one
-        if (mover_half<2>(b, m0, m0 + 1, m0 + 1 < m1, b.w.sp[s0], src.GN, src.GS, src.MS, src.GM, lds)) return;
+        if (mover_half<2>(b, m0, m1, b.w.sp[s0], src.GN, src.GS, src.MS, src.GM, lds)) return;
     }
     mover_one<DIFF_U, SORT_LDS>(b, m0, lds, src);
     wave_sync();
@@ -1202,7 +1160,7 @@ __device__ __forceinline__ void small_walk(const TickBufs& b, uint32_t m0, uint3
     if (b.small_halves) {
         uint32_t* L = lds + (threadIdx.x >> 6) * SMALL_SORT;
         for (uint32_t m = m0 + (threadIdx.x >> 6) * 2; m < m1; m += NWAVE * 2) {
-            if (!mover_half<3>(b, m, m + 1, m + 1 < m1, P, src.GN, src.GS, src.MS, src.GM, L)) {
+            if (!mover_half<3>(b, m, m1, P, src.GN, src.GS, src.MS, src.GM, L)) {
                 mover_one<DIFF_U, SMALL_SORT>(b, m, lds, src);
                 wave_sync();
                 if (m + 1 < m1) mover_one<DIFF_U, SMALL_SORT>(b, m + 1, lds, src);
@@ -2014,10 +1972,7 @@ void tick_diff(const TickBufs& b, hipStream_t s) {
         return;
     }
     if (b.compact) {                       // one wave per primary entry (<= one per op)
-        if (b.light_max)
-            hipLaunchKernelGGL((k_mover_lp<2>), dim3(nblk1(b.m, 1)), dim3(64), 0, s, b);
-        else
-            hipLaunchKernelGGL((k_mover_c<2>), dim3(nblk1(b.m, 1)), dim3(64), 0, s, b);
+        hipLaunchKernelGGL((k_mover_c<2>), dim3(nblk1(b.m, 1)), dim3(64), 0, s, b);
         return;
     }
     switch (b.diff_u) {                    // GW_MOVER_WPB: waves per k_mover block

@@ -538,7 +538,6 @@ int gw_init(int device_id, gw_ctx** out) {
         if (const char* e = getenv("GW_MOVER_COMPACT")) c->mover_compact = atoi(e) != 0;
         if (const char* e = getenv("GW_HEAVY_MIN")) c->heavy_min = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_HEAVY_MAXM")) c->heavy_maxm = (uint32_t)std::max(0, atoi(e));
-        if (const char* e = getenv("GW_LIGHT_PAIRS")) c->light_max = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_DIRTY_SPAN")) c->dirty_span = (uint32_t)std::min(64, std::max(1, atoi(e)));
     } while (0);
     if (rc) {
@@ -1334,8 +1333,6 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.icnt = P<uint32_t>(c->icnt); b.ioff = P<uint32_t>(c->ioff);
     b.wbits = ceil_log2(C);
     small_mode(c, b);
-    // light pairs only on k_mover_c's path (compact, not small-space, not all-pairs)
-    b.light_max = (b.compact && !b.small_ents && !b.pair_max) ? c->light_max : 0u;
     if (b.small_ents || b.pair_max || !ev_on) {
         b.rowrec = nullptr;                          // only k_mover reads the row ranges
     } else {

@@ -204,7 +204,6 @@ struct gw_ctx {
     uint32_t heavy_min = 512;            // GW_HEAVY_MIN: TickBufs.heavy_min (0: off; 1M world at 8 strips:
                                          // diff 58 -> 47 us; at 100k movers one wave per mover in cell order
                                          // balances better) ...
-    uint32_t light_max = 0;              // GW_LIGHT_PAIRS: TickBufs.light_max (candidates; 0: off)
     uint32_t heavy_maxm = 65536;         // ... for ticks of at most GW_HEAVY_MAXM ops
     uint32_t rank_sort = 12;             // GW_RANK_SORT: TickBufs.rank_sort
     // GW_DIRTY_SPAN: TickBufs.dirty_span; 0 = by the cell count: 2 up to 128k cells, 8 up to 1M cells (a hotspot wave

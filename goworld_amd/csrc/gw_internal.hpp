@@ -228,8 +228,6 @@ struct TickBufs {
     uint32_t* pidx;           // [m] k-th primary entry (written by the scan of cand; k_mover's waves)
     uint32_t* heavy;          // [m] heavy-first mode: primaries with >= heavy_min candidates, walked first
     uint32_t heavy_min;       // GW_HEAVY_MIN (0: off): longest walks first when few movers (shorter tail)
-    uint32_t light_max;       // GW_LIGHT_PAIRS (0: off): primaries with <= light_max candidates walked two
-                              // per wave (a half each), the rest listed in heavy[] and walked one per wave
     uint4* rowrec;            // [2m * RR_ROWS] per primary entry: its rows' grid / mover-grid index ranges
                               // (start, end, start, end) from k_bounds; row 0 = (1, 0, ..) when > RR_ROWS rows
     uint64_t own_cap;         // capacity of own / mir

@@ -194,6 +194,21 @@ int ensure_scan(gw_ctx* c, uint64_t n) {
     return 0;
 }
 
+// the collect stream's scan status (sc2), as ensure_scan (cleared on growth on
+// that stream, which runs every use of it)
+int ensure_scan2(gw_ctx* c, uint64_t n, hipStream_t s) {
+    const uint64_t tiles = (n + scan_tile() - 1) / scan_tile() + 2;
+    const uint64_t bytes = tiles * scan_words() * 8;
+    if (c->scan_status2.cap >= bytes) return 0;
+    int rc;
+    if ((rc = ensure(c, c->scan_status2, bytes))) return rc;
+    HIPCHK(hipMemsetAsync(c->scan_status2.p, 0, c->scan_status2.cap, s));
+    c->sc2.status = P<unsigned long long>(c->scan_status2);
+    c->sc2.max_tiles = c->scan_status2.cap / (scan_words() * 8);
+    c->sc2.tag = 0;
+    return 0;
+}
+
 int radix_tmp(gw_ctx* c, uint64_t n_max, RadixTmp& rt) {
     uint64_t nb = (n_max + radix_tile() - 1) / radix_tile();
     if (!nb) nb = 1;
@@ -521,10 +536,16 @@ int gw_init(int device_id, gw_ctx** out) {
         (void)hipMemset(c->halo, 0, sizeof(HaloStats));
         if (hipMalloc(&c->sc.ticket, 8) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "ticket"); break; }
         (void)hipMemset(c->sc.ticket, 0, 8);
+        if (hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess) { rc = set_err(c, GW_EDEVICE, "stream"); break; }
+        if (hipEventCreateWithFlags(&c->ev_diff, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_col, hipEventDisableTiming) != hipSuccess) { rc = set_err(c, GW_EDEVICE, "event"); break; }
+        if (hipMalloc(&c->sc2.ticket, 8) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "ticket"); break; }
+        (void)hipMemset(c->sc2.ticket, 0, 8);
         memset(c->hstats, 0, 2 * sizeof(DevStats));
         (void)hipMemset(c->stats, 0, 2 * sizeof(DevStats));
         (void)hipEventCreate(&c->ev_t0);
         (void)hipEventCreate(&c->ev_t1);
+        if (const char* e = getenv("GW_OVERLAP_COLLECT")) c->overlap = atoi(e) != 0;
         if (const char* e = getenv("GW_CELLS_PER_D")) c->cells_per_d = std::min(4, std::max(1, atoi(e)));
         if (const char* e = getenv("GW_MOVER_WPB")) c->diff_u = atoi(e);
         if (const char* e = getenv("GW_NB_U")) c->nb_u = atoi(e);
@@ -557,7 +578,7 @@ void gw_shutdown(gw_ctx* c) {
     DevBuf* bufs[] = {&c->ops_buf, &c->stamp_buf, &c->pay, &c->mstat, &c->k0, &c->v0, &c->k1, &c->v1,
                       &c->gm, &c->cand, &c->reg, &c->pidx, &c->heavy, &c->rowrec, &c->own, &c->big, &c->mir, &c->ownc, &c->mirc, &c->mlist,
                       &c->mcnt, &c->moff, &c->minfo, &c->icnt, &c->ioff, &c->mreg, &c->chunk_first, &c->srange, &c->bk_a, &c->bk_b, &c->bk_id, &c->bk_cnt, &c->bk_split, &c->ev_d, &c->rtable,
-                      &c->scan_status, &c->rs_hist, &c->rs_os,
+                      &c->scan_status, &c->scan_status2, &c->rs_hist, &c->rs_os,
                       &c->fbits, &c->flagged, &c->rec_cnt, &c->rec_off, &c->rec0, &c->rec1,
                       &c->gate_hist, &c->gk0, &c->gv0, &c->gk1, &c->gv1, &c->qbuf, &c->cl_slot, &c->cl_off,
                       &c->m_create.a, &c->m_create.b, &c->m_destroy.a, &c->m_destroy.b, &c->m_fanout.a,
@@ -578,7 +599,7 @@ void gw_shutdown(gw_ctx* c) {
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off, &c->h_items, &c->m_create.h,
                     &c->m_destroy.h, &c->m_fanout.h};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
-    void* ps[] = {c->halo, c->sc.ticket, c->movbit, c->gmi, c->rec, c->flags, c->gate, c->nbc, c->ol,
+    void* ps[] = {c->halo, c->sc.ticket, c->sc2.ticket, c->movbit, c->gmi, c->rec, c->flags, c->gate, c->nbc, c->ol,
                   c->gnb[0], c->gnb[1], c->sp_dev, c->stats, c->scal32, c->gsb[0],
                   c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->gm_start};
     for (void* p : ps) if (p) (void)hipFree(p);
@@ -586,6 +607,12 @@ void gw_shutdown(gw_ctx* c) {
     for (auto& s : c->stages) { (void)hipEventDestroy(s.a); (void)hipEventDestroy(s.b); }
     if (c->ev_t0) (void)hipEventDestroy(c->ev_t0);
     if (c->ev_t1) (void)hipEventDestroy(c->ev_t1);
+    if (c->ev_diff) (void)hipEventDestroy(c->ev_diff);
+    if (c->ev_col) (void)hipEventDestroy(c->ev_col);
+    if (c->st2) {
+        (void)hipStreamSynchronize(c->st2);
+        (void)hipStreamDestroy(c->st2);
+    }
     if (c->own_st) (void)hipStreamDestroy(c->own_st);
     delete c;
 }
@@ -1364,6 +1391,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     prof_begin(c, "diff");
     if (ev_on) tick_diff(b, c->st);
     size_t s_diff = prof_end(c, 0);
+    HIPCHK(hipEventRecord(c->ev_diff, c->st));        // a following collect may start here (st2)
     prof_begin(c, "events");
     if (ev_on) tick_events(b, c->sc, c->st);
     size_t s_events = prof_end(c, 0);
@@ -1432,16 +1460,29 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     if (small && (rc = ensure(c, c->srange, (size_t)n_sp * 8))) return rc;
     uint32_t* sfirst = small ? P<uint32_t>(c->srange) : nullptr;
     uint32_t* slast = small ? sfirst + n_sp : nullptr;
+    // after a deferred tick the flag, count and write passes need only its
+    // diff (the new grid, states and cached neighbour counts), not its events
+    // stage: they run on st2 beside it, and st waits for them before the
+    // statistics publish (per-stage profiling keeps one stream)
+    const bool ovl = c->overlap && c->pt.on && !c->pt.copied && c->prof != 1;
+    hipStream_t cs = c->st;
+    ScanCtx* csc = &c->sc;
+    if (ovl) {
+        if ((rc = ensure_scan2(c, C, c->st2))) return rc;
+        HIPCHK(hipStreamWaitEvent(c->st2, c->ev_diff, 0));
+        cs = c->st2;
+        csc = &c->sc2;
+    }
     prof_begin(c, "sync_flagged");
-    launch_flag_compact(c->flags, C, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), c->sc, &st->flagged,
-                        &st->overflow, sfirst, small ? 2 * n_sp : 0u, c->st);
+    launch_flag_compact(c->flags, C, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), *csc, &st->flagged,
+                        &st->overflow, sfirst, small ? 2 * n_sp : 0u, cs);
     prof_end(c, (uint64_t)C * 4 * 2);
     const uint64_t* nf = (const uint64_t*)&st->flagged;
     prof_begin(c, "sync_count");
     launch_sync_count(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint32_t>(c->rec_cnt), sfirst,
-                      slast, c->st);
-    scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), NFM, nf, c->sc,
-                 (uint64_t*)&st->rec_total, c->st);
+                      slast, cs);
+    scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), NFM, nf, *csc,
+                 (uint64_t*)&st->rec_total, cs);
     size_t s_count = prof_end(c, 0);
     // per-client grouping (GW_SYNC_BY_CLIENT): the write pass leaves (watcher,
     // entity) pairs, the sort's keys and values; the records are built once
@@ -1451,19 +1492,23 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     if (pairs && ((rc = ensure(c, c->gk0, c->rec_cap * 8)) || (rc = ensure(c, c->pay, (size_t)NFM * 16))))
         return rc;
     prof_begin(c, "sync_write");
-    auto write_pass = [&]() {
+    auto write_pass = [&](hipStream_t ws) {
         if (small)
             launch_sync_write_small(w, n_sp, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), P<uint64_t>(c->rec_off),
                                     P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st,
-                                    sfirst, slast, max_ents, max_cells, c->st);
+                                    sfirst, slast, max_ents, max_cells, ws);
         else
             launch_sync_write(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint64_t>(c->rec_off),
-                              P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, c->st,
+                              P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st, ws,
                               pairs ? P<uint64_t>(c->gk0) : nullptr, pairs ? P<float4>(c->pay) : nullptr);
     };
-    write_pass();
+    write_pass(cs);
     size_t s_write = prof_end(c, 0);
     HIPCHK(hipGetLastError());
+    if (ovl) {                                           // the publish waits for the collect's passes
+        HIPCHK(hipEventRecord(c->ev_col, c->st2));
+        HIPCHK(hipStreamWaitEvent(c->st, c->ev_col, 0));
+    }
     if ((rc = read_cstats(c))) return rc;                // the one host sync
     if ((rc = settle(c))) return rc;                     // a deferred tick: its stats came with it
     const uint64_t R = c->hcstats->rec_total;
@@ -1474,7 +1519,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
         if (pairs && (rc = ensure(c, c->gk0, c->rec_cap * 8))) return rc;
         c->hcstats->overflow = 0;
         HIPCHK(hipMemcpyAsync(c->cstats, c->hcstats, sizeof(DevStats), hipMemcpyHostToDevice, c->st));
-        write_pass();
+        write_pass(c->st);
         HIPCHK(hipGetLastError());
         if ((rc = read_cstats(c))) return rc;
         if (c->hcstats->overflow) return set_err(c, GW_ENOMEM, "sync record buffer overflowed twice");

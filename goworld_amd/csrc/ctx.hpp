@@ -140,6 +140,13 @@ struct gw_ctx {
     int dev = 0;
     hipStream_t st = nullptr;
     hipStream_t own_st = nullptr;   // the context's own stream (st may be a caller's)
+    // a collect that follows a deferred tick runs its flag / count / write
+    // passes on st2 (after ev_diff: the tick's diff stage), beside the tick's
+    // events stage on st; st waits for ev_col before the statistics publish
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_diff = nullptr, ev_col = nullptr;
+    ScanCtx sc2{};                  // the collect stream's look-back scans (sc is the tick's)
+    bool overlap = true;            // GW_OVERLAP_COLLECT
     std::string err;
 
     std::vector<SpaceHost> spaces;
@@ -198,7 +205,7 @@ struct gw_ctx {
     // grid + tick scratch
     DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, mtmp, mcell, cand, reg, pidx, heavy, rowrec, own, big, mstat;
     DevBuf mir, ownc, mirc, mlist, mcnt, moff, minfo, icnt, ioff, mreg, chunk_first, srange, bk_a, bk_b, bk_id, bk_cnt, bk_split, ev_d, rtable;
-    DevBuf scan_status, rs_hist, rs_os;   // rs_os: the one-kernel-per-pass sort's scratch (sort_u32_u32)
+    DevBuf scan_status, scan_status2, rs_hist, rs_os;   // rs_os: the one-kernel-per-pass sort's scratch (sort_u32_u32)
     uint32_t walk_min = 32;              // GW_WALK_MIN: TickBufs.walk_min (0: always walk)
     bool mover_compact = true;           // GW_MOVER_COMPACT: TickBufs.compact
     uint32_t heavy_min = 512;            // GW_HEAVY_MIN: TickBufs.heavy_min (0: off; 1M world at 8 strips:

@@ -546,6 +546,7 @@ int gw_init(int device_id, gw_ctx** out) {
         (void)hipEventCreate(&c->ev_t0);
         (void)hipEventCreate(&c->ev_t1);
         if (const char* e = getenv("GW_OVERLAP_COLLECT")) c->overlap = atoi(e) != 0;
+        if (const char* e = getenv("GW_OVERLAP_MIN")) c->overlap_min = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_CELLS_PER_D")) c->cells_per_d = std::min(4, std::max(1, atoi(e)));
         if (const char* e = getenv("GW_MOVER_WPB")) c->diff_u = atoi(e);
         if (const char* e = getenv("GW_NB_U")) c->nb_u = atoi(e);
@@ -1464,7 +1465,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     // diff (the new grid, states and cached neighbour counts), not its events
     // stage: they run on st2 beside it, and st waits for them before the
     // statistics publish (per-stage profiling keeps one stream)
-    const bool ovl = c->overlap && c->pt.on && !c->pt.copied && c->prof != 1;
+    const bool ovl = c->overlap && c->pt.on && !c->pt.copied && c->pt.M >= c->overlap_min && c->prof != 1;
     hipStream_t cs = c->st;
     ScanCtx* csc = &c->sc;
     if (ovl) {

@@ -537,7 +537,8 @@ int gw_init(int device_id, gw_ctx** out) {
         if (hipMalloc(&c->sc.ticket, 8) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "ticket"); break; }
         (void)hipMemset(c->sc.ticket, 0, 8);
         if (hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess) { rc = set_err(c, GW_EDEVICE, "stream"); break; }
-        if (hipEventCreateWithFlags(&c->ev_diff, hipEventDisableTiming) != hipSuccess ||
+        if (hipEventCreateWithFlags(&c->ev_grid, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_diff, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_col, hipEventDisableTiming) != hipSuccess) { rc = set_err(c, GW_EDEVICE, "event"); break; }
         if (hipMalloc(&c->sc2.ticket, 8) != hipSuccess) { rc = set_err(c, GW_ENOMEM, "ticket"); break; }
         (void)hipMemset(c->sc2.ticket, 0, 8);
@@ -608,6 +609,7 @@ void gw_shutdown(gw_ctx* c) {
     for (auto& s : c->stages) { (void)hipEventDestroy(s.a); (void)hipEventDestroy(s.b); }
     if (c->ev_t0) (void)hipEventDestroy(c->ev_t0);
     if (c->ev_t1) (void)hipEventDestroy(c->ev_t1);
+    if (c->ev_grid) (void)hipEventDestroy(c->ev_grid);
     if (c->ev_diff) (void)hipEventDestroy(c->ev_diff);
     if (c->ev_col) (void)hipEventDestroy(c->ev_col);
     if (c->st2) {
@@ -1381,6 +1383,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     prof_end(c, (uint64_t)M * 24);
     prof_begin(c, "grid");
     tick_grid(b, c->sc, c->st);
+    HIPCHK(hipEventRecord(c->ev_grid, c->st));        // a following collect's flag compaction may start here
     c->mpar ^= 1u;                                   // the next rebuild drops this tick's mover bits
     c->cells_zero = true;
     size_t s_grid = prof_end(c, 0);
@@ -1470,7 +1473,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     ScanCtx* csc = &c->sc;
     if (ovl) {
         if ((rc = ensure_scan2(c, C, c->st2))) return rc;
-        HIPCHK(hipStreamWaitEvent(c->st2, c->ev_diff, 0));
+        HIPCHK(hipStreamWaitEvent(c->st2, c->ev_grid, 0));   // the flags are final after the grid stage
         cs = c->st2;
         csc = &c->sc2;
     }
@@ -1478,6 +1481,7 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     launch_flag_compact(c->flags, C, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), *csc, &st->flagged,
                         &st->overflow, sfirst, small ? 2 * n_sp : 0u, cs);
     prof_end(c, (uint64_t)C * 4 * 2);
+    if (ovl) HIPCHK(hipStreamWaitEvent(c->st2, c->ev_diff, 0));   // the counts read the diff's cache
     const uint64_t* nf = (const uint64_t*)&st->flagged;
     prof_begin(c, "sync_count");
     launch_sync_count(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint32_t>(c->rec_cnt), sfirst,

@@ -144,7 +144,7 @@ struct gw_ctx {
     // passes on st2 (after ev_diff: the tick's diff stage), beside the tick's
     // events stage on st; st waits for ev_col before the statistics publish
     hipStream_t st2 = nullptr;
-    hipEvent_t ev_diff = nullptr, ev_col = nullptr;
+    hipEvent_t ev_grid = nullptr, ev_diff = nullptr, ev_col = nullptr;
     ScanCtx sc2{};                  // the collect stream's look-back scans (sc is the tick's)
     bool overlap = true;            // GW_OVERLAP_COLLECT
     uint32_t overlap_min = 65536;   // GW_OVERLAP_MIN: ... after ticks of at least this many ops (a 1M world's

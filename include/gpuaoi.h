@@ -409,7 +409,11 @@ int  gw_synchronize(gw_ctx* ctx);
 /* Run the context's work on a caller's stream (a hipStream_t of the same
  * device, e.g. torch's current stream, so that device-resident ops produced
  * there and results consumed there need no host synchronisation); NULL
- * restores the context's own stream.  Drains the previous stream first. */
+ * restores the context's own stream.  Drains the previous stream first.
+ * A collect after a big deferred tick also runs passes on a second stream of
+ * the context's own, joined back into this one (by an event) before the
+ * collect's statistics are published, so its results are ordered on this
+ * stream like everything else. */
 int  gw_set_stream(gw_ctx* ctx, void* hip_stream);
 
 /* ---- ids, client-sync decode and the wire encode (host boundary rows) -----

@@ -1339,7 +1339,10 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.pair_max = c->pair_auto ? (c->cand_mean <= gw_ctx::PAIR_MEAN ? gw_ctx::PAIR_AUTO : 0u) : c->pair_max;
     // dirty-cell span by cell count: a world strip's few cells spread over
     // more waves (1M world at 8 strips, 57k cells: grid 37 -> 30 us at 2)
-    b.dirty_span = c->dirty_span ? c->dirty_span : (NC > (1u << 20) ? 16u : NC > (1u << 17) ? 8u : 2u);
+    // (above 2M cells 64: config #4's 4.4M cells grid 270 -> 260 us, config #5's
+    // 6.9M 513 -> 484 us)
+    b.dirty_span = c->dirty_span ? c->dirty_span
+                                 : (NC > (1u << 21) ? 64u : NC > (1u << 20) ? 16u : NC > (1u << 17) ? 8u : 2u);
     // decomposed world of >= 2 strips: long movers (a one-strip world holds every pair)
     b.long_step = (c->wd.on && c->wd.g.ranks > 1) ? c->wd.g.max_step : INFINITY;
     b.longs = c->wd.tick_longs;                      // the long lists queued for this tick (world.cpp)

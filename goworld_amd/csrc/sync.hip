@@ -386,6 +386,186 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
     }
 }
 // ---------------------------------------------------------------------------
+// Short lists two per wave (GW_SW_HALVES): a wave takes flagged entries k and
+// k+1; when both have <= SW_HALF_MAX records each half-wave (32 lanes) walks
+// its own entity's window (rows and candidates from HBM, a 5-step search over
+// the half's row prefixes per 32 candidates) and stores its records directly;
+// otherwise both go through the full-wave walk of k_sync_write one after the
+// other.  A uniform world (config #5: ~38 records per entity) spends most of
+// a full-wave walk on per-entity setup.
+constexpr uint32_t SW_HALF_MAX = 64;
+
+template <int U>
+__device__ __forceinline__ void sw_full(const World& w, uint32_t e, uint32_t f, uint64_t at, uint32_t c,
+                                        gw_sync_record* rec, uint64_t rec_cap, DevStats* st,
+                                        unsigned long long* buf) {
+    const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
+    if (at + c > rec_cap) {
+        if (ln == 0) atomicOr(&st->overflow, 1ull);
+        return;
+    }
+    const AoiEnt a = w.rec[e].a;
+    const float4 p = w.rec[e].p;
+    const uint32_t gt = w.gate[e];
+    const SpaceP P = w.sp[a.meta & SPACE_MASK];
+    if (!owned_x(P, a.x)) return;
+    if ((f & GW_SIF_OWN_CLIENT) && gt) {
+        if (ln == 0) st_record_nt(rec + at, e, e, p);
+        ++at;
+    }
+    if (!(f & GW_SIF_NEIGHBOR_CLIENTS) || !(a.meta & PRESENT_BIT)) return;
+    const unsigned long long pxy = ((unsigned long long)__float_as_uint(p.y) << 32) | __float_as_uint(p.x);
+    const unsigned long long pzw = ((unsigned long long)__float_as_uint(p.w) << 32) | __float_as_uint(p.z);
+    uint32_t nb = 0;
+    wave_neighbors_of<U>(w, e, a, P, [&](bool rel, uint32_t ws, uint32_t g) {
+        const bool take = rel && g != 0;
+        const uint64_t bt = wave_ballot(take);
+        if (take) {
+            unsigned long long* r = buf + 3 * (nb + (uint32_t)popc64(bt & lt));
+            r[0] = ((unsigned long long)e << 32) | ws;
+            r[1] = pxy;
+            r[2] = pzw;
+        }
+        nb += (uint32_t)popc64(bt);
+        if (nb >= 64) {
+            wave_sync();
+            sw_flush64(buf, (unsigned long long*)(rec + at), 64);
+            at += 64;
+            nb -= 64;
+            wave_sync();
+            for (uint32_t i = (uint32_t)ln; i < 3 * nb; i += 64) buf[i] = buf[192 + i];
+            wave_sync();
+        }
+    });
+    if (nb) {
+        wave_sync();
+        sw_flush64(buf, (unsigned long long*)(rec + at), nb);
+        wave_sync();
+    }
+}
+
+template <int U>
+__global__ void __launch_bounds__(NT) k_sync_write_h(World w, const uint32_t* __restrict__ flagged,
+                                                     const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
+                                                     uint32_t nf_max, const uint64_t* __restrict__ rec_off,
+                                                     const uint32_t* __restrict__ cnt, gw_sync_record* rec,
+                                                     uint64_t rec_cap, DevStats* st) {
+    __shared__ unsigned long long sbuf[NWAVE][3 * SW_BUF];
+    unsigned long long* buf = sbuf[threadIdx.x >> 6];
+    const uint64_t nf = load_n(nf_max, nf_dev);
+    const int ln = lane_id();
+    const uint32_t half = (uint32_t)ln >> 5, hl = (uint32_t)ln & 31u, hb = half << 5;
+    const uint64_t hmask = half ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+    const uint64_t lt = lanemask_lt();
+    const uint64_t stride = (uint64_t)gridDim.x * NWAVE * 2;
+    for (uint64_t k0 = ((uint64_t)blockIdx.x * NWAVE + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) * 2;
+         k0 < nf; k0 += stride) {
+        const bool hasB = k0 + 1 < nf;
+        const uint32_t cA = cnt[k0], cB = hasB ? cnt[k0 + 1] : 0u;
+        if (max(cA, cB) > SW_HALF_MAX) {                       // wave-uniform: full-wave walks
+            sw_full<U>(w, flagged[k0], fbits[k0], rec_off[k0], cA, rec, rec_cap, st, buf);
+            if (hasB) {
+                wave_sync();
+                sw_full<U>(w, flagged[k0 + 1], fbits[k0 + 1], rec_off[k0 + 1], cB, rec, rec_cap, st, buf);
+            }
+            continue;
+        }
+        const uint64_t k = k0 + half;
+        const bool valid = k < nf;
+        uint32_t e = 0, f = 0, c = 0;
+        uint64_t at = 0;
+        if (valid) {
+            e = flagged[k];
+            f = fbits[k];
+            at = rec_off[k];
+            c = half ? cB : cA;
+        }
+        AoiEnt a;
+        a.x = a.z = 0.0f;
+        a.meta = 0;
+        float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint32_t gt = 0;
+        if (valid) {
+            a = w.rec[e].a;
+            p = w.rec[e].p;
+            gt = w.gate[e];
+        }
+        const SpaceP P = w.sp[a.meta & SPACE_MASK];
+        bool walk = false;
+        if (valid) {
+            if (at + c > rec_cap) {
+                if (hl == 0) atomicOr(&st->overflow, 1ull);
+            } else if (owned_x(P, a.x)) {
+                if ((f & GW_SIF_OWN_CLIENT) && gt) {
+                    if (hl == 0) st_record_nt(rec + at, e, e, p);
+                    ++at;
+                }
+                walk = (f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT);
+            }
+        }
+        // the half's row ranges (lane hl: row hl of its window), then its scan
+        const float d = P.d;
+        uint32_t rs = 0, rl = 0;
+        const Win we = win_of(a.x, a.z, d);
+        if (walk) {
+            const Rect r = search_rect(P, a.x, a.z);
+            const int nr = r.z1 - r.z0 + 1;
+            if ((int)hl < nr) {
+                const uint32_t base = P.cell_base + (uint32_t)(r.z0 + (int)hl) * (uint32_t)P.W;
+                rs = w.gn_start[base + (uint32_t)r.x0];
+                rl = w.gn_start[base + (uint32_t)r.x1 + 1] - rs;
+            }
+        }
+        const uint32_t inc64 = wave_incl_scan<uint32_t>(rl);
+        const uint32_t lo31 = (uint32_t)__builtin_amdgcn_readlane((int)inc64, 31);
+        const uint32_t inc = half ? inc64 - lo31 : inc64;
+        const uint32_t pre = inc - rl;
+        const uint32_t tot0 = lo31, tot1 = (uint32_t)__builtin_amdgcn_readlane((int)inc64, 63) - lo31;
+        const uint32_t total = half ? tot1 : tot0;
+        const uint32_t tmax = max(tot0, tot1);
+        const unsigned long long pxy = ((unsigned long long)__float_as_uint(p.y) << 32) | __float_as_uint(p.x);
+        const unsigned long long pzw = ((unsigned long long)__float_as_uint(p.w) << 32) | __float_as_uint(p.z);
+        unsigned long long se = 0;
+        bool have_se = false;
+        for (uint32_t B = 0; B < tmax; B += 32) {              // wave-uniform
+            const uint32_t kk = B + hl;
+            uint32_t l2 = 0;
+#pragma unroll
+            for (int step = 16; step; step >>= 1) {
+                const uint32_t cc = l2 + (uint32_t)step;
+                const uint32_t pv = (uint32_t)__shfl((int)pre, (int)(hb + min(cc, 31u)), 64);
+                if (cc < 32u && pv <= kk) l2 = cc;
+            }
+            const uint32_t ss = (uint32_t)__shfl((int)rs, (int)(hb + l2), 64);
+            const uint32_t sp = (uint32_t)__shfl((int)pre, (int)(hb + l2), 64);
+            bool take = false;
+            GEnt g;
+            g.slot = e;
+            g.meta = 0;
+            if (kk < total) g = w.gn[ss + (kk - sp)];
+            if (kk < total && g.slot != e && (g.meta & CLIENT_BIT)) {
+                const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
+                bool rel = ia;
+                if (ia != ib) {
+                    if (!have_se) { se = w.rec[e].stamp; have_se = true; }
+                    rel = resolve(ia, ib, se, w.rec[g.slot].stamp);
+                }
+                take = rel;
+            }
+            const uint64_t bt = wave_ballot(take) & hmask;
+            if (take) {
+                unsigned long long* q = (unsigned long long*)(rec + at + (uint64_t)popc64(bt & lt));
+                __builtin_nontemporal_store(((unsigned long long)e << 32) | g.slot, q);
+                __builtin_nontemporal_store(pxy, q + 1);
+                __builtin_nontemporal_store(pzw, q + 2);
+            }
+            at += (uint64_t)popc64(bt);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Small-space mode (every space's grid fits in LDS, e.g. config #4's 10k
 // spaces of 1k): one block per space loads the space's grid entries and row
 // starts into LDS once, then its waves write the records of the space's
@@ -636,6 +816,12 @@ void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* 
                        uint64_t rec_cap, DevStats* st, hipStream_t s, uint64_t* pr, float4* pay) {
     if (!nf_max) return;
     const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
+    static const bool halves = getenv("GW_SW_HALVES") && atoi(getenv("GW_SW_HALVES")) != 0;
+    if (halves && !pr) {
+        hipLaunchKernelGGL(k_sync_write_h<4>, dim3(std::min(nblk(nf_max, 2 * NWAVE), SYNC_MAX_BLOCKS)), dim3(NT), 0, s,
+                           w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec, rec_cap, st);
+        return;
+    }
     if (pr)
         hipLaunchKernelGGL((k_sync_write<4, true>), g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, rec_off, cnt,
                            rec, rec_cap, st, pr, pay);

@@ -146,6 +146,8 @@ struct gw_ctx {
     hipStream_t st2 = nullptr;
     hipEvent_t ev_grid = nullptr, ev_diff = nullptr, ev_col = nullptr;
     ScanCtx sc2{};                  // the collect stream's look-back scans (sc is the tick's)
+    int sw_halves = -1;             // GW_SW_HALVES: 1 / 0 force the write pass's half-wave mode, -1 automatic
+    double rec_per_flagged = 1e9;   // records per flagged entity of the last collect (the mode's choice)
     bool overlap = true;            // GW_OVERLAP_COLLECT
     uint32_t overlap_min = 65536;   // GW_OVERLAP_MIN: ... after ticks of at least this many ops (a 1M world's
                                     // 8-strip rank, 12.5k ops: 0.285 -> 0.294 ms with it; config #3 -25 us)

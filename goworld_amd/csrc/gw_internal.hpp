@@ -348,7 +348,7 @@ void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* 
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
                        uint64_t rec_cap, DevStats* st, hipStream_t s,
-                       uint64_t* pairs = nullptr, float4* pay = nullptr);
+                       uint64_t* pairs = nullptr, float4* pay = nullptr, bool halves = false);
 // the records and the client segment table in one pass (k_records_seg)
 void launch_records_seg(const World& w, const uint64_t* pairs, const uint32_t* idx, const uint32_t* flagged, const float4* pay, uint64_t n, gw_sync_record* out,
                         uint32_t* client_slot, uint64_t* client_off, uint32_t* n_clients, ScanCtx& sc,

@@ -813,10 +813,9 @@ void launch_sync_write_small(const World& w, uint32_t n_spaces, const uint32_t* 
 
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
-                       uint64_t rec_cap, DevStats* st, hipStream_t s, uint64_t* pr, float4* pay) {
+                       uint64_t rec_cap, DevStats* st, hipStream_t s, uint64_t* pr, float4* pay, bool halves) {
     if (!nf_max) return;
     const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
-    static const bool halves = getenv("GW_SW_HALVES") && atoi(getenv("GW_SW_HALVES")) != 0;
     if (halves && !pr) {
         hipLaunchKernelGGL(k_sync_write_h<4>, dim3(std::min(nblk(nf_max, 2 * NWAVE), SYNC_MAX_BLOCKS)), dim3(NT), 0, s,
                            w, flagged, fbits, nf_dev, nf_max, rec_off, cnt, rec, rec_cap, st);

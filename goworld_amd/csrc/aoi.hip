@@ -1559,6 +1559,28 @@ __global__ void __launch_bounds__(BK_NT) k_bk_count(TickBufs b) {
     const uint64_t n = b.st->n_sort;
     const uint64_t T = b.st->bk_tiles;
     if (blockIdx.x >= T) return;                            // block-uniform
+    const int W = b.wbits;
+    const uint64_t km = (1ull << (2 * W + 1)) - 1;
+    constexpr int IPT = BK_TILE / BK_NT;
+    // the first tile's items and their weights are loaded before the bucket
+    // table is built (its bound loads and searches overlap them); a strip's
+    // tick has a few tiles, so this pass is one load chain long
+    uint64_t k[IPT];
+    uint32_t wt[IPT];
+    auto load = [&](uint64_t tile) {
+        const uint64_t base = tile * BK_TILE;
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint64_t i = base + (uint64_t)j * BK_NT + t;
+            k[j] = i < n ? b.bk_a[i] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint64_t i = base + (uint64_t)j * BK_NT + t;
+            wt[j] = i < n ? bk_weight(b, k[j]) : 0u;
+        }
+    };
+    load(blockIdx.x);
     int lsh;
     bk_lut_build(b, lut, NB, lsh);                          // (syncs)
     // grid-stride over the tiles: the grid is sized by the last tick's items,
@@ -1567,33 +1589,17 @@ __global__ void __launch_bounds__(BK_NT) k_bk_count(TickBufs b) {
     for (uint32_t i = t; i < NB; i += BK_NT) h[i] = hw[i] = 0;
     __syncthreads();
     const uint64_t base = tile * BK_TILE;
-    {
-        const int W = b.wbits;
-        const uint64_t km = (1ull << (2 * W + 1)) - 1;
-        constexpr int IPT = BK_TILE / BK_NT;
-        uint64_t k[IPT];
 #pragma unroll
-        for (int j = 0; j < IPT; ++j) {
-            const uint64_t i = base + (uint64_t)j * BK_NT + t;
-            k[j] = i < n ? b.bk_a[i] : 0ull;
-        }
-        uint32_t wt[IPT];
-#pragma unroll
-        for (int j = 0; j < IPT; ++j) {
-            const uint64_t i = base + (uint64_t)j * BK_NT + t;
-            wt[j] = i < n ? bk_weight(b, k[j]) : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < IPT; ++j) {
-            const uint64_t i = base + (uint64_t)j * BK_NT + t;
-            if (i < n) {
-                const uint32_t q = bk_bucket(lut, lsh, (uint32_t)((k[j] & km) >> W));
-                b.bk_id[i] = (uint16_t)q;
-                atomicAdd(&h[q], 1u);
-                atomicAdd(&hw[q], wt[j]);
-            }
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t i = base + (uint64_t)j * BK_NT + t;
+        if (i < n) {
+            const uint32_t q = bk_bucket(lut, lsh, (uint32_t)((k[j] & km) >> W));
+            b.bk_id[i] = (uint16_t)q;
+            atomicAdd(&h[q], 1u);
+            atomicAdd(&hw[q], wt[j]);
         }
     }
+    if (tile + gridDim.x < T) load(tile + gridDim.x);      // the next tile's loads under the count writes
     __syncthreads();
     for (uint32_t i = t; i < NB; i += BK_NT)
         b.bk_cnt[(uint64_t)i * T + tile] = (unsigned long long)h[i] | ((unsigned long long)hw[i] << 32);
@@ -2048,30 +2054,53 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
 #endif
 __global__ void __launch_bounds__(RESET_NT) k_tick_reset(TickBufs b, const unsigned long long* __restrict__ pub_src,
                                                         unsigned long long* pub_dst, uint32_t pub_words) {
-    // the next tick's bucket bounds: their event loads go out first, the
-    // statistics copy below overlaps them
-    uint32_t v[SPLIT_PT];
-    const bool split = b.st && bk_split_load(b, b.st->ev_pk, b.st->overflow, v);
-    // the statistics the host reads after its sync, written straight into its
-    // (coherent, pinned) buffer: no blit copy between the collect and the reset.
-    // Each DevStats goes over as its header words and, per field, the sum of
-    // its shards in shard[0] (20 PCIe stores instead of 1040: the host reads
-    // shard[0] only; config #3 world strips spent ~10 us here)
+    // the statistics (at most two DevStats: the tick's and the collect's) are
+    // loaded first, every word in flight together, then the next tick's
+    // bucket bounds (their event loads depend on the tick's event totals)
     constexpr uint32_t HDR = (uint32_t)(offsetof(DevStats, shard) / 8), DSW = (uint32_t)(sizeof(DevStats) / 8);
     static_assert(STAT_SHARDS * SH_FIELDS == RESET_NT, "one shard word per thread");
-    __shared__ unsigned long long red[RESET_NT];
-    for (uint32_t q = 0; q * DSW < pub_words; ++q) {
-        const unsigned long long* src = pub_src + (size_t)q * DSW;
-        unsigned long long* dst = pub_dst + (size_t)q * DSW;
-        if (threadIdx.x < HDR) dst[threadIdx.x] = src[threadIdx.x];
-        red[threadIdx.x] = src[HDR + threadIdx.x];         // shard t / SH_FIELDS, field t % SH_FIELDS
-        __syncthreads();
-        for (uint32_t h = RESET_NT / 2; h >= SH_FIELDS; h >>= 1) {
-            if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
-            __syncthreads();
+    static_assert(SH_FIELDS <= 4 && (SH_FIELDS & (SH_FIELDS - 1)) == 0, "fields per lane group");
+    constexpr int QMAX = 2, NWR = RESET_NT / 64;
+    const uint32_t nq = min(pub_words / DSW, (uint32_t)QMAX);
+    unsigned long long hv[QMAX], sv[QMAX];
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+        hv[q] = sv[q] = 0;
+        if ((uint32_t)q < nq) {
+            const unsigned long long* src = pub_src + (size_t)q * DSW;
+            if (threadIdx.x < HDR) hv[q] = src[threadIdx.x];
+            sv[q] = src[HDR + threadIdx.x];               // shard t / SH_FIELDS, field t % SH_FIELDS
         }
-        if (threadIdx.x < SH_FIELDS) dst[HDR + threadIdx.x] = red[threadIdx.x];
-        __syncthreads();
+    }
+    uint32_t v[SPLIT_PT];
+    const bool split = b.st && bk_split_load(b, b.st->ev_pk, b.st->overflow, v);
+    // written straight into the host's (coherent, pinned) buffer: each DevStats
+    // as its header words and, per field, the sum of its shards in shard[0]
+    // (20 PCIe stores instead of 1040: the host reads shard[0] only).  The sums:
+    // lane xor-shuffles over the shards a wave holds, then the waves' partials
+    __shared__ unsigned long long red[QMAX][NWR * SH_FIELDS];
+    const int ln = lane_id(), wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+        if ((uint32_t)q >= nq) break;
+        unsigned long long x = sv[q];
+        for (int o = SH_FIELDS; o < 64; o <<= 1) {
+            const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)x, o, 64);
+            const unsigned hi = (unsigned)__shfl_xor((int)(unsigned)(x >> 32), o, 64);
+            x += ((unsigned long long)hi << 32) | lo;
+        }
+        if (ln < SH_FIELDS) red[q][wv * SH_FIELDS + ln] = x;
+        if (threadIdx.x < HDR) pub_dst[(size_t)q * DSW + threadIdx.x] = hv[q];
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)(QMAX * SH_FIELDS)) {
+        const uint32_t q = threadIdx.x / SH_FIELDS, f = threadIdx.x % SH_FIELDS;
+        if (q < nq) {
+            unsigned long long x = 0;
+#pragma unroll
+            for (int k = 0; k < NWR; ++k) x += red[q][k * SH_FIELDS + f];
+            pub_dst[(size_t)q * DSW + HDR + f] = x;
+        }
     }
     if (!b.st) {
         PUB_FENCE();

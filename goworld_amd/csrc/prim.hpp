@@ -245,10 +245,12 @@ __global__ void __launch_bounds__(NT) k_scan1(const TI* in, TO* out, uint64_t n_
     __shared__ TO lds[IPT * NWAVE];
     __shared__ uint32_t s_tile;
     __shared__ TO s_prefix;
+    // the device-side count is loaded under the ticket's round trip (not after
+    // the barrier: one dependent load less on a chain of a few microseconds)
+    const uint64_t n = load_n(n_max, n_dev);
     if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tbase);
     __syncthreads();
     const uint32_t tile = s_tile;
-    const uint64_t n = load_n(n_max, n_dev);
     const uint64_t t0 = (uint64_t)tile * (IPT * NT);
     // tiles past a device-side count do nothing (no later tile waits on them)
     if (t0 >= n && tile > 0) return;

@@ -627,18 +627,24 @@ __device__ __forceinline__ bool pair_rel(float ax, float az, unsigned long long 
 // lists hold every long mover's state before and after the tick, so the old
 // and the new relation of each pair are evaluated here even when no rank holds
 // both ends.  Events are appended to A's region before its sort.
-__device__ __forceinline__ void long_pairs(const TickBufs& b, uint32_t A, float d, uint32_t* out, uint64_t cap,
-                                        uint32_t& n, uint32_t& l_nl) {
-    const int ln = lane_id();
-    const uint64_t lt = lanemask_lt();
+// A's entry in the lists of the tick, -1 if not listed (no list queued, or
+// its owner's list missing)
+__device__ __forceinline__ int32_t long_index(const TickBufs& b, uint32_t A) {
     const uint32_t nl = b.n_long;
-    int32_t ia = -1;                                   // A's own entry
+    int32_t ia = -1;
     for (uint32_t base = 0; base < nl && ia < 0; base += 64) {
-        const uint32_t j = base + (uint32_t)ln;
+        const uint32_t j = base + (uint32_t)lane_id();
         const uint64_t hit = wave_ballot(j < nl && b.longs[j].slot == A);
         if (hit) ia = (int32_t)(base + (uint32_t)__builtin_ctzll(hit));
     }
-    if (ia < 0) return;                                // not listed (a rank's list was not queued)
+    return ia;
+}
+
+__device__ __forceinline__ void long_pairs(const TickBufs& b, uint32_t A, int32_t ia, float d, uint32_t* out,
+                                        uint64_t cap, uint32_t& n, uint32_t& l_nl) {
+    const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint32_t nl = b.n_long;
     const gw_long_move LA = b.longs[ia];
     for (uint32_t base = 0; base < nl; base += 64) {
         const uint32_t j = base + (uint32_t)ln;
@@ -662,7 +668,9 @@ __device__ __forceinline__ void long_pairs(const TickBufs& b, uint32_t A, float 
 // per wave.
 // RR (k_mover): the row ranges k_bounds gathered, loaded with the entry
 // itself (the walk then starts one round trip after the wave does).
-template <int DIFF_U, uint32_t SCAP, class Src, bool RR = false>
+// LONGS = false: a context without long movers (not a world of >= 2 strips,
+// TickBufs::long_step infinite) compiles the group-teleport paths out
+template <int DIFF_U, uint32_t SCAP, class Src, bool RR = false, bool LONGS = true>
 __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_t* lds, const Src& S) {
     const int ln = lane_id();
     const uint2 rr = (RR && ln < (int)(2 * RR_ROWS)) ? ((const uint2*)b.rowrec)[m * 2 * RR_ROWS + ln]
@@ -697,7 +705,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     const bool ownA = owned_x(P, pn ? me.x : me.ox);
     // a long mover's pairs are emitted by the owners of the other members
     // (they hold both ends of every pair that changes)
-    const bool longA = (me.tags & TAG_LONG) != 0;
+    const bool longA = LONGS && (me.tags & TAG_LONG) != 0;
     // A's stamps are read only at a boundary tie (rare): loaded up front, the
     // in-order memory counter made every first chunk wait for them too
     const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
@@ -707,6 +715,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     // per-lane counts, summed once after the walk (a ballot + popcount per
     // count and chunk was ~10 scalar instructions of every chunk's chain)
     uint32_t l_old = 0, l_new = 0, l_cli = 0, l_nl = 0, l_nml = 0;
+    uint32_t l_lc = 0;      // (LONGS) pairs with another long mover related before or after the tick
     Flat f;
     if (RR && (uint32_t)__builtin_amdgcn_readfirstlane((int)rr.x) <= (uint32_t)__builtin_amdgcn_readfirstlane((int)rr.y))
         f = flat_from(rr.x, rr.y - rr.x);
@@ -800,12 +809,26 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             nm_ += (uint32_t)popc64(bm);
             l_nl += (ev && lv) ? 1u : 0u;
             l_nml += (mev && lv) ? 1u : 0u;
+            if (LONGS) l_lc += (longA && longB && (t_ro || t_rn)) ? 1u : 0u;
         }
     }
     // group teleports: A is a long mover whose new position is owned here (not
     // its old owner, where it left); its pairs with the other long movers come
     // from the lists of every rank
-    if (longA && pn && owned_x(P, me.x) && b.n_long) long_pairs(b, A, d, out, cap, n, l_nl);
+    // If the lists do not cover A (a caller's transport skipped
+    // gw_world_submit_longs, or a rank's list is missing), nobody emits those
+    // pairs: the related ones are counted into HaloStats.conflicts, which
+    // gw_world_status reports
+    if (longA && pn && owned_x(P, me.x)) {
+        const int32_t ia = long_index(b, A);
+        if (ia >= 0) {
+            long_pairs(b, A, ia, d, out, cap, n, l_nl);
+        } else if (b.conflicts) {
+            const uint32_t lc = wave_incl_scan<uint32_t>(l_lc);
+            const uint32_t nlc = (uint32_t)__builtin_amdgcn_readlane((int)lc, 63);
+            if (ln == 0 && nlc) atomicAdd(b.conflicts, (unsigned long long)nlc);
+        }
+    }
     // the wave's sums (DPP scans, lane 63): old | new, client | own leaves, mirror leaves
     const unsigned long long s_on = wave_incl_scan<unsigned long long>(l_old | ((unsigned long long)l_new << 32));
     const unsigned long long s_cl = wave_incl_scan<unsigned long long>(l_cli | ((unsigned long long)l_nl << 32));
@@ -870,7 +893,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
 #endif
 // one wave per primary entry (pidx, cell order): no wave is dispatched for
 // the secondary entries (half the mover grid), whose zeros k_bounds wrote
-template <int DIFF_U>
+template <int DIFF_U, bool LONGS>
 __global__ void __launch_bounds__(64) KMOVER_SGPR k_mover_c(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[SORT_LDS];
     const uint64_t k = blockIdx.x;
@@ -884,7 +907,7 @@ __global__ void __launch_bounds__(64) KMOVER_SGPR k_mover_c(TickBufs b) {
         m = b.pidx[k];                            // in bounds (k < ops), read with the count
         if (k >= np) return;
     }
-    mover_one<DIFF_U, SORT_LDS, GlobalSrc, true>(b, m, lds, GlobalSrc{b.w.gn, b.w.gn_start, b.gm_start, b.gm});
+    mover_one<DIFF_U, SORT_LDS, GlobalSrc, true, LONGS>(b, m, lds, GlobalSrc{b.w.gn, b.w.gn_start, b.gm_start, b.gm});
 }
 
 template <int DIFF_U, int WPB>
@@ -1978,7 +2001,10 @@ void tick_diff(const TickBufs& b, hipStream_t s) {
         return;
     }
     if (b.compact) {                       // one wave per primary entry (<= one per op)
-        hipLaunchKernelGGL((k_mover_c<2>), dim3(nblk1(b.m, 1)), dim3(64), 0, s, b);
+        if (std::isinf(b.long_step))       // no long movers: the group-teleport paths compiled out
+            hipLaunchKernelGGL((k_mover_c<2, false>), dim3(nblk1(b.m, 1)), dim3(64), 0, s, b);
+        else
+            hipLaunchKernelGGL((k_mover_c<2, true>), dim3(nblk1(b.m, 1)), dim3(64), 0, s, b);
         return;
     }
     switch (b.diff_u) {                    // GW_MOVER_WPB: waves per k_mover block

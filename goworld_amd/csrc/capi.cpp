@@ -1348,6 +1348,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.long_step = (c->wd.on && c->wd.g.ranks > 1) ? c->wd.g.max_step : INFINITY;
     b.longs = c->wd.tick_longs;                      // the long lists queued for this tick (world.cpp)
     b.n_long = c->wd.tick_nlong;
+    b.conflicts = c->wd.on ? &c->halo->conflicts : nullptr;
     c->wd.tick_longs = nullptr;
     c->wd.tick_nlong = 0;
     b.ol = c->ol;

@@ -262,6 +262,8 @@ struct TickBufs {
                               // mover (its pairs are attributed to the targets' owners); +inf otherwise
     const gw_long_move* longs;   // decomposed world: every rank's long movers of the tick (group teleports:
     uint32_t n_long;             // their pairs are evaluated from these by the owner of the watcher)
+    unsigned long long* conflicts;   // decomposed world (else null): long-mover pairs the lists did not
+                                     // cover (no list queued, or the watcher missing from it), HaloStats
     uint32_t dirty_span;      // GW_DIRTY_SPAN: cells whose dirty flags one k_grid_dirty wave scans (1..64)
     uint32_t compact;         // GW_MOVER_COMPACT (default 1): k_mover runs one wave per primary entry
                               // (pidx), else one per mover-grid entry, the others exiting

@@ -477,8 +477,10 @@ inline int radix_sort(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n_max, 
 
 // ---------------------------------------------------------------------------
 // Stable LSD radix sort of (u32 key, u32 value) pairs, ONE kernel per pass
-// ("onesweep"), DB-bit digits (8, 10 or 11: keys of 17-22 bits sort in two
-// passes instead of three): the digit counts of every pass are
+// ("onesweep"), DB-bit digits (8: 10- and 11-bit digits measured slower, two
+// passes of 214 us against three of 103 us over config #3's 14.7M fan-out
+// pairs -- a wider digit's runs per tile are shorter write segments -- and
+// were dropped): the digit counts of every pass are
 // order-independent, so one upfront pass over the keys gives each pass's
 // global digit bases; a pass then ranks its 4096-pair tile in LDS, publishes
 // the tile's per-digit counts and gets the counts of all earlier tiles by a
@@ -498,8 +500,8 @@ constexpr int RS2_TILE = 4096;
 constexpr int RS2_WAVE_KEYS = RS2_TILE / RS2_NW;     // 512 per wave
 constexpr int RS2_CHUNKS = RS2_WAVE_KEYS / 64;      // 8
 constexpr int RS2_MAX_PASSES = 4;
-constexpr int RS2_MAX_RADIX = 2048;                 // DB <= 11
-constexpr int RS2_STATUS_PER_TILE = 4096;           // max over the digit widths of passes * radix
+constexpr int RS2_MAX_RADIX = 256;                  // DB = 8
+constexpr int RS2_STATUS_PER_TILE = RS2_MAX_PASSES * RS2_MAX_RADIX;   // status words per tile
 constexpr int RS2_GBLOCKS = 1024;                   // blocks of the upfront histogram (grid-stride)
 constexpr uint32_t OS_AGG = 1u << 30, OS_INC = 2u << 30, OS_VAL = (1u << 30) - 1;
 constexpr int OS_LB = 4;                             // predecessors a look-back step reads
@@ -507,7 +509,7 @@ constexpr int OS_LB = 4;                             // predecessors a look-back
 template <int DB>
 struct OsCfg {
     static constexpr int RD = 1 << DB;                                  // digits
-    static constexpr int MAXP = DB == 8 ? RS2_MAX_PASSES : 2;
+    static constexpr int MAXP = RS2_MAX_PASSES;
     static constexpr int DPT = RD > RS2_NT ? RD / RS2_NT : 1;           // digits per pass thread
     static constexpr int DT = RD / DPT;                                 // pass threads owning digits
     static_assert(MAXP * RD <= RS2_STATUS_PER_TILE, "status words per tile");
@@ -766,8 +768,7 @@ inline int radix_sort2_db(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1
 
 // Sorts (k0,v0) by bits [lo_bit, hi_bit) (at most 32 bits) with (k1,v1) as
 // ping-pong; scratch holds radix2_scratch_words(n_max) u32 (no clearing
-// needed by the caller).  Digit width: 8 bits; with GW_SORT_DB >= 10, 17-20
-// key bits in two 10-bit passes, 21-22 in two 11-bit passes.  With aos, the last pass
+// needed by the caller).  Digit width: 8 bits.  With aos, the last pass
 // writes gw_event {key & aos_mask, value} there (and the return value is
 // meaningless).  Returns 0 if the result is in (k0,v0), 1 if in (k1,v1).
 inline int radix_sort2(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n_max, const uint64_t* n_dev,
@@ -776,16 +777,6 @@ inline int radix_sort2(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, u
     const uint64_t nt = radix2_tiles(n_max);
     if (nt == 0 || hi_bit <= lo_bit) return 0;
     const int bits = hi_bit - lo_bit;
-    // 8-bit digits unless GW_SORT_DB asks for wider ones: two 10-bit passes
-    // over config #3's 14.7M fan-out pairs took 214 us each, three 8-bit
-    // passes 103 us each (a wider digit's runs per tile are shorter segments)
-    static const int db_max = getenv("GW_SORT_DB") ? atoi(getenv("GW_SORT_DB")) : 8;
-    if (db_max <= 8)
-        return radix_sort2_db<8>(k0, v0, k1, v1, n_max, n_dev, lo_bit, (bits + 7) / 8, scratch, st, aos, aos_mask);
-    if (bits > 16 && bits <= 20)
-        return radix_sort2_db<10>(k0, v0, k1, v1, n_max, n_dev, lo_bit, 2, scratch, st, aos, aos_mask);
-    if (bits > 20 && bits <= 22)
-        return radix_sort2_db<11>(k0, v0, k1, v1, n_max, n_dev, lo_bit, 2, scratch, st, aos, aos_mask);
     return radix_sort2_db<8>(k0, v0, k1, v1, n_max, n_dev, lo_bit, (bits + 7) / 8, scratch, st, aos, aos_mask);
 }
 
@@ -798,11 +789,6 @@ inline int radix_sort2_p64(uint64_t* p0, uint64_t* p1, uint64_t n_max, const uin
     const int bits = hi_bit - lo_bit;
     uint32_t* a = reinterpret_cast<uint32_t*>(p0);
     uint32_t* b = reinterpret_cast<uint32_t*>(p1);
-    static const int db_max = getenv("GW_SORT_DB") ? atoi(getenv("GW_SORT_DB")) : 8;   // (as radix_sort2)
-    if (db_max > 8 && bits > 16 && bits <= 20)
-        return radix_sort2_db<10, true>(a, nullptr, b, nullptr, n_max, n_dev, lo_bit, 2, scratch, st, nullptr, 0);
-    if (db_max > 8 && bits > 20 && bits <= 22)
-        return radix_sort2_db<11, true>(a, nullptr, b, nullptr, n_max, n_dev, lo_bit, 2, scratch, st, nullptr, 0);
     return radix_sort2_db<8, true>(a, nullptr, b, nullptr, n_max, n_dev, lo_bit, (bits + 7) / 8, scratch, st,
                                    nullptr, 0);
 }

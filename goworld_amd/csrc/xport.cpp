@@ -69,6 +69,19 @@ int broken(gw_ctx* c, LocalGroup* G, const char* what) {
     return set_err(c, GW_EDEVICE, "loopback group: %s", what);
 }
 
+// A HIP failure inside a loopback group end breaks the group (its flag set and
+// the peers woken) before returning, so the peers fail at once instead of
+// waiting out GW_LOOPBACK_TIMEOUT_S for posts or copies that never come
+#define LGCHK(expr)                                                                              \
+    do {                                                                                         \
+        hipError_t _e = (expr);                                                                  \
+        if (_e != hipSuccess) {                                                                  \
+            char _m[256];                                                                        \
+            snprintf(_m, sizeof _m, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+            return broken(c, G, _m);                                                             \
+        }                                                                                        \
+    } while (0)
+
 int local_group_end(gw_ctx* c) {
     LocalGroup* G = c->lgrp;
     const int R = G->R, me = c->c_rank;
@@ -78,8 +91,11 @@ int local_group_end(gw_ctx* c) {
     for (const P2P& x : pend) {                      // 1. every send is posted before any wait
         if (!x.send) continue;
         hipEvent_t ev = nullptr;
-        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(ev, c->st));
+        LGCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        if (hipError_t e = hipEventRecord(ev, c->st)) {
+            (void)hipEventDestroy(ev);
+            LGCHK(e);
+        }
         std::lock_guard<std::mutex> lk(G->mu);
         G->posts[(size_t)me * R + x.peer].push_back(LocalGroup::Post{x.p, x.bytes, ev});
     }
@@ -102,12 +118,12 @@ int local_group_end(gw_ctx* c) {
             snprintf(msg, sizeof msg, "rank %d sent %zu bytes, rank %d receives %zu", x.peer, po.bytes, me, x.bytes);
             return broken(c, G, msg);
         }
-        HIPCHK(hipStreamWaitEvent(c->st, po.ready, 0));
+        LGCHK(hipStreamWaitEvent(c->st, po.ready, 0));
         (void)hipEventDestroy(po.ready);           // released once the recorded work completes
-        if (x.bytes) HIPCHK(hipMemcpyAsync(x.p, po.p, x.bytes, hipMemcpyDeviceToDevice, c->st));
+        if (x.bytes) LGCHK(hipMemcpyAsync(x.p, po.p, x.bytes, hipMemcpyDeviceToDevice, c->st));
         hipEvent_t dn = nullptr;
-        HIPCHK(hipEventCreateWithFlags(&dn, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(dn, c->st));
+        LGCHK(hipEventCreateWithFlags(&dn, hipEventDisableTiming));
+        LGCHK(hipEventRecord(dn, c->st));
         {
             std::lock_guard<std::mutex> lk(G->mu);
             G->done[(size_t)x.peer * R + me].push_back(dn);
@@ -126,7 +142,7 @@ int local_group_end(gw_ctx* c) {
             dn = q.front();
             q.pop_front();
         }
-        HIPCHK(hipStreamWaitEvent(c->st, dn, 0));
+        LGCHK(hipStreamWaitEvent(c->st, dn, 0));
         (void)hipEventDestroy(dn);
     }
     return 0;

@@ -177,3 +177,79 @@ def test_loopback_world_1m_8_strips_equals_single_context():
             assert _sort_rec(got).tobytes() == _sort_rec(exp).tobytes(), f"tick {t}: records differ"
             n_rec += len(exp)
     assert n_ev > 100_000 and n_rec > 1_000_000
+
+
+def test_world_missing_long_lists_are_reported_as_conflicts():
+    """Group teleports need every rank's long-mover list (gw_world_submit_longs):
+    a long mover's pairs with the other long movers are emitted only from the
+    lists.  Two strip contexts driven by pointer (gw_world_route -> world_far ->
+    world_longs -> gw_world_submit / submit_far / submit_longs, as a caller's
+    own transport would); rank 1 never gets the lists, so the pairs of the long
+    movers landing in its strip are lost, and gw_world_status must say so
+    (conflicts > 0 there, 0 on rank 0, which got them)."""
+    from goworld_amd.traces import LONG_DTYPE
+    R, TR, skip = 2, GROUPS, 1
+    tr = T.strip_world_trace(TR["seed"], TR["n"], R, TR["strip_w"], TR["height"], TR["d"], TR["ticks"],
+                             TR["max_step"], teleports=TR["teleports"], groups=TR["groups"])
+    geom = dworld.Strips(0.0, tr.strip_w, R, tr.d, tr.max_step)
+    gs, bufs = [], []
+    try:
+        for r in range(R):
+            g = gpuaoi.GpuAOI(0)
+            gs.append(g)
+            lo, hi = geom.ext(r)
+            b = (max(lo, tr.bounds[0]), tr.bounds[1], min(hi, tr.bounds[2]), tr.bounds[3])
+            g.world_create(geom.x0, geom.w, geom.d, geom.max_step, R, r, tr.n, b)
+            g.set_clients(np.arange(tr.n, dtype=np.uint32), tr.gates)
+        conflicts = [0] * R
+        n_long = 0
+        for t in range(len(tr.ticks)):
+            ptrs = []
+            for r, g in enumerate(gs):
+                ops = np.ascontiguousarray(tr.rank_ops(t, r))
+                p = g.dev_alloc(max(ops.nbytes, 64))
+                bufs.append((g, p))
+                if len(ops):
+                    g.h2d(p, ops)
+                ptrs.append((p, len(ops)))
+            sends = []
+            for g, (p, m) in zip(gs, ptrs):
+                g.synchronize()
+                sends.append(g.world_route(p, m))
+            fars = [g.world_far() for g in gs]
+            parts = []
+            for g in gs:
+                lp, ln_ = g.world_longs()
+                if ln_:
+                    a = np.zeros(ln_, LONG_DTYPE)
+                    g.d2h(a, lp)
+                    parts.append(a)
+            longs = np.concatenate(parts) if parts else np.zeros(0, LONG_DTYPE)
+            n_long += len(longs)
+            lptr = 0
+            if len(longs):
+                lptr = gs[0].dev_alloc(longs.nbytes)
+                bufs.append((gs[0], lptr))
+                gs[0].h2d(lptr, longs)
+            for r, g in enumerate(gs):
+                left = sends[r - 1][1] if r > 0 else (0, 0)
+                right = sends[r + 1][0] if r + 1 < R else (0, 0)
+                g.world_submit([left, right])
+                for q in range(R):
+                    if r in fars[q]:
+                        g.world_submit_far(*fars[q][r])
+                if len(longs) and r != skip:
+                    g.world_submit_longs(lptr, len(longs))
+            for g in gs:
+                g.tick(copy=False)
+                g.sync_collect(copy=False)
+            for r, g in enumerate(gs):
+                conflicts[r] += g.world_status()[1]        # local counters (no communicator)
+    finally:
+        for g, p in bufs:
+            g.synchronize()
+            g.dev_free(p)
+        for g in gs:
+            g.close()
+    assert n_long > 0
+    assert conflicts[skip] > 0 and conflicts[1 - skip] == 0, conflicts

@@ -586,7 +586,8 @@ def test_tick_statistics_match_oracle(ctx_factory):
 def test_client_paths_wide_slot_keys(ctx_factory, pad):
     """The client paths' stable sorts by watcher slot at wider keys: an empty
     first space of `pad` slots puts the traced space's slots past 2^17 (18-bit
-    keys: two 10-bit passes) or 2^20 (21-bit keys: two 11-bit passes).  Client
+    keys) or 2^20 (21-bit keys), three 8-bit onesweep passes instead of the two
+    of a 16-bit key (the last pass's digit then spans fewer bits).  Client
     messages, fan-out and the per-client collect equal the oracle's, slots
     shifted by the space's base."""
     tr = T.config2(ticks=3, n=20_000)

@@ -26,6 +26,16 @@ $(LIBDIR)/libgpuaoi.so: $(OBJ)
 $(LIBDIR)/c_harness: tests/c_harness.c include/gpuaoi.h $(LIBDIR)/libgpuaoi.so
 	gcc -O2 -std=c99 -Wall -Iinclude -o $@ tests/c_harness.c -L$(LIBDIR) -lgpuaoi -Wl,-rpath,'$$ORIGIN'
 
+# the plain-C harness with ASan + UBSan on its host code (gcc; the library it
+# calls is not instrumented): tests/test_c_harness.py runs it where no GPU is
+# needed (argument, input and error paths)
+$(LIBDIR)/c_harness_san: tests/c_harness.c include/gpuaoi.h $(LIBDIR)/libgpuaoi.so
+	gcc -O1 -g -std=c99 -Wall -fsanitize=address,undefined -fno-sanitize-recover=all -fno-omit-frame-pointer \
+	    -Iinclude -o $@ tests/c_harness.c -L$(LIBDIR) -lgpuaoi -Wl,-rpath,'$$ORIGIN'
+
+san: $(LIBDIR)/c_harness_san
+	$(MAKE) -s -C oracle san
+
 oracle:
 	$(MAKE) -s -C oracle
 
@@ -33,4 +43,4 @@ clean:
 	rm -rf $(LIBDIR)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle san clean

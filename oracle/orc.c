@@ -18,9 +18,16 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* qsort of n elements; qsort(NULL, 0, ...) is undefined behaviour (its base
+ * is declared non-null), so empty and single-element arrays are left alone */
+static void sort_n(void* base, size_t n, size_t size, int (*cmp)(const void*, const void*)) {
+    if (n > 1) qsort(base, n, size, cmp);
+}
+
 /* ------------------------------------------------------------------------ */
 /* small growable u32 set (Go map[*T]struct{} stand-in: order is irrelevant) */
 typedef struct { uint32_t* a; uint32_t n, cap; } vec32;
+
 
 static void v_push(vec32* v, uint32_t x) {
     if (v->n == v->cap) {
@@ -348,7 +355,7 @@ static void grid_build(grid_t* g, const orc_space* s, const uint32_t* slots, siz
         g->e[i].key = cell_key(cell_of(s->ac[0][b], g->d), cell_of(s->ac[1][b], g->d));
         g->e[i].slot = b;
     }
-    qsort(g->e, n, sizeof(gent), cmp_gent);
+    sort_n(g->e, n, sizeof(gent), cmp_gent);
 }
 static size_t lower_key(const grid_t* g, uint64_t k) {
     size_t lo = 0, hi = g->n;
@@ -416,7 +423,7 @@ int orc_bulk_enter(orc_space* s, uint32_t n, const uint32_t* slots,
         lent* L = (lent*)malloc((size_t)(n ? n : 1) * sizeof(lent));
         for (int ax = 0; ax < 2; ++ax) {
             for (uint32_t i = 0; i < n; ++i) { L[i].c = s->ac[ax][slots[i]]; L[i].ord = (int32_t)i; L[i].slot = (int32_t)slots[i]; }
-            qsort(L, n, sizeof(lent), cmp_lent);
+            sort_n(L, n, sizeof(lent), cmp_lent);
             for (uint32_t i = 0; i < n; ++i) {
                 int32_t a = L[i].slot;
                 s->node[a].prev[ax] = i ? L[i - 1].slot : -1;
@@ -505,8 +512,8 @@ static void seqrule_relations(orc_space* s, const uint32_t* touched, uint32_t nt
     for (uint32_t i = 0; i < naff; ++i) {
         uint32_t b = afflist[i];
         vec32* o = &s->nb[b]; vec32* n = &nw[b];
-        qsort(o->a, o->n, 4, cmp_u32);
-        qsort(n->a, n->n, 4, cmp_u32);
+        sort_n(o->a, o->n, 4, cmp_u32);
+        sort_n(n->a, n->n, 4, cmp_u32);
         uint32_t p = 0, q = 0;
         while (p < o->n || q < n->n) {
             if (q >= n->n || (p < o->n && o->a[p] < n->a[q])) { push_ev(&s->leave, &s->n_leave, &capl, b, o->a[p]); ++p; }
@@ -521,8 +528,8 @@ static void seqrule_relations(orc_space* s, const uint32_t* touched, uint32_t nt
     }
     for (uint32_t i = 0; i < s->cap; ++i) v_free(&nw[i]);
     free(nw); free(afflist); free(g.e); free(pres); free(movers);
-    qsort(s->enter, s->n_enter, sizeof(gw_event), cmp_ev);
-    qsort(s->leave, s->n_leave, sizeof(gw_event), cmp_ev);
+    sort_n(s->enter, s->n_enter, sizeof(gw_event), cmp_ev);
+    sort_n(s->leave, s->n_leave, sizeof(gw_event), cmp_ev);
 }
 
 /* raw stream -> net events by cancellation */
@@ -531,7 +538,7 @@ static int cmp_raw(const void* a, const void* b) {
     return x->key < y->key ? -1 : x->key > y->key;
 }
 static int net_from_raw(orc_space* s) {
-    qsort(s->raw, s->nraw, sizeof(rawev), cmp_raw);
+    sort_n(s->raw, s->nraw, sizeof(rawev), cmp_raw);
     uint64_t cape = 0, capl = 0;
     for (size_t i = 0; i < s->nraw;) {
         size_t j = i; int sum = 0;
@@ -656,7 +663,7 @@ uint64_t orc_collect(orc_space* s) {
         }
     }
     g_sort_gate = s->gate;
-    qsort(s->rec, s->n_rec, sizeof(gw_sync_record), cmp_rec);
+    sort_n(s->rec, s->n_rec, sizeof(gw_sync_record), cmp_rec);
     return s->n_rec;
 }
 void orc_records_copy(const orc_space* s, gw_sync_record* out) {
@@ -705,7 +712,7 @@ uint64_t orc_encode_wire(const orc_space* s, uint8_t* out) {
 static uint32_t copy_sorted(const vec32* v, uint32_t* buf, uint32_t cap) {
     uint32_t* tmp = (uint32_t*)malloc((size_t)(v->n ? v->n : 1) * 4);
     if (v->n) memcpy(tmp, v->a, (size_t)v->n * 4);
-    qsort(tmp, v->n, 4, cmp_u32);
+    sort_n(tmp, v->n, 4, cmp_u32);
     uint32_t k = v->n < cap ? v->n : cap;
     if (buf && k) memcpy(buf, tmp, (size_t)k * 4);
     free(tmp);
@@ -799,7 +806,7 @@ uint64_t orc_fanout(const orc_space* s, const uint32_t* slots, uint32_t n, uint3
     }
     if (out && k) {
         g_fs = s;
-        qsort(out, k, 12, cmp_gate_rec3);
+        sort_n(out, k, 12, cmp_gate_rec3);
     }
     return k;
 }

@@ -764,38 +764,35 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
         for (int u = 0; u < DIFF_U; ++u) {
             if (base + 64u * u >= f.total) break;              // wave-uniform
             const Cand& e = cc[u];
-            bool ev = false, lv = false, nmv = false;
-            bool t_ro = false, t_rn = false, t_cli = false, b_o = false, b_n = false;
-            uint32_t key = 0;
-            if (e.slot != A) {
-                nmv = (e.info & CAND_NONMOVER) != 0;
-                const bool iao = wo.has(e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, me.ox, me.oz);
-                const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, me.x, me.z);
-                bool ro = iao, rn = ian;
-                b_o = iao != ibo;
-                b_n = ian != ibn;
-                if (b_o || b_n) {
-                    const unsigned long long sA = w.rec[A].stamp, soA = w.rec[A].pv.ostamp;
-                    const unsigned long long sb = w.rec[e.slot].stamp;
-                    const unsigned long long sbo = nmv ? sb : w.rec[e.slot].pv.ostamp;
-                    if (b_o) ro = resolve(iao, ibo, soA, sbo);
-                    if (b_n) rn = resolve(ian, ibn, sA, sb);
-                }
-                const bool take = ((e.info & TAG_OLD) && ro) || ((e.info & TAG_NEW) && rn && !ro);
-                if (take) {
-                    t_ro = ro; t_rn = rn;
-                    t_cli = rn && (e.info & CAND_CLIENT) != 0;
-                    ev = ro != rn;
-                    lv = ro;
-                    key = (lv ? 0x80000000u : 0u) | e.slot;      // own events sort as (leave, target)
-                }
+            // branch-free but for the rounding band (rare): the relation,
+            // take / event / count bits as lane values (a branch per test made
+            // the compiler keep every bit as an exec mask: scalar ALU work in
+            // every chunk)
+            const bool iao = wo.has(e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, me.ox, me.oz);
+            const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, me.x, me.z);
+            const bool nmv = (e.info & CAND_NONMOVER) != 0;
+            bool ro = iao, rn = ian;
+            if ((iao != ibo) | (ian != ibn)) {
+                const unsigned long long sA = w.rec[A].stamp, soA = w.rec[A].pv.ostamp;
+                const unsigned long long sb = w.rec[e.slot].stamp;
+                const unsigned long long sbo = nmv ? sb : w.rec[e.slot].pv.ostamp;
+                ro = resolve(iao, ibo, soA, sbo);
+                rn = resolve(ian, ibn, sA, sb);
             }
-            l_old += t_ro ? 1u : 0u;
-            l_new += t_rn ? 1u : 0u;
-            l_cli += t_cli ? 1u : 0u;
+            // the pair is taken at B's old entry when related before, else at its new one
+            const bool take = (e.slot != A) & ((((e.info & TAG_OLD) != 0) & ro) |
+                                               (((e.info & TAG_NEW) != 0) & rn & !ro));
+            const bool t_ro = take & ro, t_rn = take & rn;
+            const bool t_cli = t_rn & ((e.info & CAND_CLIENT) != 0);
+            bool ev = take & (ro != rn);
+            const bool lv = ro;
+            const uint32_t key = (lv ? 0x80000000u : 0u) | e.slot;      // own events sort as (leave, target)
+            l_old += (uint32_t)t_ro;
+            l_new += (uint32_t)t_rn;
+            l_cli += (uint32_t)t_cli;
             // B has no op: (B,A) is B's event too (kept in A's region; the
             // events stage places it)
-            const bool mev = ev && nmv && owned_x(P, e.x);
+            const bool mev = ev & nmv & owned_x(P, e.x);
             // a long mover's pairs: with a short mover B by B's owner (it holds
             // both ends); with another long mover from the long lists (below)
             const bool longB = (e.info & TAG_LONG) != 0;

@@ -175,18 +175,32 @@ __device__ __forceinline__ void flat_map_walk(Flat& f, uint32_t B, uint32_t (&id
     }
 }
 
+// (x, z) inside [lox, hix] x [loz, hiz], exactly: an IEEE difference keeps
+// the sign of the exact one (ties give +0; f32 denormals are not flushed in
+// these kernels), so lo <= x  <=>  lo - x <= 0, and the four comparisons
+// become one: max(lox - x, x - hix, loz - z, z - hiz) <= 0.  One VALU chain
+// and one compare instead of four compares ANDed as lane masks (scalar ALU
+// work in every candidate chunk of the walks).  NaN: an absent entity has
+// both coordinates NaN and an absent centre all four bounds, so every term is
+// NaN, the max is NaN (maxnum drops a NaN only beside a number) and the test
+// is false, as the four comparisons were.
+__device__ __forceinline__ bool box_has(float lox, float hix, float loz, float hiz, float x, float z) {
+    return fmaxf(fmaxf(lox - x, x - hix), fmaxf(loz - z, z - hiz)) <= 0.0f;
+}
+
 // A's rounded window, computed once per watcher
 struct Win {
     float lox, hix, loz, hiz;
-    __device__ bool has(float x, float z) const { return x >= lox && x <= hix && z >= loz && z <= hiz; }
+    __device__ bool has(float x, float z) const { return box_has(lox, hix, loz, hiz, x, z); }
 };
 __device__ __forceinline__ Win win_of(float x, float z, float d) {
     Win w;
     w.lox = x - d; w.hix = x + d; w.loz = z - d; w.hiz = z + d;   // NaN centre -> empty window
     return w;
 }
+// o inside c's window [fl(c-d), fl(c+d)]^2
 __device__ __forceinline__ bool in_win(float cx, float cz, float d, float ox, float oz) {
-    return ox >= cx - d && ox <= cx + d && oz >= cz - d && oz <= cz + d;
+    return box_has(cx - d, cx + d, cz - d, cz + d, ox, oz);
 }
 
 // related(A,B) from A's window test ia and B's window test ib: they agree

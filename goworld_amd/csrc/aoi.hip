@@ -708,7 +708,9 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     const bool longA = LONGS && (me.tags & TAG_LONG) != 0;
     // A's stamps are read only at a boundary tie (rare): loaded up front, the
     // in-order memory counter made every first chunk wait for them too
-    const Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
+    Win wo = win_of(me.ox, me.oz, d), wn = win_of(me.x, me.z, d);
+    wo.to_vgprs();
+    wn.to_vgprs();
     uint32_t* out = b.own + reg;
     uint64_t* mir = b.mir + reg;
     uint32_t n = 0, nm_ = 0;
@@ -717,7 +719,10 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     uint32_t l_old = 0, l_new = 0, l_cli = 0, l_nl = 0, l_nml = 0;
     uint32_t l_lc = 0;      // (LONGS) pairs with another long mover related before or after the tick
     Flat f;
-    if (RR && (uint32_t)__builtin_amdgcn_readfirstlane((int)rr.x) <= (uint32_t)__builtin_amdgcn_readfirstlane((int)rr.y))
+    // the row ranges k_bounds gathered (<= RR_ROWS rows x 2 grids: lanes 0..15)
+    const bool rr_ok =
+        RR && (uint32_t)__builtin_amdgcn_readfirstlane((int)rr.x) <= (uint32_t)__builtin_amdgcn_readfirstlane((int)rr.y);
+    if (rr_ok)
         f = flat_from(rr.x, rr.y - rr.x);
     else
         f = S.flat(P, mover_rects(P, po, me.ox, me.oz, pn, me.x, me.z));
@@ -727,6 +732,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     for (uint32_t base = 0; base < f.total; base += 64u * DIFF_U) {
         uint32_t idx[DIFF_U], kd[DIFF_U];
         if (walk) flat_map_walk<DIFF_U, 2>(f, base, idx, kd);
+        else if (rr_ok) flat_map<DIFF_U, 2, 2 * RR_ROWS>(f, base, idx, kd);
         else flat_map<DIFF_U, 2>(f, base, idx, kd);
         // branch-free candidate loads: every lane reads two 16-B words from its
         // grid's entry (a gn entry twice), lanes past the end read lane 0's, so
@@ -768,16 +774,21 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             // take / event / count bits as lane values (a branch per test made
             // the compiler keep every bit as an exec mask: scalar ALU work in
             // every chunk)
-            const bool iao = wo.has(e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, me.ox, me.oz);
-            const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, me.x, me.z);
+            // A's tests of B; B's tests of A only in the rounding band (Win::eps)
+            bool iao, ian, near_o, near_n;
+            wo.test(e.ox, e.oz, iao, near_o);
+            wn.test(e.x, e.z, ian, near_n);
             const bool nmv = (e.info & CAND_NONMOVER) != 0;
             bool ro = iao, rn = ian;
-            if ((iao != ibo) | (ian != ibn)) {
-                const unsigned long long sA = w.rec[A].stamp, soA = w.rec[A].pv.ostamp;
-                const unsigned long long sb = w.rec[e.slot].stamp;
-                const unsigned long long sbo = nmv ? sb : w.rec[e.slot].pv.ostamp;
-                ro = resolve(iao, ibo, soA, sbo);
-                rn = resolve(ian, ibn, sA, sb);
+            if (near_o | near_n) {
+                const bool ibo = in_win(e.ox, e.oz, d, me.ox, me.oz), ibn = in_win(e.x, e.z, d, me.x, me.z);
+                if ((iao != ibo) | (ian != ibn)) {
+                    const unsigned long long sA = w.rec[A].stamp, soA = w.rec[A].pv.ostamp;
+                    const unsigned long long sb = w.rec[e.slot].stamp;
+                    const unsigned long long sbo = nmv ? sb : w.rec[e.slot].pv.ostamp;
+                    ro = resolve(iao, ibo, soA, sbo);
+                    rn = resolve(ian, ibn, sA, sb);
+                }
             }
             // the pair is taken at B's old entry when related before, else at its new one
             const bool take = (e.slot != A) & ((((e.info & TAG_OLD) != 0) & ro) |

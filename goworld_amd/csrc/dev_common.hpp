@@ -121,12 +121,16 @@ __device__ __forceinline__ Flat flat_from(uint32_t s, uint32_t l) {
 // Maps the lane's candidates k = B + 64u + lane (u < U) to (grid, index);
 // idx = ~0 past the end.  Each lane finds its range by a binary search over
 // the ranges' exclusive prefixes (the largest range j with pre[j] <= k; empty
-// ranges share their successor's prefix and lose the tie), 6 shuffle steps
-// per chunk instead of a serial walk over every live range with readlanes
-// (a VALU cost per range that dominated the walk for short candidate lists).
-template <int U, int NK>
+// ranges share their successor's prefix and lose the tie), log2(SPAN) shuffle
+// steps per chunk instead of a serial walk over every live range with
+// readlanes (a VALU cost per range that dominated the walk for short candidate
+// lists).  SPAN: the ranges live in lanes [0, SPAN) (16 for the row ranges
+// k_bounds hands to k_mover: two fewer dependent shuffles per chunk); the
+// index is then one more shuffle, of start - pre (mod 2^32).
+template <int U, int NK, int SPAN = 64>
 __device__ __forceinline__ void flat_map(Flat& f, uint32_t B, uint32_t (&idx)[U], uint32_t (&kind)[U]) {
     const int ln = lane_id();
+    const uint32_t off = f.start - f.pre;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         idx[u] = ~0u;
@@ -138,14 +142,13 @@ __device__ __forceinline__ void flat_map(Flat& f, uint32_t B, uint32_t (&idx)[U]
         const uint32_t k = B + 64u * u + (uint32_t)ln;
         uint32_t lo = 0;
 #pragma unroll
-        for (int step = 32; step; step >>= 1) {
+        for (int step = SPAN / 2; step; step >>= 1) {
             const uint32_t c = lo + (uint32_t)step;
-            const uint32_t p = (uint32_t)__shfl((int)f.pre, (int)min(c, 63u), 64);
-            if (c < 64u && p <= k) lo = c;
+            const uint32_t p = (uint32_t)__shfl((int)f.pre, (int)(SPAN == 64 ? min(c, 63u) : c), 64);
+            if ((SPAN < 64 || c < 64u) && p <= k) lo = c;
         }
-        const uint32_t ss = (uint32_t)__shfl((int)f.start, (int)lo, 64);
-        const uint32_t sp = (uint32_t)__shfl((int)f.pre, (int)lo, 64);
-        idx[u] = k < f.total ? ss + (k - sp) : ~0u;
+        const uint32_t o = (uint32_t)__shfl((int)off, (int)lo, 64);
+        idx[u] = k < f.total ? o + k : ~0u;
         kind[u] = NK == 2 ? (lo & 1u) : 0u;
     }
 }
@@ -188,14 +191,37 @@ __device__ __forceinline__ bool box_has(float lox, float hix, float loz, float h
     return fmaxf(fmaxf(lox - x, x - hix), fmaxf(loz - z, z - hiz)) <= 0.0f;
 }
 
-// A's rounded window, computed once per watcher
+// Keep a wave-uniform value in a vector register: the walks are short of
+// scalar registers (k_mover_c is capped at 80 for residency), and a spilled
+// scalar is reloaded by a v_readlane in every chunk.  An empty asm with a
+// VGPR constraint: no instruction.
+__device__ __forceinline__ void in_vgpr(float& v) { asm volatile("" : "+v"(v)); }
+
+// A's rounded window, computed once per watcher.  eps bounds the rounding
+// band: B's own window test of A, fl(b -+ d) <= a <= ..., can disagree with
+// A's test of B only where B lies within 2 max(ulp(a -+ d), ulp(b +- d)) of
+// an edge of A's window (the two tests are one exact inequality, each side
+// rounded once), i.e. within 2^-23 (|a| + d) per axis; eps is 8 times that
+// (plus a floor for tiny coordinates), so outside eps of every edge the
+// relation is A's test alone.  NaN centre: empty window, eps NaN (no band).
 struct Win {
-    float lox, hix, loz, hiz;
+    float lox, hix, loz, hiz, eps;
     __device__ bool has(float x, float z) const { return box_has(lox, hix, loz, hiz, x, z); }
+    // has(x, z), and whether (x, z) is within eps of an edge (where the
+    // member with the later op decides the pair)
+    __device__ __forceinline__ void to_vgprs() {
+        in_vgpr(lox); in_vgpr(hix); in_vgpr(loz); in_vgpr(hiz); in_vgpr(eps);
+    }
+    __device__ __forceinline__ void test(float x, float z, bool& in, bool& near) const {
+        const float t0 = lox - x, t1 = x - hix, t2 = loz - z, t3 = z - hiz;
+        in = fmaxf(fmaxf(t0, t1), fmaxf(t2, t3)) <= 0.0f;
+        near = fminf(fminf(fabsf(t0), fabsf(t1)), fminf(fabsf(t2), fabsf(t3))) <= eps;
+    }
 };
 __device__ __forceinline__ Win win_of(float x, float z, float d) {
     Win w;
     w.lox = x - d; w.hix = x + d; w.loz = z - d; w.hiz = z + d;   // NaN centre -> empty window
+    w.eps = (fabsf(x) + fabsf(z) + d) * 0x1p-20f + 0x1p-120f;
     return w;
 }
 // o inside c's window [fl(c-d), fl(c+d)]^2

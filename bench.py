@@ -101,6 +101,10 @@ def parse():
     ap.add_argument("--warmup5", type=int, default=5)
     ap.add_argument("--steps5", type=int, default=10, help="config #5 timed ticks (SURVEY 8(d): 10)")
     ap.add_argument("--device", type=int, default=None, help="force a device (rehearsals on one GPU)")
+    ap.add_argument("--gates", type=int, default=1,
+                    help="config #2/#3: gate processes the clients are spread over (SURVEY 8(d): G = 1 by default, "
+                         "optionally G = 4; goworld_actions.ini deploys 3); the collect then partitions its records "
+                         "by gate (Entity.go:1208-1219)")
     ap.add_argument("--sync-by-client", action="store_true",
                     help="collect grouped per client (GW_SYNC_BY_CLIENT, the gate's regroup on the GPU)")
     ap.add_argument("--client-msgs", type=int, default=5,
@@ -372,6 +376,9 @@ class SpaceRun:
             self.tr = traces.config2(ticks=ticks, seed=2 + ctl.rank)
         else:
             self.tr = traces.config3(ticks=ticks, seed=3 + ctl.rank, n=a.entities, side=a.side)
+        if a.gates > 1:                                 # clients spread round-robin over the gates
+            self.tr.gates = np.where(self.tr.gates > 0, 1 + np.arange(len(self.tr.gates)) % a.gates,
+                                     0).astype(np.uint16)
         if a.capacity:
             self.tr.capacity = max(a.capacity, a.entities)
             self.tr.gates = np.concatenate([self.tr.gates, np.zeros(self.tr.capacity - a.entities, np.uint16)])
@@ -990,7 +997,8 @@ def run(a, ctl):
         "data": f"synthetic (seeded SplitMix64 traces, SURVEY 8(d) config #{cfg_no})",
         "config": {"workload": workload, "world_entities": n_world, "entities_per_gpu": n_world // R,
                    "movers_per_tick_per_gpu": m_rank, "aoi_dist": 100.0,
-                   "world_side": {2: 10240.0, 4: 1024.0, 5: 131072.0}.get(cfg_no, a.side), "gates": 1,
+                   "world_side": {2: 10240.0, 4: 1024.0, 5: 131072.0}.get(cfg_no, a.side),
+                   "gates": a.gates if kind in ("c2", "c3") else 1,
                    "parallelism": parallelism},
         "events_per_sec": res["sum_events"] / mx,
         "records_per_sec": res["sum_records"] / mx,

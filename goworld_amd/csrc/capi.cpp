@@ -1474,10 +1474,19 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     // stage: they run on st2 beside it, and st waits for them before the
     // statistics publish (per-stage profiling keeps one stream)
     const bool ovl = c->overlap && c->pt.on && !c->pt.copied && c->pt.M >= c->overlap_min && c->prof != 1;
+    const bool by_client = (flags & GW_SYNC_BY_CLIENT) != 0;
+    // several gate ids in use: records straight into their gates' partitions
+    // (counts and offsets per (gate, entry), gate-major; sync.hip)
+    static const bool gdirect_on = !getenv("GW_GATE_DIRECT") || atoi(getenv("GW_GATE_DIRECT")) != 0;
+    const bool gdirect = gdirect_on && G > 2 && G <= GATE_DIRECT_MAX && !by_client && !small;
+    const uint64_t NG = gdirect ? (uint64_t)G * NFM : NFM;   // count / offset entries
+    if (gdirect && ((rc = ensure(c, c->rec_cnt, NG * 4)) || (rc = ensure(c, c->rec_off, NG * 8)) ||
+                    (rc = ensure_scan(c, NG))))
+        return rc;
     hipStream_t cs = c->st;
     ScanCtx* csc = &c->sc;
     if (ovl) {
-        if ((rc = ensure_scan2(c, C, c->st2))) return rc;
+        if ((rc = ensure_scan2(c, std::max<uint64_t>(C, NG), c->st2))) return rc;
         HIPCHK(hipStreamWaitEvent(c->st2, c->ev_grid, 0));   // the flags are final after the grid stage
         cs = c->st2;
         csc = &c->sc2;
@@ -1489,15 +1498,20 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     if (ovl) HIPCHK(hipStreamWaitEvent(c->st2, c->ev_diff, 0));   // the counts read the diff's cache
     const uint64_t* nf = (const uint64_t*)&st->flagged;
     prof_begin(c, "sync_count");
-    launch_sync_count(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint32_t>(c->rec_cnt), sfirst,
-                      slast, cs);
-    scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), NFM, nf, *csc,
-                 (uint64_t*)&st->rec_total, cs);
+    if (gdirect) {
+        launch_sync_gates(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, G, P<uint32_t>(c->rec_cnt), cs);
+        scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), NG, nullptr, *csc,
+                     (uint64_t*)&st->rec_total, cs);
+    } else {
+        launch_sync_count(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, P<uint32_t>(c->rec_cnt), sfirst,
+                          slast, cs);
+        scan_u32_u64(P<uint32_t>(c->rec_cnt), P<uint64_t>(c->rec_off), NFM, nf, *csc,
+                     (uint64_t*)&st->rec_total, cs);
+    }
     size_t s_count = prof_end(c, 0);
     // per-client grouping (GW_SYNC_BY_CLIENT): the write pass leaves (watcher,
     // entity) pairs, the sort's keys and values; the records are built once
     // after the sort (not written, keyed, sorted and gathered at 24 B)
-    const bool by_client = (flags & GW_SYNC_BY_CLIENT) != 0;
     const bool pairs = by_client && !small;
     if (pairs && ((rc = ensure(c, c->gk0, c->rec_cap * 8)) || (rc = ensure(c, c->pay, (size_t)NFM * 16))))
         return rc;
@@ -1506,7 +1520,10 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     // flagged entity (config #5: write 1081 -> 852 us; config #3's 146: +4 us)
     const bool sw_halves = c->sw_halves < 0 ? c->rec_per_flagged <= 64.0 : c->sw_halves > 0;
     auto write_pass = [&](hipStream_t ws) {
-        if (small)
+        if (gdirect)
+            launch_sync_write_gates(w, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), nf, NFM, G,
+                                    P<uint64_t>(c->rec_off), P<gw_sync_record>(c->rec0), c->rec_cap, st, ws);
+        else if (small)
             launch_sync_write_small(w, n_sp, P<uint32_t>(c->flagged), P<uint32_t>(c->fbits), P<uint64_t>(c->rec_off),
                                     P<uint32_t>(c->rec_cnt), P<gw_sync_record>(c->rec0), c->rec_cap, st,
                                     sfirst, slast, max_ents, max_cells, ws);
@@ -1541,6 +1558,11 @@ int gw_sync_collect(gw_ctx* c, uint32_t flags, gw_sync_out* out) {
     }
     gw_sync_record* recs = P<gw_sync_record>(c->rec0);
     bool gates_done = false;
+    if (gdirect) {                                       // the partitions' first records came with the sync
+        for (uint32_t g = 0; g < G; ++g) c->gate_off[g] = c->hcstats->gate_base[g];
+        c->gate_off[G] = R;
+        gates_done = true;
+    }
     if (pairs) {
         // (watcher, flagged index) pairs, packed u64, in entity order -> stable
         // sort by watcher -> with several gates in use a stable sort of the

@@ -116,6 +116,10 @@ constexpr int SH_MOVERS = 0;  // distinct slots with an AOI op (k_ops3)
 constexpr int SH_AOLD = 1;    // a_old | a_new << 32 (per-shard sums stay below 2^32)
 
 // Device-side counters of one tick / collect (read back once per call).
+// a collect with at most this many gate ids (0 = no client included) writes
+// each record straight into its gate's partition (count and write passes per
+// (gate, entity); no sort, no second host sync)
+constexpr uint32_t GATE_DIRECT_MAX = 16;
 struct DevStats {
     unsigned long long n_present;     // entities in the grid
     unsigned long long n_movers;      // unused (movers are counted in shard[][SH_MOVERS])
@@ -135,6 +139,7 @@ struct DevStats {
     unsigned long long rec_total;     // sync: records
     unsigned long long n_heavy;       // heavy-first k_mover: primaries with >= heavy_min candidates (heavy[])
     unsigned long long pad_;
+    unsigned long long gate_base[GATE_DIRECT_MAX];   // sync, several gates: first record of gate g (gate_off)
     unsigned long long shard[STAT_SHARDS][SH_FIELDS];   // per-field sums in shard[0] on the host
 };
 
@@ -347,6 +352,14 @@ void launch_flag_compact(uint32_t* flags, uint32_t cap, uint32_t* flagged, uint3
 // sfirst / slast (small-space mode, else null): each space's run of the flagged list
 void launch_sync_count(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, uint32_t* cnt, uint32_t* sfirst, uint32_t* slast, hipStream_t s);
+// several gates (G <= GATE_DIRECT_MAX): counts per (gate, entry), gate-major
+// cnt[g * nf_max + k]; then, after their exclusive scan off, every record at
+// its gate's position (sync.hip)
+void launch_sync_gates(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
+                       uint32_t nf_max, uint32_t G, uint32_t* cnt, hipStream_t s);
+void launch_sync_write_gates(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
+                             uint32_t nf_max, uint32_t G, const uint64_t* off, gw_sync_record* rec, uint64_t rec_cap,
+                             DevStats* st, hipStream_t s);
 void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, const uint64_t* rec_off, const uint32_t* cnt, gw_sync_record* rec,
                        uint64_t rec_cap, DevStats* st, hipStream_t s,

@@ -835,6 +835,116 @@ void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* 
                            rec_cap, st, pr, pay);
 }
 
+// ---------------------------------------------------------------------------
+// Several gates in use (G = max gate id + 1 <= GATE_DIRECT_MAX): the records
+// of each gate form one contiguous partition, in the order of the one-gate
+// stream restricted to that gate (entities ascending, the own record first,
+// then the neighbours in walk order) -- what a stable sort of the stream by
+// gate gives (Entity.go:1208-1219 sends one packet per gate), computed
+// without the sort and without a second host sync:
+//   count: a wave per flagged entry, counts per (gate, entry) in gate-major
+//          cnt[g * nf_max + k] (the diff's cached neighbour counts have no
+//          gates, so every neighbour list is walked, the watcher's gate read
+//          per related candidate with a client);
+//   scan:  one exclusive scan over the G * nf_max counts gives every (gate,
+//          entry) its first record, and gate g's first record at g * nf_max;
+//   write: a wave per entry holds the next position of each gate in lanes
+//          0..G-1 and stores each record at its gate's position (ranks inside
+//          a chunk by one ballot per gate); the gates' first records go to
+//          DevStats.gate_base, read with the collect's one host sync.
+template <int U>
+__global__ void __launch_bounds__(NT) k_sync_count_g(World w, const uint32_t* __restrict__ flagged,
+                                                     const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
+                                                     uint32_t nf_max, uint32_t G, uint32_t* __restrict__ cnt) {
+    const uint64_t nf = load_n(nf_max, nf_dev);
+    const int ln = lane_id();
+    const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
+    for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+         k < nf_max; k += stride) {
+        uint32_t c = 0;                                   // lane g: records of gate g
+        if (k < nf) {
+            const uint32_t e = flagged[k], f = fbits[k];
+            const AoiEnt a = w.rec[e].a;
+            const uint32_t gt = w.gate[e];
+            const SpaceP P = w.sp[a.meta & SPACE_MASK];
+            if (owned_x(P, a.x)) {
+                if ((f & GW_SIF_OWN_CLIENT) && gt && (uint32_t)ln == gt) c = 1;
+                if ((f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
+                    wave_neighbors_of<U>(w, e, a, P, [&](bool rel, uint32_t ws, uint32_t g) {
+                        const uint32_t gw = (rel && g != 0) ? (uint32_t)w.gate[ws] : 0u;   // 0: no record
+                        for (uint32_t q = 1; q < G; ++q) {
+                            const uint32_t n = (uint32_t)popc64(wave_ballot(gw == q));
+                            if ((uint32_t)ln == q) c += n;
+                        }
+                    });
+                }
+            }
+        }
+        if ((uint32_t)ln < G) cnt[(uint64_t)ln * nf_max + k] = c;   // gate 0 (no client): always 0
+    }
+}
+
+template <int U>
+__global__ void __launch_bounds__(NT) k_sync_write_g(World w, const uint32_t* __restrict__ flagged,
+                                                     const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
+                                                     uint32_t nf_max, uint32_t G, const uint64_t* __restrict__ off,
+                                                     gw_sync_record* rec, uint64_t rec_cap, DevStats* st) {
+    const uint64_t nf = load_n(nf_max, nf_dev);
+    const int ln = lane_id();
+    const uint64_t lt = lanemask_lt();
+    if (st->rec_total > rec_cap) {                        // kernel-uniform: the host grows the buffer, reruns
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&st->overflow, 1ull);
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < G) st->gate_base[threadIdx.x] = off[(uint64_t)threadIdx.x * nf_max];
+    const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
+    for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+         k < nf; k += stride) {
+        const uint32_t e = flagged[k], f = fbits[k];
+        const AoiEnt a = w.rec[e].a;
+        const uint32_t gt = w.gate[e];
+        const SpaceP P = w.sp[a.meta & SPACE_MASK];
+        if (!owned_x(P, a.x)) continue;
+        const float4 p = w.rec[e].p;
+        uint64_t at = (uint32_t)ln < G ? off[(uint64_t)ln * nf_max + k] : 0ull;   // lane g: gate g's next record
+        if ((f & GW_SIF_OWN_CLIENT) && gt) {
+            const uint64_t o = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(at >> 32), (int)gt) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)at, (int)gt);
+            if (ln == 0) st_record_nt(rec + o, e, e, p);
+            if ((uint32_t)ln == gt) ++at;
+        }
+        if (!(f & GW_SIF_NEIGHBOR_CLIENTS) || !(a.meta & PRESENT_BIT)) continue;
+        wave_neighbors_of<U>(w, e, a, P, [&](bool rel, uint32_t ws, uint32_t g) {
+            const uint32_t gw = (rel && g != 0) ? (uint32_t)w.gate[ws] : 0u;
+            uint64_t pos = 0;
+            for (uint32_t q = 1; q < G; ++q) {
+                const uint64_t bq = wave_ballot(gw == q);
+                if (!bq) continue;                        // wave-uniform
+                const uint64_t o = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(at >> 32), (int)q) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)at, (int)q);
+                if (gw == q) pos = o + (uint64_t)popc64(bq & lt);
+                if ((uint32_t)ln == q) at += (uint64_t)popc64(bq);
+            }
+            if (gw != 0) st_record_nt(rec + pos, ws, e, p);
+        });
+    }
+}
+
+void launch_sync_gates(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
+                       uint32_t nf_max, uint32_t G, uint32_t* cnt, hipStream_t s) {
+    if (!nf_max) return;
+    const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
+    hipLaunchKernelGGL(k_sync_count_g<4>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, G, cnt);
+}
+void launch_sync_write_gates(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
+                             uint32_t nf_max, uint32_t G, const uint64_t* off, gw_sync_record* rec, uint64_t rec_cap,
+                             DevStats* st, hipStream_t s) {
+    if (!nf_max) return;
+    const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
+    hipLaunchKernelGGL(k_sync_write_g<4>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, G, off, rec, rec_cap,
+                       st);
+}
+
 // 24-B records from sorted (watcher, entity) pairs (through idx, the gate
 // grouping's permutation, when given; the entity's payload from its slot)
 // and, in the same pass, the client segment table of the stream (what

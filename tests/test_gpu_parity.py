@@ -627,3 +627,24 @@ def test_client_paths_wide_slot_keys(ctx_factory, pad):
         n_fo += len(f.records)
         n_rec += len(r.records)
     assert n_fo > 1000 and n_rec > 10_000
+
+
+@pytest.mark.parametrize("ngates", [3, 15, 20])
+def test_multi_gate_partitions(ctx_factory, ngates):
+    """Clients spread over several gates (Entity.go:1208-1219 sends one packet
+    per gate): the records come grouped by gate, inside a gate in the one-gate
+    stream's order, with gate_off partitioning them.  Up to GATE_DIRECT_MAX gate
+    ids (3 and 15 gates + "no client") the count and write passes place every
+    record straight into its gate's partition; 20 gates take the stable sort by
+    gate.  Exact stream order against the oracle."""
+    tr = T.config2(ticks=3, n=20_000)
+    cap = tr.capacity
+    tr.gates = np.where(np.arange(cap) % 11 == 10, 0, 1 + np.arange(cap) % ngates).astype(np.uint16)
+    h = Harness(ctx_factory(), [tr])
+    r = h.check_collect()
+    assert len(r.gate_off) == ngates + 2
+    for t in range(len(tr.ticks)):
+        h.step(t)
+        r = h.check_collect()
+        assert int(r.gate_off[1]) == 0                   # gate 0 (no client) holds no record
+        assert np.all(np.diff(r.gate_off[1:].astype(np.int64)) > 0)   # every gate has records

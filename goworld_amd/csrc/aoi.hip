@@ -1002,6 +1002,8 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     uint64_t* mir = b.mir + reg;
     uint32_t n = 0, nl = 0, nm_ = 0, nml = 0;
     uint32_t c_old = 0, c_new = 0, c_cli = 0;
+    uint64_t l_on = 0, l_cl = 0;      // per lane: old | new << 32, client | own leaves << 32
+    uint32_t l_ml = 0;                // per lane: mirror leaves
     // the half's first candidate (its first non-empty range): what a lane past
     // the half's end reads
     const uint32_t f_lane = (uint32_t)__builtin_ctzll((wave_ballot(rl != 0) & hmask) | (1ull << 63));
@@ -1059,40 +1061,38 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
         for (int u = 0; u < HU; ++u) {
             if (base + 32u * u >= tmax) break;               // wave-uniform
             const Cand& e = cc[u];
-            bool ev = false, lv = false, nmv = false;
-            bool t_ro = false, t_rn = false, t_cli = false, b_o = false, b_n = false;
-            uint32_t key = 0;
-            if (go && e.slot != A) {
-                nmv = (e.info & CAND_NONMOVER) != 0;
-                const bool iao = wo.has(e.ox, e.oz), ibo = in_win(e.ox, e.oz, d, me.ox, me.oz);
-                const bool ian = wn.has(e.x, e.z), ibn = in_win(e.x, e.z, d, me.x, me.z);
-                bool ro = iao, rn = ian;
-                b_o = iao != ibo;
-                b_n = ian != ibn;
-                if (b_o || b_n) {
+            // as mover_one: branch-free but for the rounding band (Win::eps),
+            // counts per lane, summed per half after the walk
+            bool iao, ian, near_o, near_n;
+            wo.test(e.ox, e.oz, iao, near_o);
+            wn.test(e.x, e.z, ian, near_n);
+            const bool nmv = (e.info & CAND_NONMOVER) != 0;
+            bool ro = iao, rn = ian;
+            if (near_o | near_n) {
+                const bool ibo = in_win(e.ox, e.oz, d, me.ox, me.oz), ibn = in_win(e.x, e.z, d, me.x, me.z);
+                if ((iao != ibo) | (ian != ibn)) {
                     const unsigned long long sA = w.rec[A].stamp, soA = w.rec[A].pv.ostamp;
                     const unsigned long long sb = w.rec[e.slot].stamp;
                     const unsigned long long sbo = nmv ? sb : w.rec[e.slot].pv.ostamp;
-                    if (b_o) ro = resolve(iao, ibo, soA, sbo);
-                    if (b_n) rn = resolve(ian, ibn, sA, sb);
-                }
-                const bool take = ((e.info & TAG_OLD) && ro) || ((e.info & TAG_NEW) && rn && !ro);
-                if (take) {
-                    t_ro = ro; t_rn = rn;
-                    t_cli = rn && (e.info & CAND_CLIENT) != 0;
-                    ev = ro != rn;
-                    lv = ro;
-                    key = (lv ? 0x80000000u : 0u) | e.slot;
+                    ro = resolve(iao, ibo, soA, sbo);
+                    rn = resolve(ian, ibn, sA, sb);
                 }
             }
-            c_old += (uint32_t)popc64(wave_ballot(t_ro) & hmask);
-            c_new += (uint32_t)popc64(wave_ballot(t_rn) & hmask);
-            c_cli += (uint32_t)popc64(wave_ballot(t_cli) & hmask);
-            const bool mev = ev && nmv && owned_x(P, e.x);
+            const bool take = go & (e.slot != A) & ((((e.info & TAG_OLD) != 0) & ro) |
+                                                    (((e.info & TAG_NEW) != 0) & rn & !ro));
+            const bool t_ro = take & ro, t_rn = take & rn;
+            const bool t_cli = t_rn & ((e.info & CAND_CLIENT) != 0);
+            bool ev = take & (ro != rn);
+            const bool lv = ro;
+            const uint32_t key = (lv ? 0x80000000u : 0u) | e.slot;
+            l_on += (uint64_t)t_ro | ((uint64_t)t_rn << 32);
+            const bool mev = ev & nmv & owned_x(P, e.x);
             const bool longB = (e.info & TAG_LONG) != 0;
             // (long movers never come here: k_mover_pair runs them through mover_one)
             ev = ev && (longA ? !longB && owned_x(P, e.x == e.x ? e.x : e.ox) : ownA);
-            const uint64_t be = wave_ballot(ev) & hmask, bl = wave_ballot(ev && lv) & hmask;
+            l_cl += (uint64_t)t_cli | ((uint64_t)(ev & lv) << 32);
+            l_ml += (uint32_t)(mev & lv);
+            const uint64_t be = wave_ballot(ev) & hmask;
             const uint64_t bm = wave_ballot(mev) & hmask;
             const uint32_t at = n + (uint32_t)popc64(be & lt);
             if (ev && at < 32u) L[hb + at] = key;
@@ -1100,10 +1100,29 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
             const uint32_t atm = nm_ + (uint32_t)popc64(bm & lt);
             if (mev && atm < cap && reg + cap <= own_cap) mir[atm] = ((uint64_t)e.slot << 32) | (A << 1) | (lv ? 1u : 0u);
             n += (uint32_t)popc64(be);
-            nl += (uint32_t)popc64(bl);
             nm_ += (uint32_t)popc64(bm);
-            nml += (uint32_t)popc64(wave_ballot(mev && lv) & hmask);
         }
+    }
+    // the halves' sums of the per-lane counts: lane 31 (half 0), lane 63 - lane 31 (half 1)
+    {
+        const uint64_t s_on = wave_incl_scan<unsigned long long>(l_on);
+        const uint64_t s_cl = wave_incl_scan<unsigned long long>(l_cl);
+        const uint32_t s_ml = wave_incl_scan<uint32_t>(l_ml);
+        auto half_sum64 = [&](uint64_t v) {
+            const uint64_t lo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), 31) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 31);
+            const uint64_t hi = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), 63) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+            return half ? hi - lo : lo;
+        };
+        const uint64_t on = half_sum64(s_on), cl = half_sum64(s_cl);
+        const uint32_t ml_lo = (uint32_t)__builtin_amdgcn_readlane((int)s_ml, 31);
+        const uint32_t ml_hi = (uint32_t)__builtin_amdgcn_readlane((int)s_ml, 63);
+        c_old = (uint32_t)on;
+        c_new = (uint32_t)(on >> 32);
+        c_cli = (uint32_t)cl;
+        nl = (uint32_t)(cl >> 32);
+        nml = half ? ml_hi - ml_lo : ml_lo;
     }
     // own events by (leave, target): <= 32 in registers inside the half, more
     // by the block sort (the first 32 written out of L unsorted)

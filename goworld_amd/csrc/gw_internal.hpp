@@ -57,7 +57,7 @@ static_assert(sizeof(SlotRec) == 64, "SlotRec is one 64-B line");
 // session reads as -1 (ol_get), so nothing is reset between ticks.
 struct alignas(64) OpLast {
     unsigned long long pos, aoi, leave, clr[2];
-    unsigned long long rb[2];   // routing (halo.hip r2): sync bit c set since the last Leave clearing it (tag only)
+    unsigned long long rb[2];   // routing (halo.hip): the last non-Leave op setting sync bit c
     unsigned long long pad;
 };
 __device__ __forceinline__ unsigned long long ol_put(uint32_t tag, uint32_t i) {

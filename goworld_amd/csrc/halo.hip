@@ -8,9 +8,10 @@
 //   r1  last AOI op / last payload op / last Leave per slot (u64 atomicMax
 //       into the session-tagged OpLast words, exactly k_ops1 of the tick,
 //       which reuses them); the ops' stamps in the world path
-//   r2  the sync bits of the ops after the last Leave clearing each bit (a
-//       Leave's sync_flags is the mask of bits it keeps, as in the tick),
-//       one session-tagged word per bit in the same record
+//   r2  the fix-up of r1's plain stores where a slot has several ops; r1
+//       also keeps, per sync bit, the last non-Leave op setting it (r3 compares
+//       it with the last Leave clearing the bit: a Leave's sync_flags is the
+//       mask of bits it keeps, as in the tick)
 //   r3  the entity's last op writes up to 3 rows per destination, entities
 //       placed by one wave-aggregated atomic per wave and destination
 //   r4  (fixed-size buffers only) zero (NOP) rows past the entities placed
@@ -44,25 +45,47 @@ __global__ void __launch_bounds__(NT) k_route1(const gw_op* __restrict__ ops, ui
         atomicAdd(&hs->bad_ops, 1ull);
         return;
     }
+    // plain stores of the tagged index (as k_ops1): the fix-up in k_route2
+    // takes the maximum only where a slot has several ops (device-scope
+    // atomics run memory-side: one per word and op cost the pass its latency)
     const unsigned long long v = ol_put(tag, i);
-    if (op.kind != GW_OP_LEAVE) atomicMax(&ol[op.slot].pos, v);
-    if (op.kind != GW_OP_SYNC) atomicMax(&ol[op.slot].aoi, v);
+    OpLast& o = ol[op.slot];
+    if (op.kind != GW_OP_LEAVE) {
+        o.pos = v;
+        for (int c = 0; c < 2; ++c)                  // the last op setting bit c (rb[c], compared with clr[c])
+            if ((op.sync_flags >> c) & 1) o.rb[c] = v;
+    }
+    if (op.kind != GW_OP_SYNC) o.aoi = v;
     if (op.kind == GW_OP_LEAVE) {
-        atomicMax(&ol[op.slot].leave, v);
+        o.leave = v;
         for (int c = 0; c < 2; ++c)
-            if (!((op.sync_flags >> c) & 1)) atomicMax(&ol[op.slot].clr[c], v);
+            if (!((op.sync_flags >> c) & 1)) o.clr[c] = v;
     }
 }
 
+// the fix-up: an op whose index is above the stored one takes the maximum
+// (only where a slot had several ops this call)
 __global__ void __launch_bounds__(NT) k_route2(const gw_op* __restrict__ ops, uint32_t n, uint32_t cap,
                                                 OpLast* ol, uint32_t tag) {
     const uint32_t i = blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
     const gw_op op = ops[i];
-    if (!op_valid(op, cap) || op.kind == GW_OP_LEAVE || !(op.sync_flags & SIF_ROUTED)) return;
-    for (int c = 0; c < 2; ++c)                      // every writer stores the same word: no atomic
-        if (((op.sync_flags >> c) & 1) && (int32_t)i > ol_get(ol[op.slot].clr[c], tag))
-            ol[op.slot].rb[c] = ol_put(tag, 1);
+    if (op.kind == GW_OP_NOP || !op_valid(op, cap)) return;
+    const unsigned long long v = ol_put(tag, i);
+    OpLast& w = ol[op.slot];
+    const OpLast o = w;
+    const int32_t me = (int32_t)i;
+    if (op.kind != GW_OP_LEAVE) {
+        if (ol_get(o.pos, tag) < me) atomicMax(&w.pos, v);
+        for (int c = 0; c < 2; ++c)
+            if (((op.sync_flags >> c) & 1) && ol_get(o.rb[c], tag) < me) atomicMax(&w.rb[c], v);
+    }
+    if (op.kind != GW_OP_SYNC && ol_get(o.aoi, tag) < me) atomicMax(&w.aoi, v);
+    if (op.kind == GW_OP_LEAVE) {
+        if (ol_get(o.leave, tag) < me) atomicMax(&w.leave, v);
+        for (int c = 0; c < 2; ++c)
+            if (!((op.sync_flags >> c) & 1) && ol_get(o.clr[c], tag) < me) atomicMax(&w.clr[c], v);
+    }
 }
 
 __device__ __forceinline__ gw_op mk_op(uint8_t kind, uint8_t flags, uint32_t slot, const gw_op* payload,
@@ -164,8 +187,9 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
         // did not clear, OR'd with the bits set since the Leave that cleared them
         uint32_t keep = 0, rbits = 0;
         for (int c = 0; c < 2; ++c) {
-            if (ol_get(ol[s].clr[c], tag) < 0) keep |= 1u << c;
-            if (ol_get(ol[s].rb[c], tag) >= 0) rbits |= 1u << c;
+            const int32_t lc = ol_get(ol[s].clr[c], tag);
+            if (lc < 0) keep |= 1u << c;
+            if (ol_get(ol[s].rb[c], tag) > lc) rbits |= 1u << c;   // bit c set after the last Leave clearing it
         }
         f = ((flag_get(w.flags, s) & keep) | rbits) & SIF_ROUTED;
     }

@@ -959,7 +959,7 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     // (no loop over R.r[q]: a dynamically indexed Rects lives in scratch)
     const int nr0 = R.n > 0 ? R.r[0].z1 - R.r[0].z0 + 1 : 0;
     const int nr1 = R.n > 1 ? R.r[1].z1 - R.r[1].z0 + 1 : 0;
-    if (wave_ballot(nr0 + nr1 > 16)) return false;         // wave-uniform
+    if (wave_ballot(nr0 + nr1 > (int)b.half_rows)) return false;   // wave-uniform (<= 16 rows: one half's lanes)
     const World& w = b.w;
     // the HBM reads of this pair (region) are first needed at the first
     // write: the row ranges and candidates (LDS) go first; stamps only at a
@@ -1204,16 +1204,21 @@ __global__ void __launch_bounds__(64) k_mover_pair(TickBufs b) {
 constexpr uint32_t SMALL_SORT = 256;    // own events sorted in LDS up to this many (more: block sort)
 constexpr uint32_t SMALL_GM = 256;      // mover-grid entries of a space staged in LDS (more: read from HBM)
 
-template <int DIFF_U>
+template <int DIFF_U, bool HALVES>
 __device__ __forceinline__ void small_walk(const TickBufs& b, uint32_t m0, uint32_t m1, const SpaceP& P,
                                            const GlobalSrc& src, uint32_t* lds) {
-    if (b.small_halves) {
+    if (HALVES) {
+        // a pair the half-wave walk cannot take (a window of more rows than a
+        // half holds) goes to k_mover_list, one wave per entry from the global
+        // grids: with no mover_one inlined here the kernel fits 96 VGPRs, 5
+        // waves per SIMD instead of 4 (128 VGPRs)
         uint32_t* L = lds + (threadIdx.x >> 6) * SMALL_SORT;
         for (uint32_t m = m0 + (threadIdx.x >> 6) * 2; m < m1; m += NWAVE * 2) {
-            if (!mover_half<3>(b, m, m1, P, src.GN, src.GS, src.MS, src.GM, L)) {
-                mover_one<DIFF_U, SMALL_SORT>(b, m, lds, src);
-                wave_sync();
-                if (m + 1 < m1) mover_one<DIFF_U, SMALL_SORT>(b, m + 1, lds, src);
+            if (!mover_half<2>(b, m, m1, P, src.GN, src.GS, src.MS, src.GM, L) && lane_id() == 0) {
+                const uint32_t k = m + 1 < m1 ? 2u : 1u;
+                const uint32_t at = (uint32_t)atomicAdd(&b.st->n_fall, (unsigned long long)k);
+                b.fall[at] = m;
+                if (k == 2) b.fall[at + 1] = m + 1;
             }
             wave_sync();
         }
@@ -1225,14 +1230,18 @@ __device__ __forceinline__ void small_walk(const TickBufs& b, uint32_t m0, uint3
     }
 }
 
-template <int DIFF_U>
 // (GW_MS_MINB: blocks per CU the register allocation must allow; 4 caps the
 // VGPRs at 128: 4 waves per SIMD instead of 3 at 129, as LDS allows 5 blocks;
-// config #4 diff 854 -> 711 us)
+// config #4 diff 854 -> 711 us.  The half-wave kernel without mover_one fits
+// 96 at 5.)
 #ifndef GW_MS_MINB
 #define GW_MS_MINB 4
 #endif
-__global__ void __launch_bounds__(NT, GW_MS_MINB) k_mover_small(TickBufs b) {
+#ifndef GW_MSH_MINB
+#define GW_MSH_MINB 5
+#endif
+template <int DIFF_U, bool HALVES>
+__global__ void __launch_bounds__(NT, HALVES ? GW_MSH_MINB : GW_MS_MINB) k_mover_small(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[NWAVE * SMALL_SORT];
     extern __shared__ uint4 dyn_lds[];
     const uint32_t s = blockIdx.x;
@@ -1256,8 +1265,20 @@ __global__ void __launch_bounds__(NT, GW_MS_MINB) k_mover_small(TickBufs b) {
         for (uint32_t i = threadIdx.x; i < m1 - m0; i += NT) GL[i] = b.gm[m0 + i];
     __syncthreads();
     // every mover's own entry and its mover-grid candidates from LDS when staged
-    if (stage) small_walk<DIFF_U>(b, m0, m1, P, GlobalSrc{G - g0, S - cb, MS - cb, GL - m0}, lds);
-    else small_walk<DIFF_U>(b, m0, m1, P, GlobalSrc{G - g0, S - cb, MS - cb, b.gm}, lds);
+    if (stage) small_walk<DIFF_U, HALVES>(b, m0, m1, P, GlobalSrc{G - g0, S - cb, MS - cb, GL - m0}, lds);
+    else small_walk<DIFF_U, HALVES>(b, m0, m1, P, GlobalSrc{G - g0, S - cb, MS - cb, b.gm}, lds);
+}
+
+// the entries k_mover_small's half-wave walk left (fall[], n_fall on the
+// device): one wave each, candidates from the global grids
+template <int DIFF_U>
+__global__ void __launch_bounds__(64) k_mover_list(TickBufs b) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[SORT_LDS];
+    const uint64_t nf = b.st->n_fall;
+    for (uint64_t k = blockIdx.x; k < nf; k += gridDim.x) {
+        mover_one<DIFF_U, SORT_LDS>(b, b.fall[k], lds, GlobalSrc{b.w.gn, b.w.gn_start, b.gm_start, b.gm});
+        wave_sync();
+    }
 }
 
 // A_old | A_new << 32 of every mover-grid entry, one shard per
@@ -2020,7 +2041,12 @@ void tick_diff(const TickBufs& b, hipStream_t s) {
     if (b.small_ents) {                    // small-space mode: a block per space
         const size_t lds = ((size_t)b.small_ents + (2 * ((size_t)b.small_cells + 1) + 3) / 4) * 16 +
                            (size_t)SMALL_GM * sizeof(MEnt);
-        hipLaunchKernelGGL((k_mover_small<2>), dim3(b.n_spaces), dim3(NT), lds, s, b);
+        if (b.small_halves) {
+            hipLaunchKernelGGL((k_mover_small<2, true>), dim3(b.n_spaces), dim3(NT), lds, s, b);
+            hipLaunchKernelGGL((k_mover_list<2>), dim3(std::min<uint32_t>(nblk1(nmax, 1), 1024)), dim3(64), 0, s, b);
+        } else {
+            hipLaunchKernelGGL((k_mover_small<2, false>), dim3(b.n_spaces), dim3(NT), lds, s, b);
+        }
         return;
     }
     if (b.pair_max) {                      // two short-list movers per wave (GW_PAIR_MAX, 0 = off)

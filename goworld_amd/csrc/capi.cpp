@@ -563,6 +563,7 @@ int gw_init(int device_id, gw_ctx** out) {
         if (const char* e = getenv("GW_HEAVY_MIN")) c->heavy_min = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_HEAVY_MAXM")) c->heavy_maxm = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_DIRTY_SPAN")) c->dirty_span = (uint32_t)std::min(64, std::max(1, atoi(e)));
+        if (const char* e = getenv("GW_HALF_ROWS")) c->half_rows = (uint32_t)std::min(16, std::max(0, atoi(e)));
     } while (0);
     if (rc) {
         (void)hipGetLastError();
@@ -1296,6 +1297,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
         (rc = ensure(c, c->mcell, (size_t)M * 16)) ||
         (rc = ensure(c, c->cand, M2 * 8)) || (rc = ensure(c, c->reg, M2 * 8)) ||
         (rc = ensure(c, c->ownc, M2 * 8)) || (rc = ensure(c, c->mirc, M2 * 8)) || (rc = ensure(c, c->big, M2 * 4)) ||
+        (rc = ensure(c, c->fall, M2 * 4)) ||
         (rc = ensure(c, c->mstat, M2 * 8)) || (rc = ensure(c, c->pidx, (size_t)M * 4)) ||
         (rc = ensure(c, c->heavy, (size_t)M * 4)) ||
         (rc = ensure(c, c->mlist, (size_t)M * 4)) || (rc = ensure(c, c->mcnt, (size_t)M * 8)) ||
@@ -1360,6 +1362,8 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.cand = P<uint64_t>(c->cand); b.reg = P<uint64_t>(c->reg); b.pidx = P<uint32_t>(c->pidx);
     b.ownc = P<unsigned long long>(c->ownc); b.mirc = P<unsigned long long>(c->mirc);
     b.big = P<uint32_t>(c->big);
+    b.fall = P<uint32_t>(c->fall);
+    b.half_rows = c->half_rows;
     b.mstat = P<unsigned long long>(c->mstat);
     b.movbit = c->movbit; b.gmi = c->gmi;
     b.mlist = P<uint32_t>(c->mlist);

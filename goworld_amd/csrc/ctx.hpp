@@ -207,7 +207,7 @@ struct gw_ctx {
     gw_tick_out last_out{};
 
     // grid + tick scratch
-    DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, mtmp, mcell, cand, reg, pidx, heavy, rowrec, own, big, mstat;
+    DevBuf ops_buf, stamp_buf, k0, v0, k1, v1, gm, mtmp, mcell, cand, reg, pidx, heavy, rowrec, own, big, fall, mstat;
     DevBuf mir, ownc, mirc, mlist, mcnt, moff, minfo, icnt, ioff, mreg, chunk_first, srange, bk_a, bk_b, bk_id, bk_cnt, bk_split, ev_d, rtable;
     DevBuf scan_status, scan_status2, rs_hist, rs_os;   // rs_os: the one-kernel-per-pass sort's scratch (sort_u32_u32)
     uint32_t walk_min = 32;              // GW_WALK_MIN: TickBufs.walk_min (0: always walk)
@@ -221,6 +221,7 @@ struct gw_ctx {
     // merges fewer dirty cells in a row: config #3 grid 63 -> 58 us), 16 above (fewer idle waves:
     // config #4's 4.4M cells at 4 per wave cost +50 us)
     uint32_t dirty_span = 0;
+    uint32_t half_rows = 16;             // GW_HALF_ROWS: TickBufs.half_rows (tests of the fallback paths)
     // GW_PAIR_MAX: TickBufs.pair_max.  Unset: automatic, PAIR_AUTO when the last
     // tick had >= PAIR_MOVERS movers averaging <= PAIR_MEAN candidates (many
     // uniform short lists: config #5 diff 1677 -> 1573 us), else 0 (hotspots:

@@ -138,7 +138,7 @@ struct DevStats {
     unsigned long long flagged;       // sync: flagged entities
     unsigned long long rec_total;     // sync: records
     unsigned long long n_heavy;       // heavy-first k_mover: primaries with >= heavy_min candidates (heavy[])
-    unsigned long long pad_;
+    unsigned long long n_fall;        // small-space diff: mover-grid entries left to k_mover_list (fall[])
     unsigned long long gate_base[GATE_DIRECT_MAX];   // sync, several gates: first record of gate g (gate_off)
     unsigned long long shard[STAT_SHARDS][SH_FIELDS];   // per-field sums in shard[0] on the host
 };
@@ -242,6 +242,7 @@ struct TickBufs {
     unsigned long long* mirc; // [2m] mirror enters | leaves<<32 per entry
     unsigned long long* mstat;   // [2m] A_old | A_new << 32 per entry (k_mover -> k_mover_post)
     uint32_t* big;            // [2m] entries whose own events need the block sort
+    uint32_t* fall;           // [2m] small-space mode: entries the half-wave walk could not take (k_mover_list)
     // canonical events: movers in slot order, their events flattened, one
     // stable radix sort by (leave, watcher) -> (watcher, target) order
     uint32_t* movbit;         // [cap/32 + 1] movers, zero between ticks
@@ -285,6 +286,8 @@ struct TickBufs {
     uint32_t small_ents;      // small-space mode: max entries per space (0: off)
     uint32_t small_cells;     //   and max cells per space
     int small_halves;         //   two movers per wave (GW_MOVER_HALVES, default on)
+    uint32_t half_rows;       //   rows a half-wave walk takes (16; GW_HALF_ROWS lowers it in tests: more
+                              //   pairs left to mover_one / k_mover_list)
     int diff_u;               // candidate chunks of 64 in flight per k_mover iteration
     uint32_t walk_min;        // mean candidates per row range from which a walk maps chunks by readlanes
     uint32_t rank_sort;       // own events sorted by rank (readlanes) up to this many, more by a network

@@ -180,3 +180,25 @@ def test_mover_pairing_modes(gpu, pair_max, monkeypatch):
         r = g.sync_collect()
         assert G.sha(canonical(r.records, tr.gates)) == exp["rec_sha"], f"tick {t}: records"
     g.close()
+
+
+def test_pair_mode_fallback_digests(gpu, monkeypatch):
+    """The paired diff (k_mover_pair, GW_PAIR_MAX) with GW_HALF_ROWS=0: every
+    pair falls back to one mover_one walk per entry; config #2 digests."""
+    monkeypatch.setenv("GW_PAIR_MAX", "96")
+    monkeypatch.setenv("GW_HALF_ROWS", "0")
+    name = "config2_100k"
+    d = G.digests()[name]
+    tr = G.DIGEST_TRACES[name]()
+    g = gpu()
+    monkeypatch.delenv("GW_PAIR_MAX")
+    monkeypatch.delenv("GW_HALF_ROWS")
+    gpuaoi.load_space(g, tr)
+    for t, ops in enumerate(tr.ticks):
+        exp = d["ticks"][t]
+        g.submit(ops)
+        res = g.tick()
+        assert G.sha(res.enter) == exp["enter_sha"] and G.sha(res.leave) == exp["leave_sha"], f"tick {t}"
+        r = g.sync_collect()
+        assert G.sha(canonical(r.records, tr.gates)) == exp["rec_sha"], f"tick {t}: records"
+    g.close()

@@ -648,3 +648,25 @@ def test_multi_gate_partitions(ctx_factory, ngates):
         r = h.check_collect()
         assert int(r.gate_off[1]) == 0                   # gate 0 (no client) holds no record
         assert np.all(np.diff(r.gate_off[1:].astype(np.int64)) > 0)   # every gate has records
+
+
+@pytest.mark.parametrize("half_rows", [0, 4])
+def test_half_wave_walk_fallbacks(ctx_factory, half_rows, monkeypatch):
+    """Small-space mode walks movers two per wave (a half-wave each) when both
+    windows fit a half's row lanes; other pairs go to k_mover_list (one wave
+    per entry from the global grids).  GW_HALF_ROWS lowers the row limit so
+    that every pair (0) or the pairs with windows of more than 4 rows take the
+    fallback: events, records and neighbour lists stay exact against the
+    oracle over 40 small spaces with 3 gates."""
+    monkeypatch.setenv("GW_HALF_ROWS", str(half_rows))
+    g = ctx_factory()                                   # gw_init reads GW_HALF_ROWS
+    monkeypatch.delenv("GW_HALF_ROWS")
+    trs = [T.config4_space(s, ticks=3, n=300) for s in range(40)]
+    for i, tr in enumerate(trs):
+        tr.gates = np.where(tr.gates > 0, 1 + (i % 3), 0).astype(np.uint16)
+    h = Harness(g, trs)
+    h.check_collect()
+    for t in range(3):
+        h.step(t)
+        h.check_collect()
+    h.check_lists()

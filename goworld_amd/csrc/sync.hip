@@ -43,11 +43,15 @@ __device__ __forceinline__ void wave_neighbors_of(const World& w, uint32_t e, co
             bool rel = false;
             const GEnt g = gg[u];
             if (g.slot != e) {
-                const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
+                bool ia, near;
+                we.test(g.x, g.z, ia, near);              // B's test of A only in the rounding band
                 rel = ia;
-                if (ia != ib) {
-                    if (!have_se) { se = w.rec[e].stamp; have_se = true; }
-                    rel = resolve(ia, ib, se, w.rec[g.slot].stamp);
+                if (near) {
+                    const bool ib = in_win(g.x, g.z, d, a.x, a.z);
+                    if (ia != ib) {
+                        if (!have_se) { se = w.rec[e].stamp; have_se = true; }
+                        rel = resolve(ia, ib, se, w.rec[g.slot].stamp);
+                    }
                 }
             }
             f(rel, g.slot, (g.meta & CLIENT_BIT) ? 1u : 0u);
@@ -445,8 +449,13 @@ __device__ __forceinline__ void sw_full(const World& w, uint32_t e, uint32_t f, 
     }
 }
 
+// (GW_SWH_MINB 8 caps it at 64 VGPRs, 8 waves per SIMD instead of 7 at 66,
+// but spills 2 VGPRs to scratch: config #5 write 851 -> 907-930 us; uncapped)
+#ifndef GW_SWH_MINB
+#define GW_SWH_MINB 1
+#endif
 template <int U>
-__global__ void __launch_bounds__(NT) k_sync_write_h(World w, const uint32_t* __restrict__ flagged,
+__global__ void __launch_bounds__(NT, GW_SWH_MINB) k_sync_write_h(World w, const uint32_t* __restrict__ flagged,
                                                      const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
                                                      uint32_t nf_max, const uint64_t* __restrict__ rec_off,
                                                      const uint32_t* __restrict__ cnt, gw_sync_record* rec,
@@ -545,11 +554,15 @@ __global__ void __launch_bounds__(NT) k_sync_write_h(World w, const uint32_t* __
             g.meta = 0;
             if (kk < total) g = w.gn[ss + (kk - sp)];
             if (kk < total && g.slot != e && (g.meta & CLIENT_BIT)) {
-                const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
+                bool ia, near;
+                we.test(g.x, g.z, ia, near);              // B's test of A only in the rounding band
                 bool rel = ia;
-                if (ia != ib) {
-                    if (!have_se) { se = w.rec[e].stamp; have_se = true; }
-                    rel = resolve(ia, ib, se, w.rec[g.slot].stamp);
+                if (near) {
+                    const bool ib = in_win(g.x, g.z, d, a.x, a.z);
+                    if (ia != ib) {
+                        if (!have_se) { se = w.rec[e].stamp; have_se = true; }
+                        rel = resolve(ia, ib, se, w.rec[g.slot].stamp);
+                    }
                 }
                 take = rel;
             }
@@ -595,11 +608,15 @@ __device__ __forceinline__ void wave_neighbors_lds(const World& w, uint32_t e, c
             g.meta = 0;
             if (idx[u] != ~0u) g = G[idx[u] - g0];
             if (g.slot != e) {
-                const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
+                bool ia, near;
+                we.test(g.x, g.z, ia, near);              // B's test of A only in the rounding band
                 rel = ia;
-                if (ia != ib) {
-                    if (!have_se) { se = w.rec[e].stamp; have_se = true; }
-                    rel = resolve(ia, ib, se, w.rec[g.slot].stamp);
+                if (near) {
+                    const bool ib = in_win(g.x, g.z, d, a.x, a.z);
+                    if (ia != ib) {
+                        if (!have_se) { se = w.rec[e].stamp; have_se = true; }
+                        rel = resolve(ia, ib, se, w.rec[g.slot].stamp);
+                    }
                 }
             }
             f(rel, g.slot, (g.meta & CLIENT_BIT) ? 1u : 0u);
@@ -768,11 +785,15 @@ __global__ void __launch_bounds__(NT) k_sync_write_small2(World w, const uint32_
             g.meta = 0;
             if (kk < total) g = G[ss + (kk - sp) - g0];
             if (kk < total && g.slot != e && (g.meta & CLIENT_BIT)) {
-                const bool ia = we.has(g.x, g.z), ib = in_win(g.x, g.z, d, a.x, a.z);
+                bool ia, near;
+                we.test(g.x, g.z, ia, near);              // B's test of A only in the rounding band
                 bool rel = ia;
-                if (ia != ib) {
-                    if (!have_se) { se = w.rec[e].stamp; have_se = true; }
-                    rel = resolve(ia, ib, se, w.rec[g.slot].stamp);
+                if (near) {
+                    const bool ib = in_win(g.x, g.z, d, a.x, a.z);
+                    if (ia != ib) {
+                        if (!have_se) { se = w.rec[e].stamp; have_se = true; }
+                        rel = resolve(ia, ib, se, w.rec[g.slot].stamp);
+                    }
                 }
                 take = rel;
             }

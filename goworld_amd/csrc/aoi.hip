@@ -1492,7 +1492,10 @@ __global__ void __launch_bounds__(NT) k_flatten(TickBufs b) {
 // their events at output time.
 constexpr int BK_RUN_BIT = BK_KEY_BITS;               // just above the (leave, watcher, target) bits
 constexpr uint64_t BK_RUN = 1ull << BK_RUN_BIT;
-__device__ __forceinline__ void flat_chunk(const TickBufs& b, uint64_t c, uint64_t NI, uint64_t nl_, int ln) {
+// item of flat position p = 64c + ln (wave-uniform c; every lane runs the
+// shuffles) and the events it stands for (bk_weight); false past NI
+__device__ __forceinline__ bool flat_item(const TickBufs& b, uint64_t c, uint64_t NI, uint64_t nl_, int ln,
+                                          uint64_t& item, uint32_t& wt) {
     const uint32_t q0 = b.chunk_first[c];
     const uint64_t k = (uint64_t)q0 + ln;
     uint32_t at = 0xffffffffu, end = 0xffffffffu;
@@ -1520,20 +1523,26 @@ __device__ __forceinline__ void flat_chunk(const TickBufs& b, uint64_t c, uint64
                           (uint32_t)__shfl((int)(uint32_t)reg, q, 64);
     const uint32_t qA = (uint32_t)__shfl((int)mi.x, q, 64);
     const uint32_t qe = (uint32_t)__shfl((int)mi.y, q, 64), ql = (uint32_t)__shfl((int)mi.z, q, 64);
-    if (p >= NI) return;                                       // (lane-local: the caller's loop is wave-uniform)
+    if (p >= NI) return false;
     const uint32_t W = (uint32_t)b.wbits;
     const uint32_t lvb = 1u << W;
     const uint32_t j = p - qat;
     const uint32_t nr = (qe ? 1u : 0u) + (ql ? 1u : 0u);
-    uint64_t item;
     if (j < nr) {
         const bool leave = (j == 1) || !qe;
         item = BK_RUN | ((uint64_t)((leave ? lvb : 0u) | qA) << W) | (q0 + (uint32_t)q);
+        wt = leave ? ql : qe;
     } else {
         const uint64_t e = b.mir[qreg + (j - nr)];
         item = ((uint64_t)(((e & 1u) ? lvb : 0u) | (uint32_t)hi32(e)) << W) | (uint32_t)(lo32(e) >> 1);
+        wt = 1u;
     }
-    b.bk_a[p] = item;
+    return true;
+}
+__device__ __forceinline__ void flat_chunk(const TickBufs& b, uint64_t c, uint64_t NI, uint64_t nl_, int ln) {
+    uint64_t item;
+    uint32_t wt;
+    if (flat_item(b, c, NI, nl_, ln, item, wt)) b.bk_a[(c << 6) + ln] = item;
 }
 
 __global__ void __launch_bounds__(NT) k_flat_items(TickBufs b) {
@@ -1622,13 +1631,32 @@ __device__ __forceinline__ uint32_t bk_weight(const TickBufs& b, uint64_t item) 
 }
 
 // per (bucket, tile): items | events << 32
+// FLAT: the items are made here (flat_item) and stored for the scatter, in
+// place of a k_flat_items launch before this one: the run weights come with
+// the item, and the sizes k_flat_items published are computed by every block
+// (block 0 publishes them)
+template <bool FLAT>
 __global__ void __launch_bounds__(BK_NT) k_bk_count(TickBufs b) {
     __shared__ uint32_t h[1 << BK_MAXBITS], hw[1 << BK_MAXBITS];
     __shared__ BkLut lut;
     const int t = threadIdx.x;
     const uint32_t NB = 1u << b.bk_bits;
-    const uint64_t n = b.st->n_sort;
-    const uint64_t T = b.st->bk_tiles;
+    uint64_t n, T, nl_ = 0;
+    if (FLAT) {
+        const uint64_t E = lo32(b.st->ev_pk) + hi32(b.st->ev_pk);
+        n = E > b.ev_cap ? 0 : b.st->n_items;               // nothing is sorted on overflow (the host redoes)
+        T = (n + BK_TILE - 1) / BK_TILE;
+        nl_ = b.st->n_mlist;
+        if (blockIdx.x == 0 && t == 0) {
+            if (E > b.ev_cap) atomicOr(&b.st->overflow, 1ull);
+            b.st->n_sort = n;
+            b.st->bk_tiles = T;
+            b.st->bk_cells = T << b.bk_bits;
+        }
+    } else {
+        n = b.st->n_sort;
+        T = b.st->bk_tiles;
+    }
     if (blockIdx.x >= T) return;                            // block-uniform
     const int W = b.wbits;
     const uint64_t km = (1ull << (2 * W + 1)) - 1;
@@ -1640,6 +1668,83 @@ __global__ void __launch_bounds__(BK_NT) k_bk_count(TickBufs b) {
     uint32_t wt[IPT];
     auto load = [&](uint64_t tile) {
         const uint64_t base = tile * BK_TILE;
+        if (FLAT) {
+            // flat_item's chain for the IPT chunks of this wave, stage by
+            // stage, so each stage's loads of all chunks are in flight together
+            const int ln = lane_id();
+            const uint64_t c0 = (base >> 6) + (uint64_t)(t >> 6);
+            uint32_t q0[IPT];
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                const uint64_t c = c0 + (uint64_t)j * (BK_NT / 64);
+                q0[j] = (c << 6) < n ? b.chunk_first[c] : 0u;
+            }
+            uint32_t at[IPT], end[IPT], ma[IPT], me[IPT], ml[IPT];
+            uint64_t reg[IPT];
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                const uint64_t c = c0 + (uint64_t)j * (BK_NT / 64);
+                const uint64_t kk = (uint64_t)q0[j] + ln;
+                at[j] = end[j] = 0xffffffffu;
+                ma[j] = me[j] = ml[j] = 0;
+                reg[j] = 0;
+                if ((c << 6) < n && kk < nl_) {
+                    at[j] = b.ioff[kk];
+                    end[j] = b.icnt[kk];
+                    const uint4 mi = b.minfo[kk];
+                    ma[j] = mi.x;
+                    me[j] = mi.y;
+                    ml[j] = mi.z;
+                    reg[j] = b.mreg[kk];
+                }
+            }
+            const uint32_t W = (uint32_t)b.wbits;
+            const uint32_t lvb = 1u << W;
+            uint64_t mj[IPT];                                       // mirror event index, ~0: a run or nothing
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                const uint64_t c = c0 + (uint64_t)j * (BK_NT / 64);
+                k[j] = 0;
+                wt[j] = 0;
+                mj[j] = ~0ull;
+                if ((c << 6) >= n) continue;                        // wave-uniform
+                if (end[j] != 0xffffffffu) end[j] += at[j];
+                const uint32_t p = (uint32_t)((c << 6) + ln);
+                uint32_t lo = 0, hi = 64;
+#pragma unroll
+                for (int s = 0; s < 7; ++s) {
+                    const uint32_t mid = min((lo + hi) >> 1, 63u);
+                    const uint32_t e = (uint32_t)__shfl((int)end[j], (int)mid, 64);
+                    if (lo < hi) {
+                        if (e <= p) lo = mid + 1; else hi = mid;
+                    }
+                }
+                const int q = (int)min(lo, 63u);
+                const uint32_t qat = (uint32_t)__shfl((int)at[j], q, 64);
+                const uint64_t qreg = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(reg[j] >> 32), q, 64) << 32) |
+                                      (uint32_t)__shfl((int)(uint32_t)reg[j], q, 64);
+                const uint32_t qA = (uint32_t)__shfl((int)ma[j], q, 64);
+                const uint32_t qe = (uint32_t)__shfl((int)me[j], q, 64), ql = (uint32_t)__shfl((int)ml[j], q, 64);
+                if (p >= n) continue;
+                const uint32_t jj = p - qat;
+                const uint32_t nr = (qe ? 1u : 0u) + (ql ? 1u : 0u);
+                if (jj < nr) {
+                    const bool leave = (jj == 1) || !qe;
+                    k[j] = BK_RUN | ((uint64_t)((leave ? lvb : 0u) | qA) << W) | (q0[j] + (uint32_t)q);
+                    wt[j] = leave ? ql : qe;
+                } else {
+                    mj[j] = qreg + (jj - nr);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                if (mj[j] == ~0ull) continue;
+                const uint64_t e = b.mir[mj[j]];
+                k[j] = ((uint64_t)(((e & 1u) ? lvb : 0u) | (uint32_t)hi32(e)) << W) | (uint32_t)(lo32(e) >> 1);
+                wt[j] = 1u;
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
             const uint64_t i = base + (uint64_t)j * BK_NT + t;
@@ -1666,6 +1771,7 @@ __global__ void __launch_bounds__(BK_NT) k_bk_count(TickBufs b) {
         if (i < n) {
             const uint32_t q = bk_bucket(lut, lsh, (uint32_t)((k[j] & km) >> W));
             b.bk_id[i] = (uint16_t)q;
+            if (FLAT) b.bk_a[i] = k[j];
             atomicAdd(&h[q], 1u);
             atomicAdd(&hw[q], wt[j]);
         }
@@ -2091,12 +2197,24 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
                                                std::max<uint64_t>(8192, (2 * b.it_hint + 63) / 64));
         uint32_t fb = nblk1(fw, NWAVE);
         if (b.grid_cap) fb = std::min(fb, b.grid_cap);
-        hipLaunchKernelGGL(k_flat_items, dim3(fb), dim3(NT), 0, s, b);
         // tile passes: grid-stride over a grid sized by the last tick's items
         uint32_t bt = (uint32_t)std::min<uint64_t>(
             b.bk_tiles, std::max<uint64_t>(256, (2 * b.it_hint + BK_TILE - 1) / BK_TILE));
         if (b.grid_cap) bt = std::min(bt, b.grid_cap);
-        hipLaunchKernelGGL(k_bk_count, dim3(bt), dim3(BK_NT), 0, s, b);
+        // the items made by the count pass when there are many tiles (config #3
+        // events 134 -> 131 us, #4 217 -> 214 us); with a few tiles (config #2,
+        // world strips) a few blocks would walk every item's chain alone (+5 us
+        // at #2), so k_flat_items spreads them over the chip first
+        // (GW_BK_FLAT=0 / 1 forces either)
+        const char* fe = getenv("GW_BK_FLAT");                // (read per tick: the tests switch it)
+        const int flat_env = fe ? atoi(fe) : -1;
+        const bool flat_in_count = flat_env >= 0 ? flat_env != 0 : b.it_hint >= 16ull * BK_TILE;
+        if (flat_in_count) {
+            hipLaunchKernelGGL(k_bk_count<true>, dim3(bt), dim3(BK_NT), 0, s, b);
+        } else {
+            hipLaunchKernelGGL(k_flat_items, dim3(fb), dim3(NT), 0, s, b);
+            hipLaunchKernelGGL(k_bk_count<false>, dim3(bt), dim3(BK_NT), 0, s, b);
+        }
         scan_exclusive<uint64_t, uint64_t>((const uint64_t*)b.bk_cnt, (uint64_t*)b.bk_cnt,
                                            (uint64_t)NB * b.bk_tiles, (const uint64_t*)&b.st->bk_cells, sc,
                                            (uint64_t*)nullptr, s);

@@ -201,6 +201,22 @@ def test_config2_uniform_100k(ctx_factory):
     h.check_lists(sample=range(0, tr.capacity, 97))
 
 
+@pytest.mark.parametrize("flat", ["0", "1"])
+def test_bucket_items_made_by_count_pass(ctx_factory, flat, monkeypatch):
+    """The bucket path's items (own runs + mirror events) are made either by
+    k_flat_items ahead of the count pass or by the count pass itself (the
+    default from 16 tiles of items up); GW_BK_FLAT forces either on a 100k
+    space of a few tiles and on the 200k hotspot space (tens of tiles):
+    events and records stay exact against the oracle."""
+    monkeypatch.setenv("GW_BK_FLAT", flat)
+    for tr in (T.config2(ticks=2), T.config3(ticks=1, n=200_000, side=14654.0)):
+        h = Harness(ctx_factory(), [tr])
+        h.check_collect()
+        for t in range(len(tr.ticks)):
+            h.step(t)
+            h.check_collect()
+
+
 def test_hotspot_clustered_200k(ctx_factory):
     tr = T.config3(ticks=2, n=200_000, side=14654.0)   # 1M-config density, smaller world
     h = Harness(ctx_factory(), [tr])

@@ -1286,10 +1286,11 @@ __global__ void __launch_bounds__(64) k_mover_list(TickBufs b) {
 // Blocks [0, STAT_SHARDS) sum the statistics; the others block-sort the own
 // events of movers with too many for LDS (k_mover listed them in big[]): one
 // launch for both small jobs.
-__global__ void __launch_bounds__(NT) k_mover_post(TickBufs b) {
-    if (blockIdx.x >= (uint32_t)STAT_SHARDS) {              // block-uniform role
+// (role index r < STAT_SHARDS: a shard of the sums; above: the block sorts)
+__device__ __forceinline__ void mover_post(const TickBufs& b, uint32_t r, uint32_t nr) {
+    if (r >= (uint32_t)STAT_SHARDS) {                       // block-uniform role
         const uint64_t nb = b.st->n_big;
-        for (uint64_t k = blockIdx.x - STAT_SHARDS; k < nb; k += gridDim.x - STAT_SHARDS) {
+        for (uint64_t k = r - STAT_SHARDS; k < nb; k += nr - STAT_SHARDS) {
             const uint32_t m = b.big[k];
             const uint64_t c = b.ownc[m];
             const uint32_t n = (uint32_t)(lo32(c) + hi32(c));
@@ -1304,7 +1305,7 @@ __global__ void __launch_bounds__(NT) k_mover_post(TickBufs b) {
     __shared__ unsigned long long red[2][NWAVE];
     const uint64_t n = b.st->n_gm;
     unsigned long long a = 0, e = 0;
-    for (uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x; m < n; m += (uint64_t)STAT_SHARDS * NT) {
+    for (uint64_t m = (uint64_t)r * NT + threadIdx.x; m < n; m += (uint64_t)STAT_SHARDS * NT) {
         a += b.mstat[m];
         e += b.ownc[m] + b.mirc[m];
     }
@@ -1315,21 +1316,29 @@ __global__ void __launch_bounds__(NT) k_mover_post(TickBufs b) {
     if (threadIdx.x == 0) {
         a = e = 0;
         for (int i = 0; i < NWAVE; ++i) { a += red[0][i]; e += red[1][i]; }
-        shard_add(b.st, blockIdx.x, SH_AOLD, a);
+        shard_add(b.st, r, SH_AOLD, a);
         if (e) atomicAdd(&b.st->ev_pk, e);
     }
 }
+__global__ void __launch_bounds__(NT) k_mover_post(TickBufs b) { mover_post(b, blockIdx.x, gridDim.x); }
 
 
 // ---------------------------------------------------------------------------
 // events stage.  (1) movers with events in slot order: compaction of the
 // mover bitmap (one 32-slot word per thread, striped tiles, decoupled
 // look-back; words are cleared as they are read).
+// Blocks [nt, gridDim) do k_mover_post's work (the statistics sums and the
+// block sorts; neither waits on anything), so the two small jobs share one
+// launch; the tiles take tickets among themselves only.
 template <int IPT>
 __global__ void __launch_bounds__(NT) k_bits_list(uint32_t* __restrict__ bits, uint64_t nwords,
                                                   uint32_t* __restrict__ list, unsigned long long* __restrict__ status,
                                                   unsigned long long* __restrict__ ticket, unsigned long long tbase,
-                                                  uint32_t tag, unsigned long long* total) {
+                                                  uint32_t tag, unsigned long long* total, TickBufs pb, uint32_t nt) {
+    if (blockIdx.x >= nt) {                                 // block-uniform role
+        mover_post(pb, blockIdx.x - nt, gridDim.x - nt);
+        return;
+    }
     __shared__ uint32_t lds[IPT * NWAVE];
     __shared__ uint32_t s_tile, s_prefix;
     if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tbase);
@@ -1363,7 +1372,7 @@ __global__ void __launch_bounds__(NT) k_bits_list(uint32_t* __restrict__ bits, u
         }
         bits[i] = 0;
     }
-    if (tile == gridDim.x - 1 && threadIdx.x == 0) *total = pre + tot;
+    if (tile == nt - 1 && threadIdx.x == 0) *total = pre + tot;
 }
 
 // (2) per listed mover: all its events (own + mirror), packed enters | leaves<<32,
@@ -2174,18 +2183,21 @@ void tick_diff(const TickBufs& b, hipStream_t s) {
 }
 void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint64_t nmax = 2ull * b.m;
-    hipLaunchKernelGGL(k_mover_post, dim3(STAT_SHARDS + 64), dim3(NT), 0, s, b);
-    // movers in slot order
+    // movers in slot order, and k_mover_post's work in the same launch
+    // (GW_POST_SPLIT=1: a launch of its own first)
     const uint64_t nwords = (uint64_t)b.w.cap / 32 + 1;
     const uint64_t tile = (uint64_t)SCAN_IPT * NT;
     const uint32_t nb = nblk1(nwords, (uint32_t)tile);
+    const char* ps = getenv("GW_POST_SPLIT");
+    const bool split = ps && atoi(ps) != 0;
+    if (split) hipLaunchKernelGGL(k_mover_post, dim3(STAT_SHARDS + 64), dim3(NT), 0, s, b);
     if (sc.tag >= SCAN_TAG_MAX) {
         (void)hipMemsetAsync(sc.status, 0, sc.max_tiles * SCAN_WORDS * 8, s);
         sc.tag = 0;
     }
     ++sc.tag;
-    hipLaunchKernelGGL(k_bits_list<SCAN_IPT>, dim3(nb), dim3(NT), 0, s, b.movbit, nwords, b.mlist, sc.status,
-                       sc.ticket, sc.tbase, sc.tag, &b.st->n_mlist);
+    hipLaunchKernelGGL(k_bits_list<SCAN_IPT>, dim3(nb + (split ? 0 : STAT_SHARDS + 64)), dim3(NT), 0, s, b.movbit,
+                       nwords, b.mlist, sc.status, sc.ticket, sc.tbase, sc.tag, &b.st->n_mlist, b, nb);
     sc.tbase += nb;
     const uint64_t* nml = (const uint64_t*)&b.st->n_mlist;
     hipLaunchKernelGGL(k_mover_counts, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);

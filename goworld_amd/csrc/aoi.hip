@@ -327,8 +327,7 @@ __global__ void __launch_bounds__(NT) k_cellcnt(TickBufs b) {
 
 // per mover: its mover-grid entries (the cursor counts gm_cnt back to zero)
 // and, for an arrival, its grid entry behind the kept entries of the new cell
-__global__ void __launch_bounds__(NT) k_place(TickBufs b) {
-    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+__device__ __forceinline__ void place_one(const TickBufs& b, uint32_t i) {
     if (i >= b.m) return;
     const uint4 cc = b.mcell[i];
     if (cc.w) atomicOr(&b.w.flags[flag_word(cc.z)], cc.w << flag_sh(cc.z));   // op i's syncInfoFlag bits
@@ -373,9 +372,9 @@ __global__ void __launch_bounds__(NT) k_place(TickBufs b) {
 // clean cells move as a block: new index = start_nxt + offset in the cell
 // (grid-stride over the present entries: the grid is sized by the slot
 // capacity, a world strip holds a fraction of it)
-__global__ void __launch_bounds__(NT) k_grid_copy(TickBufs b) {
+__device__ __forceinline__ void grid_copy(const TickBufs& b, uint32_t blk, uint32_t nblk) {
     const uint32_t n = b.w.gn_start[b.w.ncells];
-    for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < n; i += gridDim.x * NT) {
+    for (uint32_t i = blk * NT + threadIdx.x; i < n; i += nblk * NT) {
         GEnt e = b.w.gn[i];
         if (e.slot == DEPARTED) continue;
         const uint32_t c = e.meta & CELL_MASK;
@@ -383,6 +382,14 @@ __global__ void __launch_bounds__(NT) k_grid_copy(TickBufs b) {
         e.meta &= ~b.mstale;                                      // the last tick's mover bit
         b.gn_nxt[b.start_nxt[c] + (i - b.w.gn_start[c])] = e;   // gidx (offset in the cell) unchanged
     }
+}
+__global__ void __launch_bounds__(NT) k_place(TickBufs b) { place_one(b, blockIdx.x * NT + threadIdx.x); }
+__global__ void __launch_bounds__(NT) k_grid_copy(TickBufs b) { grid_copy(b, blockIdx.x, gridDim.x); }
+// both in one launch (they touch disjoint cells of the new grid: arrivals
+// into dirty cells, clean cells as blocks): blocks [0, np) place, the rest copy
+__global__ void __launch_bounds__(NT) k_place_copy(TickBufs b, uint32_t np) {
+    if (blockIdx.x < np) place_one(b, blockIdx.x * NT + threadIdx.x);
+    else grid_copy(b, blockIdx.x - np, gridDim.x - np);
 }
 
 // Dirty cells: the kept entries (already in slot order) merge with the
@@ -475,8 +482,14 @@ void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     // +23 us at config #4 -- the tiles post their aggregates later.)
     scan_pair32(b.cnt_new, b.gm_cnt, b.start_nxt, b.gm_start, (uint64_t)NC + 1, sc, (uint32_t*)&b.st->n_present,
                 (uint32_t*)&b.st->n_gm, s);
-    hipLaunchKernelGGL(k_place, dim3(nblk1(b.m, NT)), dim3(NT), 0, s, b);
-    hipLaunchKernelGGL(k_grid_copy, dim3(std::min<uint32_t>(nblk1(b.w.cap, NT), 16384)), dim3(NT), 0, s, b);
+    const uint32_t np = nblk1(b.m, NT), nc = std::min<uint32_t>(nblk1(b.w.cap, NT), 16384);
+    const char* ps = getenv("GW_PLACE_SPLIT");              // 1: two launches (for comparison)
+    if (ps && atoi(ps) != 0) {
+        hipLaunchKernelGGL(k_place, dim3(np), dim3(NT), 0, s, b);
+        hipLaunchKernelGGL(k_grid_copy, dim3(nc), dim3(NT), 0, s, b);
+    } else {
+        hipLaunchKernelGGL(k_place_copy, dim3(np + nc), dim3(NT), 0, s, b, np);
+    }
     hipLaunchKernelGGL(k_grid_dirty, dim3(nblk1((uint64_t)NC, b.dirty_span * NWAVE)), dim3(NT), 0, s, b);
 }
 

@@ -398,11 +398,11 @@ __global__ void __launch_bounds__(NT) k_place_copy(TickBufs b, uint32_t np) {
 // kept entries and arrivals with a smaller slot.  A wave scans the flags of
 // dirty_span cells and merges its dirty ones; cells with more than 64
 // arrivals are compacted and sorted by the wave (bitonic, in place).
-__global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) {
+__device__ __forceinline__ void grid_dirty(const TickBufs& b, uint32_t blk) {
     const int ln = lane_id();
     const uint64_t lt = lanemask_lt();
     const uint32_t span = b.dirty_span;
-    const uint32_t c0 = (blockIdx.x * NWAVE + (threadIdx.x >> 6)) * span;
+    const uint32_t c0 = (blk * NWAVE + (threadIdx.x >> 6)) * span;
     if (c0 >= b.w.ncells) return;
     const uint32_t cl = c0 + ln;
     uint64_t dm = wave_ballot(ln < (int)span && cl < b.w.ncells && (b.dep[cl] & CELL_DIRTY));
@@ -471,9 +471,11 @@ __global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) {
         if (ln == 0) b.dep[c] = 0;
     }
 }
+__global__ void __launch_bounds__(NT) k_grid_dirty(TickBufs b) { grid_dirty(b, blockIdx.x); }
+static uint32_t dirty_blocks(const TickBufs& b) { return nblk1((uint64_t)b.w.ncells, b.dirty_span * NWAVE); }
 
 
-void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
+void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s, bool dirty) {
     const uint32_t NC = b.w.ncells;
     hipLaunchKernelGGL(k_cellcnt, dim3(nblk1((uint64_t)NC + 1, NT)), dim3(NT), 0, s, b);
     // both cell scans in one launch; totals land in the low words of the
@@ -490,7 +492,7 @@ void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     } else {
         hipLaunchKernelGGL(k_place_copy, dim3(np + nc), dim3(NT), 0, s, b, np);
     }
-    hipLaunchKernelGGL(k_grid_dirty, dim3(nblk1((uint64_t)NC, b.dirty_span * NWAVE)), dim3(NT), 0, s, b);
+    if (dirty) hipLaunchKernelGGL(k_grid_dirty, dim3(dirty_blocks(b)), dim3(NT), 0, s, b);
 }
 
 // ---------------------------------------------------------------------------
@@ -526,8 +528,9 @@ __device__ __forceinline__ Rects mover_rects(const SpaceP& P, bool po, float ox,
 // its cells) -> the size of its own-event region.  The index ranges of its
 // rows (<= RR_ROWS) go to rowrec for k_mover, whose wave then starts its walk
 // one load after its entry instead of three (entry -> space -> row starts).
-__global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
-    const uint64_t m = (uint64_t)blockIdx.x * NT + threadIdx.x;
+// (gs: the new grid's row starts -- b.w.gn_start once b.w is the new grid,
+// b.start_nxt before)
+__device__ __forceinline__ void bounds_one(const TickBufs& b, uint64_t m, const uint32_t* __restrict__ gs) {
     const uint64_t ngm = b.st->n_gm;
     if (m >= ngm && !(b.heavy_min && m - lane_id() < ngm)) return;   // heavy mode: whole waves reach the ballot
     MEnt e;
@@ -545,7 +548,7 @@ __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
             const Rect rr = q == 0 ? R.r[0] : R.r[1];
             for (int cz = rr.z0; cz <= rr.z1; ++cz, ++nr) {
                 const uint32_t row = P.cell_base + (uint32_t)cz * (uint32_t)P.W;
-                const uint32_t g0 = b.w.gn_start[row + rr.x0], g1 = b.w.gn_start[row + rr.x1 + 1];
+                const uint32_t g0 = gs[row + rr.x0], g1 = gs[row + rr.x1 + 1];
                 const uint32_t m0 = b.gm_start[row + rr.x0], m1 = b.gm_start[row + rr.x1 + 1];
                 c += (g1 - g0) + (m1 - m0);
                 if (rec && nr < RR_ROWS) rec[nr] = make_uint4(g0, g1, m0, m1);
@@ -573,6 +576,16 @@ __global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
     }
     if (m < ngm) b.cand[m] = c | ((e.tags & TAG_PRIMARY) && !hv ? PRIM_ONE : 0ull);
 }
+__global__ void __launch_bounds__(NT) k_bounds(TickBufs b) {
+    bounds_one(b, (uint64_t)blockIdx.x * NT + threadIdx.x, b.w.gn_start);
+}
+// the dirty cells' merges and the bounds in one launch: the bounds read the
+// new grid's row starts and the mover grid, not its entries (b: the buffers
+// before the flip to the new grid; blocks [0, nd) merge)
+__global__ void __launch_bounds__(NT) k_dirty_bounds(TickBufs b, uint32_t nd) {
+    if (blockIdx.x < nd) grid_dirty(b, blockIdx.x);
+    else bounds_one(b, (uint64_t)(blockIdx.x - nd) * NT + threadIdx.x, b.start_nxt);
+}
 
 // the scan of the tagged bounds lists the primary entries in mover-grid
 // (cell) order: pidx[k] = the k-th, k_mover's wave k
@@ -584,10 +597,15 @@ struct PrimPost {
     }
 };
 
-void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
+void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s, const TickBufs* pre) {
     const uint64_t nmax = 2ull * b.m;
     const uint64_t* ngm = (const uint64_t*)&b.st->n_gm;
-    hipLaunchKernelGGL(k_bounds, dim3(nblk1(nmax, NT)), dim3(NT), 0, s, b);
+    if (pre) {
+        const uint32_t nd = dirty_blocks(*pre);
+        hipLaunchKernelGGL(k_dirty_bounds, dim3(nd + nblk1(nmax, NT)), dim3(NT), 0, s, *pre, nd);
+    } else {
+        hipLaunchKernelGGL(k_bounds, dim3(nblk1(nmax, NT)), dim3(NT), 0, s, b);
+    }
     scan_exclusive<uint64_t, uint64_t>(b.cand, b.reg, nmax, ngm, sc, (uint64_t*)&b.st->cand_total, s,
                                        PrimPost{b.compact && !b.small_ents && !b.pair_max ? b.pidx : nullptr});
 }

@@ -1391,15 +1391,19 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     tick_ops(b, c->st);
     prof_end(c, (uint64_t)M * 24);
     prof_begin(c, "grid");
-    tick_grid(b, c->sc, c->st);
+    // with events, the dirty cells are merged in the bounds' launch (GW_DIRTY_SPLIT=1: their own)
+    const char* dsv = getenv("GW_DIRTY_SPLIT");
+    const bool dirty_later = ev_on && !(dsv && atoi(dsv) != 0);
+    tick_grid(b, c->sc, c->st, !dirty_later);
     HIPCHK(hipEventRecord(c->ev_grid, c->st));        // a following collect's flag compaction may start here
     c->mpar ^= 1u;                                   // the next rebuild drops this tick's mover bits
     c->cells_zero = true;
     size_t s_grid = prof_end(c, 0);
     c->gcur ^= 1;                                    // the new grid is current from here on
+    const TickBufs bg = b;                           // (the buffers before the flip)
     b.w = world(c);
     prof_begin(c, "movers");
-    if (ev_on) tick_movers(b, c->sc, c->st);
+    if (ev_on) tick_movers(b, c->sc, c->st, dirty_later ? &bg : nullptr);
     size_t s_movers = prof_end(c, 0);
     prof_begin(c, "diff");
     if (ev_on) tick_diff(b, c->st);

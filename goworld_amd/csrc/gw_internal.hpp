@@ -318,8 +318,11 @@ void grid_rebuild(const World& w, DevStats* st, uint32_t* k0, uint32_t* v0, uint
                   RadixTmp& rt, int key_bits, hipStream_t s);
 // one tick, in launch order (device-side counts only: no host sync inside)
 void tick_ops(const TickBufs& b, hipStream_t s);
-void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s);     // gn -> gn_nxt, start_nxt
-void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s);   // b.w: the new grid
+// gn -> gn_nxt, start_nxt (dirty = false: the dirty cells' merges are left to tick_movers)
+void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s, bool dirty = true);
+// b.w: the new grid; pre: the buffers before the flip, whose dirty cells it
+// merges in the bounds' launch (tick_grid ran with dirty = false)
+void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s, const TickBufs* pre = nullptr);
 void tick_diff(const TickBufs& b, hipStream_t s);                  // own + mirror events per mover
 void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s);   // canonical event arrays
 // after the host read the counts (given by value); zeroes the tick's DevStats

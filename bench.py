@@ -237,10 +237,12 @@ def dry_run(a, ctl):
 
 # the diff stage's kernel: k_mover_c (one wave per primary mover entry), k_mover (one wave per
 # mover-grid entry, GW_MOVER_COMPACT=0), or k_mover_pair when GW_PAIR_MAX > 0
+# (k_mover_c<2, false>: the variant without the group-teleport paths, launched unless the context is a
+# world of >= 2 strips; k_mover_small<2, true>: the half-wave walk)
 STAGE_KERNEL = {"diff": "k_mover_pair<2>" if int(os.environ.get("GW_PAIR_MAX", "0") or 0) > 0
-                else "k_mover<2, 1>" if os.environ.get("GW_MOVER_COMPACT", "1") == "0" else "k_mover_c<2>"}
+                else "k_mover<2, 1>" if os.environ.get("GW_MOVER_COMPACT", "1") == "0" else "k_mover_c<2, false>"}
 # the stage's kernel differs in small-space mode (config #4: many spaces whose grids fit LDS)
-STAGE_KERNEL_C4 = {"diff": "k_mover_small<2>", "sync_write": "k_sync_write_small2"}
+STAGE_KERNEL_C4 = {"diff": "k_mover_small<2, true>", "sync_write": "k_sync_write_small2"}
 PMC_DIR = os.path.join(ROOT, "profiles")
 
 
@@ -772,7 +774,12 @@ def roofline_fields(res, K, config, ws):
         kern, psrc, pstamp = pmc_traffic(config) if ws == 1 else (None, None, "n/a (N>1)")
 
         def traffic(k):
-            return (kern or {}).get(k, {}).get("hbm_bytes") if kern else None
+            if not kern:
+                return None
+            if k not in kern:                   # a template's other instantiation, if only one was profiled
+                alt = [n for n in kern if n.split("<")[0] == k.split("<")[0]]
+                k = alt[0] if len(alt) == 1 else k
+            return kern.get(k, {}).get("hbm_bytes")
         names = STAGE_KERNEL_C4 if config == 4 else STAGE_KERNEL
         mv = names["diff"]
         sw = names.get("sync_write", "k_sync_write<4, false>")

@@ -485,8 +485,7 @@ void tick_grid(const TickBufs& b, ScanCtx& sc, hipStream_t s, bool dirty) {
     scan_pair32(b.cnt_new, b.gm_cnt, b.start_nxt, b.gm_start, (uint64_t)NC + 1, sc, (uint32_t*)&b.st->n_present,
                 (uint32_t*)&b.st->n_gm, s);
     const uint32_t np = nblk1(b.m, NT), nc = std::min<uint32_t>(nblk1(b.w.cap, NT), 16384);
-    const char* ps = getenv("GW_PLACE_SPLIT");              // 1: two launches (for comparison)
-    if (ps && atoi(ps) != 0) {
+    if (b.place_split) {                                    // two launches (for comparison)
         hipLaunchKernelGGL(k_place, dim3(np), dim3(NT), 0, s, b);
         hipLaunchKernelGGL(k_grid_copy, dim3(nc), dim3(NT), 0, s, b);
     } else {
@@ -2219,8 +2218,7 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
     const uint64_t nwords = (uint64_t)b.w.cap / 32 + 1;
     const uint64_t tile = (uint64_t)SCAN_IPT * NT;
     const uint32_t nb = nblk1(nwords, (uint32_t)tile);
-    const char* ps = getenv("GW_POST_SPLIT");
-    const bool split = ps && atoi(ps) != 0;
+    const bool split = b.post_split != 0;
     if (split) hipLaunchKernelGGL(k_mover_post, dim3(STAT_SHARDS + 64), dim3(NT), 0, s, b);
     if (sc.tag >= SCAN_TAG_MAX) {
         (void)hipMemsetAsync(sc.status, 0, sc.max_tiles * SCAN_WORDS * 8, s);
@@ -2249,9 +2247,7 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
         // world strips) a few blocks would walk every item's chain alone (+5 us
         // at #2), so k_flat_items spreads them over the chip first
         // (GW_BK_FLAT=0 / 1 forces either)
-        const char* fe = getenv("GW_BK_FLAT");                // (read per tick: the tests switch it)
-        const int flat_env = fe ? atoi(fe) : -1;
-        const bool flat_in_count = flat_env >= 0 ? flat_env != 0 : b.it_hint >= 16ull * BK_TILE;
+        const bool flat_in_count = b.bk_flat >= 0 ? b.bk_flat != 0 : b.it_hint >= 16ull * BK_TILE;
         if (flat_in_count) {
             hipLaunchKernelGGL(k_bk_count<true>, dim3(bt), dim3(BK_NT), 0, s, b);
         } else {

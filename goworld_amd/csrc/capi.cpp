@@ -548,6 +548,10 @@ int gw_init(int device_id, gw_ctx** out) {
         (void)hipEventCreate(&c->ev_t1);
         if (const char* e = getenv("GW_OVERLAP_COLLECT")) c->overlap = atoi(e) != 0;
         if (const char* e = getenv("GW_SW_HALVES")) c->sw_halves = atoi(e) != 0 ? 1 : 0;
+        if (const char* e = getenv("GW_BK_FLAT")) c->bk_flat = atoi(e) != 0 ? 1 : 0;
+        if (const char* e = getenv("GW_POST_SPLIT")) c->post_split = atoi(e) != 0;
+        if (const char* e = getenv("GW_PLACE_SPLIT")) c->place_split = atoi(e) != 0;
+        if (const char* e = getenv("GW_DIRTY_SPLIT")) c->dirty_split = atoi(e) != 0;
         if (const char* e = getenv("GW_OVERLAP_MIN")) c->overlap_min = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_CELLS_PER_D")) c->cells_per_d = std::min(4, std::max(1, atoi(e)));
         if (const char* e = getenv("GW_MOVER_WPB")) c->diff_u = atoi(e);
@@ -1364,6 +1368,9 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.big = P<uint32_t>(c->big);
     b.fall = P<uint32_t>(c->fall);
     b.half_rows = c->half_rows;
+    b.bk_flat = c->bk_flat;
+    b.post_split = c->post_split;
+    b.place_split = c->place_split;
     b.mstat = P<unsigned long long>(c->mstat);
     b.movbit = c->movbit; b.gmi = c->gmi;
     b.mlist = P<uint32_t>(c->mlist);
@@ -1392,8 +1399,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     prof_end(c, (uint64_t)M * 24);
     prof_begin(c, "grid");
     // with events, the dirty cells are merged in the bounds' launch (GW_DIRTY_SPLIT=1: their own)
-    const char* dsv = getenv("GW_DIRTY_SPLIT");
-    const bool dirty_later = ev_on && !(dsv && atoi(dsv) != 0);
+    const bool dirty_later = ev_on && !c->dirty_split;
     tick_grid(b, c->sc, c->st, !dirty_later);
     HIPCHK(hipEventRecord(c->ev_grid, c->st));        // a following collect's flag compaction may start here
     c->mpar ^= 1u;                                   // the next rebuild drops this tick's mover bits

@@ -271,6 +271,11 @@ struct TickBufs {
     unsigned long long* conflicts;   // decomposed world (else null): long-mover pairs the lists did not
                                      // cover (no list queued, or the watcher missing from it), HaloStats
     uint32_t dirty_span;      // GW_DIRTY_SPAN: cells whose dirty flags one k_grid_dirty wave scans (1..64)
+    // launch-merge knobs (A/B and tests; gw_ctx reads them at gw_init): GW_BK_FLAT (-1 automatic,
+    // 0 / 1: the bucket items made by k_flat_items / the count pass), GW_POST_SPLIT (k_mover_post
+    // in a launch of its own), GW_PLACE_SPLIT (k_place and k_grid_copy apart)
+    int32_t bk_flat;
+    uint32_t post_split, place_split;
     uint32_t compact;         // GW_MOVER_COMPACT (default 1): k_mover runs one wave per primary entry
                               // (pidx), else one per mover-grid entry, the others exiting
     uint32_t pair_max;        // GW_PAIR_MAX: k_mover_pair runs two movers per wave when both have at

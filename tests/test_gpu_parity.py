@@ -217,6 +217,23 @@ def test_bucket_items_made_by_count_pass(ctx_factory, flat, monkeypatch):
             h.check_collect()
 
 
+def test_unmerged_launches(ctx_factory, monkeypatch):
+    """The launch merges of round 5 each keep their separate-launch path for
+    comparison (GW_POST_SPLIT: k_mover_post apart from k_bits_list;
+    GW_PLACE_SPLIT: k_place and k_grid_copy apart; GW_DIRTY_SPLIT: k_grid_dirty
+    apart from k_bounds): with all three set, events, records and neighbour
+    lists of the 200k hotspot space stay exact against the oracle."""
+    for k in ("GW_POST_SPLIT", "GW_PLACE_SPLIT", "GW_DIRTY_SPLIT"):
+        monkeypatch.setenv(k, "1")
+    tr = T.config3(ticks=2, n=200_000, side=14654.0)
+    h = Harness(ctx_factory(), [tr])                    # gw_init reads the knobs
+    h.check_collect()
+    for t in range(len(tr.ticks)):
+        h.step(t)
+        h.check_collect()
+    h.check_lists(sample=range(0, tr.capacity, 401))
+
+
 def test_hotspot_clustered_200k(ctx_factory):
     tr = T.config3(ticks=2, n=200_000, side=14654.0)   # 1M-config density, smaller world
     h = Harness(ctx_factory(), [tr])

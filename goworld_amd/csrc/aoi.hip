@@ -2243,11 +2243,12 @@ void tick_events(const TickBufs& b, ScanCtx& sc, hipStream_t s) {
             b.bk_tiles, std::max<uint64_t>(256, (2 * b.it_hint + BK_TILE - 1) / BK_TILE));
         if (b.grid_cap) bt = std::min(bt, b.grid_cap);
         // the items made by the count pass when there are many tiles (config #3
-        // events 134 -> 131 us, #4 217 -> 214 us); with a few tiles (config #2,
-        // world strips) a few blocks would walk every item's chain alone (+5 us
-        // at #2), so k_flat_items spreads them over the chip first
+        // events 134 -> 131 us, #4 217 -> 214 us); with fewer (config #2, world
+        // strips: tens of tiles) those blocks would walk every item's chain
+        // alone (+5 us at #2, +5-6 us on #3 / #5 strips), so small ticks keep
+        // k_flat_items, which spreads the chains over the chip first
         // (GW_BK_FLAT=0 / 1 forces either)
-        const bool flat_in_count = b.bk_flat >= 0 ? b.bk_flat != 0 : b.it_hint >= 16ull * BK_TILE;
+        const bool flat_in_count = b.bk_flat >= 0 ? b.bk_flat != 0 : b.it_hint >= 128ull * BK_TILE;
         if (flat_in_count) {
             hipLaunchKernelGGL(k_bk_count<true>, dim3(bt), dim3(BK_NT), 0, s, b);
         } else {

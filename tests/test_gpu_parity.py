@@ -205,7 +205,7 @@ def test_config2_uniform_100k(ctx_factory):
 def test_bucket_items_made_by_count_pass(ctx_factory, flat, monkeypatch):
     """The bucket path's items (own runs + mirror events) are made either by
     k_flat_items ahead of the count pass or by the count pass itself (the
-    default from 16 tiles of items up); GW_BK_FLAT forces either on a 100k
+    default from 128 tiles of items up); GW_BK_FLAT forces either on a 100k
     space of a few tiles and on the 200k hotspot space (tens of tiles):
     events and records stay exact against the oracle."""
     monkeypatch.setenv("GW_BK_FLAT", flat)

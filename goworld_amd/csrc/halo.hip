@@ -13,7 +13,7 @@
 //       it with the last Leave clearing the bit: a Leave's sync_flags is the
 //       mask of bits it keeps, as in the tick)
 //   r3  the entity's last op writes up to 3 rows per destination, entities
-//       placed by one wave-aggregated atomic per wave and destination
+//       placed by one counter add per block and destination
 //   r4  (fixed-size buffers only) zero (NOP) rows past the entities placed
 // Nothing is reset afterwards: the words age out with their session tag.  The
 // placement counters are zeroed by r1 of the next call.  Integer/byte work
@@ -145,10 +145,20 @@ __device__ __forceinline__ void put_far(const HaloFar& F, HaloStats* hs, uint32_
     F.dest[t] = q;
 }
 
-__global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, const unsigned long long* __restrict__ stamps,
+// Entities are placed in a destination's buffer by one counter add per block
+// and destination (the waves' ballots summed in LDS): one add per wave put a
+// few thousand adds on each of two words per call, which serialise
+// memory-side (a 16M world's 8-strip rank, 200k ops: route 74 -> 57 us with
+// 1024-thread blocks).  Small calls keep 256-thread blocks (a 1M world's
+// 8-strip rank, 12.5k ops: 1024-thread blocks cost it 4 us).
+template <uint32_t RNT>
+__global__ void __launch_bounds__(RNT) k_route3(const gw_op* __restrict__ ops, const unsigned long long* __restrict__ stamps,
                                                 uint32_t n, World w, const OpLast* __restrict__ ol, uint32_t tag,
                                                 float max_step, HaloDsts D, HaloStats* hs, HaloFar F) {
-    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    constexpr uint32_t RNW = RNT / 64;
+    __shared__ uint32_t s_cnt[2][RNW];
+    __shared__ uint32_t s_base[2];
+    const uint32_t i = blockIdx.x * RNT + threadIdx.x;
     // every lane reaches the wave-aggregated appends below
     bool rep = false;
     uint32_t s = 0;
@@ -194,32 +204,51 @@ __global__ void __launch_bounds__(NT) k_route3(const gw_op* __restrict__ ops, co
         f = ((flag_get(w.flags, s) & keep) | rbits) & SIF_ROUTED;
     }
     const uint16_t res = lng ? RES_LONG : 0;
-    for (uint32_t d = 0; d < D.n; ++d) {
-        const HaloDst& dst = D.d[d];
-        const bool was = old_p && old_x >= dst.x_lo && old_x < dst.x_hi;
-        const bool now = new_p && new_x >= dst.x_lo && new_x < dst.x_hi;
-        RowKinds k{GW_OP_NOP, GW_OP_NOP, GW_OP_NOP};
-        if (rep) k = row_kinds(was, now, la, ll, lp, f);
-        const bool emit = rep && (k.k0 | k.k1 | k.k2);
-        const uint64_t bm = wave_ballot(emit);
-        if (!bm) continue;
-        const int leader = __builtin_ctzll(bm);
+    const uint32_t wv = threadIdx.x >> 6;
+    RowKinds k[2];
+    bool emit[2];
+    uint64_t bm[2];
+#pragma unroll
+    for (uint32_t d = 0; d < 2; ++d) {
+        k[d] = RowKinds{GW_OP_NOP, GW_OP_NOP, GW_OP_NOP};
+        emit[d] = false;
+        if (d < D.n && rep) {
+            const HaloDst& dst = D.d[d];
+            const bool was = old_p && old_x >= dst.x_lo && old_x < dst.x_hi;
+            const bool now = new_p && new_x >= dst.x_lo && new_x < dst.x_hi;
+            k[d] = row_kinds(was, now, la, ll, lp, f);
+            emit[d] = (k[d].k0 | k[d].k1 | k[d].k2) != 0;
+        }
+        bm[d] = wave_ballot(emit[d]);
+        if (lane_id() == 0) s_cnt[d][wv] = (uint32_t)popc64(bm[d]);
+    }
+    __syncthreads();
+    if (threadIdx.x < D.n) {
+        const uint32_t d = threadIdx.x;
+        uint32_t tot = 0;
+        for (uint32_t q = 0; q < RNW; ++q) tot += s_cnt[d][q];
         uint32_t base = 0;
-        if (lane_id() == leader) {
-            base = atomicAdd(&hs->cnt[d], (uint32_t)popc64(bm));
+        if (tot) {
+            base = atomicAdd(&hs->cnt[d], tot);
             // the same count by side in the all-gathered vector (>= 3 ranks: it
             // replaces the neighbours' count round); one destination = the
             // outer rank's only neighbour
-            if (F.cnt) atomicAdd(&F.cnt[F.nranks + 2 + (D.n == 2 ? d : (F.self == 0 ? 1u : 0u))], (uint32_t)popc64(bm));
+            if (F.cnt) atomicAdd(&F.cnt[F.nranks + 2 + (D.n == 2 ? d : (F.self == 0 ? 1u : 0u))], tot);
         }
-        base = __shfl(base, leader, 64);
-        if (!emit) continue;
-        const uint32_t e = base + (uint32_t)popc64(bm & lanemask_lt());
+        s_base[d] = base;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t d = 0; d < 2; ++d) {
+        if (!emit[d]) continue;
+        uint32_t e = s_base[d] + (uint32_t)popc64(bm[d] & lanemask_lt());
+        for (uint32_t q = 0; q < wv; ++q) e += s_cnt[d][q];
+        const HaloDst& dst = D.d[d];
         if (e >= dst.cap) {
             atomicAdd(&hs->overflow, 1ull);
             continue;
         }
-        put_triple(dst.rows + (size_t)e * ROWS, k, s, oa, op_pos, f, res, stamps, ll, la, i);
+        put_triple(dst.rows + (size_t)e * ROWS, k[d], s, oa, op_pos, f, res, stamps, ll, la, i);
     }
     if (lng && F.longs) {
         // the long-mover list (group teleports): state before and after the
@@ -314,7 +343,12 @@ void launch_route_halo(const World& w, const gw_op* ops, const unsigned long lon
         for (uint32_t d = 0; d < D.n; ++d) rows = std::max<uint64_t>(rows, (uint64_t)D.d[d].cap * ROWS);
     hipLaunchKernelGGL(k_route1, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, ol_tag, hs, stamps_out, stamp_base, F);
     hipLaunchKernelGGL(k_route2, dim3(nb), dim3(NT), 0, s, ops, n, w.cap, ol, ol_tag);
-    hipLaunchKernelGGL(k_route3, dim3(nb), dim3(NT), 0, s, ops, stamps, n, w, ol, ol_tag, max_step, D, hs, F);
+    if (n >= 65536)
+        hipLaunchKernelGGL(k_route3<1024>, dim3(nblk1(n, 1024)), dim3(1024), 0, s, ops, stamps, n, w, ol, ol_tag,
+                           max_step, D, hs, F);
+    else
+        hipLaunchKernelGGL(k_route3<NT>, dim3(nblk1(std::max<uint32_t>(n, 1u), NT)), dim3(NT), 0, s, ops, stamps, n, w,
+                           ol, ol_tag, max_step, D, hs, F);
     if (rows) hipLaunchKernelGGL(k_route4, dim3(nblk1(rows, NT)), dim3(NT), 0, s, D, hs);
 }
 

@@ -705,33 +705,53 @@ __global__ void __launch_bounds__(NT) k_sync_write_small2(World w, const uint32_
     const uint64_t lt = lanemask_lt();
     const float d = P.d;
     // the entity's list entry, then its state: position and gate are loaded
-    // with the AOI state (not behind the ownership test), and the next
-    // entity's list entry is in flight during this one's walk
+    // with the AOI state (not behind the ownership test)
     const auto entry = [&](uint32_t k, uint32_t& e, uint32_t& f, uint64_t& at, uint32_t& c) {
         e = f = c = 0;
         at = 0;
         if (k < hi) { e = flagged[k]; f = fbits[k]; at = rec_off[k]; c = cnt[k]; }
     };
-    uint32_t ne, nf, nc_;
-    uint64_t nat;
-    entry(lo + (threadIdx.x >> 6) * 2 + half, ne, nf, nat, nc_);
-    for (uint32_t k0 = lo + (threadIdx.x >> 6) * 2; k0 < hi; k0 += NWAVE * 2) {
+    // the next pair's states are loaded during this pair's walks and its list
+    // entries two pairs ahead (config #4 write 430 -> 422 us; the same in
+    // k_sync_write_h took it from 66 to 92 VGPRs and the 16M world's write
+    // from 852 to 976 us)
+    struct SwSt {
+        AoiEnt a;
+        float4 p;
+        uint32_t gt;
+    };
+    const auto state = [&](uint32_t k, uint32_t e, SwSt& x) {
+        x.a.x = x.a.z = 0.0f;
+        x.a.meta = 0;
+        x.p = make_float4(0, 0, 0, 0);
+        x.gt = 0;
+        if (k < hi) {
+            x.a = w.rec[e].a;
+            x.p = w.rec[e].p;
+            x.gt = w.gate[e];
+        }
+    };
+    constexpr uint32_t STEP = NWAVE * 2;
+    const uint32_t kfirst = lo + (threadIdx.x >> 6) * 2;
+    uint32_t ne, nf, nc_, ne2, nf2, nc2;
+    uint64_t nat, nat2;
+    entry(kfirst + half, ne, nf, nat, nc_);
+    entry(kfirst + STEP + half, ne2, nf2, nat2, nc2);
+    SwSt nst;
+    state(kfirst + half, ne, nst);
+    for (uint32_t k0 = kfirst; k0 < hi; k0 += STEP) {
         const uint32_t k = k0 + half;
         const bool valid = k < hi;
         const uint32_t e = ne, f = nf, c = nc_;
         uint64_t at = nat;
-        entry(k0 + NWAVE * 2 + half, ne, nf, nat, nc_);
+        const SwSt cs = nst;
+        ne = ne2; nf = nf2; nat = nat2; nc_ = nc2;
+        entry(k0 + 2 * STEP + half, ne2, nf2, nat2, nc2);
+        state(k0 + STEP + half, ne, nst);
         bool walk = false;
-        AoiEnt a;
-        a.x = a.z = 0.0f;
-        a.meta = 0;
-        float4 p = make_float4(0, 0, 0, 0);
-        uint32_t gt = 0;
-        if (valid) {
-            a = w.rec[e].a;
-            p = w.rec[e].p;
-            gt = w.gate[e];
-        }
+        const AoiEnt a = cs.a;
+        const float4 p = cs.p;
+        const uint32_t gt = cs.gt;
         if (valid) {
             if (at + c > rec_cap) {
                 if (hl == 0) atomicOr(&st->overflow, 1ull);

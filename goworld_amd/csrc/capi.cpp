@@ -1099,7 +1099,7 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
         bind_events(c, b);
         choose_buckets(c, b, bk_over || b.ev_full);
         DevStats* h = c->hstats;
-        h->overflow = 0; h->n_big = 0; h->ev_pk = 0; h->n_mlist = 0; h->n_sort = 0; h->bk_max = 0; h->n_items = 0; h->bk_tiles = 0; h->bk_cells = 0;
+        h->overflow = 0; h->n_big = 0; h->ev_pk = 0; h->n_mlist = 0; h->n_fall = 0; h->n_conflicts = 0; h->n_sort = 0; h->bk_max = 0; h->n_items = 0; h->bk_tiles = 0; h->bk_cells = 0;
         for (int i = 0; i < STAT_SHARDS; ++i)      // the diff's shards restart; the mover count (its
             for (int f = 0; f < SH_FIELDS; ++f)      // total in shard[0]) stays
                 if (f != SH_MOVERS || i) h->shard[i][f] = 0;
@@ -1124,6 +1124,7 @@ static int finish_tick(gw_ctx* c, gw_tick_out* out) {
     HIPCHK(hipGetLastError());
     DevStats& hs = *c->hstats;
     c->h_present = hs.n_present;
+    if (c->wd.on) c->wd.conflicts_acc += hs.n_conflicts;   // the final attempt's count (gw_world_status)
     gw_tick_out o{};
     const uint64_t n_enter = hs.ev_pk & 0xffffffffull, n_leave = hs.ev_pk >> 32;
     if (!(flags & GW_TICK_NO_EVENTS)) {                // sizes the next tick's buckets
@@ -1354,7 +1355,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.long_step = (c->wd.on && c->wd.g.ranks > 1) ? c->wd.g.max_step : INFINITY;
     b.longs = c->wd.tick_longs;                      // the long lists queued for this tick (world.cpp)
     b.n_long = c->wd.tick_nlong;
-    b.conflicts = c->wd.on ? &c->halo->conflicts : nullptr;
+    b.conflicts = c->wd.on ? &st->n_conflicts : nullptr;   // per attempt: a redo must not count twice
     c->wd.tick_longs = nullptr;
     c->wd.tick_nlong = 0;
     b.ol = c->ol;

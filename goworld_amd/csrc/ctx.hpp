@@ -83,6 +83,7 @@ struct WorldHost {
     uint32_t long_cap = 0, own_nlong = 0;
     const gw_long_move* tick_longs = nullptr;    // queued for the next gw_tick (then cleared)
     uint32_t tick_nlong = 0;
+    uint64_t conflicts_acc = 0;                  // long-mover conflicts of the ticks since gw_world_status
     std::vector<float> ext_h;                    // [2 * ranks] held x-range of every rank
     // host ops of a tick (gw_world_stage_ops): pinned staging, device copy, and
     // the event after the upload (the pinned buffer is reused once it fired)

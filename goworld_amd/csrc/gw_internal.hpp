@@ -139,6 +139,8 @@ struct DevStats {
     unsigned long long rec_total;     // sync: records
     unsigned long long n_heavy;       // heavy-first k_mover: primaries with >= heavy_min candidates (heavy[])
     unsigned long long n_fall;        // small-space diff: mover-grid entries left to k_mover_list (fall[])
+    unsigned long long n_conflicts;   // decomposed world: long-mover pairs the lists did not cover (this
+                                      // attempt; folded into the world's counter once per tick by the host)
     unsigned long long gate_base[GATE_DIRECT_MAX];   // sync, several gates: first record of gate g (gate_off)
     unsigned long long shard[STAT_SHARDS][SH_FIELDS];   // per-field sums in shard[0] on the host
 };
@@ -268,7 +270,7 @@ struct TickBufs {
                               // mover (its pairs are attributed to the targets' owners); +inf otherwise
     const gw_long_move* longs;   // decomposed world: every rank's long movers of the tick (group teleports:
     uint32_t n_long;             // their pairs are evaluated from these by the owner of the watcher)
-    unsigned long long* conflicts;   // decomposed world (else null): long-mover pairs the lists did not
+    unsigned long long* conflicts;   // decomposed world (else null; DevStats.n_conflicts): long-mover pairs the lists did not
                                      // cover (no list queued, or the watcher missing from it), HaloStats
     uint32_t dirty_span;      // GW_DIRTY_SPAN: cells whose dirty flags one k_grid_dirty wave scans (1..64)
     // launch-merge knobs (A/B and tests; gw_ctx reads them at gw_init): GW_BK_FLAT (-1 automatic,

@@ -589,6 +589,15 @@ int gw_world_status(gw_ctx* c, uint64_t* overflow, uint64_t* conflicts, uint64_t
     if (!c) return GW_EINVAL;
     if (int rs = settle(c)) return rs;
     (void)hipSetDevice(c->dev);
+    if (c->wd.conflicts_acc) {                       // the ticks' conflicts (DevStats, counted per attempt)
+        HaloStats h0{};
+        HIPCHK(hipMemcpyAsync(&h0, c->halo, sizeof h0, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        h0.conflicts += c->wd.conflicts_acc;
+        c->wd.conflicts_acc = 0;
+        HIPCHK(hipMemcpyAsync(c->halo, &h0, sizeof h0, hipMemcpyHostToDevice, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+    }
     if (xp_on(c) && c->c_nranks > 1) {                // the three counters are the first three u64 of HaloStats
         if (int rc = xp_allreduce_u64(c, (unsigned long long*)c->halo, 3, GW_RED_SUM)) return rc;
     }

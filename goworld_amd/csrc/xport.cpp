@@ -118,12 +118,16 @@ int local_group_end(gw_ctx* c) {
             snprintf(msg, sizeof msg, "rank %d sent %zu bytes, rank %d receives %zu", x.peer, po.bytes, me, x.bytes);
             return broken(c, G, msg);
         }
-        LGCHK(hipStreamWaitEvent(c->st, po.ready, 0));
-        (void)hipEventDestroy(po.ready);           // released once the recorded work completes
+        const hipError_t we = hipStreamWaitEvent(c->st, po.ready, 0);
+        (void)hipEventDestroy(po.ready);           // released once the recorded work completes (or on error)
+        LGCHK(we);
         if (x.bytes) LGCHK(hipMemcpyAsync(x.p, po.p, x.bytes, hipMemcpyDeviceToDevice, c->st));
         hipEvent_t dn = nullptr;
         LGCHK(hipEventCreateWithFlags(&dn, hipEventDisableTiming));
-        LGCHK(hipEventRecord(dn, c->st));
+        if (hipError_t e = hipEventRecord(dn, c->st)) {
+            (void)hipEventDestroy(dn);
+            LGCHK(e);
+        }
         {
             std::lock_guard<std::mutex> lk(G->mu);
             G->done[(size_t)x.peer * R + me].push_back(dn);

@@ -304,13 +304,17 @@ def config1(ticks: int = 1000, seed: int = 1, n: int = 1000, big_steps: bool = F
 
 
 def adversarial_trace(seed: int, n: int = 400, ticks: int = 30, d: float = 100.0,
-                      churn: bool = True, leave_masks: bool = False) -> SpaceTrace:
+                      churn: bool = True, leave_masks: bool = False, with_y: bool = False) -> SpaceTrace:
     """Non-dyadic float32 positions placed on the rounding edge of each other's
     windows (other.x == fl(c.x +- d) +- 1 ulp), so the rounded-bounds test is
     asymmetric and the seq rule decides.  With churn, ticks also contain
     Leave / re-Enter / Sync ops and repeated ops on one slot.  leave_masks:
     Leave ops carry a random keep-mask of pending sync bits (0..3; the entity
-    stays in the game in the nil space, Space.go:219-242) instead of 0."""
+    stays in the game in the nil space, Space.go:219-242) instead of 0.
+    with_y: every entity has a non-zero Position.Y and yaw, and every Enter /
+    Moved gives it a new Y and yaw (setPositionYaw sets both around
+    Space.move, Entity.go:1189-1205; SetYaw only the yaw): the sync payload
+    then differs from (x, 0, z, yaw) in every record."""
     d32 = np.float32(d)
     base_x = (rand_unit(stream_key(seed, 1), n) * 600 - 300).astype(np.float32)
     base_z = (rand_unit(stream_key(seed, 2), n) * 600 - 300).astype(np.float32)
@@ -328,10 +332,14 @@ def adversarial_trace(seed: int, n: int = 400, ticks: int = 30, d: float = 100.0
         base_z[i] = base_z[p] + np.float32(rand_unit(stream_key(seed, 7, int(i)), 1)[0] * 50)
     x, z = base_x.copy(), base_z.copy()
     yaw = np.zeros(n, np.float32)
+    y = np.zeros(n, np.float32)
+    if with_y:
+        y = (rand_unit(stream_key(seed, 8), n) * 97 - 40).astype(np.float32)
+        yaw = (rand_unit(stream_key(seed, 9), n) * 360 - 180).astype(np.float32)
     present = np.ones(n, dtype=bool)
     tr = SpaceTrace(n=n, capacity=n, d=float(d), bounds=(-500.0, -500.0, 500.0, 500.0),
                     init_slots=np.arange(n, dtype=np.uint32), init_x=x.copy(),
-                    init_y=np.zeros(n, np.float32), init_z=z.copy(), init_yaw=yaw.copy(), ticks=[])
+                    init_y=y.copy(), init_z=z.copy(), init_yaw=yaw.copy(), ticks=[])
     tr.gates = np.where(np.arange(n) % 5 == 4, 0, 1 + np.arange(n) % 3).astype(np.uint16)
     for t in range(ticks):
         k = stream_key(seed, 200, t)
@@ -340,6 +348,8 @@ def adversarial_trace(seed: int, n: int = 400, ticks: int = 30, d: float = 100.0
         kinds_r = rand_unit(stream_key(seed, 201, t), cnt)
         tgt = rand_int(stream_key(seed, 202, t), cnt, 0, n)
         edge_sgn = rand_unit(stream_key(seed, 203, t), cnt) < 0.5
+        ny = (rand_unit(stream_key(seed, 204, t), cnt) * 211 - 100).astype(np.float32)
+        nyaw = (rand_unit(stream_key(seed, 205, t), cnt) * 360 - 180).astype(np.float32)
         rows = []
         for j in range(cnt):
             a = int(picks[j])
@@ -348,16 +358,18 @@ def adversarial_trace(seed: int, n: int = 400, ticks: int = 30, d: float = 100.0
                     b = int(tgt[j])
                     nx = np.float32(x[b] + d32) if edge_sgn[j] else np.float32(x[b] - d32)
                     x[a], z[a] = nx, np.float32(z[b] + np.float32(kinds_r[j] * 30))
+                    if with_y:
+                        y[a], yaw[a] = ny[j], nyaw[j]
                     present[a] = True
-                    rows.append((OP_ENTER, 3, a, x[a], z[a], yaw[a]))
+                    rows.append((OP_ENTER, 3, a, x[a], y[a], z[a], yaw[a]))
                 continue
             if churn and kinds_r[j] < 0.05:
                 present[a] = False
                 mask = int(kinds_r[j] * 80) & 3 if leave_masks else 0
-                rows.append((OP_LEAVE, mask, a, x[a], z[a], yaw[a]))
+                rows.append((OP_LEAVE, mask, a, x[a], y[a], z[a], yaw[a]))
             elif churn and kinds_r[j] < 0.10:
-                yaw[a] = np.float32(kinds_r[j] * 31)
-                rows.append((OP_SYNC, 3, a, x[a], z[a], yaw[a]))
+                yaw[a] = nyaw[j] if with_y else np.float32(kinds_r[j] * 31)
+                rows.append((OP_SYNC, 3, a, x[a], y[a], z[a], yaw[a]))
             else:
                 b = int(tgt[j])
                 nx = np.float32(x[b] + d32) if edge_sgn[j] else np.float32(x[b] - d32)
@@ -365,7 +377,9 @@ def adversarial_trace(seed: int, n: int = 400, ticks: int = 30, d: float = 100.0
                     nx = np.nextafter(nx, np.float32(np.inf), dtype=np.float32)
                 x[a] = nx
                 z[a] = np.float32(z[b] + np.float32((kinds_r[j] - 0.5) * 120))
-                rows.append((OP_MOVED, 2 if kinds_r[j] < 0.5 else 3, a, x[a], z[a], yaw[a]))
+                if with_y:
+                    y[a], yaw[a] = ny[j], nyaw[j]
+                rows.append((OP_MOVED, 2 if kinds_r[j] < 0.5 else 3, a, x[a], y[a], z[a], yaw[a]))
         ops = make_ops(len(rows))
         if rows:
             arr = np.array(rows, dtype=object)
@@ -373,8 +387,9 @@ def adversarial_trace(seed: int, n: int = 400, ticks: int = 30, d: float = 100.0
             ops["sync_flags"] = arr[:, 1].astype(np.uint8)
             ops["slot"] = arr[:, 2].astype(np.uint32)
             ops["x"] = arr[:, 3].astype(np.float32)
-            ops["z"] = arr[:, 4].astype(np.float32)
-            ops["yaw"] = arr[:, 5].astype(np.float32)
+            ops["y"] = arr[:, 4].astype(np.float32)
+            ops["z"] = arr[:, 5].astype(np.float32)
+            ops["yaw"] = arr[:, 6].astype(np.float32)
         tr.ticks.append(ops)
     return tr
 

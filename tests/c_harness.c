@@ -14,7 +14,11 @@
  *             host); gw_sync_collect + gw_sync_encode_wire (the game->gate
  *             packets, Entity.go:1210-1266)
  *
- * usage: c_harness IN OUT
+ * usage: c_harness IN OUT [--server]
+ *   --server: every op goes through gw_submit with its own y / yaw payload
+ *             (the server-side Space.enter / Space.move / SetYaw path,
+ *             Space.go:179-252, Entity.go:1185-1205,1284-1290), none through
+ *             the client-record decode
  *   IN  (little-endian): "GWH1", u32 capacity, f32 d, f32 bounds[4], u32 n_init,
  *       u32 n_ticks; n_init x {u32 slot, f32 x, y, z, yaw}; capacity x u16 gate;
  *       per tick u32 n_ops + n_ops x gw_op (24 B)
@@ -59,13 +63,17 @@ static void fixed_uuid(uint32_t v, char out[16]) {
     }
 }
 
+static int server_only;   /* --server */
+
 static int is_client_move(const gw_op* o) {
-    return o->kind == GW_OP_MOVED && o->sync_flags == GW_SIF_NEIGHBOR_CLIENTS;
+    return !server_only && o->kind == GW_OP_MOVED && o->sync_flags == GW_SIF_NEIGHBOR_CLIENTS;
 }
 
 int main(int argc, char** argv) {
-    if (argc != 3) {
-        fprintf(stderr, "usage: c_harness IN OUT\n");
+    if (argc == 4 && !strcmp(argv[3], "--server")) {
+        server_only = 1;
+    } else if (argc != 3) {
+        fprintf(stderr, "usage: c_harness IN OUT [--server]\n");
         return 2;
     }
     FILE* in = fopen(argv[1], "rb");

@@ -5,7 +5,10 @@ usage: python3 tests/golden/export_gwh.py OUTDIR NAME...
   OUTDIR/NAME.gwh     the trace in the c_harness input format (tests/c_harness.c)
   OUTDIR/NAME.events  per tick: u64 n_enter, enters (u32 watcher, u32 target),
                       u64 n_leave, leaves -- the fixture's canonical net events
-Data only: the expected events are the committed fixtures' (tests/golden/*.npz).
+  OUTDIR/NAME.wire    per tick: u64 records of the collect, the 32-byte SHA-256
+                      of the game->gate packets with the records in canonical
+                      (gate(watcher), entity, watcher) order
+Data only: the expected outputs are the committed fixtures' (tests/golden/*.npz).
 """
 import os
 import struct
@@ -31,6 +34,10 @@ def main(argv):
                 for a in (e, l):
                     f.write(struct.pack("<Q", len(a)))
                     f.write(a.tobytes())
+        with open(os.path.join(out, f"{name}.wire"), "wb") as f:
+            for t in range(fx.ticks):
+                f.write(struct.pack("<Q", fx.n_rec(t)))
+                f.write(bytes.fromhex(fx.wire_sha(t)))
 
 
 if __name__ == "__main__":

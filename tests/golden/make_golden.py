@@ -150,6 +150,10 @@ def small_fixtures():
         # rounding-edge positions (asymmetric rounded windows) + Leave/re-Enter/Sync churn
         ("adversarial_s11", T.adversarial_trace(11, n=300, ticks=20), True),
         ("adversarial_s12", T.adversarial_trace(12, n=300, ticks=20), True),
+        # the same churn with non-zero Position.Y and yaw on every entity and
+        # op, server-side moves (OWN | NEIGHBOR) beside client ones, Leave
+        # keep-masks: the sync payload is (x, y, z, yaw) of the last op
+        ("server_y_s13", T.adversarial_trace(13, n=300, ticks=20, leave_masks=True, with_y=True), True),
         # dyadic walk (configs #2-#5 shape) with hotspots, 3 gates, 80% clients
         ("dyadic_hot_2k", T.dyadic_walk_trace(21, 2000, 2048.0, 100.0, 20, move_frac=0.25,
                                               hot_frac=0.4, n_hot=4, gate_count=3,

@@ -12,7 +12,7 @@ import numpy as np
 from goworld_amd import traces as T
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SMALL = ["cfg1_walk", "cfg1b_steps", "adversarial_s11", "adversarial_s12", "dyadic_hot_2k"]
+SMALL = ["cfg1_walk", "cfg1b_steps", "adversarial_s11", "adversarial_s12", "dyadic_hot_2k", "server_y_s13"]
 
 EVENT_DTYPE = np.dtype([("watcher", "<u4"), ("target", "<u4")])
 REC_DTYPE = np.dtype([("watcher", "<u4"), ("entity", "<u4"), ("x", "<f4"), ("y", "<f4"),

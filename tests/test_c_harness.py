@@ -122,24 +122,33 @@ def test_harness_is_built_and_fails_loudly_without_a_device(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["cfg1_walk", "dyadic_hot_2k", "adversarial_s11"])
-def test_c_harness_replays_golden_through_the_abi(tmp_path, name):
+@pytest.mark.parametrize("name,server", [("cfg1_walk", False), ("dyadic_hot_2k", False), ("adversarial_s11", False),
+                                         ("server_y_s13", False), ("server_y_s13", True)])
+def test_c_harness_replays_golden_through_the_abi(tmp_path, name, server):
+    """server: every op through gw_submit with its y / yaw (Space.enter /
+    Space.move / SetYaw on the game side); else the client moves go through the
+    32-B record decode.  server_y_s13 has a non-zero Y and yaw in every op and
+    initial position, so the records' payload is checked field by field."""
     fx = G.Fixture(name)
     tr = fx.trace
     _write_input(tmp_path / "in.bin", fx)
-    r = subprocess.run([HARNESS, str(tmp_path / "in.bin"), str(tmp_path / "out.bin")], capture_output=True,
-                       text=True, timeout=100)
+    r = subprocess.run([HARNESS, str(tmp_path / "in.bin"), str(tmp_path / "out.bin")] + (["--server"] if server else []),
+                       capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr
     out, applied = _read_output(tmp_path / "out.bin", fx.ticks)
     n_client = sum(int(np.sum((ops["kind"] == 2) & (ops["sync_flags"] == 2))) for ops in tr.ticks)
-    assert applied == n_client                              # every client record decoded into a Moved op
+    assert applied == (0 if server else n_client)           # every client record decoded into a Moved op
     if name == "cfg1_walk":
         assert applied > 1000
+    if name == "server_y_s13":
+        assert all(np.count_nonzero(ops["y"]) == len(ops) for ops in tr.ticks)
     for t, (e, l, wire, pk) in enumerate(out):
         ee, ll = fx.events(t)
         assert e.tobytes() == ee.tobytes() and l.tobytes() == ll.tobytes(), f"{name} tick {t}: events"
         recs = _parse_wire(wire, pk, tr.capacity)
         assert len(recs) == fx.n_rec(t)
+        if name == "server_y_s13" and len(recs):
+            assert np.count_nonzero(recs["y"]) == len(recs)     # Position.Y travels in every record
         canon = G.canonical_records(recs, tr.gates)
         assert G.sha(canon) == fx.rec_sha(t), f"{name} tick {t}: records"
         assert hashlib.sha256(_encode_like_oracle(canon, tr.gates)).hexdigest() == fx.wire_sha(t), \

@@ -64,13 +64,15 @@ def test_client_sync_decode_matches_op_stream():
                 s = int(op["slot"])
                 for rep in range(1 + (s % 7 == 0)):
                     x, z = float(op["x"]) + rep * 0.5, float(op["z"])
-                    recs.append(pyorc.fixed_uuid(s) + struct.pack("<4f", x, 0.0, z, float(op["yaw"])))
+                    # a non-zero Position.Y (the client's, Entity.go:430-435) that varies per record
+                    y = float(np.float32(17.25 - 0.37 * ((s * 31 + t * 7 + rep) % 101)))
+                    recs.append(pyorc.fixed_uuid(s) + struct.pack("<4f", x, y, z, float(op["yaw"])))
                     if syncing[s]:
                         e = np.zeros(1, T.OP_DTYPE)
                         e["kind"] = T.OP_MOVED
                         e["sync_flags"] = 2
                         e["slot"] = s
-                        e["x"], e["y"], e["z"], e["yaw"] = x, 0.0, z, op["yaw"]
+                        e["x"], e["y"], e["z"], e["yaw"] = x, y, z, op["yaw"]
                         expect.append(e)
                 if s % 11 == 0:                               # an id nobody registered
                     recs.append(pyorc.fixed_uuid(0x40000000 | s) + struct.pack("<4f", 1, 2, 3, 4))
@@ -88,6 +90,8 @@ def test_client_sync_decode_matches_op_stream():
             got_c["watcher"] -= base
             got_c["entity"] -= base
             assert got_c.tobytes() == exp.tobytes(), f"tick {t} records"
+            moved = np.isin(got_c["entity"], [int(e_["slot"][0]) for e_ in expect])
+            assert np.count_nonzero(got_c["y"][moved]) == np.count_nonzero(moved) > 0   # the decoded Y is in the records
     finally:
         g.close()
         o.close()

@@ -703,3 +703,42 @@ def test_half_wave_walk_fallbacks(ctx_factory, half_rows, monkeypatch):
         h.step(t)
         h.check_collect()
     h.check_lists()
+
+
+def test_small_space_redo_with_fallbacks(ctx_factory, monkeypatch):
+    """Small-space mode with every pair on the fallback list (GW_HALF_ROWS=0)
+    and dense spaces whose first tick overflows the own-event regions and the
+    event buffers, so the tick's diff + events are redone: the redo must start
+    the fallback list (DevStats.n_fall) afresh instead of appending the first
+    attempt's entries again.  Events, records and neighbour lists
+    against the oracle over 6 dense spaces with 2 gates."""
+    monkeypatch.setenv("GW_HALF_ROWS", "0")
+    g = ctx_factory()                                   # gw_init reads GW_HALF_ROWS
+    monkeypatch.delenv("GW_HALF_ROWS")
+    trs = []
+    for s in range(6):
+        n = 480
+        rng = np.random.default_rng(900 + s)
+        x = (rng.integers(0, 240, n) * 0.5).astype(np.float32)
+        z = (rng.integers(0, 240, n) * 0.5).astype(np.float32)
+        tr = T.SpaceTrace(n=n, capacity=n, d=100.0, bounds=(-200, -200, 320, 320),
+                          init_slots=np.arange(n, dtype=np.uint32), init_x=x, init_y=np.zeros(n, np.float32),
+                          init_z=z, init_yaw=np.zeros(n, np.float32), ticks=[],
+                          gates=np.where(np.arange(n) % 3 == 0, 0, 1 + (np.arange(n) + s) % 2).astype(np.uint16))
+        for t in range(3):
+            m = n // 3
+            ops = T.make_ops(m)
+            ops["kind"] = T.OP_MOVED
+            ops["sync_flags"] = 3
+            ops["slot"] = np.arange(t, n, 3)[:m]
+            ops["x"] = np.where(np.arange(m) % 2 == 0, 150.0 + 4 * t, 10.0 + t).astype(np.float32)
+            ops["z"] = (rng.integers(0, 240, m) * 0.5).astype(np.float32)
+            ops["yaw"] = np.float32(t)
+            tr.ticks.append(ops)
+        trs.append(tr)
+    h = Harness(g, trs)
+    h.check_collect()
+    for t in range(3):
+        h.step(t)
+        h.check_collect()
+    h.check_lists()

@@ -127,29 +127,42 @@ __device__ __forceinline__ Flat flat_from(uint32_t s, uint32_t l) {
 // lists).  SPAN: the ranges live in lanes [0, SPAN) (16 for the row ranges
 // k_bounds hands to k_mover: two fewer dependent shuffles per chunk); the
 // index is then one more shuffle, of start - pre (mod 2^32).
+// The U chunks' searches run step by step together (their shuffles of one
+// step in flight at once, one wait), and the first step, whose probe is the
+// same lane for every lane, is a readlane: a chain of log2(SPAN) dependent
+// shuffle rounds per U chunks instead of U * (log2(SPAN) + 1).
 template <int U, int NK, int SPAN = 64>
 __device__ __forceinline__ void flat_map(Flat& f, uint32_t B, uint32_t (&idx)[U], uint32_t (&kind)[U]) {
     const int ln = lane_id();
     const uint32_t off = f.start - f.pre;
+    uint32_t k[U], lo[U];
+    const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)f.pre, SPAN / 2);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        idx[u] = ~0u;
-        kind[u] = 0;
+        k[u] = B + 64u * u + (uint32_t)ln;
+        lo[u] = p0 <= k[u] ? (uint32_t)(SPAN / 2) : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        if (B + 64u * u >= f.total) break;                  // wave-uniform: chunk past the end
-        const uint32_t k = B + 64u * u + (uint32_t)ln;
-        uint32_t lo = 0;
+    for (int step = SPAN / 4; step; step >>= 1) {
+        uint32_t p[U];
 #pragma unroll
-        for (int step = SPAN / 2; step; step >>= 1) {
-            const uint32_t c = lo + (uint32_t)step;
-            const uint32_t p = (uint32_t)__shfl((int)f.pre, (int)(SPAN == 64 ? min(c, 63u) : c), 64);
-            if ((SPAN < 64 || c < 64u) && p <= k) lo = c;
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = lo[u] + (uint32_t)step;
+            p[u] = (uint32_t)__shfl((int)f.pre, (int)(SPAN == 64 ? min(c, 63u) : c), 64);
         }
-        const uint32_t o = (uint32_t)__shfl((int)off, (int)lo, 64);
-        idx[u] = k < f.total ? o + k : ~0u;
-        kind[u] = NK == 2 ? (lo & 1u) : 0u;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = lo[u] + (uint32_t)step;
+            if ((SPAN < 64 || c < 64u) && p[u] <= k[u]) lo[u] = c;
+        }
+    }
+    uint32_t o[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) o[u] = (uint32_t)__shfl((int)off, (int)lo[u], 64);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        idx[u] = k[u] < f.total ? o[u] + k[u] : ~0u;
+        kind[u] = NK == 2 ? (lo[u] & 1u) : 0u;
     }
 }
 

@@ -103,7 +103,7 @@ __global__ void __launch_bounds__(NT) k_ops2(TickBufs b) {
 // last Leave that cleared c.  The slot's last Leave clears in k_ops3, every
 // op's bits after it are OR'd in by k_place (a later launch: clear, then OR).
 __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, uint32_t A, const AoiEnt& a,
-                                                const PrevEnt& p, bool lng, bool cl, uint32_t gidx);
+                                                const PrevEnt& p, bool lng, uint32_t gate, uint32_t gidx);
 
 // Per op: the syncInfoFlag bits, the sync payload of the slot's last
 // non-Leave op; the slot's last AOI op saves the pre-tick position and stamp
@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
     uint32_t s = 0, fbits = 0;
     AoiEnt a;
     PrevEnt p;
-    bool cl = false;
+    uint32_t gate = 0;
     uint32_t gidx = 0;
     if (i < b.m) {
         const gw_op op = b.ops[i];
@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
             const AoiEnt a0 = b.w.rec[s].a;
             const unsigned long long st0 = b.w.rec[s].stamp;
             gidx = b.w.rec[s].gidx;
-            cl = b.w.gate[s] != 0;
+            gate = b.w.gate[s];
             struct { int32_t pos, aoi, leave, clr[2]; } ol;
             ol.pos = ol_get(o.pos, b.ol_tag);
             ol.aoi = ol_get(o.aoi, b.ol_tag);
@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
     const uint32_t nw = (uint32_t)popc64(wave_ballot(mv));
     if (lane_id() == 0 && nw) shard_add(b.st, blockIdx.x * NWAVE + (threadIdx.x >> 6), SH_MOVERS, nw);
     uint2 cc = make_uint2(NO_CELL, NO_CELL);
-    if (mv) cc = classify_mover(b, i, s, a, p, lng, cl, gidx);
+    if (mv) cc = classify_mover(b, i, s, a, p, lng, gate, gidx);
     if (i < b.m) b.mcell[i] = make_uint4(cc.x, cc.y, s, fbits);   // k_place reads them back coalesced
 }
 
@@ -230,7 +230,7 @@ __global__ void __launch_bounds__(NT) k_grid_fill(World w, const uint32_t* __res
         const AoiEnt a = w.rec[s].a;
         GEnt e;
         e.x = a.x; e.z = a.z; e.slot = s;
-        e.meta = key | (w.gate[s] ? CLIENT_BIT : 0u);
+        e.meta = key | gate_meta(w.gate[s]);
         w.gn[i] = e;
     }
 }
@@ -279,7 +279,7 @@ void grid_rebuild(const World& w, DevStats* st, uint32_t* k0, uint32_t* v0, uint
 // mover's mover-grid entry (tags aside) goes to mtmp[i] and its cells are
 // returned for mcell[i], so k_place reads them coalesced.
 __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, uint32_t A, const AoiEnt& a,
-                                                const PrevEnt& p, bool lng, bool cl, uint32_t gidx) {
+                                                const PrevEnt& p, bool lng, uint32_t gate, uint32_t gidx) {
     const SpaceP P = b.w.sp[a.meta & SPACE_MASK];
     uint32_t co = NO_CELL, cn = NO_CELL;
     if (p.ox == p.ox) co = cell_of(P, p.ox, p.oz);
@@ -289,7 +289,7 @@ __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, u
         MEnt m;
         m.x = pn ? a.x : qnan(); m.z = pn ? a.z : qnan();
         m.ox = p.ox; m.oz = p.oz;
-        m.slot = A; m.tags = lng ? TAG_LONG : 0u; m.client = cl ? 1u : 0u; m.space = a.meta & SPACE_MASK;
+        m.slot = A; m.tags = lng ? TAG_LONG : 0u; m.client = gate; m.space = a.meta & SPACE_MASK;   // client: its gate
         b.mtmp[i] = m;
     }
     const uint32_t at = co != NO_CELL ? b.w.gn_start[co] + gidx : 0u;   // (loaded before the atomics)
@@ -298,7 +298,7 @@ __device__ __forceinline__ uint2 classify_mover(const TickBufs& b, uint32_t i, u
     if (co != NO_CELL && co == cn) {
         GEnt e;
         e.x = a.x; e.z = a.z; e.slot = A;
-        e.meta = cn | (cl ? CLIENT_BIT : 0u) | b.mbit;
+        e.meta = cn | gate_meta(gate) | b.mbit;
         b.w.gn[at] = e;
     } else {
         if (co != NO_CELL) {
@@ -353,7 +353,7 @@ __device__ __forceinline__ void place_one(const TickBufs& b, uint32_t i) {
         rn = atomicSub(&b.gm_cnt[cn], 1u);
         ra = atomicSub(&b.arr[cn], 1u);
     }
-    const bool cl = e.client != 0;
+    const uint32_t gm_meta = gate_meta(e.client);            // (the mover's gate)
     if (co != NO_CELL) {
         e.tags = (e.tags & TAG_LONG) | TAG_OLD | (cn == co ? TAG_NEW | TAG_PRIMARY : 0u) | (pn ? 0u : TAG_PRIMARY);
         b.gm[so + ro - 1u] = e;
@@ -364,7 +364,7 @@ __device__ __forceinline__ void place_one(const TickBufs& b, uint32_t i) {
         const uint32_t kept = (g1 - g0) - (dp & ~CELL_DIRTY);
         GEnt g;
         g.x = e.x; g.z = e.z; g.slot = e.slot;
-        g.meta = cn | (cl ? CLIENT_BIT : 0u) | b.mbit;
+        g.meta = cn | gm_meta | b.mbit;
         b.gn_nxt[nx + kept + ra - 1u] = g;
     }
 }
@@ -624,10 +624,11 @@ void tick_movers(const TickBufs& b, ScanCtx& sc, hipStream_t s, const TickBufs* 
 struct Cand {
     float x, z, ox, oz;
     uint32_t slot;
-    uint32_t info;       // tags | CAND_CLIENT | CAND_NONMOVER
+    uint32_t info;       // tags | CAND_CLIENT | CAND_NONMOVER | (GW) gate id & 15 << CAND_GATE
 };
 constexpr uint32_t CAND_NONMOVER = 1u << 31;
 constexpr uint32_t CAND_CLIENT = 1u << 30;
+constexpr int CAND_GATE = 24;
 
 // Where a walk reads its candidates: the row starts of both grids (Flat of a
 // mover's rectangles) and the entries, in HBM or, in small-space mode, LDS
@@ -699,8 +700,11 @@ __device__ __forceinline__ void long_pairs(const TickBufs& b, uint32_t A, int32_
 // RR (k_mover): the row ranges k_bounds gathered, loaded with the entry
 // itself (the walk then starts one round trip after the wave does).
 // LONGS = false: a context without long movers (not a world of >= 2 strips,
-// TickBufs::long_step infinite) compiles the group-teleport paths out
-template <int DIFF_U, uint32_t SCAP, class Src, bool RR = false, bool LONGS = true>
+// TickBufs::long_step infinite) compiles the group-teleport paths out.
+// GW > 0 (2 < G <= 4 * GW gates): the new neighbours with a client are also
+// counted per gate (World.nbg), so a multi-gate collect right after the tick
+// takes its per-gate record counts from there instead of walking the window
+template <int DIFF_U, uint32_t SCAP, class Src, bool RR = false, bool LONGS = true, int GW = 0>
 __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_t* lds, const Src& S) {
     const int ln = lane_id();
     const uint2 rr = (RR && ln < (int)(2 * RR_ROWS)) ? ((const uint2*)b.rowrec)[m * 2 * RR_ROWS + ln]
@@ -748,6 +752,11 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     // count and chunk was ~10 scalar instructions of every chunk's chain)
     uint32_t l_old = 0, l_new = 0, l_cli = 0, l_nl = 0, l_nml = 0;
     uint32_t l_lc = 0;      // (LONGS) pairs with another long mover related before or after the tick
+    // (GW) per-lane counts by gate: 8 bits per gate, gate g in byte g % 4 of
+    // l_g[g / 4] (GW VGPRs: 16-bit fields cost k_mover_c a wave of residency);
+    // exact while every lane's l_cli <= 255, else the split is not published
+    constexpr bool GATES = GW > 0;
+    uint32_t l_g[GW > 0 ? GW : 1] = {};
     Flat f;
     // the row ranges k_bounds gathered (<= RR_ROWS rows x 2 grids: lanes 0..15)
     const bool rr_ok =
@@ -794,7 +803,10 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
                                      : (TAG_OLD | TAG_NEW | (meta & CLIENT_BIT ? CAND_CLIENT : 0u) | CAND_NONMOVER);
             const bool valid = idx[u] != ~0u;
             cc[u].slot = valid ? slot : A;                     // invalid: skipped below
-            cc[u].info = valid ? info : 0u;
+            const uint32_t gbits = !GATES ? 0u
+                                 : gm   ? (q1[u].z & 15u) << CAND_GATE
+                                        : (meta & GATE_MASK) >> (GATE_SHIFT - CAND_GATE);
+            cc[u].info = valid ? info | gbits : 0u;
         }
 #pragma unroll
         for (int u = 0; u < DIFF_U; ++u) {
@@ -831,6 +843,12 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             l_old += (uint32_t)t_ro;
             l_new += (uint32_t)t_rn;
             l_cli += (uint32_t)t_cli;
+            if (GATES) {
+                const uint32_t gid = (e.info >> CAND_GATE) & 15u;
+                const uint32_t inc = t_cli ? (1u << (8u * (gid & 3u))) : 0u;
+#pragma unroll
+                for (uint32_t j = 0; j < (uint32_t)GW; ++j) l_g[j] += (gid >> 2) == j ? inc : 0u;
+            }
             // B has no op: (B,A) is B's event too (kept in A's region; the
             // events stage places it)
             const bool mev = ev & nmv & owned_x(P, e.x);
@@ -902,6 +920,24 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
         }
     }
     const uint32_t so = c_old, sn = c_new, scl = c_cli;
+    // (GATES) the split is exact when no lane's byte can have wrapped
+    const bool g_ok = GATES && pn && !wave_ballot(l_cli > 255u);
+    if (g_ok) {
+        // the wave's per-gate sums in 16-bit fields (<= 64 x 255): bytes 0, 2
+        // and 1, 3 of each word summed apart, then laid out as World.nbg
+        unsigned long long v = 0;
+#pragma unroll
+        for (int j = 0; j < GW; ++j) {
+            const uint32_t se = wave_incl_scan<uint32_t>(l_g[j] & 0x00ff00ffu);         // gates 4j, 4j+2
+            const uint32_t so_ = wave_incl_scan<uint32_t>((l_g[j] >> 8) & 0x00ff00ffu); // gates 4j+1, 4j+3
+            const uint32_t te = (uint32_t)__builtin_amdgcn_readlane((int)se, 63);
+            const uint32_t to = (uint32_t)__builtin_amdgcn_readlane((int)so_, 63);
+            const unsigned long long t = (unsigned long long)(te & 0xffffu) | ((unsigned long long)(to & 0xffffu) << 16) |
+                                         ((unsigned long long)(te >> 16) << 32) | ((unsigned long long)(to >> 16) << 48);
+            if (ln == j) v = t;
+        }
+        if (ln < 4) w.nbg[(uint64_t)A * 4 + ln] = v;
+    }
     if (ln == 0) {
         b.ownc[m] = (unsigned long long)(n - nl) | ((unsigned long long)nl << 32);
         b.mirc[m] = (unsigned long long)(nm_ - nml) | ((unsigned long long)nml << 32);
@@ -909,7 +945,7 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             atomicOr(&b.movbit[A >> 5], 1u << (A & 31u));
             b.gmi[A] = (uint32_t)m;
         }
-        if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | scl;
+        if (pn) w.nbc[A] = ((unsigned long long)w.epoch << 32) | scl | (g_ok ? NBC_GATES : 0u);
         // per-mover statistics, summed by k_mover_post (no atomics here: 2 per
         // mover into 256 shards cost 25 us at config #3 and 180 us at config #4)
         b.mstat[m] = (unsigned long long)so | ((unsigned long long)sn << 32);
@@ -929,10 +965,13 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
 #else
 #define KMOVER_SGPR
 #endif
+// 8 waves per SIMD also with the split by gate (GW = 2: 65 VGPRs uncapped, 7
+// waves; capped, no spill)
+#define KMOVER_OCC __attribute__((amdgpu_waves_per_eu(8, 8)))
 // one wave per primary entry (pidx, cell order): no wave is dispatched for
 // the secondary entries (half the mover grid), whose zeros k_bounds wrote
-template <int DIFF_U, bool LONGS>
-__global__ void __launch_bounds__(64) KMOVER_SGPR k_mover_c(TickBufs b) {
+template <int DIFF_U, bool LONGS, int GW>
+__global__ void __launch_bounds__(64) KMOVER_SGPR KMOVER_OCC k_mover_c(TickBufs b) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[SORT_LDS];
     const uint64_t k = blockIdx.x;
     const uint64_t np = b.st->cand_total >> PRIM_SHIFT;
@@ -945,7 +984,8 @@ __global__ void __launch_bounds__(64) KMOVER_SGPR k_mover_c(TickBufs b) {
         m = b.pidx[k];                            // in bounds (k < ops), read with the count
         if (k >= np) return;
     }
-    mover_one<DIFF_U, SORT_LDS, GlobalSrc, true, LONGS>(b, m, lds, GlobalSrc{b.w.gn, b.w.gn_start, b.gm_start, b.gm});
+    mover_one<DIFF_U, SORT_LDS, GlobalSrc, true, LONGS, GW>(b, m, lds,
+                                                               GlobalSrc{b.w.gn, b.w.gn_start, b.gm_start, b.gm});
 }
 
 template <int DIFF_U, int WPB>
@@ -2199,10 +2239,18 @@ void tick_diff(const TickBufs& b, hipStream_t s) {
         return;
     }
     if (b.compact) {                       // one wave per primary entry (<= one per op)
-        if (std::isinf(b.long_step))       // no long movers: the group-teleport paths compiled out
-            hipLaunchKernelGGL((k_mover_c<2, false>), dim3(nblk1(b.m, 1)), dim3(64), 0, s, b);
-        else
-            hipLaunchKernelGGL((k_mover_c<2, true>), dim3(nblk1(b.m, 1)), dim3(64), 0, s, b);
+        const dim3 g(nblk1(b.m, 1));
+        // gate words: 0, or 2 (<= 8 gate ids) / 4 per lane for the split by gate
+        const int gw = b.gate_counts ? (b.gate_counts <= 8 ? 2 : 4) : 0;
+        if (std::isinf(b.long_step)) {     // no long movers: the group-teleport paths compiled out
+            if (gw == 2) hipLaunchKernelGGL((k_mover_c<2, false, 2>), g, dim3(64), 0, s, b);
+            else if (gw == 4) hipLaunchKernelGGL((k_mover_c<2, false, 4>), g, dim3(64), 0, s, b);
+            else hipLaunchKernelGGL((k_mover_c<2, false, 0>), g, dim3(64), 0, s, b);
+        } else {
+            if (gw == 2) hipLaunchKernelGGL((k_mover_c<2, true, 2>), g, dim3(64), 0, s, b);
+            else if (gw == 4) hipLaunchKernelGGL((k_mover_c<2, true, 4>), g, dim3(64), 0, s, b);
+            else hipLaunchKernelGGL((k_mover_c<2, true, 0>), g, dim3(64), 0, s, b);
+        }
         return;
     }
     switch (b.diff_u) {                    // GW_MOVER_WPB: waves per k_mover block

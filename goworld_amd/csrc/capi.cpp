@@ -233,6 +233,7 @@ int grow_slots(gw_ctx* c, uint32_t new_total) {
     if ((rc = grow_preserve(c, c->flags, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->gate, oc, nc))) return rc;
     if ((rc = grow_preserve(c, c->nbc, oc, nc))) return rc;
+    if ((rc = grow_preserve(c, c->nbg, (size_t)oc * 4, (size_t)nc * 4))) return rc;   // read only under NBC_GATES
     if ((rc = grow_preserve(c, c->movbit, 0, (size_t)nc / 32 + 1))) return rc;
     if ((rc = grow_preserve(c, c->gmi, 0, (size_t)nc))) return rc;
     if ((rc = grow_preserve(c, c->eid_dev, oc, nc))) return rc;
@@ -383,6 +384,7 @@ World world(gw_ctx* c) {
     w.rec = c->rec; w.flags = c->flags; w.gate = c->gate;
     w.gn = c->gnb[c->gcur]; w.gn_start = c->gsb[c->gcur];
     w.nbc = c->nbc;
+    w.nbg = c->nbg;
     w.epoch = c->epoch;
     w.nb_u = c->nb_u;
     return w;
@@ -607,7 +609,7 @@ void gw_shutdown(gw_ctx* c) {
     DevBuf* hb[] = {&c->h_enter, &c->h_leave, &c->h_rec, &c->h_cl_slot, &c->h_cl_off, &c->h_items, &c->m_create.h,
                     &c->m_destroy.h, &c->m_fanout.h};
     for (DevBuf* b : hb) if (b->p) (void)hipHostFree(b->p);
-    void* ps[] = {c->halo, c->sc.ticket, c->sc2.ticket, c->movbit, c->gmi, c->rec, c->flags, c->gate, c->nbc, c->ol,
+    void* ps[] = {c->halo, c->sc.ticket, c->sc2.ticket, c->movbit, c->gmi, c->rec, c->flags, c->gate, c->nbc, c->nbg, c->ol,
                   c->gnb[0], c->gnb[1], c->sp_dev, c->stats, c->scal32, c->gsb[0],
                   c->gsb[1], c->dep, c->arr, c->gm_cnt, c->cnt_new, c->dirty, c->gm_start};
     for (void* p : ps) if (p) (void)hipFree(p);
@@ -640,7 +642,8 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
     if (!(b[2] > b[0]) || !(b[3] > b[1]) || !std::isfinite(b[0]) || !std::isfinite(b[1]) || !std::isfinite(b[2]) ||
         !std::isfinite(b[3]))
         return set_err(c, GW_EINVAL, "bad bounds");
-    // square cells of side >= d / cells_per_d; at most 8192 cells per axis; a
+    // square cells of side >= d / cells_per_d; at most 4096 cells per axis (a
+    // space's cells then fit the 25 cell bits of a grid entry); a
     // search window (2d plus the rounding margin of dev_common.hpp
     // search_rect) spans at most 11 rows, so a mover's two windows fit the
     // 32 row ranges of one wave (Flat)
@@ -648,7 +651,7 @@ int gw_space_create(gw_ctx* c, float aoi_dist, uint32_t capacity, const float* b
     double maxabs = std::max(std::max(std::fabs((double)b[0]), std::fabs((double)b[2])),
                              std::max(std::fabs((double)b[1]), std::fabs((double)b[3])));
     double span = 2.0 * aoi_dist + 4e-6 * (maxabs + aoi_dist) + 1e-3;
-    double cs = std::max((double)aoi_dist / c->cells_per_d, std::max(ex, ez) / 8192.0);
+    double cs = std::max((double)aoi_dist / c->cells_per_d, std::max(ex, ez) / 4096.0);
     cs = std::max(cs, span / 9.0);
     SpaceHost s{};
     s.d = aoi_dist;
@@ -1356,6 +1359,9 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.longs = c->wd.tick_longs;                      // the long lists queued for this tick (world.cpp)
     b.n_long = c->wd.tick_nlong;
     b.conflicts = c->wd.on ? &st->n_conflicts : nullptr;   // per attempt: a redo must not count twice
+    // (the multi-gate collect; GW_GATE_COUNTS=0: its count pass walks every window, A/B)
+    static const bool gcounts_on = !getenv("GW_GATE_COUNTS") || atoi(getenv("GW_GATE_COUNTS")) != 0;
+    b.gate_counts = (gcounts_on && c->max_gate + 1u > 2u && c->max_gate + 1u <= GATE_DIRECT_MAX) ? c->max_gate + 1u : 0u;
     c->wd.tick_longs = nullptr;
     c->wd.tick_nlong = 0;
     b.ol = c->ol;

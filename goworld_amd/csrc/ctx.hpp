@@ -176,6 +176,7 @@ struct gw_ctx {
     uint32_t* flags = nullptr;
     uint16_t* gate = nullptr;
     unsigned long long* nbc = nullptr;       // [slot_cap] epoch<<32 | neighbours with a client
+    unsigned long long* nbg = nullptr;       // [slot_cap * 4] the same split by gate (World.nbg)
     uint32_t* movbit = nullptr;              // [slot_cap/32 + 1] movers of the tick, zero between ticks
     uint32_t* gmi = nullptr;                 // [slot_cap] primary mover-grid entry of a mover
     gw::OpLast* ol = nullptr;                // [slot_cap] per-op dedupe state (session-tagged words)

@@ -71,7 +71,7 @@ __device__ __forceinline__ int32_t ol_get(unsigned long long v, uint32_t tag) {
 struct alignas(16) GEnt {
     float x, z;
     uint32_t slot;     // DEPARTED: the entity left this cell during the tick being built
-    uint32_t meta;     // cell | CLIENT_BIT | MOVER_A / MOVER_B
+    uint32_t meta;     // cell | gate id (< 16) | CLIENT_BIT | MOVER_A / MOVER_B
 };
 // moved this tick (its pairs come from the mover grid): the tick's bit
 // alternates between ticks (TickBufs::mbit), and the grid rebuild of the next
@@ -79,7 +79,16 @@ struct alignas(16) GEnt {
 constexpr uint32_t MOVER_A = 0x80000000u;
 constexpr uint32_t MOVER_B = 0x20000000u;
 constexpr uint32_t CLIENT_BIT = 0x40000000u;   // has a client (GameClient != nil)
-constexpr uint32_t CELL_MASK = 0x1fffffffu;
+constexpr uint32_t CELL_MASK = 0x01ffffffu;    // cells of a context: < 2^25 (capi.cpp)
+// the client's gate id when it is below 16 (a collect with at most 16 gate
+// ids reads a watcher's gate from its grid entry, no gather of gate[slot])
+constexpr uint32_t NBC_GATES = 0x80000000u;    // nbc low word: nbg holds the per-gate split (World.nbg)
+constexpr uint32_t NBC_COUNT = 0x7fffffffu;
+constexpr int GATE_SHIFT = 25;
+constexpr uint32_t GATE_MASK = 0xfu << GATE_SHIFT;
+__host__ __device__ inline uint32_t gate_meta(uint32_t gate) {
+    return gate ? (CLIENT_BIT | ((gate < 16u ? gate : 0u) << GATE_SHIFT)) : 0u;
+}
 constexpr uint32_t DEPARTED = 0xffffffffu;
 constexpr uint32_t CELL_DIRTY = 0x80000000u;   // flag in dep[c]: the cell is re-sorted this tick
 
@@ -191,6 +200,10 @@ struct World {
     // (epoch<<32 | count), written for every present mover by the diff; a
     // collect right after that tick takes it instead of walking e's window
     unsigned long long* nbc;
+    // with NBC_GATES set in nbc[e]: nbg[4e .. 4e+3] = the same count split by
+    // the watchers' gate ids (16 bits per gate, gate g in word g / 4 at bit
+    // 16 * (g % 4)), written by k_mover_c in a context with 2 < G <= 16
+    unsigned long long* nbg;
     uint32_t epoch;            // current epoch (bumped by every tick and client change)
     int nb_u;                  // candidate chunks of 64 in flight in the sync walks
 };
@@ -270,6 +283,7 @@ struct TickBufs {
                               // mover (its pairs are attributed to the targets' owners); +inf otherwise
     const gw_long_move* longs;   // decomposed world: every rank's long movers of the tick (group teleports:
     uint32_t n_long;             // their pairs are evaluated from these by the owner of the watcher)
+    uint32_t gate_counts;     // G when 2 < G <= GATE_DIRECT_MAX (k_mover_c splits nbc by gate, World.nbg), else 0
     unsigned long long* conflicts;   // decomposed world (else null; DevStats.n_conflicts): long-mover pairs the lists did not
                                      // cover (no list queued, or the watcher missing from it), HaloStats
     uint32_t dirty_span;      // GW_DIRTY_SPAN: cells whose dirty flags one k_grid_dirty wave scans (1..64)

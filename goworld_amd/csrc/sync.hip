@@ -15,7 +15,8 @@ namespace gw {
 
 // ---------------------------------------------------------------------------
 // neighbours of a present entity e from the current grid: calls
-// f(rel, w, has_client) per lane for every candidate (rel: w != e is related to e).
+// f(rel, w, client) per lane for every candidate (rel: w != e is related to e;
+// client: w's grid-entry bits CLIENT_BIT | gate id < 16, 0 without a client).
 // The window's row ranges are walked flattened, NB_U chunks of 64 in flight.
 // (wave_neighbors_of: e's state a and its space P already loaded)
 template <int NB_U = 4, typename F>
@@ -54,7 +55,7 @@ __device__ __forceinline__ void wave_neighbors_of(const World& w, uint32_t e, co
                     }
                 }
             }
-            f(rel, g.slot, (g.meta & CLIENT_BIT) ? 1u : 0u);
+            f(rel, g.slot, g.meta & (CLIENT_BIT | GATE_MASK));
         }
     }
 }
@@ -200,7 +201,7 @@ __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __re
             if (owned_x(w.sp[a.meta & SPACE_MASK], a.x)) {
                 if ((f & GW_SIF_OWN_CLIENT) && gt) r = 1;
                 if ((f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
-                    if ((uint32_t)(c >> 32) == w.epoch) r += (uint32_t)c;   // counted by this tick's diff
+                    if ((uint32_t)(c >> 32) == w.epoch) r += (uint32_t)c & NBC_COUNT;   // counted by this tick's diff
                     else walk = true;
                 }
             }
@@ -619,7 +620,7 @@ __device__ __forceinline__ void wave_neighbors_lds(const World& w, uint32_t e, c
                     }
                 }
             }
-            f(rel, g.slot, (g.meta & CLIENT_BIT) ? 1u : 0u);
+            f(rel, g.slot, g.meta & (CLIENT_BIT | GATE_MASK));
         }
     }
 }
@@ -883,45 +884,82 @@ void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* 
 // then the neighbours in walk order) -- what a stable sort of the stream by
 // gate gives (Entity.go:1208-1219 sends one packet per gate), computed
 // without the sort and without a second host sync:
-//   count: a wave per flagged entry, counts per (gate, entry) in gate-major
-//          cnt[g * nf_max + k] (the diff's cached neighbour counts have no
-//          gates, so every neighbour list is walked, the watcher's gate read
-//          per related candidate with a client);
+//   count: a lane per flagged entry, counts per (gate, entry) in gate-major
+//          cnt[g * nf_max + k]: a mover of this tick's diff from its per-gate
+//          split (World.nbg, NBC_GATES); any other entry's window is walked by
+//          the whole wave (the watcher's gate from its grid entry);
 //   scan:  one exclusive scan over the G * nf_max counts gives every (gate,
 //          entry) its first record, and gate g's first record at g * nf_max;
 //   write: a wave per entry holds the next position of each gate in lanes
 //          0..G-1 and stores each record at its gate's position (ranks inside
 //          a chunk by one ballot per gate); the gates' first records go to
 //          DevStats.gate_base, read with the collect's one host sync.
+#ifndef GW_CG_EPW
+#define GW_CG_EPW 4
+#endif
+constexpr int CG_EPW = GW_CG_EPW;   // k_sync_count_g: flagged entries per wave
 template <int U>
 __global__ void __launch_bounds__(NT) k_sync_count_g(World w, const uint32_t* __restrict__ flagged,
                                                      const uint32_t* __restrict__ fbits, const uint64_t* nf_dev,
                                                      uint32_t nf_max, uint32_t G, uint32_t* __restrict__ cnt) {
     const uint64_t nf = load_n(nf_max, nf_dev);
     const int ln = lane_id();
-    const uint64_t stride = (uint64_t)gridDim.x * NWAVE;
-    for (uint64_t k = (uint64_t)blockIdx.x * NWAVE + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-         k < nf_max; k += stride) {
-        uint32_t c = 0;                                   // lane g: records of gate g
-        if (k < nf) {
-            const uint32_t e = flagged[k], f = fbits[k];
-            const AoiEnt a = w.rec[e].a;
-            const uint32_t gt = w.gate[e];
-            const SpaceP P = w.sp[a.meta & SPACE_MASK];
-            if (owned_x(P, a.x)) {
-                if ((f & GW_SIF_OWN_CLIENT) && gt && (uint32_t)ln == gt) c = 1;
-                if ((f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT)) {
-                    wave_neighbors_of<U>(w, e, a, P, [&](bool rel, uint32_t ws, uint32_t g) {
-                        const uint32_t gw = (rel && g != 0) ? (uint32_t)w.gate[ws] : 0u;   // 0: no record
-                        for (uint32_t q = 1; q < G; ++q) {
-                            const uint32_t n = (uint32_t)popc64(wave_ballot(gw == q));
-                            if ((uint32_t)ln == q) c += n;
-                        }
-                    });
-                }
+    const uint64_t stride = (uint64_t)gridDim.x * NWAVE * CG_EPW;
+    // a lane per flagged entry, CG_EPW entries per wave: the split of this
+    // tick's diff where it has one; the others' windows are then walked one at
+    // a time by the whole wave, lane g counting gate g (few entries per wave
+    // keep the walks spread over many waves when the split is stale)
+    for (uint64_t base = ((uint64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6)) * CG_EPW; base < nf_max; base += stride) {
+        const uint64_t k = base + ln;
+        const bool mine = ln < CG_EPW && k < nf_max;
+        uint32_t e = 0, f = 0, gt = 0;
+        AoiEnt a{};
+        unsigned long long nc = 0;
+        if (mine && k < nf) {
+            e = flagged[k];
+            f = fbits[k];
+            a = w.rec[e].a;
+            gt = w.gate[e];
+            nc = w.nbc[e];
+        }
+        bool nbr = false, walk = false;
+        if (mine && k < nf && owned_x(w.sp[a.meta & SPACE_MASK], a.x)) {
+            if (!(f & GW_SIF_OWN_CLIENT)) gt = 0;            // gt: the own record's gate, 0 for none
+            nbr = (f & GW_SIF_NEIGHBOR_CLIENTS) && (a.meta & PRESENT_BIT);
+            walk = nbr && !((uint32_t)(nc >> 32) == w.epoch && (nc & NBC_GATES));   // no split from this tick
+        } else {
+            gt = 0;                                          // (not owned here / past the list: no records)
+        }
+        if (mine && !walk) {
+            unsigned long long sw[4] = {0ull, 0ull, 0ull, 0ull};
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if (nbr && 4 * j < G) sw[j] = w.nbg[(uint64_t)e * 4 + j];
+            cnt[k] = 0;                                      // gate 0 (no client): never a record
+#pragma unroll
+            for (uint32_t q = 1; q < GATE_DIRECT_MAX; ++q) {
+                if (q >= G) break;                           // kernel-uniform
+                cnt[(uint64_t)q * nf_max + k] = ((uint32_t)(sw[q >> 2] >> (16 * (q & 3))) & 0xffffu) + (gt == q ? 1u : 0u);
             }
         }
-        if ((uint32_t)ln < G) cnt[(uint64_t)ln * nf_max + k] = c;   // gate 0 (no client): always 0
+        uint64_t todo = wave_ballot(walk);
+        while (todo) {
+            const int L = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t eq = (uint32_t)__builtin_amdgcn_readlane((int)e, L);
+            const uint32_t gq = (uint32_t)__builtin_amdgcn_readlane((int)gt, L);
+            uint32_t c = (gq && (uint32_t)ln == gq) ? 1u : 0u;   // lane g: records of gate g
+            const AoiEnt aq = w.rec[eq].a;
+            wave_neighbors_of<U>(w, eq, aq, w.sp[aq.meta & SPACE_MASK], [&](bool rel, uint32_t ws, uint32_t g) {
+                // the watcher's gate from its grid entry (ids < 16 here): no gather
+                const uint32_t gw = (rel && g != 0) ? (g >> GATE_SHIFT) & 15u : 0u;   // 0: no record
+                for (uint32_t q = 1; q < G; ++q) {
+                    const uint32_t n = (uint32_t)popc64(wave_ballot(gw == q));
+                    if ((uint32_t)ln == q) c += n;
+                }
+            });
+            if ((uint32_t)ln < G) cnt[(uint64_t)ln * nf_max + base + L] = c;
+        }
     }
 }
 
@@ -956,7 +994,7 @@ __global__ void __launch_bounds__(NT) k_sync_write_g(World w, const uint32_t* __
         }
         if (!(f & GW_SIF_NEIGHBOR_CLIENTS) || !(a.meta & PRESENT_BIT)) continue;
         wave_neighbors_of<U>(w, e, a, P, [&](bool rel, uint32_t ws, uint32_t g) {
-            const uint32_t gw = (rel && g != 0) ? (uint32_t)w.gate[ws] : 0u;
+            const uint32_t gw = (rel && g != 0) ? (g >> GATE_SHIFT) & 15u : 0u;   // (grid entry: no gather)
             uint64_t pos = 0;
             for (uint32_t q = 1; q < G; ++q) {
                 const uint64_t bq = wave_ballot(gw == q);
@@ -974,7 +1012,7 @@ __global__ void __launch_bounds__(NT) k_sync_write_g(World w, const uint32_t* __
 void launch_sync_gates(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
                        uint32_t nf_max, uint32_t G, uint32_t* cnt, hipStream_t s) {
     if (!nf_max) return;
-    const dim3 g(std::min(nblk(nf_max, NWAVE), SYNC_MAX_BLOCKS));
+    const dim3 g(std::min(nblk(nf_max, NWAVE * CG_EPW), SYNC_MAX_BLOCKS));   // CG_EPW entries per wave
     hipLaunchKernelGGL(k_sync_count_g<4>, g, dim3(NT), 0, s, w, flagged, fbits, nf_dev, nf_max, G, cnt);
 }
 void launch_sync_write_gates(const World& w, const uint32_t* flagged, const uint32_t* fbits, const uint64_t* nf_dev,
@@ -1213,7 +1251,7 @@ __global__ void __launch_bounds__(NT) k_set_clients(World w, const uint32_t* slo
         const uint32_t k = w.gn_start[cell_of(w.sp[a.meta & SPACE_MASK], a.x, a.z)] + w.rec[s].gidx;
         if (k < w.cap) {
             GEnt* g = w.gn + k;
-            if (g->slot == s) g->meta = (g->meta & ~CLIENT_BIT) | (gates[i] ? CLIENT_BIT : 0u);
+            if (g->slot == s) g->meta = (g->meta & ~(CLIENT_BIT | GATE_MASK)) | gate_meta(gates[i]);
         }
     }
 }
@@ -1374,7 +1412,7 @@ __global__ void __launch_bounds__(NT) k_fanout_count(World w, const uint32_t* __
             const unsigned long long c = w.nbc[e];
             r = g ? 1u : 0u;
             if (a.meta & PRESENT_BIT) {
-                if ((uint32_t)(c >> 32) == w.epoch) r += (uint32_t)c;
+                if ((uint32_t)(c >> 32) == w.epoch) r += (uint32_t)c & NBC_COUNT;
                 else walk = true;
             }
         }

@@ -51,7 +51,7 @@ def grid_cells(tr, x, z, cells_per_d=2):
     ex, ez = b[2] - b[0], b[3] - b[1]
     maxabs = max(abs(b[0]), abs(b[2]), abs(b[1]), abs(b[3]))
     span = 2.0 * d + 4e-6 * (maxabs + d) + 1e-3
-    cs = max(max(d / cells_per_d, max(ex, ez) / 8192.0), span / 9.0)
+    cs = max(max(d / cells_per_d, max(ex, ez) / 4096.0), span / 9.0)
     inv = np.float32(1.0 / cs)
     W, H = max(1, int(np.ceil(ex / cs))), max(1, int(np.ceil(ez / cs)))
 
@@ -519,6 +519,23 @@ def test_clients_change_between_tick_and_collect(ctx_factory):
         h.gates[sel] = newg
         for s, gg in zip(sel.tolist(), newg.tolist()):
             h.orcs[0].set_client(s, gg)
+        h.check_collect()
+
+
+@pytest.mark.parametrize("which,ng", [("config2", 3), ("config3", 3), ("config3", 15)])
+def test_gate_counts_from_diff(ctx_factory, which, ng):
+    """Several gates (2 < G <= 16): a collect right after the tick takes each
+    mover's record count per gate from the diff's split (World.nbg) instead of
+    walking its window; records and gate partitions must equal the oracle's,
+    hotspot cells included (config #3 shape at a reduced population)."""
+    tr = (T.config2(ticks=3, n=20_000) if which == "config2"
+          else T.config3(ticks=3, n=60_000, side=32768.0 * (0.06 ** 0.5)))
+    i = np.arange(tr.capacity)
+    tr.gates = np.where(i % 5 == 4, 0, 1 + i % ng).astype(np.uint16)
+    h = Harness(ctx_factory(), [tr])
+    h.check_collect()
+    for t in range(len(tr.ticks)):
+        h.step(t)
         h.check_collect()
 
 

@@ -237,10 +237,11 @@ def dry_run(a, ctl):
 
 # the diff stage's kernel: k_mover_c (one wave per primary mover entry), k_mover (one wave per
 # mover-grid entry, GW_MOVER_COMPACT=0), or k_mover_pair when GW_PAIR_MAX > 0
-# (k_mover_c<2, false>: the variant without the group-teleport paths, launched unless the context is a
-# world of >= 2 strips; k_mover_small<2, true>: the half-wave walk)
+# (k_mover_c<2, false, 0>: the variant without the group-teleport paths, launched unless the context is a
+# world of >= 2 strips, and without the per-gate split of a context with 3-16 gate ids;
+# k_mover_small<2, true>: the half-wave walk)
 STAGE_KERNEL = {"diff": "k_mover_pair<2>" if int(os.environ.get("GW_PAIR_MAX", "0") or 0) > 0
-                else "k_mover<2, 1>" if os.environ.get("GW_MOVER_COMPACT", "1") == "0" else "k_mover_c<2, false>"}
+                else "k_mover<2, 1>" if os.environ.get("GW_MOVER_COMPACT", "1") == "0" else "k_mover_c<2, false, 0>"}
 # the stage's kernel differs in small-space mode (config #4: many spaces whose grids fit LDS)
 STAGE_KERNEL_C4 = {"diff": "k_mover_small<2, true>", "sync_write": "k_sync_write_small2"}
 PMC_DIR = os.path.join(ROOT, "profiles")

@@ -752,11 +752,12 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     // count and chunk was ~10 scalar instructions of every chunk's chain)
     uint32_t l_old = 0, l_new = 0, l_cli = 0, l_nl = 0, l_nml = 0;
     uint32_t l_lc = 0;      // (LONGS) pairs with another long mover related before or after the tick
-    // (GW) per-lane counts by gate: 8 bits per gate, gate g in byte g % 4 of
-    // l_g[g / 4] (GW VGPRs: 16-bit fields cost k_mover_c a wave of residency);
-    // exact while every lane's l_cli <= 255, else the split is not published
+    // (GW) per-lane counts by gate: 8 bits per gate, gate g in byte g % 8 of
+    // l_g[g / 8] (GW VGPRs: 16-bit fields cost k_mover_c a wave of residency;
+    // one 64-bit add per candidate); exact while every lane's l_cli <= 255
+    // (TickBufs.gate_lane_max), else the split is not published
     constexpr bool GATES = GW > 0;
-    uint32_t l_g[GW > 0 ? GW : 1] = {};
+    unsigned long long l_g[GW > 0 ? GW / 2 : 1] = {};
     Flat f;
     // the row ranges k_bounds gathered (<= RR_ROWS rows x 2 grids: lanes 0..15)
     const bool rr_ok =
@@ -844,10 +845,17 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
             l_new += (uint32_t)t_rn;
             l_cli += (uint32_t)t_cli;
             if (GATES) {
-                const uint32_t gid = (e.info >> CAND_GATE) & 15u;
-                const uint32_t inc = t_cli ? (1u << (8u * (gid & 3u))) : 0u;
-#pragma unroll
-                for (uint32_t j = 0; j < (uint32_t)GW; ++j) l_g[j] += (gid >> 2) == j ? inc : 0u;
+                // bits CAND_GATE - 3 .. CAND_GATE - 1 of info are clear: this
+                // is 8 * (gate % 8), the gate's byte in its word
+                const uint32_t sh = (e.info >> (CAND_GATE - 3)) & 0x38u;
+                const unsigned long long inc = (unsigned long long)(t_cli ? 1u : 0u) << sh;
+                if (GW == 2) {
+                    l_g[0] += inc;
+                } else {
+                    const bool hi = ((e.info >> (CAND_GATE + 3)) & 1u) != 0;   // gates 8..15
+                    l_g[0] += hi ? 0ull : inc;
+                    l_g[GW / 2 - 1] += hi ? inc : 0ull;
+                }
             }
             // B has no op: (B,A) is B's event too (kept in A's region; the
             // events stage places it)
@@ -921,15 +929,16 @@ __device__ __forceinline__ void mover_one(const TickBufs& b, uint64_t m, uint32_
     }
     const uint32_t so = c_old, sn = c_new, scl = c_cli;
     // (GATES) the split is exact when no lane's byte can have wrapped
-    const bool g_ok = GATES && pn && !wave_ballot(l_cli > 255u);
+    const bool g_ok = GATES && pn && !wave_ballot(l_cli > b.gate_lane_max);
     if (g_ok) {
         // the wave's per-gate sums in 16-bit fields (<= 64 x 255): bytes 0, 2
         // and 1, 3 of each word summed apart, then laid out as World.nbg
         unsigned long long v = 0;
 #pragma unroll
         for (int j = 0; j < GW; ++j) {
-            const uint32_t se = wave_incl_scan<uint32_t>(l_g[j] & 0x00ff00ffu);         // gates 4j, 4j+2
-            const uint32_t so_ = wave_incl_scan<uint32_t>((l_g[j] >> 8) & 0x00ff00ffu); // gates 4j+1, 4j+3
+            const uint32_t lw = (uint32_t)(l_g[j >> 1] >> (32 * (j & 1)));               // gates 4j .. 4j+3
+            const uint32_t se = wave_incl_scan<uint32_t>(lw & 0x00ff00ffu);              // gates 4j, 4j+2
+            const uint32_t so_ = wave_incl_scan<uint32_t>((lw >> 8) & 0x00ff00ffu);      // gates 4j+1, 4j+3
             const uint32_t te = (uint32_t)__builtin_amdgcn_readlane((int)se, 63);
             const uint32_t to = (uint32_t)__builtin_amdgcn_readlane((int)so_, 63);
             const unsigned long long t = (unsigned long long)(te & 0xffffu) | ((unsigned long long)(to & 0xffffu) << 16) |

@@ -570,6 +570,7 @@ int gw_init(int device_id, gw_ctx** out) {
         if (const char* e = getenv("GW_HEAVY_MAXM")) c->heavy_maxm = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_DIRTY_SPAN")) c->dirty_span = (uint32_t)std::min(64, std::max(1, atoi(e)));
         if (const char* e = getenv("GW_HALF_ROWS")) c->half_rows = (uint32_t)std::min(16, std::max(0, atoi(e)));
+        if (const char* e = getenv("GW_GATE_LANE_MAX")) c->gate_lane_max = (uint32_t)std::min(255, std::max(0, atoi(e)));
     } while (0);
     if (rc) {
         (void)hipGetLastError();
@@ -1375,6 +1376,7 @@ int gw_tick(gw_ctx* c, uint32_t flags, gw_tick_out* out) {
     b.big = P<uint32_t>(c->big);
     b.fall = P<uint32_t>(c->fall);
     b.half_rows = c->half_rows;
+    b.gate_lane_max = c->gate_lane_max;
     b.bk_flat = c->bk_flat;
     b.post_split = c->post_split;
     b.place_split = c->place_split;

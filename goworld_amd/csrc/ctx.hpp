@@ -224,6 +224,7 @@ struct gw_ctx {
     // config #4's 4.4M cells at 4 per wave cost +50 us)
     uint32_t dirty_span = 0;
     uint32_t half_rows = 16;             // GW_HALF_ROWS: TickBufs.half_rows (tests of the fallback paths)
+    uint32_t gate_lane_max = 255;        // GW_GATE_LANE_MAX: TickBufs.gate_lane_max (tests of the fallback)
     int32_t bk_flat = -1;                // GW_BK_FLAT, GW_POST_SPLIT, GW_PLACE_SPLIT: TickBufs' launch-merge knobs
     uint32_t post_split = 0, place_split = 0;
     bool dirty_split = false;            // GW_DIRTY_SPLIT=1: the dirty cells' merges in a launch of their own

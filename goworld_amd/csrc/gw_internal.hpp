@@ -309,6 +309,8 @@ struct TickBufs {
     int small_halves;         //   two movers per wave (GW_MOVER_HALVES, default on)
     uint32_t half_rows;       //   rows a half-wave walk takes (16; GW_HALF_ROWS lowers it in tests: more
                               //   pairs left to mover_one / k_mover_list)
+    uint32_t gate_lane_max;   // per-gate split: a lane's client count up to which it is exact (255, the
+                              // 8-bit counters; GW_GATE_LANE_MAX lowers it in tests: more walked entries)
     int diff_u;               // candidate chunks of 64 in flight per k_mover iteration
     uint32_t walk_min;        // mean candidates per row range from which a walk maps chunks by readlanes
     uint32_t rank_sort;       // own events sorted by rank (readlanes) up to this many, more by a network

@@ -892,7 +892,8 @@ void launch_sync_write(const World& w, const uint32_t* flagged, const uint32_t* 
 //          entry) its first record, and gate g's first record at g * nf_max;
 //   write: a wave per entry holds the next position of each gate in lanes
 //          0..G-1 and stores each record at its gate's position (ranks inside
-//          a chunk by one ballot per gate); the gates' first records go to
+//          a chunk from four ballots, the bit planes of the gate ids, whatever
+//          G); the gates' first records go to
 //          DevStats.gate_base, read with the collect's one host sync.
 #ifndef GW_CG_EPW
 #define GW_CG_EPW 4
@@ -953,10 +954,15 @@ __global__ void __launch_bounds__(NT) k_sync_count_g(World w, const uint32_t* __
             wave_neighbors_of<U>(w, eq, aq, w.sp[aq.meta & SPACE_MASK], [&](bool rel, uint32_t ws, uint32_t g) {
                 // the watcher's gate from its grid entry (ids < 16 here): no gather
                 const uint32_t gw = (rel && g != 0) ? (g >> GATE_SHIFT) & 15u : 0u;   // 0: no record
-                for (uint32_t q = 1; q < G; ++q) {
-                    const uint32_t n = (uint32_t)popc64(wave_ballot(gw == q));
-                    if ((uint32_t)ln == q) c += n;
-                }
+                const uint64_t any = wave_ballot(gw != 0);
+                if (!any) return;                         // wave-uniform
+                // lane q counts the lanes whose id is q, from the ids' bit planes
+                const uint64_t b0 = wave_ballot(gw & 1u), b1 = wave_ballot(gw & 2u);
+                const uint64_t b2 = wave_ballot(gw & 4u), b3 = wave_ballot(gw & 8u);
+                const uint32_t q = (uint32_t)ln;
+                const uint64_t mq = any & ((q & 1u) ? b0 : ~b0) & ((q & 2u) ? b1 : ~b1) & ((q & 4u) ? b2 : ~b2) &
+                                    ((q & 8u) ? b3 : ~b3);
+                if (q < G) c += (uint32_t)popc64(mq);
             });
             if ((uint32_t)ln < G) cnt[(uint64_t)ln * nf_max + base + L] = c;
         }
@@ -995,15 +1001,21 @@ __global__ void __launch_bounds__(NT) k_sync_write_g(World w, const uint32_t* __
         if (!(f & GW_SIF_NEIGHBOR_CLIENTS) || !(a.meta & PRESENT_BIT)) continue;
         wave_neighbors_of<U>(w, e, a, P, [&](bool rel, uint32_t ws, uint32_t g) {
             const uint32_t gw = (rel && g != 0) ? (g >> GATE_SHIFT) & 15u : 0u;   // (grid entry: no gather)
-            uint64_t pos = 0;
-            for (uint32_t q = 1; q < G; ++q) {
-                const uint64_t bq = wave_ballot(gw == q);
-                if (!bq) continue;                        // wave-uniform
-                const uint64_t o = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(at >> 32), (int)q) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)at, (int)q);
-                if (gw == q) pos = o + (uint64_t)popc64(bq & lt);
-                if ((uint32_t)ln == q) at += (uint64_t)popc64(bq);
-            }
+            const uint64_t any = wave_ballot(gw != 0);
+            if (!any) return;                             // wave-uniform
+            // the lanes of each gate from the gate ids' four bit planes (one
+            // ballot each, whatever G): lanes_of(q) = the lanes whose id is q
+            const uint64_t b0 = wave_ballot(gw & 1u), b1 = wave_ballot(gw & 2u);
+            const uint64_t b2 = wave_ballot(gw & 4u), b3 = wave_ballot(gw & 8u);
+            auto lanes_of = [&](uint32_t q) {
+                return any & ((q & 1u) ? b0 : ~b0) & ((q & 2u) ? b1 : ~b1) & ((q & 4u) ? b2 : ~b2) &
+                       ((q & 8u) ? b3 : ~b3);
+            };
+            // my gate's next position sits in lane gw
+            const uint32_t olo = (uint32_t)__shfl((int)(uint32_t)at, (int)gw, 64);
+            const uint32_t ohi = (uint32_t)__shfl((int)(uint32_t)(at >> 32), (int)gw, 64);
+            const uint64_t pos = (((uint64_t)ohi << 32) | olo) + (uint64_t)popc64(lanes_of(gw) & lt);
+            if ((uint32_t)ln < G) at += (uint64_t)popc64(lanes_of((uint32_t)ln));   // lane 0: none (any excludes id 0)
             if (gw != 0) st_record_nt(rec + pos, ws, e, p);
         });
     }

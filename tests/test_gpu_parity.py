@@ -522,12 +522,18 @@ def test_clients_change_between_tick_and_collect(ctx_factory):
         h.check_collect()
 
 
-@pytest.mark.parametrize("which,ng", [("config2", 3), ("config3", 3), ("config3", 15)])
-def test_gate_counts_from_diff(ctx_factory, which, ng):
+@pytest.mark.parametrize("which,ng,lane_max", [("config2", 3, None), ("config3", 3, None), ("config3", 15, None),
+                                                ("config3", 5, 1)])
+def test_gate_counts_from_diff(ctx_factory, monkeypatch, which, ng, lane_max):
     """Several gates (2 < G <= 16): a collect right after the tick takes each
     mover's record count per gate from the diff's split (World.nbg) instead of
     walking its window; records and gate partitions must equal the oracle's,
-    hotspot cells included (config #3 shape at a reduced population)."""
+    hotspot cells included (config #3 shape at a reduced population).  With
+    GW_GATE_LANE_MAX=1 every mover with more than one client candidate on a
+    lane is left without a split (as past 255 per lane), so one collect mixes
+    split and walked entries."""
+    if lane_max is not None:
+        monkeypatch.setenv("GW_GATE_LANE_MAX", str(lane_max))
     tr = (T.config2(ticks=3, n=20_000) if which == "config2"
           else T.config3(ticks=3, n=60_000, side=32768.0 * (0.06 ** 0.5)))
     i = np.arange(tr.capacity)

@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(NT) k_ops3(TickBufs b) {
             const AoiEnt a0 = b.w.rec[s].a;
             const unsigned long long st0 = b.w.rec[s].stamp;
             gidx = b.w.rec[s].gidx;
-            gate = b.w.gate[s];
+            gate = b.w.rec[s].gate;
             struct { int32_t pos, aoi, leave, clr[2]; } ol;
             ol.pos = ol_get(o.pos, b.ol_tag);
             ol.aoi = ol_get(o.aoi, b.ol_tag);
@@ -230,7 +230,7 @@ __global__ void __launch_bounds__(NT) k_grid_fill(World w, const uint32_t* __res
         const AoiEnt a = w.rec[s].a;
         GEnt e;
         e.x = a.x; e.z = a.z; e.slot = s;
-        e.meta = key | gate_meta(w.gate[s]);
+        e.meta = key | gate_meta(w.rec[s].gate);
         w.gn[i] = e;
     }
 }

@@ -44,7 +44,7 @@ struct alignas(64) SlotRec {
     PrevEnt pv;                // pre-tick position and stamp (this tick's movers)
     unsigned long long stamp;  // global stamp of the slot's last AOI op
     uint32_t gidx;             // offset of the slot's entry inside its cell's range of gn
-    uint32_t pad;
+    uint32_t gate;             // World.gate[slot] again, read with the state (one line less per op / entity)
 };
 static_assert(sizeof(SlotRec) == 64, "SlotRec is one 64-B line");
 

@@ -55,6 +55,7 @@ __global__ void __launch_bounds__(NT) k_slots_clear(World w, OpLast* __restrict_
     w.rec[s].stamp = 0ull;
     w.rec[s].p = make_float4(0.f, 0.f, 0.f, 0.f);
     w.gate[s] = 0;
+    w.rec[s].gate = 0;
     w.nbc[s] = 0ull;
     OpLast z{};
     ol[s] = z;

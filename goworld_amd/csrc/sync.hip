@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(NT) k_sync_count(World w, const uint32_t* __re
         }
         if (valid) {
             a = w.rec[e].a;
-            gt = w.gate[e];                                 // loaded with the state, not behind the test
+            gt = w.rec[e].gate;                             // loaded with the state, not behind the test
             c = w.nbc[e];
         }
         if (sfirst) {
@@ -307,7 +307,7 @@ __global__ void __launch_bounds__(NT, GW_SW_MINB) k_sync_write(World w, const ui
         SwEnt x{};
         if (q < nf) {
             x.a = w.rec[h.e].a;
-            x.gt = w.gate[h.e];
+            x.gt = w.rec[h.e].gate;
         }
         return x;
     };
@@ -412,7 +412,7 @@ __device__ __forceinline__ void sw_full(const World& w, uint32_t e, uint32_t f, 
     }
     const AoiEnt a = w.rec[e].a;
     const float4 p = w.rec[e].p;
-    const uint32_t gt = w.gate[e];
+    const uint32_t gt = w.rec[e].gate;
     const SpaceP P = w.sp[a.meta & SPACE_MASK];
     if (!owned_x(P, a.x)) return;
     if ((f & GW_SIF_OWN_CLIENT) && gt) {
@@ -499,7 +499,7 @@ __global__ void __launch_bounds__(NT, GW_SWH_MINB) k_sync_write_h(World w, const
         if (valid) {
             a = w.rec[e].a;
             p = w.rec[e].p;
-            gt = w.gate[e];
+            gt = w.rec[e].gate;
         }
         const SpaceP P = w.sp[a.meta & SPACE_MASK];
         bool walk = false;
@@ -659,7 +659,7 @@ __global__ void __launch_bounds__(NT) k_sync_write_small(World w, const uint32_t
         const AoiEnt a = w.rec[e].a;
         if (!owned_x(P, a.x)) continue;
         const float4 p = w.rec[e].p;
-        if ((f & GW_SIF_OWN_CLIENT) && w.gate[e]) {
+        if ((f & GW_SIF_OWN_CLIENT) && w.rec[e].gate) {
             if (ln == 0) st_record_nt(rec + at, e, e, p);
             ++at;
         }
@@ -729,7 +729,7 @@ __global__ void __launch_bounds__(NT) k_sync_write_small2(World w, const uint32_
         if (k < hi) {
             x.a = w.rec[e].a;
             x.p = w.rec[e].p;
-            x.gt = w.gate[e];
+            x.gt = w.rec[e].gate;
         }
     };
     constexpr uint32_t STEP = NWAVE * 2;
@@ -920,7 +920,7 @@ __global__ void __launch_bounds__(NT) k_sync_count_g(World w, const uint32_t* __
             e = flagged[k];
             f = fbits[k];
             a = w.rec[e].a;
-            gt = w.gate[e];
+            gt = w.rec[e].gate;
             nc = w.nbc[e];
         }
         bool nbr = false, walk = false;
@@ -987,7 +987,7 @@ __global__ void __launch_bounds__(NT) k_sync_write_g(World w, const uint32_t* __
          k < nf; k += stride) {
         const uint32_t e = flagged[k], f = fbits[k];
         const AoiEnt a = w.rec[e].a;
-        const uint32_t gt = w.gate[e];
+        const uint32_t gt = w.rec[e].gate;
         const SpaceP P = w.sp[a.meta & SPACE_MASK];
         if (!owned_x(P, a.x)) continue;
         const float4 p = w.rec[e].p;
@@ -1249,7 +1249,7 @@ void launch_gather_records(const gw_sync_record* in, const uint32_t* idx, const 
 // ---------------------------------------------------------------------------
 // client attach / detach (GameClient.go:14-27): the gate copy in the grid entry
 // is patched too, so a collect after set_clients sees the new gates
-// gate[] always; the CLIENT_BIT of the slot's grid entry only while the grid
+// gate[] (and its copy in the slot record) always; the CLIENT_BIT of the slot's grid entry only while the grid
 // is current (grid_ok: a rebuild takes the bits from gate[] anyway, and gidx
 // of slots entered since the last build is not valid)
 __global__ void __launch_bounds__(NT) k_set_clients(World w, const uint32_t* slots, const uint16_t* gates,
@@ -1258,6 +1258,7 @@ __global__ void __launch_bounds__(NT) k_set_clients(World w, const uint32_t* slo
     if (i >= n || slots[i] >= w.cap) return;
     const uint32_t s = slots[i];
     w.gate[s] = gates[i];
+    w.rec[s].gate = gates[i];
     const AoiEnt a = w.rec[s].a;
     if (grid_ok && (a.meta & PRESENT_BIT)) {
         const uint32_t k = w.gn_start[cell_of(w.sp[a.meta & SPACE_MASK], a.x, a.z)] + w.rec[s].gidx;
@@ -1420,7 +1421,7 @@ __global__ void __launch_bounds__(NT) k_fanout_count(World w, const uint32_t* __
         if (valid) {
             e = items[k];
             const AoiEnt a = w.rec[e].a;
-            const uint32_t g = w.gate[e];
+            const uint32_t g = w.rec[e].gate;
             const unsigned long long c = w.nbc[e];
             r = g ? 1u : 0u;
             if (a.meta & PRESENT_BIT) {

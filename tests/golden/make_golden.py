@@ -203,6 +203,67 @@ def run_digest(tr) -> dict:
                 nbr_total=int(o.total_neighbors()))
 
 
+def config5_world_trace(ticks: int = 3):
+    """Config #5 (the 16M world) as the single-context op stream
+    of tests/test_gpu_config5.py: the world walk's ops of each tick split by
+    the strip that owns each mover before the tick (8 strips) and concatenated
+    rank-major, the order the world's stamps give them; the population
+    entered in slot order (the test's restore), one gate for every entity."""
+    from goworld_amd.dworld import Strips
+    n, side, ranks = 16_000_000, 131072.0, 8
+    walk = T.WorldWalk(seed=5, n=n, side=side)
+    x0, z0, yaw0 = walk.x(), walk.z(), walk.yaw.copy()
+    geom = Strips(-side / 2, side / ranks, ranks, 100.0, 4.0)
+    ops_t = []
+    for _ in range(ticks):
+        ops, xb = walk.next_tick()
+        own = geom.owner(xb)
+        ops_t.append(np.concatenate([ops[own == r] for r in range(ranks)]))
+    return T.SpaceTrace(n=n, capacity=n, d=100.0, bounds=(-side / 2, -side / 2, side / 2, side / 2),
+                        init_slots=np.arange(n, dtype=np.uint32), init_x=x0, init_y=np.zeros(n, np.float32),
+                        init_z=z0, init_yaw=yaw0, ticks=ops_t, gates=np.ones(n, np.uint16))
+
+
+def rec_digest(recs: np.ndarray):
+    """Order-free digest of a record multiset, (count, sum h1, sum h2) mod 2^64:
+    the one tests/test_gpu_config5.py takes of the GPU's records."""
+    m1, m2 = np.uint64(0x9E3779B97F4A7C15), np.uint64(0xBF58476D1CE4E5B9)
+
+    def mix(z):
+        z = z.copy()
+        z ^= z >> np.uint64(30)
+        z *= m2
+        z ^= z >> np.uint64(27)
+        z *= np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+        return z
+    w = np.ascontiguousarray(recs).view(np.uint64).reshape(-1, 3)
+    with np.errstate(over="ignore"):
+        h1 = mix(w[:, 0] ^ mix(w[:, 1] + m1) ^ mix(w[:, 2] * m2 + np.uint64(7)))
+        h2 = mix((w[:, 0] * m1) ^ mix(w[:, 1] ^ m2) ^ mix(w[:, 2] + np.uint64(0x632BE59BD9B4E019)))
+        return [len(recs), int(h1.sum(dtype=np.uint64)), int(h2.sum(dtype=np.uint64))]
+
+
+def run_config5_digest(tr) -> dict:
+    """gridmt (oracle/gridmt.c, equal to ORC_SEQRULE on every trace of
+    tests/test_oracle.py and on the #2 / #3 / #4 digests above) over the 16M
+    world as one space: per tick the canonical events' SHA-256 and the
+    records' order-free digest.  The load's own collect is not digested."""
+    g = pyorc.GridMT(tr.capacity, tr.d, tr.bounds)
+    g.load(tr)
+    g.collect()
+    ticks = []
+    for t, ops in enumerate(tr.ticks):
+        assert g.tick(ops) == 0
+        e, l = g.events()
+        r = g.collect()
+        ticks.append(dict(n_enter=len(e), n_leave=len(l), n_rec=len(r), enter_sha=sha(e), leave_sha=sha(l),
+                          rec_digest=rec_digest(r)))
+        print(f"  tick {t}: {len(e)} enter, {len(l)} leave, {len(r)} records", flush=True)
+        del r
+    return dict(input_sha=trace_input_sha(tr), ticks=ticks, engine="gridmt")
+
+
 def multi_digest_configs():
     return [("config4_10k", lambda: [T.config4_space(s, ticks=2) for s in range(10_000)])]
 
@@ -268,7 +329,7 @@ def main(argv):
             continue
         print(f"{name}: N={tr.n}, {len(tr.ticks)} ticks", flush=True)
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **run_small(tr, brute))
-    digest_names = [n for n, _, _ in digest_configs()] + [n for n, _ in multi_digest_configs()]
+    digest_names = [n for n, _, _ in digest_configs()] + [n for n, _ in multi_digest_configs()] + ["config5_16m"]
     if only and not any(n in only for n in digest_names):
         return
     out = {"_note": "SHA-256 of canonical outputs (tests/golden/make_golden.py); "
@@ -283,6 +344,9 @@ def main(argv):
             continue
         print(f"{name}", flush=True)
         out[name] = run_multi_digest(make())
+    if "config5_16m" in only:                  # (on request only: ~16 GB, minutes on 8 cores)
+        print("config5_16m", flush=True)
+        out["config5_16m"] = run_config5_digest(config5_world_trace())
     path = os.path.join(HERE, "digests.json")
     if only and os.path.exists(path):
         with open(path) as f:

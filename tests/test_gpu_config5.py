@@ -11,10 +11,14 @@ stamps order them).  Per tick: the union of the strips' owned enter / leave
 events equals the single context's, byte for byte after a (watcher, target)
 sort; the union of their sync records equals the single context's as a
 multiset (count + two independent order-free 64-bit digests: each strip emits
-its entities' records in its own grid order)."""
+its entities' records in its own grid order).  The single context is in turn
+checked against the CPU oracle: oracle/gridmt.c (equal to ORC_SEQRULE on every
+oracle test trace) ran the same op stream, and tests/golden/digests.json keeps
+its per-tick event SHA-256s and record digests (make_golden.py config5_16m)."""
 import numpy as np
 import pytest
 
+import golden_data as G
 from goworld_amd import dworld, gpuaoi
 from goworld_amd import traces as T
 
@@ -75,6 +79,8 @@ def test_config5_16m_world_8_strips_equals_single_context():
         single.set_clients(np.arange(N, dtype=np.uint32), np.ones(N, np.uint16))
         single.sync_collect(copy=False)
         n_ev = n_rec = 0
+        oracle = G.digests()["config5_16m"]
+        single_out, single_ops = [], []
         for t, (ops, xb) in enumerate(tk):
             parts = lw.split(ops, xb)
             lw.route_submit([lw.upload(r, p) for r, p in enumerate(parts)], [len(p) for p in parts])
@@ -86,13 +92,16 @@ def test_config5_16m_world_8_strips_equals_single_context():
                 s = g.sync_collect(copy=False)
                 g.synchronize()
                 got_r.append(rec_digest(_dev_records(g, s)))
-            single.submit(np.concatenate(parts))          # the world's stamp order: rank-major
+            single_ops.append(np.concatenate(parts))
+            single.submit(single_ops[-1])                 # the world's stamp order: rank-major
             res = single.tick(copy=False)
             exp_e = _dev_events(single, res.enter_dev, res.n_enter)
             exp_l = _dev_events(single, res.leave_dev, res.n_leave)
             s = single.sync_collect(copy=False)
             single.synchronize()
             exp_r = rec_digest(_dev_records(single, s))
+            single_out.append(dict(n_enter=len(exp_e), n_leave=len(exp_l), enter_sha=G.sha(exp_e),
+                                   leave_sha=G.sha(exp_l), rec_digest=list(exp_r)))
             for name, got, exp in (("enter", got_e, exp_e), ("leave", got_l, exp_l)):
                 g_all = np.concatenate(got)
                 assert len(g_all) == len(exp), (t, name, len(g_all), len(exp))
@@ -105,6 +114,15 @@ def test_config5_16m_world_8_strips_equals_single_context():
             n_rec += cnt
         lw.check()
         assert n_ev > TICKS * 3_000_000 and n_rec > TICKS * 50_000_000    # config #5 density
+        # the single context against the oracle's run of the same stream
+        tr = T.SpaceTrace(n=N, capacity=N, d=100.0, bounds=(-SIDE / 2, -SIDE / 2, SIDE / 2, SIDE / 2),
+                          init_slots=np.arange(N, dtype=np.uint32), init_x=x0, init_y=np.zeros(N, np.float32),
+                          init_z=z0, init_yaw=yaw0, ticks=single_ops, gates=np.ones(N, np.uint16))
+        assert G.trace_input_sha(tr) == oracle["input_sha"], "trace generator changed (not a parity failure)"
+        for t, (got, exp) in enumerate(zip(single_out, oracle["ticks"])):
+            assert got["n_enter"] == exp["n_enter"] and got["n_leave"] == exp["n_leave"], t
+            assert got["enter_sha"] == exp["enter_sha"] and got["leave_sha"] == exp["leave_sha"], f"tick {t}: events"
+            assert got["rec_digest"] == exp["rec_digest"], f"tick {t}: records"
     finally:
         single.close()
         lw.close()

@@ -1015,10 +1015,13 @@ __global__ void __launch_bounds__(64 * WPB) k_mover(TickBufs b) {
 // 64 LDS words, the first 32 own events of each half (sorted from there, no
 // read-back of HBM).  Returns false (nothing done) when either entry needs
 // more rows: the caller then runs both through mover_one.
+// RC (k_mover_small with its space's entries staged): region offset | bound
+// << 32 of entry m at RC[m - rc0], read from LDS instead of HBM
 template <int HU>
 __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint64_t m_end, const SpaceP& P,
                                            const GEnt* GN, const uint32_t* GS, const uint32_t* MS,
-                                           const MEnt* GM, uint32_t* L) {
+                                           const MEnt* GM, uint32_t* L, const uint2* RC = nullptr,
+                                           uint32_t rc0 = 0) {
     const int ln = lane_id();
     const uint32_t half = (uint32_t)ln >> 5, hl = (uint32_t)ln & 31u, hb = half << 5;
     const uint64_t hmask = half ? 0xffffffff00000000ull : 0x00000000ffffffffull;
@@ -1047,8 +1050,14 @@ __device__ __forceinline__ bool mover_half(const TickBufs& b, uint64_t m0, uint6
     const bool go = prim;
     const uint32_t A = me.slot;
     if (prim) {
-        reg = b.reg[m] & CAND_MASK;
-        cap = b.cand[m] & CAND_MASK;
+        if (RC) {
+            const uint2 rc = RC[m - rc0];
+            reg = rc.x;
+            cap = rc.y;
+        } else {
+            reg = b.reg[m] & CAND_MASK;
+            cap = b.cand[m] & CAND_MASK;
+        }
     }
     const uint64_t own_cap = b.own_cap;
     const float d = P.d;
@@ -1282,18 +1291,22 @@ __global__ void __launch_bounds__(64) k_mover_pair(TickBufs b) {
 // candidates, ~10 % of them, stay global).
 constexpr uint32_t SMALL_SORT = 256;    // own events sorted in LDS up to this many (more: block sort)
 constexpr uint32_t SMALL_GM = 256;      // mover-grid entries of a space staged in LDS (more: read from HBM)
+// half-wave mode: a wave's own-event words (2 halves x 32), then (from word
+// NWAVE * SMALL_HL of the sort space) the staged entries' regions and bounds
+constexpr uint32_t SMALL_HL = 64;
+static_assert(NWAVE * SMALL_HL + 2 * SMALL_GM <= NWAVE * SMALL_SORT, "staged regions fit the sort space");
 
 template <int DIFF_U, bool HALVES>
 __device__ __forceinline__ void small_walk(const TickBufs& b, uint32_t m0, uint32_t m1, const SpaceP& P,
-                                           const GlobalSrc& src, uint32_t* lds) {
+                                           const GlobalSrc& src, uint32_t* lds, const uint2* RC = nullptr) {
     if (HALVES) {
         // a pair the half-wave walk cannot take (a window of more rows than a
         // half holds) goes to k_mover_list, one wave per entry from the global
         // grids: with no mover_one inlined here the kernel fits 96 VGPRs, 5
         // waves per SIMD instead of 4 (128 VGPRs)
-        uint32_t* L = lds + (threadIdx.x >> 6) * SMALL_SORT;
+        uint32_t* L = lds + (threadIdx.x >> 6) * SMALL_HL;
         for (uint32_t m = m0 + (threadIdx.x >> 6) * 2; m < m1; m += NWAVE * 2) {
-            if (!mover_half<2>(b, m, m1, P, src.GN, src.GS, src.MS, src.GM, L) && lane_id() == 0) {
+            if (!mover_half<2>(b, m, m1, P, src.GN, src.GS, src.MS, src.GM, L, RC, m0) && lane_id() == 0) {
                 const uint32_t k = m + 1 < m1 ? 2u : 1u;
                 const uint32_t at = (uint32_t)atomicAdd(&b.st->n_fall, (unsigned long long)k);
                 b.fall[at] = m;
@@ -1340,11 +1353,18 @@ __global__ void __launch_bounds__(NT, HALVES ? GW_MSH_MINB : GW_MS_MINB) k_mover
         S[i] = b.w.gn_start[cb + i];
         MS[i] = b.gm_start[cb + i];
     }
+    // half-wave mode: the entries' regions and bounds too (no HBM read in the
+    // walk loop but the rare boundary-tie stamps: the pairs' event stores are
+    // not drained by the next pair's region loads), while offsets fit 32 bits
+    uint2* RC = (HALVES && stage && b.own_cap <= 0xffffffffull) ? (uint2*)(lds + NWAVE * SMALL_HL) : nullptr;
     if (stage)
-        for (uint32_t i = threadIdx.x; i < m1 - m0; i += NT) GL[i] = b.gm[m0 + i];
+        for (uint32_t i = threadIdx.x; i < m1 - m0; i += NT) {
+            GL[i] = b.gm[m0 + i];
+            if (RC) RC[i] = make_uint2((uint32_t)(b.reg[m0 + i] & CAND_MASK), (uint32_t)(b.cand[m0 + i] & CAND_MASK));
+        }
     __syncthreads();
     // every mover's own entry and its mover-grid candidates from LDS when staged
-    if (stage) small_walk<DIFF_U, HALVES>(b, m0, m1, P, GlobalSrc{G - g0, S - cb, MS - cb, GL - m0}, lds);
+    if (stage) small_walk<DIFF_U, HALVES>(b, m0, m1, P, GlobalSrc{G - g0, S - cb, MS - cb, GL - m0}, lds, RC);
     else small_walk<DIFF_U, HALVES>(b, m0, m1, P, GlobalSrc{G - g0, S - cb, MS - cb, b.gm}, lds);
 }
 

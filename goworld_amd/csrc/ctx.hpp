@@ -150,8 +150,9 @@ struct gw_ctx {
     int sw_halves = -1;             // GW_SW_HALVES: 1 / 0 force the write pass's half-wave mode, -1 automatic
     double rec_per_flagged = 1e9;   // records per flagged entity of the last collect (the mode's choice)
     bool overlap = true;            // GW_OVERLAP_COLLECT
-    uint32_t overlap_min = 65536;   // GW_OVERLAP_MIN: ... after ticks of at least this many ops (a 1M world's
-                                    // 8-strip rank, 12.5k ops: 0.285 -> 0.294 ms with it; config #3 -25 us)
+    uint32_t overlap_min = 0;       // GW_OVERLAP_MIN: ... after ticks of at least this many ops (round 4: 65536,
+                                    // a 1M world's 8-strip rank got 9 us slower with it; round 6, same box:
+                                    // that rank 0.281 -> 0.272 ms, config #2 0.177 -> 0.162 ms with it)
     std::string err;
 
     std::vector<SpaceHost> spaces;

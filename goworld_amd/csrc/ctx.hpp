@@ -216,9 +216,9 @@ struct gw_ctx {
     uint32_t walk_min = 32;              // GW_WALK_MIN: TickBufs.walk_min (0: always walk)
     bool mover_compact = true;           // GW_MOVER_COMPACT: TickBufs.compact
     uint32_t heavy_min = 512;            // GW_HEAVY_MIN: TickBufs.heavy_min (0: off; 1M world at 8 strips:
-                                         // diff 58 -> 47 us; at 100k movers one wave per mover in cell order
-                                         // balances better) ...
-    uint32_t heavy_maxm = 65536;         // ... for ticks of at most GW_HEAVY_MAXM ops
+                                         // diff 58 -> 47 us; round 6, config #3's 100k movers: diff 148 ->
+                                         // 135 us, step -5..-8 us; rounds 3-4 measured cell order better there) ...
+    uint32_t heavy_maxm = 262144;        // ... for ticks of at most GW_HEAVY_MAXM ops (round 4: 65536)
     uint32_t rank_sort = 12;             // GW_RANK_SORT: TickBufs.rank_sort
     // GW_DIRTY_SPAN: TickBufs.dirty_span; 0 = by the cell count: 2 up to 128k cells, 8 up to 1M cells (a hotspot wave
     // merges fewer dirty cells in a row: config #3 grid 63 -> 58 us), 16 above (fewer idle waves:

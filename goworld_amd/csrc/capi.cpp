@@ -561,6 +561,7 @@ int gw_init(int device_id, gw_ctx** out) {
         if (const char* e = getenv("GW_WALK_MIN")) c->walk_min = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_RANK_SORT")) c->rank_sort = (uint32_t)std::max(0, atoi(e));
         if (const char* e = getenv("GW_GRID_CAP")) c->grid_cap = (uint32_t)std::max(0, atoi(e));
+        if (const char* e = getenv("GW_PAIR_AUTO")) c->pair_auto = atoi(e) != 0;
         if (const char* e = getenv("GW_PAIR_MAX")) {
             c->pair_max = (uint32_t)std::max(0, atoi(e));
             c->pair_auto = false;

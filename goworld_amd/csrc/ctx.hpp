@@ -229,13 +229,13 @@ struct gw_ctx {
     int32_t bk_flat = -1;                // GW_BK_FLAT, GW_POST_SPLIT, GW_PLACE_SPLIT: TickBufs' launch-merge knobs
     uint32_t post_split = 0, place_split = 0;
     bool dirty_split = false;            // GW_DIRTY_SPLIT=1: the dirty cells' merges in a launch of their own
-    // GW_PAIR_MAX: TickBufs.pair_max.  Unset: automatic, PAIR_AUTO when the last
-    // tick had >= PAIR_MOVERS movers averaging <= PAIR_MEAN candidates (many
-    // uniform short lists: config #5 diff 1677 -> 1573 us), else 0 (hotspots:
-    // two long movers in one wave made config #3's diff 192 -> 239 us; few
-    // movers: half the waves, config #2's 10k movers 15 -> 18 us)
+    // GW_PAIR_MAX: TickBufs.pair_max (0: off, the default).  GW_PAIR_AUTO=1:
+    // PAIR_AUTO when the last tick had >= PAIR_MOVERS movers averaging <=
+    // PAIR_MEAN candidates (round 3: config #5 diff 1677 -> 1573 us with it;
+    // round 6, same box, against k_mover_c: config #5 diff 1060 -> 1503 us,
+    // step 3.62 -> 3.92 ms, a 16M-world strip's diff 136 -> 180 us)
     uint32_t pair_max = 0;
-    bool pair_auto = true;
+    bool pair_auto = false;
     uint64_t cand_mean = ~0ull;          // candidates per mover of the last tick
     uint32_t grid_cap = 0;               // GW_GRID_CAP: TickBufs.grid_cap (tests of the grid-stride loops)
     uint64_t ev_cap = 0;                 // events the flatten/sort buffers hold (grows on overflow)
